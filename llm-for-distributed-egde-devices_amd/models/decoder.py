@@ -1,0 +1,245 @@
+"""One decoder implementation for Llama 2/3/3.2, GPT-NeoX (Pythia), Phi-2 and GPT-2.
+
+Replaces the reference's ``AutoModelForCausalLM`` + accelerate stack
+(Code/Base Models/combine_model_fp_updated.py:32-42).  Per-layer data flow:
+
+  sequential (llama, gpt2):  h = x + res ; a = attn(norm1(h)) ; h2 = a + h ; out = mlp(norm2(h2))
+  parallel   (phi):          h = x + res ; n = norm(h)        ; out = attn(n) + mlp(n)
+  parallel   (gpt_neox):     h = x + res ; out = attn(norm1(h)) + mlp(norm2(h))
+
+The residual add is fused into the next norm kernel (``ops.rms_norm(x, w, eps, residual)``),
+so each layer returns ``(x, residual)`` and never materialises the sum separately.
+Weights use fused layouts: qkv = [q heads | k heads | v heads] rows, GLU up = [gate | up] rows.
+
+The KV cache is head-major ``[B, Hkv, S, D]`` per layer (edgellm.engine.kv_cache) so that
+HeadInfer-style head offload is a contiguous copy.  A model can be cut into pipeline stages
+(``stage(first, last)``): a stage owns layers [first, last), the embedding if first == 0 and
+the head if last == num_layers; it exchanges a single bf16 hidden tensor with its neighbours.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .configs import ModelConfig
+from .layers import Linear, Norm, QAct, act_fn, quant_if
+
+
+@dataclass
+class AttnCtx:
+    """Per-forward attention metadata.
+
+    mode       "prefill" (T tokens per sequence, causal over cache + new) or "decode" (T == 1)
+    start_pos  int32 [B]: cache position of the first new token of each sequence
+    seq_lens   int32 [B]: valid cache length after this forward (decode attention)
+    max_len    host-side upper bound of seq_lens (sizes the split-K grid; graph-capture bucket)
+    kv         object with ``layer(i) -> (k [B,Hkv,S,D], v)``, i = global layer index
+    """
+    mode: str
+    B: int
+    T: int
+    start_pos: torch.Tensor
+    seq_lens: torch.Tensor
+    max_len: int
+    kv: object
+    rope: Optional[torch.Tensor] = None
+    causal: bool = True
+    attn_hook: Optional[object] = None   # HeadInfer offload manager (edgellm.offload)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int, dtype, device):
+        super().__init__()
+        self.cfg, self.layer_idx = cfg, layer_idx
+        self.qkv = Linear(cfg.hidden_size, cfg.qkv_size, cfg.qkv_bias, dtype, device)
+        self.o = Linear(cfg.q_size, cfg.hidden_size, cfg.o_bias, dtype, device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    def forward(self, x, ctx: AttnCtx):
+        cfg = self.cfg
+        qkv = self.qkv(x)                                   # [B*T, qkv]
+        k_cache, v_cache = ctx.kv.layer(self.layer_idx)
+        rot = cfg.rotary_dim if cfg.pos_emb == "rope" else 0
+        if ctx.attn_hook is not None:
+            attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
+        else:
+            q = ops.rope_kv_write(qkv, ctx.start_pos, ctx.rope if rot else None, k_cache, v_cache,
+                                  cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, rot)  # [B,T,Hq,D]
+            if ctx.mode == "decode":
+                attn = ops.decode_attention(q.view(ctx.B, cfg.num_heads, cfg.head_dim), k_cache, v_cache,
+                                            ctx.seq_lens, self.scale, ctx.max_len)
+            else:
+                attn = ops.prefill_attention(q, k_cache, v_cache, ctx.start_pos, self.scale, ctx.causal)
+        attn = attn.reshape(ctx.B * ctx.T, cfg.q_size)
+        return self.o(quant_if(attn, self.o))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype, device):
+        super().__init__()
+        self.act = cfg.act
+        up_out = 2 * cfg.intermediate_size if cfg.is_glu else cfg.intermediate_size
+        self.up = Linear(cfg.hidden_size, up_out, cfg.mlp_bias, dtype, device)
+        self.down = Linear(cfg.intermediate_size, cfg.hidden_size, cfg.mlp_bias, dtype, device)
+
+    def forward(self, x):
+        h = self.up(x)
+        h = act_fn(h, self.act, getattr(self.down, "takes_quantized_input", False))
+        return self.down(h)
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, idx: int, dtype, device):
+        super().__init__()
+        self.cfg, self.idx = cfg, idx
+        self.norm1 = Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device)
+        self.norm2 = (None if cfg.shared_input_norm else Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device))
+        self.attn = Attention(cfg, idx, dtype, device)
+        self.mlp = MLP(cfg, dtype, device)
+
+    def forward(self, x, residual, ctx: AttnCtx):
+        cfg = self.cfg
+        qa = self.attn.qkv.takes_quantized_input
+        qm = self.mlp.up.takes_quantized_input
+        if not cfg.parallel_residual:
+            n1, h = self.norm1(x, residual, quant=qa)
+            a = self.attn(n1, ctx)
+            n2, h2 = self.norm2(a, h, quant=qm)
+            return self.mlp(n2), h2
+        if cfg.shared_input_norm:                      # phi
+            n, h = self.norm1(x, residual, quant=qa and qm)
+            if qa != qm:                               # mixed modes: feed each consumer its form
+                n, h = self.norm1(x, residual, quant=False)
+                na, nm = quant_if(n, self.attn.qkv), quant_if(n, self.mlp.up)
+            else:
+                na = nm = n
+            return self.attn(na, ctx) + self.mlp(nm), h
+        n1, h = self.norm1(x, residual, quant=qa)      # gpt_neox
+        n2, _ = self.norm2(h, None, quant=qm)
+        return self.attn(n1, ctx) + self.mlp(n2), h
+
+
+class DecoderLM(nn.Module):
+    """A (possibly partial) causal LM.  ``first``/``last`` select the layers this instance
+    owns; embedding and head are present only on the first / last stage."""
+
+    def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None, first: int = 0,
+                 last: Optional[int] = None):
+        super().__init__()
+        self.cfg = cfg
+        self.dtype = dtype
+        self.first = first
+        self.last = cfg.num_layers if last is None else last
+        self.has_embed = first == 0
+        self.has_head = self.last == cfg.num_layers
+        if self.has_embed:
+            self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size, dtype=dtype, device=device),
+                                      requires_grad=False)
+            self.pos_embed = (nn.Parameter(torch.empty(cfg.max_position_embeddings, cfg.hidden_size, dtype=dtype,
+                                                       device=device), requires_grad=False)
+                              if cfg.pos_emb == "learned" else None)
+        self.layers = nn.ModuleList([DecoderLayer(cfg, i, dtype, device) for i in range(self.first, self.last)])
+        if self.has_head:
+            self.final_norm = Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device)
+            if cfg.tie_word_embeddings and self.has_embed:
+                self.lm_head = None
+            else:
+                self.lm_head = Linear(cfg.hidden_size, cfg.vocab_size, cfg.lm_head_bias, dtype, device)
+        self._rope = None
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
+    def rope_table(self, device=None) -> Optional[torch.Tensor]:
+        cfg = self.cfg
+        if cfg.pos_emb != "rope":
+            return None
+        device = device or self.device
+        if self._rope is None or self._rope.device != torch.device(device):
+            self._rope = ops.rope_tables(cfg.rotary_dim, cfg.max_position_embeddings, cfg.rope_theta,
+                                         cfg.rope_scaling, device=device)
+        return self._rope
+
+    def head_weight(self) -> torch.Tensor:
+        return self.embed if self.lm_head is None else self.lm_head.weight
+
+    def embed_tokens(self, ids: torch.Tensor, start_pos: torch.Tensor) -> torch.Tensor:
+        """ids [B, T] -> hidden [B*T, H]"""
+        B, T = ids.shape
+        x = ops.embedding(ids.reshape(-1), self.embed)
+        if self.pos_embed is not None:
+            pos = (start_pos.long()[:, None] + torch.arange(T, device=ids.device)[None]).reshape(-1)
+            x = x + self.pos_embed[pos]
+        return x
+
+    # ------------------------------------------------------------------ forward
+    def forward_layers(self, x: torch.Tensor, ctx: AttnCtx, residual: Optional[torch.Tensor] = None):
+        for layer in self.layers:
+            x, residual = layer(x, residual, ctx)
+        return x, residual
+
+    def head(self, x: torch.Tensor, residual: Optional[torch.Tensor], ctx: AttnCtx,
+             logits: str = "last") -> torch.Tensor:
+        """Final norm + LM head. logits: "last" (one row per sequence) or "all"."""
+        if logits == "last" and ctx.T > 1:
+            idx = torch.arange(ctx.B, device=x.device) * ctx.T + (ctx.T - 1)
+            x = x.index_select(0, idx)
+            residual = residual.index_select(0, idx) if residual is not None else None
+        h, _ = self.final_norm(x, residual)
+        out = self.lm_head(h) if self.lm_head is not None else torch.nn.functional.linear(h, self.embed)
+        return out
+
+    def forward(self, ids: Optional[torch.Tensor], ctx: AttnCtx, hidden: Optional[torch.Tensor] = None,
+                logits: str = "last"):
+        """First stage: ids [B, T]; later stages: hidden [B*T, H] from the previous stage.
+        Returns logits on the last stage, otherwise the hidden handed to the next stage."""
+        x = self.embed_tokens(ids, ctx.start_pos) if self.has_embed else hidden
+        x, residual = self.forward_layers(x, ctx, None)
+        if self.has_head:
+            return self.head(x, residual, ctx, logits)
+        return x + residual if residual is not None else x
+
+
+# --------------------------------------------------------------------------- initialisation
+
+
+@torch.no_grad()
+def init_random_(model: DecoderLM, seed: int = 0, std: float = 0.02) -> DecoderLM:
+    """Random-init weights (HF-style N(0, 0.02), norms = 1, biases = 0), generated on the
+    model's device.  Used for benchmarks and tests (no checkpoints are downloaded)."""
+    for name, p in global_named_parameters(model):
+        if name.endswith("norm1.weight") or name.endswith("norm2.weight") or name.endswith("final_norm.weight"):
+            p.fill_(1.0)
+        elif name.endswith("bias"):
+            p.zero_()
+        else:
+            # seeded by the GLOBAL parameter name: a pipeline stage holding layers [a, b) gets
+            # bit-identical weights to the same layers of the unsplit model
+            g = torch.Generator(device=p.device).manual_seed((seed * 1000003 + zlib.crc32(name.encode())) % (2 ** 63))
+            p.copy_(torch.randn(p.shape, generator=g, device=p.device, dtype=torch.float32).mul_(std).to(p.dtype))
+    return model
+
+
+def global_named_parameters(model: DecoderLM):
+    """named_parameters() with layer indices rewritten to global layer numbers."""
+    for name, p in model.named_parameters():
+        if name.startswith("layers."):
+            _, local, rest = name.split(".", 2)
+            name = f"layers.{model.layers[int(local)].idx}.{rest}"
+        yield name, p
+
+
+def build_model(cfg: ModelConfig, dtype=torch.bfloat16, device=None, first: int = 0, last: Optional[int] = None,
+                seed: Optional[int] = 0) -> DecoderLM:
+    m = DecoderLM(cfg, dtype=dtype, device=device, first=first, last=last).eval()
+    if seed is not None:
+        init_random_(m, seed)
+    return m

@@ -1,0 +1,84 @@
+"""Building blocks shared by every decoder family.
+
+``Linear`` is the bf16 projection (a plain library GEMM: hipBLASLt through ``F.linear``);
+quantised replacements live in ``edgellm.quant`` and expose the same interface:
+
+    forward(x)                 -> y     x is bf16, or a QAct (int8 + per-token scale) when
+    takes_quantized_input      -> bool  the layer wants its producer to emit int8 directly
+                                        (the W8A8 fusion: norm/activation kernels quantise in
+                                        their epilogue, so no bf16 activation round trip).
+"""
+from __future__ import annotations
+
+from typing import NamedTuple, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+class QAct(NamedTuple):
+    """Per-token symmetric INT8 activation: x ~= q * scale[:, None]."""
+    q: torch.Tensor
+    scale: torch.Tensor
+
+
+class Linear(nn.Module):
+    takes_quantized_input = False
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = False, dtype=torch.bfloat16,
+                 device=None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=dtype, device=device),
+                                   requires_grad=False)
+        self.bias = (nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device), requires_grad=False)
+                     if bias else None)
+
+    def forward(self, x):
+        if isinstance(x, QAct):
+            x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
+        return F.linear(x, self.weight, self.bias)
+
+    def extra_repr(self):
+        return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, bf16"
+
+
+class Norm(nn.Module):
+    """RMSNorm or LayerNorm with fused residual add and optional fused INT8 quant epilogue."""
+
+    def __init__(self, hidden: int, kind: str, eps: float, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.kind, self.eps = kind, eps
+        self.weight = nn.Parameter(torch.ones(hidden, dtype=dtype, device=device), requires_grad=False)
+        self.bias = (nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device), requires_grad=False)
+                     if kind == "layer" else None)
+
+    def forward(self, x, residual=None, quant: bool = False):
+        """Returns (y, residual_out) where residual_out = x + residual; y is a QAct when quant."""
+        if self.kind == "rms":
+            if quant:
+                q, s, r = ops.rms_norm_quant(x, self.weight, self.eps, residual)
+                return QAct(q, s), r
+            return ops.rms_norm(x, self.weight, self.eps, residual)
+        if quant:
+            q, s, r = ops.layer_norm_quant(x, self.weight, self.bias, self.eps, residual)
+            return QAct(q, s), r
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual)
+
+
+def act_fn(x, act: str, quant: bool):
+    if quant:
+        q, s = ops.activation_quant(x, act)
+        return QAct(q, s)
+    return ops.activation(x, act)
+
+
+def quant_if(x: torch.Tensor, layer) -> object:
+    """Quantise a bf16 activation when the consumer wants INT8 input."""
+    if getattr(layer, "takes_quantized_input", False):
+        q, s = ops.quant_per_token(x)
+        return QAct(q, s)
+    return x

@@ -1,0 +1,201 @@
+"""edgellm op layer: every hot op of the decoder, one function each.
+
+GPU tensors run the hand-written CDNA4 kernels in ``ops/csrc`` (compiled in-tree to
+``ops/_C*.so`` by ``ops/build.py``); CPU tensors run the fp32 PyTorch reference in
+``ops/_ref.py`` (CPU plumbing configs and unit tests).  There is no silent fallback on the
+GPU: if the extension is missing or was built for another arch, GPU calls raise.
+Setting ``EDGELLM_REF_ON_GPU=1`` explicitly routes GPU tensors through the reference (used
+only for A/B numerics checks).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Optional, Tuple
+
+import torch
+
+from . import _ref
+
+_C = None
+_C_ERR: Optional[BaseException] = None
+
+
+def _load():
+    global _C, _C_ERR
+    if _C is None and _C_ERR is None:
+        try:
+            _C = importlib.import_module(__name__ + "._C")
+        except BaseException as e:  # noqa: BLE001 - re-raised on first GPU use
+            _C_ERR = e
+    return _C
+
+
+def ext():
+    """The compiled extension; raises with the import error when it is unavailable."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "edgellm HIP extension not available (build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f" or ops/build.py): {_C_ERR!r}")
+    return m
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+_REF_ON_GPU = os.environ.get("EDGELLM_REF_ON_GPU", "0") == "1"
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda and not _REF_ON_GPU
+
+
+# --------------------------------------------------------------------------- norms
+
+
+def rms_norm(x, weight, eps, residual=None):
+    if _gpu(x):
+        y, _, r = ext().norm(x, residual, weight, None, eps, True, False)
+        return y, r
+    return _ref.rms_norm(x, weight, eps, residual)
+
+
+def layer_norm(x, weight, bias, eps, residual=None):
+    if _gpu(x):
+        y, _, r = ext().norm(x, residual, weight, bias, eps, False, False)
+        return y, r
+    return _ref.layer_norm(x, weight, bias, eps, residual)
+
+
+def rms_norm_quant(x, weight, eps, residual=None):
+    if _gpu(x):
+        return ext().norm(x, residual, weight, None, eps, True, True)
+    return _ref.rms_norm_quant(x, weight, eps, residual)
+
+
+def layer_norm_quant(x, weight, bias, eps, residual=None):
+    if _gpu(x):
+        return ext().norm(x, residual, weight, bias, eps, False, True)
+    return _ref.layer_norm_quant(x, weight, bias, eps, residual)
+
+
+def quant_per_token(x):
+    if _gpu(x):
+        return ext().quant(x)
+    return _ref.quant_per_token(x)
+
+
+# --------------------------------------------------------------------------- activations
+_ACT_MODE = {"silu_glu": 0, "gelu_tanh": 1, "gelu": 2}
+
+
+def activation(x, act: str):
+    if _gpu(x):
+        return ext().act(x, _ACT_MODE[act], False)[0]
+    if act == "silu_glu":
+        return _ref.silu_mul(x)
+    return _ref.gelu(x, "tanh" if act == "gelu_tanh" else "none")
+
+
+def activation_quant(x, act: str):
+    if _gpu(x):
+        return ext().act(x, _ACT_MODE[act], True)
+    if act == "silu_glu":
+        return _ref.silu_mul_quant(x)
+    return _ref.gelu_quant(x, "tanh" if act == "gelu_tanh" else "none")
+
+
+# --------------------------------------------------------------------------- rope / attention
+
+
+def rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim, rotary_dim):
+    if _gpu(qkv):
+        return ext().rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim,
+                                   rotary_dim)
+    return _ref.rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim, rotary_dim)
+
+
+def decode_attention(q, k_cache, v_cache, seq_lens, scale, max_len_hint: Optional[int] = None):
+    if _gpu(q):
+        hint = int(max_len_hint) if max_len_hint is not None else int(k_cache.shape[2])
+        return ext().decode_attn(q, k_cache, v_cache, seq_lens, scale, hint)
+    return _ref.decode_attention(q, k_cache, v_cache, seq_lens, scale)
+
+
+def prefill_attention(q, k_cache, v_cache, start_pos, scale, causal=True):
+    if _gpu(q):
+        return ext().prefill_attn(q, k_cache, v_cache, start_pos, scale, causal)
+    return _ref.prefill_attention(q, k_cache, v_cache, start_pos, scale, causal)
+
+
+# --------------------------------------------------------------------------- INT8 GEMM
+
+
+def pack_int8_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] int8 -> MFMA-fragment-packed 1 KiB tiles (see csrc/gemm_i8.hip header).
+    N is padded to 16 and K to 64 with zeros."""
+    N, K = w.shape
+    NT, KT = (N + 15) // 16, (K + 63) // 64
+    wp = torch.zeros(NT * 16, KT * 64, dtype=torch.int8, device=w.device)
+    wp[:N, :K] = w
+    # [NT, n16, KT, kc4, b16] -> [NT, KT, kc4, n16, b16]
+    return wp.view(NT, 16, KT, 4, 16).permute(0, 2, 3, 1, 4).contiguous().view(-1)
+
+
+def unpack_int8_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    NT, KT = (N + 15) // 16, (K + 63) // 64
+    w = wp.view(NT, KT, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(NT * 16, KT * 64)
+    return w[:N, :K].contiguous()
+
+
+def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None):
+    """INT8 x INT8 -> int32 MFMA GEMM with per-token x per-channel dequant (+bias) -> bf16.
+    ``w_ref`` (canonical [N, K]) is only needed by the CPU path."""
+    if _gpu(qx):
+        return ext().w8a8_gemm(qx, x_scale, w_packed, w_scale, bias, N, K)
+    w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
+    shp = qx.shape[:-1]
+    out = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, torch.bfloat16)
+    return out.view(*shp, N)
+
+
+# --------------------------------------------------------------------------- sampling / misc
+
+
+def sample(logits, seen, temperature, top_k, top_p, repetition_penalty, rng: torch.Tensor,
+           do_sample: bool = True):
+    """Fused sampler. ``rng`` = int32 tensor [seed, step] on the logits' device (the step is
+    read on device so the launch is graph-capturable)."""
+    if _gpu(logits):
+        out = ext().sample(logits, seen, float(temperature), int(top_k or 0), float(top_p if top_p is not None else 1.0),
+                           float(repetition_penalty), bool(do_sample), rng)
+        if out.numel() > 0 or logits.shape[0] == 0:
+            return out
+        # top-p without top-k (or top-k > 1024): needs a full sort -> torch path on device
+        seed, step = (int(v) for v in rng.tolist())
+        tok = _ref.sample(logits, seen, temperature, top_k, top_p, repetition_penalty, seed, step, do_sample)
+        if seen is not None:
+            seen.scatter_(1, tok[:, None], 1)
+        return tok
+    seed, step = (int(v) for v in rng.tolist())
+    tok = _ref.sample(logits, seen, temperature, top_k, top_p, repetition_penalty, seed, step, do_sample)
+    if seen is not None:
+        seen.scatter_(1, tok[:, None], 1)
+    return tok
+
+
+def max_softmax_prob(logits):
+    if _gpu(logits):
+        return ext().max_prob(logits.contiguous())
+    return _ref.max_softmax_prob(logits)
+
+
+def embedding(ids, table):
+    if _gpu(table):
+        return ext().embedding(ids.long().contiguous(), table)
+    return _ref.embedding(ids, table)
+
+
+rope_tables = _ref.rope_tables

@@ -1,0 +1,269 @@
+// Split-K flash-decoding over a head-major KV cache.
+//
+// q [B, Hq, D] (one new token per sequence), caches [B, Hkv, S, D] with row stride D, valid
+// positions [0, seq_lens[b]).  Decode attention is HBM-bound on the K/V read, so the kernel is
+// shaped for streaming rather than MFMA: one workgroup = (split, kv-head, batch); its G = Hq/Hkv
+// query heads share every K/V row it loads (GQA reuse), and LPK lanes cooperate on one key row
+// (LPK*16 B contiguous per key, 1 KiB per wave-instruction at D=128 -> fully coalesced).
+//   phase 1: scores s[h][k] = q_h . k  -> LDS   (UNROLL rows in flight per lane)
+//   phase 2: per-head max / exp2 / sum in LDS (one wave per head)
+//   phase 3: acc[h][d] += p[h][k] * v[k][d], reduced over lanes, then over the 4 waves
+// With nsplit > 1 each split writes (acc, m, l) and a combine kernel merges them; with one
+// split the normalised output is written directly.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+constexpr int NW = NT / 64;
+constexpr int UNROLL = 4;
+
+template <int D> struct Lanes { static constexpr int v = (D / 8 <= 8) ? 8 : ((D / 8 <= 16) ? 16 : 32); };
+
+template <int D, int G, bool DIRECT>
+__global__ void __launch_bounds__(NT) decode_attn_kernel(
+    const bf16_t* __restrict__ q, int64_t q_sb, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    int64_t c_sb, int64_t c_sh, const int* __restrict__ seq_lens, float scale_log2, int CH, int nsplit,
+    bf16_t* __restrict__ out, int64_t o_sb, float* __restrict__ part_acc, float* __restrict__ part_ml) {
+  constexpr int LPK = Lanes<D>::v;        // lanes per key row
+  constexpr int KPW = 64 / LPK;           // keys per wave-instruction
+  constexpr int KPB = KPW * NW;           // keys per workgroup step
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sc = smem;                       // [G][CH]
+  float* red = smem + G * CH;             // [NW][G][D]
+  float* mstat = red + NW * G * D;        // [G]
+  float* lstat = mstat + G;               // [G]
+
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int Hq = gridDim.y * G;
+  const int len = seq_lens[b];
+  const int start = split * CH;
+  const int end = min(start + CH, len);
+  const int n = end - start;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int dl = lane % LPK, kl = lane / LPK;
+  const int d0 = dl * 8;
+  const bool dvalid = d0 < D;
+
+  if (n <= 0) {  // empty split (seq shorter than the grid's hint): publish an empty partial
+    if (!DIRECT) {
+      for (int i = threadIdx.x; i < G * D; i += NT) {
+        const int h = i / D, d = i - h * D;
+        part_acc[(((size_t)b * Hq + kvh * G + h) * nsplit + split) * D + d] = 0.f;
+      }
+      if (threadIdx.x < G) {
+        float* ml = part_ml + (((size_t)b * Hq + kvh * G + threadIdx.x) * nsplit + split) * 2;
+        ml[0] = -INFINITY; ml[1] = 0.f;
+      }
+    }
+    return;
+  }
+
+  const bf16_t* kb = kc + b * c_sb + kvh * c_sh + (size_t)start * D;
+  const bf16_t* vb = vc + b * c_sb + kvh * c_sh + (size_t)start * D;
+
+  float qf[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    if (dvalid) {
+      unpack8(*reinterpret_cast<const uint4*>(q + b * q_sb + (size_t)(kvh * G + h) * D + d0), qf[h]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[h][j] *= scale_log2;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[h][j] = 0.f;
+    }
+  }
+
+  // ---- phase 1: scores
+  for (int kb0 = wave * KPW; kb0 < n; kb0 += KPB * UNROLL) {  // wave-uniform trip count (shuffles inside)
+    const int k0 = kb0 + kl;
+    uint4 kv[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = k0 + u * KPB;
+      kv[u] = (dvalid && k < n) ? *reinterpret_cast<const uint4*>(kb + (size_t)k * D + d0) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      float kf[8];
+      unpack8(kv[u], kf);
+      float s[G];
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a += qf[h][j] * kf[j];
+        s[h] = a;
+      }
+#pragma unroll
+      for (int o = LPK / 2; o > 0; o >>= 1)
+#pragma unroll
+        for (int h = 0; h < G; ++h) s[h] += __shfl_xor(s[h], o, 64);
+      const int k = k0 + u * KPB;
+      if (dl == 0 && k < n) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) sc[h * CH + k] = s[h];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: softmax statistics per head (log2 domain)
+  for (int h = wave; h < G; h += NW) {
+    float m = -INFINITY;
+    for (int k = lane; k < n; k += 64) m = fmaxf(m, sc[h * CH + k]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int k = lane; k < n; k += 64) {
+      const float p = exp2f(sc[h * CH + k] - m);
+      sc[h * CH + k] = p;
+      l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) { mstat[h] = m; lstat[h] = l; }
+  }
+  __syncthreads();
+
+  // ---- phase 3: P.V
+  float acc[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
+  for (int kb0 = wave * KPW; kb0 < n; kb0 += KPB * UNROLL) {
+    const int k0 = kb0 + kl;
+    uint4 vv[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = k0 + u * KPB;
+      vv[u] = (dvalid && k < n) ? *reinterpret_cast<const uint4*>(vb + (size_t)k * D + d0) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = k0 + u * KPB;
+      if (k < n) {
+        float vf[8];
+        unpack8(vv[u], vf);
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          const float p = sc[h * CH + k];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[h][j] += p * vf[j];
+        }
+      }
+    }
+  }
+  // reduce over the KPW key groups of this wave (lanes sharing dl)
+#pragma unroll
+  for (int o = LPK; o < 64; o <<= 1)
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[h][j] += __shfl_xor(acc[h][j], o, 64);
+  if (kl == 0 && dvalid) {
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(wave * G + h) * D + d0 + j] = acc[h][j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * D; i += NT) {
+    const int h = i / D, d = i - h * D;
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) a += red[(w * G + h) * D + d];
+    const int hq = kvh * G + h;
+    if (DIRECT) {
+      out[b * o_sb + (size_t)hq * D + d] = f2bf(a / lstat[h]);
+    } else {
+      part_acc[(((size_t)b * Hq + hq) * nsplit + split) * D + d] = a;
+    }
+  }
+  if (!DIRECT && threadIdx.x < G) {
+    float* ml = part_ml + (((size_t)b * Hq + kvh * G + threadIdx.x) * nsplit + split) * 2;
+    ml[0] = mstat[threadIdx.x];
+    ml[1] = lstat[threadIdx.x];
+  }
+}
+
+__global__ void __launch_bounds__(256) decode_combine_kernel(const float* __restrict__ part_acc,
+                                                             const float* __restrict__ part_ml, int nsplit, int D,
+                                                             bf16_t* __restrict__ out, int64_t o_sb) {
+  const int hq = blockIdx.x, b = blockIdx.y, Hq = gridDim.x;
+  const float* ml = part_ml + ((size_t)b * Hq + hq) * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float L = 0.f;
+  for (int s = 0; s < nsplit; ++s)
+    if (ml[2 * s] != -INFINITY) L += exp2f(ml[2 * s] - M) * ml[2 * s + 1];
+  const float invL = 1.f / L;
+  const float* pa = part_acc + ((size_t)b * Hq + hq) * nsplit * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float a = 0.f;
+    for (int s = 0; s < nsplit; ++s)
+      if (ml[2 * s] != -INFINITY) a += exp2f(ml[2 * s] - M) * pa[(size_t)s * D + d];
+    out[b * o_sb + (size_t)hq * D + d] = f2bf(a * invL);
+  }
+}
+}  // namespace
+
+// Workspace sizes (floats) for a given launch; the binding allocates them.
+extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out) {
+  const int target_wg = 1024;
+  int per = B * Hkv;
+  int nsplit = (target_wg + per - 1) / per;
+  int ch = (max_len + nsplit - 1) / nsplit;
+  ch = ((ch + 63) / 64) * 64;
+  if (ch < 64) ch = 64;
+  if (ch > 1024) ch = 1024;
+  nsplit = (max_len + ch - 1) / ch;
+  if (nsplit < 1) nsplit = 1;
+  *ch_out = ch;
+  *nsplit_out = nsplit;
+  return 0;
+}
+
+extern "C" int edge_decode_attn(const void* q, int64_t q_sb, const void* k_cache, const void* v_cache, int64_t c_sb,
+                                int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale,
+                                int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
+                                hipStream_t st) {
+  if (B == 0) return 0;
+  const int G = Hq / Hkv;
+  if (G * Hkv != Hq) return -2;
+  const float sl2 = scale * 1.4426950408889634f;
+  const size_t lds = (size_t)(G * ch + NW * G * D + 2 * G) * sizeof(float);
+  const dim3 grid(nsplit, Hkv, B);
+  const bool direct = nsplit == 1;
+#define DLAUNCH(DD, GG)                                                                                       \
+  do {                                                                                                        \
+    if (direct)                                                                                               \
+      hipLaunchKernelGGL((decode_attn_kernel<DD, GG, true>), grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, \
+                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit,  \
+                         (bf16_t*)out, o_sb, part_acc, part_ml);                                              \
+    else                                                                                                      \
+      hipLaunchKernelGGL((decode_attn_kernel<DD, GG, false>), grid, dim3(NT), lds, st, (const bf16_t*)q,      \
+                         q_sb, (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, seq_lens, sl2, ch,  \
+                         nsplit, (bf16_t*)out, o_sb, part_acc, part_ml);                                      \
+  } while (0)
+#define GSW(DD)                                   \
+  switch (G) {                                    \
+    case 1: DLAUNCH(DD, 1); break;                \
+    case 2: DLAUNCH(DD, 2); break;                \
+    case 4: DLAUNCH(DD, 4); break;                \
+    case 8: DLAUNCH(DD, 8); break;                \
+    default: return -3;                           \
+  }
+  switch (D) {
+    case 64: GSW(64); break;
+    case 80: GSW(80); break;
+    case 128: GSW(128); break;
+    case 256: GSW(256); break;
+    default: return -4;
+  }
+#undef GSW
+#undef DLAUNCH
+  if (!direct)
+    hipLaunchKernelGGL(decode_combine_kernel, dim3(Hq, B), dim3(D <= 128 ? 128 : 256), 0, st, part_acc, part_ml, nsplit,
+                       D, (bf16_t*)out, o_sb);
+  return (int)hipGetLastError();
+}

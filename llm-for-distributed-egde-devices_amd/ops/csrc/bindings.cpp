@@ -1,0 +1,280 @@
+// Python bindings for the edgellm HIP kernels.
+// The kernels live in .hip translation units with plain C launchers (raw pointers + stream) so
+// they compile without torch headers; this file validates tensors, allocates outputs through
+// torch's caching allocator (graph-capture safe) and launches on torch's current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <optional>
+#include <tuple>
+
+extern "C" {
+int edge_norm(const void* x, const void* res, const void* w, const void* b, void* y, void* yq, float* ys,
+              void* res_out, int rows, int H, float eps, int rms, int quant, hipStream_t st);
+int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant, hipStream_t st);
+int edge_quant(const void* x, void* q, float* s, int rows, int H, hipStream_t st);
+int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, hipStream_t st);
+int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st);
+int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, void* q_out, void* k_cache,
+                       void* v_cache, int B, int T, int Hq, int Hkv, int D, int rot, int64_t c_sb, int64_t c_sh,
+                       int S, hipStream_t st);
+int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out);
+int edge_decode_attn(const void* q, int64_t q_sb, const void* k_cache, const void* v_cache, int64_t c_sb,
+                     int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch,
+                     int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml, hipStream_t st);
+int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
+                      const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
+                      int causal, hipStream_t st);
+int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                   int M, int N, int K, int KT, hipStream_t st);
+int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
+                float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
+                int64_t* out_tok, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "edgellm HIP kernel '", what, "' failed with code ", rc,
+              rc > 0 ? std::string(" (") + hipGetErrorString((hipError_t)rc) + ")" : std::string(""));
+}
+
+void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+int64_t rows_of(const at::Tensor& x) { return x.numel() / x.size(-1); }
+
+// ---------------------------------------------------------------------------------- norms
+std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Tensor& x,
+                                                                    const std::optional<at::Tensor>& residual,
+                                                                    const at::Tensor& w,
+                                                                    const std::optional<at::Tensor>& b, double eps,
+                                                                    bool rms, bool quant) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "weight");
+  const int64_t H = x.size(-1), R = rows_of(x);
+  TORCH_CHECK(w.numel() == H, "norm weight size mismatch");
+  if (b) { need(*b, at::kBFloat16, "bias"); TORCH_CHECK(b->numel() == H); }
+  at::Tensor res_out = x;
+  if (residual) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->sizes() == x.sizes(), "residual shape mismatch");
+    res_out = at::empty_like(x);
+  }
+  at::Tensor y, s;
+  if (quant) {
+    y = at::empty(x.sizes(), x.options().dtype(at::kChar));
+    auto ss = x.sizes().vec();
+    ss.pop_back();
+    s = at::empty(ss, x.options().dtype(at::kFloat));
+  } else {
+    y = at::empty_like(x);
+  }
+  check(edge_norm(x.data_ptr(), residual ? residual->data_ptr() : nullptr, w.data_ptr(),
+                  b ? b->data_ptr() : nullptr, quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr,
+                  quant ? s.data_ptr<float>() : nullptr, residual ? res_out.data_ptr() : nullptr, (int)R, (int)H,
+                  (float)eps, rms, quant, stream()),
+        "norm");
+  return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
+}
+
+// ---------------------------------------------------------------------------------- activations
+std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64_t mode, bool quant) {
+  need(x, at::kBFloat16, "x");
+  const int64_t W = x.size(-1), R = rows_of(x);
+  const int64_t F = mode == 0 ? W / 2 : W;
+  auto os = x.sizes().vec();
+  os.back() = F;
+  at::Tensor y, s;
+  if (quant) {
+    y = at::empty(os, x.options().dtype(at::kChar));
+    auto ss = os;
+    ss.pop_back();
+    s = at::empty(ss, x.options().dtype(at::kFloat));
+  } else {
+    y = at::empty(os, x.options());
+  }
+  check(edge_act(x.data_ptr(), quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr,
+                 quant ? s.data_ptr<float>() : nullptr, (int)R, (int)F, (int)mode, quant, stream()),
+        "act");
+  return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt};
+}
+
+std::tuple<at::Tensor, at::Tensor> quant(const at::Tensor& x) {
+  need(x, at::kBFloat16, "x");
+  const int64_t H = x.size(-1), R = rows_of(x);
+  auto q = at::empty(x.sizes(), x.options().dtype(at::kChar));
+  auto ss = x.sizes().vec();
+  ss.pop_back();
+  auto s = at::empty(ss, x.options().dtype(at::kFloat));
+  check(edge_quant(x.data_ptr(), q.data_ptr(), s.data_ptr<float>(), (int)R, (int)H, stream()), "quant");
+  return {q, s};
+}
+
+at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
+  need(ids, at::kLong, "ids");
+  need(table, at::kBFloat16, "table");
+  auto os = ids.sizes().vec();
+  os.push_back(table.size(1));
+  auto out = at::empty(os, table.options());
+  check(edge_embedding(ids.data_ptr<int64_t>(), table.data_ptr(), out.data_ptr(), (int)ids.numel(),
+                       (int)table.size(1), (int)table.size(0), stream()),
+        "embedding");
+  return out;
+}
+
+at::Tensor max_prob(const at::Tensor& logits) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous());
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
+  const int64_t V = logits.size(-1), R = rows_of(logits);
+  auto os = logits.sizes().vec();
+  os.pop_back();
+  auto out = at::empty(os, logits.options().dtype(at::kFloat));
+  check(edge_max_prob(logits.data_ptr(), out.data_ptr<float>(), (int)R, (int)V, bf, stream()), "max_prob");
+  return out;
+}
+
+// ---------------------------------------------------------------------------------- rope + kv
+void check_cache(const at::Tensor& c, const char* name, int64_t D) {
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(c.dim() == 4 && c.size(3) == D && c.stride(3) == 1 && c.stride(2) == D,
+              name, " must be [B, Hkv, S, D] with contiguous rows");
+}
+
+at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, const std::optional<at::Tensor>& rope,
+                         at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot) {
+  need(qkv, at::kBFloat16, "qkv");
+  need(start_pos, at::kInt, "start_pos");
+  check_cache(k_cache, "k_cache", D);
+  check_cache(v_cache, "v_cache", D);
+  TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.sizes() == v_cache.sizes());
+  const int64_t B = k_cache.size(0);
+  TORCH_CHECK(start_pos.numel() == B, "start_pos must have one entry per cache row");
+  TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D && k_cache.size(1) == Hkv);
+  const int64_t ntok = rows_of(qkv);
+  TORCH_CHECK(ntok % B == 0, "qkv rows must be B*T");
+  const int64_t T = ntok / B;
+  if (rot > 0) {
+    TORCH_CHECK(rope.has_value(), "rope table required when rot > 0");
+    need(*rope, at::kFloat, "rope");
+    TORCH_CHECK(rope->size(1) == rot / 2);
+  }
+  auto q = at::empty({B, T, Hq, D}, qkv.options());
+  check(edge_rope_kv_write(qkv.data_ptr(), start_pos.data_ptr<int>(), rot > 0 ? rope->data_ptr<float>() : nullptr,
+                           q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), (int)B, (int)T, (int)Hq, (int)Hkv,
+                           (int)D, (int)rot, k_cache.stride(0), k_cache.stride(1), (int)k_cache.size(2), stream()),
+        "rope_kv_write");
+  return q;
+}
+
+// ---------------------------------------------------------------------------------- attention
+at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                       const at::Tensor& seq_lens, double scale, int64_t max_len_hint) {
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && q.dim() == 3, "q must be bf16 [B, Hq, D]");
+  TORCH_CHECK(q.stride(2) == 1 && q.stride(1) == q.size(2), "q heads must be contiguous");
+  const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
+  check_cache(k_cache, "k_cache", D);
+  check_cache(v_cache, "v_cache", D);
+  TORCH_CHECK(k_cache.strides() == v_cache.strides());
+  need(seq_lens, at::kInt, "seq_lens");
+  TORCH_CHECK(seq_lens.numel() == B && k_cache.size(0) == B);
+  const int64_t Hkv = k_cache.size(1);
+  TORCH_CHECK(max_len_hint > 0 && max_len_hint <= k_cache.size(2), "max_len_hint out of range");
+  int ch = 0, nsplit = 0;
+  edge_decode_attn_plan((int)B, (int)Hkv, (int)max_len_hint, &ch, &nsplit);
+  auto out = at::empty({B, Hq, D}, q.options());
+  at::Tensor pacc, pml;
+  if (nsplit > 1) {
+    pacc = at::empty({B, Hq, nsplit, D}, q.options().dtype(at::kFloat));
+    pml = at::empty({B, Hq, nsplit, 2}, q.options().dtype(at::kFloat));
+  }
+  check(edge_decode_attn(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0),
+                         k_cache.stride(1), seq_lens.data_ptr<int>(), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                         ch, nsplit, out.data_ptr(), out.stride(0), nsplit > 1 ? pacc.data_ptr<float>() : nullptr,
+                         nsplit > 1 ? pml.data_ptr<float>() : nullptr, stream()),
+        "decode_attn");
+  return out;
+}
+
+at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                        const at::Tensor& start_pos, double scale, bool causal) {
+  need(q, at::kBFloat16, "q");
+  TORCH_CHECK(q.dim() == 4, "q must be [B, T, Hq, D]");
+  const int64_t B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3);
+  check_cache(k_cache, "k_cache", D);
+  check_cache(v_cache, "v_cache", D);
+  TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.size(0) == B);
+  need(start_pos, at::kInt, "start_pos");
+  TORCH_CHECK(start_pos.numel() == B);
+  auto out = at::empty_like(q);
+  check(edge_prefill_attn(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1),
+                          start_pos.data_ptr<int>(), out.data_ptr(), (int)B, (int)T, (int)Hq, (int)k_cache.size(1),
+                          (int)D, (float)scale, causal, stream()),
+        "prefill_attn");
+  return out;
+}
+
+// ---------------------------------------------------------------------------------- int8 gemm
+at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
+                     const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  need(a, at::kChar, "a");
+  need(sa, at::kFloat, "a_scale");
+  need(wp, at::kChar, "w_packed");
+  need(sw, at::kFloat, "w_scale");
+  TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
+  const int64_t M = rows_of(a);
+  TORCH_CHECK(sa.numel() == M && sw.numel() == N);
+  const int64_t KT = (K + 63) / 64, NTt = (N + 15) / 16;
+  TORCH_CHECK(wp.numel() == NTt * KT * 1024, "packed weight has wrong size");
+  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+  auto os = a.sizes().vec();
+  os.back() = N;
+  auto out = at::empty(os, a.options().dtype(at::kBFloat16));
+  check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                       bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N, (int)K, (int)KT, stream()),
+        "w8a8_gemm");
+  return out;
+}
+
+// ---------------------------------------------------------------------------------- sampler
+// Returns an empty tensor when the configuration needs the host fallback.
+at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& seen, double temperature,
+                  int64_t top_k, double top_p, double penalty, bool do_sample, const at::Tensor& rng) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat);
+  need(rng, at::kInt, "rng");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  if (seen) { need(*seen, at::kByte, "seen"); TORCH_CHECK(seen->sizes() == logits.sizes()); }
+  auto out = at::empty({B}, logits.options().dtype(at::kLong));
+  const double inv_t = temperature > 0 ? 1.0 / temperature : 1.0;
+  const int rc = edge_sample(logits.data_ptr(), bf, seen ? seen->data_ptr<uint8_t>() : nullptr, (int)B, (int)V,
+                             (float)temperature, (float)inv_t, (float)penalty, (int)top_k, (float)top_p, do_sample,
+                             rng.data_ptr<int>(), out.data_ptr<int64_t>(), stream());
+  if (rc == -5) return at::Tensor();
+  check(rc, "sample");
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "edgellm CDNA4 (gfx950) HIP kernels";
+  m.def("norm", &norm);
+  m.def("act", &act);
+  m.def("quant", &quant);
+  m.def("embedding", &embedding);
+  m.def("max_prob", &max_prob);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("decode_attn", &decode_attn);
+  m.def("prefill_attn", &prefill_attn);
+  m.def("w8a8_gemm", &w8a8_gemm);
+  m.def("sample", &sample);
+}

@@ -1,0 +1,217 @@
+// W8A8 INT8 GEMM on CDNA4 MFMA (v_mfma_i32_16x16x64_i8) with fused dequant epilogue.
+//   out[m][n] = (sum_k A[m][k] * W[n][k]) * a_scale[m] * w_scale[n] (+ bias[n])   -> bf16
+// the kernel behind both the SmoothQuant W8A8 mode and the LLM.int8 inlier GEMM.
+//
+// Weight layout ("MFMA-packed"): the [N, K] int8 matrix is stored as 1 KiB tiles of
+// 16 output channels x 64 k; tile (nt, kt) sits at byte ((nt * KT) + kt) * 1024 and lane l's
+// 16 bytes are W[nt*16 + (l & 15)][kt*64 + 16*(l >> 4) .. +16] — exactly the B fragment of
+// the i8 16x16x64 MFMA, so a wave fetches one fragment with one fully-coalesced 1 KiB load
+// and a workgroup streams a column panel as one contiguous byte range.  A (activations) is
+// row-major [M, K]; its fragment is lane l <- A[m0 + (l & 15)][k0 + 16*(l >> 4) .. +16].
+// Both operands use the same (lane, byte) -> k map, so the MFMA sums the right products.
+//
+// Kernels:
+//   gemv:  M <= 64 per block-row (decode). HBM-bound on W: each workgroup owns one 16-column
+//          panel, its 4 waves split K and keep UNROLL fragments in flight (no LDS staging:
+//          the weights are read exactly once), partial sums reduced through LDS.
+//   tiled: M > 64 (prefill). 128x128 block tile, BK=64, 4 waves in 2x2, A and B staged with
+//          global_load_lds (16 B/lane, lane-linear fragment-ordered LDS images -> conflict-free
+//          ds_read_b128), LDS double buffer.
+#include "common.h"
+
+namespace {
+constexpr int NT = 256;
+
+__device__ __forceinline__ v4i mfma_i8(const v4i& a, const v4i& b, const v4i& c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void store_out(bf16_t* __restrict__ out, int M, int N, int row, int col, int acc,
+                                          const float* __restrict__ sa, const float* __restrict__ sw,
+                                          const bf16_t* __restrict__ bias) {
+  if (row < M && col < N) {
+    float v = (float)acc * sa[row] * sw[col];
+    if (bias) v += bf2f(bias[col]);
+    out[(size_t)row * N + col] = f2bf(v);
+  }
+}
+
+// ------------------------------------------------------------------------------------ gemv
+template <int MT, int UNROLL>
+__global__ void __launch_bounds__(NT) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                       const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                       const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                       int M, int N, int K, int KT) {
+  __shared__ v4i red[4][MT][64];
+  const int nt = blockIdx.x;
+  const int m0 = blockIdx.y * (16 * MT);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kt0 = (KT * wave) / 4, kt1 = (KT * (wave + 1)) / 4;
+  const int arow = lane & 15, akc = 16 * (lane >> 4);
+
+  v4i acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = v4i{0, 0, 0, 0};
+
+  const v4i* wp = reinterpret_cast<const v4i*>(Wp + ((size_t)nt * KT) * 1024) + lane;
+  const int8_t* arows[MT];
+  bool aval[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int r = m0 + i * 16 + arow;
+    aval[i] = r < M;
+    arows[i] = A + (size_t)(aval[i] ? r : 0) * K;
+  }
+
+  for (int kt = kt0; kt < kt1; kt += UNROLL) {
+    v4i b[UNROLL];
+    v4i a[UNROLL][MT];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = kt + u;
+      b[u] = (k < kt1) ? __builtin_nontemporal_load(wp + (size_t)k * 64) : v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int kk = (kt + u) * 64 + akc;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        if (aval[i] && kt + u < kt1 && kk + 16 <= K) a[u][i] = *reinterpret_cast<const v4i*>(arows[i] + kk);
+        else if (aval[i] && kt + u < kt1 && kk < K) {
+          // ragged K tail (K % 16 != 0): byte-wise, zero padded
+          int8_t t[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = (kk + j < K) ? arows[i][kk + j] : 0;
+          a[u][i] = *reinterpret_cast<v4i*>(t);
+        } else a[u][i] = v4i{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[i] = mfma_i8(a[u][i], b[u], acc[i]);
+  }
+
+#pragma unroll
+  for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
+  __syncthreads();
+  // 4 waves -> each wave finalises MT/4.. m-tiles round-robin
+  for (int i = wave; i < MT; i += 4) {
+    v4i s = red[0][i][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) s += red[w][i][lane];
+    const int col = nt * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store_out(out, M, N, m0 + i * 16 + 4 * (lane >> 4) + j, col, s[j], sa, sw, bias);
+  }
+}
+
+// ------------------------------------------------------------------------------------ tiled
+// Block tile 128 x 128, BK = 64. LDS image per buffer: A 8 x 1 KiB fragments, B 8 x 1 KiB.
+constexpr int BM = 128, BN = 128;
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+__global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                             const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                             int M, int N, int K, int KT, int NTt, int grid_n) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];  // 2 x (8 KiB A + 8 KiB B)
+  // XCD-aware remap: consecutive dispatch ids round-robin over 8 XCDs; give each XCD a
+  // contiguous run of tiles along N so blocks sharing an A panel share an L2.
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  int wgid = orig;
+  if (nwg % 8 == 0) wgid = (orig % 8) * (nwg / 8) + orig / 8;
+  const int bn = wgid % grid_n, bm = wgid / grid_n;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;   // 2 x 2 waves, 64 x 64 each
+
+  // per-lane global sources for this wave's 2 A fragments and 2 B fragments
+  const int8_t* asrc[2];
+  const int8_t* bsrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int msub = wave * 2 + j;                       // 0..7
+    int r = bm * BM + msub * 16 + (lane & 15);
+    r = r < M ? r : M - 1;
+    asrc[j] = A + (size_t)r * K + 16 * (lane >> 4);
+    int ntile = bn * (BN / 16) + wave * 2 + j;            // 0..NTt-1
+    ntile = ntile < NTt ? ntile : NTt - 1;
+    bsrc[j] = Wp + ((size_t)ntile * KT) * 1024 + lane * 16;
+  }
+
+  auto stage = [&](int buf, int kt) {
+    int8_t* base = smem + buf * 16384;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      glds16(asrc[j] + (size_t)kt * 64, base + (wave * 2 + j) * 1024);
+      glds16(bsrc[j] + (size_t)kt * 1024, base + 8192 + (wave * 2 + j) * 1024);
+    }
+  };
+
+  v4i acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + 1 < KT) stage(cur ^ 1, kt + 1);
+    const int8_t* base = smem + cur * 16384;
+    v4i a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v4i*>(base + (wm * 4 + i) * 1024 + lane * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const v4i*>(base + 8192 + (wn * 4 + j) * 1024 + lane * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_i8(a[i], b[j], acc[i][j]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = bn * BN + (wn * 4 + j) * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm * BM + (wm * 4 + i) * 16 + 4 * (lane >> 4) + r;
+        store_out(out, M, N, row, col, acc[i][j][r], sa, sw, bias);
+      }
+    }
+}
+}  // namespace
+
+extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
+                              void* out, int M, int N, int K, int KT, hipStream_t st) {
+  if (M == 0 || N == 0) return 0;
+  const int NTt = (N + 15) / 16;
+  if (M > 64 && K % 64 == 0 && K / 64 == KT) {
+    const int grid_n = (NTt * 16 + BN - 1) / BN;
+    const int grid_m = (M + BM - 1) / BM;
+    hipLaunchKernelGGL(w8a8_gemm_tiled_kernel, dim3(grid_n * grid_m), dim3(NT), 2 * 16384, st, (const int8_t*)A, sa,
+                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_n);
+    return (int)hipGetLastError();
+  }
+  const int mblocks16 = (M + 15) / 16;
+  constexpr int U = 8;
+#define GEMV(MT)                                                                                             \
+  hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U>), dim3(NTt, (M + 16 * MT - 1) / (16 * MT)), dim3(NT), 0, st,    \
+                     (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT)
+  if (mblocks16 <= 1) GEMV(1);
+  else if (mblocks16 <= 2) GEMV(2);
+  else GEMV(4);
+#undef GEMV
+  return (int)hipGetLastError();
+}

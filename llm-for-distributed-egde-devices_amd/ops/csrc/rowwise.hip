@@ -1,0 +1,304 @@
+// Row-wise memory-bound kernels (one 256-thread workgroup per row, 16-byte vector I/O).
+//   * RMSNorm / LayerNorm with fused residual add            
+//   * the same with a fused per-token symmetric INT8 quant   (W8A8 activation quant)
+//   * SiLU*mul (SwiGLU) and GELU (tanh / erf), optional quant (K7)
+//   * per-token INT8 quant of a bf16 row
+//   * embedding gather (K1), max-softmax-probability "confidence" reduction (K13)
+// Every row is held in registers between its reduction and its write: one HBM read and one
+// write per element (Guideline 13: bf16 always moved as 8-element uint4).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <int NCH>
+struct Row {
+  float v[NCH][8];
+};
+
+// Load a bf16 row (optionally + residual) into registers. Elements >= H read as 0.
+template <int NCH>
+__device__ __forceinline__ void load_row(const bf16_t* __restrict__ x, int H, float (&v)[NCH][8]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * NT + threadIdx.x) * 8;
+    if (e < H) {
+      uint4 u = *reinterpret_cast<const uint4*>(x + e);
+      unpack8(u, v[c]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void store_row(bf16_t* __restrict__ y, int H, const float (&v)[NCH][8]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * NT + threadIdx.x) * 8;
+    if (e < H) *reinterpret_cast<uint4*>(y + e) = pack8(v[c]);
+  }
+}
+
+// Quantise registers to int8 with a per-row scale (block-reduced absmax).
+template <int NCH>
+__device__ __forceinline__ void quant_store(float (&v)[NCH][8], int H, int8_t* __restrict__ q,
+                                            float* __restrict__ scale_out, float* red) {
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[c][j]));
+  amax = block_max<NT>(amax, red);
+  amax = fmaxf(amax, 1e-8f);
+  const float scale = amax / 127.f;
+  const float inv = 127.f / amax;
+  if (threadIdx.x == 0) *scale_out = scale;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * NT + threadIdx.x) * 8;
+    if (e < H) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[c][j], inv)) << (8 * j);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[c][4 + j], inv)) << (8 * j);
+      *reinterpret_cast<uint2*>(q + e) = make_uint2(lo, hi);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- norms
+template <int NCH, bool RMS, bool HAS_RES, bool QUANT>
+__global__ void __launch_bounds__(NT) norm_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ b, bf16_t* __restrict__ y, int8_t* __restrict__ yq,
+    float* __restrict__ ys, bf16_t* __restrict__ res_out, int H, float eps) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  float v[NCH][8];
+  load_row<NCH>(x + row * H, H, v);
+  if constexpr (HAS_RES) {
+    float r[NCH][8];
+    load_row<NCH>(res + row * H, H, r);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] += r[c][j];
+    // the residual stream is kept in bf16 (as HF does); normalise the rounded value
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * NT + threadIdx.x) * 8;
+      if (e < H) {
+        uint4 u = pack8(v[c]);
+        *reinterpret_cast<uint4*>(res_out + row * H + e) = u;
+        unpack8(u, v[c]);
+      }
+    }
+  }
+  float mean = 0.f;
+  if constexpr (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    mean = block_sum<NT>(s, red) / (float)H;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * NT + threadIdx.x) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = (e < H) ? v[c][j] - mean : 0.f;
+      ss += d * d;
+    }
+  }
+  const float rstd = rsqrtf(block_sum<NT>(ss, red) / (float)H + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * NT + threadIdx.x) * 8;
+    if (e < H) {
+      float wf[8], bfv[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + e), wf);
+      if constexpr (!RMS) {
+        if (b != nullptr) unpack8(*reinterpret_cast<const uint4*>(b + e), bfv);
+        else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bfv[j] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = (v[c][j] - mean) * rstd * wf[j];
+        if constexpr (!RMS) t += bfv[j];
+        v[c][j] = t;
+      }
+    }
+  }
+  if constexpr (QUANT) {
+    quant_store<NCH>(v, H, yq + row * H, ys + row, red);
+  } else {
+    store_row<NCH>(y + row * H, H, v);
+  }
+}
+
+// ----------------------------------------------------------------------------- activations
+// MODE 0: silu(gate)*up with input [gate | up] of width 2F; 1: gelu tanh; 2: gelu erf
+template <int NCH, int MODE, bool QUANT>
+__global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                 int8_t* __restrict__ yq, float* __restrict__ ys, int F) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  float v[NCH][8];
+  if constexpr (MODE == 0) {
+    const bf16_t* xr = x + row * (size_t)(2 * F);
+    float u[NCH][8];
+    load_row<NCH>(xr, F, v);
+    load_row<NCH>(xr + F, F, u);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = v[c][j];
+        v[c][j] = g / (1.f + __expf(-g)) * u[c][j];
+      }
+  } else {
+    load_row<NCH>(x + row * (size_t)F, F, v);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = v[c][j];
+        if constexpr (MODE == 1) {
+          const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+          v[c][j] = 0.5f * a * (1.f + tanhf(k0 * (a + k1 * a * a * a)));
+        } else {
+          v[c][j] = 0.5f * a * (1.f + erff(a * 0.7071067811865476f));
+        }
+      }
+  }
+  if constexpr (QUANT) quant_store<NCH>(v, F, yq + row * (size_t)F, ys + row, red);
+  else store_row<NCH>(y + row * (size_t)F, F, v);
+}
+
+template <int NCH>
+__global__ void __launch_bounds__(NT) quant_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
+                                                   float* __restrict__ s, int H) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  float v[NCH][8];
+  load_row<NCH>(x + row * (size_t)H, H, v);
+  quant_store<NCH>(v, H, q + row * (size_t)H, s + row, red);
+}
+
+// ----------------------------------------------------------------------------- embedding
+__global__ void __launch_bounds__(NT) embed_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
+                                                   bf16_t* __restrict__ out, int H, int V) {
+  const size_t row = blockIdx.x;
+  int64_t id = ids[row];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)id * H);
+  uint4* dst = reinterpret_cast<uint4*>(out + row * H);
+  for (int e = threadIdx.x; e < H / 8; e += NT) dst[e] = src[e];
+}
+
+// ----------------------------------------------------------------------------- confidence
+// out[row] = max_v softmax(l)[v] = 1 / sum_v exp(l_v - max)   (online, one pass)
+template <bool BF16>
+__global__ void __launch_bounds__(NT) max_prob_kernel(const void* __restrict__ logits, float* __restrict__ out, int V) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  float m = -INFINITY, s = 0.f;
+  for (int i = threadIdx.x; i < V; i += NT) {
+    float l;
+    if constexpr (BF16) l = bf2f(reinterpret_cast<const bf16_t*>(logits)[row * V + i]);
+    else l = reinterpret_cast<const float*>(logits)[row * V + i];
+    if (l > m) { s = s * __expf(m - l) + 1.f; m = l; }
+    else s += __expf(l - m);
+  }
+  const float gm = block_max<NT>(m, red);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+  s = block_sum<NT>(s, red);
+  if (threadIdx.x == 0) out[row] = 1.f / s;
+}
+
+}  // namespace
+
+// ============================================================================= launchers
+#define NCH_DISPATCH(H, ...)                                        \
+  do {                                                              \
+    const int need = ((H) + NT * 8 - 1) / (NT * 8);                 \
+    if (need <= 1) { constexpr int NCH = 1; __VA_ARGS__; }          \
+    else if (need <= 2) { constexpr int NCH = 2; __VA_ARGS__; }     \
+    else if (need <= 4) { constexpr int NCH = 4; __VA_ARGS__; }     \
+    else if (need <= 8) { constexpr int NCH = 8; __VA_ARGS__; }     \
+    else return -1;                                                 \
+  } while (0)
+
+extern "C" int edge_norm(const void* x, const void* res, const void* w, const void* b, void* y, void* yq,
+                         float* ys, void* res_out, int rows, int H, float eps, int rms, int quant,
+                         hipStream_t st) {
+  if (H % 8) return -2;
+  if (rows == 0) return 0;
+  const bf16_t *X = (const bf16_t*)x, *R = (const bf16_t*)res, *W = (const bf16_t*)w, *Bb = (const bf16_t*)b;
+  bf16_t *Y = (bf16_t*)y, *RO = (bf16_t*)res_out;
+  int8_t* Q = (int8_t*)yq;
+#define LAUNCH_NORM(RMS, HR, QU) \
+  hipLaunchKernelGGL((norm_kernel<NCH, RMS, HR, QU>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, eps)
+  NCH_DISPATCH(H, {
+    if (rms) {
+      if (res) { if (quant) LAUNCH_NORM(true, true, true); else LAUNCH_NORM(true, true, false); }
+      else { if (quant) LAUNCH_NORM(true, false, true); else LAUNCH_NORM(true, false, false); }
+    } else {
+      if (res) { if (quant) LAUNCH_NORM(false, true, true); else LAUNCH_NORM(false, true, false); }
+      else { if (quant) LAUNCH_NORM(false, false, true); else LAUNCH_NORM(false, false, false); }
+    }
+  });
+#undef LAUNCH_NORM
+  return (int)hipGetLastError();
+}
+
+extern "C" int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant,
+                        hipStream_t st) {
+  if (F % 8) return -2;
+  if (rows == 0) return 0;
+  const bf16_t* X = (const bf16_t*)x;
+  bf16_t* Y = (bf16_t*)y;
+  int8_t* Q = (int8_t*)yq;
+#define LAUNCH_ACT(M, QU) hipLaunchKernelGGL((act_kernel<NCH, M, QU>), dim3(rows), dim3(NT), 0, st, X, Y, Q, ys, F)
+  NCH_DISPATCH(F, {
+    if (mode == 0) { if (quant) LAUNCH_ACT(0, true); else LAUNCH_ACT(0, false); }
+    else if (mode == 1) { if (quant) LAUNCH_ACT(1, true); else LAUNCH_ACT(1, false); }
+    else { if (quant) LAUNCH_ACT(2, true); else LAUNCH_ACT(2, false); }
+  });
+#undef LAUNCH_ACT
+  return (int)hipGetLastError();
+}
+
+extern "C" int edge_quant(const void* x, void* q, float* s, int rows, int H, hipStream_t st) {
+  if (H % 8) return -2;
+  if (rows == 0) return 0;
+  NCH_DISPATCH(H, {
+    hipLaunchKernelGGL((quant_kernel<NCH>), dim3(rows), dim3(NT), 0, st, (const bf16_t*)x, (int8_t*)q, s, H);
+  });
+  return (int)hipGetLastError();
+}
+
+extern "C" int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V,
+                              hipStream_t st) {
+  if (H % 8) return -2;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, (bf16_t*)out, H, V);
+  return (int)hipGetLastError();
+}
+
+extern "C" int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st) {
+  if (rows == 0) return 0;
+  if (is_bf16) hipLaunchKernelGGL((max_prob_kernel<true>), dim3(rows), dim3(NT), 0, st, logits, out, V);
+  else hipLaunchKernelGGL((max_prob_kernel<false>), dim3(rows), dim3(NT), 0, st, logits, out, V);
+  return (int)hipGetLastError();
+}

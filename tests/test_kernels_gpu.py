@@ -1,0 +1,210 @@
+"""Numerics of every HIP kernel against the fp32 PyTorch reference (ops/_ref.py).
+
+Run on the MI355X box: ``python -m pytest tests -m gpu``.  Each test calls the extension
+directly (``edgellm.ops.ext()``) so a missing/broken build fails loudly instead of
+silently testing the reference against itself.
+"""
+import math
+
+import pytest
+import torch
+
+from edgellm import ops
+from edgellm.ops import _ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} / {a.numel()} elements off, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("H", [128, 2048, 4096, 5120, 11008])
+@pytest.mark.parametrize("rms", [True, False])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_norm(cuda, H, rms, with_res):
+    C = ops.ext()
+    torch.manual_seed(0)
+    x = torch.randn(7, H, device=cuda, dtype=torch.bfloat16)
+    r = torch.randn(7, H, device=cuda, dtype=torch.bfloat16) if with_res else None
+    w = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    b = None if rms else torch.randn(H, device=cuda).bfloat16()
+    y, _, ro = C.norm(x, r, w, b, 1e-5, rms, False)
+    if rms:
+        yr, ror = _ref.rms_norm(x, w, 1e-5, r)
+    else:
+        yr, ror = _ref.layer_norm(x, w, b, 1e-5, r)
+    _close(y, yr, 2e-2, 1e-2)
+    _close(ro, ror, 0)
+    q, s, ro2 = C.norm(x, r, w, b, 1e-5, rms, True)
+    if rms:
+        qr, sr, _ = _ref.rms_norm_quant(x, w, 1e-5, r)
+    else:
+        qr, sr, _ = _ref.layer_norm_quant(x, w, b, 1e-5, r)
+    _close(s, sr, 0, 1e-3)
+    assert (q.int() - qr.int().to(cuda)).abs().max().item() <= 1
+
+
+@pytest.mark.parametrize("mode,act", [(0, "silu_glu"), (1, "gelu_tanh"), (2, "gelu")])
+@pytest.mark.parametrize("F", [256, 8192, 11008])
+def test_act(cuda, mode, act, F):
+    C = ops.ext()
+    W = 2 * F if mode == 0 else F
+    x = torch.randn(5, W, device=cuda, dtype=torch.bfloat16) * 2
+    y, _ = C.act(x, mode, False)
+    yr = _ref.silu_mul(x) if mode == 0 else _ref.gelu(x, "tanh" if mode == 1 else "none")
+    _close(y, yr, 2e-2, 1e-2)
+    q, s = C.act(x, mode, True)
+    qr, sr = _ref.silu_mul_quant(x) if mode == 0 else _ref.gelu_quant(x, "tanh" if mode == 1 else "none")
+    _close(s, sr, 0, 2e-3)
+    assert (q.int() - qr.int()).abs().max().item() <= 1
+
+
+def test_quant_embedding_maxprob(cuda):
+    C = ops.ext()
+    x = torch.randn(9, 4096, device=cuda, dtype=torch.bfloat16)
+    q, s = C.quant(x)
+    qr, sr = _ref.quant_per_token(x)
+    _close(s, sr, 0, 1e-6)
+    assert (q.int() - qr.int()).abs().max().item() <= 1
+    table = torch.randn(1000, 256, device=cuda).bfloat16()
+    ids = torch.randint(0, 1000, (3, 5), device=cuda)
+    assert torch.equal(C.embedding(ids, table), table[ids])
+    logits = torch.randn(6, 50304, device=cuda) * 3
+    _close(C.max_prob(logits), _ref.max_softmax_prob(logits), 1e-6, 1e-4)
+    _close(C.max_prob(logits.bfloat16()), _ref.max_softmax_prob(logits.bfloat16()), 1e-6, 1e-4)
+
+
+@pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 32, 128, 128), (32, 8, 64, 64), (32, 32, 80, 32), (8, 8, 256, 64)])
+def test_rope_kv_write(cuda, Hq, Hkv, D, rot):
+    C = ops.ext()
+    B, T, S = 3, 5, 64
+    qkv = torch.randn(B * T, (Hq + 2 * Hkv) * D, device=cuda).bfloat16()
+    start = torch.tensor([0, 7, 30], device=cuda, dtype=torch.int32)
+    rope = _ref.rope_tables(rot, S, 10000.0, device=cuda)
+    kc = torch.zeros(B, Hkv, S, D, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kr, vr = kc.clone(), vc.clone()
+    q = C.rope_kv_write(qkv, start, rope, kc, vc, Hq, Hkv, D, rot)
+    qr = _ref.rope_kv_write(qkv, start, rope, kr, vr, Hq, Hkv, D, rot)
+    _close(q, qr, 2e-2, 1e-2)
+    _close(kc, kr, 2e-2, 1e-2)
+    assert torch.equal(vc, vr)
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 32, 128), (32, 8, 128), (32, 8, 64), (32, 32, 80), (8, 8, 256), (16, 2, 128)])
+@pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333)])
+def test_decode_attention(cuda, Hq, Hkv, D, lens):
+    C = ops.ext()
+    B = len(lens)
+    S = max(lens) + 5
+    q = torch.randn(B, Hq, D, device=cuda).bfloat16()
+    kc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    vc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    sl = torch.tensor(lens, device=cuda, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = C.decode_attn(q, kc, vc, sl, scale, max(lens))
+    ref = _ref.decode_attention(q, kc, vc, sl, scale)
+    _close(out, ref, 2e-2, 2e-2)
+    # a larger hint (graph-captured grid) must not change the answer
+    out2 = C.decode_attn(q, kc, vc, sl, scale, S)
+    _close(out2, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 32, 128), (32, 8, 64), (32, 32, 80), (8, 8, 256), (8, 2, 128)])
+@pytest.mark.parametrize("T,starts", [(64, (0, 0)), (100, (0, 37)), (1, (5, 130)), (257, (0, 0))])
+def test_prefill_attention(cuda, Hq, Hkv, D, T, starts):
+    C = ops.ext()
+    B = len(starts)
+    S = max(starts) + T + 3
+    q = torch.randn(B, T, Hq, D, device=cuda).bfloat16()
+    kc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    vc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    sp = torch.tensor(starts, device=cuda, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = C.prefill_attn(q, kc, vc, sp, scale, True)
+    ref = _ref.prefill_attention(q, kc, vc, sp, scale, True)
+    _close(out, ref, 2e-2, 2e-2)
+
+
+def test_prefill_attention_noncausal(cuda):
+    C = ops.ext()
+    q = torch.randn(2, 70, 4, 64, device=cuda).bfloat16()
+    kc = torch.randn(2, 4, 70, 64, device=cuda).bfloat16()
+    vc = torch.randn(2, 4, 70, 64, device=cuda).bfloat16()
+    sp = torch.zeros(2, device=cuda, dtype=torch.int32)
+    _close(C.prefill_attn(q, kc, vc, sp, 0.125, False), _ref.prefill_attention(q, kc, vc, sp, 0.125, False), 2e-2, 2e-2)
+
+
+def test_mfma_i8_layout_exact(cuda):
+    """Exact-integer check of the packed-weight / fragment mapping with an asymmetric W."""
+    C = ops.ext()
+    M, N, K = 16, 32, 128
+    a = torch.zeros(M, K, dtype=torch.int8, device=cuda)
+    a[torch.arange(M), torch.arange(M) * 3] = 1          # A selects column 3m
+    w = (torch.arange(N * K, device=cuda).view(N, K) % 113 - 56).to(torch.int8)  # asymmetric
+    wp = ops.pack_int8_weight(w)
+    out = C.w8a8_gemm(a, torch.ones(M, device=cuda), wp, torch.ones(N, device=cuda), None, N, K)
+    exp = w[:, torch.arange(M) * 3].t().float()
+    assert torch.equal(out.float(), exp.bfloat16().float())
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 100, 256, 1000])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (512, 11008), (160, 96), (12288, 4096)])
+def test_w8a8_gemm(cuda, M, N, K):
+    if M * N * K > 2 ** 32:
+        pytest.skip("reference too slow")
+    C = ops.ext()
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.02 + 1e-3
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.02 + 1e-3
+    bias = torch.randn(N, device=cuda).bfloat16()
+    wp = ops.pack_int8_weight(w)
+    out = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+    ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
+    _close(out, ref, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("V", [512, 50304, 128256])
+@pytest.mark.parametrize("cfg", [(0.7, 50, 0.9, 1.1), (0.5, 30, 0.85, 1.2), (1.0, 0, 1.0, 1.0), (0.8, 20, 1.0, 1.3)])
+def test_sampler_matches_reference(cuda, V, cfg):
+    C = ops.ext()
+    temp, k, p, pen = cfg
+    B = 4
+    torch.manual_seed(1)
+    logits = (torch.randn(B, V, device=cuda) * 4).bfloat16()
+    seen = (torch.rand(B, V, device=cuda) < 0.01).to(torch.uint8)
+    mism = 0
+    for step in range(16):
+        rng = torch.tensor([1234, step], dtype=torch.int32, device=cuda)
+        s1 = seen.clone()
+        tok = C.sample(logits, s1, temp, k, p, pen, True, rng)
+        ref = _ref.sample(logits, seen, temp, k, p, pen, 1234, step, True)
+        mism += (tok.cpu() != ref.cpu()).sum().item()
+        assert s1[torch.arange(B), tok].all()
+    assert mism <= 1, f"{mism} mismatches"
+
+
+def test_sampler_greedy_and_topk_support(cuda):
+    C = ops.ext()
+    logits = torch.randn(3, 1000, device=cuda)
+    rng = torch.tensor([0, 0], dtype=torch.int32, device=cuda)
+    tok = C.sample(logits, None, 0.0, 0, 1.0, 1.0, False, rng)
+    assert torch.equal(tok, logits.argmax(-1))
+    # top_k = 1 is greedy whatever the noise
+    tok = C.sample(logits, None, 0.7, 1, 0.9, 1.0, True, rng)
+    assert torch.equal(tok, logits.argmax(-1))
+    # empirical distribution of top-k=3 sampling
+    logits = torch.tensor([[2.0, 1.0, 0.5, -5.0] + [-9.0] * 60], device=cuda)
+    counts = torch.zeros(64)
+    for step in range(3000):
+        rng = torch.tensor([7, step], dtype=torch.int32, device=cuda)
+        counts[C.sample(logits, None, 1.0, 3, 1.0, 1.0, True, rng).item()] += 1
+    p = torch.softmax(torch.tensor([2.0, 1.0, 0.5]), 0)
+    assert counts[3:].sum() == 0
+    assert torch.allclose(counts[:3] / 3000, p, atol=0.03)
