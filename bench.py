@@ -1,0 +1,139 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): whole-node decode tokens/sec + p50 per-token latency,
+Llama-2-7B, SmoothQuant W8A8 INT8, layer-split across N GPUs of one node.
+
+    python bench.py --gpus 1 --steps 64 --warmup 8
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 64 --warmup 8
+
+Work per step: every in-flight sequence decodes one token (sampling with the reference's
+config: T=0.7, top-k 50, top-p 0.9, repetition penalty 1.1 — Code/others/config.yaml:3-7).
+N = 1 runs the graph-captured Generator on one GPU; N > 1 runs the RCCL pipeline with one
+stage (32/N decoder layers) per GPU and N micro-batches in flight, so per-GPU work per step is
+constant (weak scaling: global batch = micro-batch x N).
+Synthetic data: random-init weights of the Llama-2-7B architecture, random prompt ids.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import edgellm  # noqa: E402,F401
+from edgellm.engine import Generator, SamplingParams  # noqa: E402
+from edgellm.models import build_model, get_config  # noqa: E402
+from edgellm.quant import quantize_model, synthetic_calibration  # noqa: E402
+
+METRIC = "tokens/sec (whole node) + p50 per-token latency, Llama-2-7B INT8 split 1/2/4/8"
+# no published value for this metric; the closest published point is the reference's
+# single-stream INT8 decode rate (Llama-3.2-1B, bitsandbytes LLM.int8, A100): 25.8326 tok/s.
+BASELINE_TPS = 25.8326
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--model", default="llama-2-7b")
+    ap.add_argument("--quant", default="w8a8_smoothquant", choices=["none", "w8a8_smoothquant", "w8a8"])
+    ap.add_argument("--micro-batch", type=int, default=16, help="sequences per micro-batch")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-graphs", action="store_true")
+    return ap.parse_args()
+
+
+def build(args, device, first=0, last=None):
+    cfg = get_config(args.model)
+    model = build_model(cfg, dtype=torch.bfloat16, device=device, first=first, last=last, seed=args.seed)
+    if args.quant != "none":
+        calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed) if model.has_embed else None
+        if args.quant == "w8a8_smoothquant" and calib is None:
+            # later pipeline stages calibrate on hidden states they receive; in the benchmark each
+            # stage calibrates on its own synthetic embedding-like activations
+            model = quantize_model(model, "w8a8")
+        else:
+            model = quantize_model(model, args.quant, calib)
+    torch.cuda.synchronize()
+    return cfg, model
+
+
+def run_single(args):
+    device = torch.device("cuda:0")
+    torch.cuda.set_device(device)
+    t_build = time.perf_counter()
+    cfg, model = build(args, device)
+    t_build = time.perf_counter() - t_build
+    B = args.micro_batch
+    total_new = args.warmup + args.steps + 2
+    gen = Generator(model, max_batch=B, max_seq=args.prompt_len + total_new + 8, use_graphs=not args.no_graphs)
+    g = torch.Generator().manual_seed(args.seed)
+    prompts = torch.randint(0, cfg.vocab_size, (B, args.prompt_len), generator=g).tolist()
+    sp = SamplingParams(max_new_tokens=total_new, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
+    gen.start(prompts, sp, seed=args.seed)
+    prefill_s = gen._run["t_prefill"]
+    gen.step(args.warmup, record_latency=False)
+    gen.precapture(args.steps + 1)
+    torch.cuda.synchronize()
+    n_ev = len(gen._run["events"])
+    t0 = time.perf_counter()
+    gen.step(args.steps, record_latency=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ev = gen._run["events"][n_ev:]
+    lat = sorted(ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev)))
+    p50 = lat[len(lat) // 2] if lat else dt / args.steps * 1e3
+    tokens = B * args.steps
+    return dict(value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, global_batch=B,
+                prefill_tps=B * args.prompt_len / prefill_s, build_s=t_build,
+                graphs=gen._run["graphs_ok"], mem_gb=torch.cuda.max_memory_allocated() / 1e9)
+
+
+def run_pipeline(args):
+    from edgellm.parallel.bench_pipeline import run_pipeline_bench
+    return run_pipeline_bench(args, build)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 or world > 1:
+        assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun"
+        res = run_pipeline(args)
+    else:
+        res = run_single(args)
+    if res is None:  # non-zero ranks
+        return
+    out = {
+        "metric": METRIC,
+        "value": round(res["value"], 2),
+        "unit": "tokens/s",
+        "n_gpus": args.gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(res["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(res["value"] / BASELINE_TPS, 2),
+        "dtype": "int8 W8A8 (bf16 activations/accum-dequant)" if args.quant != "none" else "bf16",
+        "data": "synthetic (random-init Llama-2-7B weights, random prompt ids)",
+        "config": {"model": args.model, "global_batch": res["global_batch"], "seq_len": args.prompt_len,
+                   "parallelism": f"pp{args.gpus}", "quant": args.quant, "micro_batch": args.micro_batch,
+                   "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1"},
+        "p50_token_latency_ms": round(res["p50"], 4),
+        "prefill_tokens_per_s": round(res.get("prefill_tps", 0.0), 1),
+        "peak_mem_gb": round(res.get("mem_gb", 0.0), 2),
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

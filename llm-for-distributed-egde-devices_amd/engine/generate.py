@@ -1,0 +1,281 @@
+"""Batched generation engine: prefill + HIP-graph-captured decode loop.
+
+Replaces HF ``model.generate`` as called by the reference (``get_response`` /
+``refine_summary``, combine_model_fp_updated.py:86-135).  Differences by design:
+  * KV cache preallocated, head-major (no per-step ``torch.cat``);
+  * one decode step = one HIP graph replay: embedding -> layers -> head -> fused sampler ->
+    position/step counters, all on device; no host sync per token (EOS is polled every
+    ``eos_check_every`` steps from a device token buffer);
+  * seedable, counter-based sampling (reference sets no seed anywhere — SURVEY §2.2).
+Timing follows both reference TPS definitions (``GenerationResult``).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from .. import ops
+from ..models.decoder import AttnCtx, DecoderLM
+from .kv_cache import KVCache
+
+GRAPH_BUCKET = 256
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 200
+    temperature: float = 0.7
+    top_k: int = 50
+    top_p: float = 0.9
+    repetition_penalty: float = 1.1
+    do_sample: bool = True
+
+    @classmethod
+    def from_config(cls, s) -> "SamplingParams":
+        return cls(s.max_new_tokens, s.temperature, s.top_k, s.top_p, s.repetition_penalty,
+                   getattr(s, "do_sample", True))
+
+    def key(self):
+        return (self.temperature, self.top_k, self.top_p, self.repetition_penalty, self.do_sample)
+
+
+@dataclass
+class GenerationResult:
+    tokens: List[List[int]]          # generated ids per sequence (EOS included if produced)
+    prompt_lens: List[int]
+    elapsed_s: float                 # prefill + decode wall time (reference timer span)
+    prefill_s: float
+    decode_s: float
+    step_ms: List[float] = field(default_factory=list)  # per decode-step latency (device events)
+
+    @property
+    def num_generated(self) -> int:
+        return sum(len(t) for t in self.tokens)
+
+    def tps_generated(self) -> float:
+        """Generated tokens / time (combiners, combine_model_fp_updated.py:106-108)."""
+        return self.num_generated / self.elapsed_s if self.elapsed_s > 0 else 0.0
+
+    def tps_incl_prompt(self) -> float:
+        """(prompt + generated) tokens / time (single-model scripts, Llama_bf16_updated.py:89-90)."""
+        n = self.num_generated + sum(self.prompt_lens)
+        return n / self.elapsed_s if self.elapsed_s > 0 else 0.0
+
+    def p50_ms(self) -> float:
+        if not self.step_ms:
+            return float("nan")
+        s = sorted(self.step_ms)
+        return s[len(s) // 2]
+
+
+def needs_host_sampler(sp: SamplingParams, V: int) -> bool:
+    """True when the fused sampler cannot express the config (top-p without top-k, or
+    top-k > 1024): the step then syncs with the host and cannot be graph-captured."""
+    if not sp.do_sample or sp.temperature <= 0:
+        return False
+    full = (sp.top_k is None or sp.top_k <= 0 or sp.top_k >= V)
+    if full and (sp.top_p is None or sp.top_p >= 1.0):
+        return False
+    return not (sp.top_k and 0 < sp.top_k <= 1024 and sp.top_k < V)
+
+
+class _DecodeState:
+    """Static device buffers read and advanced by the (captured) decode step."""
+
+    def __init__(self, B: int, V: int, max_new: int, device):
+        self.tok = torch.zeros(B, dtype=torch.long, device=device)
+        self.pos = torch.zeros(B, dtype=torch.int32, device=device)       # position of tok
+        self.seq_lens = torch.ones(B, dtype=torch.int32, device=device)   # pos + 1
+        self.rng = torch.zeros(2, dtype=torch.int32, device=device)       # [seed, step]
+        self.step = torch.zeros(1, dtype=torch.long, device=device)       # column in out
+        self.out = torch.zeros(B, max_new, dtype=torch.long, device=device)
+        self.seen = torch.zeros(B, V, dtype=torch.uint8, device=device)
+
+
+class Generator:
+    def __init__(self, model: DecoderLM, max_batch: int = 1, max_seq: Optional[int] = None,
+                 use_graphs: Optional[bool] = None, eos_check_every: int = 8, kv: Optional[KVCache] = None):
+        assert model.has_embed and model.has_head, "Generator needs a full model (use parallel.pipeline for stages)"
+        self.model = model
+        self.cfg = model.cfg
+        self.device = model.device
+        max_seq = max_seq or self.cfg.max_position_embeddings
+        self.max_seq = max_seq
+        self.kv = kv if kv is not None else KVCache(self.cfg, max_batch, max_seq, device=self.device,
+                                                    dtype=model.dtype)
+        self.rope = model.rope_table(self.device)
+        self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
+        self.eos_check_every = eos_check_every
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._pool = None
+        self._state: Optional[_DecodeState] = None
+
+    # ------------------------------------------------------------------ forward pieces
+    @torch.no_grad()
+    def prefill(self, ids: torch.Tensor, row0: int = 0, start: int = 0) -> torch.Tensor:
+        """ids [B, T] (equal lengths) into cache rows [row0, row0+B) at positions start.. ;
+        returns last-position logits [B, V]."""
+        B, T = ids.shape
+        assert start + T <= self.max_seq, "prompt exceeds the KV cache"
+        sp = torch.full((B,), start, dtype=torch.int32, device=self.device)
+        ctx = AttnCtx("prefill", B, T, sp, sp + T, start + T, self.kv.rows(row0, row0 + B), self.rope)
+        return self.model(ids, ctx)
+
+    def _decode_step(self, st: _DecodeState, B: int, max_len: int, sp: SamplingParams):
+        ctx = AttnCtx("decode", B, 1, st.pos, st.seq_lens, max_len, self.kv.rows(0, B), self.rope)
+        logits = self.model(st.tok.view(B, 1), ctx)
+        nxt = ops.sample(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
+                         sp.do_sample)
+        st.tok.copy_(nxt)
+        st.out.scatter_(1, st.step.view(1, 1).expand(B, 1), nxt.view(B, 1))
+        st.pos.add_(1)
+        st.seq_lens.add_(1)
+        st.rng[1:].add_(1)
+        st.step.add_(1)
+
+    def _graph_for(self, st: _DecodeState, B: int, bucket: int, sp: SamplingParams):
+        key = (B, bucket, sp.key(), id(st))
+        g = self._graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, pool=self._pool):
+                self._decode_step(st, B, bucket, sp)
+            if self._pool is None:
+                self._pool = g.pool()
+            self._graphs[key] = g
+        return g
+
+    def reset_graphs(self):
+        self._graphs.clear()
+        self._pool = None
+
+    # ------------------------------------------------------------------ generate
+    @torch.no_grad()
+    def start(self, prompts: Sequence[Sequence[int]], sampling: SamplingParams, seed: int = 0) -> None:
+        """Prefill ``prompts`` and sample their first token; decode then advances with ``step``."""
+        B = len(prompts)
+        assert B <= self.kv.max_batch
+        V = self.cfg.vocab_size
+        plens = [len(p) for p in prompts]
+        max_new = sampling.max_new_tokens
+        assert max(plens) + max_new <= self.max_seq, "prompt + max_new_tokens exceeds max_seq"
+        st = self._state
+        if st is None or st.tok.shape[0] != B or st.out.shape[1] < max_new:
+            self.reset_graphs()
+            st = self._state = _DecodeState(B, V, max_new, self.device)
+        st.seen.zero_()
+        st.out.zero_()
+        st.step.zero_()
+        st.rng[0] = seed & 0x7FFFFFFF
+        st.rng[1] = 0
+        cuda = self.device.type == "cuda"
+        if cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        # equal lengths: one batched pass; otherwise one pass per sequence (own cache row)
+        if len(set(plens)) == 1:
+            logits = self.prefill(torch.tensor(prompts, dtype=torch.long, device=self.device), 0, 0)
+        else:
+            logits = torch.cat([self.prefill(torch.tensor([p], dtype=torch.long, device=self.device), b, 0)
+                                for b, p in enumerate(prompts)], 0)
+        for b, p in enumerate(prompts):
+            st.seen[b, torch.tensor(p, dtype=torch.long, device=self.device)] = 1
+        st.pos.copy_(torch.tensor(plens, dtype=torch.int32, device=self.device))
+        st.seq_lens.copy_(st.pos + 1)
+        nxt = ops.sample(logits, st.seen, sampling.temperature, sampling.top_k, sampling.top_p,
+                         sampling.repetition_penalty, st.rng, sampling.do_sample)
+        st.tok.copy_(nxt)
+        st.out[:, 0] = nxt
+        st.rng[1] = 1
+        st.step.fill_(1)
+        if cuda:
+            torch.cuda.synchronize()
+        self._run = dict(B=B, plens=plens, sampling=sampling, t0=t0, t_prefill=time.perf_counter() - t0,
+                         produced=1, host_max=max(plens), events=[], cuda=cuda,
+                         graphs_ok=self.use_graphs and cuda and self.graph_safe and not needs_host_sampler(sampling, V))
+
+    @property
+    def graph_safe(self) -> bool:
+        return all(getattr(m, "graph_safe", True) for m in self.model.modules())
+
+    @torch.no_grad()
+    def step(self, n: int = 1, record_latency: bool = True) -> int:
+        """Advance every sequence by up to ``n`` decode tokens; returns tokens produced so far."""
+        r, st = self._run, self._state
+        B, sampling = r["B"], r["sampling"]
+        for _ in range(n):
+            if r["produced"] >= sampling.max_new_tokens:
+                break
+            max_len = r["host_max"] + 1
+            if r["graphs_ok"]:
+                bucket = min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
+                if not self._graphs:
+                    self._decode_step(st, B, bucket, sampling)      # warm-up step (a real step)
+                else:
+                    self._graph_for(st, B, bucket, sampling).replay()
+            else:
+                self._decode_step(st, B, max_len, sampling)
+            if record_latency and r["cuda"]:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                r["events"].append(ev)
+            r["produced"] += 1
+            r["host_max"] += 1
+        return r["produced"]
+
+    @torch.no_grad()
+    def precapture(self, n_steps: int) -> int:
+        """Capture the decode graphs of every length bucket the next ``n_steps`` will touch
+        (capture records, it does not execute), so no capture lands in a timed region."""
+        r = self._run
+        if not r["graphs_ok"] or not self._graphs:
+            return 0
+        lo = r["host_max"] + 1
+        hi = min(self.max_seq, lo + n_steps)
+        made = 0
+        b = ((lo + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET
+        while True:
+            bucket = min(self.max_seq, b)
+            key = (r["B"], bucket, r["sampling"].key(), id(self._state))
+            if key not in self._graphs:
+                self._graph_for(self._state, r["B"], bucket, r["sampling"])
+                made += 1
+            if b >= hi:
+                break
+            b += GRAPH_BUCKET
+        return made
+
+    def all_hit(self, eos_token_id: int) -> bool:
+        st, r = self._state, self._run
+        return bool((st.out[:, :r["produced"]] == eos_token_id).any(1).all().item())
+
+    @torch.no_grad()
+    def collect(self, eos_token_id: Optional[int] = None, stop_at_eos: bool = True) -> GenerationResult:
+        r, st = self._run, self._state
+        if r["cuda"]:
+            torch.cuda.synchronize()
+        t_end = time.perf_counter()
+        toks = []
+        for row in st.out[:, :r["produced"]].tolist():
+            if stop_at_eos and eos_token_id is not None and eos_token_id in row:
+                row = row[:row.index(eos_token_id) + 1]
+            toks.append(row)
+        ev = r["events"]
+        step_ms = [ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev))] if ev else []
+        return GenerationResult(toks, r["plens"], t_end - r["t0"], r["t_prefill"], t_end - r["t0"] - r["t_prefill"],
+                                step_ms)
+
+    @torch.no_grad()
+    def generate(self, prompts: Sequence[Sequence[int]], sampling: SamplingParams, seed: int = 0,
+                 eos_token_id: Optional[int] = None, stop_at_eos: bool = True,
+                 record_step_latency: bool = True) -> GenerationResult:
+        self.start(prompts, sampling, seed)
+        while self._run["produced"] < sampling.max_new_tokens:
+            self.step(self.eos_check_every, record_step_latency)
+            if stop_at_eos and eos_token_id is not None and self.all_hit(eos_token_id):
+                break
+        return self.collect(eos_token_id, stop_at_eos)

@@ -175,6 +175,21 @@ def from_hf_dir(path: str) -> ModelConfig:
         return from_hf_config(json.load(f))
 
 
+def _rope_params(c: dict, default_theta: float, default_partial: float = 1.0):
+    """(theta, partial_rotary_factor, scaling) from either the transformers-5 ``rope_parameters``
+    dict or the older flat keys (rope_theta / rotary_emb_base / rotary_pct / rope_scaling)."""
+    rp = dict(c.get("rope_parameters") or {})
+    theta = rp.get("rope_theta", c.get("rope_theta", c.get("rotary_emb_base", default_theta)))
+    partial = rp.get("partial_rotary_factor",
+                     c.get("partial_rotary_factor", c.get("rotary_pct", default_partial)))
+    scaling = c.get("rope_scaling")
+    if rp.get("rope_type", "default") not in ("default", None):
+        scaling = {k: v for k, v in rp.items() if k not in ("rope_theta", "partial_rotary_factor")}
+    if scaling and scaling.get("rope_type", scaling.get("type")) in ("default", None):
+        scaling = None
+    return float(theta), float(partial), scaling
+
+
 def from_hf_config(c: dict) -> ModelConfig:
     """Map a Hugging Face ``config.json`` onto ModelConfig."""
     mt = c.get("model_type")
@@ -183,14 +198,15 @@ def from_hf_config(c: dict) -> ModelConfig:
         eos = eos[0]
     if mt in ("llama", "mistral"):
         h, nh = c["hidden_size"], c["num_attention_heads"]
+        theta, _, scaling = _rope_params(c, 10000.0)
         return ModelConfig(arch="llama", vocab_size=c["vocab_size"], hidden_size=h,
                            num_layers=c["num_hidden_layers"], num_heads=nh,
                            num_kv_heads=c.get("num_key_value_heads", nh),
                            intermediate_size=c["intermediate_size"],
                            head_dim=c.get("head_dim") or h // nh,
                            max_position_embeddings=c.get("max_position_embeddings", 4096),
-                           norm_eps=c.get("rms_norm_eps", 1e-5), rope_theta=c.get("rope_theta", 1e4),
-                           rope_scaling=c.get("rope_scaling"),
+                           norm_eps=c.get("rms_norm_eps", 1e-5), rope_theta=theta,
+                           rope_scaling=scaling,
                            qkv_bias=c.get("attention_bias", False), o_bias=c.get("attention_bias", False),
                            mlp_bias=c.get("mlp_bias", False),
                            tie_word_embeddings=c.get("tie_word_embeddings", False),
@@ -199,6 +215,7 @@ def from_hf_config(c: dict) -> ModelConfig:
     if mt == "gpt_neox":
         h, nh = c["hidden_size"], c["num_attention_heads"]
         hd = h // nh
+        theta, partial, scaling = _rope_params(c, 10000.0, 0.25)
         return ModelConfig(arch="gpt_neox", vocab_size=c["vocab_size"], hidden_size=h,
                            num_layers=c["num_hidden_layers"], num_heads=nh, num_kv_heads=nh,
                            intermediate_size=c["intermediate_size"],
@@ -206,14 +223,14 @@ def from_hf_config(c: dict) -> ModelConfig:
                            norm="layer", norm_eps=c.get("layer_norm_eps", 1e-5),
                            act="gelu" if c.get("hidden_act", "gelu") == "gelu" else "gelu_tanh",
                            parallel_residual=c.get("use_parallel_residual", True),
-                           rotary_dim=int(hd * c.get("rotary_pct", 0.25)),
-                           rope_theta=c.get("rotary_emb_base", c.get("rope_theta", 10000)),
+                           rotary_dim=int(hd * partial), rope_theta=theta, rope_scaling=scaling,
                            qkv_bias=c.get("attention_bias", True), o_bias=c.get("attention_bias", True),
                            mlp_bias=True, tie_word_embeddings=c.get("tie_word_embeddings", False),
                            bos_token_id=c.get("bos_token_id"), eos_token_id=eos, name="gpt_neox")
     if mt == "phi":
         h, nh = c["hidden_size"], c["num_attention_heads"]
         hd = h // nh
+        theta, partial, scaling = _rope_params(c, 10000.0, 0.4)
         return ModelConfig(arch="phi", vocab_size=c["vocab_size"], hidden_size=h,
                            num_layers=c["num_hidden_layers"], num_heads=nh,
                            num_kv_heads=c.get("num_key_value_heads") or nh,
@@ -221,8 +238,8 @@ def from_hf_config(c: dict) -> ModelConfig:
                            max_position_embeddings=c.get("max_position_embeddings", 2048),
                            norm="layer", norm_eps=c.get("layer_norm_eps", 1e-5), act="gelu_tanh",
                            parallel_residual=True, shared_input_norm=True,
-                           rotary_dim=int(hd * c.get("partial_rotary_factor", 0.4)),
-                           rope_theta=c.get("rope_theta", 10000.0), qkv_bias=True, o_bias=True,
+                           rotary_dim=int(hd * partial), rope_theta=theta, rope_scaling=scaling,
+                           qkv_bias=True, o_bias=True,
                            mlp_bias=True, lm_head_bias=True,
                            tie_word_embeddings=c.get("tie_word_embeddings", False),
                            bos_token_id=c.get("bos_token_id"), eos_token_id=eos, name="phi")

@@ -223,6 +223,8 @@ def init_random_(model: DecoderLM, seed: int = 0, std: float = 0.02) -> DecoderL
         else:
             # seeded by the GLOBAL parameter name: a pipeline stage holding layers [a, b) gets
             # bit-identical weights to the same layers of the unsplit model
+            if name == "lm_head.weight" and model.cfg.tie_word_embeddings:
+                name = "embed"  # head-only stage of a tied model: same values as the embedding
             g = torch.Generator(device=p.device).manual_seed((seed * 1000003 + zlib.crc32(name.encode())) % (2 ** 63))
             p.copy_(torch.randn(p.shape, generator=g, device=p.device, dtype=torch.float32).mul_(std).to(p.dtype))
     return model

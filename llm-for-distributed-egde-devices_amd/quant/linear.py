@@ -1,0 +1,173 @@
+"""Quantised linear layers (drop-in for ``models.layers.Linear``).
+
+* ``W8A8Linear``   — SmoothQuant-style W8A8: int8 weights with per-output-channel scales,
+  int8 activations with per-token scales produced by the *previous* kernel's epilogue (fused
+  norm/activation quant), INT8 MFMA GEMM with fused dequant (+bias) epilogue.  The north-star
+  quantised path (new capability: the reference has no SmoothQuant code).
+* ``LLMInt8Linear`` — compatibility mode for the reference's bitsandbytes ``LLM.int8()``
+  (``BitsAndBytesConfig(load_in_8bit=True)``, Code/Quantised Models/models_quant_updated.py:30-32):
+  weights int8 with per-row absmax ``SCB``; activation columns with any |x| > threshold (6.0)
+  are "outliers" computed in bf16 against the dequantised weight columns, the rest goes
+  through the same INT8 GEMM with per-token scales.
+* ``CPUDynamicLinear`` — the reference's CPU edge path, ``torch.quantization.quantize_dynamic``
+  on nn.Linear with qint8 (Code/C-DAC Server/try.py:198-206).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..models.layers import Linear, QAct
+
+
+def quantize_weight_per_channel(w: torch.Tensor):
+    """Symmetric per-output-row int8: returns (q [N,K] int8, scale [N] f32)."""
+    wf = w.float()
+    amax = wf.abs().amax(1).clamp_min(1e-8)
+    scale = amax / 127.0
+    q = torch.round(wf / scale[:, None]).clamp_(-127, 127).to(torch.int8)
+    return q, scale
+
+
+class W8A8Linear(nn.Module):
+    takes_quantized_input = True
+    graph_safe = True
+
+    def __init__(self, in_features: int, out_features: int, bias: bool, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        kt, nt = (in_features + 63) // 64, (out_features + 15) // 16
+        self.register_buffer("w_packed", torch.zeros(nt * kt * 1024, dtype=torch.int8, device=device))
+        self.register_buffer("w_scale", torch.ones(out_features, dtype=torch.float32, device=device))
+        self.register_buffer("bias", torch.zeros(out_features, dtype=dtype, device=device) if bias else None)
+        self._w_cpu = None
+
+    @classmethod
+    @torch.no_grad()
+    def from_float(cls, lin: Linear, smooth: Optional[torch.Tensor] = None) -> "W8A8Linear":
+        """smooth[k] multiplies input column k of W (the activation is divided by it upstream)."""
+        w = lin.weight.float()
+        if smooth is not None:
+            w = w * smooth.float()[None, :].to(w.device)
+        q, s = quantize_weight_per_channel(w)
+        m = cls(lin.in_features, lin.out_features, lin.bias is not None, device=w.device, dtype=lin.weight.dtype)
+        m.load_int8(q, s, lin.bias)
+        return m
+
+    @torch.no_grad()
+    def load_int8(self, q: torch.Tensor, scale: torch.Tensor, bias: Optional[torch.Tensor] = None):
+        self.w_packed.copy_(ops.pack_int8_weight(q.to(self.w_packed.device)))
+        self.w_scale.copy_(scale.float())
+        if bias is not None:
+            self.bias.copy_(bias)
+        self._w_cpu = None
+
+    def int8_weight(self) -> torch.Tensor:
+        return ops.unpack_int8_weight(self.w_packed, self.out_features, self.in_features)
+
+    def dequant_weight(self) -> torch.Tensor:
+        return self.int8_weight().float() * self.w_scale[:, None]
+
+    def forward(self, x):
+        if not isinstance(x, QAct):
+            x = QAct(*ops.quant_per_token(x))
+        K, N = self.in_features, self.out_features
+        shp = x.q.shape[:-1]
+        wref = None
+        if not x.q.is_cuda:
+            if self._w_cpu is None:
+                self._w_cpu = self.int8_weight()
+            wref = self._w_cpu
+        out = ops.w8a8_linear(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias,
+                              N, K, w_ref=wref)
+        return out.view(*shp, N)
+
+    def extra_repr(self):
+        return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, W8A8 int8"
+
+
+class LLMInt8Linear(nn.Module):
+    takes_quantized_input = False
+    graph_safe = False   # outlier-column discovery is data dependent (host sync), like bnb
+
+    def __init__(self, in_features: int, out_features: int, bias: bool, threshold: float = 6.0, device=None,
+                 dtype=torch.bfloat16):
+        super().__init__()
+        self.in_features, self.out_features, self.threshold = in_features, out_features, threshold
+        kt, nt = (in_features + 63) // 64, (out_features + 15) // 16
+        self.register_buffer("weight_i8", torch.zeros(out_features, in_features, dtype=torch.int8, device=device))
+        self.register_buffer("w_packed", torch.zeros(nt * kt * 1024, dtype=torch.int8, device=device))
+        self.register_buffer("SCB", torch.ones(out_features, dtype=torch.float32, device=device))
+        self.register_buffer("bias", torch.zeros(out_features, dtype=dtype, device=device) if bias else None)
+
+    @classmethod
+    @torch.no_grad()
+    def from_float(cls, lin: Linear, threshold: float = 6.0) -> "LLMInt8Linear":
+        w = lin.weight.float()
+        scb = w.abs().amax(1).clamp_min(1e-8)              # bnb: per-row absmax (SCB)
+        q = torch.round(w * (127.0 / scb[:, None])).clamp_(-127, 127).to(torch.int8)
+        m = cls(lin.in_features, lin.out_features, lin.bias is not None, threshold, device=w.device,
+                dtype=lin.weight.dtype)
+        m.load_int8(q, scb, lin.bias)
+        return m
+
+    @torch.no_grad()
+    def load_int8(self, q, scb, bias=None):
+        self.weight_i8.copy_(q)
+        self.w_packed.copy_(ops.pack_int8_weight(q))
+        self.SCB.copy_(scb.float())
+        if bias is not None:
+            self.bias.copy_(bias)
+
+    def forward(self, x):
+        if isinstance(x, QAct):
+            x = (x.q.float() * x.scale[..., None]).to(torch.bfloat16)
+        K, N = self.in_features, self.out_features
+        shp = x.shape[:-1]
+        x2 = x.reshape(-1, K)
+        cols = (x2.abs() > self.threshold).any(0).nonzero().flatten()
+        w_scale = self.SCB / 127.0
+        if cols.numel() > 0:
+            x_in = x2.clone()
+            x_in[:, cols] = 0
+            w_out = (self.weight_i8[:, cols].float() * w_scale[:, None]).to(x.dtype)
+            out_o = x2[:, cols] @ w_out.t()
+        else:
+            x_in, out_o = x2, None
+        q, s = ops.quant_per_token(x_in.contiguous())
+        out = ops.w8a8_linear(q, s, self.w_packed, w_scale, self.bias, N, K,
+                              w_ref=None if q.is_cuda else self.weight_i8)
+        if out_o is not None:
+            out = (out.float() + out_o.float()).to(out.dtype)
+        return out.view(*shp, N)
+
+    def extra_repr(self):
+        return f"{self.in_features}->{self.out_features}, LLM.int8 threshold={self.threshold}"
+
+
+class CPUDynamicLinear(nn.Module):
+    """torch dynamic-quantised qint8 linear on CPU (reference try.py:205 equivalent)."""
+    takes_quantized_input = False
+    graph_safe = False
+
+    def __init__(self, lin: Linear):
+        super().__init__()
+        self.in_features, self.out_features = lin.in_features, lin.out_features
+        f = nn.Linear(lin.in_features, lin.out_features, bias=lin.bias is not None)
+        with torch.no_grad():
+            f.weight.copy_(lin.weight.float().cpu())
+            if lin.bias is not None:
+                f.bias.copy_(lin.bias.float().cpu())
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            self.q = torch.ao.quantization.quantize_dynamic(nn.Sequential(f), {nn.Linear}, dtype=torch.qint8)[0]
+        self.out_dtype = lin.weight.dtype
+
+    def forward(self, x):
+        if isinstance(x, QAct):
+            x = x.q.float() * x.scale[..., None]
+        return self.q(x.float()).to(self.out_dtype)

@@ -1,0 +1,161 @@
+"""SmoothQuant calibration / smoothing and whole-model quantisation.
+
+SmoothQuant (Xiao et al., 2211.10438 — listed in the reference's paper library but never
+implemented there) migrates activation outliers into the weights with a
+per-input-channel factor  s_j = max|X_j|^alpha / max|W_j|^(1-alpha):  X' = X / s, W' = W * s.
+Every division of X is FOLDED into the producer so inference costs nothing extra:
+
+  qkv input   = norm1 output      -> norm1.weight (and LayerNorm bias) /= s
+  up input    = norm2 output      -> norm2.weight /= s      (phi: norm1, joint s for qkv+up)
+  o input     = attention output  -> v rows of the qkv weight /= s   (attention is linear in V;
+                                     with GQA s is shared by the q heads of a kv group)
+  down input  = silu(gate) * up   -> up rows of the fused [gate|up] weight /= s  (GLU only;
+                                     GELU is not homogeneous, so non-GLU down is not smoothed)
+
+The lm_head and embeddings stay bf16 (as bitsandbytes/HF also skip the output head).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from ..models.decoder import AttnCtx, DecoderLM
+from ..models.layers import Linear
+from .linear import CPUDynamicLinear, LLMInt8Linear, W8A8Linear
+
+QUANT_MODES = ("none", "w8a8_smoothquant", "w8a8", "llm_int8", "cpu_dynamic")
+
+
+@torch.no_grad()
+def collect_act_absmax(model: DecoderLM, calib_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """Per-input-channel max|x| of every projection input over calibration tokens [N, T]."""
+    from ..engine.kv_cache import KVCache
+    stats: Dict[str, torch.Tensor] = {}
+    hooks = []
+    for name, mod in model.named_modules():
+        if isinstance(mod, Linear) and ".attn." in f".{name}" or (isinstance(mod, Linear) and ".mlp." in f".{name}"):
+            def hook(m, inp, name=name):
+                x = inp[0]
+                a = x.detach().reshape(-1, x.shape[-1]).abs().amax(0).float()
+                stats[name] = torch.maximum(stats[name], a) if name in stats else a
+            hooks.append(mod.register_forward_pre_hook(hook))
+    try:
+        N, T = calib_ids.shape
+        kv = KVCache(model.cfg, 1, T, first_layer=model.first, last_layer=model.last, dtype=model.dtype,
+                     device=calib_ids.device)
+        rope = model.rope_table(calib_ids.device)
+        for i in range(N):
+            sp = torch.zeros(1, dtype=torch.int32, device=calib_ids.device)
+            ctx = AttnCtx("prefill", 1, T, sp, sp + T, T, kv, rope)
+            model(calib_ids[i:i + 1], ctx)
+    finally:
+        for h in hooks:
+            h.remove()
+    return stats
+
+
+def _smooth_factor(x_absmax: torch.Tensor, w_colmax: torch.Tensor, alpha: float) -> torch.Tensor:
+    s = x_absmax.clamp_min(1e-5).pow(alpha) / w_colmax.clamp_min(1e-5).pow(1 - alpha)
+    return s.clamp_min(1e-5)
+
+
+@torch.no_grad()
+def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float = 0.5) -> Dict[str, torch.Tensor]:
+    """Fold SmoothQuant factors into norms / producer weights in place.  Returns the per-linear
+    factors (the quantiser multiplies W's input columns by them)."""
+    cfg = model.cfg
+    hq, hk, d = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
+    g = hq // hk
+    factors: Dict[str, torch.Tensor] = {}
+    for j, layer in enumerate(model.layers):
+        pre = f"layers.{j}."
+        qkv, o, up, down = layer.attn.qkv, layer.attn.o, layer.mlp.up, layer.mlp.down
+        dev = qkv.weight.device
+        # ---- qkv (+ up when phi shares the norm)
+        xs = stats.get(pre + "attn.qkv")
+        if xs is not None:
+            wmax = qkv.weight.float().abs().amax(0)
+            if cfg.shared_input_norm:
+                xs = torch.maximum(xs, stats.get(pre + "mlp.up", xs))
+                wmax = torch.maximum(wmax, up.weight.float().abs().amax(0))
+            s = _smooth_factor(xs.to(dev), wmax, alpha)
+            _fold_norm(layer.norm1, s)
+            factors[pre + "attn.qkv"] = s
+            if cfg.shared_input_norm:
+                factors[pre + "mlp.up"] = s
+        # ---- up (separate norm2)
+        if not cfg.shared_input_norm and pre + "mlp.up" in stats:
+            s = _smooth_factor(stats[pre + "mlp.up"].to(dev), up.weight.float().abs().amax(0), alpha)
+            _fold_norm(layer.norm2, s)
+            factors[pre + "mlp.up"] = s
+        # ---- o: fold into v rows (shared across the q heads of a kv group)
+        if pre + "attn.o" in stats:
+            xs = stats[pre + "attn.o"].to(dev).view(hk, g, d).amax(1)              # [hk, d]
+            wm = o.weight.float().abs().amax(0).view(hk, g, d).amax(1)
+            s_kv = _smooth_factor(xs, wm, alpha)                                    # [hk, d]
+            vs = cfg.q_size + cfg.kv_size
+            qkv.weight[vs:] = (qkv.weight[vs:].float() / s_kv.reshape(-1, 1)).to(qkv.weight.dtype)
+            if qkv.bias is not None:
+                qkv.bias[vs:] = (qkv.bias[vs:].float() / s_kv.reshape(-1)).to(qkv.bias.dtype)
+            factors[pre + "attn.o"] = s_kv[:, None, :].expand(hk, g, d).reshape(-1)
+        # ---- down: fold into the up half of the GLU weight
+        if cfg.is_glu and pre + "mlp.down" in stats:
+            f = cfg.intermediate_size
+            s = _smooth_factor(stats[pre + "mlp.down"].to(dev), down.weight.float().abs().amax(0), alpha)
+            up.weight[f:] = (up.weight[f:].float() / s[:, None]).to(up.weight.dtype)
+            if up.bias is not None:
+                up.bias[f:] = (up.bias[f:].float() / s).to(up.bias.dtype)
+            factors[pre + "mlp.down"] = s
+    return factors
+
+
+def _fold_norm(norm, s: torch.Tensor):
+    norm.weight.copy_((norm.weight.float() / s).to(norm.weight.dtype))
+    if norm.bias is not None:
+        norm.bias.copy_((norm.bias.float() / s).to(norm.bias.dtype))
+
+
+def synthetic_calibration(cfg, n: int = 4, T: int = 64, device=None, seed: int = 0) -> torch.Tensor:
+    """Random token ids for calibrating random-init models (no datasets offline)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, cfg.vocab_size, (n, T), generator=g).to(device)
+
+
+@torch.no_grad()
+def quantize_model(model: DecoderLM, mode: str, calib_ids: Optional[torch.Tensor] = None, alpha: float = 0.5,
+                   threshold: float = 6.0) -> DecoderLM:
+    """Replace every attention/MLP projection of ``model`` in place.
+
+    mode: "w8a8_smoothquant" (calibrate + smooth + W8A8), "w8a8" (no smoothing),
+          "llm_int8" (bitsandbytes-compatible), "cpu_dynamic" (torch qint8 dynamic, CPU)."""
+    assert mode in QUANT_MODES, mode
+    if mode == "none":
+        return model
+    factors: Dict[str, torch.Tensor] = {}
+    if mode == "w8a8_smoothquant":
+        if calib_ids is None:
+            calib_ids = synthetic_calibration(model.cfg, device=model.device)
+        stats = collect_act_absmax(model, calib_ids.to(model.device))
+        factors = smooth_model_(model, stats, alpha)
+    for j, layer in enumerate(model.layers):
+        pre = f"layers.{j}."
+        for parent, attr, key in ((layer.attn, "qkv", "attn.qkv"), (layer.attn, "o", "attn.o"),
+                                  (layer.mlp, "up", "mlp.up"), (layer.mlp, "down", "mlp.down")):
+            lin = getattr(parent, attr)
+            if mode in ("w8a8_smoothquant", "w8a8"):
+                new = W8A8Linear.from_float(lin, factors.get(pre + key))
+            elif mode == "llm_int8":
+                new = LLMInt8Linear.from_float(lin, threshold)
+            else:
+                new = CPUDynamicLinear(lin)
+            setattr(parent, attr, new)
+    model.quant_mode = mode
+    if mode == "w8a8_smoothquant":
+        model.smooth_factors = {k: v.detach().cpu() for k, v in factors.items()}
+    return model
+
+
+def is_graph_safe(model: nn.Module) -> bool:
+    return all(getattr(m, "graph_safe", True) for m in model.modules())

@@ -1,0 +1,51 @@
+import torch
+
+from edgellm.engine import Generator, KVCache, SamplingParams
+from edgellm.models import AttnCtx, build_model, tiny
+
+
+def _full_logits(model, ids):
+    T = ids.shape[1]
+    kv = KVCache(model.cfg, 1, T, dtype=model.dtype)
+    sp = torch.zeros(1, dtype=torch.int32)
+    return model(ids, AttnCtx("prefill", 1, T, sp, sp + T, T, kv, model.rope_table()), logits="last")
+
+
+def test_greedy_generation_matches_recompute():
+    cfg = tiny("llama")
+    m = build_model(cfg, dtype=torch.float32, seed=5)
+    gen = Generator(m, max_batch=2, max_seq=64)
+    prompt = [3, 14, 15, 92, 65]
+    res = gen.generate([prompt], SamplingParams(max_new_tokens=10, do_sample=False, repetition_penalty=1.0))
+    ids = list(prompt)
+    for _ in range(10):
+        ids.append(int(_full_logits(m, torch.tensor([ids])).argmax(-1)))
+    assert res.tokens[0] == ids[len(prompt):]
+
+
+def test_sampling_is_seeded_and_batched():
+    cfg = tiny("gpt_neox")
+    m = build_model(cfg, dtype=torch.float32, seed=5)
+    gen = Generator(m, max_batch=4, max_seq=64)
+    sp = SamplingParams(max_new_tokens=12, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
+    a = gen.generate([[1, 2, 3], [4, 5, 6]], sp, seed=11)
+    b = gen.generate([[1, 2, 3], [4, 5, 6]], sp, seed=11)
+    c = gen.generate([[1, 2, 3], [4, 5, 6]], sp, seed=12)
+    assert a.tokens == b.tokens and a.tokens != c.tokens
+    # variable-length prompts in one batch == each alone (greedy)
+    gp = SamplingParams(max_new_tokens=6, do_sample=False)
+    both = gen.generate([[7, 8, 9, 10], [11, 12]], gp)
+    one = gen.generate([[7, 8, 9, 10]], gp)
+    two = gen.generate([[11, 12]], gp)
+    assert both.tokens == [one.tokens[0], two.tokens[0]]
+
+
+def test_eos_stop_and_tps_definitions():
+    cfg = tiny("phi")
+    m = build_model(cfg, dtype=torch.float32, seed=9)
+    gen = Generator(m, max_batch=1, max_seq=64, eos_check_every=2)
+    free = gen.generate([[5, 6, 7]], SamplingParams(max_new_tokens=12, do_sample=False))
+    eos = free.tokens[0][3]
+    res = gen.generate([[5, 6, 7]], SamplingParams(max_new_tokens=12, do_sample=False), eos_token_id=eos)
+    assert res.tokens[0][-1] == eos and len(res.tokens[0]) == free.tokens[0].index(eos) + 1
+    assert res.tps_incl_prompt() > res.tps_generated() > 0

@@ -1,0 +1,94 @@
+import copy
+
+import pytest
+import torch
+
+from edgellm.engine import KVCache
+from edgellm.models import AttnCtx, build_model, tiny
+from edgellm.quant import (LLMInt8Linear, W8A8Linear, collect_act_absmax, load_quantized, quantize_model,
+                           save_quantized, smooth_model_, synthetic_calibration)
+
+
+def _logits(model, ids):
+    B, T = ids.shape
+    kv = KVCache(model.cfg, B, T + 1, dtype=model.dtype)
+    sp = torch.zeros(B, dtype=torch.int32)
+    ctx = AttnCtx("prefill", B, T, sp, sp + T, T, kv, model.rope_table())
+    return model(ids, ctx, logits="all").float()
+
+
+@pytest.mark.parametrize("arch", ["llama", "llama2", "phi", "gpt_neox", "gpt2"])
+def test_smoothing_fold_is_exact_in_fp32(arch):
+    """Folding s into norms / v rows / up rows and W columns must not change the function."""
+    cfg = tiny(arch)
+    m = build_model(cfg, dtype=torch.float32, seed=3)
+    ids = torch.randint(0, cfg.vocab_size, (2, 9))
+    ref = _logits(m, ids)
+    stats = collect_act_absmax(m, synthetic_calibration(cfg, 2, 16))
+    factors = smooth_model_(m, stats, alpha=0.5)
+    assert factors
+    # apply the W side of the migration in fp32 (what the quantiser does before rounding)
+    for j, layer in enumerate(m.layers):
+        for mod, key in ((layer.attn.qkv, "attn.qkv"), (layer.attn.o, "attn.o"), (layer.mlp.up, "mlp.up"),
+                         (layer.mlp.down, "mlp.down")):
+            s = factors.get(f"layers.{j}.{key}")
+            if s is not None:
+                mod.weight.mul_(s[None, :])
+    out = _logits(m, ids)
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("mode", ["w8a8_smoothquant", "w8a8", "llm_int8", "cpu_dynamic"])
+@pytest.mark.parametrize("arch", ["llama", "phi", "gpt_neox"])
+def test_quantized_model_tracks_float(mode, arch):
+    cfg = tiny(arch)
+    m = build_model(cfg, dtype=torch.float32, seed=1)
+    ids = torch.randint(0, cfg.vocab_size, (2, 12))
+    ref = _logits(m, ids)
+    q = quantize_model(copy.deepcopy(m).to(torch.bfloat16), mode)
+    out = _logits(q, ids)
+    rel = (out - ref).norm() / ref.norm()
+    assert rel < 0.08, float(rel)
+    # top-1 agreement on most positions
+    agree = (out.argmax(-1) == ref.argmax(-1)).float().mean()
+    assert agree > 0.7
+
+
+def test_w8a8_linear_matches_dequant():
+    torch.manual_seed(0)
+    from edgellm.models.layers import Linear
+    lin = Linear(96, 48, bias=True, dtype=torch.bfloat16)
+    lin.weight.data.normal_(0, 0.05)
+    lin.bias.data.normal_(0, 0.1)
+    q = W8A8Linear.from_float(lin)
+    x = torch.randn(5, 96).bfloat16()
+    from edgellm import ops
+    qx, sx = ops.quant_per_token(x)
+    ref = (qx.float() * sx[:, None]) @ q.dequant_weight().t() + lin.bias.float()
+    assert torch.allclose(q(x).float(), ref, atol=2e-2, rtol=1e-2)
+
+
+def test_llm_int8_outlier_path():
+    from edgellm.models.layers import Linear
+    lin = Linear(64, 32, bias=False, dtype=torch.bfloat16)
+    lin.weight.data.normal_(0, 0.05)
+    q = LLMInt8Linear.from_float(lin, threshold=6.0)
+    x = torch.randn(4, 64).bfloat16()
+    x[:, 5] = 40.0                     # an outlier column goes through the bf16 path
+    out = q(x).float()
+    ref = x.float() @ lin.weight.float().t()
+    assert ((out - ref).norm() / ref.norm()) < 0.02
+
+
+@pytest.mark.parametrize("mode", ["w8a8_smoothquant", "llm_int8"])
+def test_checkpoint_roundtrip(tmp_path, mode):
+    cfg = tiny("llama")
+    m = quantize_model(build_model(cfg, dtype=torch.bfloat16, seed=2), mode)
+    ids = torch.randint(0, cfg.vocab_size, (1, 8))
+    ref = _logits(m, ids)
+    save_quantized(m, str(tmp_path))
+    m2 = load_quantized(str(tmp_path))
+    assert torch.equal(_logits(m2, ids), ref)
+    # stage-sliced load gets the same layer weights
+    st = load_quantized(str(tmp_path), first=1, last=2)
+    assert st.layers[0].idx == 1 and isinstance(st.layers[0].attn.qkv, type(m.layers[1].attn.qkv))
