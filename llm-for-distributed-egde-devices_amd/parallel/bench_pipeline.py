@@ -1,0 +1,77 @@
+"""Multi-GPU leg of bench.py: pipeline of N stages (one per GPU), N micro-batches in flight.
+
+Timed region = ticks [t_a, t_b) with the pipeline full: t_a = M + W*M + (P-1), t_b = t_a + K*M,
+i.e. exactly K decode steps of every sequence (K*M micro-batch items per stage), bracketed on
+every rank by cuda-synchronize + barrier; the reported time is the max over ranks.
+p50 per-token latency = median interval between consecutive tokens of one sequence (M ticks),
+from device events on the last stage.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..engine.generate import SamplingParams
+from ..models.configs import get_config
+from .partition import partition_model, stage_costs
+from .pipeline import PipelineStage, init_distributed
+
+
+def run_pipeline_bench(args, build):
+    rank, world = init_distributed("nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    cfg = get_config(args.model)
+    wbytes = 1.0 if args.quant != "none" else 2.0
+    bounds = partition_model(cfg, world, "balanced", weight_bytes=wbytes)
+    _, model = build(args, device, first=bounds[rank], last=bounds[rank + 1])
+    M, P, b, T = world, world, args.micro_batch, args.prompt_len
+    W, K = args.warmup, args.steps
+    S = W + K + 1
+    g = torch.Generator().manual_seed(args.seed)
+    prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)] if rank == 0 else None
+    stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs)
+    # initialise the RCCL communicator with a collective every rank joins
+    x = torch.ones(1, device=device)
+    dist.all_reduce(x)
+    torch.cuda.synchronize()
+    t_a = M + W * M + (P - 1)
+    t_b = t_a + K * M
+    marks = {}
+    events = []
+
+    def hook(t):
+        if t in (t_a, t_b):
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+            marks[t] = time.perf_counter()
+        if stage.is_last and t_a <= t <= t_b and (t - t_a) % M == 0:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            events.append(ev)
+
+    sp = SamplingParams(max_new_tokens=S + 1, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
+    stage.run(prompts, T, sp, S, seed=args.seed, hook=hook)
+    dt = torch.tensor([marks[t_b] - marks[t_a]], device=device, dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    lat = torch.zeros(1, device=device, dtype=torch.float64)
+    if stage.is_last and len(events) > 1:
+        iv = sorted(events[i - 1].elapsed_time(events[i]) for i in range(1, len(events)))
+        lat[0] = iv[len(iv) // 2]
+    dist.all_reduce(lat, op=dist.ReduceOp.MAX)
+    mem = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9], device=device, dtype=torch.float64)
+    dist.all_reduce(mem, op=dist.ReduceOp.MAX)
+    elapsed = float(dt.item())
+    res = None
+    if rank == 0:
+        tokens = K * M * b
+        res = dict(value=tokens / elapsed, ms_per_step=elapsed / K * 1e3, p50=float(lat.item()), global_batch=M * b,
+                   mem_gb=float(mem.item()), partition=bounds,
+                   stage_cost_mb=[round(c / 1e6, 1) for c in stage_costs(cfg, bounds, wbytes)])
+    dist.barrier()
+    dist.destroy_process_group()
+    return res
