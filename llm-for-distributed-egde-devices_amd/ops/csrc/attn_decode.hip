@@ -208,8 +208,11 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __rest
 }  // namespace
 
 // Workspace sizes (floats) for a given launch; the binding allocates them.
+static int g_target_wg = 512;   // >= 2 workgroups per CU before splitting K
+extern "C" void edge_decode_attn_config(int target_wg) { g_target_wg = target_wg > 0 ? target_wg : 512; }
+
 extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out) {
-  const int target_wg = 1024;
+  const int target_wg = g_target_wg;
   int per = B * Hkv;
   int nsplit = (target_wg + per - 1) / per;
   int ch = (max_len + nsplit - 1) / nsplit;

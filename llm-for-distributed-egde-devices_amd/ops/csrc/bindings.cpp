@@ -31,6 +31,9 @@ int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* 
 int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, hipStream_t st);
+void edge_w8a8_gemv_config(int nw, int unroll);
+void edge_w8a8_gemv_ntw(int ntw);
+void edge_decode_attn_config(int target_wg);
 }
 
 namespace {
@@ -277,4 +280,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("prefill_attn", &prefill_attn);
   m.def("w8a8_gemm", &w8a8_gemm);
   m.def("sample", &sample);
+  m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
+    if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
+    else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
+    else if (what == "decode_attn") edge_decode_attn_config((int)a);
+    else TORCH_CHECK(false, "unknown tunable ", what);
+  });
 }

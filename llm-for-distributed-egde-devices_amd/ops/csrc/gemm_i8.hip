@@ -37,16 +37,18 @@ __device__ __forceinline__ void store_out(bf16_t* __restrict__ out, int M, int N
 }
 
 // ------------------------------------------------------------------------------------ gemv
-template <int MT, int UNROLL>
-__global__ void __launch_bounds__(NT) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
-                                                       const int8_t* __restrict__ Wp, const float* __restrict__ sw,
-                                                       const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                       int M, int N, int K, int KT) {
-  __shared__ v4i red[4][MT][64];
+// NW waves per workgroup split K; k-tile kt goes to wave kt % NW, so at each unrolled step the
+// workgroup's NW waves read NW consecutive 1 KiB tiles = one contiguous NW KiB run of the panel.
+// UNROLL tiles per wave are in flight before the first MFMA (nontemporal: read-once weights).
+template <int MT, int UNROLL, int NW>
+__global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                            const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                            const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                            int M, int N, int K, int KT) {
+  __shared__ v4i red[NW][MT][64];
   const int nt = blockIdx.x;
   const int m0 = blockIdx.y * (16 * MT);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kt0 = (KT * wave) / 4, kt1 = (KT * (wave + 1)) / 4;
   const int arow = lane & 15, akc = 16 * (lane >> 4);
 
   v4i acc[MT];
@@ -62,24 +64,25 @@ __global__ void __launch_bounds__(NT) w8a8_gemv_kernel(const int8_t* __restrict_
     aval[i] = r < M;
     arows[i] = A + (size_t)(aval[i] ? r : 0) * K;
   }
+  const bool k16 = (K % 16) == 0;
 
-  for (int kt = kt0; kt < kt1; kt += UNROLL) {
+  for (int kt = wave; kt < KT; kt += NW * UNROLL) {
     v4i b[UNROLL];
     v4i a[UNROLL][MT];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u;
-      b[u] = (k < kt1) ? __builtin_nontemporal_load(wp + (size_t)k * 64) : v4i{0, 0, 0, 0};
+      const int k = kt + u * NW;
+      b[u] = (k < KT) ? __builtin_nontemporal_load(wp + (size_t)k * 64) : v4i{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int kk = (kt + u) * 64 + akc;
+      const int k = kt + u * NW;
+      const int kk = k * 64 + akc;
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        if (aval[i] && kt + u < kt1 && kk + 16 <= K) a[u][i] = *reinterpret_cast<const v4i*>(arows[i] + kk);
-        else if (aval[i] && kt + u < kt1 && kk < K) {
-          // ragged K tail (K % 16 != 0): byte-wise, zero padded
-          int8_t t[16];
+        if (aval[i] && k < KT && kk + 16 <= K && k16) a[u][i] = *reinterpret_cast<const v4i*>(arows[i] + kk);
+        else if (aval[i] && k < KT && kk < K) {
+          int8_t t[16];  // ragged K (K % 16 != 0): byte-wise, zero padded
 #pragma unroll
           for (int j = 0; j < 16; ++j) t[j] = (kk + j < K) ? arows[i][kk + j] : 0;
           a[u][i] = *reinterpret_cast<v4i*>(t);
@@ -95,14 +98,79 @@ __global__ void __launch_bounds__(NT) w8a8_gemv_kernel(const int8_t* __restrict_
 #pragma unroll
   for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
   __syncthreads();
-  // 4 waves -> each wave finalises MT/4.. m-tiles round-robin
-  for (int i = wave; i < MT; i += 4) {
+  for (int i = wave; i < MT; i += NW) {
     v4i s = red[0][i][lane];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) s += red[w][i][lane];
+    for (int w = 1; w < NW; ++w) s += red[w][i][lane];
     const int col = nt * 16 + (lane & 15);
 #pragma unroll
     for (int j = 0; j < 4; ++j) store_out(out, M, N, m0 + i * 16 + 4 * (lane >> 4) + j, col, s[j], sa, sw, bias);
+  }
+}
+
+// M <= 16 variant with NTW n-tiles per workgroup: each A fragment (one per k-tile) feeds NTW
+// MFMAs, cutting the L2->CU activation traffic NTW-fold (at M = 16 an A fragment is as large as
+// a weight fragment, so with NTW = 1 the kernel moves twice the bytes it must).
+template <int UNROLL, int NW, int NTW>
+__global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                                const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                                const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                                int M, int N, int K, int KT, int NTt) {
+  __shared__ v4i red[NW][NTW][64];
+  const int nt0 = blockIdx.x * NTW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int arow = lane & 15, akc = 16 * (lane >> 4);
+  v4i acc[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) acc[j] = v4i{0, 0, 0, 0};
+  const v4i* wp[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = min(nt0 + j, NTt - 1);
+    wp[j] = reinterpret_cast<const v4i*>(Wp + ((size_t)nt * KT) * 1024) + lane;
+  }
+  const bool aval = arow < M;
+  const int8_t* arow_p = A + (size_t)(aval ? arow : 0) * K;
+  const bool k16 = (K % 16) == 0;
+
+  for (int kt = wave; kt < KT; kt += NW * UNROLL) {
+    v4i b[UNROLL][NTW];
+    v4i a[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = kt + u * NW;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        b[u][j] = (k < KT) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = kt + u * NW;
+      const int kk = k * 64 + akc;
+      if (aval && k < KT && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
+      else if (aval && k < KT && kk < K) {
+        int8_t t[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) t[jj] = (kk + jj < K) ? arow_p[kk + jj] : 0;
+        a[u] = *reinterpret_cast<v4i*>(t);
+      } else a[u] = v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) red[wave][j][lane] = acc[j];
+  __syncthreads();
+  for (int j = wave; j < NTW; j += NW) {
+    if (nt0 + j >= NTt) continue;
+    v4i s = red[0][j][lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) s += red[w][j][lane];
+    const int col = (nt0 + j) * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) store_out(out, M, N, 4 * (lane >> 4) + r, col, s[r], sa, sw, bias);
   }
 }
 
@@ -193,6 +261,11 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 }
 }  // namespace
 
+static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0;
+// tuning hook (microbenchmarks): 0 = automatic choice
+extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
+extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
+
 extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                               void* out, int M, int N, int K, int KT, hipStream_t st) {
   if (M == 0 || N == 0) return 0;
@@ -205,13 +278,41 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     return (int)hipGetLastError();
   }
   const int mblocks16 = (M + 15) / 16;
-  constexpr int U = 8;
-#define GEMV(MT)                                                                                             \
-  hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U>), dim3(NTt, (M + 16 * MT - 1) / (16 * MT)), dim3(NT), 0, st,    \
-                     (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT)
-  if (mblocks16 <= 1) GEMV(1);
-  else if (mblocks16 <= 2) GEMV(2);
-  else GEMV(4);
+  // waves per workgroup: enough that every wave owns >= 2 k-tiles, at most 16
+  int nw = g_gemv_nw > 0 ? g_gemv_nw : (KT >= 128 ? 16 : (KT >= 32 ? 8 : 4));
+#define GEMV_NW(MT, U, NWV)                                                                                    \
+  hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV>), dim3(NTt, (M + 16 * MT - 1) / (16 * MT)), dim3(NWV * 64), 0, \
+                     st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT)
+#define GEMV(MT, U)                                   \
+  do {                                                \
+    if (nw >= 16) GEMV_NW(MT, U, 16);                 \
+    else if (nw >= 8) GEMV_NW(MT, U, 8);              \
+    else GEMV_NW(MT, U, 4);                           \
+  } while (0)
+  const int un = g_gemv_unroll > 0 ? g_gemv_unroll : 4;
+  // n-tiles per workgroup for M <= 16: amortise each activation fragment over several MFMAs
+  // while keeping >= ~2 workgroups per CU
+  int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : (M <= 2 ? 1 : (NTt >= 1024 ? 4 : (NTt >= 512 ? 2 : 1)));
+  if (mblocks16 <= 1 && ntw > 1) {
+#define NTWL(U, NWV, NTWV)                                                                                           \
+  hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV>), dim3((NTt + NTWV - 1) / NTWV), dim3(NWV * 64), 0, st,    \
+                     (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt)
+#define NTWN(NWV)                                                   \
+  do {                                                              \
+    if (ntw >= 4) { if (un >= 4) NTWL(4, NWV, 4); else NTWL(2, NWV, 4); } \
+    else { if (un >= 4) NTWL(4, NWV, 2); else NTWL(2, NWV, 2); }   \
+  } while (0)
+    if (nw >= 16) NTWN(16);
+    else if (nw >= 8) NTWN(8);
+    else NTWN(4);
+#undef NTWN
+#undef NTWL
+    return (int)hipGetLastError();
+  }
+  if (mblocks16 <= 1) { if (un >= 8) GEMV(1, 8); else if (un >= 4) GEMV(1, 4); else GEMV(1, 2); }
+  else if (mblocks16 <= 2) { if (un >= 4) GEMV(2, 4); else GEMV(2, 2); }
+  else GEMV(4, 2);
 #undef GEMV
+#undef GEMV_NW
   return (int)hipGetLastError();
 }

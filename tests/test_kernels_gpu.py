@@ -170,6 +170,26 @@ def test_w8a8_gemm(cuda, M, N, K):
     _close(out, ref, 1e-2, 1e-2)
 
 
+@pytest.mark.parametrize("ntw,nw,u", [(2, 4, 2), (4, 8, 4), (4, 16, 2), (2, 16, 4)])
+@pytest.mark.parametrize("M,N,K", [(16, 160, 96), (7, 22016, 4096), (16, 4096, 11008), (3, 1040, 128)])
+def test_w8a8_gemv_variants(cuda, ntw, nw, u, M, N, K):
+    """Every tuning variant of the skinny kernel (incl. multi-n-tile workgroups with ragged tails)."""
+    C = ops.ext()
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.02 + 1e-3
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.02 + 1e-3
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("gemv", nw, u)
+        C.tune("gemv_ntw", ntw, 0)
+        out = C.w8a8_gemm(qx, sx, wp, sw, None, N, K)
+    finally:
+        C.tune("gemv", 0, 0)
+        C.tune("gemv_ntw", 0, 0)
+    _close(out, _ref.w8a8_linear(qx, sx, w, sw, None, torch.float32), 1e-2, 1e-2)
+
+
 @pytest.mark.parametrize("V", [512, 50304, 128256])
 @pytest.mark.parametrize("cfg", [(0.7, 50, 0.9, 1.1), (0.5, 30, 0.85, 1.2), (1.0, 0, 1.0, 1.0), (0.8, 20, 1.0, 1.3)])
 def test_sampler_matches_reference(cuda, V, cfg):

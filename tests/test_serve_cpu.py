@@ -1,0 +1,98 @@
+"""Serving / comm layer on CPU: TimeService + REST compatibility with the reference demo
+(Code/gRPC/*), and the BASELINE.json CPU config — a GPT-2 2-stage layer split over localhost
+gRPC — checked token-for-token against the single-process engine, with injected drops."""
+import re
+
+import pytest
+import torch
+
+from edgellm.engine import Generator, SamplingParams
+from edgellm.models import build_model, tiny
+from edgellm.serve import wire
+from edgellm.serve.stage_service import (EdgePipeline, FaultInjector, RemoteStage, StageForward, StageServer,
+                                         decode_tensor, encode_tensor, serve_stage)
+from edgellm.serve.time_service import (decode_time_response, encode_time_response, get_current_time, make_server)
+
+TIME_RE = re.compile(r"^\d{4}-\d{2}-\d{2} \d{2}:\d{2}:\d{2}$")
+
+
+def test_time_response_wire_format():
+    # protoc encoding of TimeResponse{current_time="2025-02-24 13:24:31"}: tag 0x0A, len 19, utf-8
+    s = "2025-02-24 13:24:31"
+    enc = encode_time_response(s)
+    assert enc == b"\x0a\x13" + s.encode()
+    assert decode_time_response(enc) == s
+
+
+def test_time_service_roundtrip():
+    server = make_server(port=0, host="127.0.0.1")
+    try:
+        t = get_current_time(f"127.0.0.1:{server.port}", timeout=5)
+        assert TIME_RE.match(t), t
+    finally:
+        server.stop(0)
+
+
+def test_time_service_unreachable_raises_after_retries():
+    with pytest.raises(RuntimeError):
+        get_current_time("127.0.0.1:1", timeout=0.2, retries=1, backoff=0.01)
+
+
+def test_rest_time_endpoint():
+    from fastapi.testclient import TestClient
+    from edgellm.serve.rest import make_app
+    c = TestClient(make_app())
+    r = c.get("/")
+    assert r.status_code == 200 and set(r.json()) == {"current_time"} and TIME_RE.match(r.json()["current_time"])
+    assert c.get("/health").json()["status"] == "ok"
+
+
+def test_tensor_codec_roundtrip():
+    for t in (torch.randn(3, 5).bfloat16(), torch.randn(2, 2), torch.arange(7)):
+        u = decode_tensor(encode_tensor(t))
+        assert u.dtype == t.dtype and torch.equal(u, t)
+    m = StageForward(7, 3, 1, torch.randn(2, 4).bfloat16(), 11, SamplingParams(temperature=0.5, top_k=30), 99,
+                     torch.tensor([[1, 2]]))
+    d = StageForward.decode(m.encode())
+    assert (d.seq_id, d.step, d.kind, d.start_pos, d.seed) == (7, 3, 1, 11, 99)
+    assert d.sampling.top_k == 30 and abs(d.sampling.temperature - 0.5) < 1e-7
+    assert torch.equal(d.hidden, m.hidden)
+    assert wire.unpack_varints(wire.field_packed_varints(1, [1, 300, 70000])[2:]) == [1, 300, 70000]
+
+
+@pytest.mark.parametrize("do_sample", [False, True])
+@pytest.mark.parametrize("faults", [None, "drops"])
+def test_gpt2_two_stage_grpc_matches_single_process(do_sample, faults):
+    cfg = tiny("gpt2", num_layers=4)
+    full = build_model(cfg, dtype=torch.float32, seed=11)
+    s0 = build_model(cfg, dtype=torch.float32, first=0, last=2, seed=11)
+    s1 = build_model(cfg, dtype=torch.float32, first=2, last=4, seed=11)
+    stage = StageServer(s1, max_seq=64)
+    server = serve_stage(stage, port=0)
+    try:
+        fi = FaultInjector(drop_prob=0.3, seed=1, drop_first_n=1) if faults else None
+        remote = RemoteStage(f"127.0.0.1:{server.port}", timeout=10, retries=8, backoff=0.001, faults=fi)
+        pipe = EdgePipeline(s0, [remote], max_seq=64)
+        prompts = [[5, 6, 7, 8], [9, 10, 11, 12]]
+        sp = SamplingParams(max_new_tokens=8, do_sample=do_sample, temperature=0.7, top_k=50, top_p=0.9,
+                            repetition_penalty=1.1)
+        got = pipe.generate(prompts, sp, seed=3)
+        ref = Generator(full, max_batch=2, max_seq=64).generate(prompts, sp, seed=3)
+        assert got.tokens == ref.tokens
+        if faults:
+            assert fi.dropped > 0 and remote.retried >= fi.dropped
+        remote.close()
+    finally:
+        server.stop(0)
+
+
+def test_stage_server_replays_retried_step():
+    cfg = tiny("gpt2", num_layers=2)
+    s1 = build_model(cfg, dtype=torch.float32, first=1, last=2, seed=1)
+    st = StageServer(s1, max_seq=32)
+    h = torch.randn(3, cfg.hidden_size)
+    sp = SamplingParams(temperature=0.7, top_k=5)
+    m = StageForward(1, 0, 0, h, 0, sp, 5, torch.tensor([[1, 2, 3]]))
+    a = st.forward(m)
+    b = st.forward(m)          # same (seq, step): served from the replay cache
+    assert a == b and st.replays == 1

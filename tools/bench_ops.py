@@ -1,0 +1,156 @@
+#!/usr/bin/env python
+"""Per-op microbenchmarks of the HIP kernels at Llama-2-7B decode shapes (MI355X).
+
+Reports time and achieved HBM bandwidth per op; tuning sweeps of the INT8 GEMV (waves per
+workgroup x unroll) are timed interleaved in one process (cdna guide §5.4 rule 24) on random
+data.  Writes a JSON summary (``--out``).
+
+    python tools/bench_ops.py --out profiles/bench_ops.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import edgellm  # noqa: E402,F401
+from edgellm import ops  # noqa: E402
+
+
+def timeit(fn, iters=50, warm=3, per_graph=20):
+    """Median per-call device time (us): ``per_graph`` calls captured in one HIP graph, replayed
+    ``iters`` times — removes host launch overhead, keeps the in-graph kernel boundaries that the
+    real decode step also pays."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+    ev[0].record()
+    for i in range(iters):
+        g.replay()
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(iters))
+    return ts[len(ts) // 2] * 1e3 / per_graph  # median us per call
+
+
+def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True):
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
+              "lm_head_int8": (32000, 4096)}
+    out = []
+    variants = [(0, 0, 0)]
+    if sweep:
+        variants += [(nw, u, ntw) for nw in (4, 8, 16) for u in (2, 4, 8) for ntw in (1, 2, 4)]
+    for name, (N, K) in shapes.items():
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wp = ops.pack_int8_weight(w)
+        sw = torch.rand(N, device=dev) * 0.01
+        for M in Ms:
+            qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            sx = torch.rand(M, device=dev) * 0.01
+            res = {}
+            for rnd in range(2):  # interleaved rounds
+                for nw, u, ntw in variants:
+                    if (M > 16 and (u == 8 or ntw > 1)) or (ntw > 1 and u == 8):
+                        continue
+                    C.tune("gemv", nw, u)
+                    C.tune("gemv_ntw", ntw, 0)
+                    t = timeit(lambda: C.w8a8_gemm(qx, sx, wp, sw, None, N, K), iters=10)
+                    res.setdefault((nw, u, ntw), []).append(t)
+            C.tune("gemv", 0, 0)
+            C.tune("gemv_ntw", 0, 0)
+            best = min(res, key=lambda k: min(res[k]))
+            auto = min(res[(0, 0, 0)])
+            nbytes = N * K + M * K + M * N * 2
+            out.append(dict(op="w8a8_gemv", shape=name, M=M, N=N, K=K, auto_us=round(auto, 2),
+                            auto_TBps=round(nbytes / auto / 1e6, 2), best=list(best),
+                            best_us=round(min(res[best]), 2), best_TBps=round(nbytes / min(res[best]) / 1e6, 2)))
+            print(out[-1], flush=True)
+    return out
+
+
+def other_rows(C, dev):
+    out = []
+    B, H, Hq, D = 16, 4096, 32, 128
+    for L in (256, 1024, 4096):
+        S = L + 8
+        q = torch.randn(B, Hq, D, device=dev).bfloat16()
+        kc = torch.randn(B, Hq, S, D, device=dev).bfloat16()
+        vc = torch.randn_like(kc)
+        sl = torch.full((B,), L, dtype=torch.int32, device=dev)
+        for tw in (256, 512, 1024):
+            C.tune("decode_attn", tw, 0)
+            t = timeit(lambda: C.decode_attn(q, kc, vc, sl, 1 / math.sqrt(D), L))
+            nbytes = 2 * B * Hq * L * D * 2
+            out.append(dict(op="decode_attn", B=B, Hkv=Hq, ctx=L, target_wg=tw, us=round(t, 2),
+                            TBps=round(nbytes / t / 1e6, 2)))
+            print(out[-1], flush=True)
+        C.tune("decode_attn", 0, 0)
+    x = torch.randn(B, H, device=dev).bfloat16()
+    r = torch.randn(B, H, device=dev).bfloat16()
+    w = torch.ones(H, device=dev).bfloat16()
+    out.append(dict(op="rmsnorm_res_quant", rows=B, H=H, us=round(timeit(lambda: C.norm(x, r, w, None, 1e-5, True, True)), 2)))
+    gu = torch.randn(B, 2 * 11008, device=dev).bfloat16()
+    out.append(dict(op="silu_mul_quant", rows=B, F=11008, us=round(timeit(lambda: C.act(gu, 0, True)), 2)))
+    qkv = torch.randn(B, 3 * H, device=dev).bfloat16()
+    kc = torch.zeros(B, Hq, 512, D, device=dev).bfloat16()
+    vc = torch.zeros_like(kc)
+    sp = torch.full((B,), 100, dtype=torch.int32, device=dev)
+    rope = ops.rope_tables(D, 512, 10000.0, device=dev)
+    out.append(dict(op="rope_kv_write", tokens=B, us=round(timeit(lambda: C.rope_kv_write(qkv, sp, rope, kc, vc, Hq, Hq, D, D)), 2)))
+    logits = torch.randn(B, 32000, device=dev).bfloat16()
+    seen = torch.zeros(B, 32000, dtype=torch.uint8, device=dev)
+    rng = torch.tensor([1, 0], dtype=torch.int32, device=dev)
+    out.append(dict(op="sample_topk50_topp0.9", rows=B, V=32000,
+                    us=round(timeit(lambda: C.sample(logits, seen, 0.7, 50, 0.9, 1.1, True, rng)), 2)))
+    # prefill attention (MFMA)
+    for T in (512, 2048):
+        q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
+        kc = torch.randn(1, Hq, T, D, device=dev).bfloat16()
+        vc = torch.randn_like(kc)
+        sp0 = torch.zeros(1, dtype=torch.int32, device=dev)
+        t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=20)
+        flops = 4 * T * T * D * Hq / 2
+        out.append(dict(op="prefill_attn_causal", T=T, H=Hq, D=D, us=round(t, 2), TFLOPs=round(flops / t / 1e6, 1)))
+    # tiled int8 GEMM (prefill)
+    for M in (512, 2048):
+        N, K = 12288, 4096
+        a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wp = ops.pack_int8_weight(w)
+        s1, s2 = torch.rand(M, device=dev), torch.rand(N, device=dev)
+        t = timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K), iters=20)
+        out.append(dict(op="w8a8_gemm_tiled", M=M, N=N, K=K, us=round(t, 2), TOPs=round(2 * M * N * K / t / 1e6, 1)))
+    for r in out[-12:]:
+        print(r, flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--no-sweep", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    C = ops.ext()
+    rows = gemv_rows(C, dev, sweep=not a.no_sweep) + other_rows(C, dev)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
