@@ -1,0 +1,133 @@
+"""The reference's nine per-sample metrics and their aggregation.
+
+Per sample (combine_model_fp_updated.py:203-212): ROUGE-1/2/L F1, BERTScore F1, BLEU, cosine
+similarity of sentence embeddings, confidence (an extra forward pass of the scoring LM:
+mean over positions of the max softmax probability — K13, here the fused
+``ops.max_softmax_prob`` kernel), and tokens/sec.  Error policy = the reference's: any metric
+exception zeroes every metric of that sample, TPS included (``strict=True`` raises instead).
+Progress can be appended to a JSONL file and resumed (the reference restarts all 1000 samples
+after a crash — SURVEY §5.4).
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..engine.kv_cache import KVCache
+from ..models.decoder import AttnCtx, DecoderLM
+from .text_metrics import evaluate_bleu, evaluate_rouge
+
+METRIC_KEYS = ("rouge1", "rouge2", "rougeL", "bertscore", "bleu", "cosine", "confidence", "tps")
+
+
+@torch.no_grad()
+def confidence_score(model: DecoderLM, ids: List[int]) -> float:
+    """mean_t max_v softmax(logits[t])  over the text's own tokens (one prefill pass)."""
+    if not ids:
+        return 0.0
+    dev = model.device
+    T = len(ids)
+    kv = KVCache(model.cfg, 1, T, dtype=model.dtype, device=dev)
+    sp = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctx = AttnCtx("prefill", 1, T, sp, sp + T, T, kv, model.rope_table(dev))
+    logits = model(torch.tensor([ids], device=dev), ctx, logits="all")
+    return float(ops.max_softmax_prob(logits).mean())
+
+
+class Embedder:
+    """Sentence embeddings + contextual token embeddings from a BERT-style encoder."""
+
+    def __init__(self, encoder, tokenizer, device=None, max_len: int = 256):
+        self.enc, self.tok, self.device, self.max_len = encoder, tokenizer, device, max_len
+
+    def _ids(self, text: str) -> torch.Tensor:
+        ids = self.tok.encode(text)[: self.max_len]
+        vmax = self.enc.cfg.vocab_size
+        return torch.tensor([[i % vmax for i in ids] or [0]], device=self.device)
+
+    @torch.no_grad()
+    def sentence(self, text: str) -> torch.Tensor:
+        return self.enc.sentence_embedding(self._ids(text))[0]
+
+    @torch.no_grad()
+    def tokens(self, text: str) -> torch.Tensor:
+        return self.enc(self._ids(text))[0].float()
+
+
+def cosine_similarity(pred: str, ref: str, embedder: Embedder) -> float:
+    """util.pytorch_cos_sim of the two sentence embeddings (combine_model_fp_updated.py:70-73)."""
+    return float(F.cosine_similarity(embedder.sentence(pred), embedder.sentence(ref), dim=0))
+
+
+def bertscore_f1(pred: str, ref: str, embedder: Embedder) -> float:
+    """BERTScore F1 (greedy max-cosine matching, no idf, no baseline rescale — evaluate's
+    defaults).  Parity with roberta-large scores needs that checkpoint: "parity unpinned"."""
+    p = F.normalize(embedder.tokens(pred), dim=-1)
+    r = F.normalize(embedder.tokens(ref), dim=-1)
+    sim = r @ p.t()
+    rec = sim.max(1).values.mean()
+    prec = sim.max(0).values.mean()
+    return float(2 * prec * rec / (prec + rec)) if float(prec + rec) > 0 else 0.0
+
+
+@dataclass
+class MetricSuite:
+    embedder: Optional[Embedder] = None
+    bert_embedder: Optional[Embedder] = None
+    strict: bool = False
+
+    def score(self, pred: str, ref: str, scorer: Optional[DecoderLM] = None, scorer_tok=None,
+              tps: float = 0.0) -> Dict[str, float]:
+        try:
+            r1, r2, rl = evaluate_rouge(pred, ref)
+            bs = bertscore_f1(pred, ref, self.bert_embedder or self.embedder) if (self.bert_embedder or self.embedder) else 0.0
+            bl = evaluate_bleu(pred, ref)
+            cs = cosine_similarity(pred, ref, self.embedder) if self.embedder else 0.0
+            conf = confidence_score(scorer, scorer_tok.encode(pred)) if scorer is not None else 0.0
+            return dict(rouge1=r1, rouge2=r2, rougeL=rl, bertscore=bs, bleu=bl, cosine=cs, confidence=conf, tps=tps)
+        except Exception:
+            if self.strict:
+                raise
+            return {k: 0.0 for k in METRIC_KEYS}
+
+
+@dataclass
+class Results:
+    rows: List[Dict[str, float]] = field(default_factory=list)
+
+    def add(self, row: Dict[str, float]):
+        self.rows.append(row)
+
+    def means(self) -> Dict[str, float]:
+        return {k: float(np.mean([r.get(k, 0.0) for r in self.rows])) if self.rows else 0.0 for k in METRIC_KEYS}
+
+
+class ProgressLog:
+    """Append-only JSONL of per-sample results; ``done()`` lists finished indices for resume."""
+
+    def __init__(self, path: Optional[str]):
+        self.path = path
+
+    def done(self) -> Dict[int, dict]:
+        out = {}
+        if self.path and os.path.exists(self.path):
+            with open(self.path) as f:
+                for line in f:
+                    line = line.strip()
+                    if line:
+                        rec = json.loads(line)
+                        out[int(rec["index"])] = rec
+        return out
+
+    def append(self, index: int, rec: dict):
+        if not self.path:
+            return
+        with open(self.path, "a") as f:
+            f.write(json.dumps({"index": index, **rec}) + "\n")

@@ -289,10 +289,16 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     else if (nw >= 8) GEMV_NW(MT, U, 8);              \
     else GEMV_NW(MT, U, 4);                           \
   } while (0)
-  const int un = g_gemv_unroll > 0 ? g_gemv_unroll : 4;
-  // n-tiles per workgroup for M <= 16: amortise each activation fragment over several MFMAs
-  // while keeping >= ~2 workgroups per CU
-  int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : (M <= 2 ? 1 : (NTt >= 1024 ? 4 : (NTt >= 512 ? 2 : 1)));
+  // Defaults from the graph-timed sweep on MI355X (profiles/bench_ops_*.json, Llama-2-7B shapes):
+  //   M <= 2 : one n-tile per workgroup, unroll 4, waves by K (6-6.8 TB/s)
+  //   M <= 16: unroll 2; N >= 16K columns: 2 n-tiles x 4 waves; 8K..16K: 4 n-tiles x 8 waves;
+  //            smaller N: 1 n-tile, 16 waves (K <= 8K) or 8 waves (larger K)
+  int un = g_gemv_unroll > 0 ? g_gemv_unroll : (M <= 2 ? 4 : 2);
+  int ntw = 1;
+  if (g_gemv_ntw > 0) ntw = g_gemv_ntw;
+  else if (M > 2 && NTt >= 1024) ntw = 2;
+  else if (M > 2 && NTt >= 512) ntw = 4;
+  if (g_gemv_nw <= 0 && M > 2) nw = (NTt >= 1024) ? 4 : (NTt >= 512 ? 8 : (KT >= 128 ? 8 : 16));
   if (mblocks16 <= 1 && ntw > 1) {
 #define NTWL(U, NWV, NTWV)                                                                                           \
   hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV>), dim3((NTt + NTWV - 1) / NTWV), dim3(NWV * 64), 0, st,    \
