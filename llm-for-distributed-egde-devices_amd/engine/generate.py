@@ -107,6 +107,9 @@ class Generator:
         self.kv = kv if kv is not None else KVCache(self.cfg, max_batch, max_seq, device=self.device,
                                                     dtype=model.dtype)
         self.rope = model.rope_table(self.device)
+        # HeadInfer (edgellm.offload) caches carry an attention hook and a prefill chunk size
+        self.attn_hook = getattr(self.kv, "attn_hook", None)
+        self.prefill_chunk = getattr(self.kv, "chunk_size", None) if self.attn_hook is not None else None
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self.eos_check_every = eos_check_every
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -120,12 +123,19 @@ class Generator:
         returns last-position logits [B, V]."""
         B, T = ids.shape
         assert start + T <= self.max_seq, "prompt exceeds the KV cache"
+        if self.prefill_chunk and T > self.prefill_chunk:     # chunked prefill (HeadInfer)
+            out = None
+            for c0 in range(0, T, self.prefill_chunk):
+                out = self.prefill(ids[:, c0:c0 + self.prefill_chunk], row0, start + c0)
+            return out
         sp = torch.full((B,), start, dtype=torch.int32, device=self.device)
-        ctx = AttnCtx("prefill", B, T, sp, sp + T, start + T, self.kv.rows(row0, row0 + B), self.rope)
+        ctx = AttnCtx("prefill", B, T, sp, sp + T, start + T, self.kv.rows(row0, row0 + B), self.rope,
+                      attn_hook=self.attn_hook)
         return self.model(ids, ctx)
 
     def _decode_step(self, st: _DecodeState, B: int, max_len: int, sp: SamplingParams):
-        ctx = AttnCtx("decode", B, 1, st.pos, st.seq_lens, max_len, self.kv.rows(0, B), self.rope)
+        ctx = AttnCtx("decode", B, 1, st.pos, st.seq_lens, max_len, self.kv.rows(0, B), self.rope,
+                      attn_hook=self.attn_hook)
         logits = self.model(st.tok.view(B, 1), ctx)
         nxt = ops.sample(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
                          sp.do_sample)
@@ -163,6 +173,7 @@ class Generator:
         plens = [len(p) for p in prompts]
         max_new = sampling.max_new_tokens
         assert max(plens) + max_new <= self.max_seq, "prompt + max_new_tokens exceeds max_seq"
+        assert self.attn_hook is None or len(set(plens)) == 1, "HeadInfer offload batches equal-length prompts"
         st = self._state
         if st is None or st.tok.shape[0] != B or st.out.shape[1] < max_new:
             self.reset_graphs()
@@ -200,7 +211,8 @@ class Generator:
 
     @property
     def graph_safe(self) -> bool:
-        return all(getattr(m, "graph_safe", True) for m in self.model.modules())
+        return getattr(self.kv, "graph_safe", True) and \
+            all(getattr(m, "graph_safe", True) for m in self.model.modules())
 
     @torch.no_grad()
     def step(self, n: int = 1, record_latency: bool = True) -> int:

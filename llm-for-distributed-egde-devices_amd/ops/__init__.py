@@ -110,11 +110,23 @@ def activation_quant(x, act: str):
 # --------------------------------------------------------------------------- rope / attention
 
 
-def rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim, rotary_dim):
+def rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim, rotary_dim,
+                  k2=None, v2=None, split: int = -1, cpos2=None):
+    """RoPE on q/k + KV append.  With ``split`` (HeadInfer), kv heads >= split go to (k2, v2)
+    at positions cpos2[b] + t instead of the main cache."""
     if _gpu(qkv):
         return ext().rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim,
-                                   rotary_dim)
-    return _ref.rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim, rotary_dim)
+                                   rotary_dim, k2, v2, split, cpos2)
+    return _ref.rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_heads, head_dim, rotary_dim,
+                              k2, v2, split, cpos2)
+
+
+def copy_head_block(dst, src):
+    """Async strided copy of a [B, c, L, D] KV head block (pinned host <-> device) on the
+    current stream (native hipMemcpy2DAsync on GPU)."""
+    if (dst.is_cuda or src.is_cuda) and not _REF_ON_GPU:
+        return ext().copy_head_block(dst, src)
+    dst.copy_(src)
 
 
 def decode_attention(q, k_cache, v_cache, seq_lens, scale, max_len_hint: Optional[int] = None):

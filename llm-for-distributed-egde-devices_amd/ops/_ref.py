@@ -125,7 +125,9 @@ def _rotate(x: torch.Tensor, cs: torch.Tensor, rotary_dim: int) -> torch.Tensor:
 
 def rope_kv_write(qkv: torch.Tensor, start_pos: torch.Tensor, rope: Optional[torch.Tensor],
                   k_cache: torch.Tensor, v_cache: torch.Tensor,
-                  num_heads: int, num_kv_heads: int, head_dim: int, rotary_dim: int) -> torch.Tensor:
+                  num_heads: int, num_kv_heads: int, head_dim: int, rotary_dim: int,
+                  k2: Optional[torch.Tensor] = None, v2: Optional[torch.Tensor] = None, split: int = -1,
+                  cpos2: Optional[torch.Tensor] = None) -> torch.Tensor:
     """qkv [B*T, (Hq+2Hkv)*D]; token t of sequence b sits at position start_pos[b]+t.
     Rotates q and k (rotate_half on the first ``rotary_dim`` dims), writes k,v into the
     head-major caches ``[B, Hkv, S, D]`` and returns q ``[B, T, Hq, D]``."""
@@ -141,10 +143,15 @@ def rope_kv_write(qkv: torch.Tensor, start_pos: torch.Tensor, rope: Optional[tor
         cs = rope[pos][:, :, None]  # [B,T,1,rot/2,2]
         q = _rotate(q, cs, rotary_dim)
         k = _rotate(k, cs, rotary_dim)
+    sh = hk if split is None or split < 0 else split
     for b in range(B):
         p = pos[b]
-        k_cache[b, :, p] = k[b].transpose(0, 1).to(k_cache.dtype)
-        v_cache[b, :, p] = v[b].transpose(0, 1).to(v_cache.dtype)
+        k_cache[b, :, p] = k[b, :, :sh].transpose(0, 1).to(k_cache.dtype)
+        v_cache[b, :, p] = v[b, :, :sh].transpose(0, 1).to(v_cache.dtype)
+        if sh < hk:
+            p2 = (cpos2.long()[b] if cpos2 is not None else start_pos.long()[b]) + torch.arange(T, device=qkv.device)
+            k2[b, :, p2] = k[b, :, sh:].transpose(0, 1).to(k2.dtype)
+            v2[b, :, p2] = v[b, :, sh:].transpose(0, 1).to(v2.dtype)
     return q.to(qkv.dtype)
 
 

@@ -18,7 +18,8 @@ int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, i
 int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st);
 int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, void* q_out, void* k_cache,
                        void* v_cache, int B, int T, int Hq, int Hkv, int D, int rot, int64_t c_sb, int64_t c_sh,
-                       int S, hipStream_t st);
+                       int S, void* k2, void* v2, int64_t c2_sb, int64_t c2_sh, int S2, int split_h,
+                       const int* cpos2, hipStream_t st);
 int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out);
 int edge_decode_attn(const void* q, int64_t q_sb, const void* k_cache, const void* v_cache, int64_t c_sb,
                      int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch,
@@ -31,6 +32,8 @@ int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* 
 int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, hipStream_t st);
+int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
+                         int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_decode_attn_config(int target_wg);
@@ -152,7 +155,9 @@ void check_cache(const at::Tensor& c, const char* name, int64_t D) {
 }
 
 at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, const std::optional<at::Tensor>& rope,
-                         at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot) {
+                         at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot,
+                         const std::optional<at::Tensor>& k2, const std::optional<at::Tensor>& v2, int64_t split,
+                         const std::optional<at::Tensor>& cpos2) {
   need(qkv, at::kBFloat16, "qkv");
   need(start_pos, at::kInt, "start_pos");
   check_cache(k_cache, "k_cache", D);
@@ -160,7 +165,15 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
   TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.sizes() == v_cache.sizes());
   const int64_t B = k_cache.size(0);
   TORCH_CHECK(start_pos.numel() == B, "start_pos must have one entry per cache row");
-  TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D && k_cache.size(1) == Hkv);
+  const int64_t split_h = split < 0 ? Hkv : split;
+  TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D && k_cache.size(1) == split_h, "qkv / cache head mismatch");
+  if (split_h < Hkv) {
+    TORCH_CHECK(k2.has_value() && v2.has_value(), "split cache needs k2/v2");
+    check_cache(*k2, "k2", D);
+    check_cache(*v2, "v2", D);
+    TORCH_CHECK(k2->strides() == v2->strides() && k2->size(0) == B && k2->size(1) == Hkv - split_h);
+    if (cpos2) { need(*cpos2, at::kInt, "cpos2"); TORCH_CHECK(cpos2->numel() == B); }
+  }
   const int64_t ntok = rows_of(qkv);
   TORCH_CHECK(ntok % B == 0, "qkv rows must be B*T");
   const int64_t T = ntok / B;
@@ -170,9 +183,13 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
     TORCH_CHECK(rope->size(1) == rot / 2);
   }
   auto q = at::empty({B, T, Hq, D}, qkv.options());
+  const bool sp2 = split_h < Hkv;
   check(edge_rope_kv_write(qkv.data_ptr(), start_pos.data_ptr<int>(), rot > 0 ? rope->data_ptr<float>() : nullptr,
                            q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), (int)B, (int)T, (int)Hq, (int)Hkv,
-                           (int)D, (int)rot, k_cache.stride(0), k_cache.stride(1), (int)k_cache.size(2), stream()),
+                           (int)D, (int)rot, k_cache.stride(0), k_cache.stride(1), (int)k_cache.size(2),
+                           sp2 ? k2->data_ptr() : nullptr, sp2 ? v2->data_ptr() : nullptr, sp2 ? k2->stride(0) : 0,
+                           sp2 ? k2->stride(1) : 0, sp2 ? (int)k2->size(2) : 0, (int)split_h,
+                           (sp2 && cpos2) ? cpos2->data_ptr<int>() : nullptr, stream()),
         "rope_kv_write");
   return q;
 }
@@ -266,16 +283,36 @@ at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& see
   return out;
 }
 
+// ---------------------------------------------------------------------------------- offload
+// dst/src: [B, c, L, D] views of head-major caches (last two dims contiguous), any mix of pinned
+// host and device memory; async on the current stream.
+void copy_head_block(at::Tensor& dst, const at::Tensor& src) {
+  TORCH_CHECK(dst.dim() == 4 && src.dim() == 4 && dst.sizes() == src.sizes(), "head blocks must match [B,c,L,D]");
+  TORCH_CHECK(dst.scalar_type() == src.scalar_type());
+  const int64_t D = dst.size(3), L = dst.size(2);
+  TORCH_CHECK(dst.stride(3) == 1 && src.stride(3) == 1 && dst.stride(2) == D && src.stride(2) == D,
+              "positions x head_dim must be contiguous");
+  TORCH_CHECK(dst.is_cuda() || dst.is_pinned(), "host side must be pinned");
+  TORCH_CHECK(src.is_cuda() || src.is_pinned(), "host side must be pinned");
+  const int es = (int)dst.element_size();
+  check(edge_copy_head_block(dst.data_ptr(), dst.stride(0), dst.stride(1), src.data_ptr(), src.stride(0),
+                             src.stride(1), (int)dst.size(0), (int)dst.size(1), L * D * es, es, stream()),
+        "copy_head_block");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("copy_head_block", &copy_head_block);
   m.doc() = "edgellm CDNA4 (gfx950) HIP kernels";
   m.def("norm", &norm);
   m.def("act", &act);
   m.def("quant", &quant);
   m.def("embedding", &embedding);
   m.def("max_prob", &max_prob);
-  m.def("rope_kv_write", &rope_kv_write);
+  m.def("rope_kv_write", &rope_kv_write, py::arg("qkv"), py::arg("start_pos"), py::arg("rope"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("rot"), py::arg("k2") = py::none(),
+        py::arg("v2") = py::none(), py::arg("split") = -1, py::arg("cpos2") = py::none());
   m.def("decode_attn", &decode_attn);
   m.def("prefill_attn", &prefill_attn);
   m.def("w8a8_gemm", &w8a8_gemm);
