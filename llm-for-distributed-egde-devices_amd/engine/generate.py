@@ -102,7 +102,7 @@ class Generator:
         self.model = model
         self.cfg = model.cfg
         self.device = model.device
-        max_seq = max_seq or self.cfg.max_position_embeddings
+        max_seq = min(max_seq or self.cfg.max_position_embeddings, self.cfg.max_position_embeddings)
         self.max_seq = max_seq
         self.kv = kv if kv is not None else KVCache(self.cfg, max_batch, max_seq, device=self.device,
                                                     dtype=model.dtype)

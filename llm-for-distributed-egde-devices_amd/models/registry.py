@@ -1,0 +1,88 @@
+"""Resolve the reference's model names/paths to a loaded edgellm model + tokenizer.
+
+The reference loads ``AutoModelForCausalLM.from_pretrained(path, torch_dtype=..., device_map="auto")``
+from local ``save_pretrained`` dirs or HF ids (Code/others/config.yaml:13-16, config_2.yaml:5-8).
+Here: a checkpoint directory that exists locally is loaded (safetensors, streamed); otherwise —
+no network, SURVEY Appendix B — the architecture named by the id is random-initialised (logged
+loudly) so every pipeline still runs end to end on synthetic weights.
+"""
+from __future__ import annotations
+
+import zlib
+from typing import Optional, Tuple
+
+import torch
+
+from ..utils.log import get_logger
+from ..utils.tokenizer import ByteTokenizer, load_tokenizer
+from .configs import ModelConfig, PRESETS, get_config
+from .decoder import DecoderLM, build_model
+from .hf import load_hf_model, resolve_model_dir
+
+log = get_logger("registry")
+
+_ALIASES = [("phi-2", "phi-2"), ("phi2", "phi-2"), ("pythia-1b", "pythia-1b"), ("pythia", "pythia-1b"),
+            ("llama-3.2-1b", "llama-3.2-1b"), ("llama3.2-1b", "llama-3.2-1b"), ("llama-2-7b", "llama-2-7b"),
+            ("llama2-7b", "llama-2-7b"), ("llama-3-8b", "llama-3-8b"), ("meta-llama-3-8b", "llama-3-8b"),
+            ("llama3-8b", "llama-3-8b"), ("gpt2", "gpt2"), ("minilm", "minilm-l6")]
+
+
+def preset_for(name: str) -> Optional[str]:
+    n = name.lower().replace("_", "-")
+    if n.startswith("tiny:"):
+        return n
+    if n in PRESETS:
+        return n
+    for key, preset in _ALIASES:
+        if key in n:
+            return preset
+    return None
+
+
+def precision_dtype(precision: str, device) -> torch.dtype:
+    """The HIP kernels run bf16; the reference's fp16 agents (combine_model_fp_updated.py:32-34)
+    therefore execute in bf16 on the GPU (same bytes, wider range).  CPU keeps the request."""
+    p = (precision or "bf16").lower()
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda":
+        return torch.bfloat16
+    return {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}.get(p, torch.bfloat16)
+
+
+def load_model(name_or_path: str, precision: str = "bf16", quant: str = "none", device=None,
+               base_dir: Optional[str] = None, first: int = 0, last: Optional[int] = None,
+               config_override: Optional[ModelConfig] = None) -> Tuple[DecoderLM, object, str]:
+    """Returns (model, tokenizer, source) with source "checkpoint:<dir>" or "random-init:<preset>"."""
+    dtype = precision_dtype(precision, device)
+    path = resolve_model_dir(name_or_path, base_dir)
+    if path is not None:
+        model = load_hf_model(path, dtype=dtype, device=device, first=first, last=last)
+        tok = load_tokenizer(path, model.cfg.vocab_size)
+        source = f"checkpoint:{path}"
+    else:
+        preset = preset_for(name_or_path)
+        if preset is None and config_override is None:
+            raise FileNotFoundError(f"no checkpoint at '{name_or_path}' and no architecture preset matches it")
+        if config_override is not None:
+            cfg = config_override
+        elif preset.startswith("tiny:"):     # "tiny:<arch>" test/smoke architectures
+            from .configs import tiny
+            cfg = tiny(preset.split(":", 1)[1].replace("gpt-neox", "gpt_neox"))
+        else:
+            cfg = get_config(preset)
+        seed = zlib.crc32(name_or_path.encode()) & 0xFFFF
+        model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=seed)
+        tok = ByteTokenizer(max(259, cfg.vocab_size))
+        source = f"random-init:{cfg.name or preset}"
+        log.warning(f"No checkpoint for '{name_or_path}': using random-init {cfg.name or preset} weights "
+                    f"(synthetic; quality metrics are meaningless)")
+    if quant and quant != "none":
+        from ..quant import quantize_model
+        calib = None
+        if quant == "w8a8_smoothquant" and model.has_embed:
+            text = ("Question: when did the first world war begin and which countries fought in it? Answer: "
+                    "The First World War began in 1914 after the assassination of Archduke Franz Ferdinand.")
+            ids = tok.encode(text)[:64]
+            calib = torch.tensor([[i % model.cfg.vocab_size for i in ids]], device=model.device)
+        model = quantize_model(model, "w8a8" if (quant == "w8a8_smoothquant" and calib is None) else quant, calib)
+    return model, tok, source

@@ -162,14 +162,16 @@ def unpack_int8_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
     return w[:N, :K].contiguous()
 
 
-def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None):
-    """INT8 x INT8 -> int32 MFMA GEMM with per-token x per-channel dequant (+bias) -> bf16.
-    ``w_ref`` (canonical [N, K]) is only needed by the CPU path."""
+def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,
+                out_dtype=torch.bfloat16):
+    """INT8 x INT8 -> int32 MFMA GEMM with per-token x per-channel dequant (+bias) -> bf16
+    (``out_dtype`` applies on CPU, where fp16/fp32 agents run).  ``w_ref`` (canonical [N, K]) is
+    only needed by the CPU path."""
     if _gpu(qx):
         return ext().w8a8_gemm(qx, x_scale, w_packed, w_scale, bias, N, K)
     w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
     shp = qx.shape[:-1]
-    out = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, torch.bfloat16)
+    out = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, out_dtype)
     return out.view(*shp, N)
 
 

@@ -44,6 +44,7 @@ class W8A8Linear(nn.Module):
         self.register_buffer("w_scale", torch.ones(out_features, dtype=torch.float32, device=device))
         self.register_buffer("bias", torch.zeros(out_features, dtype=dtype, device=device) if bias else None)
         self._w_cpu = None
+        self.out_dtype = dtype
 
     @classmethod
     @torch.no_grad()
@@ -82,7 +83,7 @@ class W8A8Linear(nn.Module):
                 self._w_cpu = self.int8_weight()
             wref = self._w_cpu
         out = ops.w8a8_linear(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias,
-                              N, K, w_ref=wref)
+                              N, K, w_ref=wref, out_dtype=self.out_dtype)
         return out.view(*shp, N)
 
     def extra_repr(self):
@@ -139,7 +140,7 @@ class LLMInt8Linear(nn.Module):
             x_in, out_o = x2, None
         q, s = ops.quant_per_token(x_in.contiguous())
         out = ops.w8a8_linear(q, s, self.w_packed, w_scale, self.bias, N, K,
-                              w_ref=None if q.is_cuda else self.weight_i8)
+                              w_ref=None if q.is_cuda else self.weight_i8, out_dtype=x.dtype)
         if out_o is not None:
             out = (out.float() + out_o.float()).to(out.dtype)
         return out.view(*shp, N)
