@@ -6,12 +6,15 @@ Llama-2-7B, SmoothQuant W8A8 INT8, layer-split across N GPUs of one node.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 64 --warmup 8
 
-Work per step: every in-flight sequence decodes one token (sampling with the reference's
-config: T=0.7, top-k 50, top-p 0.9, repetition penalty 1.1 — Code/others/config.yaml:3-7).
+Work per step: every in-flight sequence decodes one token, sampled with the reference's config
+(T=0.7, top-k 50, top-p 0.9, repetition penalty 1.1 — Code/others/config.yaml:3-7).
 N = 1 runs the graph-captured Generator on one GPU; N > 1 runs the RCCL pipeline with one
-stage (32/N decoder layers) per GPU and N micro-batches in flight, so per-GPU work per step is
+stage (~32/N decoder layers) per GPU and N micro-batches in flight, so per-GPU work per step is
 constant (weak scaling: global batch = micro-batch x N).
-Synthetic data: random-init weights of the Llama-2-7B architecture, random prompt ids.
+Weights: random-init Llama-2-7B architecture; the FULL model is SmoothQuant-calibrated on
+synthetic tokens and smoothed once, then each rank keeps its layers, so every split runs
+bit-identical INT8 weights.  Data: random prompt ids.  ``--device cpu --model tiny:llama``
+exercises the same code paths on CPU (gloo) for tests.
 """
 from __future__ import annotations
 
@@ -28,8 +31,9 @@ import torch  # noqa: E402
 
 import edgellm  # noqa: E402,F401
 from edgellm.engine import Generator, SamplingParams  # noqa: E402
-from edgellm.models import build_model, get_config  # noqa: E402
+from edgellm.models import build_model, get_config, tiny  # noqa: E402
 from edgellm.quant import quantize_model, synthetic_calibration  # noqa: E402
+from edgellm.quant.smoothquant import smoothquant_stage  # noqa: E402
 
 METRIC = "tokens/sec (whole node) + p50 per-token latency, Llama-2-7B INT8 split 1/2/4/8"
 # no published value for this metric; the closest published point is the reference's
@@ -37,7 +41,7 @@ METRIC = "tokens/sec (whole node) + p50 per-token latency, Llama-2-7B INT8 split
 BASELINE_TPS = 25.8326
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
@@ -48,27 +52,45 @@ def parse():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
+    ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
+    return ap.parse_args(argv)
+
+
+def model_config(args):
+    if args.model.startswith("tiny:"):
+        return tiny(args.model.split(":", 1)[1], num_layers=4)
+    return get_config(args.model)
 
 
 def build(args, device, first=0, last=None):
-    cfg = get_config(args.model)
-    model = build_model(cfg, dtype=torch.bfloat16, device=device, first=first, last=last, seed=args.seed)
-    if args.quant != "none":
-        calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed) if model.has_embed else None
-        if args.quant == "w8a8_smoothquant" and calib is None:
-            # later pipeline stages calibrate on hidden states they receive; in the benchmark each
-            # stage calibrates on its own synthetic embedding-like activations
-            model = quantize_model(model, "w8a8")
-        else:
-            model = quantize_model(model, args.quant, calib)
-    torch.cuda.synchronize()
+    """Stage [first, last) of the benchmark model, quantised exactly as the unsplit model."""
+    cfg = model_config(args)
+    dtype = torch.bfloat16
+    if args.quant == "w8a8_smoothquant":
+        full = build_model(cfg, dtype=dtype, device=device, seed=args.seed)
+        calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed)
+        model = smoothquant_stage(full, first, cfg.num_layers if last is None else last, calib, device=device)
+        del full
+    else:
+        model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=args.seed)
+        if args.quant != "none":
+            model = quantize_model(model, args.quant)
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
     return cfg, model
 
 
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def run_single(args):
-    device = torch.device("cuda:0")
-    torch.cuda.set_device(device)
+    device = torch.device(args.device or ("cuda:0" if torch.cuda.is_available() else "cpu"))
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
     t_build = time.perf_counter()
     cfg, model = build(args, device)
     t_build = time.perf_counter() - t_build
@@ -82,28 +104,29 @@ def run_single(args):
     prefill_s = gen._run["t_prefill"]
     gen.step(args.warmup, record_latency=False)
     gen.precapture(args.steps + 1)
-    torch.cuda.synchronize()
+    _sync(device)
     n_ev = len(gen._run["events"])
     t0 = time.perf_counter()
-    gen.step(args.steps, record_latency=True)
-    torch.cuda.synchronize()
+    gen.step(args.steps, record_latency=device.type == "cuda")
+    _sync(device)
     dt = time.perf_counter() - t0
     ev = gen._run["events"][n_ev:]
     lat = sorted(ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev)))
     p50 = lat[len(lat) // 2] if lat else dt / args.steps * 1e3
     tokens = B * args.steps
+    mem = torch.cuda.max_memory_allocated() / 1e9 if device.type == "cuda" else 0.0
     return dict(value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, global_batch=B,
-                prefill_tps=B * args.prompt_len / prefill_s, build_s=t_build,
-                graphs=gen._run["graphs_ok"], mem_gb=torch.cuda.max_memory_allocated() / 1e9)
+                prefill_tps=B * args.prompt_len / prefill_s, build_s=t_build, graphs=gen._run["graphs_ok"],
+                mem_gb=mem, partition=[0, cfg.num_layers])
 
 
 def run_pipeline(args):
     from edgellm.parallel.bench_pipeline import run_pipeline_bench
-    return run_pipeline_bench(args, build)
+    return run_pipeline_bench(args, build, model_config)
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 or world > 1:
         assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun"
@@ -111,7 +134,7 @@ def main():
     else:
         res = run_single(args)
     if res is None:  # non-zero ranks
-        return
+        return None
     out = {
         "metric": METRIC,
         "value": round(res["value"], 2),
@@ -123,16 +146,19 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(res["value"] / BASELINE_TPS, 2),
-        "dtype": "int8 W8A8 (bf16 activations/accum-dequant)" if args.quant != "none" else "bf16",
-        "data": "synthetic (random-init Llama-2-7B weights, random prompt ids)",
+        "dtype": "int8" if args.quant != "none" else "bf16",
+        "data": "synthetic (random-init Llama-2-7B weights, SmoothQuant-calibrated on random tokens; random prompts)",
         "config": {"model": args.model, "global_batch": res["global_batch"], "seq_len": args.prompt_len,
                    "parallelism": f"pp{args.gpus}", "quant": args.quant, "micro_batch": args.micro_batch,
-                   "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1"},
+                   "micro_batches_in_flight": max(1, args.gpus), "partition": res.get("partition"),
+                   "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1",
+                   "compute": "W8A8 INT8 MFMA GEMMs, bf16 attention/norms, bf16 LM head"},
         "p50_token_latency_ms": round(res["p50"], 4),
         "prefill_tokens_per_s": round(res.get("prefill_tps", 0.0), 1),
         "peak_mem_gb": round(res.get("mem_gb", 0.0), 2),
     }
     print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":

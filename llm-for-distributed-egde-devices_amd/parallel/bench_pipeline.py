@@ -2,9 +2,11 @@
 
 Timed region = ticks [t_a, t_b) with the pipeline full: t_a = M + W*M + (P-1), t_b = t_a + K*M,
 i.e. exactly K decode steps of every sequence (K*M micro-batch items per stage), bracketed on
-every rank by cuda-synchronize + barrier; the reported time is the max over ranks.
+every rank by device-synchronize + barrier; the reported time is the max over ranks.
 p50 per-token latency = median interval between consecutive tokens of one sequence (M ticks),
-from device events on the last stage.
+from device events on the last stage (host timestamps on CPU).
+Runs on CPU with gloo when no GPU is present (``--device cpu``), which is how the multi-process
+path is tested without GPUs.
 """
 from __future__ import annotations
 
@@ -15,18 +17,21 @@ import torch
 import torch.distributed as dist
 
 from ..engine.generate import SamplingParams
-from ..models.configs import get_config
 from .partition import partition_model, stage_costs
 from .pipeline import PipelineStage, init_distributed
 
 
-def run_pipeline_bench(args, build):
-    rank, world = init_distributed("nccl")
+def run_pipeline_bench(args, build, model_config):
+    """``build(args, device, first, last) -> (cfg, stage_model)``; ``model_config(args) -> cfg``."""
+    use_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
+    rank, world = init_distributed("nccl" if use_cuda else "gloo")
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local)
-    cfg = get_config(args.model)
+    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    cfg = model_config(args)
     wbytes = 1.0 if args.quant != "none" else 2.0
-    bounds = partition_model(cfg, world, "balanced", weight_bytes=wbytes)
+    explicit = args.partition if "," in args.partition else None
+    bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
+                             weight_bytes=wbytes, explicit=explicit)
     _, model = build(args, device, first=bounds[rank], last=bounds[rank + 1])
     M, P, b, T = world, world, args.micro_batch, args.prompt_len
     W, K = args.warmup, args.steps
@@ -34,36 +39,46 @@ def run_pipeline_bench(args, build):
     g = torch.Generator().manual_seed(args.seed)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)] if rank == 0 else None
     stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs)
-    # initialise the RCCL communicator with a collective every rank joins
+    # initialise the communicator with a collective every rank joins
     x = torch.ones(1, device=device)
     dist.all_reduce(x)
-    torch.cuda.synchronize()
+    if use_cuda:
+        torch.cuda.synchronize()
     t_a = M + W * M + (P - 1)
     t_b = t_a + K * M
     marks = {}
-    events = []
+    stamps = []
 
     def hook(t):
         if t in (t_a, t_b):
-            torch.cuda.synchronize()
+            if use_cuda:
+                torch.cuda.synchronize()
             dist.barrier()
-            torch.cuda.synchronize()
+            if use_cuda:
+                torch.cuda.synchronize()
             marks[t] = time.perf_counter()
         if stage.is_last and t_a <= t <= t_b and (t - t_a) % M == 0:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            events.append(ev)
+            if use_cuda:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                stamps.append(ev)
+            else:
+                stamps.append(time.perf_counter())
 
     sp = SamplingParams(max_new_tokens=S + 1, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
     stage.run(prompts, T, sp, S, seed=args.seed, hook=hook)
-    dt = torch.tensor([marks[t_b] - marks[t_a]], device=device, dtype=torch.float64)
+    fdt = torch.float64
+    dt = torch.tensor([marks[t_b] - marks[t_a]], device=device, dtype=fdt)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    lat = torch.zeros(1, device=device, dtype=torch.float64)
-    if stage.is_last and len(events) > 1:
-        iv = sorted(events[i - 1].elapsed_time(events[i]) for i in range(1, len(events)))
+    lat = torch.zeros(1, device=device, dtype=fdt)
+    if stage.is_last and len(stamps) > 1:
+        if use_cuda:
+            iv = sorted(stamps[i - 1].elapsed_time(stamps[i]) for i in range(1, len(stamps)))
+        else:
+            iv = sorted((stamps[i] - stamps[i - 1]) * 1e3 for i in range(1, len(stamps)))
         lat[0] = iv[len(iv) // 2]
     dist.all_reduce(lat, op=dist.ReduceOp.MAX)
-    mem = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9], device=device, dtype=torch.float64)
+    mem = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9 if use_cuda else 0.0], device=device, dtype=fdt)
     dist.all_reduce(mem, op=dist.ReduceOp.MAX)
     elapsed = float(dt.item())
     res = None

@@ -58,10 +58,8 @@ def save_quantized(model: DecoderLM, path: str, extra: Optional[dict] = None) ->
         if any(name.startswith(q + ".") for q in quant_names):
             continue
         tensors[name] = prm.detach().cpu().contiguous()
-    for name, s in (getattr(model, "smooth_factors", None) or {}).items():
-        lname = name.split(".", 2)
-        glob_name = f"layers.{model.layers[int(lname[1])].idx}.{lname[2]}"
-        tensors["smooth." + glob_name] = s.float().contiguous()
+    for name, s in (getattr(model, "smooth_factors", None) or {}).items():   # keys: global layer index
+        tensors["smooth." + name] = s.float().contiguous()
     save_file(tensors, os.path.join(path, "model.safetensors"))
     meta = {"format": FORMAT, "version": VERSION, "mode": mode, "model_config": model.cfg.to_dict(),
             "smoothing": "folded" if mode == "w8a8_smoothquant" else "none", "first": model.first,

@@ -70,7 +70,8 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
     g = hq // hk
     factors: Dict[str, torch.Tensor] = {}
     for j, layer in enumerate(model.layers):
-        pre = f"layers.{j}."
+        pre = f"layers.{j}."                       # stats are keyed by local module names
+        gpre = f"layers.{layer.idx}."               # factors by GLOBAL layer index
         qkv, o, up, down = layer.attn.qkv, layer.attn.o, layer.mlp.up, layer.mlp.down
         dev = qkv.weight.device
         # ---- qkv (+ up when phi shares the norm)
@@ -82,14 +83,14 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
                 wmax = torch.maximum(wmax, up.weight.float().abs().amax(0))
             s = _smooth_factor(xs.to(dev), wmax, alpha)
             _fold_norm(layer.norm1, s)
-            factors[pre + "attn.qkv"] = s
+            factors[gpre + "attn.qkv"] = s
             if cfg.shared_input_norm:
-                factors[pre + "mlp.up"] = s
+                factors[gpre + "mlp.up"] = s
         # ---- up (separate norm2)
         if not cfg.shared_input_norm and pre + "mlp.up" in stats:
             s = _smooth_factor(stats[pre + "mlp.up"].to(dev), up.weight.float().abs().amax(0), alpha)
             _fold_norm(layer.norm2, s)
-            factors[pre + "mlp.up"] = s
+            factors[gpre + "mlp.up"] = s
         # ---- o: fold into v rows (shared across the q heads of a kv group)
         if pre + "attn.o" in stats:
             xs = stats[pre + "attn.o"].to(dev).view(hk, g, d).amax(1)              # [hk, d]
@@ -99,7 +100,7 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
             qkv.weight[vs:] = (qkv.weight[vs:].float() / s_kv.reshape(-1, 1)).to(qkv.weight.dtype)
             if qkv.bias is not None:
                 qkv.bias[vs:] = (qkv.bias[vs:].float() / s_kv.reshape(-1)).to(qkv.bias.dtype)
-            factors[pre + "attn.o"] = s_kv[:, None, :].expand(hk, g, d).reshape(-1)
+            factors[gpre + "attn.o"] = s_kv[:, None, :].expand(hk, g, d).reshape(-1)
         # ---- down: fold into the up half of the GLU weight
         if cfg.is_glu and pre + "mlp.down" in stats:
             f = cfg.intermediate_size
@@ -107,7 +108,7 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
             up.weight[f:] = (up.weight[f:].float() / s[:, None]).to(up.weight.dtype)
             if up.bias is not None:
                 up.bias[f:] = (up.bias[f:].float() / s).to(up.bias.dtype)
-            factors[pre + "mlp.down"] = s
+            factors[gpre + "mlp.down"] = s
     return factors
 
 
@@ -125,27 +126,31 @@ def synthetic_calibration(cfg, n: int = 4, T: int = 64, device=None, seed: int =
 
 @torch.no_grad()
 def quantize_model(model: DecoderLM, mode: str, calib_ids: Optional[torch.Tensor] = None, alpha: float = 0.5,
-                   threshold: float = 6.0) -> DecoderLM:
+                   threshold: float = 6.0, factors: Optional[Dict[str, torch.Tensor]] = None) -> DecoderLM:
     """Replace every attention/MLP projection of ``model`` in place.
 
     mode: "w8a8_smoothquant" (calibrate + smooth + W8A8), "w8a8" (no smoothing),
-          "llm_int8" (bitsandbytes-compatible), "cpu_dynamic" (torch qint8 dynamic, CPU)."""
+          "llm_int8" (bitsandbytes-compatible), "cpu_dynamic" (torch qint8 dynamic, CPU).
+    ``factors`` (keyed by GLOBAL layer index) = smoothing already folded into this model's norms
+    (pipeline stages cut from a calibrated full model, see ``smoothquant_stage``)."""
     assert mode in QUANT_MODES, mode
     if mode == "none":
         return model
-    factors: Dict[str, torch.Tensor] = {}
-    if mode == "w8a8_smoothquant":
-        if calib_ids is None:
-            calib_ids = synthetic_calibration(model.cfg, device=model.device)
-        stats = collect_act_absmax(model, calib_ids.to(model.device))
-        factors = smooth_model_(model, stats, alpha)
-    for j, layer in enumerate(model.layers):
-        pre = f"layers.{j}."
+    if factors is None:
+        factors = {}
+        if mode == "w8a8_smoothquant":
+            if calib_ids is None:
+                calib_ids = synthetic_calibration(model.cfg, device=model.device)
+            stats = collect_act_absmax(model, calib_ids.to(model.device))
+            factors = smooth_model_(model, stats, alpha)
+    for layer in model.layers:
+        gpre = f"layers.{layer.idx}."
         for parent, attr, key in ((layer.attn, "qkv", "attn.qkv"), (layer.attn, "o", "attn.o"),
                                   (layer.mlp, "up", "mlp.up"), (layer.mlp, "down", "mlp.down")):
             lin = getattr(parent, attr)
             if mode in ("w8a8_smoothquant", "w8a8"):
-                new = W8A8Linear.from_float(lin, factors.get(pre + key))
+                s = factors.get(gpre + key)
+                new = W8A8Linear.from_float(lin, s.to(lin.weight.device) if s is not None else None)
             elif mode == "llm_int8":
                 new = LLMInt8Linear.from_float(lin, threshold)
             else:
@@ -153,8 +158,26 @@ def quantize_model(model: DecoderLM, mode: str, calib_ids: Optional[torch.Tensor
             setattr(parent, attr, new)
     model.quant_mode = mode
     if mode == "w8a8_smoothquant":
-        model.smooth_factors = {k: v.detach().cpu() for k, v in factors.items()}
+        model.smooth_factors = {k: v.detach().cpu() for k, v in factors.items()
+                                if model.first <= int(k.split(".")[1]) < model.last}
     return model
+
+
+@torch.no_grad()
+def smoothquant_stage(full: DecoderLM, first: int, last: int, calib_ids: torch.Tensor, alpha: float = 0.5,
+                      device=None) -> DecoderLM:
+    """Calibrate + smooth the FULL model once, then cut layers [first, last) into a W8A8 stage.
+    Every pipeline split (1/2/4/8) therefore gets bit-identical quantised weights for a layer."""
+    from ..models.decoder import global_named_parameters
+    stats = collect_act_absmax(full, calib_ids.to(full.device))
+    factors = smooth_model_(full, stats, alpha)
+    stage = DecoderLM(full.cfg, dtype=full.dtype, device=device or full.device, first=first, last=last).eval()
+    src = dict(global_named_parameters(full))
+    for name, p in global_named_parameters(stage):
+        if name == "lm_head.weight" and name not in src:
+            name = "embed"                     # tied head on a head-only stage
+        p.copy_(src[name])
+    return quantize_model(stage, "w8a8_smoothquant", factors=factors)
 
 
 def is_graph_safe(model: nn.Module) -> bool:

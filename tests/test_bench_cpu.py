@@ -1,0 +1,51 @@
+"""bench.py contract on CPU: single-process and torchrun (gloo, 2 ranks) legs print one JSON
+line with the required fields (the driver runs the same script on MI355X with RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _last_json(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+COMMON = ["--device", "cpu", "--model", "tiny:llama", "--micro-batch", "2", "--steps", "3", "--warmup", "1",
+          "--prompt-len", "6"]
+
+
+def test_bench_single_cpu():
+    r = subprocess.run([sys.executable, "bench.py", *COMMON], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert REQUIRED <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
+    assert d["config"]["global_batch"] == 2 and d["config"]["parallelism"] == "pp1"
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_pipeline_torchrun_cpu(n):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *COMMON]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n and d["value"] > 0
+    assert d["config"]["parallelism"] == f"pp{n}" and len(d["config"]["partition"]) == n + 1
