@@ -97,7 +97,8 @@ class _DecodeState:
 
 class Generator:
     def __init__(self, model: DecoderLM, max_batch: int = 1, max_seq: Optional[int] = None,
-                 use_graphs: Optional[bool] = None, eos_check_every: int = 8, kv: Optional[KVCache] = None):
+                 use_graphs: Optional[bool] = None, eos_check_every: int = 8, kv: Optional[KVCache] = None,
+                 prefill_chunk: Optional[int] = None):
         assert model.has_embed and model.has_head, "Generator needs a full model (use parallel.pipeline for stages)"
         self.model = model
         self.cfg = model.cfg
@@ -109,7 +110,8 @@ class Generator:
         self.rope = model.rope_table(self.device)
         # HeadInfer (edgellm.offload) caches carry an attention hook and a prefill chunk size
         self.attn_hook = getattr(self.kv, "attn_hook", None)
-        self.prefill_chunk = getattr(self.kv, "chunk_size", None) if self.attn_hook is not None else None
+        self.prefill_chunk = prefill_chunk or (getattr(self.kv, "chunk_size", None) if self.attn_hook is not None
+                                               else None)
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self.eos_check_every = eos_check_every
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}

@@ -141,9 +141,12 @@ class PipelineStage:
     # ------------------------------------------------------------------ schedule
     @torch.no_grad()
     def run(self, prompts: Optional[Sequence[torch.Tensor]], prompt_len: int, sampling: SamplingParams,
-            decode_steps: int, seed: int = 0, hook: Optional[Callable[[int], None]] = None) -> PipelineResult:
+            decode_steps: int, seed: int = 0, hook: Optional[Callable[[int], None]] = None,
+            watchdog=None, fault: Optional[Callable[[int], None]] = None) -> PipelineResult:
         """prompts: M tensors [b, T] of token ids (needed on rank 0 only; T = prompt_len).
-        decode_steps = tokens generated per sequence after the first (prefill-sampled) one."""
+        decode_steps = tokens generated per sequence after the first (prefill-sampled) one.
+        ``watchdog`` (parallel.watchdog.Watchdog) gets a heartbeat per tick; ``fault(tick)`` is a
+        test hook that may delay or raise before a tick's exchange (fault injection)."""
         M, P, b, T = self.M, self.world, self.b, prompt_len
         S = decode_steps
         assert T + S + 1 <= self.max_seq
@@ -193,6 +196,10 @@ class PipelineStage:
         for t in range(n_ticks):
             if hook is not None:
                 hook(t)
+            if watchdog is not None:
+                watchdog.beat(f"rank {self.rank} tick {t}/{n_ticks}")
+            if fault is not None:
+                fault(t)
             cur, prv = t - self.rank, t - 1 - self.rank
             sends, recvs = [], []
             if P > 1:

@@ -14,7 +14,9 @@ def _run(device, h_on, chunk_heads, chunk_size, kvh=4, arch="llama", dtype=torch
     m = build_model(cfg, dtype=dtype, device=device, seed=9)
     prompts = [[(7 * i + 3 * b) % cfg.vocab_size for i in range(T)] for b in range(2)]
     sp = SamplingParams(max_new_tokens=new, temperature=0.8, top_k=20, top_p=0.95, repetition_penalty=1.1)
-    ref = Generator(m, max_batch=2, max_seq=64, use_graphs=False).generate(prompts, sp, seed=4)
+    # same chunked prefill on both sides: only the offload differs (chunking changes bf16 GEMM shapes)
+    ref = Generator(m, max_batch=2, max_seq=64, use_graphs=False, prefill_chunk=chunk_size).generate(prompts, sp,
+                                                                                                   seed=4)
     kv = HeadInferKV(cfg, 2, 64, h_on=h_on, device=device, chunk_heads=chunk_heads, chunk_size=chunk_size,
                      dtype=dtype)
     got = Generator(m, max_batch=2, max_seq=64, kv=kv).generate(prompts, sp, seed=4)

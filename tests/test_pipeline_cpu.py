@@ -77,6 +77,49 @@ def test_pipeline_matches_unsplit(world, M, do_sample):
     assert got == _reference(arch, M, b, T, S, do_sample)
 
 
+def _stall_worker(rank, world, port, marker):
+    import time as _t
+    import edgellm  # noqa: F401
+    from edgellm.parallel.pipeline import PipelineStage
+    from edgellm.parallel.watchdog import Watchdog
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = tiny("llama", num_layers=2)
+    model = build_model(cfg, dtype=torch.float32, first=rank, last=rank + 1, seed=7)
+    st = PipelineStage(model, rank, world, 1, 2, max_seq=32)
+    def on_timeout(msg):
+        with open(marker, "w") as f:
+            f.write(f"{rank}|{msg}")
+        os._exit(0)
+
+    wd = Watchdog(timeout_s=1.5, on_timeout=on_timeout)
+
+    def fault(t):  # rank 1 hangs at tick 3 (a dead peer); rank 0's watchdog must fire
+        if rank == 1 and t == 3:
+            _t.sleep(30)
+            os._exit(0)
+
+    prompts = [torch.randint(0, cfg.vocab_size, (1, 4)) for _ in range(2)]
+    with wd:
+        st.run(prompts if rank == 0 else None, 4, SamplingParams(max_new_tokens=8, do_sample=False), 6,
+               watchdog=wd, fault=fault)
+
+
+def test_watchdog_detects_stalled_peer(tmp_path):
+    ctx = mp.get_context("spawn")
+    marker = str(tmp_path / "fired")
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, marker)) for r in range(2)]
+    for p in procs:
+        p.start()
+    procs[0].join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    rank, msg = open(marker).read().split("|", 1)
+    assert rank == "0" and "no progress" in msg
+
+
 def test_balanced_partition():
     costs = [1.0] * 32
     b = balanced_partition(costs, 8, head_cost=1.3)
