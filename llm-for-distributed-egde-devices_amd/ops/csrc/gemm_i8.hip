@@ -111,15 +111,25 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
 // M <= 16 variant with NTW n-tiles per workgroup: each A fragment (one per k-tile) feeds NTW
 // MFMAs, cutting the L2->CU activation traffic NTW-fold (at M = 16 an A fragment is as large as
 // a weight fragment, so with NTW = 1 the kernel moves twice the bytes it must).
+// For M > 16 every 16-row block is its own workgroup; the block order is XCD-grouped: dispatch
+// ids b, b+8, b+16, ... land on one XCD, so the MB row blocks of a weight panel are consecutive
+// ids within one XCD (id = xcd + 8 * (mb + MB * panel_group)) and re-read the panel from that
+// XCD's L2 instead of HBM (placement is a speed assumption only, never a correctness one).
 template <int UNROLL, int NW, int NTW>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                 const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                 const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                                 int M, int N, int K, int KT, int NTt) {
   __shared__ v4i red[NW][NTW][64];
-  const int nt0 = blockIdx.x * NTW;
+  const int MB = (M + 15) / 16;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, r = bid >> 3;
+  const int mb = r % MB, panel = xcd + 8 * (r / MB);
+  const int nt0 = panel * NTW;
+  if (nt0 >= NTt) return;                                   // grid padded to a multiple of 8 panels
+  const int m0 = mb * 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int arow = lane & 15, akc = 16 * (lane >> 4);
+  const int arow = m0 + (lane & 15), akc = 16 * (lane >> 4);
   v4i acc[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) acc[j] = v4i{0, 0, 0, 0};
@@ -170,7 +180,7 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
     for (int w = 1; w < NW; ++w) s += red[w][j][lane];
     const int col = (nt0 + j) * 16 + (lane & 15);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) store_out(out, M, N, 4 * (lane >> 4) + r, col, s[r], sa, sw, bias);
+    for (int q = 0; q < 4; ++q) store_out(out, M, N, m0 + 4 * (lane >> 4) + q, col, s[q], sa, sw, bias);
   }
 }
 
@@ -296,12 +306,15 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   int un = g_gemv_unroll > 0 ? g_gemv_unroll : (M <= 2 ? 4 : 2);
   int ntw = 1;
   if (g_gemv_ntw > 0) ntw = g_gemv_ntw;
+  else if (mblocks16 > 1) ntw = 4;                   // M in (16, 64]: amortise A over 4 n-tiles
   else if (M > 2 && NTt >= 1024) ntw = 2;
   else if (M > 2 && NTt >= 512) ntw = 4;
   if (g_gemv_nw <= 0 && M > 2) nw = (NTt >= 1024) ? 4 : (NTt >= 512 ? 8 : (KT >= 128 ? 8 : 16));
-  if (mblocks16 <= 1 && ntw > 1) {
+  if (ntw > 1) {
+    // XCD-grouped 1-D grid: panels padded to a multiple of 8, one workgroup per (panel, 16-row block)
 #define NTWL(U, NWV, NTWV)                                                                                           \
-  hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV>), dim3((NTt + NTWV - 1) / NTWV), dim3(NWV * 64), 0, st,    \
+  hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV>),                                                           \
+                     dim3(((NTt + NTWV - 1) / NTWV + 7) / 8 * 8 * mblocks16), dim3(NWV * 64), 0, st,                  \
                      (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt)
 #define NTWN(NWV)                                                   \
   do {                                                              \

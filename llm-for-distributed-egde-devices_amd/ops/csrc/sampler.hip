@@ -65,6 +65,27 @@ __device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int*
   __syncthreads();
 }
 
+// Block-wide reduction of a u32 (OP 0 = min, 1 = max, 2 = sum); `scratch` holds >= NW words.
+template <int OP>
+__device__ __forceinline__ uint32_t block_reduce_u32(uint32_t v, uint32_t* scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = OP == 0 ? min(v, w) : (OP == 1 ? max(v, w) : v + w);
+  }
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[wv] = v;
+  __syncthreads();
+  uint32_t r = scratch[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) {
+    const uint32_t w = scratch[i];
+    r = OP == 0 ? min(r, w) : (OP == 1 ? max(r, w) : r + w);
+  }
+  return r;
+}
+
 __device__ __forceinline__ float gumbel(uint32_t seed, uint32_t row, uint32_t step, uint32_t idx) {
   const float u = uniform_hash(seed, row, step, idx);
   return -logf(-logf(u));
@@ -98,40 +119,43 @@ __global__ void __launch_bounds__(NT) sample_kernel(const void* __restrict__ log
     }
     block_argmax(bv, bi, rv, ri);
   } else {
-    // ---- radix select: key of the k-th largest processed score
-    uint32_t prefix = 0, pmask = 0;
-    if (tid == 0) k_rem = top_k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      for (int i = lane; i < 256; i += 64) hist[wave][i] = 0;
-      __syncthreads();
-      for (int i = tid; i < V; i += NT) {
-        const uint32_t key = f2key(proc<BF16>(logits, seen, base, i, inv_t, pen));
-        if ((key & pmask) == prefix) atomicAdd(&hist[wave][(key >> shift) & 255u], 1u);
-      }
-      __syncthreads();
-      if (tid < 256) {
-        uint32_t c = 0;
+    // ---- candidate threshold by bisection on order-preserving u32 keys: find thr with
+    // k <= count(key >= thr) <= CAP using block-wide count reductions only (no LDS atomics:
+    // logit keys cluster in a few radix bins, which serialised the old histogram select).
+    // Keys of up to PT elements per thread stay in registers; larger vocabularies re-read L2.
+    constexpr int PT = 48;
+    uint32_t kr[PT];
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) c += hist[w][tid];
-        hist[0][tid] = c;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        int need = k_rem;
-        int b = 255;
-        for (; b > 0; --b) {
-          const int c = (int)hist[0][b];
-          if (c >= need) break;
-          need -= c;
-        }
-        sel_bin = b;
-        k_rem = need;
-      }
-      __syncthreads();
-      prefix |= ((uint32_t)sel_bin) << shift;
-      pmask |= 255u << shift;
+    for (int j = 0; j < PT; ++j) {
+      const int i = tid + j * NT;
+      kr[j] = (i < V) ? f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) : 0u;
+      if (i < V) { kmin = min(kmin, kr[j]); kmax = max(kmax, kr[j]); }
     }
-    const uint32_t thr = prefix;  // key of the k-th largest
+    for (int i = tid + PT * NT; i < V; i += NT) {
+      const uint32_t k = f2key(proc<BF16>(logits, seen, base, i, inv_t, pen));
+      kmin = min(kmin, k);
+      kmax = max(kmax, k);
+    }
+    kmin = block_reduce_u32<0>(kmin, &hist[0][0]);
+    kmax = block_reduce_u32<1>(kmax, &hist[0][0]);
+    uint32_t lo = kmin, hi = kmax;   // invariant: count(>= lo) >= k ; count(>= hi + 1) < k or hi = max
+    uint32_t thr = lo;
+    for (int it = 0; it < 40 && lo < hi; ++it) {
+      const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < PT; ++j) c += (tid + j * NT < V && kr[j] >= mid) ? 1 : 0;
+      for (int i = tid + PT * NT; i < V; i += NT) c += f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) >= mid;
+      c = (int)block_reduce_u32<2>((uint32_t)c, &hist[0][0]);
+      if (c >= top_k) {
+        lo = mid;
+        if (c <= CAP) break;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    thr = lo;
     // ---- compact candidates (key >= thr)
     if (tid == 0) ncand = 0;
     __syncthreads();
@@ -164,9 +188,19 @@ __global__ void __launch_bounds__(NT) sample_kernel(const void* __restrict__ log
         __syncthreads();
       }
     }
+    // ---- exact top-k cut: keep every candidate >= the k-th largest value (ties kept, as HF)
+    __shared__ int nkeep_s;
+    if (tid == 0) {
+      int nk = min(top_k, n);
+      const float kth = cv[nk - 1];
+      while (nk < n && cv[nk] >= kth) ++nk;
+      nkeep_s = nk;
+    }
+    __syncthreads();
+    const int nk = nkeep_s;
     // ---- top-p: exclusive prefix of softmax mass in descending order
     const float m = cv[0];
-    for (int i = tid; i < P; i += NT) pref[i] = (i < n) ? __expf(cv[i] - m) : 0.f;
+    for (int i = tid; i < P; i += NT) pref[i] = (i < nk) ? __expf(cv[i] - m) : 0.f;
     __syncthreads();
     // Hillis-Steele inclusive scan over P <= 1024 entries
     for (int off = 1; off < P; off <<= 1) {
@@ -176,9 +210,9 @@ __global__ void __launch_bounds__(NT) sample_kernel(const void* __restrict__ log
       if (tid < P && tid >= off) pref[tid] += t;
       __syncthreads();
     }
-    const float total = pref[n - 1];
+    const float total = pref[nk - 1];
     // ---- Gumbel-argmax over kept candidates
-    if (tid < n) {
+    if (tid < nk) {
       const float excl = (tid == 0) ? 0.f : pref[tid - 1];
       const bool keep = (tid == 0) || (top_p >= 1.f) || (excl / total < top_p);
       if (keep) {

@@ -171,7 +171,8 @@ def test_w8a8_gemm(cuda, M, N, K):
 
 
 @pytest.mark.parametrize("ntw,nw,u", [(2, 4, 2), (4, 8, 4), (4, 16, 2), (2, 16, 4)])
-@pytest.mark.parametrize("M,N,K", [(16, 160, 96), (7, 22016, 4096), (16, 4096, 11008), (3, 1040, 128)])
+@pytest.mark.parametrize("M,N,K", [(16, 160, 96), (7, 22016, 4096), (16, 4096, 11008), (3, 1040, 128),
+                                   (33, 4096, 4096), (64, 12288, 4096), (50, 1040, 128)])
 def test_w8a8_gemv_variants(cuda, ntw, nw, u, M, N, K):
     """Every tuning variant of the skinny kernel (incl. multi-n-tile workgroups with ragged tails)."""
     C = ops.ext()
