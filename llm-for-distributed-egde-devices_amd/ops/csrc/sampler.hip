@@ -1,4 +1,4 @@
-// Fused token sampler — one 1024-thread workgroup per row, one launch per step.
+// Fused token sampler — one workgroup per row, one launch per step.
 //
 // Semantics = HF generate(do_sample=True) processor order used by the reference
 // (combine_model_fp_updated.py:95-105): repetition penalty on already-seen ids (divide positive,
@@ -8,16 +8,18 @@
 // sampling from the processed softmax, deterministic and bit-reproducible against
 // ops/_ref.py::sample.  HF launches ~10 kernels per token for this; here it is one.
 //
-// top-k threshold: 4-pass MSB radix select on order-preserving u32 keys with per-wave LDS
-// histograms (no global sort).  Candidates (>= threshold, <= CAP) are compacted to LDS,
-// bitonic-sorted, softmax-scanned for top-p, then Gumbel-argmaxed.
+// top-k / top-p (MODE 2, 256 threads): the processed scores' order-preserving u32 keys stay in
+// registers; a bisection on the key space with block-wide count reductions (no atomics — logit
+// keys cluster in a few radix bins) finds a threshold with k <= count <= TARGET; the candidates
+// are compacted to LDS and every thread ranks its candidate against all others (O(n^2) reads of
+// broadcast LDS words, no sort stages / barriers), which gives the exact k-th value, the
+// descending-order softmax prefix for top-p and the Gumbel-max winner.
 // The step counter is read from device memory (rng[1]) so the launch can live in a HIP graph.
 #include "common.h"
 
 namespace {
-constexpr int NT = 1024;
-constexpr int NW = NT / 64;
-constexpr int CAP = 1024;
+constexpr int CAP = 1024;     // max candidates kept (ties beyond are truncated)
+constexpr int TARGET = 128;   // bisection stops once k <= count <= max(TARGET, k)
 
 __device__ __forceinline__ uint32_t f2key(float f) {
   uint32_t u = __float_as_uint(f);
@@ -37,8 +39,9 @@ __device__ __forceinline__ float proc(const void* lg, const uint8_t* seen, size_
   return s * inv_t;
 }
 
-// argmax with lowest-index tie break, block-wide (NT threads)
+template <int NT>
 __device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int* ri) {
+  constexpr int NW = NT / 64;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ov = __shfl_xor(v, o, 64);
@@ -46,27 +49,18 @@ __device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int*
     if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
   }
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (l == 0) { rv[w] = v; ri[w] = idx; }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    v = threadIdx.x < NW ? rv[threadIdx.x] : -INFINITY;
-    idx = threadIdx.x < NW ? ri[threadIdx.x] : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(v, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-    }
-    if (threadIdx.x == 0) { rv[0] = v; ri[0] = idx; }
-  }
+  if (l == 0) { rv[w] = v; ri[w] = idx; }
   __syncthreads();
   v = rv[0];
   idx = ri[0];
-  __syncthreads();
+#pragma unroll
+  for (int i = 1; i < NW; ++i)
+    if (rv[i] > v || (rv[i] == v && ri[i] < idx)) { v = rv[i]; idx = ri[i]; }
 }
 
-// Block-wide reduction of a u32 (OP 0 = min, 1 = max, 2 = sum); `scratch` holds >= NW words.
-template <int OP>
+// Block-wide reduction of a u32 (OP 0 = min, 1 = max, 2 = sum); `scratch` holds >= NT/64 words.
+template <int NT, int OP>
 __device__ __forceinline__ uint32_t block_reduce_u32(uint32_t v, uint32_t* scratch) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -79,7 +73,7 @@ __device__ __forceinline__ uint32_t block_reduce_u32(uint32_t v, uint32_t* scrat
   __syncthreads();
   uint32_t r = scratch[0];
 #pragma unroll
-  for (int i = 1; i < NW; ++i) {
+  for (int i = 1; i < NT / 64; ++i) {
     const uint32_t w = scratch[i];
     r = OP == 0 ? min(r, w) : (OP == 1 ? max(r, w) : r + w);
   }
@@ -91,137 +85,172 @@ __device__ __forceinline__ float gumbel(uint32_t seed, uint32_t row, uint32_t st
   return -logf(-logf(u));
 }
 
-// MODE 0: greedy argmax of penalised logits; 1: Gumbel over full vocab; 2: top-k (+ top-p)
+// ---------------------------------------------------------------- greedy / full-vocab sampling
 template <bool BF16, int MODE>
-__global__ void __launch_bounds__(NT) sample_kernel(const void* __restrict__ logits, uint8_t* __restrict__ seen, int V,
-                                                    float inv_t, float pen, int top_k, float top_p,
-                                                    const int* __restrict__ rng, int64_t* __restrict__ out_tok) {
-  __shared__ float rv[NW];
-  __shared__ int ri[NW];
-  __shared__ uint32_t hist[NW][256];
-  __shared__ float cv[CAP];
-  __shared__ int ci[CAP];
-  __shared__ float pref[CAP];
-  __shared__ int ncand, sel_bin, k_rem;
-
+__global__ void __launch_bounds__(1024) sample_argmax_kernel(const void* __restrict__ logits, uint8_t* __restrict__ seen,
+                                                             int V, float inv_t, float pen,
+                                                             const int* __restrict__ rng, int64_t* __restrict__ out_tok) {
+  constexpr int NT = 1024;
+  __shared__ float rv[NT / 64];
+  __shared__ int ri[NT / 64];
   const int row = blockIdx.x;
   const size_t base = (size_t)row * V;
   const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-
-  if constexpr (MODE == 0 || MODE == 1) {
-    for (int i = tid; i < V; i += NT) {
-      float s = proc<BF16>(logits, seen, base, i, MODE == 0 ? 1.f : inv_t, pen);
-      if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
-      if (s > bv || (s == bv && i < bi)) { bv = s; bi = i; }
-    }
-    block_argmax(bv, bi, rv, ri);
-  } else {
-    // ---- candidate threshold by bisection on order-preserving u32 keys: find thr with
-    // k <= count(key >= thr) <= CAP using block-wide count reductions only (no LDS atomics:
-    // logit keys cluster in a few radix bins, which serialised the old histogram select).
-    // Keys of up to PT elements per thread stay in registers; larger vocabularies re-read L2.
-    constexpr int PT = 48;
-    uint32_t kr[PT];
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
-#pragma unroll
-    for (int j = 0; j < PT; ++j) {
-      const int i = tid + j * NT;
-      kr[j] = (i < V) ? f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) : 0u;
-      if (i < V) { kmin = min(kmin, kr[j]); kmax = max(kmax, kr[j]); }
-    }
-    for (int i = tid + PT * NT; i < V; i += NT) {
-      const uint32_t k = f2key(proc<BF16>(logits, seen, base, i, inv_t, pen));
-      kmin = min(kmin, k);
-      kmax = max(kmax, k);
-    }
-    kmin = block_reduce_u32<0>(kmin, &hist[0][0]);
-    kmax = block_reduce_u32<1>(kmax, &hist[0][0]);
-    uint32_t lo = kmin, hi = kmax;   // invariant: count(>= lo) >= k ; count(>= hi + 1) < k or hi = max
-    uint32_t thr = lo;
-    for (int it = 0; it < 40 && lo < hi; ++it) {
-      const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
-      int c = 0;
-#pragma unroll
-      for (int j = 0; j < PT; ++j) c += (tid + j * NT < V && kr[j] >= mid) ? 1 : 0;
-      for (int i = tid + PT * NT; i < V; i += NT) c += f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) >= mid;
-      c = (int)block_reduce_u32<2>((uint32_t)c, &hist[0][0]);
-      if (c >= top_k) {
-        lo = mid;
-        if (c <= CAP) break;
-      } else {
-        hi = mid - 1;
-      }
-    }
-    thr = lo;
-    // ---- compact candidates (key >= thr)
-    if (tid == 0) ncand = 0;
-    __syncthreads();
-    for (int i = tid; i < V; i += NT) {
-      const float s = proc<BF16>(logits, seen, base, i, inv_t, pen);
-      if (f2key(s) >= thr) {
-        const int slot = atomicAdd(&ncand, 1);
-        if (slot < CAP) { cv[slot] = s; ci[slot] = i; }
-      }
-    }
-    __syncthreads();
-    const int n = min(ncand, CAP);
-    int P = 1;
-    while (P < n) P <<= 1;
-    for (int i = n + tid; i < P; i += NT) { cv[i] = -INFINITY; ci[i] = 0x7fffffff; }
-    __syncthreads();
-    // ---- bitonic sort, descending by value, ascending index on ties
-    for (int k = 2; k <= P; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < P; i += NT) {
-          const int p = i ^ j;
-          if (p > i) {
-            const bool desc = (i & k) == 0;
-            const float a = cv[i], b = cv[p];
-            const int ia = ci[i], ib = ci[p];
-            const bool a_first = (a > b) || (a == b && ia < ib);
-            if (desc ? !a_first : a_first) { cv[i] = b; cv[p] = a; ci[i] = ib; ci[p] = ia; }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    // ---- exact top-k cut: keep every candidate >= the k-th largest value (ties kept, as HF)
-    __shared__ int nkeep_s;
-    if (tid == 0) {
-      int nk = min(top_k, n);
-      const float kth = cv[nk - 1];
-      while (nk < n && cv[nk] >= kth) ++nk;
-      nkeep_s = nk;
-    }
-    __syncthreads();
-    const int nk = nkeep_s;
-    // ---- top-p: exclusive prefix of softmax mass in descending order
-    const float m = cv[0];
-    for (int i = tid; i < P; i += NT) pref[i] = (i < nk) ? __expf(cv[i] - m) : 0.f;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over P <= 1024 entries
-    for (int off = 1; off < P; off <<= 1) {
-      float t = 0.f;
-      if (tid < P && tid >= off) t = pref[tid - off];
-      __syncthreads();
-      if (tid < P && tid >= off) pref[tid] += t;
-      __syncthreads();
-    }
-    const float total = pref[nk - 1];
-    // ---- Gumbel-argmax over kept candidates
-    if (tid < nk) {
-      const float excl = (tid == 0) ? 0.f : pref[tid - 1];
-      const bool keep = (tid == 0) || (top_p >= 1.f) || (excl / total < top_p);
-      if (keep) {
-        bv = cv[tid] + gumbel(seed, row, step, ci[tid]);
-        bi = ci[tid];
-      }
-    }
-    block_argmax(bv, bi, rv, ri);
+  for (int i = threadIdx.x; i < V; i += NT) {
+    float s = proc<BF16>(logits, seen, base, i, MODE == 0 ? 1.f : inv_t, pen);
+    if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
+    if (s > bv || (s == bv && i < bi)) { bv = s; bi = i; }
   }
+  block_argmax<NT>(bv, bi, rv, ri);
+  if (threadIdx.x == 0) {
+    out_tok[row] = bi;
+    if (seen != nullptr) seen[base + bi] = 1;
+  }
+}
+
+// ---------------------------------------------------------------- top-k (+ top-p)
+template <bool BF16, int PT>
+__global__ void __launch_bounds__(256) sample_topk_kernel(const void* __restrict__ logits, uint8_t* __restrict__ seen,
+                                                          int V, float inv_t, float pen, int top_k, float top_p,
+                                                          const int* __restrict__ rng, int64_t* __restrict__ out_tok) {
+  constexpr int NT = 256;
+  __shared__ uint32_t scratch[NT / 64];
+  __shared__ float rv[NT / 64];
+  __shared__ int ri[NT / 64];
+  __shared__ float cv[CAP];
+  __shared__ int ci[CAP];
+  __shared__ int ncand;
+  __shared__ float kth_s;
+  __shared__ float tot_s[NT / 64];
+  const int row = blockIdx.x;
+  const size_t base = (size_t)row * V;
+  const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
+  const int tid = threadIdx.x;
+
+  // keys in registers (elements beyond PT*NT are re-read from L2 each pass)
+  uint32_t kr[PT];
+  uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = tid + j * NT;
+    kr[j] = (i < V) ? f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) : 0u;
+    if (i < V) { kmin = min(kmin, kr[j]); kmax = max(kmax, kr[j]); }
+  }
+  for (int i = tid + PT * NT; i < V; i += NT) {
+    const uint32_t k = f2key(proc<BF16>(logits, seen, base, i, inv_t, pen));
+    kmin = min(kmin, k);
+    kmax = max(kmax, k);
+  }
+  kmin = block_reduce_u32<NT, 0>(kmin, scratch);
+  kmax = block_reduce_u32<NT, 1>(kmax, scratch);
+  const int target = max(TARGET, top_k);
+  // bisection: invariant count(key >= lo) >= top_k
+  uint32_t lo = kmin, hi = kmax;
+  for (int it = 0; it < 40 && lo < hi; ++it) {
+    const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) c += (tid + j * NT < V && kr[j] >= mid) ? 1 : 0;
+    for (int i = tid + PT * NT; i < V; i += NT) c += f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) >= mid;
+    c = (int)block_reduce_u32<NT, 2>((uint32_t)c, scratch);
+    if (c >= top_k) {
+      lo = mid;
+      if (c <= target) break;
+    } else {
+      hi = mid - 1;
+    }
+  }
+  const uint32_t thr = lo;
+  // compact candidates (key >= thr) into LDS
+  if (tid == 0) ncand = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = tid + j * NT;
+    if (i < V && kr[j] >= thr) {
+      const int slot = atomicAdd(&ncand, 1);
+      if (slot < CAP) { cv[slot] = proc<BF16>(logits, seen, base, i, inv_t, pen); ci[slot] = i; }
+    }
+  }
+  for (int i = tid + PT * NT; i < V; i += NT) {
+    const float s = proc<BF16>(logits, seen, base, i, inv_t, pen);
+    if (f2key(s) >= thr) {
+      const int slot = atomicAdd(&ncand, 1);
+      if (slot < CAP) { cv[slot] = s; ci[slot] = i; }
+    }
+  }
+  __syncthreads();
+  const int n = min(ncand, CAP);
+  // rank every candidate: descending value, ascending token id on ties
+  constexpr int PER = (CAP + NT - 1) / NT;
+  int rank[PER];
+  float myv[PER];
+  int myi[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int c = tid + q * NT;
+    rank[q] = 0x7fffffff;
+    if (c < n) {
+      const float v = cv[c];
+      const int id = ci[c];
+      int r = 0;
+      for (int j = 0; j < n; ++j) {
+        const float w = cv[j];
+        r += (w > v || (w == v && ci[j] < id)) ? 1 : 0;
+      }
+      rank[q] = r;
+      myv[q] = v;
+      myi[q] = id;
+    }
+  }
+  const int kk = min(top_k, n);
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+    if (rank[q] == kk - 1) kth_s = myv[q];
+  if (tid == 0 && n > 0 && kk == 0) kth_s = -INFINITY;
+  __syncthreads();
+  const float kth = kth_s;
+  float vmax = -INFINITY;                               // value of rank 0
+  for (int j = 0; j < n; ++j) vmax = fmaxf(vmax, cv[j]);
+  // softmax mass of the top-k survivors and each one's exclusive prefix in descending order
+  float tot = 0.f;
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+    if (rank[q] != 0x7fffffff && myv[q] >= kth) tot += __expf(myv[q] - vmax);
+  {
+    float t = tot;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if ((tid & 63) == 0) tot_s[tid >> 6] = t;
+    __syncthreads();
+    tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) tot += tot_s[i];
+  }
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (rank[q] == 0x7fffffff || myv[q] < kth) continue;
+    bool keep = rank[q] == 0 || top_p >= 1.f;
+    if (!keep) {
+      float excl = 0.f;
+      const float v = myv[q];
+      const int id = myi[q];
+      for (int j = 0; j < n; ++j) {
+        const float w = cv[j];
+        if (w >= kth && (w > v || (w == v && ci[j] < id))) excl += __expf(w - vmax);
+      }
+      keep = excl / tot < top_p;
+    }
+    if (keep) {
+      const float g = myv[q] + gumbel(seed, row, step, myi[q]);
+      if (g > bv || (g == bv && myi[q] < bi)) { bv = g; bi = myi[q]; }
+    }
+  }
+  block_argmax<NT>(bv, bi, rv, ri);
   if (tid == 0) {
     out_tok[row] = bi;
     if (seen != nullptr) seen[base + bi] = 1;
@@ -232,8 +261,8 @@ __global__ void __launch_bounds__(NT) sample_kernel(const void* __restrict__ log
 // mode: 0 greedy, 1 full-vocab sampling, 2 top-k(+top-p). Returns -5 when the configuration
 // needs the host fallback (top-p without top-k, or top-k beyond CAP).
 extern "C" int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
-                           float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng, int64_t* out_tok,
-                           hipStream_t st) {
+                           float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
+                           int64_t* out_tok, hipStream_t st) {
   if (B == 0) return 0;
   int mode;
   if (!do_sample || temperature <= 0.f) mode = 0;
@@ -241,10 +270,18 @@ extern "C" int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B
   else if (top_k > 0 && top_k <= CAP && top_k < V) mode = 2;
   else return -5;
   const float inv_t = (mode == 0) ? 1.f : inv_temperature;  // host computes 1/T in f64 (matches _ref)
-#define SL(BF, MD) hipLaunchKernelGGL((sample_kernel<BF, MD>), dim3(B), dim3(NT), 0, st, logits, seen, V, inv_t, penalty, \
-                                      top_k, top_p, rng, out_tok)
-  if (is_bf16) { if (mode == 0) SL(true, 0); else if (mode == 1) SL(true, 1); else SL(true, 2); }
-  else { if (mode == 0) SL(false, 0); else if (mode == 1) SL(false, 1); else SL(false, 2); }
+  if (mode == 2) {
+#define TK(BF, PTV) hipLaunchKernelGGL((sample_topk_kernel<BF, PTV>), dim3(B), dim3(256), 0, st, logits, seen, V, inv_t, \
+                                       penalty, top_k, top_p, rng, out_tok)
+    if (is_bf16) { if (V <= 256 * 64) TK(true, 64); else TK(true, 128); }
+    else { if (V <= 256 * 64) TK(false, 64); else TK(false, 128); }
+#undef TK
+  } else {
+#define SL(BF, MD) hipLaunchKernelGGL((sample_argmax_kernel<BF, MD>), dim3(B), dim3(1024), 0, st, logits, seen, V, inv_t, \
+                                      penalty, rng, out_tok)
+    if (is_bf16) { if (mode == 0) SL(true, 0); else SL(true, 1); }
+    else { if (mode == 0) SL(false, 0); else SL(false, 1); }
 #undef SL
+  }
   return (int)hipGetLastError();
 }
