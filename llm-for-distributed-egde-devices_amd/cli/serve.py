@@ -1,0 +1,72 @@
+"""Start the serving front-ends.
+
+    python -m edgellm.cli.serve                                   # TimeService :50051 + REST :8000
+    python -m edgellm.cli.serve --model tiny:llama --rest-port 8000     # + POST /generate engine
+    python -m edgellm.cli.serve --model gpt2 --stage 6:12 --grpc-port 50052  # a gRPC pipeline stage
+
+TimeService and ``GET /`` are wire-compatible with the reference demo (Code/gRPC/server.py,
+rest_api.py); the stage service speaks edgellm.Stage (serve/proto/edgellm_stage.proto).
+"""
+from __future__ import annotations
+
+import argparse
+import threading
+from typing import List, Optional
+
+from ..utils.log import get_logger
+
+log = get_logger("serve")
+
+
+def main(argv: Optional[List[str]] = None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--grpc-port", type=int, default=50051)
+    ap.add_argument("--rest-port", type=int, default=8000)
+    ap.add_argument("--no-rest", action="store_true")
+    ap.add_argument("--model", default=None, help="attach a generation engine (preset, tiny:<arch> or HF dir)")
+    ap.add_argument("--quant", default="none")
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--max-batch", type=int, default=8)
+    ap.add_argument("--max-seq", type=int, default=2048)
+    ap.add_argument("--stage", default=None, help="first:last — serve these layers as a gRPC pipeline stage")
+    args = ap.parse_args(argv)
+
+    import torch
+    from ..serve.time_service import time_service_handler
+    device = args.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+    engine = None
+    extra = []
+    if args.model and args.stage:
+        from ..models.registry import load_model
+        from ..serve.stage_service import StageServer
+        a, b = (int(x) for x in args.stage.split(":"))
+        model, _, src = load_model(args.model, "bf16", args.quant, device, first=a, last=b)
+        extra.append(StageServer(model, max_seq=args.max_seq).handler())
+        log.info(f"stage layers [{a}, {b}) of {src}")
+    elif args.model:
+        from ..engine import Generator
+        from ..models.registry import load_model
+        from ..serve.server import ServingEngine
+        model, tok, src = load_model(args.model, "bf16", args.quant, device)
+        engine = ServingEngine(Generator(model, max_batch=args.max_batch, max_seq=args.max_seq), tok, args.max_batch)
+        log.info(f"generation engine: {src}")
+
+    import grpc
+    from concurrent import futures
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10))
+    server.add_generic_rpc_handlers((time_service_handler(), *extra))
+    server.add_insecure_port(f"[::]:{args.grpc_port}")
+    server.start()
+    print(f"gRPC Server running on port {args.grpc_port}...")
+    if args.no_rest:
+        server.wait_for_termination()
+        return
+    from ..serve.rest import make_app
+    import uvicorn
+    threading.Thread(target=server.wait_for_termination, daemon=True).start()
+    uvicorn.run(make_app(engine), host=args.host, port=args.rest_port)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,8 @@ int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* 
                    int M, int N, int K, int KT, hipStream_t st);
 int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
-                int64_t* out_tok, hipStream_t st);
+                int64_t* out_tok, void* workspace, hipStream_t st);
+size_t edge_sample_workspace(int B, int V);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
@@ -274,10 +275,11 @@ at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& see
   const int64_t B = logits.size(0), V = logits.size(1);
   if (seen) { need(*seen, at::kByte, "seen"); TORCH_CHECK(seen->sizes() == logits.sizes()); }
   auto out = at::empty({B}, logits.options().dtype(at::kLong));
+  auto ws = at::empty({(int64_t)edge_sample_workspace((int)B, (int)V)}, logits.options().dtype(at::kByte));
   const double inv_t = temperature > 0 ? 1.0 / temperature : 1.0;
   const int rc = edge_sample(logits.data_ptr(), bf, seen ? seen->data_ptr<uint8_t>() : nullptr, (int)B, (int)V,
                              (float)temperature, (float)inv_t, (float)penalty, (int)top_k, (float)top_p, do_sample,
-                             rng.data_ptr<int>(), out.data_ptr<int64_t>(), stream());
+                             rng.data_ptr<int>(), out.data_ptr<int64_t>(), ws.data_ptr(), stream());
   if (rc == -5) return at::Tensor();
   check(rc, "sample");
   return out;

@@ -4,8 +4,7 @@
 ``POST /generate`` -> run the attached engine (edgellm.serve.server.ServingEngine)
 ``GET /health``, ``GET /metrics`` (JSON counters: requests, tokens, p50/p99 step latency)
 """
-from __future__ import annotations
-
+# no ``from __future__ import annotations``: FastAPI must resolve the locally defined request model
 from typing import List, Optional
 
 from .time_service import now_string

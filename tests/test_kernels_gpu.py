@@ -191,12 +191,15 @@ def test_w8a8_gemv_variants(cuda, ntw, nw, u, M, N, K):
     _close(out, _ref.w8a8_linear(qx, sx, w, sw, None, torch.float32), 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("V", [512, 50304, 128256])
-@pytest.mark.parametrize("cfg", [(0.7, 50, 0.9, 1.1), (0.5, 30, 0.85, 1.2), (1.0, 0, 1.0, 1.0), (0.8, 20, 1.0, 1.3)])
+@pytest.mark.parametrize("V", [512, 32000, 50304, 128256])
+@pytest.mark.parametrize("cfg", [(0.7, 50, 0.9, 1.1), (0.5, 30, 0.85, 1.2), (1.0, 0, 1.0, 1.0), (0.8, 20, 1.0, 1.3),
+                                 (0.9, 200, 0.95, 1.0), (0.0, 0, 1.0, 1.3)])
 def test_sampler_matches_reference(cuda, V, cfg):
+    """Split-row top-k (k <= 128), single-WG fallback (k = 200), full-vocab and greedy paths."""
     C = ops.ext()
     temp, k, p, pen = cfg
-    B = 4
+    do_sample = temp > 0
+    B = 16 if V == 32000 else 4
     torch.manual_seed(1)
     logits = (torch.randn(B, V, device=cuda) * 4).bfloat16()
     seen = (torch.rand(B, V, device=cuda) < 0.01).to(torch.uint8)
@@ -204,8 +207,8 @@ def test_sampler_matches_reference(cuda, V, cfg):
     for step in range(16):
         rng = torch.tensor([1234, step], dtype=torch.int32, device=cuda)
         s1 = seen.clone()
-        tok = C.sample(logits, s1, temp, k, p, pen, True, rng)
-        ref = _ref.sample(logits, seen, temp, k, p, pen, 1234, step, True)
+        tok = C.sample(logits, s1, temp, k, p, pen, do_sample, rng)
+        ref = _ref.sample(logits, seen, temp, k, p, pen, 1234, step, do_sample)
         mism += (tok.cpu() != ref.cpu()).sum().item()
         assert s1[torch.arange(B), tok].all()
     assert mism <= 1, f"{mism} mismatches"

@@ -86,6 +86,33 @@ def test_gpt2_two_stage_grpc_matches_single_process(do_sample, faults):
         server.stop(0)
 
 
+def test_serving_engine_batches_concurrent_requests():
+    import threading
+    from fastapi.testclient import TestClient
+    from edgellm.serve.rest import make_app
+    from edgellm.serve.server import ServingEngine
+    from edgellm.utils.tokenizer import ByteTokenizer
+    cfg = tiny("llama")
+    m = build_model(cfg, dtype=torch.float32, seed=2)
+    eng = ServingEngine(Generator(m, max_batch=4, max_seq=128), ByteTokenizer(cfg.vocab_size), max_batch=4,
+                        batch_wait_s=0.05)
+    try:
+        sp = SamplingParams(max_new_tokens=5, do_sample=False)
+        futs = [eng.submit([1, 2, 3 + i], sp) for i in range(4)]
+        outs = [f.result(timeout=60) for f in futs]
+        assert all(len(o["tokens"]) == 5 for o in outs)
+        assert eng.metrics()["requests"] == 4 and eng.metrics()["batches"] <= 2
+        # batched results equal the single-request results
+        alone = Generator(m, max_batch=1, max_seq=128).generate([[1, 2, 4]], sp)
+        assert outs[1]["tokens"] == alone.tokens[0]
+        c = TestClient(make_app(eng))
+        r = c.post("/generate", json={"prompt": "hello", "max_new_tokens": 3, "do_sample": False})
+        assert r.status_code == 200 and len(r.json()["tokens"]) == 3
+        assert c.get("/metrics").json()["requests"] == 5
+    finally:
+        eng.close()
+
+
 def test_stage_server_replays_retried_step():
     cfg = tiny("gpt2", num_layers=2)
     s1 = build_model(cfg, dtype=torch.float32, first=1, last=2, seed=1)
