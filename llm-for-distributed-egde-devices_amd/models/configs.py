@@ -170,6 +170,40 @@ def get_config(name: str) -> ModelConfig:
     raise KeyError(f"unknown model '{name}'; presets: {sorted(PRESETS)}")
 
 
+def to_hf_config(cfg: ModelConfig) -> dict:
+    """ModelConfig -> a Hugging Face ``config.json`` dict (inverse of ``from_hf_config``)."""
+    common = dict(vocab_size=cfg.vocab_size, max_position_embeddings=cfg.max_position_embeddings,
+                  tie_word_embeddings=cfg.tie_word_embeddings, bos_token_id=cfg.bos_token_id,
+                  eos_token_id=cfg.eos_token_id, torch_dtype="bfloat16")
+    partial = cfg.rotary_dim / cfg.head_dim
+    if cfg.arch == "llama":
+        return dict(common, model_type="llama", architectures=["LlamaForCausalLM"], hidden_size=cfg.hidden_size,
+                    intermediate_size=cfg.intermediate_size, num_hidden_layers=cfg.num_layers,
+                    num_attention_heads=cfg.num_heads, num_key_value_heads=cfg.num_kv_heads,
+                    head_dim=cfg.head_dim, rms_norm_eps=cfg.norm_eps, rope_theta=cfg.rope_theta,
+                    rope_scaling=cfg.rope_scaling, attention_bias=cfg.qkv_bias, mlp_bias=cfg.mlp_bias,
+                    hidden_act="silu")
+    if cfg.arch == "gpt_neox":
+        return dict(common, model_type="gpt_neox", architectures=["GPTNeoXForCausalLM"],
+                    hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+                    num_hidden_layers=cfg.num_layers, num_attention_heads=cfg.num_heads,
+                    layer_norm_eps=cfg.norm_eps, rotary_pct=partial, rotary_emb_base=cfg.rope_theta,
+                    use_parallel_residual=cfg.parallel_residual,
+                    hidden_act="gelu" if cfg.act == "gelu" else "gelu_new", attention_bias=cfg.qkv_bias)
+    if cfg.arch == "phi":
+        return dict(common, model_type="phi", architectures=["PhiForCausalLM"], hidden_size=cfg.hidden_size,
+                    intermediate_size=cfg.intermediate_size, num_hidden_layers=cfg.num_layers,
+                    num_attention_heads=cfg.num_heads, num_key_value_heads=cfg.num_kv_heads,
+                    layer_norm_eps=cfg.norm_eps, partial_rotary_factor=partial, rope_theta=cfg.rope_theta,
+                    hidden_act="gelu_new")
+    if cfg.arch == "gpt2":
+        return dict(common, model_type="gpt2", architectures=["GPT2LMHeadModel"], n_embd=cfg.hidden_size,
+                    n_layer=cfg.num_layers, n_head=cfg.num_heads, n_inner=cfg.intermediate_size,
+                    n_positions=cfg.max_position_embeddings, layer_norm_epsilon=cfg.norm_eps,
+                    activation_function="gelu_new")
+    raise ValueError(f"no HF config mapping for {cfg.arch}")
+
+
 def from_hf_dir(path: str) -> ModelConfig:
     with open(os.path.join(path, "config.json")) as f:
         return from_hf_config(json.load(f))

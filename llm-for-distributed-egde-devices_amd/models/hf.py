@@ -169,6 +169,104 @@ def from_hf_module(hf_model, cfg: Optional[ModelConfig] = None, dtype=torch.bflo
     return load_into(model, convert_hf_tensors(cfg, iter(hf_model.state_dict().items())))
 
 
+def export_hf_tensors(model: DecoderLM) -> Dict[str, torch.Tensor]:
+    """edgellm parameters -> HF names/layouts (inverse of ``convert_hf_tensors``; full model only)."""
+    from .decoder import global_named_parameters
+    cfg = model.cfg
+    assert model.first == 0 and model.last == cfg.num_layers, "export needs the whole model"
+    p = {k: v.detach() for k, v in global_named_parameters(model)}
+    hq, hk, d = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
+    qs, ks = hq * d, hk * d
+    out: Dict[str, torch.Tensor] = {}
+    arch = cfg.arch
+    top = {"llama": ("model.embed_tokens.weight", "model.norm", "lm_head"),
+           "phi": ("model.embed_tokens.weight", "model.final_layernorm", "lm_head"),
+           "gpt_neox": ("gpt_neox.embed_in.weight", "gpt_neox.final_layer_norm", "embed_out"),
+           "gpt2": ("transformer.wte.weight", "transformer.ln_f", None)}[arch]
+    out[top[0]] = p["embed"]
+    for w in ("weight", "bias"):
+        if f"final_norm.{w}" in p:
+            out[f"{top[1]}.{w}"] = p[f"final_norm.{w}"]
+    if top[2] and not cfg.tie_word_embeddings:
+        for w in ("weight", "bias"):
+            if f"lm_head.{w}" in p:
+                out[f"{top[2]}.{w}"] = p[f"lm_head.{w}"]
+    if arch == "gpt2":
+        out["transformer.wpe.weight"] = p["pos_embed"]
+    for i in range(cfg.num_layers):
+        s = f"layers.{i}."
+        g = lambda n: p.get(s + n)  # noqa: E731
+        if arch in ("llama", "phi"):
+            h = f"model.layers.{i}."
+            for w in ("weight", "bias"):
+                qkv = g(f"attn.qkv.{w}")
+                if qkv is not None:
+                    out[h + f"self_attn.q_proj.{w}"], out[h + f"self_attn.k_proj.{w}"], \
+                        out[h + f"self_attn.v_proj.{w}"] = qkv[:qs], qkv[qs:qs + ks], qkv[qs + ks:]
+                if g(f"norm1.{w}") is not None:
+                    out[h + f"input_layernorm.{w}"] = g(f"norm1.{w}")
+            if arch == "llama":
+                out[h + "post_attention_layernorm.weight"] = g("norm2.weight")
+                out[h + "self_attn.o_proj.weight"] = g("attn.o.weight")
+                up = g("mlp.up.weight")
+                out[h + "mlp.gate_proj.weight"], out[h + "mlp.up_proj.weight"] = up[:cfg.intermediate_size], \
+                    up[cfg.intermediate_size:]
+                out[h + "mlp.down_proj.weight"] = g("mlp.down.weight")
+            else:
+                for w in ("weight", "bias"):
+                    out[h + f"self_attn.dense.{w}"] = g(f"attn.o.{w}")
+                    out[h + f"mlp.fc1.{w}"] = g(f"mlp.up.{w}")
+                    out[h + f"mlp.fc2.{w}"] = g(f"mlp.down.{w}")
+        elif arch == "gpt_neox":
+            h = f"gpt_neox.layers.{i}."
+            for w in ("weight", "bias"):
+                out[h + f"input_layernorm.{w}"] = g(f"norm1.{w}")
+                out[h + f"post_attention_layernorm.{w}"] = g(f"norm2.{w}")
+                qkv = g(f"attn.qkv.{w}")
+                out[h + f"attention.query_key_value.{w}"] = \
+                    qkv.reshape(3, hq, d, *qkv.shape[1:]).transpose(0, 1).reshape(qkv.shape).contiguous()
+                out[h + f"attention.dense.{w}"] = g(f"attn.o.{w}")
+                out[h + f"mlp.dense_h_to_4h.{w}"] = g(f"mlp.up.{w}")
+                out[h + f"mlp.dense_4h_to_h.{w}"] = g(f"mlp.down.{w}")
+        elif arch == "gpt2":
+            h = f"transformer.h.{i}."
+            for w in ("weight", "bias"):
+                out[h + f"ln_1.{w}"] = g(f"norm1.{w}")
+                out[h + f"ln_2.{w}"] = g(f"norm2.{w}")
+            for ours, theirs in (("attn.qkv", "attn.c_attn"), ("attn.o", "attn.c_proj"), ("mlp.up", "mlp.c_fc"),
+                                 ("mlp.down", "mlp.c_proj")):
+                out[h + f"{theirs}.weight"] = g(f"{ours}.weight").t()
+                out[h + f"{theirs}.bias"] = g(f"{ours}.bias")
+    return {k: v.contiguous() for k, v in out.items()}
+
+
+def save_hf_model(model: DecoderLM, path: str, shard_bytes: int = 4 << 30) -> str:
+    """Write ``config.json`` + safetensors shards readable by both edgellm and transformers."""
+    from safetensors.torch import save_file
+    from .configs import to_hf_config
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, "config.json"), "w") as f:
+        json.dump(to_hf_config(model.cfg), f, indent=2)
+    tensors = export_hf_tensors(model)
+    shards, cur, size = [], {}, 0
+    for k, v in tensors.items():
+        if cur and size + v.numel() * v.element_size() > shard_bytes:
+            shards.append(cur)
+            cur, size = {}, 0
+        cur[k] = v.cpu()
+        size += v.numel() * v.element_size()
+    shards.append(cur)
+    index = {}
+    for n, sh in enumerate(shards):
+        fn = "model.safetensors" if len(shards) == 1 else f"model-{n + 1:05d}-of-{len(shards):05d}.safetensors"
+        save_file(sh, os.path.join(path, fn), metadata={"format": "pt"})
+        index.update({k: fn for k in sh})
+    if len(shards) > 1:
+        with open(os.path.join(path, "model.safetensors.index.json"), "w") as f:
+            json.dump({"metadata": {}, "weight_map": index}, f)
+    return path
+
+
 def resolve_model_dir(name_or_path: str, base_dir: Optional[str] = None) -> Optional[str]:
     """Find a checkpoint directory the way the reference's scripts/downloader lay them out:
     a direct path, ``base_dir/<name>`` (Llama_bf16_updated.py:165-167) or

@@ -33,6 +33,7 @@ int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, fl
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, void* workspace, hipStream_t st);
 size_t edge_sample_workspace(int B, int V);
+int edge_sample_timestamps(int enable, unsigned long long* host_out16);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
@@ -285,6 +286,12 @@ at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& see
   return out;
 }
 
+std::vector<int64_t> sample_timestamps(bool enable) {
+  std::vector<unsigned long long> ts(16, 0);
+  check(edge_sample_timestamps(enable ? 1 : 0, ts.data()), "sample_timestamps");
+  return std::vector<int64_t>(ts.begin(), ts.end());
+}
+
 // ---------------------------------------------------------------------------------- offload
 // dst/src: [B, c, L, D] views of head-major caches (last two dims contiguous), any mix of pinned
 // host and device memory; async on the current stream.
@@ -319,6 +326,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("prefill_attn", &prefill_attn);
   m.def("w8a8_gemm", &w8a8_gemm);
   m.def("sample", &sample);
+  m.def("sample_timestamps", &sample_timestamps);
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);

@@ -10,30 +10,62 @@
 //
 // Split-row design: a decode batch has only B rows (16..64), so one workgroup per row leaves
 // >90% of the 256 CUs idle and serialises ~V/256 elements per thread.  Phase 1 cuts every row
-// into CH-element chunks (grid C x B, 4 elements per thread in registers):
+// into 2048/4096-score chunks (grid C x B, 8/16 scores per thread in registers):
 //   * greedy / full-vocab sampling: per-chunk argmax of the (noised) processed scores;
-//   * top-k: the chunk's exact top-k set (all scores >= the chunk's k-th value, ties kept up
-//     to CCAP) by bisection on order-preserving u32 keys; counts are wave ballots + one LDS
-//     word per wave (parity double-buffered: one barrier per bisection step).
-// The union of chunk top-k sets contains the row's top-k, and the row's k-th value is >= the
-// largest chunk threshold T0, so phase 2 (one WG per row) keeps only candidates >= T0, bisects
-// once more down to <= FCAP, ranks each survivor against the others in LDS (exact k-th cut,
-// descending softmax prefix for top-p) and takes the Gumbel-max winner.
+//   * top-k: a superset of the chunk's top-k (every score >= a threshold t_c with
+//     k <= count <= CCAP).  Thresholds are searched on order-preserving u32 keys, probing at the
+//     VALUE midpoint first (logit-like distributions land in the [k, CCAP] window in 2-4 probes)
+//     and at the key midpoint once that stalls, so the search always terminates.  Counts are
+//     wave ballots + one LDS word per wave (parity double-buffered: one barrier per probe).
+// Candidates travel as one 64-bit composite (key<<32 | ~index: orders by value, then lower index;
+// unused slots 0), so the merge pays a single cross-XCD memory round trip.  The row's k-th value
+// is >= T0 = max_c t_c, so phase 2 (one WG per row) gathers only the candidates >= T0 (if they
+// would overflow LDS it first searches the chunk lists in global memory), narrows them to
+// <= FCAP, and ranks every survivor against the others with one 64-bit LDS read per comparison —
+// giving the exact k-th cut, the descending softmax prefix for top-p, and the Gumbel-max winner.
 // The step counter is read from device memory (rng[1]) so both launches live in a HIP graph.
 #include "common.h"
 
 namespace {
 constexpr int NT = 256, NW = NT / 64;
-constexpr int CH = 1024;      // phase-1 chunk (EPT = 4 scores per thread)
-constexpr int EPT = CH / NT;
+// Phase-1 chunk = NT * EPT scores (EPT 8 for V <= 64K, else 16).  Chunk candidate sets are
+// ~k/chunk of the row; bigger chunks keep the phase-2 survivor count (~k * V / chunk) in MCAP.
+__host__ __device__ constexpr int chunk_ept(int V) { return V <= 65536 ? 8 : 16; }
 constexpr int CCAP = 128;     // candidates kept per chunk; the split path needs top_k <= CCAP
-constexpr int MCAP = 2048;    // phase-2 candidates >= T0 (ties beyond are truncated)
-constexpr int FCAP = 256;     // candidates ranked exactly
+constexpr int CCAP_LOG2 = 7;
+constexpr int MCAP = 2048;    // phase-2 candidates >= T0
+constexpr int FCAP = 256;     // candidates ranked exactly (ties beyond the caps are truncated)
 constexpr int CAP = 1024;     // single-workgroup fallback for CCAP < top_k <= CAP
 
+// Phase timestamps of row 0's merge workgroup (wall_clock64 ticks), recorded when g_ts_on.
+__device__ unsigned long long g_ts[16];
+__device__ int g_ts_on;
+#define TS(i) do { if (g_ts_on && blockIdx.x == 0 && threadIdx.x == 0) g_ts[i] = wall_clock64(); } while (0)
+#define TS1(i) do { if (g_ts_on && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_ts[i] = wall_clock64(); } while (0)
+
 __device__ __forceinline__ uint32_t f2key(float f) {
-  uint32_t u = __float_as_uint(f);
+  const uint32_t u = __float_as_uint(f + 0.0f);       // -0 -> +0 so equal scores tie
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+// Composite rank key: larger = better (higher score, then lower token id).
+__device__ __forceinline__ uint64_t ckey(float v, int i) { return ((uint64_t)f2key(v) << 32) | (uint32_t)(~i); }
+__device__ __forceinline__ float cval(uint64_t c) { return key2f((uint32_t)(c >> 32)); }
+__device__ __forceinline__ int cidx(uint64_t c) { return (int)(~(uint32_t)c); }
+
+// Next probe in (lo, hi]: the value midpoint while it is finite and strictly inside, else the
+// key midpoint.
+__device__ __forceinline__ uint32_t probe(uint32_t lo, uint32_t hi, int it) {
+  if (it < 12) {
+    const float a = key2f(lo), b = key2f(hi);
+    if (isfinite(a) && isfinite(b)) {
+      const uint32_t m = f2key(0.5f * a + 0.5f * b);
+      if (m > lo && m <= hi) return m;
+    }
+  }
+  return lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
 }
 
 template <bool BF16>
@@ -69,24 +101,36 @@ __device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int*
     if (better(rv[i], ri[i], v, idx)) { v = rv[i]; idx = ri[i]; }
 }
 
-// OP 0 = min, 1 = max, 2 = sum over the block; `scratch` holds >= NW words.
-template <int OP>
-__device__ __forceinline__ uint32_t block_reduce_u32(uint32_t v, uint32_t* scratch) {
+// Block-wide (min, max) of u32 keys; `scratch` holds >= 2*NW words.
+__device__ __forceinline__ void block_minmax_u32(uint32_t& mn, uint32_t& mx, uint32_t* scratch) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
-    v = OP == 0 ? min(v, w) : (OP == 1 ? max(v, w) : v + w);
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
   }
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
   __syncthreads();
-  if (l == 0) scratch[wv] = v;
+  if ((threadIdx.x & 63) == 0) { scratch[w] = mn; scratch[NW + w] = mx; }
   __syncthreads();
-  uint32_t r = scratch[0];
 #pragma unroll
-  for (int i = 1; i < NW; ++i) {
-    const uint32_t w = scratch[i];
-    r = OP == 0 ? min(r, w) : (OP == 1 ? max(r, w) : r + w);
-  }
+  for (int i = 0; i < NW; ++i) { mn = min(mn, scratch[i]); mx = max(mx, scratch[NW + i]); }
+}
+
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t* scratch) {
+  uint32_t dummy = 0xffffffffu;
+  block_minmax_u32(dummy, v, scratch);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += scratch[i];
   return r;
 }
 
@@ -108,82 +152,108 @@ __device__ __forceinline__ float gumbel(uint32_t seed, uint32_t row, uint32_t st
   return -logf(-logf(u));
 }
 
-// Exact top-k (ties at the k-th value kept) -> top-p -> Gumbel-max over n <= PER*NT candidates
-// held in LDS.  Every thread ranks its candidates against all others (broadcast LDS reads, no
-// sort stages).  Result in (bv, bi) on every thread.
+// Wave-aggregated slot allocation: one LDS atomic per wave instead of one per lane (all lanes of
+// a wave hitting one counter serialise).  Returns this lane's slot; meaningful only if `pred`.
+__device__ __forceinline__ int wave_alloc(bool pred, int* counter) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return -1;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Exact top-k (ties at the k-th value kept) -> top-p -> Gumbel-max over the n <= PER*NT
+// composite keys in `fc` (LDS, zero-padded to a multiple of 8).  `fe` is LDS scratch of the same
+// length.  One pass gives each candidate its rank and the softmax mass of the strictly better
+// candidates (those all sit at or above the k-th value, so no k-th cut is needed in the pass);
+// the reads are unrolled x8 so the broadcast LDS loads overlap.  Result on every thread.
 template <int PER>
-__device__ __forceinline__ void rank_and_sample(const float* cv, const int* ci, int n, int top_k, float top_p,
-                                                uint32_t seed, uint32_t row, uint32_t step, float* kth_s,
-                                                float* tot_s, float* rv, int* ri, float& bv, int& bi) {
+__device__ __forceinline__ void rank_and_sample(const uint64_t* fc, float* fe, int n, int top_k, float top_p,
+                                                uint32_t seed, uint32_t row, uint32_t step, float* sh,
+                                                uint32_t* red, float* rv, int* ri, float& bv, int& bi) {
+  // sh: [0] k-th value, [1..1+NW) partial sums
   const int tid = threadIdx.x;
-  int rank[PER];
-  float myv[PER];
-  int myi[PER];
+  uint64_t my[PER];
+  uint32_t kmax = 0u, kmin_unused = 0xffffffffu;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int c = tid + q * NT;
-    rank[q] = 0x7fffffff;
-    if (c < n) {
-      const float v = cv[c];
-      const int id = ci[c];
-      int r = 0;
-      for (int j = 0; j < n; ++j) r += better(cv[j], ci[j], v, id) ? 1 : 0;
-      rank[q] = r;
-      myv[q] = v;
-      myi[q] = id;
-    }
+    my[q] = c < n ? fc[c] : 0ull;
+    kmax = max(kmax, (uint32_t)(my[q] >> 32));
+  }
+  block_minmax_u32(kmin_unused, kmax, red);
+  const float vmax = key2f(kmax);
+  float e[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int c = tid + q * NT;
+    e[q] = c < n ? __expf(cval(my[q]) - vmax) : 0.f;
+    if (c < ((n + 7) & ~7)) fe[c] = e[q];
+  }
+  __syncthreads();
+  int rank[PER];
+  float excl[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) { rank[q] = 0; excl[q] = 0.f; }
+  for (int j = 0; j < n; j += 8) {
+    uint64_t f[8];
+    float g[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { f[u] = fc[j + u]; g[u] = fe[j + u]; }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < PER; ++q)
+        if (f[u] > my[q]) { rank[q] += 1; excl[q] += g[u]; }
   }
   const int kk = min(top_k, n);
 #pragma unroll
   for (int q = 0; q < PER; ++q)
-    if (rank[q] == kk - 1) *kth_s = myv[q];
-  if (tid == 0 && kk == 0) *kth_s = -INFINITY;
+    if (tid + q * NT < n && rank[q] == kk - 1) sh[0] = cval(my[q]);
   __syncthreads();
-  const float kth = *kth_s;
-  float vmax = -INFINITY;
-  for (int j = 0; j < n; ++j) vmax = fmaxf(vmax, cv[j]);
+  const float kth = sh[0];
   float tot = 0.f;
 #pragma unroll
   for (int q = 0; q < PER; ++q)
-    if (rank[q] != 0x7fffffff && myv[q] >= kth) tot += __expf(myv[q] - vmax);
+    if (tid + q * NT < n && cval(my[q]) >= kth) tot += e[q];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  if ((tid & 63) == 0) tot_s[tid >> 6] = tot;
+  if ((tid & 63) == 0) sh[1 + (tid >> 6)] = tot;
   __syncthreads();
   tot = 0.f;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) tot += tot_s[i];
+  for (int i = 0; i < NW; ++i) tot += sh[1 + i];
   bv = -INFINITY;
   bi = 0x7fffffff;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    if (rank[q] == 0x7fffffff || myv[q] < kth) continue;
-    bool keep = rank[q] == 0 || top_p >= 1.f;
-    if (!keep) {
-      float excl = 0.f;
-      const float v = myv[q];
-      const int id = myi[q];
-      for (int j = 0; j < n; ++j) {
-        const float w = cv[j];
-        if (w >= kth && better(w, ci[j], v, id)) excl += __expf(w - vmax);
-      }
-      keep = excl / tot < top_p;
-    }
-    if (keep) {
-      const float g = myv[q] + gumbel(seed, row, step, myi[q]);
-      if (better(g, myi[q], bv, bi)) { bv = g; bi = myi[q]; }
+    const float v = cval(my[q]);
+    if (tid + q * NT >= n || v < kth) continue;
+    if (rank[q] == 0 || top_p >= 1.f || excl[q] / tot < top_p) {
+      const int id = cidx(my[q]);
+      const float g = v + gumbel(seed, row, step, id);
+      if (better(g, id, bv, bi)) { bv = g; bi = id; }
     }
   }
   block_argmax(bv, bi, rv, ri);
 }
 
+// Zero-pad fc[n .. round_up(n, 8)) (0 ranks below every real candidate).
+__device__ __forceinline__ void pad8(uint64_t* fc, int n) {
+  const int t = n + (int)threadIdx.x;
+  if (t < ((n + 7) & ~7)) fc[t] = 0ull;
+}
+
 // ---------------------------------------------------------------- phase 1
-// Per-chunk argmax of the processed (MODE 1: + Gumbel noise) scores -> pv/pi[row*C + c].
-template <bool BF16, int MODE>
+// Per-chunk best composite (value, then lower id) of the processed (MODE 1: + Gumbel noise)
+// scores -> pc[row*C + c].
+template <bool BF16, int MODE, int EPT>
 __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict__ logits,
                                                           const uint8_t* __restrict__ seen, int V, int C, float inv_t,
                                                           float pen, const int* __restrict__ rng,
-                                                          float* __restrict__ pv, int* __restrict__ pi) {
+                                                          uint64_t* __restrict__ pc) {
   __shared__ float rv[NW];
   __shared__ int ri[NW];
   const int c = blockIdx.x, row = blockIdx.y;
@@ -193,7 +263,7 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
   int bi = 0x7fffffff;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int i = c * CH + j * NT + threadIdx.x;
+    const int i = c * (NT * EPT) + j * NT + threadIdx.x;
     if (i < V) {
       float s = proc<BF16>(logits, seen, base, i, inv_t, pen);
       if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
@@ -201,26 +271,24 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
     }
   }
   block_argmax(bv, bi, rv, ri);
-  if (threadIdx.x == 0) {
-    pv[(size_t)row * C + c] = bv;
-    pi[(size_t)row * C + c] = bi;
-  }
+  if (threadIdx.x == 0) pc[(size_t)row * C + c] = ckey(bv, bi);
 }
 
-// Per-chunk exact top-k set -> pv/pi[(row*C + c)*CCAP + s], pn = kept count, pthr = key threshold.
-template <bool BF16>
+// Per-chunk candidate superset -> pc[(row*C + c)*CCAP + s] as composite keys (unused slots 0),
+// pthr[row*C + c] = threshold key.
+template <bool BF16, int EPT>
 __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__ logits,
                                                         const uint8_t* __restrict__ seen, int V, int C, float inv_t,
-                                                        float pen, int top_k, float* __restrict__ pv,
-                                                        int* __restrict__ pi, uint32_t* __restrict__ pthr,
-                                                        int* __restrict__ pn) {
-  __shared__ uint32_t red[NW];
+                                                        float pen, int top_k, uint64_t* __restrict__ pc,
+                                                        uint32_t* __restrict__ pthr) {
+  __shared__ uint32_t red[2 * NW];
   __shared__ int scr[2 * NW];
   __shared__ int cnt;
   const int c = blockIdx.x, row = blockIdx.y, tid = threadIdx.x;
   const size_t base = (size_t)row * V;
-  const int c0 = c * CH;
-  const int nvalid = min(CH, V - c0);
+  const int c0 = c * (NT * EPT);
+  const int nvalid = min(NT * EPT, V - c0);
+  TS1(10);
   float sv[EPT];
   uint32_t kr[EPT];
   uint32_t kmin = 0xffffffffu, kmax = 0u;
@@ -231,18 +299,19 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
     kr[j] = o < nvalid ? f2key(sv[j]) : 0u;
     if (o < nvalid) { kmin = min(kmin, kr[j]); kmax = max(kmax, kr[j]); }
   }
-  uint32_t thr = 0u;                       // chunk no larger than k: keep everything
+  if (tid == 0) cnt = 0;
+  uint32_t thr = 1u;                       // chunk no larger than k: keep every valid score
   if (nvalid > top_k) {
-    kmin = block_reduce_u32<0>(kmin, red);
-    kmax = block_reduce_u32<1>(kmax, red);
-    // invariant: count(key >= lo) >= top_k
-    uint32_t lo = kmin, hi = kmax;
+    block_minmax_u32(kmin, kmax, red);
+    TS1(11);
+    uint32_t lo = kmin, hi = kmax;         // invariant: count(key >= lo) >= top_k
     int parity = 0;
-    for (int it = 0; it < 34 && lo < hi; ++it) {
-      const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+    int it = 0;
+    for (; it < 48 && lo < hi; ++it) {
+      const uint32_t mid = probe(lo, hi, it);
       int wc = 0;
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) wc += ballot_count(j * NT + tid < nvalid && kr[j] >= mid);
+      for (int j = 0; j < EPT; ++j) wc += ballot_count(kr[j] >= mid);   // invalid keys are 0 < mid
       const int n = block_count(wc, scr, parity);
       if (n >= top_k) {
         lo = mid;
@@ -251,122 +320,173 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
         hi = mid - 1;
       }
     }
-    thr = lo;
+    thr = max(lo, 1u);
+    if (g_ts_on && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) g_ts[14] = it;
   }
-  if (tid == 0) cnt = 0;
+  TS1(12);
   __syncthreads();
   const size_t slot0 = ((size_t)row * C + c) * CCAP;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int o = j * NT + tid;
-    if (o < nvalid && kr[j] >= thr) {
-      const int s = atomicAdd(&cnt, 1);
-      if (s < CCAP) { pv[slot0 + s] = sv[j]; pi[slot0 + s] = c0 + o; }
-    }
+    const bool ok = o < nvalid && kr[j] >= thr;
+    const int s = wave_alloc(ok, &cnt);
+    if (ok && s < CCAP) pc[slot0 + s] = ckey(sv[j], c0 + o);
   }
   __syncthreads();
-  if (tid == 0) {
-    pn[(size_t)row * C + c] = min(cnt, CCAP);
-    pthr[(size_t)row * C + c] = thr;
-  }
+  for (int s = min(cnt, CCAP) + tid; s < CCAP; s += NT) pc[slot0 + s] = 0ull;
+  if (tid == 0) pthr[(size_t)row * C + c] = thr;
+  TS1(13);
 }
 
 // ---------------------------------------------------------------- phase 2
-__global__ void __launch_bounds__(64) argmax_merge_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
-                                                          int C, int V, uint8_t* __restrict__ seen,
-                                                          int64_t* __restrict__ out_tok) {
+__global__ void __launch_bounds__(64) argmax_merge_kernel(const uint64_t* __restrict__ pc, int C, int V,
+                                                          uint8_t* __restrict__ seen, int64_t* __restrict__ out_tok) {
   const int row = blockIdx.x;
-  float bv = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int c = threadIdx.x; c < C; c += 64) {
-    const float v = pv[(size_t)row * C + c];
-    const int i = pi[(size_t)row * C + c];
-    if (better(v, i, bv, bi)) { bv = v; bi = i; }
+  uint64_t best = 0ull;
+  for (int c = threadIdx.x; c < C; c += 64) best = max(best, pc[(size_t)row * C + c]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(best >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl_xor((int)(uint32_t)best, o, 64);
+    best = max(best, other);
   }
-  wave_argmax(bv, bi);
   if (threadIdx.x == 0) {
+    const int bi = cidx(best);
     out_tok[row] = bi;
     if (seen != nullptr) seen[(size_t)row * V + bi] = 1;
   }
 }
 
-__global__ void __launch_bounds__(NT) topk_merge_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
-                                                        const uint32_t* __restrict__ pthr, const int* __restrict__ pn,
-                                                        int C, int V, int top_k, float top_p,
-                                                        const int* __restrict__ rng, uint8_t* __restrict__ seen,
-                                                        int64_t* __restrict__ out_tok) {
-  __shared__ float cv[MCAP];
-  __shared__ int ci[MCAP];
-  __shared__ float fv[FCAP];
-  __shared__ int fi[FCAP];
-  __shared__ uint32_t red[NW];
+constexpr int G = 16;                      // candidate slots per thread per gather round
+
+// Append the composites of one gather round with key >= thr to cv (LDS); count in *ncand.
+__device__ __forceinline__ void collect(const uint64_t (&v)[G], uint32_t thr, uint64_t* cv, int* ncand) {
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const bool ok = (uint32_t)(v[u] >> 32) >= thr;
+    const int slot = wave_alloc(ok, ncand);
+    if (ok && slot < MCAP) cv[slot] = v[u];
+  }
+}
+
+__device__ __forceinline__ void load_round(const uint64_t* pc, size_t s0, int nslots, int r0, uint64_t (&v)[G]) {
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const int sidx = r0 + u * NT + (int)threadIdx.x;
+    v[u] = sidx < nslots ? pc[s0 + sidx] : 0ull;
+  }
+}
+
+__global__ void __launch_bounds__(NT) topk_merge_kernel(const uint64_t* __restrict__ pc,
+                                                        const uint32_t* __restrict__ pthr, int C, int V, int top_k,
+                                                        float top_p, const int* __restrict__ rng,
+                                                        uint8_t* __restrict__ seen, int64_t* __restrict__ out_tok) {
+  __shared__ uint64_t cv[MCAP];
+  __shared__ uint64_t fc[FCAP];
+  __shared__ float fe[FCAP];
+  __shared__ uint32_t red[2 * NW];
   __shared__ int scr[2 * NW];
   __shared__ int ncand, nfin;
-  __shared__ float kth_s, tot_s[NW], rv[NW];
+  __shared__ float sh[1 + NW], rv[NW];
   __shared__ int ri[NW];
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  TS(0);
   const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
+  const int nslots = C * CCAP;
+  const size_t s0 = (size_t)row * nslots;
+  // The lists were written by other XCDs, so every load misses L2: issue the thresholds and the
+  // first round of candidates together (one memory round trip), then filter.
   uint32_t t0 = 0u;
   for (int c = tid; c < C; c += NT) t0 = max(t0, pthr[(size_t)row * C + c]);
-  t0 = block_reduce_u32<1>(t0, red);
+  uint64_t v[G];
+  load_round(pc, s0, nslots, 0, v);
   if (tid == 0) { ncand = 0; nfin = 0; }
-  __syncthreads();
-  for (int c = w; c < C; c += NW) {                     // one wave per chunk, lanes over its slots
-    const int nc = pn[(size_t)row * C + c];
-    const size_t s0 = ((size_t)row * C + c) * CCAP;
-    for (int s = lane; s < nc; s += 64) {
-      const float v = pv[s0 + s];
-      if (f2key(v) >= t0) {
-        const int slot = atomicAdd(&ncand, 1);
-        if (slot < MCAP) { cv[slot] = v; ci[slot] = pi[s0 + s]; }
-      }
-    }
+  t0 = block_max_u32(t0, red);
+  TS(1);
+  collect(v, t0, cv, &ncand);
+  for (int r0 = G * NT; r0 < nslots; r0 += G * NT) {
+    load_round(pc, s0, nslots, r0, v);
+    collect(v, t0, cv, &ncand);
   }
   __syncthreads();
-  const int n = min(ncand, MCAP);
+  int total = ncand;
+  TS(2);
+  if (g_ts_on && blockIdx.x == 0 && tid == 0) g_ts[8] = total;
+  if (total > MCAP) {
+    // Rare: too many survivors for LDS.  Search the chunk lists in global memory for a
+    // threshold leaving top_k..MCAP candidates, then gather again.
+    uint32_t lo = t0, hi = 0xffffffffu;
+    for (int it = 0; it < 48 && lo < hi; ++it) {
+      const uint32_t mid = probe(lo, hi, it);
+      uint32_t cntm = 0;
+      for (int sidx = tid; sidx < nslots; sidx += NT) cntm += (uint32_t)(pc[s0 + sidx] >> 32) >= mid ? 1u : 0u;
+      cntm = block_sum_u32(cntm, red);
+      if ((int)cntm >= top_k) {
+        lo = mid;
+        if ((int)cntm <= MCAP) break;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) ncand = 0;
+    __syncthreads();
+    for (int r0 = 0; r0 < nslots; r0 += G * NT) {
+      load_round(pc, s0, nslots, r0, v);
+      collect(v, lo, cv, &ncand);
+    }
+    __syncthreads();
+    total = ncand;
+  }
+  const int n = min(total, MCAP);
   constexpr int PM = MCAP / NT;
   uint32_t thr = 0u;
-  if (n > FCAP) {                                        // bisect the survivors down to <= CCAP
+  if (n > FCAP) {                                        // narrow the survivors to <= FCAP
     uint32_t kmin = 0xffffffffu, kmax = 0u;
+    uint32_t kr[PM];
 #pragma unroll
     for (int q = 0; q < PM; ++q) {
       const int j = tid + q * NT;
-      if (j < n) { const uint32_t k = f2key(cv[j]); kmin = min(kmin, k); kmax = max(kmax, k); }
+      kr[q] = j < n ? (uint32_t)(cv[j] >> 32) : 0u;
+      if (j < n) { kmin = min(kmin, kr[q]); kmax = max(kmax, kr[q]); }
     }
-    kmin = block_reduce_u32<0>(kmin, red);
-    kmax = block_reduce_u32<1>(kmax, red);
+    block_minmax_u32(kmin, kmax, red);
     uint32_t lo = kmin, hi = kmax;
     int parity = 0;
-    for (int it = 0; it < 34 && lo < hi; ++it) {
-      const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+    for (int it = 0; it < 48 && lo < hi; ++it) {
+      const uint32_t mid = probe(lo, hi, it);
       int wc = 0;
 #pragma unroll
-      for (int q = 0; q < PM; ++q) {
-        const int j = tid + q * NT;
-        wc += ballot_count(j < n && f2key(cv[j]) >= mid);
-      }
+      for (int q = 0; q < PM; ++q) wc += ballot_count(kr[q] >= mid);
       const int cn = block_count(wc, scr, parity);
       if (cn >= top_k) {
         lo = mid;
-        if (cn <= CCAP) break;
+        if (cn <= FCAP) break;
       } else {
         hi = mid - 1;
       }
     }
     thr = lo;
   }
+  TS(3);
 #pragma unroll
   for (int q = 0; q < PM; ++q) {
     const int j = tid + q * NT;
-    if (j < n && f2key(cv[j]) >= thr) {
-      const int slot = atomicAdd(&nfin, 1);
-      if (slot < FCAP) { fv[slot] = cv[j]; fi[slot] = ci[j]; }
-    }
+    const uint64_t x = j < n ? cv[j] : 0ull;
+    const bool ok = j < n && (uint32_t)(x >> 32) >= thr;
+    const int slot = wave_alloc(ok, &nfin);
+    if (ok && slot < FCAP) fc[slot] = x;
   }
   __syncthreads();
+  const int nf = min(nfin, FCAP);
+  pad8(fc, nf);
+  TS(4);
+  if (g_ts_on && blockIdx.x == 0 && tid == 0) g_ts[9] = nfin;
   float bv;
   int bi;
-  rank_and_sample<FCAP / NT>(fv, fi, min(nfin, FCAP), top_k, top_p, seed, row, step, &kth_s, tot_s, rv, ri, bv, bi);
+  rank_and_sample<FCAP / NT>(fc, fe, nf, top_k, top_p, seed, row, step, sh, red, rv, ri, bv, bi);
+  TS(5);
   if (tid == 0) {
     out_tok[row] = bi;
     if (seen != nullptr) seen[(size_t)row * V + bi] = 1;
@@ -378,11 +498,11 @@ template <bool BF16>
 __global__ void __launch_bounds__(NT) topk_row_kernel(const void* __restrict__ logits, uint8_t* __restrict__ seen,
                                                       int V, float inv_t, float pen, int top_k, float top_p,
                                                       const int* __restrict__ rng, int64_t* __restrict__ out_tok) {
-  __shared__ uint32_t red[NW];
-  __shared__ float cv[CAP];
-  __shared__ int ci[CAP];
+  __shared__ uint32_t red[2 * NW];
+  __shared__ uint64_t fc[CAP];
+  __shared__ float fe[CAP];
   __shared__ int ncand;
-  __shared__ float kth_s, tot_s[NW], rv[NW];
+  __shared__ float sh[1 + NW], rv[NW];
   __shared__ int ri[NW];
   const int row = blockIdx.x, tid = threadIdx.x;
   const size_t base = (size_t)row * V;
@@ -393,14 +513,14 @@ __global__ void __launch_bounds__(NT) topk_row_kernel(const void* __restrict__ l
     kmin = min(kmin, k);
     kmax = max(kmax, k);
   }
-  kmin = block_reduce_u32<0>(kmin, red);
-  kmax = block_reduce_u32<1>(kmax, red);
+  if (tid == 0) ncand = 0;
+  block_minmax_u32(kmin, kmax, red);
   uint32_t lo = kmin, hi = kmax;
-  for (int it = 0; it < 34 && lo < hi; ++it) {
-    const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+  for (int it = 0; it < 48 && lo < hi; ++it) {
+    const uint32_t mid = probe(lo, hi, it);
     uint32_t c = 0;
     for (int i = tid; i < V; i += NT) c += f2key(proc<BF16>(logits, seen, base, i, inv_t, pen)) >= mid;
-    c = block_reduce_u32<2>(c, red);
+    c = block_sum_u32(c, red);
     if ((int)c >= top_k) {
       lo = mid;
       if ((int)c <= CAP) break;
@@ -408,19 +528,18 @@ __global__ void __launch_bounds__(NT) topk_row_kernel(const void* __restrict__ l
       hi = mid - 1;
     }
   }
-  if (tid == 0) ncand = 0;
-  __syncthreads();
   for (int i = tid; i < V; i += NT) {
     const float s = proc<BF16>(logits, seen, base, i, inv_t, pen);
-    if (f2key(s) >= lo) {
-      const int slot = atomicAdd(&ncand, 1);
-      if (slot < CAP) { cv[slot] = s; ci[slot] = i; }
-    }
+    const bool ok = f2key(s) >= lo;
+    const int slot = wave_alloc(ok, &ncand);          // divergent tail: inactive lanes are not in the ballot
+    if (ok && slot < CAP) fc[slot] = ckey(s, i);
   }
   __syncthreads();
+  const int nf = min(ncand, CAP);
+  pad8(fc, nf);
   float bv;
   int bi;
-  rank_and_sample<CAP / NT>(cv, ci, min(ncand, CAP), top_k, top_p, seed, row, step, &kth_s, tot_s, rv, ri, bv, bi);
+  rank_and_sample<CAP / NT>(fc, fe, nf, top_k, top_p, seed, row, step, sh, red, rv, ri, bv, bi);
   if (tid == 0) {
     out_tok[row] = bi;
     if (seen != nullptr) seen[base + bi] = 1;
@@ -428,10 +547,19 @@ __global__ void __launch_bounds__(NT) topk_row_kernel(const void* __restrict__ l
 }
 }  // namespace
 
+// Debug: enable/read the merge-phase timestamps (ticks of the 100 MHz wall clock).
+extern "C" int edge_sample_timestamps(int enable, unsigned long long* host_out16) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_ts_on), &enable, sizeof(int)) != hipSuccess) return -1;
+  if (host_out16 != nullptr && hipMemcpyFromSymbol(host_out16, HIP_SYMBOL(g_ts), 16 * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  return 0;
+}
+
 // Device workspace (bytes) the split sampler needs for B rows of V scores.
 extern "C" size_t edge_sample_workspace(int B, int V) {
-  const size_t C = (size_t)(V + CH - 1) / CH;
-  return (size_t)B * C * (CCAP * (sizeof(float) + sizeof(int)) + sizeof(uint32_t) + sizeof(int));
+  const int ch = NT * chunk_ept(V);
+  const size_t C = (size_t)(V + ch - 1) / ch;
+  return (size_t)B * C * (CCAP * sizeof(uint64_t) + sizeof(uint32_t));
 }
 
 // mode: 0 greedy, 1 full-vocab sampling, 2 top-k(+top-p). Returns -5 when the configuration
@@ -446,12 +574,10 @@ extern "C" int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B
   else if (top_k > 0 && top_k <= CAP && top_k < V) mode = 2;
   else return -5;
   const float inv_t = (mode == 0) ? 1.f : inv_temperature;  // host computes 1/T in f64 (matches _ref)
-  const int C = (V + CH - 1) / CH;
-  const size_t nslot = (size_t)B * C * CCAP;
-  float* pv = reinterpret_cast<float*>(workspace);
-  int* pi = reinterpret_cast<int*>(pv + nslot);
-  uint32_t* pthr = reinterpret_cast<uint32_t*>(pi + nslot);
-  int* pn = reinterpret_cast<int*>(pthr + (size_t)B * C);
+  const int ept = chunk_ept(V);
+  const int C = (V + NT * ept - 1) / (NT * ept);
+  uint64_t* pc = reinterpret_cast<uint64_t*>(workspace);
+  uint32_t* pthr = reinterpret_cast<uint32_t*>(pc + (size_t)B * C * CCAP);
   const dim3 g1(C, B);
   if (mode == 2 && top_k > CCAP) {
     if (is_bf16) hipLaunchKernelGGL(topk_row_kernel<true>, dim3(B), dim3(NT), 0, st, logits, seen, V, inv_t, penalty,
@@ -459,19 +585,22 @@ extern "C" int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B
     else hipLaunchKernelGGL(topk_row_kernel<false>, dim3(B), dim3(NT), 0, st, logits, seen, V, inv_t, penalty, top_k,
                             top_p, rng, out_tok);
   } else if (mode == 2) {
-    if (is_bf16) hipLaunchKernelGGL(topk_chunk_kernel<true>, g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, penalty,
-                                    top_k, pv, pi, pthr, pn);
-    else hipLaunchKernelGGL(topk_chunk_kernel<false>, g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, penalty, top_k,
-                            pv, pi, pthr, pn);
-    hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(NT), 0, st, pv, pi, pthr, pn, C, V, top_k, top_p, rng, seen,
+#define TC(BF, E) hipLaunchKernelGGL((topk_chunk_kernel<BF, E>), g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, \
+                                     penalty, top_k, pc, pthr)
+    if (is_bf16) { if (ept == 8) TC(true, 8); else TC(true, 16); }
+    else { if (ept == 8) TC(false, 8); else TC(false, 16); }
+#undef TC
+    hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(NT), 0, st, pc, pthr, C, V, top_k, top_p, rng, seen,
                        out_tok);
   } else {
-#define AC(BF, MD) hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD>), g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, \
-                                      penalty, rng, pv, pi)
+#define AC(BF, MD) do { if (ept == 8) hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 8>), g1, dim3(NT), 0, st, logits, \
+                                                        seen, V, C, inv_t, penalty, rng, pc); \
+                           else hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 16>), g1, dim3(NT), 0, st, logits, seen, \
+                                                   V, C, inv_t, penalty, rng, pc); } while (0)
     if (is_bf16) { if (mode == 0) AC(true, 0); else AC(true, 1); }
     else { if (mode == 0) AC(false, 0); else AC(false, 1); }
 #undef AC
-    hipLaunchKernelGGL(argmax_merge_kernel, dim3(B), dim3(64), 0, st, pv, pi, C, V, seen, out_tok);
+    hipLaunchKernelGGL(argmax_merge_kernel, dim3(B), dim3(64), 0, st, pc, C, V, seen, out_tok);
   }
   return (int)hipGetLastError();
 }

@@ -90,10 +90,11 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True):
     return out
 
 
-def other_rows(C, dev):
+def other_rows(C, dev, only=None):
+    want = lambda sec: only is None or sec in only  # noqa: E731
     out = []
     B, H, Hq, D = 16, 4096, 32, 128
-    for L in (256, 1024, 4096):
+    for L in ((256, 1024, 4096) if want("attn") else ()):
         S = L + 8
         q = torch.randn(B, Hq, D, device=dev).bfloat16()
         kc = torch.randn(B, Hq, S, D, device=dev).bfloat16()
@@ -107,6 +108,19 @@ def other_rows(C, dev):
                             TBps=round(nbytes / t / 1e6, 2)))
             print(out[-1], flush=True)
         C.tune("decode_attn", 0, 0)
+    if want("small"):
+        out += small_rows(C, dev, B, H, Hq, D)
+    if want("sample"):
+        out += sample_rows(C, dev)
+    if want("prefill"):
+        out += prefill_rows(C, dev, Hq, D)
+    for r in out[-12:]:
+        print(r, flush=True)
+    return out
+
+
+def small_rows(C, dev, B, H, Hq, D):
+    out = []
     x = torch.randn(B, H, device=dev).bfloat16()
     r = torch.randn(B, H, device=dev).bfloat16()
     w = torch.ones(H, device=dev).bfloat16()
@@ -119,11 +133,34 @@ def other_rows(C, dev):
     sp = torch.full((B,), 100, dtype=torch.int32, device=dev)
     rope = ops.rope_tables(D, 512, 10000.0, device=dev)
     out.append(dict(op="rope_kv_write", tokens=B, us=round(timeit(lambda: C.rope_kv_write(qkv, sp, rope, kc, vc, Hq, Hq, D, D)), 2)))
-    logits = torch.randn(B, 32000, device=dev).bfloat16()
-    seen = torch.zeros(B, 32000, dtype=torch.uint8, device=dev)
+    return out
+
+
+def sample_rows(C, dev):
+    out = []
     rng = torch.tensor([1, 0], dtype=torch.int32, device=dev)
-    out.append(dict(op="sample_topk50_topp0.9", rows=B, V=32000,
-                    us=round(timeit(lambda: C.sample(logits, seen, 0.7, 50, 0.9, 1.1, True, rng)), 2)))
+    for B, V in ((16, 32000), (64, 32000), (16, 128256)):
+        logits = (torch.randn(B, V, device=dev) * 3).bfloat16()
+        seen = (torch.rand(B, V, device=dev) < 0.005).to(torch.uint8)
+        for name, args in (("topk50_topp0.9", (0.7, 50, 0.9, 1.1, True)), ("greedy", (0.0, 0, 1.0, 1.1, False)),
+                           ("full", (1.0, 0, 1.0, 1.0, True))):
+            out.append(dict(op=f"sample_{name}", rows=B, V=V,
+                            us=round(timeit(lambda: C.sample(logits, seen, *args, rng)), 2)))
+            if name.startswith("topk"):       # merge-kernel phase split (100 MHz wall clock)
+                C.sample_timestamps(True)
+                C.sample(logits, seen, *args, rng)
+                torch.cuda.synchronize()
+                ts = C.sample_timestamps(False)
+                out[-1]["merge_phases_us"] = [round((ts[i + 1] - ts[i]) / 100.0, 2) for i in range(5)]
+                out[-1]["merge_counts"] = [ts[8], ts[9]]
+                out[-1]["chunk_phases_us"] = [round((ts[i + 1] - ts[i]) / 100.0, 2) for i in range(10, 13)]
+                out[-1]["chunk_probes"] = ts[14]
+            print(out[-1], flush=True)
+    return out
+
+
+def prefill_rows(C, dev, Hq, D):
+    out = []
     # prefill attention (MFMA)
     for T in (512, 2048):
         q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
@@ -142,8 +179,6 @@ def other_rows(C, dev):
         s1, s2 = torch.rand(M, device=dev), torch.rand(N, device=dev)
         t = timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K), iters=20)
         out.append(dict(op="w8a8_gemm_tiled", M=M, N=N, K=K, us=round(t, 2), TOPs=round(2 * M * N * K / t / 1e6, 1)))
-    for r in out[-12:]:
-        print(r, flush=True)
     return out
 
 
@@ -151,10 +186,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,attn,small,sample,prefill")
     a = ap.parse_args()
+    only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
     C = ops.ext()
-    rows = gemv_rows(C, dev, sweep=not a.no_sweep) + other_rows(C, dev)
+    rows = gemv_rows(C, dev, sweep=not a.no_sweep) if only is None or "gemv" in only else []
+    rows += other_rows(C, dev, only)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
