@@ -148,9 +148,9 @@ def tiny(arch: str = "llama", **kw) -> ModelConfig:
                                         num_kv_heads=2, intermediate_size=320, rotary_dim=32,
                                         max_position_embeddings=512, name="tiny-phi"),
         "gpt_neox": PRESETS["pythia-1b"].replace(vocab_size=512, hidden_size=128, num_layers=2,
-                                                 num_heads=2, num_kv_heads=2, intermediate_size=256,
-                                                 rotary_dim=16, max_position_embeddings=512,
-                                                 name="tiny-neox"),
+                                                 num_heads=2, num_kv_heads=2, head_dim=64,
+                                                 intermediate_size=256, rotary_dim=16,
+                                                 max_position_embeddings=512, name="tiny-neox"),
         "gpt2": PRESETS["gpt2"].replace(vocab_size=512, hidden_size=128, num_layers=2, num_heads=2,
                                         num_kv_heads=2, intermediate_size=256,
                                         max_position_embeddings=512, name="tiny-gpt2"),

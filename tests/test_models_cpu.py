@@ -87,3 +87,39 @@ def test_stage_split_weights_identical():
         for n, p in global_named_parameters(st):
             ref = full["embed"] if (n == "lm_head.weight" and cfg.tie_word_embeddings) else full[n]
             assert torch.equal(p, ref), n
+
+
+@pytest.mark.parametrize("arch", ["llama", "llama2", "gpt_neox", "phi", "gpt2"])
+def test_hf_export_roundtrip_loads_in_transformers(arch, tmp_path):
+    """save_hf_model writes a save_pretrained-format dir: edgellm reloads it bit-exactly and
+    transformers' own loader produces the same logits (the exporter is the inverse converter)."""
+    from edgellm.models import build_model, global_named_parameters
+    from edgellm.models.hf import load_hf_model, save_hf_model
+    cfg = tiny(arch)
+    m = build_model(cfg, dtype=torch.float32, seed=5)
+    save_hf_model(m, str(tmp_path / "ck"))
+    back = load_hf_model(str(tmp_path / "ck"), dtype=torch.float32)
+    a, b = dict(global_named_parameters(m)), dict(global_named_parameters(back))
+    assert a.keys() == b.keys() and all(torch.equal(a[k], b[k]) for k in a)
+    hf = transformers.AutoModelForCausalLM.from_pretrained(str(tmp_path / "ck"), torch_dtype=torch.float32).eval()
+    ids = torch.randint(0, cfg.vocab_size, (2, 12))
+    with torch.no_grad():
+        ref = hf(ids).logits.float()
+    kv = KVCache(cfg, 2, 32, dtype=torch.float32)
+    out = _run(m, ids, kv, 0, "prefill").view(2, 12, -1)
+    assert torch.allclose(out, ref, atol=2e-4, rtol=1e-3), (out - ref).abs().max()
+
+
+def test_fetch_random_init_layout(tmp_path):
+    """cli.fetch writes the reference downloader's BASE_DIR/<org>_<name> layout (download.py:22)
+    offline, and the registry resolves the model from it."""
+    from edgellm.cli.fetch import fetch_dataset, fetch_model
+    from edgellm.models.registry import load_model
+    base = str(tmp_path)
+    d = fetch_model("acme/tiny-llama", base, random_init=True, cfg_override=tiny("llama"))
+    assert d == str(tmp_path / "acme_tiny-llama") and (tmp_path / "acme_tiny-llama" / "RANDOM_INIT").exists()
+    assert fetch_model("acme/tiny-llama", base) == d           # present: kept
+    model, tok, src = load_model("acme/tiny-llama", "fp32", "none", "cpu", base_dir=base)
+    assert model.cfg.hidden_size == tiny("llama").hidden_size and "acme_tiny-llama" in src
+    csv_path = fetch_dataset("sentence-transformers/natural-questions", "train[:3]", base)
+    assert open(csv_path).read().splitlines()[0] == "query,answer"
