@@ -68,14 +68,19 @@ class Attention(nn.Module):
         rot = cfg.rotary_dim if cfg.pos_emb == "rope" else 0
         if ctx.attn_hook is not None:
             attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
+        elif ctx.mode == "decode":
+            # one launch: RoPE + KV append + attention (+ per-group int8 output for a W8A8 o-proj)
+            quant = self.o.takes_quantized_input and cfg.head_dim % 64 == 0
+            out, s = ops.decode_attention_fused(qkv.view(ctx.B, -1), ctx.start_pos, ctx.rope if rot else None,
+                                                k_cache, v_cache, ctx.seq_lens, cfg.num_heads, self.scale,
+                                                ctx.max_len, rot, quant)
+            if quant:
+                return self.o(QAct(out, s))
+            attn = out
         else:
             q = ops.rope_kv_write(qkv, ctx.start_pos, ctx.rope if rot else None, k_cache, v_cache,
                                   cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, rot)  # [B,T,Hq,D]
-            if ctx.mode == "decode":
-                attn = ops.decode_attention(q.view(ctx.B, cfg.num_heads, cfg.head_dim), k_cache, v_cache,
-                                            ctx.seq_lens, self.scale, ctx.max_len)
-            else:
-                attn = ops.prefill_attention(q, k_cache, v_cache, ctx.start_pos, self.scale, ctx.causal)
+            attn = ops.prefill_attention(q, k_cache, v_cache, ctx.start_pos, self.scale, ctx.causal)
         attn = attn.reshape(ctx.B * ctx.T, cfg.q_size)
         return self.o(quant_if(attn, self.o))
 
@@ -89,6 +94,12 @@ class MLP(nn.Module):
         self.down = Linear(cfg.intermediate_size, cfg.hidden_size, cfg.mlp_bias, dtype, device)
 
     def forward(self, x):
+        if getattr(self.up, "glu_blocked", False):
+            # W8A8 SwiGLU with 64-blocked gate_up rows: decode-sized batches take the fused
+            # GEMV + SwiGLU + per-group quant epilogue; larger ones the blocked activation kernel
+            if isinstance(x, QAct) and x.q.dim() == 2 and x.q.shape[0] <= 64 and x.scale.dim() == 1:
+                return self.down(self.up.glu(x))
+            return self.down(act_fn(self.up(x), "silu_glu_blocked", True))
         h = self.up(x)
         h = act_fn(h, self.act, getattr(self.down, "takes_quantized_input", False))
         return self.down(h)

@@ -88,14 +88,18 @@ def quant_per_token(x):
 
 
 # --------------------------------------------------------------------------- activations
-_ACT_MODE = {"silu_glu": 0, "gelu_tanh": 1, "gelu": 2}
+_ACT_MODE = {"silu_glu": 0, "gelu_tanh": 1, "gelu": 2, "silu_glu_blocked": 3}
 
 
 def activation(x, act: str):
+    """``silu_glu``: x = [gate | up]; ``silu_glu_blocked``: 64-blocked [gate(64) | up(64)] rows
+    (the packing of W8A8 gate_up weights, see quant.linear.W8A8Linear.glu_blocked)."""
     if _gpu(x):
         return ext().act(x, _ACT_MODE[act], False)[0]
     if act == "silu_glu":
         return _ref.silu_mul(x)
+    if act == "silu_glu_blocked":
+        return _ref.silu_mul(_ref.unblock_glu(x))
     return _ref.gelu(x, "tanh" if act == "gelu_tanh" else "none")
 
 
@@ -104,6 +108,8 @@ def activation_quant(x, act: str):
         return ext().act(x, _ACT_MODE[act], True)
     if act == "silu_glu":
         return _ref.silu_mul_quant(x)
+    if act == "silu_glu_blocked":
+        return _ref.silu_mul_quant(_ref.unblock_glu(x))
     return _ref.gelu_quant(x, "tanh" if act == "gelu_tanh" else "none")
 
 
@@ -136,6 +142,23 @@ def decode_attention(q, k_cache, v_cache, seq_lens, scale, max_len_hint: Optiona
     return _ref.decode_attention(q, k_cache, v_cache, seq_lens, scale)
 
 
+def decode_attention_fused(qkv, start_pos, rope, k_cache, v_cache, seq_lens, num_heads: int, scale: float,
+                           max_len_hint: int, rotary_dim: int, quant_out: bool = False):
+    """Decode step straight from the QKV projection: RoPE on q, append of the new k/v at
+    ``start_pos`` and attention over ``[0, seq_lens)`` in one launch.  ``quant_out`` returns
+    ``(int8 [B, Hq*D], scales [Hq*D/64, Mpad])`` for a W8A8 o-projection, else ``(bf16 [B, Hq, D], None)``."""
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    if _gpu(qkv):
+        return ext().decode_attn_fused(qkv, start_pos, rope if rotary_dim else None, k_cache, v_cache, seq_lens,
+                                       num_heads, scale, int(max_len_hint), rotary_dim, quant_out)
+    q = _ref.rope_kv_write(qkv, start_pos, rope if rotary_dim else None, k_cache, v_cache, num_heads, Hkv, D,
+                           rotary_dim)
+    out = _ref.decode_attention(q.view(qkv.shape[0], num_heads, D), k_cache, v_cache, seq_lens, scale)
+    if quant_out:
+        return _ref.quant_per_group(out.reshape(qkv.shape[0], num_heads * D))
+    return out, None
+
+
 def prefill_attention(q, k_cache, v_cache, start_pos, scale, causal=True):
     if _gpu(q):
         return ext().prefill_attn(q, k_cache, v_cache, start_pos, scale, causal)
@@ -164,15 +187,29 @@ def unpack_int8_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
 
 def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,
                 out_dtype=torch.bfloat16):
-    """INT8 x INT8 -> int32 MFMA GEMM with per-token x per-channel dequant (+bias) -> bf16
-    (``out_dtype`` applies on CPU, where fp16/fp32 agents run).  ``w_ref`` (canonical [N, K]) is
-    only needed by the CPU path."""
+    """INT8 x INT8 -> int32 MFMA GEMM with per-channel weight dequant (+bias) -> bf16.
+    ``x_scale`` is per token ([M]) or per (token, 64-column group) ([K/64, Mpad], M <= 64, from the
+    fused producers).  ``out_dtype`` applies on CPU, where fp16/fp32 agents run; ``w_ref``
+    (canonical [N, K]) is only needed by the CPU path."""
     if _gpu(qx):
         return ext().w8a8_gemm(qx, x_scale, w_packed, w_scale, bias, N, K)
     w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
     shp = qx.shape[:-1]
-    out = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, out_dtype)
+    xs = x_scale if x_scale.dim() == 2 else x_scale.reshape(-1)
+    out = _ref.w8a8_linear(qx.reshape(-1, K), xs, w, w_scale, bias, out_dtype)
     return out.view(*shp, N)
+
+
+def w8a8_glu(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None):
+    """Fused decode MLP front half: gate_up projection (64-blocked rows, N = 2F) -> silu(g)*u ->
+    int8 with per-(token, 64-feature) scales ``[F/64, Mpad]`` (one launch on GPU, M <= 64)."""
+    if _gpu(qx):
+        return ext().w8a8_gemm_glu(qx, x_scale, w_packed, w_scale, bias, N, K)
+    w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
+    y = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, torch.bfloat16)
+    h = _ref.unblock_glu(y).float()
+    f = h.shape[-1] // 2
+    return _ref.quant_per_group(torch.nn.functional.silu(h[:, :f]) * h[:, f:])
 
 
 # --------------------------------------------------------------------------- sampling / misc

@@ -47,6 +47,42 @@ def quant_per_token(y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return q, scale
 
 
+def quant_per_group(y: torch.Tensor, group: int = 64) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Symmetric int8 with one scale per (row, ``group`` columns); scales laid out
+    ``[K/group, Mpad]`` (Mpad = rows rounded up to 16, zero padded) — the decode-GEMV layout."""
+    y = y.float()
+    M, K = y.shape
+    assert K % group == 0
+    amax = y.view(M, K // group, group).abs().amax(-1).clamp_min(1e-8)        # [M, G]
+    scale = amax / 127.0
+    q = torch.round(y.view(M, K // group, group) / scale[..., None]).clamp_(-127, 127).to(torch.int8)
+    mpad = (M + 15) // 16 * 16
+    s = torch.zeros(K // group, mpad, dtype=torch.float32, device=y.device)
+    s[:, :M] = scale.t()
+    return q.view(M, K), s
+
+
+def unblock_glu(x: torch.Tensor, block: int = 64) -> torch.Tensor:
+    """64-blocked [gate(64) | up(64)] columns -> [gate | up]."""
+    M, W = x.shape[:-1], x.shape[-1]
+    v = x.reshape(*M, W // (2 * block), 2, block)
+    return torch.cat([v[..., 0, :].reshape(*M, W // 2), v[..., 1, :].reshape(*M, W // 2)], -1)
+
+
+def block_glu_rows(w: torch.Tensor, block: int = 64) -> torch.Tensor:
+    """Rows [gate | up] (2F, ...) -> 64-blocked [gate(64) | up(64)] order (inverse of unblock_glu)."""
+    F = w.shape[0] // 2
+    g, u = w[:F].reshape(F // block, block, *w.shape[1:]), w[F:].reshape(F // block, block, *w.shape[1:])
+    return torch.stack([g, u], 1).reshape(2 * F, *w.shape[1:])
+
+
+def unblock_glu_rows(w: torch.Tensor, block: int = 64) -> torch.Tensor:
+    """Inverse of block_glu_rows: 64-blocked rows -> [gate | up]."""
+    F = w.shape[0] // 2
+    v = w.reshape(F // block, 2, block, *w.shape[1:])
+    return torch.cat([v[:, 0].reshape(F, *w.shape[1:]), v[:, 1].reshape(F, *w.shape[1:])], 0)
+
+
 def rms_norm_quant(x, weight, eps, residual=None):
     # the residual stream is kept in the activation dtype (as HF does): normalise the rounded sum
     res_out = x if residual is None else (x.float() + residual.float()).to(x.dtype)
@@ -204,7 +240,16 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
 def w8a8_linear(qx: torch.Tensor, x_scale: torch.Tensor, qw: torch.Tensor, w_scale: torch.Tensor,
                 bias: Optional[torch.Tensor] = None, out_dtype=torch.bfloat16) -> torch.Tensor:
     """out[m,n] = (sum_k qx[m,k]*qw[n,k]) * x_scale[m] * w_scale[n] (+ bias[n]).
-    int32 accumulation is exact in fp64 for K < 2^31/127^2."""
+    int32 accumulation is exact in fp64 for K < 2^31/127^2.  A 2-D ``x_scale`` [K/64, Mpad] is
+    per (token, 64-column group): each group's exact partial sum takes its own scale."""
+    if x_scale.dim() == 2:
+        M, K = qx.shape
+        xs = x_scale[:, :M].t().double().repeat_interleave(64, dim=1)[:, :K]
+        acc = (qx.double() * xs) @ qw.double().t()
+        out = acc * w_scale.double()[None, :]
+        if bias is not None:
+            out = out + bias.double()
+        return out.to(out_dtype)
     acc = qx.double() @ qw.double().t()
     out = acc * x_scale.double()[:, None] * w_scale.double()[None, :]
     if bias is not None:

@@ -10,6 +10,13 @@
 //   phase 3: acc[h][d] += p[h][k] * v[k][d], reduced over lanes, then over the 4 waves
 // With nsplit > 1 each split writes (acc, m, l) and a combine kernel merges them; with one
 // split the normalised output is written directly.
+//
+// FUSED variant (decode step of the model): q comes straight from the QKV projection row and is
+// rotated in-kernel (HF rotate_half on the first `rot` dims, cos/sin from the host table, rounded
+// to bf16 exactly like ops.rope_kv_write), and the split that owns the new position appends the
+// rotated k and the v row to the head-major cache before reading it — the separate RoPE/KV-write
+// launch disappears.  QOUT additionally emits the output as int8 with one scale per (token, 64
+// columns) (layout [cols/64][Mpad]) for the W8A8 o-projection, replacing the per-token quant launch.
 #include "common.h"
 
 namespace {
@@ -17,13 +24,46 @@ constexpr int NT = 256;
 constexpr int NW = NT / 64;
 constexpr int UNROLL = 4;
 
+struct Fuse {
+  const int* pos;       // [B] cache position of the new token (seq_lens - 1)
+  const float* cs;      // rope table [max_pos, rot/2] float2 (cos, sin) or null
+  int rot;              // rotary dims (0: no rotation)
+  int64_t qkv_sb;       // row stride of the QKV input (elements)
+  int8_t* out_q;        // QOUT: [B, Hq*D] int8
+  float* out_s;         // QOUT: [(Hq*D)/64][Mpad] scales
+  int Mpad;
+};
+
+// Rotate the 8 values at head offset e0 (HF rotate_half convention), x/partner read from `head`.
+__device__ __forceinline__ void rope8(const bf16_t* __restrict__ head, int e0, int rot, const float2* csp,
+                                      float (&v)[8]) {
+  const int half = rot / 2;
+  const bool lo = e0 < half;
+  const int pe = lo ? e0 + half : e0 - half;
+  const int fi = lo ? e0 : e0 - half;
+  float p[8];
+  unpack8(*reinterpret_cast<const uint4*>(head + pe), p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 r = csp[fi + j];
+    v[j] = lo ? (v[j] * r.x - p[j] * r.y) : (v[j] * r.x + p[j] * r.y);
+  }
+}
+
+// Quantise one 64-column group held one value per lane (a full wave) and store it.
+__device__ __forceinline__ void quant_group_store(float v, int8_t* q, float* s_slot, int lane) {
+  const float amax = fmaxf(wave_max(fabsf(v)), 1e-8f);
+  *q = quant_i8(v, 127.f / amax);
+  if (lane == 0) *s_slot = amax / 127.f;
+}
+
 template <int D> struct Lanes { static constexpr int v = (D / 8 <= 8) ? 8 : ((D / 8 <= 16) ? 16 : 32); };
 
-template <int D, int G, bool DIRECT>
+template <int D, int G, bool DIRECT, bool FUSED, bool QOUT>
 __global__ void __launch_bounds__(NT) decode_attn_kernel(
-    const bf16_t* __restrict__ q, int64_t q_sb, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const bf16_t* __restrict__ q, int64_t q_sb, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     int64_t c_sb, int64_t c_sh, const int* __restrict__ seq_lens, float scale_log2, int CH, int nsplit,
-    bf16_t* __restrict__ out, int64_t o_sb, float* __restrict__ part_acc, float* __restrict__ part_ml) {
+    bf16_t* __restrict__ out, int64_t o_sb, float* __restrict__ part_acc, float* __restrict__ part_ml, Fuse fz) {
   constexpr int LPK = Lanes<D>::v;        // lanes per key row
   constexpr int KPW = 64 / LPK;           // keys per wave-instruction
   constexpr int KPB = KPW * NW;           // keys per workgroup step
@@ -61,11 +101,41 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
   const bf16_t* kb = kc + b * c_sb + kvh * c_sh + (size_t)start * D;
   const bf16_t* vb = vc + b * c_sb + kvh * c_sh + (size_t)start * D;
 
+  if constexpr (FUSED) {
+    // append the new token's rotated k and its v (only the split that owns the position)
+    const int pos = fz.pos[b];
+    if (pos >= start && pos < end) {
+      const int Hkv = gridDim.y;
+      const bf16_t* row = q + b * fz.qkv_sb;
+      const float2* csp = reinterpret_cast<const float2*>(fz.cs) + (size_t)pos * (fz.rot / 2);
+      for (int c = threadIdx.x; c < 2 * (D / 8); c += NT) {
+        const bool is_v = c >= D / 8;
+        const int e0 = (is_v ? c - D / 8 : c) * 8;
+        const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + kvh) * D;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(head + e0), v);
+        if (!is_v && e0 < fz.rot) rope8(head, e0, fz.rot, csp, v);
+        *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + e0) = pack8(v);
+      }
+    }
+    // Only this workgroup reads the new row, so the barrier's workgroup-scope release/acquire is
+    // enough (an agent-scope __threadfence would write back L2 in every workgroup: 3x slower).
+    __syncthreads();
+  }
+
   float qf[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
     if (dvalid) {
-      unpack8(*reinterpret_cast<const uint4*>(q + b * q_sb + (size_t)(kvh * G + h) * D + d0), qf[h]);
+      const bf16_t* qh = q + b * q_sb + (size_t)(kvh * G + h) * D;
+      unpack8(*reinterpret_cast<const uint4*>(qh + d0), qf[h]);
+      if constexpr (FUSED) {
+        if (d0 < fz.rot) {
+          rope8(qh, d0, fz.rot, reinterpret_cast<const float2*>(fz.cs) + (size_t)fz.pos[b] * (fz.rot / 2), qf[h]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qf[h][j] = bf2f(f2bf(qf[h][j]));   // q is bf16 in the unfused path
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[h][j] *= scale_log2;
     } else {
@@ -174,7 +244,14 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
     for (int w = 0; w < NW; ++w) a += red[(w * G + h) * D + d];
     const int hq = kvh * G + h;
     if (DIRECT) {
-      out[b * o_sb + (size_t)hq * D + d] = f2bf(a / lstat[h]);
+      if constexpr (QOUT) {     // D % 64 == 0: each 64-column group is one wave of this loop
+        const float vq = bf2f(f2bf(a / lstat[h]));
+        const int col = hq * D + d;
+        quant_group_store(vq, fz.out_q + (size_t)b * Hq * D + col, fz.out_s + (size_t)(col >> 6) * fz.Mpad + b,
+                          threadIdx.x & 63);
+      } else {
+        out[b * o_sb + (size_t)hq * D + d] = f2bf(a / lstat[h]);
+      }
     } else {
       part_acc[(((size_t)b * Hq + hq) * nsplit + split) * D + d] = a;
     }
@@ -186,9 +263,10 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
   }
 }
 
+template <bool QOUT>
 __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __restrict__ part_acc,
                                                              const float* __restrict__ part_ml, int nsplit, int D,
-                                                             bf16_t* __restrict__ out, int64_t o_sb) {
+                                                             bf16_t* __restrict__ out, int64_t o_sb, Fuse fz) {
   const int hq = blockIdx.x, b = blockIdx.y, Hq = gridDim.x;
   const float* ml = part_ml + ((size_t)b * Hq + hq) * nsplit * 2;
   float M = -INFINITY;
@@ -202,7 +280,13 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __rest
     float a = 0.f;
     for (int s = 0; s < nsplit; ++s)
       if (ml[2 * s] != -INFINITY) a += exp2f(ml[2 * s] - M) * pa[(size_t)s * D + d];
-    out[b * o_sb + (size_t)hq * D + d] = f2bf(a * invL);
+    if constexpr (QOUT) {
+      const int col = hq * D + d;
+      quant_group_store(bf2f(f2bf(a * invL)), fz.out_q + (size_t)b * Hq * D + col,
+                        fz.out_s + (size_t)(col >> 6) * fz.Mpad + b, threadIdx.x & 63);
+    } else {
+      out[b * o_sb + (size_t)hq * D + d] = f2bf(a * invL);
+    }
   }
 }
 }  // namespace
@@ -226,27 +310,38 @@ extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, i
   return 0;
 }
 
-extern "C" int edge_decode_attn(const void* q, int64_t q_sb, const void* k_cache, const void* v_cache, int64_t c_sb,
+// q: [B, *] rows with the Hq query heads at offset 0 (q_sb elements apart).  FUSED (pos != null):
+// q points at the QKV projection output, rows hold [q heads | k heads | v heads], the new token's
+// k/v are appended to the caches at pos[b] and q is rotated in-kernel.  QOUT (out_q != null,
+// D % 64 == 0): int8 output + [Hq*D/64][Mpad] scales instead of bf16 `out`.
+extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb,
                                 int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale,
                                 int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
+                                const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
                                 hipStream_t st) {
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -2;
+  const bool fused = pos != nullptr, qout = out_q != nullptr;
+  if (qout && (D % 64 != 0 || Mpad < B)) return -2;
+  if (fused && rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
+  const Fuse fz{pos, cs, fused ? rot : 0, q_sb, (int8_t*)out_q, out_s, Mpad};
   const float sl2 = scale * 1.4426950408889634f;
   const size_t lds = (size_t)(G * ch + NW * G * D + 2 * G) * sizeof(float);
   const dim3 grid(nsplit, Hkv, B);
   const bool direct = nsplit == 1;
-#define DLAUNCH(DD, GG)                                                                                       \
-  do {                                                                                                        \
-    if (direct)                                                                                               \
-      hipLaunchKernelGGL((decode_attn_kernel<DD, GG, true>), grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, \
-                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit,  \
-                         (bf16_t*)out, o_sb, part_acc, part_ml);                                              \
-    else                                                                                                      \
-      hipLaunchKernelGGL((decode_attn_kernel<DD, GG, false>), grid, dim3(NT), lds, st, (const bf16_t*)q,      \
-                         q_sb, (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, seq_lens, sl2, ch,  \
-                         nsplit, (bf16_t*)out, o_sb, part_acc, part_ml);                                      \
+#define DK(DD, GG, DI, FU, QO)                                                                                 \
+  hipLaunchKernelGGL((decode_attn_kernel<DD, GG, DI, FU, QO>), grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, \
+                     (bf16_t*)k_cache, (bf16_t*)v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, (bf16_t*)out, o_sb, \
+                     part_acc, part_ml, fz)
+#define DLAUNCH(DD, GG)                                                     \
+  do {                                                                      \
+    if (direct) {                                                           \
+      if (fused) { if (qout) DK(DD, GG, true, true, true); else DK(DD, GG, true, true, false); } \
+      else { if (qout) DK(DD, GG, true, false, true); else DK(DD, GG, true, false, false); }     \
+    } else {                                                                \
+      if (fused) DK(DD, GG, false, true, false); else DK(DD, GG, false, false, false);           \
+    }                                                                       \
   } while (0)
 #define GSW(DD)                                   \
   switch (G) {                                    \
@@ -265,8 +360,13 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, const void* k_cache
   }
 #undef GSW
 #undef DLAUNCH
-  if (!direct)
-    hipLaunchKernelGGL(decode_combine_kernel, dim3(Hq, B), dim3(D <= 128 ? 128 : 256), 0, st, part_acc, part_ml, nsplit,
-                       D, (bf16_t*)out, o_sb);
+#undef DK
+  if (!direct) {
+    const dim3 cg(Hq, B), cb(D <= 128 ? 128 : 256);
+    if (qout) hipLaunchKernelGGL(decode_combine_kernel<true>, cg, cb, 0, st, part_acc, part_ml, nsplit, D, (bf16_t*)out,
+                                 o_sb, fz);
+    else hipLaunchKernelGGL(decode_combine_kernel<false>, cg, cb, 0, st, part_acc, part_ml, nsplit, D, (bf16_t*)out,
+                            o_sb, fz);
+  }
   return (int)hipGetLastError();
 }

@@ -21,14 +21,15 @@ int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, v
                        int S, void* k2, void* v2, int64_t c2_sb, int64_t c2_sh, int S2, int split_h,
                        const int* cpos2, hipStream_t st);
 int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out);
-int edge_decode_attn(const void* q, int64_t q_sb, const void* k_cache, const void* v_cache, int64_t c_sb,
-                     int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch,
-                     int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml, hipStream_t st);
+int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb, int64_t c_sh,
+                     const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch, int nsplit, void* out,
+                     int64_t o_sb, float* part_acc, float* part_ml, const int* pos, const float* cs, int rot,
+                     void* out_q, float* out_s, int Mpad, hipStream_t st);
 int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
                       const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
                       int causal, hipStream_t st);
 int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
-                   int M, int N, int K, int KT, hipStream_t st);
+                   int M, int N, int K, int KT, int a_mpad, void* glu_q, float* glu_s, int glu_mpad, hipStream_t st);
 int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, void* workspace, hipStream_t st);
@@ -96,7 +97,8 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
 std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64_t mode, bool quant) {
   need(x, at::kBFloat16, "x");
   const int64_t W = x.size(-1), R = rows_of(x);
-  const int64_t F = mode == 0 ? W / 2 : W;
+  const int64_t F = (mode == 0 || mode == 3) ? W / 2 : W;
+  TORCH_CHECK(mode != 3 || F % 64 == 0, "blocked GLU needs F % 64 == 0");
   auto os = x.sizes().vec();
   os.back() = F;
   at::Tensor y, s;
@@ -220,9 +222,62 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   check(edge_decode_attn(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0),
                          k_cache.stride(1), seq_lens.data_ptr<int>(), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
                          ch, nsplit, out.data_ptr(), out.stride(0), nsplit > 1 ? pacc.data_ptr<float>() : nullptr,
-                         nsplit > 1 ? pml.data_ptr<float>() : nullptr, stream()),
+                         nsplit > 1 ? pml.data_ptr<float>() : nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0,
+                         stream()),
         "decode_attn");
   return out;
+}
+
+// Decode step straight from the QKV projection: rotates q, appends the new k/v at start_pos[b]
+// and attends over [0, seq_lens[b]).  quant_out: returns (int8 [B, Hq*D], scales [Hq*D/64, Mpad])
+// for a W8A8 consumer; else (bf16 [B, Hq, D], None).
+std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_fused(
+    const at::Tensor& qkv, const at::Tensor& start_pos, const std::optional<at::Tensor>& rope, at::Tensor& k_cache,
+    at::Tensor& v_cache, const at::Tensor& seq_lens, int64_t Hq, double scale, int64_t max_len_hint, int64_t rot,
+    bool quant_out) {
+  need(qkv, at::kBFloat16, "qkv");
+  TORCH_CHECK(qkv.dim() == 2, "qkv must be [B, (Hq + 2 Hkv) * D]");
+  const int64_t B = qkv.size(0), D = k_cache.size(3), Hkv = k_cache.size(1);
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width does not match the cache geometry");
+  check_cache(k_cache, "k_cache", D);
+  check_cache(v_cache, "v_cache", D);
+  TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.size(0) == B);
+  need(start_pos, at::kInt, "start_pos");
+  need(seq_lens, at::kInt, "seq_lens");
+  TORCH_CHECK(start_pos.numel() == B && seq_lens.numel() == B);
+  TORCH_CHECK(max_len_hint > 0 && max_len_hint <= k_cache.size(2), "max_len_hint out of range");
+  const float* cs = nullptr;
+  if (rot > 0) {
+    TORCH_CHECK(rope.has_value(), "rope table required for rot > 0");
+    need(*rope, at::kFloat, "rope");
+    TORCH_CHECK(rope->size(-2) * 2 == rot, "rope table width must be rot/2");
+    cs = rope->data_ptr<float>();
+  }
+  int ch = 0, nsplit = 0;
+  edge_decode_attn_plan((int)B, (int)Hkv, (int)max_len_hint, &ch, &nsplit);
+  at::Tensor pacc, pml, out, oq;
+  std::optional<at::Tensor> os;
+  if (nsplit > 1) {
+    pacc = at::empty({B, Hq, nsplit, D}, qkv.options().dtype(at::kFloat));
+    pml = at::empty({B, Hq, nsplit, 2}, qkv.options().dtype(at::kFloat));
+  }
+  const int64_t Mpad = (B + 15) / 16 * 16;
+  if (quant_out) {
+    TORCH_CHECK(D % 64 == 0, "quantised attention output needs head_dim % 64 == 0");
+    oq = at::empty({B, Hq * D}, qkv.options().dtype(at::kChar));
+    os = at::empty({Hq * D / 64, Mpad}, qkv.options().dtype(at::kFloat));
+  } else {
+    out = at::empty({B, Hq, D}, qkv.options());
+  }
+  check(edge_decode_attn(qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0),
+                         k_cache.stride(1), seq_lens.data_ptr<int>(), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                         ch, nsplit, quant_out ? nullptr : out.data_ptr(), quant_out ? 0 : out.stride(0),
+                         nsplit > 1 ? pacc.data_ptr<float>() : nullptr, nsplit > 1 ? pml.data_ptr<float>() : nullptr,
+                         start_pos.data_ptr<int>(), cs, (int)rot, quant_out ? oq.data_ptr() : nullptr,
+                         quant_out ? os->data_ptr<float>() : nullptr, (int)Mpad, stream()),
+        "decode_attn_fused");
+  if (quant_out) return {oq, os};
+  return {out, std::nullopt};
 }
 
 at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -244,25 +299,62 @@ at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at
 }
 
 // ---------------------------------------------------------------------------------- int8 gemm
-at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
-                     const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
-  need(a, at::kChar, "a");
+// Activation scales: per token (sa [M]) or per (token, 64-column group) (sa [KT, Mpad], M <= 64).
+int64_t a_scale_mpad(const at::Tensor& sa, int64_t M, int64_t KT) {
   need(sa, at::kFloat, "a_scale");
+  if (sa.dim() == 2) {
+    TORCH_CHECK(sa.size(0) == KT && sa.size(1) >= (M + 15) / 16 * 16 && sa.size(1) % 16 == 0,
+                "grouped a_scale must be [K/64, Mpad]");
+    TORCH_CHECK(M <= 64, "grouped activation scales are a decode (M <= 64) feature");
+    return sa.size(1);
+  }
+  TORCH_CHECK(sa.numel() == M, "a_scale must have one entry per row");
+  return 0;
+}
+
+void check_w8a8_operands(const at::Tensor& a, const at::Tensor& wp, const at::Tensor& sw,
+                         const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  need(a, at::kChar, "a");
   need(wp, at::kChar, "w_packed");
   need(sw, at::kFloat, "w_scale");
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
-  const int64_t M = rows_of(a);
-  TORCH_CHECK(sa.numel() == M && sw.numel() == N);
-  const int64_t KT = (K + 63) / 64, NTt = (N + 15) / 16;
-  TORCH_CHECK(wp.numel() == NTt * KT * 1024, "packed weight has wrong size");
+  TORCH_CHECK(sw.numel() == N);
+  TORCH_CHECK(wp.numel() == (N + 15) / 16 * ((K + 63) / 64) * 1024, "packed weight has wrong size");
   if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+}
+
+at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
+                     const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  check_w8a8_operands(a, wp, sw, bias, N, K);
+  const int64_t M = rows_of(a), KT = (K + 63) / 64;
+  const int64_t mpad = a_scale_mpad(sa, M, KT);
   auto os = a.sizes().vec();
   os.back() = N;
   auto out = at::empty(os, a.options().dtype(at::kBFloat16));
   check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
-                       bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N, (int)K, (int)KT, stream()),
+                       bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N, (int)K, (int)KT, (int)mpad,
+                       nullptr, nullptr, 0, stream()),
         "w8a8_gemm");
   return out;
+}
+
+// gate_up projection (64-blocked rows) fused with silu(g)*u and per-group int8 quantisation:
+// returns (h int8 [M, N/2], scales [N/128, Mpad]).  M <= 64, per-token sa.
+std::tuple<at::Tensor, at::Tensor> w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp,
+                                                 const at::Tensor& sw, const std::optional<at::Tensor>& bias,
+                                                 int64_t N, int64_t K) {
+  check_w8a8_operands(a, wp, sw, bias, N, K);
+  const int64_t M = rows_of(a), KT = (K + 63) / 64;
+  TORCH_CHECK(M <= 64 && N % 128 == 0, "fused GLU needs M <= 64 and N % 128 == 0");
+  TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GLU takes per-token activation scales");
+  const int64_t Mpad = (M + 15) / 16 * 16;
+  auto hq = at::empty({M, N / 2}, a.options());
+  auto hs = at::empty({N / 128, Mpad}, a.options().dtype(at::kFloat));
+  check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                       bias ? bias->data_ptr() : nullptr, nullptr, (int)M, (int)N, (int)K, (int)KT, 0, hq.data_ptr(),
+                       hs.data_ptr<float>(), (int)Mpad, stream()),
+        "w8a8_gemm_glu");
+  return {hq, hs};
 }
 
 // ---------------------------------------------------------------------------------- sampler
@@ -325,6 +417,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_attn", &decode_attn);
   m.def("prefill_attn", &prefill_attn);
   m.def("w8a8_gemm", &w8a8_gemm);
+  m.def("decode_attn_fused", &decode_attn_fused);
+  m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
   m.def("sample", &sample);
   m.def("sample_timestamps", &sample_timestamps);
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {

@@ -37,14 +37,36 @@ __device__ __forceinline__ void store_out(bf16_t* __restrict__ out, int M, int N
 }
 
 // ------------------------------------------------------------------------------------ gemv
+// Activation scales: per token (sa[M], AG = false; int32 accumulation over all of K) or per
+// (token, 64-column group) (AG = true; sa laid out [KT][Mpad], written by the fused producers —
+// attention and the GLU epilogue below).  With AG each k-tile's MFMA starts from zero and is
+// folded into a float accumulator with its group scale (4 cvt + 4 fma per 16x16 tile).
+__device__ __forceinline__ v4f group_scales(const float* __restrict__ sa, int k, int KT, int Mpad, int r0) {
+  return k < KT ? *reinterpret_cast<const v4f*>(sa + (size_t)k * Mpad + r0) : v4f{0.f, 0.f, 0.f, 0.f};
+}
+
+__device__ __forceinline__ void fold(v4f& accf, const v4i& t, const v4f& s) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) accf[q] += (float)t[q] * s[q];
+}
+
+__device__ __forceinline__ void store_out_f(bf16_t* __restrict__ out, int M, int N, int row, int col, float v,
+                                            const float* __restrict__ sw, const bf16_t* __restrict__ bias) {
+  if (row < M && col < N) {
+    v *= sw[col];
+    if (bias) v += bf2f(bias[col]);
+    out[(size_t)row * N + col] = f2bf(v);
+  }
+}
+
 // NW waves per workgroup split K; k-tile kt goes to wave kt % NW, so at each unrolled step the
 // workgroup's NW waves read NW consecutive 1 KiB tiles = one contiguous NW KiB run of the panel.
 // UNROLL tiles per wave are in flight before the first MFMA (nontemporal: read-once weights).
-template <int MT, int UNROLL, int NW>
+template <int MT, int UNROLL, int NW, bool AG>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                             const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                            int M, int N, int K, int KT) {
+                                                            int M, int N, int K, int KT, int Mpad) {
   __shared__ v4i red[NW][MT][64];
   const int nt = blockIdx.x;
   const int m0 = blockIdx.y * (16 * MT);
@@ -52,8 +74,9 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
   const int arow = lane & 15, akc = 16 * (lane >> 4);
 
   v4i acc[MT];
+  v4f accf[MT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) acc[i] = v4i{0, 0, 0, 0};
+  for (int i = 0; i < MT; ++i) { acc[i] = v4i{0, 0, 0, 0}; accf[i] = v4f{0.f, 0.f, 0.f, 0.f}; }
 
   const v4i* wp = reinterpret_cast<const v4i*>(Wp + ((size_t)nt * KT) * 1024) + lane;
   const int8_t* arows[MT];
@@ -69,6 +92,7 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
   for (int kt = wave; kt < KT; kt += NW * UNROLL) {
     v4i b[UNROLL];
     v4i a[UNROLL][MT];
+    v4f sg[UNROLL][MT];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int k = kt + u * NW;
@@ -80,6 +104,7 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
       const int kk = k * 64 + akc;
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
+        if constexpr (AG) sg[u][i] = group_scales(sa, k, KT, Mpad, m0 + i * 16 + 4 * (lane >> 4));
         if (aval[i] && k < KT && kk + 16 <= K && k16) a[u][i] = *reinterpret_cast<const v4i*>(arows[i] + kk);
         else if (aval[i] && k < KT && kk < K) {
           int8_t t[16];  // ragged K (K % 16 != 0): byte-wise, zero padded
@@ -92,35 +117,58 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int i = 0; i < MT; ++i) acc[i] = mfma_i8(a[u][i], b[u], acc[i]);
+      for (int i = 0; i < MT; ++i) {
+        if constexpr (AG) fold(accf[i], mfma_i8(a[u][i], b[u], v4i{0, 0, 0, 0}), sg[u][i]);
+        else acc[i] = mfma_i8(a[u][i], b[u], acc[i]);
+      }
   }
 
 #pragma unroll
-  for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
+  for (int i = 0; i < MT; ++i) {
+    if constexpr (AG) red[wave][i][lane] = __builtin_bit_cast(v4i, accf[i]);
+    else red[wave][i][lane] = acc[i];
+  }
   __syncthreads();
   for (int i = wave; i < MT; i += NW) {
-    v4i s = red[0][i][lane];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) s += red[w][i][lane];
     const int col = nt * 16 + (lane & 15);
+    if constexpr (AG) {
+      v4f s = __builtin_bit_cast(v4f, red[0][i][lane]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store_out(out, M, N, m0 + i * 16 + 4 * (lane >> 4) + j, col, s[j], sa, sw, bias);
+      for (int w = 1; w < NW; ++w) s += __builtin_bit_cast(v4f, red[w][i][lane]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) store_out_f(out, M, N, m0 + i * 16 + 4 * (lane >> 4) + j, col, s[j], sw, bias);
+    } else {
+      v4i s = red[0][i][lane];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) s += red[w][i][lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) store_out(out, M, N, m0 + i * 16 + 4 * (lane >> 4) + j, col, s[j], sa, sw, bias);
+    }
   }
 }
 
-// M <= 16 variant with NTW n-tiles per workgroup: each A fragment (one per k-tile) feeds NTW
-// MFMAs, cutting the L2->CU activation traffic NTW-fold (at M = 16 an A fragment is as large as
-// a weight fragment, so with NTW = 1 the kernel moves twice the bytes it must).
+// NTW n-tiles per workgroup: each A fragment (one per k-tile) feeds NTW MFMAs, cutting the
+// L2->CU activation traffic NTW-fold (at M = 16 an A fragment is as large as a weight fragment,
+// so with NTW = 1 the kernel moves twice the bytes it must).
 // For M > 16 every 16-row block is its own workgroup; the block order is XCD-grouped: dispatch
 // ids b, b+8, b+16, ... land on one XCD, so the MB row blocks of a weight panel are consecutive
 // ids within one XCD (id = xcd + 8 * (mb + MB * panel_group)) and re-read the panel from that
 // XCD's L2 instead of HBM (placement is a speed assumption only, never a correctness one).
-template <int UNROLL, int NW, int NTW>
+//
+// EPI 1 (fused SwiGLU + quant, decode MLP): the gate_up weight rows are packed 64-blocked
+// ([gate f0..f0+63 | up f0..f0+63] per 128 rows), so one 8-tile panel holds both halves of 64
+// features.  Waves 0-3 each pair gate tile w with up tile w+4, round both to bf16 (as the
+// unfused GEMM output would be), form silu(g)*u, and the panel writes int8 h with one scale per
+// (token, 64 features) — exactly the per-group input the down projection's AG mode reads.
+template <int UNROLL, int NW, int NTW, bool AG, int EPI>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                 const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                 const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                                int M, int N, int K, int KT, int NTt) {
+                                                                int M, int N, int K, int KT, int NTt, int Mpad,
+                                                                int8_t* __restrict__ hq, float* __restrict__ hs) {
+  static_assert(EPI == 0 || (NTW == 8 && NW >= 4 && !AG), "GLU epilogue: 8-tile panels, >= 4 waves");
   __shared__ v4i red[NW][NTW][64];
+  __shared__ float gmax[4][16];
   const int MB = (M + 15) / 16;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, r = bid >> 3;
@@ -131,8 +179,9 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int arow = m0 + (lane & 15), akc = 16 * (lane >> 4);
   v4i acc[NTW];
+  v4f accf[NTW];
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) acc[j] = v4i{0, 0, 0, 0};
+  for (int j = 0; j < NTW; ++j) { acc[j] = v4i{0, 0, 0, 0}; accf[j] = v4f{0.f, 0.f, 0.f, 0.f}; }
   const v4i* wp[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
@@ -146,6 +195,7 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
   for (int kt = wave; kt < KT; kt += NW * UNROLL) {
     v4i b[UNROLL][NTW];
     v4i a[UNROLL];
+    v4f sg[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int k = kt + u * NW;
@@ -157,6 +207,7 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
     for (int u = 0; u < UNROLL; ++u) {
       const int k = kt + u * NW;
       const int kk = k * 64 + akc;
+      if constexpr (AG) sg[u] = group_scales(sa, k, KT, Mpad, m0 + 4 * (lane >> 4));
       if (aval && k < KT && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
       else if (aval && k < KT && kk < K) {
         int8_t t[16];
@@ -168,19 +219,70 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
+      for (int j = 0; j < NTW; ++j) {
+        if constexpr (AG) fold(accf[j], mfma_i8(a[u], b[u][j], v4i{0, 0, 0, 0}), sg[u]);
+        else acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
+      }
   }
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) red[wave][j][lane] = acc[j];
+  for (int j = 0; j < NTW; ++j) {
+    if constexpr (AG) red[wave][j][lane] = __builtin_bit_cast(v4i, accf[j]);
+    else red[wave][j][lane] = acc[j];
+  }
   __syncthreads();
-  for (int j = wave; j < NTW; j += NW) {
-    if (nt0 + j >= NTt) continue;
-    v4i s = red[0][j][lane];
+  if constexpr (EPI == 0) {
+    for (int j = wave; j < NTW; j += NW) {
+      if (nt0 + j >= NTt) continue;
+      const int col = (nt0 + j) * 16 + (lane & 15);
+      if constexpr (AG) {
+        v4f s = __builtin_bit_cast(v4f, red[0][j][lane]);
 #pragma unroll
-    for (int w = 1; w < NW; ++w) s += red[w][j][lane];
-    const int col = (nt0 + j) * 16 + (lane & 15);
+        for (int w = 1; w < NW; ++w) s += __builtin_bit_cast(v4f, red[w][j][lane]);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) store_out(out, M, N, m0 + 4 * (lane >> 4) + q, col, s[q], sa, sw, bias);
+        for (int q = 0; q < 4; ++q) store_out_f(out, M, N, m0 + 4 * (lane >> 4) + q, col, s[q], sw, bias);
+      } else {
+        v4i s = red[0][j][lane];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) s += red[w][j][lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) store_out(out, M, N, m0 + 4 * (lane >> 4) + q, col, s[q], sa, sw, bias);
+      }
+    }
+  } else {
+    const int F = N / 2;
+    float h[4];
+    if (wave < 4) {
+      v4i sgt = red[0][wave][lane], sut = red[0][wave + 4][lane];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) { sgt += red[w][wave][lane]; sut += red[w][wave + 4][lane]; }
+      const int gcol = (nt0 + wave) * 16 + (lane & 15), ucol = (nt0 + 4 + wave) * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + 4 * (lane >> 4) + q;
+        const float s_a = row < M ? sa[row] : 0.f;
+        float g = (float)sgt[q] * s_a * sw[gcol], u = (float)sut[q] * s_a * sw[ucol];
+        if (bias) { g += bf2f(bias[gcol]); u += bf2f(bias[ucol]); }
+        g = bf2f(f2bf(g));
+        u = bf2f(f2bf(u));
+        h[q] = g / (1.f + __expf(-g)) * u;
+        float m = fabsf(h[q]);
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if ((lane & 15) == 0) gmax[wave][4 * (lane >> 4) + q] = m;
+      }
+    }
+    __syncthreads();
+    if (wave < 4) {
+      const int grp = nt0 / 8;
+      const int f = grp * 64 + wave * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 4 * (lane >> 4) + q, row = m0 + rr;
+        const float amax = fmaxf(fmaxf(fmaxf(gmax[0][rr], gmax[1][rr]), fmaxf(gmax[2][rr], gmax[3][rr])), 1e-8f);
+        if (row < M) hq[(size_t)row * F + f] = quant_i8(h[q], 127.f / amax);
+        if (wave == 0 && (lane & 15) == 0) hs[(size_t)grp * Mpad + row] = amax / 127.f;
+      }
+    }
   }
 }
 
@@ -276,10 +378,26 @@ static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0;
 extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
 
+// sa: per-token [M] (a_mpad == 0) or per-group [KT][a_mpad] (a_mpad > 0, GEMV shapes only).
+// glu_q/glu_s != null: fused SwiGLU + per-group quant epilogue (64-blocked gate_up weights,
+// M <= 64, per-token sa): writes int8 [M, N/2] and scales [N/128][a_mpad_out] instead of `out`.
 extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
-                              void* out, int M, int N, int K, int KT, hipStream_t st) {
+                              void* out, int M, int N, int K, int KT, int a_mpad, void* glu_q, float* glu_s,
+                              int glu_mpad, hipStream_t st) {
   if (M == 0 || N == 0) return 0;
   const int NTt = (N + 15) / 16;
+  const bool ag = a_mpad > 0;
+  const int mblocks16 = (M + 15) / 16;
+  if (glu_q != nullptr) {
+    if (ag || M > 64 || N % 128 != 0 || glu_mpad < mblocks16 * 16) return -2;
+    const int panels = NTt / 8;
+    const dim3 grid(((panels + 7) / 8) * 8 * mblocks16);
+    hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<2, 4, 8, false, 1>), grid, dim3(256), 0, st, (const int8_t*)A, sa,
+                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, glu_mpad,
+                       (int8_t*)glu_q, glu_s);
+    return (int)hipGetLastError();
+  }
+  if (ag && (M > 64 || a_mpad < mblocks16 * 16)) return -2;
   if (M > 64 && K % 64 == 0 && K / 64 == KT) {
     const int grid_n = (NTt * 16 + BN - 1) / BN;
     const int grid_m = (M + BM - 1) / BM;
@@ -287,12 +405,16 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
                        (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_n);
     return (int)hipGetLastError();
   }
-  const int mblocks16 = (M + 15) / 16;
   // waves per workgroup: enough that every wave owns >= 2 k-tiles, at most 16
   int nw = g_gemv_nw > 0 ? g_gemv_nw : (KT >= 128 ? 16 : (KT >= 32 ? 8 : 4));
-#define GEMV_NW(MT, U, NWV)                                                                                    \
-  hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV>), dim3(NTt, (M + 16 * MT - 1) / (16 * MT)), dim3(NWV * 64), 0, \
-                     st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT)
+#define GEMV_NW(MT, U, NWV)                                                                                       \
+  do {                                                                                                            \
+    const dim3 g(NTt, (M + 16 * MT - 1) / (16 * MT));                                                            \
+    if (ag) hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV, true>), g, dim3(NWV * 64), 0, st, (const int8_t*)A,  \
+                               sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad); \
+    else hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV, false>), g, dim3(NWV * 64), 0, st, (const int8_t*)A,    \
+                            sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad);    \
+  } while (0)
 #define GEMV(MT, U)                                   \
   do {                                                \
     if (nw >= 16) GEMV_NW(MT, U, 16);                 \
@@ -313,9 +435,15 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   if (ntw > 1) {
     // XCD-grouped 1-D grid: panels padded to a multiple of 8, one workgroup per (panel, 16-row block)
 #define NTWL(U, NWV, NTWV)                                                                                           \
-  hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV>),                                                           \
-                     dim3(((NTt + NTWV - 1) / NTWV + 7) / 8 * 8 * mblocks16), dim3(NWV * 64), 0, st,                  \
-                     (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt)
+  do {                                                                                                               \
+    const dim3 g(((NTt + NTWV - 1) / NTWV + 7) / 8 * 8 * mblocks16);                                                 \
+    if (ag) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, true, 0>), g, dim3(NWV * 64), 0, st,              \
+                               (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N,  \
+                               K, KT, NTt, a_mpad, nullptr, nullptr);                                                \
+    else hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, false, 0>), g, dim3(NWV * 64), 0, st,                \
+                            (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K,  \
+                            KT, NTt, a_mpad, nullptr, nullptr);                                                      \
+  } while (0)
 #define NTWN(NWV)                                                   \
   do {                                                              \
     if (ntw >= 4) { if (un >= 4) NTWL(4, NWV, 4); else NTWL(2, NWV, 4); } \

@@ -147,7 +147,8 @@ __global__ void __launch_bounds__(NT) norm_kernel(
 }
 
 // ----------------------------------------------------------------------------- activations
-// MODE 0: silu(gate)*up with input [gate | up] of width 2F; 1: gelu tanh; 2: gelu erf
+// MODE 0: silu(gate)*up with input [gate | up] of width 2F; 1: gelu tanh; 2: gelu erf;
+// 3: silu GLU over the 64-blocked [gate(64) | up(64)] layout (F % 64 == 0)
 template <int NCH, int MODE, bool QUANT>
 __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                  int8_t* __restrict__ yq, float* __restrict__ ys, int F) {
@@ -166,6 +167,25 @@ __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, b
         const float g = v[c][j];
         v[c][j] = g / (1.f + __expf(-g)) * u[c][j];
       }
+  } else if constexpr (MODE == 3) {
+    // 64-blocked GLU layout (gate_up weights packed for the fused decode epilogue): feature e's
+    // gate sits at (e/64)*128 + e%64 and its up 64 columns later
+    const bf16_t* xr = x + row * (size_t)(2 * F);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * NT + threadIdx.x) * 8;
+      if (e < F) {
+        const bf16_t* g = xr + (e >> 6) * 128 + (e & 63);
+        float u[8];
+        unpack8(*reinterpret_cast<const uint4*>(g), v[c]);
+        unpack8(*reinterpret_cast<const uint4*>(g + 64), u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = v[c][j] / (1.f + __expf(-v[c][j])) * u[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      }
+    }
   } else {
     load_row<NCH>(x + row * (size_t)F, F, v);
 #pragma unroll
@@ -273,6 +293,7 @@ extern "C" int edge_act(const void* x, void* y, void* yq, float* ys, int rows, i
   NCH_DISPATCH(F, {
     if (mode == 0) { if (quant) LAUNCH_ACT(0, true); else LAUNCH_ACT(0, false); }
     else if (mode == 1) { if (quant) LAUNCH_ACT(1, true); else LAUNCH_ACT(1, false); }
+    else if (mode == 3) { if (quant) LAUNCH_ACT(3, true); else LAUNCH_ACT(3, false); }
     else { if (quant) LAUNCH_ACT(2, true); else LAUNCH_ACT(2, false); }
   });
 #undef LAUNCH_ACT

@@ -25,7 +25,7 @@ import torch
 
 from ..models.configs import ModelConfig
 from ..models.decoder import DecoderLM, global_named_parameters
-from .linear import LLMInt8Linear, W8A8Linear
+from .linear import LLMInt8Linear, W8A8Linear, enable_fused_glu
 
 FORMAT = "edgellm-int8"
 VERSION = 1
@@ -43,17 +43,19 @@ def save_quantized(model: DecoderLM, path: str, extra: Optional[dict] = None) ->
         for a, b in _PROJ:
             mod = getattr(getattr(layer, a), b)
             p = f"layers.{layer.idx}.{a}.{b}"
-            if isinstance(mod, W8A8Linear):
-                tensors[p + ".qweight"] = mod.int8_weight().cpu()
-                tensors[p + ".w_scale"] = mod.w_scale.cpu()
+            bias = mod.bias
+            if isinstance(mod, W8A8Linear):          # canonical [gate | up] row order on disk
+                q, sc, bias = mod.canonical()
+                tensors[p + ".qweight"] = q.cpu()
+                tensors[p + ".w_scale"] = sc.cpu()
             elif isinstance(mod, LLMInt8Linear):
                 tensors[p + ".qweight"] = mod.weight_i8.cpu()
                 tensors[p + ".SCB"] = mod.SCB.cpu()
             else:
                 continue
             quant_names.add(p)
-            if mod.bias is not None:
-                tensors[p + ".bias"] = mod.bias.cpu()
+            if bias is not None:
+                tensors[p + ".bias"] = bias.cpu()
     for name, prm in global_named_parameters(model):
         if any(name.startswith(q + ".") for q in quant_names):
             continue
@@ -104,4 +106,6 @@ def load_quantized(path: str, device=None, first: int = 0, last: Optional[int] =
                 src = "embed"
             prm.copy_(sf.get_tensor(src).to(device=prm.device, dtype=prm.dtype))
     model.quant_mode = mode
+    if mode in ("w8a8_smoothquant", "w8a8"):
+        enable_fused_glu(model)
     return model

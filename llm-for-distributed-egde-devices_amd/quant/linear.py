@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops import _ref
 from ..models.layers import Linear, QAct
 
 
@@ -45,6 +46,7 @@ class W8A8Linear(nn.Module):
         self.register_buffer("bias", torch.zeros(out_features, dtype=dtype, device=device) if bias else None)
         self._w_cpu = None
         self.out_dtype = dtype
+        self.glu_blocked = False      # rows stored 64-blocked [gate(64) | up(64)] (fused decode GLU)
 
     @classmethod
     @torch.no_grad()
@@ -72,19 +74,49 @@ class W8A8Linear(nn.Module):
     def dequant_weight(self) -> torch.Tensor:
         return self.int8_weight().float() * self.w_scale[:, None]
 
+    @torch.no_grad()
+    def block_glu_(self) -> "W8A8Linear":
+        """Re-pack a [gate | up] projection 64-blocked so one GEMV panel holds both halves of 64
+        features (the fused SwiGLU + quant epilogue, ops.w8a8_glu).  Outputs of ``forward`` are
+        then in blocked order (activation ``silu_glu_blocked``)."""
+        if not self.glu_blocked:
+            q, sc, b = self.canonical()
+            self.load_int8(_ref.block_glu_rows(q), _ref.block_glu_rows(sc),
+                           _ref.block_glu_rows(b) if b is not None else None)
+            self.glu_blocked = True
+        return self
+
+    def canonical(self):
+        """(int8 weight, w_scale, bias) in the un-blocked [gate | up] row order (checkpoints)."""
+        q, sc, b = self.int8_weight(), self.w_scale, self.bias
+        if self.glu_blocked:
+            q, sc = _ref.unblock_glu_rows(q), _ref.unblock_glu_rows(sc)
+            b = _ref.unblock_glu_rows(b) if b is not None else None
+        return q, sc, b
+
+    def _wref(self, x):
+        if x.is_cuda:
+            return None
+        if self._w_cpu is None:
+            self._w_cpu = self.int8_weight()
+        return self._w_cpu
+
     def forward(self, x):
         if not isinstance(x, QAct):
             x = QAct(*ops.quant_per_token(x))
         K, N = self.in_features, self.out_features
         shp = x.q.shape[:-1]
-        wref = None
-        if not x.q.is_cuda:
-            if self._w_cpu is None:
-                self._w_cpu = self.int8_weight()
-            wref = self._w_cpu
-        out = ops.w8a8_linear(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias,
-                              N, K, w_ref=wref, out_dtype=self.out_dtype)
+        scale = x.scale if x.scale.dim() == 2 and x.q.dim() == 2 else x.scale.reshape(-1)
+        out = ops.w8a8_linear(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale, self.bias,
+                              N, K, w_ref=self._wref(x.q), out_dtype=self.out_dtype)
         return out.view(*shp, N)
+
+    def glu(self, x: QAct) -> QAct:
+        """Fused gate_up -> silu(g)*u -> per-group int8 (blocked layout, M <= 64)."""
+        K, N = self.in_features, self.out_features
+        q, s = ops.w8a8_glu(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,
+                            w_ref=self._wref(x.q))
+        return QAct(q, s)
 
     def extra_repr(self):
         return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, W8A8 int8"
@@ -172,3 +204,18 @@ class CPUDynamicLinear(nn.Module):
         if isinstance(x, QAct):
             x = x.q.float() * x.scale[..., None]
         return self.q(x.float()).to(self.out_dtype)
+
+
+def enable_fused_glu(model) -> int:
+    """Block the W8A8 gate_up projections of SwiGLU layers (F % 64 == 0) so the decode MLP runs
+    as GEMV+SwiGLU+quant -> down GEMV (two launches instead of three).  Returns layers changed."""
+    cfg = model.cfg
+    if not (cfg.is_glu and cfg.act == "silu_glu" and cfg.intermediate_size % 64 == 0):
+        return 0
+    n = 0
+    for layer in model.layers:
+        up = layer.mlp.up
+        if isinstance(up, W8A8Linear) and isinstance(layer.mlp.down, W8A8Linear) and not up.glu_blocked:
+            up.block_glu_()
+            n += 1
+    return n

@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from ..models.decoder import AttnCtx, DecoderLM
 from ..models.layers import Linear
-from .linear import CPUDynamicLinear, LLMInt8Linear, W8A8Linear
+from .linear import CPUDynamicLinear, LLMInt8Linear, W8A8Linear, enable_fused_glu
 
 QUANT_MODES = ("none", "w8a8_smoothquant", "w8a8", "llm_int8", "cpu_dynamic")
 
@@ -157,6 +157,8 @@ def quantize_model(model: DecoderLM, mode: str, calib_ids: Optional[torch.Tensor
                 new = CPUDynamicLinear(lin)
             setattr(parent, attr, new)
     model.quant_mode = mode
+    if mode in ("w8a8_smoothquant", "w8a8"):
+        enable_fused_glu(model)
     if mode == "w8a8_smoothquant":
         model.smooth_factors = {k: v.detach().cpu() for k, v in factors.items()
                                 if model.first <= int(k.split(".")[1]) < model.last}

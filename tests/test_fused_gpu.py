@@ -1,0 +1,108 @@
+"""Fused decode-path kernels vs the fp32 reference composition of the unfused ops.
+
+* decode attention straight from the QKV projection (RoPE + KV append + attention, optional
+  per-group int8 output) == ops._ref rope_kv_write -> decode_attention (-> quant_per_group)
+* W8A8 GEMV with per-(token, 64-column) activation scales == _ref.w8a8_linear (2-D x_scale)
+* gate_up GEMV + SwiGLU + per-group quant epilogue == _ref composition on the blocked layout
+* blocked-layout activation kernel (prefill path of the same packing)
+"""
+import math
+
+import pytest
+import torch
+
+from edgellm import ops
+from edgellm.ops import _ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    bad = (err > atol + rtol * b.abs()).sum().item()
+    assert bad == 0, f"{bad} / {a.numel()} elements off, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 32, 128, 128), (32, 8, 128, 128), (32, 8, 64, 64), (32, 32, 80, 32),
+                                          (8, 8, 256, 64), (12, 12, 64, 0)])
+@pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333)])
+@pytest.mark.parametrize("quant", [False, True])
+def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant):
+    if quant and D % 64:
+        pytest.skip("per-group output needs D % 64 == 0")
+    C = ops.ext()
+    torch.manual_seed(3)
+    B = len(lens)
+    S = max(lens) + 5
+    W = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(B, W, device=cuda).bfloat16()
+    kc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    vc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    kr, vr = kc.clone(), vc.clone()
+    sl = torch.tensor(lens, device=cuda, dtype=torch.int32)
+    pos = sl - 1
+    rope = ops.rope_tables(rot, S, 10000.0, device=cuda) if rot else None
+    scale = 1 / math.sqrt(D)
+    out, s = C.decode_attn_fused(qkv, pos, rope, kc, vc, sl, Hq, scale, max(lens), rot, quant)
+    q = _ref.rope_kv_write(qkv, pos, rope, kr, vr, Hq, Hkv, D, rot)
+    ref = _ref.decode_attention(q.view(B, Hq, D), kr, vr, sl, scale)
+    assert torch.equal(kc, kr) and torch.equal(vc, vr), "KV append differs from rope_kv_write"
+    if quant:
+        qr, sr = _ref.quant_per_group(ref.reshape(B, Hq * D))
+        deq = out.float() * s[:, :B].t().repeat_interleave(64, 1)
+        _close(deq, ref.reshape(B, -1), 3e-2, 3e-2)
+        _close(s[:, :B], sr[:, :B], 1e-3, 2e-2)
+    else:
+        _close(out, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (1040, 128), (22016, 4096)])
+def test_w8a8_gemm_group_scales(cuda, M, N, K):
+    C = ops.ext()
+    torch.manual_seed(M)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    mpad = (M + 15) // 16 * 16
+    sx = torch.rand(K // 64, mpad, device=cuda) * 0.02 + 1e-3
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.02 + 1e-3
+    bias = torch.randn(N, device=cuda).bfloat16()
+    out = C.w8a8_gemm(qx, sx, ops.pack_int8_weight(w), sw, bias, N, K)
+    _close(out, _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32), 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 3, 16, 40, 64])
+@pytest.mark.parametrize("F,K", [(1024, 4096), (11008, 4096), (256, 128)])
+def test_w8a8_glu_fused(cuda, M, F, K):
+    C = ops.ext()
+    torch.manual_seed(F + M)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (2 * F, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
+    wb, swb = _ref.block_glu_rows(w), _ref.block_glu_rows(sw)
+    hq, hs = C.w8a8_gemm_glu(qx, sx, ops.pack_int8_weight(wb), swb, None, 2 * F, K)
+    y = _ref.w8a8_linear(qx, sx, w, sw, None, torch.bfloat16).float()       # unblocked [gate | up]
+    h = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+    qr, sr = _ref.quant_per_group(h)
+    _close(hs[:, :M], sr[:, :M], 1e-6, 1e-2)
+    # g and u are rounded to bf16 (as the unfused GEMM output is); float-vs-double products can
+    # land one bf16 ulp apart, so allow one int8 step plus 1% on top of the quantisation error
+    step = hs[:, :M].t().repeat_interleave(64, 1).cpu()
+    deq = hq.float().cpu() * step
+    err = (deq - h.cpu()).abs()
+    assert (err <= 1.01 * step + 0.01 * h.abs().cpu()).all(), err.max()
+    assert (hq.int() - qr.int()).abs().max().item() <= 2
+
+
+@pytest.mark.parametrize("F", [256, 11008])
+def test_act_blocked_glu(cuda, F):
+    C = ops.ext()
+    x = torch.randn(5, 2 * F, device=cuda).bfloat16() * 2
+    y, _ = C.act(x, 3, False)
+    _close(y, _ref.silu_mul(_ref.unblock_glu(x)), 2e-2, 1e-2)
+    q, s = C.act(x, 3, True)
+    qr, sr = _ref.silu_mul_quant(_ref.unblock_glu(x))
+    _close(s, sr, 0, 2e-3)
+    assert (q.int() - qr.int()).abs().max().item() <= 1
