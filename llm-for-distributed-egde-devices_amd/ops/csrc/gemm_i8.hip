@@ -373,10 +373,11 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 }
 }  // namespace
 
-static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0;
+static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0;
 // tuning hook (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
+extern "C" void edge_w8a8_glu_unroll(int u) { g_glu_unroll = u; }
 
 // sa: per-token [M] (a_mpad == 0) or per-group [KT][a_mpad] (a_mpad > 0, GEMV shapes only).
 // glu_q/glu_s != null: fused SwiGLU + per-group quant epilogue (64-blocked gate_up weights,
@@ -392,9 +393,11 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     if (ag || M > 64 || N % 128 != 0 || glu_mpad < mblocks16 * 16) return -2;
     const int panels = NTt / 8;
     const dim3 grid(((panels + 7) / 8) * 8 * mblocks16);
-    hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<2, 4, 8, false, 1>), grid, dim3(256), 0, st, (const int8_t*)A, sa,
-                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, glu_mpad,
-                       (int8_t*)glu_q, glu_s);
+#define GLU(U) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, 4, 8, false, 1>), grid, dim3(256), 0, st, (const int8_t*)A, \
+                                  sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,      \
+                                  glu_mpad, (int8_t*)glu_q, glu_s)
+    if (g_glu_unroll >= 4) GLU(4); else GLU(2);
+#undef GLU
     return (int)hipGetLastError();
   }
   if (ag && (M > 64 || a_mpad < mblocks16 * 16)) return -2;

@@ -118,3 +118,18 @@ def test_missing_config_exits(tmp_path):
     with pytest.raises(SystemExit) as e:
         combine.main(["--config", str(tmp_path / "nope.yaml")])
     assert e.value.code == 1
+
+
+def test_shipped_configs_parse():
+    """Every YAML under configs/ loads through the reference-compatible config loader."""
+    import glob
+    import os
+    from edgellm.config import load_config
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs")
+    paths = sorted(glob.glob(os.path.join(root, "*.yaml")))
+    assert len(paths) >= 4
+    for p in paths:
+        cfg = load_config(p)
+        assert cfg["top_k"] == 50 and cfg.sampling.max_new_tokens > 0, p
+    ns = load_config(os.path.join(root, "north_star.yaml"))
+    assert ns.merge == "vote" and len(ns.agents) == 3 and ns.agents[0].gpus == [0, 1]

@@ -96,6 +96,7 @@ def _stall_worker(rank, world, port, marker):
 
     def fault(t):  # rank 1 hangs at tick 3 (a dead peer); rank 0's watchdog must fire
         if rank == 1 and t == 3:
+            wd.stop()           # a hung/dead process reports nothing itself
             _t.sleep(30)
             os._exit(0)
 

@@ -46,9 +46,11 @@ def timeit(fn, iters=50, warm=3, per_graph=20):
     return ts[len(ts) // 2] * 1e3 / per_graph  # median us per call
 
 
-def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True):
-    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
-              "lm_head_int8": (32000, 4096)}
+def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True, grouped=False, shapes=None):
+    """Cache-cold INT8 GEMV sweep.  ``grouped``: per-(token, 64-column) activation scales (the
+    decode o/down projections after the fused producers)."""
+    shapes = shapes or {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
+                        "lm_head_int8": (32000, 4096)}
     out = []
     variants = [(0, 0, 0)]
     if sweep:
@@ -62,7 +64,8 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True):
         sw = torch.rand(N, device=dev) * 0.01
         for M in Ms:
             qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-            sx = torch.rand(M, device=dev) * 0.01
+            sx = (torch.rand((K + 63) // 64, (M + 15) // 16 * 16, device=dev) if grouped
+                  else torch.rand(M, device=dev)) * 0.01
             res = {}
             ctr = [0]
 
@@ -83,9 +86,41 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True):
             best = min(res, key=lambda k: min(res[k]))
             auto = min(res[(0, 0, 0)])
             nbytes = N * K + M * K + M * N * 2
-            out.append(dict(op="w8a8_gemv", shape=name, M=M, N=N, K=K, auto_us=round(auto, 2),
+            out.append(dict(op="w8a8_gemv" + ("_grouped" if grouped else ""), shape=name, M=M, N=N, K=K,
+                            auto_us=round(auto, 2),
                             auto_TBps=round(nbytes / auto / 1e6, 2), best=list(best),
                             best_us=round(min(res[best]), 2), best_TBps=round(nbytes / min(res[best]) / 1e6, 2)))
+            print(out[-1], flush=True)
+    return out
+
+
+def glu_rows(C, dev, Ms=(1, 16, 64)):
+    """Fused gate_up + SwiGLU + per-group quant GEMV (Llama-2-7B: F = 11008), cache-cold."""
+    out = []
+    N, K = 2 * 11008, 4096
+    ncopy = max(2, (1 << 30) // (N * K) + 1)
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+    wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+    sw = torch.rand(N, device=dev) * 0.01
+    for M in Ms:
+        qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        sx = torch.rand(M, device=dev) * 0.01
+        ctr = [0]
+
+        def call():
+            ctr[0] = (ctr[0] + 1) % ncopy
+            return C.w8a8_gemm_glu(qx, sx, wps[ctr[0]], sw, None, N, K)
+
+        res = {}
+        for rnd in range(2):
+            for u in (2, 4):
+                C.tune("glu", u, 0)
+                res.setdefault(u, []).append(timeit(call, iters=10, per_graph=ncopy))
+        C.tune("glu", 0, 0)
+        nbytes = N * K + M * K + M * N // 2
+        for u, ts in res.items():
+            out.append(dict(op="w8a8_glu", M=M, N=N, K=K, unroll=u, us=round(min(ts), 2),
+                            TBps=round(nbytes / min(ts) / 1e6, 2)))
             print(out[-1], flush=True)
     return out
 
@@ -186,12 +221,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
-    ap.add_argument("--only", default=None, help="comma list of: gemv,attn,small,sample,prefill")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,small,sample,prefill")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
     C = ops.ext()
     rows = gemv_rows(C, dev, sweep=not a.no_sweep) if only is None or "gemv" in only else []
+    if only is None or "grouped" in only:
+        rows += gemv_rows(C, dev, sweep=not a.no_sweep, grouped=True,
+                          shapes={"o": (4096, 4096), "down": (4096, 11008)})
+    if only is None or "glu" in only:
+        rows += glu_rows(C, dev)
     rows += other_rows(C, dev, only)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
