@@ -40,6 +40,8 @@ int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* 
 void edge_w8a8_gemv_config(int nw, int unroll);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_glu_unroll(int u);
+void edge_w8a8_splitk(int s);
+void edge_w8a8_skew(int m);
 void edge_decode_attn_config(int target_wg);
 }
 
@@ -426,6 +428,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "glu") edge_w8a8_glu_unroll((int)a);
+    else if (what == "splitk") edge_w8a8_splitk((int)a);
+    else if (what == "skew") edge_w8a8_skew((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });

@@ -66,7 +66,7 @@ template <int MT, int UNROLL, int NW, bool AG>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                             const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                            int M, int N, int K, int KT, int Mpad) {
+                                                            int M, int N, int K, int KT, int Mpad, int skew_mul) {
   __shared__ v4i red[NW][MT][64];
   const int nt = blockIdx.x;
   const int m0 = blockIdx.y * (16 * MT);
@@ -89,18 +89,22 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
   }
   const bool k16 = (K % 16) == 0;
 
+  // workgroups start their K walk at different k-tiles so concurrent panel reads spread over
+  // HBM channels instead of all hitting the same offset of their 64 KiB-aligned panels
+  const int skew = (int)(((unsigned)nt * (unsigned)skew_mul) % (unsigned)KT);
+  auto kmap = [&](int kl) { return kl < KT ? (kl + skew < KT ? kl + skew : kl + skew - KT) : KT; };
   for (int kt = wave; kt < KT; kt += NW * UNROLL) {
     v4i b[UNROLL];
     v4i a[UNROLL][MT];
     v4f sg[UNROLL][MT];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
+      const int k = kmap(kt + u * NW);
       b[u] = (k < KT) ? __builtin_nontemporal_load(wp + (size_t)k * 64) : v4i{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
+      const int k = kmap(kt + u * NW);
       const int kk = k * 64 + akc;
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -152,29 +156,50 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
 // so with NTW = 1 the kernel moves twice the bytes it must).
 // For M > 16 every 16-row block is its own workgroup; the block order is XCD-grouped: dispatch
 // ids b, b+8, b+16, ... land on one XCD, so the MB row blocks of a weight panel are consecutive
-// ids within one XCD (id = xcd + 8 * (mb + MB * panel_group)) and re-read the panel from that
-// XCD's L2 instead of HBM (placement is a speed assumption only, never a correctness one).
+// ids within one XCD (id = xcd + 8 * (ks + S * (mb + MB * panel_group))) and re-read the panel
+// from that XCD's L2 instead of HBM (placement is a speed assumption only, never a correctness one).
+//
+// Split-K (S > 1): a CU streams at most ~22 GB/s, so a grid with fewer workgroups than CUs
+// cannot reach HBM speed.  S workgroups share a panel, each reducing K/S k-tiles and storing
+// its partial tiles to its own scratch slot; an agent-scope acquire-release counter picks the
+// last workgroup of the panel, which sums the S slots in split order (deterministic, also for
+// the float AG accumulators), resets the counter for the next launch / graph replay, and runs
+// the epilogue.
 //
 // EPI 1 (fused SwiGLU + quant, decode MLP): the gate_up weight rows are packed 64-blocked
 // ([gate f0..f0+63 | up f0..f0+63] per 128 rows), so one 8-tile panel holds both halves of 64
 // features.  Waves 0-3 each pair gate tile w with up tile w+4, round both to bf16 (as the
 // unfused GEMM output would be), form silu(g)*u, and the panel writes int8 h with one scale per
 // (token, 64 features) — exactly the per-group input the down projection's AG mode reads.
+typedef uint64_t v2u64 __attribute__((ext_vector_type(2)));
+
+struct SplitK {
+  int S;
+  v4i* part;     // [panels * MB][S][NTW][64 lanes] partial tiles (int32, AG: float bits)
+  int* cnt;      // [panels * MB], zero between launches
+};
+
 template <int UNROLL, int NW, int NTW, bool AG, int EPI>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                 const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                 const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                                 int M, int N, int K, int KT, int NTt, int Mpad,
-                                                                int8_t* __restrict__ hq, float* __restrict__ hs) {
+                                                                int8_t* __restrict__ hq, float* __restrict__ hs,
+                                                                SplitK sk, int skew_mul) {
   static_assert(EPI == 0 || (NTW == 8 && NW >= 4 && !AG), "GLU epilogue: 8-tile panels, >= 4 waves");
+  // tiles owned by a wave in the epilogue: EPI 0 -> wave, wave + NW, ...; EPI 1 -> wave, wave + 4
+  constexpr int OWN = EPI == 1 ? 2 : (NTW + NW - 1) / NW;
   __shared__ v4i red[NW][NTW][64];
   __shared__ float gmax[4][16];
-  const int MB = (M + 15) / 16;
+  __shared__ int last_flag;
+  const int MB = (M + 15) / 16, S = sk.S;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, r = bid >> 3;
-  const int mb = r % MB, panel = xcd + 8 * (r / MB);
+  const int ks = r % S, r2 = r / S;
+  const int mb = r2 % MB, panel = xcd + 8 * (r2 / MB);
   const int nt0 = panel * NTW;
   if (nt0 >= NTt) return;                                   // grid padded to a multiple of 8 panels
+  const int kt_begin = (int)((int64_t)KT * ks / S), kt_end = (int)((int64_t)KT * (ks + 1) / S);
   const int m0 = mb * 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int arow = m0 + (lane & 15), akc = 16 * (lane >> 4);
@@ -192,24 +217,31 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
   const int8_t* arow_p = A + (size_t)(aval ? arow : 0) * K;
   const bool k16 = (K % 16) == 0;
 
-  for (int kt = wave; kt < KT; kt += NW * UNROLL) {
+  const int klen = kt_end - kt_begin;
+  const int skew = klen > 0 ? (int)(((unsigned)(panel * 8 + mb) * (unsigned)skew_mul) % (unsigned)klen) : 0;
+  auto kmap = [&](int kl) {
+    if (kl >= kt_end) return kt_end;
+    const int o = kl - kt_begin + skew;
+    return kt_begin + (o < klen ? o : o - klen);
+  };
+  for (int kt = kt_begin + wave; kt < kt_end; kt += NW * UNROLL) {
     v4i b[UNROLL][NTW];
     v4i a[UNROLL];
     v4f sg[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
+      const int k = kmap(kt + u * NW);
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
-        b[u][j] = (k < KT) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
+        b[u][j] = (k < kt_end) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
+      const int k = kmap(kt + u * NW);
       const int kk = k * 64 + akc;
-      if constexpr (AG) sg[u] = group_scales(sa, k, KT, Mpad, m0 + 4 * (lane >> 4));
-      if (aval && k < KT && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
-      else if (aval && k < KT && kk < K) {
+      if constexpr (AG) sg[u] = group_scales(sa, k < kt_end ? k : KT, KT, Mpad, m0 + 4 * (lane >> 4));
+      if (aval && k < kt_end && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
+      else if (aval && k < kt_end && kk < K) {
         int8_t t[16];
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) t[jj] = (kk + jj < K) ? arow_p[kk + jj] : 0;
@@ -230,37 +262,100 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
     else red[wave][j][lane] = acc[j];
   }
   __syncthreads();
-  if constexpr (EPI == 0) {
-    for (int j = wave; j < NTW; j += NW) {
-      if (nt0 + j >= NTt) continue;
-      const int col = (nt0 + j) * 16 + (lane & 15);
+
+  // ---- per-tile totals of this workgroup for the tiles this wave owns
+  v4i tot[OWN];
+  int tile[OWN];
+#pragma unroll
+  for (int o = 0; o < OWN; ++o) {
+    tile[o] = EPI == 1 ? (wave < 4 ? wave + 4 * o : NTW) : wave + NW * o;
+    tot[o] = v4i{0, 0, 0, 0};
+    if (tile[o] < NTW) {
       if constexpr (AG) {
-        v4f s = __builtin_bit_cast(v4f, red[0][j][lane]);
+        v4f f = __builtin_bit_cast(v4f, red[0][tile[o]][lane]);
 #pragma unroll
-        for (int w = 1; w < NW; ++w) s += __builtin_bit_cast(v4f, red[w][j][lane]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) store_out_f(out, M, N, m0 + 4 * (lane >> 4) + q, col, s[q], sw, bias);
+        for (int w = 1; w < NW; ++w) f += __builtin_bit_cast(v4f, red[w][tile[o]][lane]);
+        tot[o] = __builtin_bit_cast(v4i, f);
       } else {
-        v4i s = red[0][j][lane];
+        v4i t = red[0][tile[o]][lane];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) s += red[w][j][lane];
+        for (int w = 1; w < NW; ++w) t += red[w][tile[o]][lane];
+        tot[o] = t;
+      }
+    }
+  }
+  // ---- split-K: publish this split's partials; the last workgroup of the panel continues.
+  // Partials go out as device-scope atomic stores (coherent across XCDs without an L2
+  // writeback); each wave waits for its stores to complete before the barrier, then one relaxed
+  // device-scope counter increment elects the last workgroup, which reads the partials back with
+  // device-scope atomic loads.  (An agent-scope release/acquire fence here writes back the whole
+  // L2 per workgroup and costs 5-6x the GEMV itself.)
+  if (S > 1) {
+    const size_t pbase = (size_t)(panel * MB + mb) * S;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) store_out(out, M, N, m0 + 4 * (lane >> 4) + q, col, s[q], sa, sw, bias);
+    for (int o = 0; o < OWN; ++o) {
+      if (tile[o] >= NTW) continue;
+      uint64_t* p = reinterpret_cast<uint64_t*>(sk.part + ((pbase + ks) * NTW + tile[o]) * 64 + lane);
+      const uint64_t* v = reinterpret_cast<const uint64_t*>(&tot[o]);
+      __hip_atomic_store(p, v[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, v[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int* c = sk.cnt + panel * MB + mb;
+      const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = prev == S - 1;
+      if (prev == S - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_flag) return;
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      if (tile[o] >= NTW) continue;
+      v4i parts[8];
+      for (int k2 = 0; k2 < S; k2 += 8) {
+        const int nk = min(8, S - k2);
+        for (int i = 0; i < nk; ++i) {      // issue up to 8 slot loads before summing
+          const uint64_t* p = reinterpret_cast<const uint64_t*>(sk.part + ((pbase + k2 + i) * NTW + tile[o]) * 64 + lane);
+          uint64_t lo = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint64_t hi = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          parts[i] = __builtin_bit_cast(v4i, (v2u64){lo, hi});
+        }
+        for (int i = 0; i < nk; ++i) {
+          if constexpr (AG) {
+            v4f f = k2 + i == 0 ? v4f{0.f, 0.f, 0.f, 0.f} : __builtin_bit_cast(v4f, tot[o]);
+            tot[o] = __builtin_bit_cast(v4i, f + __builtin_bit_cast(v4f, parts[i]));
+          } else {
+            tot[o] = (k2 + i == 0 ? v4i{0, 0, 0, 0} : tot[o]) + parts[i];
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (EPI == 0) {
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      if (tile[o] >= NTW || nt0 + tile[o] >= NTt) continue;
+      const int col = (nt0 + tile[o]) * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + 4 * (lane >> 4) + q;
+        if constexpr (AG) store_out_f(out, M, N, row, col, __builtin_bit_cast(v4f, tot[o])[q], sw, bias);
+        else store_out(out, M, N, row, col, tot[o][q], sa, sw, bias);
       }
     }
   } else {
     const int F = N / 2;
     float h[4];
     if (wave < 4) {
-      v4i sgt = red[0][wave][lane], sut = red[0][wave + 4][lane];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) { sgt += red[w][wave][lane]; sut += red[w][wave + 4][lane]; }
       const int gcol = (nt0 + wave) * 16 + (lane & 15), ucol = (nt0 + 4 + wave) * 16 + (lane & 15);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = m0 + 4 * (lane >> 4) + q;
         const float s_a = row < M ? sa[row] : 0.f;
-        float g = (float)sgt[q] * s_a * sw[gcol], u = (float)sut[q] * s_a * sw[ucol];
+        float g = (float)tot[0][q] * s_a * sw[gcol], u = (float)tot[1][q] * s_a * sw[ucol];
         if (bias) { g += bf2f(bias[gcol]); u += bf2f(bias[ucol]); }
         g = bf2f(f2bf(g));
         u = bf2f(f2bf(u));
@@ -373,11 +468,54 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 }
 }  // namespace
 
-static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0;
+static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0, g_splitk = 0, g_skew = 37;
 // tuning hook (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
 extern "C" void edge_w8a8_glu_unroll(int u) { g_glu_unroll = u; }
+extern "C" void edge_w8a8_splitk(int s) { g_splitk = s; }
+extern "C" void edge_w8a8_skew(int m) { g_skew = m; }
+
+// Split-K scratch: one per device, allocated (and its counters zeroed) on first use outside a
+// graph capture; every launch leaves the counters at zero again.
+namespace {
+constexpr size_t kPartBytes = 16u << 20;
+constexpr int kCounters = 1 << 16;
+struct Scratch { v4i* part = nullptr; int* cnt = nullptr; };
+Scratch g_scratch[64];
+
+Scratch* scratch(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  Scratch& s = g_scratch[dev];
+  if (s.part != nullptr) return &s;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  void *p = nullptr, *c = nullptr;
+  if (hipMalloc(&p, kPartBytes) != hipSuccess) return nullptr;
+  if (hipMalloc(&c, kCounters * sizeof(int)) != hipSuccess || hipMemset(c, 0, kCounters * sizeof(int)) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  s.part = (v4i*)p;
+  s.cnt = (int*)c;
+  return &s;
+}
+
+// Split count: opt-in (tune "splitk").  Measured on MI355X (Llama-2-7B decode shapes, M = 16)
+// the partial-tile handoff on the last workgroup's critical path costs more than the extra CUs
+// return (GLU 23.6 -> 29.2 us at S = 2, down 13.1 -> 16.3 us at S = 8), so the default is S = 1.
+SplitK choose_split(int groups, int KT, int nw, int ntw, hipStream_t st) {
+  (void)KT; (void)nw;
+  const int S = g_splitk > 0 ? g_splitk : 1;
+  if (S > 1) {
+    Scratch* sc = scratch(st);
+    if (sc != nullptr && (size_t)groups * S * ntw * 1024 <= kPartBytes && groups <= kCounters)
+      return SplitK{S, sc->part, sc->cnt};
+  }
+  return SplitK{1, nullptr, nullptr};
+}
+}  // namespace
 
 // sa: per-token [M] (a_mpad == 0) or per-group [KT][a_mpad] (a_mpad > 0, GEMV shapes only).
 // glu_q/glu_s != null: fused SwiGLU + per-group quant epilogue (64-blocked gate_up weights,
@@ -391,11 +529,12 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   const int mblocks16 = (M + 15) / 16;
   if (glu_q != nullptr) {
     if (ag || M > 64 || N % 128 != 0 || glu_mpad < mblocks16 * 16) return -2;
-    const int panels = NTt / 8;
-    const dim3 grid(((panels + 7) / 8) * 8 * mblocks16);
+    const int groups = ((NTt / 8 + 7) / 8) * 8 * mblocks16;
+    const SplitK sk = choose_split(groups, KT, 4, 8, st);
+    const dim3 grid(groups * sk.S);
 #define GLU(U) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, 4, 8, false, 1>), grid, dim3(256), 0, st, (const int8_t*)A, \
                                   sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,      \
-                                  glu_mpad, (int8_t*)glu_q, glu_s)
+                                  glu_mpad, (int8_t*)glu_q, glu_s, sk, g_skew)
     if (g_glu_unroll >= 4) GLU(4); else GLU(2);
 #undef GLU
     return (int)hipGetLastError();
@@ -408,15 +547,26 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
                        (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_n);
     return (int)hipGetLastError();
   }
-  // waves per workgroup: enough that every wave owns >= 2 k-tiles, at most 16
+  // Defaults from the graph-timed cache-cold sweeps on MI355X (profiles/bench_ops_*.json):
+  //   M <= 2 : one n-tile per workgroup, unroll 4 (2 with grouped scales), waves by K
+  //   M <= 16: unroll 2; N >= 16K columns: 2 n-tiles x 4 waves; 8K..16K: 4 n-tiles x 8 waves;
+  //            smaller N: 1 n-tile, 16 waves (K <= 8K) or 8 waves (larger K)
+  //   M in (16, 64]: 4 n-tiles per workgroup (activation fragments amortised)
+  int un = g_gemv_unroll > 0 ? g_gemv_unroll : (M <= 2 && !ag ? 4 : 2);
+  int ntw = 1;
+  if (g_gemv_ntw > 0) ntw = g_gemv_ntw;
+  else if (mblocks16 > 1) ntw = 4;
+  else if (M > 2 && NTt >= 1024) ntw = 2;
+  else if (M > 2 && NTt >= 512) ntw = 4;
   int nw = g_gemv_nw > 0 ? g_gemv_nw : (KT >= 128 ? 16 : (KT >= 32 ? 8 : 4));
+  if (g_gemv_nw <= 0 && M > 2) nw = (NTt >= 1024) ? 4 : (NTt >= 512 ? 8 : (KT >= 128 ? 8 : 16));
 #define GEMV_NW(MT, U, NWV)                                                                                       \
   do {                                                                                                            \
     const dim3 g(NTt, (M + 16 * MT - 1) / (16 * MT));                                                            \
     if (ag) hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV, true>), g, dim3(NWV * 64), 0, st, (const int8_t*)A,  \
-                               sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad); \
+                               sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad, g_skew); \
     else hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV, false>), g, dim3(NWV * 64), 0, st, (const int8_t*)A,    \
-                            sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad);    \
+                            sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad, g_skew); \
   } while (0)
 #define GEMV(MT, U)                                   \
   do {                                                \
@@ -424,28 +574,19 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     else if (nw >= 8) GEMV_NW(MT, U, 8);              \
     else GEMV_NW(MT, U, 4);                           \
   } while (0)
-  // Defaults from the graph-timed sweep on MI355X (profiles/bench_ops_*.json, Llama-2-7B shapes):
-  //   M <= 2 : one n-tile per workgroup, unroll 4, waves by K (6-6.8 TB/s)
-  //   M <= 16: unroll 2; N >= 16K columns: 2 n-tiles x 4 waves; 8K..16K: 4 n-tiles x 8 waves;
-  //            smaller N: 1 n-tile, 16 waves (K <= 8K) or 8 waves (larger K)
-  int un = g_gemv_unroll > 0 ? g_gemv_unroll : (M <= 2 ? 4 : 2);
-  int ntw = 1;
-  if (g_gemv_ntw > 0) ntw = g_gemv_ntw;
-  else if (mblocks16 > 1) ntw = 4;                   // M in (16, 64]: amortise A over 4 n-tiles
-  else if (M > 2 && NTt >= 1024) ntw = 2;
-  else if (M > 2 && NTt >= 512) ntw = 4;
-  if (g_gemv_nw <= 0 && M > 2) nw = (NTt >= 1024) ? 4 : (NTt >= 512 ? 8 : (KT >= 128 ? 8 : 16));
   if (ntw > 1) {
-    // XCD-grouped 1-D grid: panels padded to a multiple of 8, one workgroup per (panel, 16-row block)
+    // XCD-grouped 1-D grid: panels padded to a multiple of 8, S workgroups per (panel, 16-row block)
+    const int groups = ((NTt + ntw - 1) / ntw + 7) / 8 * 8 * mblocks16;
+    const SplitK sk = choose_split(groups, KT, nw, ntw, st);
 #define NTWL(U, NWV, NTWV)                                                                                           \
   do {                                                                                                               \
-    const dim3 g(((NTt + NTWV - 1) / NTWV + 7) / 8 * 8 * mblocks16);                                                 \
+    const dim3 g(groups * sk.S);                                                                                     \
     if (ag) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, true, 0>), g, dim3(NWV * 64), 0, st,              \
                                (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N,  \
-                               K, KT, NTt, a_mpad, nullptr, nullptr);                                                \
+                               K, KT, NTt, a_mpad, nullptr, nullptr, sk, g_skew);                                    \
     else hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, false, 0>), g, dim3(NWV * 64), 0, st,                \
                             (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K,  \
-                            KT, NTt, a_mpad, nullptr, nullptr);                                                      \
+                            KT, NTt, a_mpad, nullptr, nullptr, sk, g_skew);                                          \
   } while (0)
 #define NTWN(NWV)                                                   \
   do {                                                              \
@@ -459,8 +600,9 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
 #undef NTWL
     return (int)hipGetLastError();
   }
-  if (mblocks16 <= 1) { if (un >= 8) GEMV(1, 8); else if (un >= 4) GEMV(1, 4); else GEMV(1, 2); }
-  else if (mblocks16 <= 2) { if (un >= 4) GEMV(2, 4); else GEMV(2, 2); }
+  const int mblocks = mblocks16;
+  if (mblocks <= 1) { if (un >= 8) GEMV(1, 8); else if (un >= 4) GEMV(1, 4); else GEMV(1, 2); }
+  else if (mblocks <= 2) { if (un >= 4) GEMV(2, 4); else GEMV(2, 2); }
   else GEMV(4, 2);
 #undef GEMV
 #undef GEMV_NW

@@ -106,3 +106,45 @@ def test_act_blocked_glu(cuda, F):
     qr, sr = _ref.silu_mul_quant(_ref.unblock_glu(x))
     _close(s, sr, 0, 2e-3)
     assert (q.int() - qr.int()).abs().max().item() <= 1
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 8])
+@pytest.mark.parametrize("grouped", [False, True])
+@pytest.mark.parametrize("M,N,K", [(16, 4096, 4096), (7, 12288, 4096), (40, 4096, 11008), (16, 1040, 1024)])
+def test_gemv_split_k(cuda, S, grouped, M, N, K):
+    """Split-K partial tiles + last-workgroup epilogue: same answer for every split count, and
+    repeated launches (counters reset by the kernel itself) are bit-identical."""
+    C = ops.ext()
+    torch.manual_seed(S)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = (torch.rand(K // 64, (M + 15) // 16 * 16, device=cuda) if grouped else torch.rand(M, device=cuda)) * 0.02
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.02 + 1e-3
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("splitk", S, 0)
+        outs = [C.w8a8_gemm(qx, sx, wp, sw, None, N, K) for _ in range(3)]
+    finally:
+        C.tune("splitk", 0, 0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    _close(outs[0], _ref.w8a8_linear(qx, sx, w, sw, None, torch.float32), 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("S", [1, 2, 4])
+def test_glu_split_k(cuda, S):
+    C = ops.ext()
+    M, F, K = 16, 11008, 4096
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (2 * F, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
+    wp, swb = ops.pack_int8_weight(_ref.block_glu_rows(w)), _ref.block_glu_rows(sw)
+    C.tune("splitk", 1, 0)
+    base = C.w8a8_gemm_glu(qx, sx, wp, swb, None, 2 * F, K)
+    try:
+        C.tune("splitk", S, 0)
+        got = [C.w8a8_gemm_glu(qx, sx, wp, swb, None, 2 * F, K) for _ in range(2)]
+    finally:
+        C.tune("splitk", 0, 0)
+    for hq, hs in got:                         # integer partial sums: split count cannot matter
+        assert torch.equal(hq, base[0]) and torch.equal(hs, base[1])

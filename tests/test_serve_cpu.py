@@ -123,3 +123,13 @@ def test_stage_server_replays_retried_step():
     a = st.forward(m)
     b = st.forward(m)          # same (seq, step): served from the replay cache
     assert a == b and st.replays == 1
+
+
+def test_client_cli_prints_remote_time(capsys):
+    from edgellm.cli.client import main
+    server = make_server(port=0, host="127.0.0.1")
+    try:
+        t = main(["--address", f"127.0.0.1:{server.port}", "--timeout", "5"])
+        assert TIME_RE.match(t) and f"Current Time from 127.0.0.1:{server.port}: {t}" in capsys.readouterr().out
+    finally:
+        server.stop(0)
