@@ -18,54 +18,69 @@ from ..utils.log import get_logger
 log = get_logger("serve")
 
 
-def main(argv: Optional[List[str]] = None):
-    ap = argparse.ArgumentParser(description=__doc__)
+def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--grpc-port", type=int, default=50051)
     ap.add_argument("--rest-port", type=int, default=8000)
     ap.add_argument("--no-rest", action="store_true")
     ap.add_argument("--model", default=None, help="attach a generation engine (preset, tiny:<arch> or HF dir)")
+    ap.add_argument("--precision", default="bf16", help="bf16 | fp16 | fp32 (GPU always computes in bf16)")
     ap.add_argument("--quant", default="none")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--base_model_path", default=None)
     ap.add_argument("--max-batch", type=int, default=8)
     ap.add_argument("--max-seq", type=int, default=2048)
     ap.add_argument("--stage", default=None, help="first:last — serve these layers as a gRPC pipeline stage")
-    args = ap.parse_args(argv)
+    return ap.parse_args(argv)
 
+
+def build(args: argparse.Namespace):
+    """Create (started gRPC server, bound port, FastAPI app or None, serving engine or None)."""
     import torch
+    import grpc
+    from concurrent import futures
     from ..serve.time_service import time_service_handler
     device = args.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
-    engine = None
-    extra = []
+    engine, extra = None, []
     if args.model and args.stage:
         from ..models.registry import load_model
         from ..serve.stage_service import StageServer
         a, b = (int(x) for x in args.stage.split(":"))
-        model, _, src = load_model(args.model, "bf16", args.quant, device, first=a, last=b)
+        model, _, src = load_model(args.model, args.precision, args.quant, device, base_dir=args.base_model_path,
+                                   first=a, last=b)
         extra.append(StageServer(model, max_seq=args.max_seq).handler())
         log.info(f"stage layers [{a}, {b}) of {src}")
     elif args.model:
         from ..engine import Generator
         from ..models.registry import load_model
         from ..serve.server import ServingEngine
-        model, tok, src = load_model(args.model, "bf16", args.quant, device)
+        model, tok, src = load_model(args.model, args.precision, args.quant, device, base_dir=args.base_model_path)
         engine = ServingEngine(Generator(model, max_batch=args.max_batch, max_seq=args.max_seq), tok, args.max_batch)
         log.info(f"generation engine: {src}")
-
-    import grpc
-    from concurrent import futures
-    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10))
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10),           # server.py:14
+                         options=[("grpc.max_receive_message_length", 256 << 20),
+                                  ("grpc.max_send_message_length", 256 << 20)])
     server.add_generic_rpc_handlers((time_service_handler(), *extra))
-    server.add_insecure_port(f"[::]:{args.grpc_port}")
+    port = server.add_insecure_port(f"[::]:{args.grpc_port}")
     server.start()
-    print(f"gRPC Server running on port {args.grpc_port}...")
-    if args.no_rest:
+    app = None
+    if not args.no_rest:
+        from ..serve.rest import make_app
+        app = make_app(engine)
+    return server, port, app, engine
+
+
+def main(argv: Optional[List[str]] = None):
+    args = parse(argv)
+    server, port, app, _ = build(args)
+    print(f"gRPC Server running on port {port}...")
+    if app is None:
         server.wait_for_termination()
         return
-    from ..serve.rest import make_app
     import uvicorn
     threading.Thread(target=server.wait_for_termination, daemon=True).start()
-    uvicorn.run(make_app(engine), host=args.host, port=args.rest_port)
+    uvicorn.run(app, host=args.host, port=args.rest_port)
 
 
 if __name__ == "__main__":

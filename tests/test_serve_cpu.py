@@ -133,3 +133,29 @@ def test_client_cli_prints_remote_time(capsys):
         assert TIME_RE.match(t) and f"Current Time from 127.0.0.1:{server.port}: {t}" in capsys.readouterr().out
     finally:
         server.stop(0)
+
+
+def test_serve_cli_stage_and_engine():
+    """cli.serve builds a stage server that an EdgePipeline drives, and an engine-backed REST app."""
+    from fastapi.testclient import TestClient
+    from edgellm.cli.serve import build, parse
+    from edgellm.models.registry import load_model
+    server, port, app, engine = build(parse(["--model", "tiny:gpt2", "--stage", "1:2", "--grpc-port", "0",
+                                             "--no-rest", "--precision", "fp32", "--device", "cpu"]))
+    try:
+        first, _, _ = load_model("tiny:gpt2", "fp32", "none", "cpu", first=0, last=1)
+        full, _, _ = load_model("tiny:gpt2", "fp32", "none", "cpu")
+        pipe = EdgePipeline(first, [RemoteStage(f"127.0.0.1:{port}", timeout=10)], max_seq=64)
+        sp = SamplingParams(max_new_tokens=5, do_sample=False)
+        assert pipe.generate([[3, 4, 5]], sp).tokens == Generator(full, max_batch=1, max_seq=64).generate([[3, 4, 5]], sp).tokens
+        assert get_current_time(f"127.0.0.1:{port}", timeout=5)       # TimeService rides along
+    finally:
+        server.stop(0)
+    server, port, app, engine = build(parse(["--model", "tiny:llama", "--grpc-port", "0", "--precision", "fp32",
+                                             "--device", "cpu", "--max-seq", "128"]))
+    try:
+        r = TestClient(app).post("/generate", json={"prompt_ids": [1, 2, 3], "max_new_tokens": 4, "do_sample": False})
+        assert r.status_code == 200 and len(r.json()["tokens"]) == 4
+    finally:
+        engine.close()
+        server.stop(0)
