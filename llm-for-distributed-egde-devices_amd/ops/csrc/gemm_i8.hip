@@ -66,7 +66,7 @@ template <int MT, int UNROLL, int NW, bool AG>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                             const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                            int M, int N, int K, int KT, int Mpad, int skew_mul) {
+                                                            int M, int N, int K, int KT, int Mpad) {
   __shared__ v4i red[NW][MT][64];
   const int nt = blockIdx.x;
   const int m0 = blockIdx.y * (16 * MT);
@@ -89,22 +89,18 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const int8_t* __rest
   }
   const bool k16 = (K % 16) == 0;
 
-  // workgroups start their K walk at different k-tiles so concurrent panel reads spread over
-  // HBM channels instead of all hitting the same offset of their 64 KiB-aligned panels
-  const int skew = (int)(((unsigned)nt * (unsigned)skew_mul) % (unsigned)KT);
-  auto kmap = [&](int kl) { return kl < KT ? (kl + skew < KT ? kl + skew : kl + skew - KT) : KT; };
   for (int kt = wave; kt < KT; kt += NW * UNROLL) {
     v4i b[UNROLL];
     v4i a[UNROLL][MT];
     v4f sg[UNROLL][MT];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kmap(kt + u * NW);
+      const int k = kt + u * NW;
       b[u] = (k < KT) ? __builtin_nontemporal_load(wp + (size_t)k * 64) : v4i{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kmap(kt + u * NW);
+      const int k = kt + u * NW;
       const int kk = k * 64 + akc;
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -185,7 +181,7 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
                                                                 const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                                 int M, int N, int K, int KT, int NTt, int Mpad,
                                                                 int8_t* __restrict__ hq, float* __restrict__ hs,
-                                                                SplitK sk, int skew_mul) {
+                                                                SplitK sk) {
   static_assert(EPI == 0 || (NTW == 8 && NW >= 4 && !AG), "GLU epilogue: 8-tile panels, >= 4 waves");
   // tiles owned by a wave in the epilogue: EPI 0 -> wave, wave + NW, ...; EPI 1 -> wave, wave + 4
   constexpr int OWN = EPI == 1 ? 2 : (NTW + NW - 1) / NW;
@@ -217,27 +213,20 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
   const int8_t* arow_p = A + (size_t)(aval ? arow : 0) * K;
   const bool k16 = (K % 16) == 0;
 
-  const int klen = kt_end - kt_begin;
-  const int skew = klen > 0 ? (int)(((unsigned)(panel * 8 + mb) * (unsigned)skew_mul) % (unsigned)klen) : 0;
-  auto kmap = [&](int kl) {
-    if (kl >= kt_end) return kt_end;
-    const int o = kl - kt_begin + skew;
-    return kt_begin + (o < klen ? o : o - klen);
-  };
   for (int kt = kt_begin + wave; kt < kt_end; kt += NW * UNROLL) {
     v4i b[UNROLL][NTW];
     v4i a[UNROLL];
     v4f sg[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kmap(kt + u * NW);
+      const int k = kt + u * NW;
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
         b[u][j] = (k < kt_end) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = kmap(kt + u * NW);
+      const int k = kt + u * NW;
       const int kk = k * 64 + akc;
       if constexpr (AG) sg[u] = group_scales(sa, k < kt_end ? k : KT, KT, Mpad, m0 + 4 * (lane >> 4));
       if (aval && k < kt_end && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
@@ -468,13 +457,12 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 }
 }  // namespace
 
-static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0, g_splitk = 0, g_skew = 37;
+static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0, g_splitk = 0;
 // tuning hook (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
 extern "C" void edge_w8a8_glu_unroll(int u) { g_glu_unroll = u; }
 extern "C" void edge_w8a8_splitk(int s) { g_splitk = s; }
-extern "C" void edge_w8a8_skew(int m) { g_skew = m; }
 
 // Split-K scratch: one per device, allocated (and its counters zeroed) on first use outside a
 // graph capture; every launch leaves the counters at zero again.
@@ -534,7 +522,7 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     const dim3 grid(groups * sk.S);
 #define GLU(U) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, 4, 8, false, 1>), grid, dim3(256), 0, st, (const int8_t*)A, \
                                   sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,      \
-                                  glu_mpad, (int8_t*)glu_q, glu_s, sk, g_skew)
+                                  glu_mpad, (int8_t*)glu_q, glu_s, sk)
     if (g_glu_unroll >= 4) GLU(4); else GLU(2);
 #undef GLU
     return (int)hipGetLastError();
@@ -564,9 +552,9 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   do {                                                                                                            \
     const dim3 g(NTt, (M + 16 * MT - 1) / (16 * MT));                                                            \
     if (ag) hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV, true>), g, dim3(NWV * 64), 0, st, (const int8_t*)A,  \
-                               sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad, g_skew); \
+                               sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad); \
     else hipLaunchKernelGGL((w8a8_gemv_kernel<MT, U, NWV, false>), g, dim3(NWV * 64), 0, st, (const int8_t*)A,    \
-                            sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad, g_skew); \
+                            sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, a_mpad); \
   } while (0)
 #define GEMV(MT, U)                                   \
   do {                                                \
@@ -583,10 +571,10 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     const dim3 g(groups * sk.S);                                                                                     \
     if (ag) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, true, 0>), g, dim3(NWV * 64), 0, st,              \
                                (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N,  \
-                               K, KT, NTt, a_mpad, nullptr, nullptr, sk, g_skew);                                    \
+                               K, KT, NTt, a_mpad, nullptr, nullptr, sk);                                    \
     else hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, false, 0>), g, dim3(NWV * 64), 0, st,                \
                             (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K,  \
-                            KT, NTt, a_mpad, nullptr, nullptr, sk, g_skew);                                          \
+                            KT, NTt, a_mpad, nullptr, nullptr, sk);                                          \
   } while (0)
 #define NTWN(NWV)                                                   \
   do {                                                              \
