@@ -41,6 +41,7 @@ void edge_w8a8_gemv_config(int nw, int unroll);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_glu_unroll(int u);
 void edge_w8a8_splitk(int s);
+void edge_w8a8_gemv_fast(int on);
 void edge_decode_attn_config(int target_wg);
 }
 
@@ -428,6 +429,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "glu") edge_w8a8_glu_unroll((int)a);
     else if (what == "splitk") edge_w8a8_splitk((int)a);
+    else if (what == "gemv_fast") edge_w8a8_gemv_fast((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });

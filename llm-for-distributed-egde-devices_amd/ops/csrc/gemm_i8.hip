@@ -175,7 +175,7 @@ struct SplitK {
   int* cnt;      // [panels * MB], zero between launches
 };
 
-template <int UNROLL, int NW, int NTW, bool AG, int EPI>
+template <int UNROLL, int NW, int NTW, bool AG, int EPI, bool FAST>
 __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                 const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                 const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
@@ -213,37 +213,80 @@ __global__ void __launch_bounds__(NW * 64) w8a8_gemv_ntw_kernel(const int8_t* __
   const int8_t* arow_p = A + (size_t)(aval ? arow : 0) * K;
   const bool k16 = (K % 16) == 0;
 
-  for (int kt = kt_begin + wave; kt < kt_end; kt += NW * UNROLL) {
-    v4i b[UNROLL][NTW];
-    v4i a[UNROLL];
-    v4f sg[UNROLL];
+  if constexpr (FAST) {
+    // K % 64 == 0: every load is unconditional (k-tile and row indices clamped to valid memory;
+    // out-of-range contributions are skipped by wave-uniform guards on the MFMAs) and the next
+    // group of UNROLL k-tiles is prefetched into a second register set before the current
+    // group's MFMAs, so the compiler waits with a counted vmcnt instead of draining every step.
+    const int8_t* ap = A + (size_t)min(arow, M - 1) * K + akc;
+    const int nk = kt_end > kt_begin + wave ? (kt_end - kt_begin - wave + NW - 1) / NW : 0;
+    const int ng = (nk + UNROLL - 1) / UNROLL;
+    const int r0 = m0 + 4 * (lane >> 4);
+    v4i b0[UNROLL][NTW], b1[UNROLL][NTW], a0[UNROLL], a1[UNROLL];
+    v4f s0[UNROLL], s1[UNROLL];
+    auto load = [&](v4i (&b)[UNROLL][NTW], v4i (&a)[UNROLL], v4f (&sg)[UNROLL], int g) {
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
+      for (int u = 0; u < UNROLL; ++u) {
+        const int k = min(kt_begin + wave + (g * UNROLL + u) * NW, kt_end - 1);
 #pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        b[u][j] = (k < kt_end) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
-      const int kk = k * 64 + akc;
-      if constexpr (AG) sg[u] = group_scales(sa, k < kt_end ? k : KT, KT, Mpad, m0 + 4 * (lane >> 4));
-      if (aval && k < kt_end && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
-      else if (aval && k < kt_end && kk < K) {
-        int8_t t[16];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) t[jj] = (kk + jj < K) ? arow_p[kk + jj] : 0;
-        a[u] = *reinterpret_cast<v4i*>(t);
-      } else a[u] = v4i{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        if constexpr (AG) fold(accf[j], mfma_i8(a[u], b[u][j], v4i{0, 0, 0, 0}), sg[u]);
-        else acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
+        for (int j = 0; j < NTW; ++j) b[u][j] = __builtin_nontemporal_load(wp[j] + (size_t)k * 64);
+        a[u] = *reinterpret_cast<const v4i*>(ap + (size_t)k * 64);
+        if constexpr (AG) sg[u] = *reinterpret_cast<const v4f*>(sa + (size_t)k * Mpad + r0);
       }
+    };
+    auto mma = [&](const v4i (&b)[UNROLL][NTW], const v4i (&a)[UNROLL], const v4f (&sg)[UNROLL], int g) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        if (g * UNROLL + u >= nk) break;                        // wave-uniform
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          if constexpr (AG) fold(accf[j], mfma_i8(a[u], b[u][j], v4i{0, 0, 0, 0}), sg[u]);
+          else acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
+        }
+      }
+    };
+    // ping-pong register sets, no copies: the loads of one set stay in flight while the other's
+    // MFMAs run (the final prefetch re-reads the last valid group instead of branching)
+    if (ng > 0) load(b0, a0, s0, 0);
+    for (int g = 0; g < ng; g += 2) {
+      load(b1, a1, s1, min(g + 1, ng - 1));
+      mma(b0, a0, s0, g);
+      load(b0, a0, s0, min(g + 2, ng - 1));
+      mma(b1, a1, s1, g + 1);
+    }
+  } else {
+    for (int kt = kt_begin + wave; kt < kt_end; kt += NW * UNROLL) {
+      v4i b[UNROLL][NTW];
+      v4i a[UNROLL];
+      v4f sg[UNROLL];
+  #pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int k = kt + u * NW;
+  #pragma unroll
+        for (int j = 0; j < NTW; ++j)
+          b[u][j] = (k < kt_end) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
+      }
+  #pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int k = kt + u * NW;
+        const int kk = k * 64 + akc;
+        if constexpr (AG) sg[u] = group_scales(sa, k < kt_end ? k : KT, KT, Mpad, m0 + 4 * (lane >> 4));
+        if (aval && k < kt_end && kk + 16 <= K && k16) a[u] = *reinterpret_cast<const v4i*>(arow_p + kk);
+        else if (aval && k < kt_end && kk < K) {
+          int8_t t[16];
+  #pragma unroll
+          for (int jj = 0; jj < 16; ++jj) t[jj] = (kk + jj < K) ? arow_p[kk + jj] : 0;
+          a[u] = *reinterpret_cast<v4i*>(t);
+        } else a[u] = v4i{0, 0, 0, 0};
+      }
+  #pragma unroll
+      for (int u = 0; u < UNROLL; ++u)
+  #pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          if constexpr (AG) fold(accf[j], mfma_i8(a[u], b[u][j], v4i{0, 0, 0, 0}), sg[u]);
+          else acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
+        }
+    }
   }
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
@@ -457,12 +500,13 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 }
 }  // namespace
 
-static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0, g_splitk = 0;
+static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_glu_unroll = 0, g_splitk = 0, g_gemv_fast = 1;
 // tuning hook (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
 extern "C" void edge_w8a8_glu_unroll(int u) { g_glu_unroll = u; }
 extern "C" void edge_w8a8_splitk(int s) { g_splitk = s; }
+extern "C" void edge_w8a8_gemv_fast(int on) { g_gemv_fast = on; }
 
 // Split-K scratch: one per device, allocated (and its counters zeroed) on first use outside a
 // graph capture; every launch leaves the counters at zero again.
@@ -520,10 +564,12 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     const int groups = ((NTt / 8 + 7) / 8) * 8 * mblocks16;
     const SplitK sk = choose_split(groups, KT, 4, 8, st);
     const dim3 grid(groups * sk.S);
-#define GLU(U) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, 4, 8, false, 1>), grid, dim3(256), 0, st, (const int8_t*)A, \
-                                  sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,      \
-                                  glu_mpad, (int8_t*)glu_q, glu_s, sk)
-    if (g_glu_unroll >= 4) GLU(4); else GLU(2);
+#define GLU(U, FA) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, 4, 8, false, 1, FA>), grid, dim3(256), 0, st,         \
+                                      (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, \
+                                      N, K, KT, NTt, glu_mpad, (int8_t*)glu_q, glu_s, sk)
+    const bool fast = (K % 64 == 0) && g_gemv_fast;
+    if (g_glu_unroll >= 4) { if (fast) GLU(4, true); else GLU(4, false); }
+    else { if (fast) GLU(2, true); else GLU(2, false); }
 #undef GLU
     return (int)hipGetLastError();
   }
@@ -562,24 +608,36 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     else if (nw >= 8) GEMV_NW(MT, U, 8);              \
     else GEMV_NW(MT, U, 4);                           \
   } while (0)
-  if (ntw > 1) {
+  const bool fast = (K % 64 == 0) && g_gemv_fast;
+  if (fast && nw >= 16 && (ntw >= 2 || un >= 4 && ag)) nw = 8;   // 16 waves x multi-tile spills (128-VGPR cap)
+  if (ntw > 1 || fast) {
     // XCD-grouped 1-D grid: panels padded to a multiple of 8, S workgroups per (panel, 16-row block)
     const int groups = ((NTt + ntw - 1) / ntw + 7) / 8 * 8 * mblocks16;
     const SplitK sk = choose_split(groups, KT, nw, ntw, st);
 #define NTWL(U, NWV, NTWV)                                                                                           \
   do {                                                                                                               \
     const dim3 g(groups * sk.S);                                                                                     \
-    if (ag) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, true, 0>), g, dim3(NWV * 64), 0, st,              \
-                               (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N,  \
-                               K, KT, NTt, a_mpad, nullptr, nullptr, sk);                                    \
-    else hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, false, 0>), g, dim3(NWV * 64), 0, st,                \
-                            (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K,  \
-                            KT, NTt, a_mpad, nullptr, nullptr, sk);                                          \
+    if (fast) {                                                                                                      \
+      if (ag) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, true, 0, true>), g, dim3(NWV * 64), 0, st,      \
+                                 (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N,\
+                                 K, KT, NTt, a_mpad, nullptr, nullptr, sk);                                          \
+      else hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, false, 0, true>), g, dim3(NWV * 64), 0, st,        \
+                              (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K,\
+                              KT, NTt, a_mpad, nullptr, nullptr, sk);                                                \
+    } else {                                                                                                         \
+      if (ag) hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, true, 0, false>), g, dim3(NWV * 64), 0, st,     \
+                                 (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N,\
+                                 K, KT, NTt, a_mpad, nullptr, nullptr, sk);                                          \
+      else hipLaunchKernelGGL((w8a8_gemv_ntw_kernel<U, NWV, NTWV, false, 0, false>), g, dim3(NWV * 64), 0, st,       \
+                              (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K,\
+                              KT, NTt, a_mpad, nullptr, nullptr, sk);                                                \
+    }                                                                                                                \
   } while (0)
 #define NTWN(NWV)                                                   \
   do {                                                              \
     if (ntw >= 4) { if (un >= 4) NTWL(4, NWV, 4); else NTWL(2, NWV, 4); } \
-    else { if (un >= 4) NTWL(4, NWV, 2); else NTWL(2, NWV, 2); }   \
+    else if (ntw >= 2) { if (un >= 4) NTWL(4, NWV, 2); else NTWL(2, NWV, 2); } \
+    else { if (un >= 4) NTWL(4, NWV, 1); else NTWL(2, NWV, 1); }   \
   } while (0)
     if (nw >= 16) NTWN(16);
     else if (nw >= 8) NTWN(8);

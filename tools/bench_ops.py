@@ -221,14 +221,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
-    ap.add_argument("--skew", type=int, default=None, help="GEMV k-walk skew multiplier (0 = off)")
+    ap.add_argument("--tune", action="append", default=[], help="name=a[,b] passed to ext().tune (repeatable)")
     ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,small,sample,prefill")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
     C = ops.ext()
-    if a.skew is not None:
-        C.tune("skew", a.skew, 0)
+    for t in a.tune:
+        name, vals = t.split("=")
+        v = [int(x) for x in vals.split(",")] + [0]
+        C.tune(name, v[0], v[1])
     rows = gemv_rows(C, dev, sweep=not a.no_sweep) if only is None or "gemv" in only else []
     if only is None or "grouped" in only:
         rows += gemv_rows(C, dev, sweep=not a.no_sweep, grouped=True,
