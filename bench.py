@@ -54,6 +54,8 @@ def parse(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
+    ap.add_argument("--headinfer-heads", type=int, default=None,
+                    help="HeadInfer: KV heads per layer kept on the GPU, the rest offloaded to pinned host memory")
     return ap.parse_args(argv)
 
 
@@ -96,7 +98,12 @@ def run_single(args):
     t_build = time.perf_counter() - t_build
     B = args.micro_batch
     total_new = args.warmup + args.steps + 2
-    gen = Generator(model, max_batch=B, max_seq=args.prompt_len + total_new + 8, use_graphs=not args.no_graphs)
+    max_seq = args.prompt_len + total_new + 8
+    kv = None
+    if args.headinfer_heads is not None and args.headinfer_heads < cfg.num_kv_heads:
+        from edgellm.offload import HeadInferKV
+        kv = HeadInferKV(cfg, B, max_seq, args.headinfer_heads, device, chunk_size=max(args.prompt_len, 1))
+    gen = Generator(model, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs, kv=kv)
     g = torch.Generator().manual_seed(args.seed)
     prompts = torch.randint(0, cfg.vocab_size, (B, args.prompt_len), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=total_new, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
@@ -147,11 +154,14 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": round(res["value"] / BASELINE_TPS, 2),
         "dtype": "int8" if args.quant != "none" else "bf16",
-        "data": "synthetic (random-init Llama-2-7B weights, SmoothQuant-calibrated on random tokens; random prompts)",
+        "data": f"synthetic (random-init {args.model} weights"
+                + (", SmoothQuant-calibrated on random tokens" if args.quant == "w8a8_smoothquant" else "")
+                + "; random prompts)",
         "config": {"model": args.model, "global_batch": res["global_batch"], "seq_len": args.prompt_len,
                    "parallelism": f"pp{args.gpus}", "quant": args.quant, "micro_batch": args.micro_batch,
                    "micro_batches_in_flight": max(1, args.gpus), "partition": res.get("partition"),
                    "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1",
+                   "headinfer_heads": args.headinfer_heads,
                    "compute": "W8A8 INT8 MFMA GEMMs, bf16 attention/norms, bf16 LM head"},
         "p50_token_latency_ms": round(res["p50"], 4),
         "prefill_tokens_per_s": round(res.get("prefill_tps", 0.0), 1),

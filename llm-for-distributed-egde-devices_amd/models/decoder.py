@@ -95,8 +95,10 @@ class MLP(nn.Module):
 
     def forward(self, x):
         if getattr(self.up, "glu_blocked", False):
-            # W8A8 SwiGLU with 64-blocked gate_up rows: decode-sized batches take the fused
-            # GEMV + SwiGLU + per-group quant epilogue; larger ones the blocked activation kernel
+            # W8A8 SwiGLU with 16-blocked gate_up rows: decode-sized batches take the fused
+            # GEMV + SwiGLU epilogue (int8 h with per-group scales, or bf16 h that the down
+            # projection quantises per group — W8A8Linear.glu); larger ones the blocked
+            # activation kernel
             if isinstance(x, QAct) and x.q.dim() == 2 and x.q.shape[0] <= 64 and x.scale.dim() == 1:
                 return self.down(self.up.glu(x))
             return self.down(act_fn(self.up(x), "silu_glu_blocked", True))

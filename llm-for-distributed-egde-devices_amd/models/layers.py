@@ -25,6 +25,11 @@ class QAct(NamedTuple):
     scale: torch.Tensor
 
 
+class GroupQuantBF16(NamedTuple):
+    """bf16 activation that a W8A8 consumer quantises per (token, 64 columns) on the fly."""
+    x: torch.Tensor
+
+
 class Linear(nn.Module):
     takes_quantized_input = False
 

@@ -92,7 +92,7 @@ _ACT_MODE = {"silu_glu": 0, "gelu_tanh": 1, "gelu": 2, "silu_glu_blocked": 3}
 
 
 def activation(x, act: str):
-    """``silu_glu``: x = [gate | up]; ``silu_glu_blocked``: 64-blocked [gate(64) | up(64)] rows
+    """``silu_glu``: x = [gate | up]; ``silu_glu_blocked``: 16-blocked [gate(16) | up(16)] rows
     (the packing of W8A8 gate_up weights, see quant.linear.W8A8Linear.glu_blocked)."""
     if _gpu(x):
         return ext().act(x, _ACT_MODE[act], False)[0]
@@ -200,16 +200,31 @@ def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Opt
     return out.view(*shp, N)
 
 
-def w8a8_glu(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None):
-    """Fused decode MLP front half: gate_up projection (64-blocked rows, N = 2F) -> silu(g)*u ->
-    int8 with per-(token, 64-feature) scales ``[F/64, Mpad]`` (one launch on GPU, M <= 64)."""
+def w8a8_glu(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,
+             quant: bool = False):
+    """Fused decode MLP front half: gate_up projection (16-blocked rows, N = 2F) -> silu(g) * u
+    (one launch on GPU, M <= 64; gate/up rounded to bf16 as the GEMM output).
+
+    Returns bf16 h [M, F], or with ``quant`` (N % 128 == 0) the int8 per-(token, 64 features)
+    quantisation of h computed in the same kernel: (q [M, F], scales [F/64, Mpad])."""
     if _gpu(qx):
+        if quant:
+            return ext().w8a8_gemm_gluq(qx, x_scale, w_packed, w_scale, bias, N, K)
         return ext().w8a8_gemm_glu(qx, x_scale, w_packed, w_scale, bias, N, K)
     w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
     y = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, torch.bfloat16)
-    h = _ref.unblock_glu(y).float()
-    f = h.shape[-1] // 2
-    return _ref.quant_per_group(torch.nn.functional.silu(h[:, :f]) * h[:, f:])
+    if quant:
+        g, u = _ref.unblock_glu(y).float().chunk(2, dim=-1)
+        return _ref.quant_per_group(torch.nn.functional.silu(g) * u)
+    return _ref.silu_mul(_ref.unblock_glu(y))
+
+
+def quant_per_group(x):
+    """Per-(token, 64 columns) int8: (q [M, K], scales [K/64, Mpad]) — the decode-GEMV input
+    layout (ops/csrc/rowwise.hip::group_quant_kernel on GPU)."""
+    if _gpu(x):
+        return ext().group_quant(x)
+    return _ref.quant_per_group(x)
 
 
 # --------------------------------------------------------------------------- sampling / misc

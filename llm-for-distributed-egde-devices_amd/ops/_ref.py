@@ -62,22 +62,25 @@ def quant_per_group(y: torch.Tensor, group: int = 64) -> Tuple[torch.Tensor, tor
     return q.view(M, K), s
 
 
-def unblock_glu(x: torch.Tensor, block: int = 64) -> torch.Tensor:
-    """64-blocked [gate(64) | up(64)] columns -> [gate | up]."""
+GLU_BLOCK = 16   # gate_up rows packed [gate(16) | up(16)] per 32 rows for the fused decode GLU
+
+
+def unblock_glu(x: torch.Tensor, block: int = GLU_BLOCK) -> torch.Tensor:
+    """Blocked [gate(block) | up(block)] columns -> [gate | up]."""
     M, W = x.shape[:-1], x.shape[-1]
     v = x.reshape(*M, W // (2 * block), 2, block)
     return torch.cat([v[..., 0, :].reshape(*M, W // 2), v[..., 1, :].reshape(*M, W // 2)], -1)
 
 
-def block_glu_rows(w: torch.Tensor, block: int = 64) -> torch.Tensor:
-    """Rows [gate | up] (2F, ...) -> 64-blocked [gate(64) | up(64)] order (inverse of unblock_glu)."""
+def block_glu_rows(w: torch.Tensor, block: int = GLU_BLOCK) -> torch.Tensor:
+    """Rows [gate | up] (2F, ...) -> blocked [gate(block) | up(block)] order (inverse of unblock_glu)."""
     F = w.shape[0] // 2
     g, u = w[:F].reshape(F // block, block, *w.shape[1:]), w[F:].reshape(F // block, block, *w.shape[1:])
     return torch.stack([g, u], 1).reshape(2 * F, *w.shape[1:])
 
 
-def unblock_glu_rows(w: torch.Tensor, block: int = 64) -> torch.Tensor:
-    """Inverse of block_glu_rows: 64-blocked rows -> [gate | up]."""
+def unblock_glu_rows(w: torch.Tensor, block: int = GLU_BLOCK) -> torch.Tensor:
+    """Inverse of block_glu_rows: blocked rows -> [gate | up]."""
     F = w.shape[0] // 2
     v = w.reshape(F // block, 2, block, *w.shape[1:])
     return torch.cat([v[:, 0].reshape(F, *w.shape[1:]), v[:, 1].reshape(F, *w.shape[1:])], 0)

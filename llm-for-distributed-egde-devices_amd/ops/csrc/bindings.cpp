@@ -14,6 +14,7 @@ int edge_norm(const void* x, const void* res, const void* w, const void* b, void
               void* res_out, int rows, int H, float eps, int rms, int quant, hipStream_t st);
 int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant, hipStream_t st);
 int edge_quant(const void* x, void* q, float* s, int rows, int H, hipStream_t st);
+int edge_group_quant(const void* x, void* q, float* s, int M, int K, int Mpad, hipStream_t st);
 int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, hipStream_t st);
 int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st);
 int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, void* q_out, void* k_cache,
@@ -29,7 +30,7 @@ int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, i
                       const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
                       int causal, hipStream_t st);
 int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
-                   int M, int N, int K, int KT, int a_mpad, void* glu_q, float* glu_s, int glu_mpad, hipStream_t st);
+                   float* os, int M, int N, int K, int KT, int a_mode, int Mpad, int epi, hipStream_t st);
 int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, void* workspace, hipStream_t st);
@@ -39,9 +40,7 @@ int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* 
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
 void edge_w8a8_gemv_ntw(int ntw);
-void edge_w8a8_glu_unroll(int u);
 void edge_w8a8_splitk(int s);
-void edge_w8a8_gemv_fast(int on);
 void edge_decode_attn_config(int target_wg);
 }
 
@@ -101,7 +100,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64
   need(x, at::kBFloat16, "x");
   const int64_t W = x.size(-1), R = rows_of(x);
   const int64_t F = (mode == 0 || mode == 3) ? W / 2 : W;
-  TORCH_CHECK(mode != 3 || F % 64 == 0, "blocked GLU needs F % 64 == 0");
+  TORCH_CHECK(mode != 3 || F % 16 == 0, "blocked GLU needs F % 16 == 0");
   auto os = x.sizes().vec();
   os.back() = F;
   at::Tensor y, s;
@@ -315,12 +314,10 @@ int64_t a_scale_mpad(const at::Tensor& sa, int64_t M, int64_t KT) {
   return 0;
 }
 
-void check_w8a8_operands(const at::Tensor& a, const at::Tensor& wp, const at::Tensor& sw,
-                         const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
-  need(a, at::kChar, "a");
+void check_w8a8_operands(const at::Tensor& wp, const at::Tensor& sw, const std::optional<at::Tensor>& bias,
+                         int64_t N, int64_t K) {
   need(wp, at::kChar, "w_packed");
   need(sw, at::kFloat, "w_scale");
-  TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
   TORCH_CHECK(sw.numel() == N);
   TORCH_CHECK(wp.numel() == (N + 15) / 16 * ((K + 63) / 64) * 1024, "packed weight has wrong size");
   if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
@@ -328,36 +325,68 @@ void check_w8a8_operands(const at::Tensor& a, const at::Tensor& wp, const at::Te
 
 at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                      const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
-  check_w8a8_operands(a, wp, sw, bias, N, K);
+  need(a, at::kChar, "a");
+  TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
+  check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = (K + 63) / 64;
   const int64_t mpad = a_scale_mpad(sa, M, KT);
   auto os = a.sizes().vec();
   os.back() = N;
   auto out = at::empty(os, a.options().dtype(at::kBFloat16));
   check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
-                       bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N, (int)K, (int)KT, (int)mpad,
-                       nullptr, nullptr, 0, stream()),
+                       bias ? bias->data_ptr() : nullptr, out.data_ptr(), nullptr, (int)M, (int)N, (int)K, (int)KT,
+                       mpad > 0 ? 1 : 0, (int)mpad, 0, stream()),
         "w8a8_gemm");
   return out;
 }
 
-// gate_up projection (64-blocked rows) fused with silu(g)*u and per-group int8 quantisation:
-// returns (h int8 [M, N/2], scales [N/128, Mpad]).  M <= 64, per-token sa.
-std::tuple<at::Tensor, at::Tensor> w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp,
-                                                 const at::Tensor& sw, const std::optional<at::Tensor>& bias,
-                                                 int64_t N, int64_t K) {
-  check_w8a8_operands(a, wp, sw, bias, N, K);
+// Per-(token, 64 columns) int8 quantisation: (q [M, K], scales [K/64, Mpad]).
+std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 64 == 0, "group_quant needs [M, K] with K % 64 == 0");
+  const int64_t M = x.size(0), K = x.size(1), Mpad = (M + 15) / 16 * 16;
+  auto q = at::empty({M, K}, x.options().dtype(at::kChar));
+  auto s = at::empty({K / 64, Mpad}, x.options().dtype(at::kFloat));
+  check(edge_group_quant(x.data_ptr(), q.data_ptr(), s.data_ptr<float>(), (int)M, (int)K, (int)Mpad, stream()),
+        "group_quant");
+  return {q, s};
+}
+
+// gate_up projection (16-blocked rows) fused with silu(g) * u: returns bf16 h [M, N/2].
+at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
+                         const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  need(a, at::kChar, "a");
+  TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
+  check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = (K + 63) / 64;
-  TORCH_CHECK(M <= 64 && N % 128 == 0, "fused GLU needs M <= 64 and N % 128 == 0");
+  TORCH_CHECK(M <= 64 && N % 32 == 0, "fused GLU needs M <= 64 and N % 32 == 0");
   TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GLU takes per-token activation scales");
-  const int64_t Mpad = (M + 15) / 16 * 16;
-  auto hq = at::empty({M, N / 2}, a.options());
-  auto hs = at::empty({N / 128, Mpad}, a.options().dtype(at::kFloat));
+  auto h = at::empty({M, N / 2}, a.options().dtype(at::kBFloat16));
   check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
-                       bias ? bias->data_ptr() : nullptr, nullptr, (int)M, (int)N, (int)K, (int)KT, 0, hq.data_ptr(),
-                       hs.data_ptr<float>(), (int)Mpad, stream()),
+                       bias ? bias->data_ptr() : nullptr, h.data_ptr(), nullptr, (int)M, (int)N, (int)K, (int)KT, 0,
+                       0, 1, stream()),
         "w8a8_gemm_glu");
-  return {hq, hs};
+  return h;
+}
+
+// As w8a8_gemm_glu, then int8 per-(token, 64 features) quantisation in the same kernel:
+// returns (q int8 [M, N/2], scales [N/128, Mpad]).
+std::tuple<at::Tensor, at::Tensor> w8a8_gemm_gluq(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp,
+                                                  const at::Tensor& sw, const std::optional<at::Tensor>& bias,
+                                                  int64_t N, int64_t K) {
+  need(a, at::kChar, "a");
+  TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
+  check_w8a8_operands(wp, sw, bias, N, K);
+  const int64_t M = rows_of(a), KT = (K + 63) / 64, Mpad = (M + 15) / 16 * 16;
+  TORCH_CHECK(M <= 64 && N % 128 == 0, "quantising GLU needs M <= 64 and N % 128 == 0");
+  TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GLU takes per-token activation scales");
+  auto q = at::empty({M, N / 2}, a.options());
+  auto s = at::empty({N / 128, Mpad}, a.options().dtype(at::kFloat));
+  check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                       bias ? bias->data_ptr() : nullptr, q.data_ptr(), s.data_ptr<float>(), (int)M, (int)N, (int)K,
+                       (int)KT, 0, (int)Mpad, 2, stream()),
+        "w8a8_gemm_gluq");
+  return {q, s};
 }
 
 // ---------------------------------------------------------------------------------- sampler
@@ -422,14 +451,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm", &w8a8_gemm);
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
+  m.def("w8a8_gemm_gluq", &w8a8_gemm_gluq);
+  m.def("group_quant", &group_quant);
   m.def("sample", &sample);
   m.def("sample_timestamps", &sample_timestamps);
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
-    else if (what == "glu") edge_w8a8_glu_unroll((int)a);
     else if (what == "splitk") edge_w8a8_splitk((int)a);
-    else if (what == "gemv_fast") edge_w8a8_gemv_fast((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });

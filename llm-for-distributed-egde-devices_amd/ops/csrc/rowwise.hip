@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(NT) norm_kernel(
 
 // ----------------------------------------------------------------------------- activations
 // MODE 0: silu(gate)*up with input [gate | up] of width 2F; 1: gelu tanh; 2: gelu erf;
-// 3: silu GLU over the 64-blocked [gate(64) | up(64)] layout (F % 64 == 0)
+// 3: silu GLU over the 16-blocked [gate(16) | up(16)] layout (F % 16 == 0)
 template <int NCH, int MODE, bool QUANT>
 __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                  int8_t* __restrict__ yq, float* __restrict__ ys, int F) {
@@ -168,17 +168,17 @@ __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, b
         v[c][j] = g / (1.f + __expf(-g)) * u[c][j];
       }
   } else if constexpr (MODE == 3) {
-    // 64-blocked GLU layout (gate_up weights packed for the fused decode epilogue): feature e's
-    // gate sits at (e/64)*128 + e%64 and its up 64 columns later
+    // 16-blocked GLU layout (gate_up weights packed for the fused decode epilogue): feature e's
+    // gate sits at (e/16)*32 + e%16 and its up 16 columns later
     const bf16_t* xr = x + row * (size_t)(2 * F);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int e = (c * NT + threadIdx.x) * 8;
       if (e < F) {
-        const bf16_t* g = xr + (e >> 6) * 128 + (e & 63);
+        const bf16_t* g = xr + (e >> 4) * 32 + (e & 15);
         float u[8];
         unpack8(*reinterpret_cast<const uint4*>(g), v[c]);
-        unpack8(*reinterpret_cast<const uint4*>(g + 64), u);
+        unpack8(*reinterpret_cast<const uint4*>(g + 16), u);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = v[c][j] / (1.f + __expf(-v[c][j])) * u[j];
       } else {
@@ -297,6 +297,50 @@ extern "C" int edge_act(const void* x, void* y, void* yq, float* ys, int rows, i
     else { if (quant) LAUNCH_ACT(2, true); else LAUNCH_ACT(2, false); }
   });
 #undef LAUNCH_ACT
+  return (int)hipGetLastError();
+}
+
+// Per-(row, 64-column) int8 quantisation (decode GEMV input layout: scales [K/64][Mpad]).  One
+// wave covers 512 columns of a row, 8 per lane; a group's 8 lanes reduce its absmax with three
+// xor-shuffles.  Used between the fused SwiGLU GEMV and the down projection.
+__global__ void __launch_bounds__(NT) group_quant_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
+                                                         float* __restrict__ s, int M, int K, int Mpad) {
+  const int gw = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  const int wpr = (K + 511) / 512;
+  const int row = gw / wpr, wr = gw - row * wpr;
+  if (row >= M) return;
+  const int lane = threadIdx.x & 63;
+  const int e = wr * 512 + lane * 8;
+  const bool ok = e < K;                       // K % 64 == 0: a group's 8 lanes agree
+  float v[8];
+  if (ok) unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * K + e), v);
+  else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  m = fmaxf(m, 1e-8f);
+  if (!ok) return;
+  const float inv = 127.f / m;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[j], inv)) << (8 * j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[4 + j], inv)) << (8 * j);
+  *reinterpret_cast<uint2*>(q + (size_t)row * K + e) = make_uint2(lo, hi);
+  if ((lane & 7) == 0) s[(size_t)(e >> 6) * Mpad + row] = m / 127.f;
+}
+
+extern "C" int edge_group_quant(const void* x, void* q, float* s, int M, int K, int Mpad, hipStream_t st) {
+  if (K % 64 || Mpad < M) return -2;
+  if (M == 0) return 0;
+  const int waves = M * ((K + 511) / 512);
+  hipLaunchKernelGGL(group_quant_kernel, dim3((waves + 3) / 4), dim3(NT), 0, st, (const bf16_t*)x, (int8_t*)q, s, M, K,
+                     Mpad);
   return (int)hipGetLastError();
 }
 

@@ -27,6 +27,11 @@ def run_pipeline_bench(args, build, model_config):
     rank, world = init_distributed("nccl" if use_cuda else "gloo")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if use_cuda and dist.get_backend() != "nccl":
+        # rehearsal: gloo ranks sharing one GPU (EDGELLM_DIST_BACKEND=gloo); collectives on host
+        device = torch.device("cuda", 0)
+        torch.cuda.set_device(device)
+    cdev = device if dist.get_backend() == "nccl" else torch.device("cpu")
     cfg = model_config(args)
     wbytes = 1.0 if args.quant != "none" else 2.0
     explicit = args.partition if "," in args.partition else None
@@ -38,9 +43,10 @@ def run_pipeline_bench(args, build, model_config):
     S = W + K + 1
     g = torch.Generator().manual_seed(args.seed)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)] if rank == 0 else None
-    stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs)
+    stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs,
+                          headinfer_heads=getattr(args, "headinfer_heads", None))
     # initialise the communicator with a collective every rank joins
-    x = torch.ones(1, device=device)
+    x = torch.ones(1, device=cdev)
     dist.all_reduce(x)
     if use_cuda:
         torch.cuda.synchronize()
@@ -68,9 +74,9 @@ def run_pipeline_bench(args, build, model_config):
     sp = SamplingParams(max_new_tokens=S + 1, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
     stage.run(prompts, T, sp, S, seed=args.seed, hook=hook)
     fdt = torch.float64
-    dt = torch.tensor([marks[t_b] - marks[t_a]], device=device, dtype=fdt)
+    dt = torch.tensor([marks[t_b] - marks[t_a]], device=cdev, dtype=fdt)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    lat = torch.zeros(1, device=device, dtype=fdt)
+    lat = torch.zeros(1, device=cdev, dtype=fdt)
     if stage.is_last and len(stamps) > 1:
         if use_cuda:
             iv = sorted(stamps[i - 1].elapsed_time(stamps[i]) for i in range(1, len(stamps)))
@@ -78,7 +84,7 @@ def run_pipeline_bench(args, build, model_config):
             iv = sorted((stamps[i] - stamps[i - 1]) * 1e3 for i in range(1, len(stamps)))
         lat[0] = iv[len(iv) // 2]
     dist.all_reduce(lat, op=dist.ReduceOp.MAX)
-    mem = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9 if use_cuda else 0.0], device=device, dtype=fdt)
+    mem = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9 if use_cuda else 0.0], device=cdev, dtype=fdt)
     dist.all_reduce(mem, op=dist.ReduceOp.MAX)
     elapsed = float(dt.item())
     res = None

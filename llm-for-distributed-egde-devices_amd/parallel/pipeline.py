@@ -42,7 +42,10 @@ class PipelineResult:
 
 class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
-                 group=None, use_graphs: Optional[bool] = None):
+                 group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None):
+        """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
+        to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
+        HeadInfer").  The offloaded path is host-orchestrated, so its decode steps run eagerly."""
         assert n_micro >= world, "need at least as many micro-batches as stages to keep the ring full"
         self.model, self.cfg = model, model.cfg
         self.rank, self.world = rank, world
@@ -55,11 +58,21 @@ class PipelineStage:
         assert self.is_first == (rank == 0) and self.is_last == (rank == world - 1)
         self.prev = (rank - 1) % world
         self.next = (rank + 1) % world
-        self.kv = KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last, model.dtype, self.device)
+        if headinfer_heads is not None and headinfer_heads < self.cfg.num_kv_heads:
+            from ..offload import HeadInferKV
+            self.kv = HeadInferKV(self.cfg, micro_batch * n_micro, max_seq, headinfer_heads, self.device, self.first,
+                                  self.last, chunk_size=max_seq, dtype=model.dtype)
+        else:
+            self.kv = KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last, model.dtype,
+                              self.device)
+        self.attn_hook = getattr(self.kv, "attn_hook", None)
         self.rope = model.rope_table(self.device)
         cuda = self.device.type == "cuda"
         self.use_graphs = cuda if use_graphs is None else (use_graphs and cuda)
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        # gloo with device tensors (several ranks sharing one GPU for a rehearsal): P2P is staged
+        # through host memory
+        self.host_staged = cuda and dist.is_initialized() and not self.nccl
         H, b, dev = self.cfg.hidden_size, micro_batch, self.device
         self.tok = [torch.zeros(b, dtype=torch.long, device=dev) for _ in range(n_micro)]
         self.pos = [torch.zeros(b, dtype=torch.int32, device=dev) for _ in range(n_micro)]
@@ -79,6 +92,14 @@ class PipelineStage:
             p2p += [dist.P2POp(dist.irecv, t, p, self.group) for t, p in recvs]
             for w in dist.batch_isend_irecv(p2p):
                 w.wait()
+        elif self.host_staged:
+            works = [dist.isend(t.cpu(), p, self.group) for t, p in sends]
+            bufs = [torch.empty(t.shape, dtype=t.dtype) for t, _ in recvs]
+            works += [dist.irecv(h, p, self.group) for h, (_, p) in zip(bufs, recvs)]
+            for w in works:
+                w.wait()
+            for h, (t, _) in zip(bufs, recvs):
+                t.copy_(h)
         else:
             works = [dist.isend(t, p, self.group) for t, p in sends]
             works += [dist.irecv(t, p, self.group) for t, p in recvs]
@@ -92,7 +113,7 @@ class PipelineStage:
     def _prefill(self, m: int, ids: Optional[torch.Tensor], T: int, hidden: Optional[torch.Tensor]):
         b = self.b
         sp = torch.zeros(b, dtype=torch.int32, device=self.device)
-        ctx = AttnCtx("prefill", b, T, sp, sp + T, T, self._rows(m), self.rope)
+        ctx = AttnCtx("prefill", b, T, sp, sp + T, T, self._rows(m), self.rope, attn_hook=self.attn_hook)
         out = self.model(ids, ctx, hidden=hidden, logits="last")
         self.pos[m].fill_(T)
         self.lens[m].fill_(T + 1)
@@ -100,7 +121,8 @@ class PipelineStage:
 
     def _decode_body(self, m: int, max_len: int):
         b = self.b
-        ctx = AttnCtx("decode", b, 1, self.pos[m], self.lens[m], max_len, self._rows(m), self.rope)
+        ctx = AttnCtx("decode", b, 1, self.pos[m], self.lens[m], max_len, self._rows(m), self.rope,
+                      attn_hook=self.attn_hook)
         out = self.model(self.tok[m].view(b, 1) if self.is_first else None, ctx,
                          hidden=None if self.is_first else self.hin[m])
         if self.is_last:
@@ -130,7 +152,10 @@ class PipelineStage:
                 self._warm[m] = True
                 return self._decode_body(m, bucket)     # first decode of m runs eagerly (warm-up)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._pool):
+            # no P2P in flight during capture, and a thread-local capture so the process group's
+            # watchdog thread may keep querying its events meanwhile
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
                 self._decode_body(m, bucket)
             if self._pool is None:
                 self._pool = g.pool()
@@ -153,7 +178,7 @@ class PipelineStage:
         V = self.cfg.vocab_size
         self.sampling = sampling
         self.graphs_ok = self.use_graphs and not needs_host_sampler(sampling, V) and \
-            all(getattr(mm, "graph_safe", True) for mm in self.model.modules())
+            getattr(self.kv, "graph_safe", True) and all(getattr(mm, "graph_safe", True) for mm in self.model.modules())
         self._warm: Dict[int, bool] = {}
         self._graphs.clear()
         self._pool = None
@@ -172,13 +197,14 @@ class PipelineStage:
                 for m in range(M):
                     self.seen[m].scatter_(1, prompts[m].to(dev), 1)
             else:
-                pids = torch.zeros(M, b, T, dtype=torch.long, device=dev)
+                pids = torch.zeros(M, b, T, dtype=torch.long, device="cpu" if self.host_staged else dev)
                 if dist.is_initialized():
                     dist.recv(pids, 0, self.group)
+                pids = pids.to(dev)
                 for m in range(M):
                     self.seen[m].scatter_(1, pids[m], 1)
         elif self.is_first and P > 1:
-            dist.send(torch.stack([p.to(dev) for p in prompts]), P - 1, self.group)
+            dist.send(torch.stack([p.to("cpu" if self.host_staged else dev) for p in prompts]), P - 1, self.group)
 
         H = self.cfg.hidden_size
         pre_in = [None] * M
@@ -252,6 +278,7 @@ def init_distributed(backend: Optional[str] = None):
     import os
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
+    backend = os.environ.get("EDGELLM_DIST_BACKEND", backend)   # e.g. gloo: GPU ranks sharing one device
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":

@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -21,7 +22,18 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops import _ref
-from ..models.layers import Linear, QAct
+from ..models.layers import GroupQuantBF16, Linear, QAct
+
+# Decode MLP policy (A/B on MI355X, Llama-2-7B): from this many rows up the gate_up GEMV
+# quantises silu(g) * u in its own epilogue (8 tiles = 64 features per workgroup, so several
+# row blocks share each activation fragment: +3% tok/s at B = 64); below it the GEMV writes bf16
+# h from 2-tile workgroups (more workgroups for the chip) and the group-quant kernel feeds the
+# down projection (+1% at B = 16).  EDGELLM_GLU_QUANT_MIN_ROWS overrides it.
+GLU_QUANT_MIN_ROWS = int(os.environ.get("EDGELLM_GLU_QUANT_MIN_ROWS", "17"))
+
+
+def glu_quant_rows(m: int) -> bool:
+    return m >= GLU_QUANT_MIN_ROWS
 
 
 def quantize_weight_per_channel(w: torch.Tensor):
@@ -46,7 +58,7 @@ class W8A8Linear(nn.Module):
         self.register_buffer("bias", torch.zeros(out_features, dtype=dtype, device=device) if bias else None)
         self._w_cpu = None
         self.out_dtype = dtype
-        self.glu_blocked = False      # rows stored 64-blocked [gate(64) | up(64)] (fused decode GLU)
+        self.glu_blocked = False      # rows stored 16-blocked [gate(16) | up(16)] (fused decode GLU)
 
     @classmethod
     @torch.no_grad()
@@ -76,9 +88,9 @@ class W8A8Linear(nn.Module):
 
     @torch.no_grad()
     def block_glu_(self) -> "W8A8Linear":
-        """Re-pack a [gate | up] projection 64-blocked so one GEMV panel holds both halves of 64
-        features (the fused SwiGLU + quant epilogue, ops.w8a8_glu).  Outputs of ``forward`` are
-        then in blocked order (activation ``silu_glu_blocked``)."""
+        """Re-pack a [gate | up] projection 16-blocked so one 2-tile GEMV workgroup holds both
+        halves of 16 features (the fused SwiGLU epilogue, ops.w8a8_glu).  Outputs of ``forward``
+        are then in blocked order (activation ``silu_glu_blocked``)."""
         if not self.glu_blocked:
             q, sc, b = self.canonical()
             self.load_int8(_ref.block_glu_rows(q), _ref.block_glu_rows(sc),
@@ -102,6 +114,8 @@ class W8A8Linear(nn.Module):
         return self._w_cpu
 
     def forward(self, x):
+        if isinstance(x, GroupQuantBF16):             # decode: per-(token, 64) int8 input
+            x = QAct(*ops.quant_per_group(x.x.reshape(-1, self.in_features)))
         if not isinstance(x, QAct):
             x = QAct(*ops.quant_per_token(x))
         K, N = self.in_features, self.out_features
@@ -111,12 +125,16 @@ class W8A8Linear(nn.Module):
                               N, K, w_ref=self._wref(x.q), out_dtype=self.out_dtype)
         return out.view(*shp, N)
 
-    def glu(self, x: QAct) -> QAct:
-        """Fused gate_up -> silu(g)*u -> per-group int8 (blocked layout, M <= 64)."""
+    def glu(self, x: QAct):
+        """Fused gate_up -> silu(g) * u (blocked layout, M <= 64) for the down projection: int8
+        quantised per (token, 64 features) in the same kernel (``QAct`` with 2-D scales) when
+        ``glu_quant_rows(M)``, else bf16 h that the down projection quantises per group."""
         K, N = self.in_features, self.out_features
-        q, s = ops.w8a8_glu(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,
-                            w_ref=self._wref(x.q))
-        return QAct(q, s)
+        M = x.q.numel() // K
+        quant = N % 128 == 0 and glu_quant_rows(M)
+        out = ops.w8a8_glu(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,
+                           w_ref=self._wref(x.q), quant=quant)
+        return QAct(*out) if quant else GroupQuantBF16(out)
 
     def extra_repr(self):
         return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, W8A8 int8"
@@ -208,7 +226,8 @@ class CPUDynamicLinear(nn.Module):
 
 def enable_fused_glu(model) -> int:
     """Block the W8A8 gate_up projections of SwiGLU layers (F % 64 == 0) so the decode MLP runs
-    as GEMV+SwiGLU+quant -> down GEMV (two launches instead of three).  Returns layers changed."""
+    as GEMV+SwiGLU -> down GEMV with in-kernel per-group quant (two launches instead of three).
+    Returns the number of layers changed."""
     cfg = model.cfg
     if not (cfg.is_glu and cfg.act == "silu_glu" and cfg.intermediate_size % 64 == 0):
         return 0

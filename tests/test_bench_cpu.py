@@ -49,3 +49,18 @@ def test_bench_pipeline_torchrun_cpu(n):
     d = _last_json(r.stdout)
     assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n and d["value"] > 0
     assert d["config"]["parallelism"] == f"pp{n}" and len(d["config"]["partition"]) == n + 1
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_headinfer_cpu(n):
+    """BASELINE config 4 plumbing: --headinfer-heads offloads KV heads in the single-GPU engine and
+    in every pipeline stage."""
+    args = ["bench.py", "--gpus", str(n), *COMMON, "--headinfer-heads", "1"]
+    cmd = [sys.executable, *args] if n == 1 else [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                                                   f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+                                                   "--master-port", str(_port()), *args]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["config"]["headinfer_heads"] == 1 and d["value"] > 0

@@ -3,7 +3,8 @@
 * decode attention straight from the QKV projection (RoPE + KV append + attention, optional
   per-group int8 output) == ops._ref rope_kv_write -> decode_attention (-> quant_per_group)
 * W8A8 GEMV with per-(token, 64-column) activation scales == _ref.w8a8_linear (2-D x_scale)
-* gate_up GEMV + SwiGLU + per-group quant epilogue == _ref composition on the blocked layout
+* gate_up GEMV + SwiGLU epilogue (16-blocked rows) == _ref composition; per-(token, 64) group
+  quantisation kernel == _ref.quant_per_group
 * blocked-layout activation kernel (prefill path of the same packing)
 """
 import math
@@ -75,6 +76,7 @@ def test_w8a8_gemm_group_scales(cuda, M, N, K):
 @pytest.mark.parametrize("M", [1, 3, 16, 40, 64])
 @pytest.mark.parametrize("F,K", [(1024, 4096), (11008, 4096), (256, 128)])
 def test_w8a8_glu_fused(cuda, M, F, K):
+    """gate_up GEMV on 16-blocked rows with the SwiGLU epilogue == unfused GEMM -> silu(g) * u."""
     C = ops.ext()
     torch.manual_seed(F + M)
     qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
@@ -82,18 +84,44 @@ def test_w8a8_glu_fused(cuda, M, F, K):
     w = torch.randint(-127, 128, (2 * F, K), dtype=torch.int8, device=cuda)
     sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
     wb, swb = _ref.block_glu_rows(w), _ref.block_glu_rows(sw)
-    hq, hs = C.w8a8_gemm_glu(qx, sx, ops.pack_int8_weight(wb), swb, None, 2 * F, K)
-    y = _ref.w8a8_linear(qx, sx, w, sw, None, torch.bfloat16).float()       # unblocked [gate | up]
-    h = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
-    qr, sr = _ref.quant_per_group(h)
-    _close(hs[:, :M], sr[:, :M], 1e-6, 1e-2)
-    # g and u are rounded to bf16 (as the unfused GEMM output is); float-vs-double products can
-    # land one bf16 ulp apart, so allow one int8 step plus 1% on top of the quantisation error
-    step = hs[:, :M].t().repeat_interleave(64, 1).cpu()
-    deq = hq.float().cpu() * step
-    err = (deq - h.cpu()).abs()
-    assert (err <= 1.01 * step + 0.01 * h.abs().cpu()).all(), err.max()
-    assert (hq.int() - qr.int()).abs().max().item() <= 2
+    h = C.w8a8_gemm_glu(qx, sx, ops.pack_int8_weight(wb), swb, None, 2 * F, K)
+    y = _ref.w8a8_linear(qx, sx, w, sw, None, torch.bfloat16)               # unblocked [gate | up], bf16
+    ref = _ref.silu_mul(y)
+    assert h.shape == (M, F) and h.dtype == torch.bfloat16
+    # g and u are bf16-rounded on both sides; float-vs-double products can land 1 ulp apart
+    _close(h, ref, 1e-3, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 16, 33, 64])
+@pytest.mark.parametrize("F,K", [(64, 64), (192, 4096), (11008, 4096)])
+def test_w8a8_glu_quant_epilogue(cuda, M, F, K):
+    """gate_up GEMV + SwiGLU + per-(token, 64 features) int8 quantisation in one kernel ==
+    unfused GEMM -> silu(g) * u -> quant_per_group (fp32 h on both sides)."""
+    C = ops.ext()
+    torch.manual_seed(F + M + 7)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (2 * F, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
+    wb, swb = _ref.block_glu_rows(w), _ref.block_glu_rows(sw)
+    q, s = C.w8a8_gemm_gluq(qx, sx, ops.pack_int8_weight(wb), swb, None, 2 * F, K)
+    g, u = _ref.w8a8_linear(qx, sx, w, sw, None, torch.bfloat16).float().chunk(2, dim=-1)
+    qr, sr = _ref.quant_per_group(torch.nn.functional.silu(g) * u)
+    assert q.shape == (M, F) and q.dtype == torch.int8 and s.shape == sr.shape
+    _close(s, sr, 1e-7, 1e-5)
+    assert (s[:, M:] == 0).all()
+    assert (q.int() - qr.int()).abs().max().item() <= 1
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 64])
+@pytest.mark.parametrize("K", [64, 4096, 11008])
+def test_group_quant(cuda, M, K):
+    C = ops.ext()
+    x = (torch.randn(M, K, device=cuda) * 3).bfloat16()
+    q, s = C.group_quant(x)
+    qr, sr = _ref.quant_per_group(x)
+    _close(s[:, :M], sr[:, :M], 1e-7, 1e-5)
+    assert (q.int() - qr.int()).abs().max().item() <= 1
 
 
 @pytest.mark.parametrize("F", [256, 11008])
@@ -146,5 +174,5 @@ def test_glu_split_k(cuda, S):
         got = [C.w8a8_gemm_glu(qx, sx, wp, swb, None, 2 * F, K) for _ in range(2)]
     finally:
         C.tune("splitk", 0, 0)
-    for hq, hs in got:                         # integer partial sums: split count cannot matter
-        assert torch.equal(hq, base[0]) and torch.equal(hs, base[1])
+    for h in got:                              # integer partial sums: split count cannot matter
+        assert torch.equal(h, base)

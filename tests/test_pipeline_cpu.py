@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, arch, M, b, T, S, do_sample, q):
+def _worker(rank, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads=None):
     import edgellm  # noqa: F401
     from edgellm.parallel.pipeline import PipelineStage
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -36,7 +36,7 @@ def _worker(rank, world, port, arch, M, b, T, S, do_sample, q):
     model = build_model(cfg, dtype=torch.float32, first=bounds[rank], last=bounds[rank + 1], seed=7)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
-    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4)
+    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, headinfer_heads=headinfer_heads)
     sp = SamplingParams(max_new_tokens=S + 1, do_sample=do_sample, temperature=0.7, top_k=20, top_p=0.9,
                         repetition_penalty=1.1)
     res = st.run(prompts if rank == 0 else None, T, sp, S, seed=5)
@@ -75,6 +75,23 @@ def test_pipeline_matches_unsplit(world, M, do_sample):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == _reference(arch, M, b, T, S, do_sample)
+
+
+def test_pipeline_with_headinfer_offload_matches_unsplit():
+    """BASELINE config 'pipeline + HeadInfer': each stage keeps 1 of 2 KV heads on the device and
+    offloads the other to (pinned) host memory; tokens equal the unsplit, fully resident model's."""
+    world, M, arch, b, T, S = 2, 2, "llama", 2, 5, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, M, b, T, S, True, q, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == _reference(arch, M, b, T, S, True)
 
 
 def _stall_worker(rank, world, port, marker):
