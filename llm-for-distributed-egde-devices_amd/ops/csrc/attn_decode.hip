@@ -5,9 +5,11 @@
 // shaped for streaming rather than MFMA: one workgroup = (split, kv-head, batch); its G = Hq/Hkv
 // query heads share every K/V row it loads (GQA reuse), and LPK lanes cooperate on one key row
 // (LPK*16 B contiguous per key, 1 KiB per wave-instruction at D=128 -> fully coalesced).
-//   phase 1: scores s[h][k] = q_h . k  -> LDS   (UNROLL rows in flight per lane)
-//   phase 2: per-head max / exp2 / sum in LDS (one wave per head)
-//   phase 3: acc[h][d] += p[h][k] * v[k][d], reduced over lanes, then over the 4 waves
+// One pass over the split: every wave runs an online softmax (running max m, sum l, acc) over
+// its key slice with K and V rows of a chunk loaded together and the next chunk prefetched, then
+// the 4 waves are merged in LDS.  At decode contexts of a few hundred keys the kernel is bound by
+// the serial load-latency chain, so fusing the old scores / softmax / P.V phases (each a round
+// of dependent loads) is what matters.
 // With nsplit > 1 each split writes (acc, m, l) and a combine kernel merges them; with one
 // split the normalised output is written directly.
 //
@@ -68,9 +70,10 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
   constexpr int KPW = 64 / LPK;           // keys per wave-instruction
   constexpr int KPB = KPW * NW;           // keys per workgroup step
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sc = smem;                       // [G][CH]
-  float* red = smem + G * CH;             // [NW][G][D]
-  float* mstat = red + NW * G * D;        // [G]
+  float* red = smem;                      // [NW][G][D] per-wave rescaled accumulators
+  float* wm = red + NW * G * D;           // [NW][G] per-wave running max
+  float* wl = wm + NW * G;                // [NW][G] per-wave rescaled sums
+  float* mstat = wl + NW * G;             // [G]
   float* lstat = mstat + G;               // [G]
 
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
@@ -101,6 +104,28 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
   const bf16_t* kb = kc + b * c_sb + kvh * c_sh + (size_t)start * D;
   const bf16_t* vb = vc + b * c_sb + kvh * c_sh + (size_t)start * D;
 
+  // q first: its loads (and the RoPE partner loads) overlap the KV append below
+  float qf[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    if (dvalid) {
+      const bf16_t* qh = q + b * q_sb + (size_t)(kvh * G + h) * D;
+      unpack8(*reinterpret_cast<const uint4*>(qh + d0), qf[h]);
+      if constexpr (FUSED) {
+        if (d0 < fz.rot) {
+          rope8(qh, d0, fz.rot, reinterpret_cast<const float2*>(fz.cs) + (size_t)fz.pos[b] * (fz.rot / 2), qf[h]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qf[h][j] = bf2f(f2bf(qf[h][j]));   // q is bf16 in the unfused path
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[h][j] *= scale_log2;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[h][j] = 0.f;
+    }
+  }
+
   if constexpr (FUSED) {
     // append the new token's rotated k and its v (only the split that owns the position)
     const int pos = fz.pos[b];
@@ -123,118 +148,133 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
     __syncthreads();
   }
 
-  float qf[G][8];
+  // ---- one pass: each wave keeps an online softmax (m, l, acc) over its key slice; K and V rows
+  // are loaded together and the next chunk is in flight while the current one is consumed
+  // (two register buffers, alternated by a 2x unrolled loop: copying a buffer that still has
+  // loads outstanding would force a full wait).  Out-of-range keys load a clamped row and are
+  // masked in the score (unconditional 16-byte loads; a conditional one compiles to branches).
+  constexpr int STEP = KPB * UNROLL;      // keys per workgroup per chunk
+  const int dc = dvalid ? d0 : 0;
+  float m[G], l[G], acc[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    if (dvalid) {
-      const bf16_t* qh = q + b * q_sb + (size_t)(kvh * G + h) * D;
-      unpack8(*reinterpret_cast<const uint4*>(qh + d0), qf[h]);
-      if constexpr (FUSED) {
-        if (d0 < fz.rot) {
-          rope8(qh, d0, fz.rot, reinterpret_cast<const float2*>(fz.cs) + (size_t)fz.pos[b] * (fz.rot / 2), qf[h]);
+    m[h] = -INFINITY;
+    l[h] = 0.f;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qf[h][j] = bf2f(f2bf(qf[h][j]));   // q is bf16 in the unfused path
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[h][j] *= scale_log2;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[h][j] = 0.f;
-    }
+    for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
   }
-
-  // ---- phase 1: scores
-  for (int kb0 = wave * KPW; kb0 < n; kb0 += KPB * UNROLL) {  // wave-uniform trip count (shuffles inside)
-    const int k0 = kb0 + kl;
-    uint4 kv[UNROLL];
+  auto load = [&](int base, uint4 (&kr)[UNROLL], uint4 (&vr)[UNROLL]) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = k0 + u * KPB;
-      kv[u] = (dvalid && k < n) ? *reinterpret_cast<const uint4*>(kb + (size_t)k * D + d0) : make_uint4(0, 0, 0, 0);
+      const int k = base + kl + u * KPB;
+      const size_t off = (size_t)(k < n ? k : 0) * D + dc;
+      kr[u] = *reinterpret_cast<const uint4*>(kb + off);
+      vr[u] = *reinterpret_cast<const uint4*>(vb + off);
     }
+  };
+  auto consume = [&](int base, const uint4 (&kr)[UNROLL], const uint4 (&vr)[UNROLL]) {
+    float s[UNROLL][G];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       float kf[8];
-      unpack8(kv[u], kf);
-      float s[G];
+      unpack8(kr[u], kf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         float a = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) a += qf[h][j] * kf[j];
-        s[h] = a;
-      }
-#pragma unroll
-      for (int o = LPK / 2; o > 0; o >>= 1)
-#pragma unroll
-        for (int h = 0; h < G; ++h) s[h] += __shfl_xor(s[h], o, 64);
-      const int k = k0 + u * KPB;
-      if (dl == 0 && k < n) {
-#pragma unroll
-        for (int h = 0; h < G; ++h) sc[h * CH + k] = s[h];
+        s[u][h] = a;
       }
     }
-  }
-  __syncthreads();
-
-  // ---- phase 2: softmax statistics per head (log2 domain)
-  for (int h = wave; h < G; h += NW) {
-    float m = -INFINITY;
-    for (int k = lane; k < n; k += 64) m = fmaxf(m, sc[h * CH + k]);
-    m = wave_max(m);
-    float l = 0.f;
-    for (int k = lane; k < n; k += 64) {
-      const float p = exp2f(sc[h * CH + k] - m);
-      sc[h * CH + k] = p;
-      l += p;
-    }
-    l = wave_sum(l);
-    if (lane == 0) { mstat[h] = m; lstat[h] = l; }
-  }
-  __syncthreads();
-
-  // ---- phase 3: P.V
-  float acc[G][8];
 #pragma unroll
-  for (int h = 0; h < G; ++h)
+    for (int o = LPK / 2; o > 0; o >>= 1)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
-  for (int kb0 = wave * KPW; kb0 < n; kb0 += KPB * UNROLL) {
-    const int k0 = kb0 + kl;
-    uint4 vv[UNROLL];
+      for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = k0 + u * KPB;
-      vv[u] = (dvalid && k < n) ? *reinterpret_cast<const uint4*>(vb + (size_t)k * D + d0) : make_uint4(0, 0, 0, 0);
+        for (int h = 0; h < G; ++h) s[u][h] += __shfl_xor(s[u][h], o, 64);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+      if (base + kl + u * KPB >= n) {
+#pragma unroll
+        for (int h = 0; h < G; ++h) s[u][h] = -INFINITY;
+      }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float cm = s[0][h];
+#pragma unroll
+      for (int u = 1; u < UNROLL; ++u) cm = fmaxf(cm, s[u][h]);
+#pragma unroll
+      for (int o = LPK; o < 64; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+      // cm is finite: key `base` (kl = 0, u = 0) is in range whenever a chunk is consumed
+      const float mn = fmaxf(m[h], cm);
+      const float alpha = exp2f(m[h] - mn);        // 0 on the first chunk (m = -inf)
+      m[h] = mn;
+      l[h] *= alpha;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[h][j] *= alpha;
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int k = k0 + u * KPB;
-      if (k < n) {
-        float vf[8];
-        unpack8(vv[u], vf);
+      float vf[8];
+      unpack8(vr[u], vf);
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-          const float p = sc[h * CH + k];
+      for (int h = 0; h < G; ++h) {
+        const float p = exp2f(s[u][h] - m[h]);    // masked keys: exp2(-inf) = 0
+        l[h] += p;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[h][j] += p * vf[j];
-        }
+        for (int j = 0; j < 8; ++j) acc[h][j] += p * vf[j];
       }
+    }
+  };
+  {
+    uint4 ka[UNROLL], va[UNROLL], kb2[UNROLL], vb2[UNROLL];
+    int base = wave * KPW;                           // wave-uniform trip count (shuffles inside)
+    if (base < n) load(base, ka, va);
+    while (base < n) {
+      const int nb = base + STEP;
+      if (nb < n) load(nb, kb2, vb2);
+      consume(base, ka, va);
+      if (nb >= n) break;
+      const int nb2 = nb + STEP;
+      if (nb2 < n) load(nb2, ka, va);
+      consume(nb, kb2, vb2);
+      base = nb2;
     }
   }
   // reduce over the KPW key groups of this wave (lanes sharing dl)
 #pragma unroll
   for (int o = LPK; o < 64; o <<= 1)
 #pragma unroll
-    for (int h = 0; h < G; ++h)
+    for (int h = 0; h < G; ++h) {
+      l[h] += __shfl_xor(l[h], o, 64);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[h][j] += __shfl_xor(acc[h][j], o, 64);
-  if (kl == 0 && dvalid) {
+    }
+  // merge the waves: rescale each to the workgroup max
+  if (lane == 0) {
 #pragma unroll
-    for (int h = 0; h < G; ++h)
+    for (int h = 0; h < G; ++h) wm[wave * G + h] = m[h];
+  }
+  __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[(wave * G + h) * D + d0 + j] = acc[h][j];
+  for (int h = 0; h < G; ++h) {
+    float M = wm[h];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) M = fmaxf(M, wm[w * G + h]);
+    const float sc_w = m[h] == -INFINITY ? 0.f : exp2f(m[h] - M);   // wave without keys: 0
+    if (kl == 0 && dvalid) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(wave * G + h) * D + d0 + j] = acc[h][j] * sc_w;
+    }
+    if (lane == 0) wl[wave * G + h] = l[h] * sc_w;
+    if (wave == 0 && lane == 0) mstat[h] = M;
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    float L = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) L += wl[w * G + threadIdx.x];
+    lstat[threadIdx.x] = L;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < G * D; i += NT) {
@@ -327,7 +367,7 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
   if (fused && rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
   const Fuse fz{pos, cs, fused ? rot : 0, q_sb, (int8_t*)out_q, out_s, Mpad};
   const float sl2 = scale * 1.4426950408889634f;
-  const size_t lds = (size_t)(G * ch + NW * G * D + 2 * G) * sizeof(float);
+  const size_t lds = (size_t)(NW * G * D + 2 * NW * G + 2 * G) * sizeof(float);
   const dim3 grid(nsplit, Hkv, B);
   const bool direct = nsplit == 1;
 #define DK(DD, GG, DI, FU, QO)                                                                                 \

@@ -23,14 +23,15 @@ def _close(a, b, atol, rtol=0.0):
     assert bad == 0, f"{bad} / {a.numel()} elements off, max err {err.max().item():.4g}"
 
 
-@pytest.mark.parametrize("H", [128, 2048, 4096, 5120, 11008])
+@pytest.mark.parametrize("H", [128, 768, 2048, 2560, 4096, 5120, 11008])
 @pytest.mark.parametrize("rms", [True, False])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_norm(cuda, H, rms, with_res):
+@pytest.mark.parametrize("rows", [7, 300])          # wave-per-row form (H <= 4096) / workgroup per row
+def test_norm(cuda, H, rms, with_res, rows):
     C = ops.ext()
     torch.manual_seed(0)
-    x = torch.randn(7, H, device=cuda, dtype=torch.bfloat16)
-    r = torch.randn(7, H, device=cuda, dtype=torch.bfloat16) if with_res else None
+    x = torch.randn(rows, H, device=cuda, dtype=torch.bfloat16)
+    r = torch.randn(rows, H, device=cuda, dtype=torch.bfloat16) if with_res else None
     w = (torch.rand(H, device=cuda) + 0.5).bfloat16()
     b = None if rms else torch.randn(H, device=cuda).bfloat16()
     y, _, ro = C.norm(x, r, w, b, 1e-5, rms, False)

@@ -212,7 +212,11 @@ def small_rows(C, dev, B, H, Hq, D):
     x = torch.randn(B, H, device=dev).bfloat16()
     r = torch.randn(B, H, device=dev).bfloat16()
     w = torch.ones(H, device=dev).bfloat16()
-    out.append(dict(op="rmsnorm_res_quant", rows=B, H=H, us=round(timeit(lambda: C.norm(x, r, w, None, 1e-5, True, True)), 2)))
+    for rows in (B, 64):
+        xx = torch.randn(rows, H, device=dev).bfloat16()
+        rr = torch.randn(rows, H, device=dev).bfloat16()
+        t = timeit(lambda: C.norm(xx, rr, w, None, 1e-5, True, True))
+        out.append(dict(op="rmsnorm_res_quant", rows=rows, H=H, us=round(t, 2)))
     gu = torch.randn(B, 2 * 11008, device=dev).bfloat16()
     out.append(dict(op="silu_mul_quant", rows=B, F=11008, us=round(timeit(lambda: C.act(gu, 0, True)), 2)))
     qkv = torch.randn(B, 3 * H, device=dev).bfloat16()
