@@ -40,7 +40,6 @@ int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* 
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
 void edge_w8a8_gemv_ntw(int ntw);
-void edge_w8a8_splitk(int s);
 void edge_decode_attn_config(int target_wg);
 }
 
@@ -458,7 +457,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
-    else if (what == "splitk") edge_w8a8_splitk((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });

@@ -78,210 +78,239 @@ __device__ __forceinline__ v4i load_a_i8(const int8_t* __restrict__ arow_p, bool
 }
 
 // ------------------------------------------------------------------------------------ gemv
-// Split-K (S > 1, opt-in): S workgroups share a tile group, each reducing K/S k-tiles; every
-// wave publishes its partial tiles with device-scope (sc1, write-through) 8-byte stores, waits
-// for them (vmcnt 0), and after a barrier one relaxed device-scope counter increment elects
-// the last workgroup, which reads the partials back with sc1 loads, sums them in split order
-// (deterministic, also for float accumulators), resets the counter and runs the epilogue.
-// Measured on MI355X at Llama-2-7B decode shapes the handoff costs more than the extra CUs
-// return, so the launcher uses S = 1 unless tuned ("splitk").
-typedef uint64_t v2u64 __attribute__((ext_vector_type(2)));
+// Weight-stationary over the rows: one workgroup owns NTW 16-column tiles for ALL M <= 16*MB
+// rows, so every weight fragment is fetched once and feeds MB MFMAs.  NW = TG x KW waves: wave
+// (tg, kw) holds tiles [tg*TPW, (tg+1)*TPW) and k-tiles kt = kw (mod KW); per step it keeps
+// U x TPW nontemporal 1 KiB weight fragments in flight.  Sizing rule (tools/membw.hip on
+// MI355X, cache-cold): 16 waves per CU-resident workgroup and >= 172 workgroups stream a
+// 50-90 MB panel at 5.6-6.2 TB/s, while 4-wave workgroups or < 256 groups of few waves stall at
+// 2-4 TB/s — so the launcher always runs 16 waves and sizes NTW for ~256 workgroups.
+// Partial tiles are reduced across the KW k-waves through LDS (KW x NTW x MB KiB).  Everything
+// the epilogue reads from global memory (weight scales, bias, per-token scales) is loaded at
+// kernel start, so the tail of the kernel never waits on an HBM round trip.
 
-struct SplitK {
-  int S;
-  v4i* part;     // [groups][S][NTW][64 lanes] partial tiles (int32, float bits for scaled modes)
-  int* cnt;      // [groups], zero between launches
+__device__ const bf16_t g_zero_bf16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+// Epilogue operands preloaded per owned fragment (EPI_OUT) or gate/up pair (GLU).
+template <int OWN>
+struct EpiPre {
+  float s0[OWN], s1[OWN];    // sw[col] (EPI_OUT) | sw[gate col], sw[up col]
+  float b0[OWN], b1[OWN];    // bias likewise (0 when absent)
 };
 
-// Grid: XCD-grouped 1-D: dispatch ids b, b+8, b+16, ... land on one XCD, so the MB row blocks
-// (and the S splits) of a tile group are consecutive ids within one XCD and re-read the panel
-// from that XCD's L2 instead of HBM (a speed assumption only, never a correctness one).
-template <int UNROLL, int NW, int NTW, int AMODE, int EPI>
-__global__ void __launch_bounds__(NW * 64) w8a8_gemv_kernel(const void* __restrict__ Av, const float* __restrict__ sa,
-                                                            const int8_t* __restrict__ Wp, const float* __restrict__ sw,
-                                                            const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                            float* __restrict__ os, int M, int N, int K, int KT,
-                                                            int NTt, int Mpad, SplitK sk) {
-  static_assert(EPI == EPI_OUT || (AMODE == A_TOKEN && NTW % 2 == 0 && NW >= NTW / 2),
-                "GLU epilogues: gate/up tile pairs, one pair per wave, per-token A");
-  static_assert(EPI != EPI_GLUQ || NTW == 8, "quantising GLU epilogue: 64 features per workgroup");
-  constexpr bool SCALED = AMODE != A_TOKEN;        // float accumulation with per-k-tile scales
-  constexpr bool GLU = EPI != EPI_OUT;
-  constexpr int OWN = GLU ? 2 : (NTW + NW - 1) / NW;   // GLU: wave w owns tiles 2w (gate), 2w+1 (up)
-  __shared__ v4i red[NW][NTW][64];
-  __shared__ float gmax[4][16];
-  __shared__ int last_flag;
-  const int MB = (M + 15) / 16, S = sk.S;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, r = bid >> 3;
-  const int ks = r % S, r2 = r / S;
-  const int mb = r2 % MB, grp = xcd + 8 * (r2 / MB);
-  const int nt0 = grp * NTW;
-  if (nt0 >= NTt) return;                                   // grid padded to a multiple of 8 groups
-  const int kt_begin = (int)((int64_t)KT * ks / S), kt_end = (int)((int64_t)KT * (ks + 1) / S);
-  const int m0 = mb * 16;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int arow = m0 + (lane & 15), akc = 16 * (lane >> 4);
-  const bool aval = arow < M;
-  const int8_t* arow_i8 = reinterpret_cast<const int8_t*>(Av) + (size_t)(aval ? arow : 0) * K;
-  const bool k16 = (K % 16) == 0;
-  v4i acc[NTW];
-  v4f accf[NTW];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) { acc[j] = v4i{0, 0, 0, 0}; accf[j] = v4f{0.f, 0.f, 0.f, 0.f}; }
-  const v4i* wp[NTW];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int nt = min(nt0 + j, NTt - 1);
-    wp[j] = reinterpret_cast<const v4i*>(Wp + ((size_t)nt * KT) * 1024) + lane;
-  }
+template <int MB, int NTW, int NW, int EPI>
+constexpr int epi_units() { return EPI == EPI_OUT ? NTW * MB : NTW / 2 * MB; }
 
-  for (int kt = kt_begin + wave; kt < kt_end; kt += NW * UNROLL) {
-    v4i b[UNROLL][NTW];
-    v4i a[UNROLL];
-    v4f sg[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        b[u][j] = (k < kt_end) ? __builtin_nontemporal_load(wp[j] + (size_t)k * 64) : v4i{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = kt + u * NW;
-      if constexpr (AMODE == A_GROUP)
-        sg[u] = k < kt_end ? *reinterpret_cast<const v4f*>(sa + (size_t)k * Mpad + m0 + 4 * (lane >> 4))
-                           : v4f{0.f, 0.f, 0.f, 0.f};
-      a[u] = load_a_i8(arow_i8, aval, k, kt_end, akc, K, k16);
-    }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        if constexpr (SCALED) fold(accf[j], mfma_i8(a[u], b[u][j], v4i{0, 0, 0, 0}), sg[u]);
-        else acc[j] = mfma_i8(a[u], b[u][j], acc[j]);
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) red[wave][j][lane] = SCALED ? __builtin_bit_cast(v4i, accf[j]) : acc[j];
-  __syncthreads();
-
-  // ---- per-tile totals for the tiles this wave owns (EPI_GLU: wave 0 owns the gate/up pair)
-  v4i tot[OWN];
-  int tile[OWN];
+template <int MB, int NTW, int NW, int EPI>
+__device__ __forceinline__ EpiPre<(epi_units<MB, NTW, NW, EPI>() + NW - 1) / NW> epi_preload(
+    const float* __restrict__ sw, const bf16_t* __restrict__ bias, int nt0, int NTt, int wave, int lane) {
+  constexpr int UNITS = epi_units<MB, NTW, NW, EPI>(), OWN = (UNITS + NW - 1) / NW;
+  EpiPre<OWN> p;
 #pragma unroll
   for (int o = 0; o < OWN; ++o) {
-    tile[o] = GLU ? (wave < NTW / 2 ? 2 * wave + o : NTW) : wave + NW * o;
-    tot[o] = v4i{0, 0, 0, 0};
-    if (tile[o] < NTW) {
-      if constexpr (SCALED) {
-        v4f f = __builtin_bit_cast(v4f, red[0][tile[o]][lane]);
-#pragma unroll
-        for (int w = 1; w < NW; ++w) f += __builtin_bit_cast(v4f, red[w][tile[o]][lane]);
-        tot[o] = __builtin_bit_cast(v4i, f);
-      } else {
-        v4i t = red[0][tile[o]][lane];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) t += red[w][tile[o]][lane];
-        tot[o] = t;
-      }
-    }
+    const int u = wave + o * NW;
+    const int t = EPI == EPI_OUT ? u / MB : 2 * (u / MB);          // (gate) tile
+    const bool ok = u < UNITS && nt0 + t + (EPI == EPI_OUT ? 0 : 1) < NTt;
+    (void)ok;                                   // out-of-range units are never stored: clamp, no branch
+    const int N = NTt * 16;
+    const int c0 = min((nt0 + t) * 16 + (lane & 15), N - 1), c1 = min(c0 + 16, N - 1);
+    p.s0[o] = sw[c0];
+    p.s1[o] = EPI != EPI_OUT ? sw[c1] : 0.f;
+    const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;   // absent bias: read a zero word
+    p.b0[o] = bf2f(bp[bias != nullptr ? c0 : 0]);
+    p.b1[o] = EPI != EPI_OUT ? bf2f(bp[bias != nullptr ? c1 : 0]) : 0.f;
   }
-  // ---- split-K hand-off (see SplitK)
-  if (S > 1) {
-    const size_t pbase = (size_t)(grp * MB + mb) * S;
-#pragma unroll
-    for (int o = 0; o < OWN; ++o) {
-      if (tile[o] >= NTW) continue;
-      uint64_t* p = reinterpret_cast<uint64_t*>(sk.part + ((pbase + ks) * NTW + tile[o]) * 64 + lane);
-      const v2u64 v = __builtin_bit_cast(v2u64, tot[o]);
-      __hip_atomic_store(p, v[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p + 1, v[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int* c = sk.cnt + grp * MB + mb;
-      const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last_flag = prev == S - 1;
-      if (prev == S - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last_flag) return;
-#pragma unroll
-    for (int o = 0; o < OWN; ++o) {
-      if (tile[o] >= NTW) continue;
-      v4i t = v4i{0, 0, 0, 0};
-      v4f f = v4f{0.f, 0.f, 0.f, 0.f};
-      for (int k2 = 0; k2 < S; ++k2) {
-        const uint64_t* p = reinterpret_cast<const uint64_t*>(sk.part + ((pbase + k2) * NTW + tile[o]) * 64 + lane);
-        const v2u64 v = v2u64{__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                              __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
-        if constexpr (SCALED) f += __builtin_bit_cast(v4f, v);
-        else t += __builtin_bit_cast(v4i, v);
-      }
-      tot[o] = SCALED ? __builtin_bit_cast(v4i, f) : t;
-    }
-  }
+  return p;
+}
 
+// Reduce the KW partial fragments in `red` ([KW][NTW*MB][64] v4i) and write the outputs.
+// sa: per-token scales (A_TOKEN; may point to LDS), unused when SCALED.  EPI_GLUQ needs every
+// wave to arrive (it holds a workgroup barrier).
+template <int MB, int NTW, int NW, int KW, bool SCALED, int EPI, int OWN>
+__device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const float* sa, const EpiPre<OWN>& pre,
+                                              void* __restrict__ outv, float* __restrict__ os, float (*gmax)[4][16],
+                                              int M, int N, int NTt, int Mpad, int nt0, int wave, int lane) {
+  constexpr int F = NTW * MB;
+  auto total = [&](int f) -> v4i {
+    if constexpr (SCALED) {
+      v4f s = __builtin_bit_cast(v4f, red[f * 64 + lane]);
+#pragma unroll
+      for (int w = 1; w < KW; ++w) s += __builtin_bit_cast(v4f, red[(w * F + f) * 64 + lane]);
+      return __builtin_bit_cast(v4i, s);
+    } else {
+      v4i s = red[f * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < KW; ++w) s += red[(w * F + f) * 64 + lane];
+      return s;
+    }
+  };
   if constexpr (EPI == EPI_OUT) {
+    bf16_t* out = reinterpret_cast<bf16_t*>(outv);
 #pragma unroll
     for (int o = 0; o < OWN; ++o) {
-      if (tile[o] >= NTW || nt0 + tile[o] >= NTt) continue;
-      const int col = (nt0 + tile[o]) * 16 + (lane & 15);
+      const int f = wave + o * NW;
+      const int t = f / MB, i = f % MB;
+      if (f >= F || nt0 + t >= NTt) continue;
+      const v4i tot = total(f);
+      const int col = (nt0 + t) * 16 + (lane & 15);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = m0 + 4 * (lane >> 4) + q;
-        if constexpr (SCALED) store_out_f(out, M, N, row, col, __builtin_bit_cast(v4f, tot[o])[q], sw, bias);
-        else store_out(out, M, N, row, col, tot[o][q], sa, sw, bias);
+        const int row = i * 16 + 4 * (lane >> 4) + q;
+        if (row < M && col < N) {
+          float v = SCALED ? __builtin_bit_cast(v4f, tot)[q] : (float)tot[q] * sa[row];
+          v = v * pre.s0[o] + pre.b0[o];
+          out[(size_t)row * N + col] = f2bf(v);
+        }
       }
     }
   } else {
-    // pair (gate tile nt0 + 2w, up tile nt0 + 2w + 1) -> feature f = (nt0/2 + w) * 16 + lane & 15
-    const int F = N / 2;
-    const bool owner = wave < NTW / 2 && nt0 + 2 * wave + 1 < NTt;
-    const int gcol = (nt0 + 2 * wave) * 16 + (lane & 15), ucol = gcol + 16;
-    const int f = (nt0 / 2 + wave) * 16 + (lane & 15);
-    float h[4] = {0.f, 0.f, 0.f, 0.f};
-    if (owner) {
+    // pair p = (gate tile 2p, up tile 2p+1) -> feature (nt0/2 + p) * 16 + (lane & 15)
+    const int Fo = N / 2;
+    constexpr int NP = NTW / 2 * MB;
+    static_assert(EPI != EPI_GLUQ || OWN == 1, "quantising GLU: one pair per wave");
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = m0 + 4 * (lane >> 4) + q;
-        const float s_a = row < M ? sa[row] : 0.f;
-        float g = (float)tot[0][q] * s_a * sw[gcol], u = (float)tot[1][q] * s_a * sw[ucol];
-        if (bias) { g += bf2f(bias[gcol]); u += bf2f(bias[ucol]); }
-        g = bf2f(f2bf(g));                // the unfused GEMM output is bf16
-        u = bf2f(f2bf(u));
-        h[q] = g / (1.f + __expf(-g)) * u;
-        if constexpr (EPI == EPI_GLU)
-          if (row < M) out[(size_t)row * F + f] = f2bf(h[q]);
-      }
-    }
-    if constexpr (EPI == EPI_GLUQ) {
-      int8_t* hq = reinterpret_cast<int8_t*>(out);
+    for (int o = 0; o < OWN; ++o) {
+      const int pf = wave + o * NW;
+      const bool live = pf < NP;
+      const int p = live ? pf / MB : 0, i = live ? pf % MB : 0;
+      const bool owner = live && nt0 + 2 * p + 1 < NTt;
+      const int feat = (nt0 / 2 + p) * 16 + (lane & 15);
+      float h[4] = {0.f, 0.f, 0.f, 0.f};
       if (owner) {
+        const v4i g4 = total((2 * p) * MB + i), u4 = total((2 * p + 1) * MB + i);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          float m = fabsf(h[q]);
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-          if ((lane & 15) == 0) gmax[wave][4 * (lane >> 4) + q] = m;
+          const int row = i * 16 + 4 * (lane >> 4) + q;
+          const float s_a = row < M ? sa[row] : 0.f;
+          float g = (float)g4[q] * s_a * pre.s0[o] + pre.b0[o];
+          float u = (float)u4[q] * s_a * pre.s1[o] + pre.b1[o];
+          g = bf2f(f2bf(g));                // the unfused GEMM output is bf16
+          u = bf2f(f2bf(u));
+          h[q] = g / (1.f + __expf(-g)) * u;
+          if constexpr (EPI == EPI_GLU)
+            if (row < M) reinterpret_cast<bf16_t*>(outv)[(size_t)row * Fo + feat] = f2bf(h[q]);
         }
       }
-      __syncthreads();
-      if (owner) {
-        const int grp = nt0 / 8;
+      if constexpr (EPI == EPI_GLUQ) {
+        // 4 pairs = 64 features share one scale per row
+        if (owner) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rr = 4 * (lane >> 4) + q, row = m0 + rr;
-          const float amax = fmaxf(fmaxf(fmaxf(gmax[0][rr], gmax[1][rr]), fmaxf(gmax[2][rr], gmax[3][rr])), 1e-8f);
-          if (row < M) hq[(size_t)row * F + f] = quant_i8(h[q], 127.f / amax);
-          if (wave == 0 && (lane & 15) == 0) os[(size_t)grp * Mpad + row] = row < M ? amax / 127.f : 0.f;
+          for (int q = 0; q < 4; ++q) {
+            float m = fabsf(h[q]);
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+            if ((lane & 15) == 0) gmax[i][p][4 * (lane >> 4) + q] = m;
+          }
+        }
+        __syncthreads();
+        if (owner) {
+          int8_t* hq = reinterpret_cast<int8_t*>(outv);
+          const int grp = nt0 / 8;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rr = 4 * (lane >> 4) + q, row = i * 16 + rr;
+            const float amax = fmaxf(fmaxf(fmaxf(gmax[i][0][rr], gmax[i][1][rr]), fmaxf(gmax[i][2][rr], gmax[i][3][rr])), 1e-8f);
+            if (row < M) hq[(size_t)row * Fo + feat] = quant_i8(h[q], 127.f / amax);
+            if (p == 0 && (lane & 15) == 0 && row < Mpad) os[(size_t)grp * Mpad + row] = row < M ? amax / 127.f : 0.f;
+          }
         }
       }
     }
   }
+}
+
+template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI>
+__global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                                 const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                                 const bf16_t* __restrict__ bias, void* __restrict__ outv,
+                                                                 float* __restrict__ os, int M, int N, int K, int KT,
+                                                                 int NTt, int Mpad) {
+  constexpr int NW = TG * KW, TPW = NTW / TG;
+  static_assert(NTW % TG == 0, "tiles split evenly over tile groups");
+  static_assert(EPI == EPI_OUT || (AMODE == A_TOKEN && TPW % 2 == 0), "GLU: gate/up pairs per wave, per-token A");
+  static_assert(EPI != EPI_GLUQ || (NTW == 8 && NW >= 4 * MB), "quantising GLU: 64 features, one pair per wave");
+  static_assert(KW * NTW * MB * 1024 <= 131072, "LDS reduction budget");
+  constexpr bool SCALED = AMODE == A_GROUP;
+  __shared__ v4i red[KW][NTW * MB][64];
+  __shared__ float gmax[MB][4][16];
+  const int nt0 = blockIdx.x * NTW;
+  // wave index in an SGPR: every k-loop guard below is then a scalar branch (an MFMA must never
+  // sit under an EXEC-masked branch — it ignores EXEC and would add a clamped duplicate k-tile)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = wave / KW, kw = wave % KW, t0 = tg * TPW;
+  const int akc = 16 * (lane >> 4);
+
+  const v4i* wp[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int nt = min(nt0 + t0 + j, NTt - 1);
+    wp[j] = reinterpret_cast<const v4i*>(Wp + ((size_t)nt * KT) * 1024) + lane;
+  }
+  const int8_t* ap[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) ap[i] = A + (size_t)min(i * 16 + (lane & 15), M - 1) * K;
+  const bool kfull = (K & 63) == 0;
+  const auto pre = epi_preload<MB, NTW, NW, EPI>(sw, bias, nt0, NTt, wave, lane);
+  v4i acc[TPW][MB];
+  v4f accf[TPW][MB];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int i = 0; i < MB; ++i) { acc[j][i] = v4i{0, 0, 0, 0}; accf[j][i] = v4f{0.f, 0.f, 0.f, 0.f}; }
+
+  struct Step {
+    v4i b[U][TPW];
+    v4i a[U][MB];
+    v4f sg[U][MB];
+  };
+  // one step = U k-tiles: weight fragments (nontemporal), activation fragments and (SCALED)
+  // per-group scales; clamped addresses, no branches
+  auto issue = [&](Step& st, int kbase) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j)
+        st.b[u][j] = __builtin_nontemporal_load(wp[j] + (size_t)min(kbase + u * KW, KT - 1) * 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = min(kbase + u * KW, KT - 1);
+#pragma unroll
+      for (int i = 0; i < MB; ++i) {
+        if (kfull) st.a[u][i] = *reinterpret_cast<const v4i*>(ap[i] + k * 64 + akc);
+        else st.a[u][i] = load_a_i8(ap[i], true, k, KT, akc, K, (K & 15) == 0);
+        if constexpr (SCALED)
+          st.sg[u][i] = *reinterpret_cast<const v4f*>(sa + (size_t)k * Mpad + min(i * 16, Mpad - 16) + 4 * (lane >> 4));
+      }
+    }
+  };
+  auto compute = [&](const Step& st, int kbase) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (kbase + u * KW < KT) {                         // wave-uniform tail guard
+#pragma unroll
+        for (int j = 0; j < TPW; ++j)
+#pragma unroll
+          for (int i = 0; i < MB; ++i) {
+            if constexpr (SCALED) fold(accf[j][i], mfma_i8(st.a[u][i], st.b[u][j], v4i{0, 0, 0, 0}), st.sg[u][i]);
+            else acc[j][i] = mfma_i8(st.a[u][i], st.b[u][j], acc[j][i]);
+          }
+      }
+    }
+  };
+  // one step of U k-tiles per iteration: all its loads in flight, then its MFMAs (16 waves per
+  // CU hide each other's latency; a two-buffer software pipeline measured slower here)
+  for (int kt = kw; kt < KT; kt += KW * U) {
+    Step st;
+    issue(st, kt);
+    compute(st, kt);
+  }
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+      red[kw][(t0 + j) * MB + i][lane] = SCALED ? __builtin_bit_cast(v4i, accf[j][i]) : acc[j][i];
+  __syncthreads();
+  gemv_epilogue<MB, NTW, NW, KW, SCALED, EPI>(&red[0][0][0], sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------ tiled
@@ -371,76 +400,41 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 }
 }  // namespace
 
-static int g_gemv_nw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_splitk = 0;
+static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0;
 // tuning hooks (microbenchmarks): 0 = automatic choice
-extern "C" void edge_w8a8_gemv_config(int nw, int unroll) { g_gemv_nw = nw; g_gemv_unroll = unroll; }
+extern "C" void edge_w8a8_gemv_config(int kw, int unroll) { g_gemv_kw = kw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
-extern "C" void edge_w8a8_splitk(int s) { g_splitk = s; }
 
-// Split-K scratch: one per device, allocated (and its counters zeroed) on first use outside a
-// graph capture; every launch leaves the counters at zero again.
 namespace {
-constexpr size_t kPartBytes = 16u << 20;
-constexpr int kCounters = 1 << 16;
-struct Scratch { v4i* part = nullptr; int* cnt = nullptr; };
-Scratch g_scratch[64];
-
-Scratch* scratch(hipStream_t st) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  Scratch& s = g_scratch[dev];
-  if (s.part != nullptr) return &s;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  void *p = nullptr, *c = nullptr;
-  if (hipMalloc(&p, kPartBytes) != hipSuccess) return nullptr;
-  if (hipMalloc(&c, kCounters * sizeof(int)) != hipSuccess || hipMemset(c, 0, kCounters * sizeof(int)) != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
-  }
-  s.part = (v4i*)p;
-  s.cnt = (int*)c;
-  return &s;
-}
-
-SplitK choose_split(int groups, int ntw, hipStream_t st) {
-  const int S = g_splitk > 0 ? g_splitk : 1;
-  if (S > 1) {
-    Scratch* sc = scratch(st);
-    if (sc != nullptr && (size_t)groups * S * ntw * 1024 <= kPartBytes && groups <= kCounters)
-      return SplitK{S, sc->part, sc->cnt};
-  }
-  return SplitK{1, nullptr, nullptr};
-}
-
-template <int AM, int EP>
-int launch_gemv(int un, int nw, int ntw, const void* A, const float* sa, const void* Wp, const float* sw,
-                const void* bias, void* out, float* os, int M, int N, int K, int KT, int Mpad, hipStream_t st) {
-  const int NTt = (N + 15) / 16, mblocks = (M + 15) / 16;
-  const int groups = ((NTt + ntw - 1) / ntw + 7) / 8 * 8 * mblocks;
-  const SplitK sk = choose_split(groups, ntw, st);
-  const dim3 g(groups * sk.S);
-#define L(U, NWV, NTWV) hipLaunchKernelGGL((w8a8_gemv_kernel<U, NWV, NTWV, AM, EP>), g, dim3(NWV * 64), 0, st, A, sa, \
-                                           (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, os, M, N, K, \
-                                           KT, NTt, Mpad, sk)
-#define BY_NTW(U, NWV)                                                   \
-  do {                                                                   \
-    if constexpr (EP == EPI_GLUQ) L(U, NWV, 8);                          \
-    else if (ntw >= 4) L(U, NWV, 4);                                     \
-    else if (ntw >= 2 || EP == EPI_GLU) L(U, NWV, 2);                    \
-    else if constexpr (EP == EPI_OUT) L(U, NWV, 1);                      \
-  } while (0)
-#define BY_NW(U)                                                         \
-  do {                                                                   \
-    if (nw >= 16 && EP == EPI_OUT) BY_NTW(U, 16);                        \
-    else if (nw >= 8) BY_NTW(U, 8);                                      \
-    else BY_NTW(U, 4);                                                   \
-  } while (0)
-  if (un >= 4) BY_NW(4); else BY_NW(2);
-#undef BY_NW
-#undef BY_NTW
-#undef L
+template <int MB, int NTW, int TG, int KW, int U, int AM, int EP>
+int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
+               int M, int N, int K, int KT, int Mpad, hipStream_t st) {
+  const int NTt = (N + 15) / 16;
+  hipLaunchKernelGGL((w8a8_gemv_kernel<MB, NTW, TG, KW, U, AM, EP>), dim3((NTt + NTW - 1) / NTW), dim3(TG * KW * 64), 0,
+                     st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, KT, NTt, Mpad);
   return (int)hipGetLastError();
+}
+
+// EPI_OUT: 16 waves; KW = 16 while the LDS reduction fits (KW x NTW x MB KiB <= 128 KiB), else 8
+template <int MB, int AM>
+int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const void* Wp, const float* sw,
+               const void* bias, void* out, int M, int N, int K, int KT, int Mpad, hipStream_t st) {
+#define L(NTWV, KWV, UV) return launch_one<MB, NTWV, 1, KWV, UV, AM, EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, \
+                                                                          KT, Mpad, st)
+#define BY_KW(NTWV, UV)                                                   \
+  do {                                                                    \
+    if constexpr (16 * NTWV * MB > 128 || MB > 1 || (AM == A_GROUP && NTWV >= 4)) L(NTWV, 8, UV); \
+    else { if (kw <= 8) L(NTWV, 8, UV); else L(NTWV, 16, UV); }           \
+  } while (0)
+  if (ntw <= 1) {
+    if constexpr (MB == 1) { if (un >= 4) BY_KW(1, 4); }
+    BY_KW(1, 2);
+  }
+  if (ntw == 2) BY_KW(2, 2);
+  if (ntw == 3) BY_KW(3, 2);
+  BY_KW(4, 2);
+#undef BY_KW
+#undef L
 }
 }  // namespace
 
@@ -457,15 +451,16 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   if (a_mode != A_TOKEN && (M > 64 || (a_mode == A_GROUP && Mpad < mblocks * 16))) return -2;
   if (epi == EPI_GLU || epi == EPI_GLUQ) {
     if (a_mode != A_TOKEN || M > 64 || N % (epi == EPI_GLUQ ? 128 : 32) != 0) return -2;
-    if (epi == EPI_GLUQ && (os == nullptr || Mpad < mblocks * 16)) return -2;
-    const int un = g_gemv_unroll > 0 ? g_gemv_unroll : 2;
-    // one gate/up pair per wave: 2 tiles (M <= 16) or 4 (activation fragments amortised over more
-    // weight tiles when several row blocks re-read the panel); the quantising form needs 8
-    int ntw = epi == EPI_GLUQ ? 8 : (g_gemv_ntw > 0 ? g_gemv_ntw : (mblocks > 1 ? 4 : 2));
-    int nw = g_gemv_nw > 0 ? g_gemv_nw : 4;
-    if (nw < ntw / 2) nw = ntw / 2;
-    if (epi == EPI_GLUQ) return launch_gemv<A_TOKEN, EPI_GLUQ>(un, nw, 8, A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
-    return launch_gemv<A_TOKEN, EPI_GLU>(un, nw, ntw, A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
+    if (epi == EPI_GLUQ) {
+      if (os == nullptr || Mpad < mblocks * 16) return -2;
+      // 8 tiles = 64 features; 16 waves as (TG tile groups) x (KW k-waves) within the LDS budget
+      if (mblocks <= 1) return launch_one<1, 8, 2, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      return launch_one<4, 8, 4, 4, 1, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+    }
+    if (mblocks <= 1) return launch_one<1, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
+    if (mblocks <= 2) return launch_one<2, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
+    return launch_one<4, 4, 2, 4, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
   }
   if (M > 64 && K % 64 == 0 && K / 64 == KT) {
     const int grid_n = (NTt * 16 + BN - 1) / BN;
@@ -474,21 +469,27 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
                        (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_n);
     return (int)hipGetLastError();
   }
-  // Defaults from the graph-timed cache-cold sweeps on MI355X (profiles/bench_ops_*.json):
-  //   M <= 2 : one n-tile per workgroup, unroll 4 (2 with scaled A), waves by K
-  //   M <= 16: unroll 2; N >= 16K columns: 2 n-tiles x 4 waves; 8K..16K: 4 n-tiles x 8 waves;
-  //            smaller N: 1 n-tile, 16 waves (K <= 8K) or 8 waves (larger K)
-  //   M in (16, 64]: 4 n-tiles per workgroup (activation fragments amortised)
-  const int un = g_gemv_unroll > 0 ? g_gemv_unroll : (M <= 2 && a_mode == A_TOKEN ? 4 : 2);
-  int ntw = 1;
-  if (g_gemv_ntw > 0) ntw = g_gemv_ntw;
-  else if (mblocks > 1) ntw = 4;
-  else if (M > 2 && NTt >= 1024) ntw = 2;
-  else if (M > 2 && NTt >= 512) ntw = 4;
-  int nw = g_gemv_nw > 0 ? g_gemv_nw : (KT >= 128 ? 16 : (KT >= 32 ? 8 : 4));
-  if (g_gemv_nw <= 0 && M > 2) nw = (NTt >= 1024) ? 4 : (NTt >= 512 ? 8 : (KT >= 128 ? 8 : 16));
-  if (nw >= 16 && (ntw >= 2 || un >= 4) && a_mode != A_TOKEN) nw = 8;     // 128-VGPR cap at 16 waves
-  if (a_mode == A_GROUP)
-    return launch_gemv<A_GROUP, EPI_OUT>(un, nw, ntw, A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
-  return launch_gemv<A_TOKEN, EPI_OUT>(un, nw, ntw, A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
+  if (M > 64) {
+    // ragged-K prefill (tiny models): 64-row slabs through the GEMV
+    for (int m0 = 0; m0 < M; m0 += 64) {
+      const int rc = edge_w8a8_gemm((const int8_t*)A + (size_t)m0 * K, sa + m0, Wp, sw, bias,
+                                    (bf16_t*)out + (size_t)m0 * N, nullptr, min(64, M - m0), N, K, KT, a_mode, 0, 0, st);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  // NTW tiles per workgroup so that the grid is ~256 workgroups (one 16-wave group per CU)
+  int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : (NTt >= 512 ? min(4, (NTt + 128) / 256) : 1);
+  const int un = g_gemv_unroll > 0 ? g_gemv_unroll : (ntw == 1 && KT >= 128 ? 4 : 2);
+  const int kw = g_gemv_kw > 0 ? g_gemv_kw : 16;
+#define OUT(MBV, AMV) return launch_out<MBV, AMV>(ntw, un, kw, A, sa, Wp, sw, bias, out, M, N, K, KT, Mpad, st)
+  if (a_mode == A_GROUP) {
+    if (mblocks <= 1) OUT(1, A_GROUP);
+    if (mblocks <= 2) OUT(2, A_GROUP);
+    OUT(4, A_GROUP);
+  }
+  if (mblocks <= 1) OUT(1, A_TOKEN);
+  if (mblocks <= 2) OUT(2, A_TOKEN);
+  OUT(4, A_TOKEN);
+#undef OUT
 }

@@ -78,6 +78,15 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     float* __restrict__ ys, bf16_t* __restrict__ res_out, int H, float eps) {
   __shared__ float red[NT / 64];
   const size_t row = blockIdx.x;
+  // gamma (and beta) chunks are loaded up front with the row, so no global load sits between
+  // the reductions and the output (one memory round trip per kernel)
+  uint4 wv[NCH], bv[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = min((c * NT + (int)threadIdx.x) * 8, H - 8);
+    wv[c] = *reinterpret_cast<const uint4*>(w + e);
+    if constexpr (!RMS) bv[c] = b != nullptr ? *reinterpret_cast<const uint4*>(b + e) : make_uint4(0, 0, 0, 0);
+  }
   float v[NCH][8];
   load_row<NCH>(x + row * H, H, v);
   if constexpr (HAS_RES) {
@@ -123,14 +132,8 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     const int e = (c * NT + threadIdx.x) * 8;
     if (e < H) {
       float wf[8], bfv[8];
-      unpack8(*reinterpret_cast<const uint4*>(w + e), wf);
-      if constexpr (!RMS) {
-        if (b != nullptr) unpack8(*reinterpret_cast<const uint4*>(b + e), bfv);
-        else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) bfv[j] = 0.f;
-        }
-      }
+      unpack8(wv[c], wf);
+      if constexpr (!RMS) unpack8(bv[c], bfv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = (v[c][j] - mean) * rstd * wf[j];

@@ -24,12 +24,11 @@ from .. import ops
 from ..ops import _ref
 from ..models.layers import GroupQuantBF16, Linear, QAct
 
-# Decode MLP policy (A/B on MI355X, Llama-2-7B): from this many rows up the gate_up GEMV
-# quantises silu(g) * u in its own epilogue (8 tiles = 64 features per workgroup, so several
-# row blocks share each activation fragment: +3% tok/s at B = 64); below it the GEMV writes bf16
-# h from 2-tile workgroups (more workgroups for the chip) and the group-quant kernel feeds the
-# down projection (+1% at B = 16).  EDGELLM_GLU_QUANT_MIN_ROWS overrides it.
-GLU_QUANT_MIN_ROWS = int(os.environ.get("EDGELLM_GLU_QUANT_MIN_ROWS", "17"))
+# Decode MLP policy (A/B on MI355X, Llama-2-7B, profiles/bench_ops_r1_gemv16.json): the gate_up
+# GEMV quantises silu(g) * u in its own epilogue (8 tiles = 64 features per workgroup) for every
+# decode batch — 21.7 us vs 26.5 us for bf16 h + the group-quant kernel at 16 rows, and ahead at
+# 1, 33 and 64 rows too.  EDGELLM_GLU_QUANT_MIN_ROWS raises the threshold (A/B runs).
+GLU_QUANT_MIN_ROWS = int(os.environ.get("EDGELLM_GLU_QUANT_MIN_ROWS", "1"))
 
 
 def glu_quant_rows(m: int) -> bool:

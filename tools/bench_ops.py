@@ -54,7 +54,7 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True, grouped=False, shapes=None):
     out = []
     variants = [(0, 0, 0)]
     if sweep:
-        variants += [(nw, u, ntw) for nw in (4, 8, 16) for u in (2, 4, 8) for ntw in (1, 2, 4)]
+        variants += [(kw, u, ntw) for kw in (8, 16) for u in (2, 4) for ntw in (1, 2, 3, 4)]
     for name, (N, K) in shapes.items():
         # cache-cold: rotate through enough packed copies (> 1 GiB) that no call finds its weights
         # in the 256 MiB Infinity Cache — the decode regime, where 6.7 GB stream once per step
@@ -75,7 +75,7 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True, grouped=False, shapes=None):
 
             for rnd in range(2):  # interleaved rounds
                 for nw, u, ntw in variants:
-                    if u == 8 and (M > 16 or ntw > 1):
+                    if u == 4 and (M > 16 or ntw > 1):
                         continue
                     C.tune("gemv", nw, u)
                     C.tune("gemv_ntw", ntw, 0)
@@ -90,49 +90,6 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True, grouped=False, shapes=None):
                             auto_us=round(auto, 2),
                             auto_TBps=round(nbytes / auto / 1e6, 2), best=list(best),
                             best_us=round(min(res[best]), 2), best_TBps=round(nbytes / min(res[best]) / 1e6, 2)))
-            print(out[-1], flush=True)
-    return out
-
-
-def splitk_rows(C, dev, Ms=(1, 16, 64)):
-    """Split-K x tiles-per-workgroup sweep (cache-cold) at the decode projection shapes: qkv and
-    gate_up read per-token scales, o and down per-group scales (as after the fused producers)."""
-    shapes = {"qkv": (12288, 4096, False), "o": (4096, 4096, True), "gate_up": (22016, 4096, False),
-              "down": (4096, 11008, True)}
-    out = []
-    variants = [(nw, ntw, S) for nw in (4, 8) for ntw in (1, 2, 4) for S in (1, 2, 4, 8)]
-    for name, (N, K, grouped) in shapes.items():
-        ncopy = max(2, (1 << 30) // (N * K) + 1)
-        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
-        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
-        sw = torch.rand(N, device=dev) * 0.01
-        for M in Ms:
-            qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-            sx = (torch.rand((K + 63) // 64, (M + 15) // 16 * 16, device=dev) if grouped
-                  else torch.rand(M, device=dev)) * 0.01
-            ctr = [0]
-
-            def call():
-                ctr[0] = (ctr[0] + 1) % ncopy
-                return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
-
-            res = {}
-            C.w8a8_gemm(qx, sx, wps[0], sw, None, N, K)     # scratch allocated outside capture
-            for rnd in range(2):
-                for v in [(0, 0, 0)] + variants:
-                    nw, ntw, S = v
-                    C.tune("gemv", nw, 0)
-                    C.tune("gemv_ntw", ntw, 0)
-                    C.tune("splitk", S, 0)
-                    if S > 1:
-                        call()
-                    res.setdefault(v, []).append(timeit(call, iters=10, per_graph=ncopy))
-            C.tune("gemv", 0, 0)
-            C.tune("gemv_ntw", 0, 0)
-            C.tune("splitk", 0, 0)
-            ranked = sorted(res, key=lambda k: min(res[k]))
-            out.append(dict(op="gemv_splitk", shape=name, M=M, N=N, K=K, auto_us=round(min(res[(0, 0, 0)]), 2),
-                            top=[(list(k), round(min(res[k]), 2)) for k in ranked[:5]]))
             print(out[-1], flush=True)
     return out
 
@@ -160,8 +117,7 @@ def glu_rows(C, dev, Ms=(1, 16, 33, 64)):
             ctr[0] = (ctr[0] + 1) % ncopy
             return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
 
-        variants = [("bf16+group_quant", bf16_then_quant, ntw, nw) for ntw in (2, 4) for nw in (4, 8)]
-        variants += [("quant_epilogue", quant_epilogue, 8, nw) for nw in (4, 8)]
+        variants = [("bf16+group_quant", bf16_then_quant, 0, 0), ("quant_epilogue", quant_epilogue, 0, 0)]
         res = {}
         for rnd in range(2):
             for name, fn, ntw, nw in variants:
@@ -279,7 +235,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--tune", action="append", default=[], help="name=a[,b] passed to ext().tune (repeatable)")
-    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,splitk,glu,attn,small,sample,prefill")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,small,sample,prefill")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
@@ -292,8 +248,6 @@ def main():
     if only is None or "grouped" in only:
         rows += gemv_rows(C, dev, sweep=not a.no_sweep, grouped=True,
                           shapes={"o": (4096, 4096), "down": (4096, 11008)})
-    if only is not None and "splitk" in only:
-        rows += splitk_rows(C, dev)
     if only is None or "glu" in only:
         rows += glu_rows(C, dev)
     rows += other_rows(C, dev, only)
