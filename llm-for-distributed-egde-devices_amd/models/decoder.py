@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from .. import ops
 from .configs import ModelConfig
-from .layers import Linear, Norm, QAct, act_fn, quant_if
+from .layers import Linear, Norm, PartialSum, QAct, act_fn, quant_if
 
 
 @dataclass
@@ -202,6 +202,8 @@ class DecoderLM(nn.Module):
     def head(self, x: torch.Tensor, residual: Optional[torch.Tensor], ctx: AttnCtx,
              logits: str = "last") -> torch.Tensor:
         """Final norm + LM head. logits: "last" (one row per sequence) or "all"."""
+        if isinstance(x, PartialSum) and logits == "last" and ctx.T > 1:
+            x = x.materialize()
         if logits == "last" and ctx.T > 1:
             idx = torch.arange(ctx.B, device=x.device) * ctx.T + (ctx.T - 1)
             x = x.index_select(0, idx)
@@ -218,6 +220,8 @@ class DecoderLM(nn.Module):
         x, residual = self.forward_layers(x, ctx, None)
         if self.has_head:
             return self.head(x, residual, ctx, logits)
+        if isinstance(x, PartialSum):
+            x = x.materialize()
         return x + residual if residual is not None else x
 
 

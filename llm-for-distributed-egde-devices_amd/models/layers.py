@@ -25,6 +25,19 @@ class QAct(NamedTuple):
     scale: torch.Tensor
 
 
+class PartialSum(NamedTuple):
+    """Split-K output of a W8A8 decode projection: fp32 slices [S, M, N] whose in-order sum,
+    rounded to bf16, is the projection's output.  RMSNorm consumes it directly (one kernel
+    adds the slices); anything else calls ``materialize()``."""
+    parts: torch.Tensor
+
+    def materialize(self) -> torch.Tensor:
+        acc = self.parts[0].clone()
+        for s in range(1, self.parts.shape[0]):      # same order as the norm kernel
+            acc += self.parts[s]
+        return acc.to(torch.bfloat16)
+
+
 class GroupQuantBF16(NamedTuple):
     """bf16 activation that a W8A8 consumer quantises per (token, 64 columns) on the fly."""
     x: torch.Tensor
@@ -62,7 +75,13 @@ class Norm(nn.Module):
                      if kind == "layer" else None)
 
     def forward(self, x, residual=None, quant: bool = False):
-        """Returns (y, residual_out) where residual_out = x + residual; y is a QAct when quant."""
+        """Returns (y, residual_out) where residual_out = x + residual; y is a QAct when quant.
+        ``x`` may be a PartialSum (split-K projection output), summed inside the norm kernel."""
+        if isinstance(x, PartialSum):
+            if self.kind == "rms" and x.parts.is_cuda and ops.gpu_path(x.parts):
+                y, s, r = ops.rms_norm_parts(x.parts, residual, self.weight, self.eps, quant)
+                return (QAct(y, s) if quant else y), r
+            x = x.materialize()
         if self.kind == "rms":
             if quant:
                 q, s, r = ops.rms_norm_quant(x, self.weight, self.eps, residual)

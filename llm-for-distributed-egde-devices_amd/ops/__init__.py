@@ -55,6 +55,22 @@ def _gpu(t: torch.Tensor) -> bool:
 # --------------------------------------------------------------------------- norms
 
 
+def gpu_path(t: torch.Tensor) -> bool:
+    """True when ``t`` runs through the HIP kernels (not the reference ops)."""
+    return _gpu(t)
+
+
+def rms_norm_parts(parts, residual, weight, eps, quant: bool):
+    """RMSNorm of the in-order sum of split-K partial slices parts [S, M, H] (fp32) rounded to bf16
+    (+ residual): returns (y bf16 | q int8, per-token scale | None, h = bf16 sum (+ residual))."""
+    return ext().rms_norm_parts(parts, residual, weight, eps, quant)
+
+
+def w8a8_linear_splitk(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, splits: int = 0):
+    """Split-K W8A8 GEMV (GPU, M <= 64, K % 64 == 0): fp32 partial slices [S, M, N]."""
+    return ext().w8a8_gemm_splitk(qx, x_scale, w_packed, w_scale, bias, N, K, splits)
+
+
 def rms_norm(x, weight, eps, residual=None):
     if _gpu(x):
         y, _, r = ext().norm(x, residual, weight, None, eps, True, False)

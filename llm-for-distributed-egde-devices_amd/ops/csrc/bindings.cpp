@@ -11,7 +11,10 @@
 
 extern "C" {
 int edge_norm(const void* x, const void* res, const void* w, const void* b, void* y, void* yq, float* ys,
-              void* res_out, int rows, int H, float eps, int rms, int quant, hipStream_t st);
+              void* res_out, int rows, int H, float eps, int rms, int quant, const float* xpart, int S,
+              hipStream_t st);
+int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
+                          float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S, hipStream_t st);
 int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant, hipStream_t st);
 int edge_quant(const void* x, void* q, float* s, int rows, int H, hipStream_t st);
 int edge_group_quant(const void* x, void* q, float* s, int M, int K, int Mpad, hipStream_t st);
@@ -89,10 +92,41 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
   check(edge_norm(x.data_ptr(), residual ? residual->data_ptr() : nullptr, w.data_ptr(),
                   b ? b->data_ptr() : nullptr, quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr,
                   quant ? s.data_ptr<float>() : nullptr, residual ? res_out.data_ptr() : nullptr, (int)R, (int)H,
-                  (float)eps, rms, quant, stream()),
+                  (float)eps, rms, quant, nullptr, 0, stream()),
         "norm");
   return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
 }
+
+// RMSNorm whose input is S fp32 split-K partial slices [S, M, H] of a W8A8 projection (summed in
+// slice order, rounded to bf16): returns (y or q, scale, h) with h = bf16(sum) (+ residual).
+std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(const at::Tensor& parts,
+                                                                              const std::optional<at::Tensor>& residual,
+                                                                              const at::Tensor& w, double eps, bool quant) {
+  need(parts, at::kFloat, "parts");
+  need(w, at::kBFloat16, "weight");
+  TORCH_CHECK(parts.dim() == 3, "parts must be [S, M, H]");
+  const int64_t S = parts.size(0), R = parts.size(1), H = parts.size(2);
+  TORCH_CHECK(w.numel() == H, "norm weight size mismatch");
+  auto opts = w.options();
+  at::Tensor res_out = at::empty({R, H}, opts);
+  if (residual) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == R * H, "residual shape mismatch");
+  }
+  at::Tensor y, s;
+  if (quant) {
+    y = at::empty({R, H}, opts.dtype(at::kChar));
+    s = at::empty({R}, opts.dtype(at::kFloat));
+  } else {
+    y = at::empty({R, H}, opts);
+  }
+  check(edge_norm(nullptr, residual ? residual->data_ptr() : nullptr, w.data_ptr(), nullptr,
+                  quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr, quant ? s.data_ptr<float>() : nullptr,
+                  res_out.data_ptr(), (int)R, (int)H, (float)eps, 1, quant, parts.data_ptr<float>(), (int)S, stream()),
+        "rms_norm_parts");
+  return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
+}
+
 
 // ---------------------------------------------------------------------------------- activations
 std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64_t mode, bool quant) {
@@ -339,6 +373,29 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
   return out;
 }
 
+// Split-K W8A8 GEMV (decode, M <= 64): fp32 partial slices [S, M, N] (w-scale and bias applied; bias
+// in slice 0) for a consumer that sums them (rms_norm_parts).  S = 0 picks the split count.
+at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
+                            const std::optional<at::Tensor>& bias, int64_t N, int64_t K, int64_t S) {
+  need(a, at::kChar, "a");
+  TORCH_CHECK(a.size(-1) == K && K % 64 == 0, "split-K GEMV needs K % 64 == 0");
+  check_w8a8_operands(wp, sw, bias, N, K);
+  const int64_t M = rows_of(a), KT = K / 64;
+  TORCH_CHECK(M <= 64, "split-K GEMV is a decode (M <= 64) kernel");
+  const int64_t mpad = a_scale_mpad(sa, M, KT);
+  if (S <= 0) {
+    const int64_t groups = ((N + 15) / 16 + 3) / 4;
+    S = std::max<int64_t>(1, std::min<int64_t>(8, (256 + groups / 2) / groups));
+  }
+  S = std::min<int64_t>(S, KT);
+  auto part = at::empty({S, M, N}, a.options().dtype(at::kFloat));
+  check(edge_w8a8_gemm_splitk(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                              bias ? bias->data_ptr() : nullptr, part.data_ptr<float>(), (int)M, (int)N, (int)K,
+                              (int)KT, mpad > 0 ? 1 : 0, (int)mpad, (int)S, stream()),
+        "w8a8_gemm_splitk");
+  return part;
+}
+
 // Per-(token, 64 columns) int8 quantisation: (q [M, K], scales [K/64, Mpad]).
 std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
   need(x, at::kBFloat16, "x");
@@ -450,6 +507,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm", &w8a8_gemm);
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
+  m.def("w8a8_gemm_splitk", &w8a8_gemm_splitk);
+  m.def("rms_norm_parts", &rms_norm_parts);
   m.def("w8a8_gemm_gluq", &w8a8_gemm_gluq);
   m.def("group_quant", &group_quant);
   m.def("sample", &sample);

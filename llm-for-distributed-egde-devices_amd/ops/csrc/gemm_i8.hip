@@ -33,7 +33,7 @@
 namespace {
 constexpr int NT = 256;
 constexpr int A_TOKEN = 0, A_GROUP = 1;
-constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GLUQ = 2;
+constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GLUQ = 2, EPI_PART = 3;
 
 __device__ __forceinline__ v4i mfma_i8(const v4i& a, const v4i& b, const v4i& c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
@@ -99,7 +99,7 @@ struct EpiPre {
 };
 
 template <int MB, int NTW, int NW, int EPI>
-constexpr int epi_units() { return EPI == EPI_OUT ? NTW * MB : NTW / 2 * MB; }
+constexpr int epi_units() { return (EPI == EPI_OUT || EPI == EPI_PART) ? NTW * MB : NTW / 2 * MB; }
 
 template <int MB, int NTW, int NW, int EPI>
 __device__ __forceinline__ EpiPre<(epi_units<MB, NTW, NW, EPI>() + NW - 1) / NW> epi_preload(
@@ -109,16 +109,17 @@ __device__ __forceinline__ EpiPre<(epi_units<MB, NTW, NW, EPI>() + NW - 1) / NW>
 #pragma unroll
   for (int o = 0; o < OWN; ++o) {
     const int u = wave + o * NW;
-    const int t = EPI == EPI_OUT ? u / MB : 2 * (u / MB);          // (gate) tile
-    const bool ok = u < UNITS && nt0 + t + (EPI == EPI_OUT ? 0 : 1) < NTt;
+    constexpr bool PAIR = EPI == EPI_GLU || EPI == EPI_GLUQ;
+    const int t = PAIR ? 2 * (u / MB) : u / MB;                      // (gate) tile
+    const bool ok = u < UNITS && nt0 + t + (PAIR ? 1 : 0) < NTt;
     (void)ok;                                   // out-of-range units are never stored: clamp, no branch
     const int N = NTt * 16;
     const int c0 = min((nt0 + t) * 16 + (lane & 15), N - 1), c1 = min(c0 + 16, N - 1);
     p.s0[o] = sw[c0];
-    p.s1[o] = EPI != EPI_OUT ? sw[c1] : 0.f;
+    p.s1[o] = PAIR ? sw[c1] : 0.f;
     const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;   // absent bias: read a zero word
     p.b0[o] = bf2f(bp[bias != nullptr ? c0 : 0]);
-    p.b1[o] = EPI != EPI_OUT ? bf2f(bp[bias != nullptr ? c1 : 0]) : 0.f;
+    p.b1[o] = PAIR ? bf2f(bp[bias != nullptr ? c1 : 0]) : 0.f;
   }
   return p;
 }
@@ -129,7 +130,7 @@ __device__ __forceinline__ EpiPre<(epi_units<MB, NTW, NW, EPI>() + NW - 1) / NW>
 template <int MB, int NTW, int NW, int KW, bool SCALED, int EPI, int OWN>
 __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const float* sa, const EpiPre<OWN>& pre,
                                               void* __restrict__ outv, float* __restrict__ os, float (*gmax)[4][16],
-                                              int M, int N, int NTt, int Mpad, int nt0, int wave, int lane) {
+                                              int M, int N, int NTt, int Mpad, int nt0, int wave, int lane, int ks = 0) {
   constexpr int F = NTW * MB;
   auto total = [&](int f) -> v4i {
     if constexpr (SCALED) {
@@ -144,7 +145,25 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
       return s;
     }
   };
-  if constexpr (EPI == EPI_OUT) {
+  if constexpr (EPI == EPI_PART) {
+    float* part = reinterpret_cast<float*>(outv) + (size_t)ks * M * N;
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      const int f = wave + o * NW;
+      const int t = f / MB, i = f % MB;
+      if (f >= F || nt0 + t >= NTt) continue;
+      const v4i tot = total(f);
+      const int col = (nt0 + t) * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = i * 16 + 4 * (lane >> 4) + q;
+        if (row < M && col < N) {
+          const float v = SCALED ? __builtin_bit_cast(v4f, tot)[q] : (float)tot[q] * sa[row];
+          part[(size_t)row * N + col] = v * pre.s0[o] + (ks == 0 ? pre.b0[o] : 0.f);
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_OUT) {
     bf16_t* out = reinterpret_cast<bf16_t*>(outv);
 #pragma unroll
     for (int o = 0; o < OWN; ++o) {
@@ -224,16 +243,23 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
                                                                  const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                  const bf16_t* __restrict__ bias, void* __restrict__ outv,
                                                                  float* __restrict__ os, int M, int N, int K, int KT,
-                                                                 int NTt, int Mpad) {
+                                                                 int NTt, int Mpad, int S) {
   constexpr int NW = TG * KW, TPW = NTW / TG;
   static_assert(NTW % TG == 0, "tiles split evenly over tile groups");
-  static_assert(EPI == EPI_OUT || (AMODE == A_TOKEN && TPW % 2 == 0), "GLU: gate/up pairs per wave, per-token A");
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && TPW % 2 == 0),
+                "GLU: gate/up pairs per wave, per-token A");
   static_assert(EPI != EPI_GLUQ || (NTW == 8 && NW >= 4 * MB), "quantising GLU: 64 features, one pair per wave");
   static_assert(KW * NTW * MB * 1024 <= 131072, "LDS reduction budget");
   constexpr bool SCALED = AMODE == A_GROUP;
   __shared__ v4i red[KW][NTW * MB][64];
   __shared__ float gmax[MB][4][16];
-  const int nt0 = blockIdx.x * NTW;
+  // EPI_PART (split-K): workgroup (group, s) reduces k-tiles [KT*s/S, KT*(s+1)/S) of its tiles and
+  // writes fp32 partial sums part[s][M][N]; the consumer (norm kernel) adds the S slices in order
+  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
+  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
+  const int kbeg = EPI == EPI_PART ? (int)((int64_t)KT * ks / S) : 0;
+  const int kend = EPI == EPI_PART ? (int)((int64_t)KT * (ks + 1) / S) : KT;
+  const int nt0 = grp * NTW;
   // wave index in an SGPR: every k-loop guard below is then a scalar branch (an MFMA must never
   // sit under an EXEC-masked branch — it ignores EXEC and would add a clamped duplicate k-tile)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -270,10 +296,10 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < TPW; ++j)
-        st.b[u][j] = __builtin_nontemporal_load(wp[j] + (size_t)min(kbase + u * KW, KT - 1) * 64);
+        st.b[u][j] = __builtin_nontemporal_load(wp[j] + (size_t)min(kbase + u * KW, kend - 1) * 64);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = min(kbase + u * KW, KT - 1);
+      const int k = min(kbase + u * KW, kend - 1);
 #pragma unroll
       for (int i = 0; i < MB; ++i) {
         if (kfull) st.a[u][i] = *reinterpret_cast<const v4i*>(ap[i] + k * 64 + akc);
@@ -286,7 +312,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto compute = [&](const Step& st, int kbase) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (kbase + u * KW < KT) {                         // wave-uniform tail guard
+      if (kbase + u * KW < kend) {                       // wave-uniform tail guard
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
 #pragma unroll
@@ -299,7 +325,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   };
   // one step of U k-tiles per iteration: all its loads in flight, then its MFMAs (16 waves per
   // CU hide each other's latency; a two-buffer software pipeline measured slower here)
-  for (int kt = kw; kt < KT; kt += KW * U) {
+  for (int kt = kbeg + kw; kt < kend; kt += KW * U) {
     Step st;
     issue(st, kt);
     compute(st, kt);
@@ -310,7 +336,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     for (int i = 0; i < MB; ++i)
       red[kw][(t0 + j) * MB + i][lane] = SCALED ? __builtin_bit_cast(v4i, accf[j][i]) : acc[j][i];
   __syncthreads();
-  gemv_epilogue<MB, NTW, NW, KW, SCALED, EPI>(&red[0][0][0], sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane);
+  gemv_epilogue<MB, NTW, NW, KW, SCALED, EPI>(&red[0][0][0], sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane,
+                                              ks);
 }
 
 // ------------------------------------------------------------------------------------ tiled
@@ -408,10 +435,11 @@ extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
 namespace {
 template <int MB, int NTW, int TG, int KW, int U, int AM, int EP>
 int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
-               int M, int N, int K, int KT, int Mpad, hipStream_t st) {
+               int M, int N, int K, int KT, int Mpad, hipStream_t st, int S = 1) {
   const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_kernel<MB, NTW, TG, KW, U, AM, EP>), dim3((NTt + NTW - 1) / NTW), dim3(TG * KW * 64), 0,
-                     st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, KT, NTt, Mpad);
+  hipLaunchKernelGGL((w8a8_gemv_kernel<MB, NTW, TG, KW, U, AM, EP>), dim3((NTt + NTW - 1) / NTW * S), dim3(TG * KW * 64),
+                     0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, KT, NTt,
+                     Mpad, S);
   return (int)hipGetLastError();
 }
 
@@ -423,7 +451,7 @@ int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const vo
                                                                           KT, Mpad, st)
 #define BY_KW(NTWV, UV)                                                   \
   do {                                                                    \
-    if constexpr (16 * NTWV * MB > 128 || MB > 1 || (AM == A_GROUP && NTWV >= 4)) L(NTWV, 8, UV); \
+    if constexpr (16 * NTWV * MB > 128 || MB > 2 || (AM == A_GROUP && (NTWV >= 4 || (MB > 1 && NTWV > 2)))) L(NTWV, 8, UV); \
     else { if (kw <= 8) L(NTWV, 8, UV); else L(NTWV, 16, UV); }           \
   } while (0)
   if (ntw <= 1) {
@@ -437,6 +465,30 @@ int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const vo
 #undef L
 }
 }  // namespace
+
+// Split-K GEMV (M <= 64, K % 64 == 0): S workgroups per 4-tile group, each reducing KT/S k-tiles
+// into fp32 partial slices part[S][M][N].  Cuts each workgroup's activation reads S-fold — at
+// decode shapes every CU re-reads the whole activation matrix from L2, and those bytes share the
+// CU's load path with the weight stream (tools/membw.hip "a" mode: +1 L2 byte per weight byte
+// costs +13 % time at 50 MB).  The consumer adds the slices (rowwise.hip norm_kernel<PART>).
+extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
+                                     float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S,
+                                     hipStream_t st) {
+  if (M <= 0 || M > 64 || K % 64 != 0 || K / 64 != KT || S < 1 || S > KT) return -2;
+  const int mblocks = (M + 15) / 16;
+  if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
+#define SK(MBV, KWV, AMV) return launch_one<MBV, 4, 1, KWV, 2, AMV, EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, \
+                                                                          KT, Mpad, st, S)
+  if (a_mode == A_GROUP) {
+    if (mblocks <= 1) SK(1, 16, A_GROUP);
+    if (mblocks <= 2) SK(2, 8, A_GROUP);
+    SK(4, 8, A_GROUP);
+  }
+  if (mblocks <= 1) SK(1, 16, A_TOKEN);
+  if (mblocks <= 2) SK(2, 16, A_TOKEN);
+  SK(4, 8, A_TOKEN);
+#undef SK
+}
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).
 // epi 1: fused SwiGLU on 16-blocked gate/up rows, `out` is bf16 [M, N/2] (a_mode 0, M <= 64).

@@ -71,11 +71,15 @@ __device__ __forceinline__ void quant_store(float (&v)[NCH][8], int H, int8_t* _
 }
 
 // ----------------------------------------------------------------------------- norms
-template <int NCH, bool RMS, bool HAS_RES, bool QUANT>
+// PART: x arrives as S fp32 split-K partial slices [S][rows][H] of a W8A8 projection
+// (gemm_i8.hip EPI_PART); they are summed in slice order and rounded to bf16 — the value the
+// unsplit GEMV would have written — and that bf16 row is always written to res_out.
+template <int NCH, bool RMS, bool HAS_RES, bool QUANT, bool PART>
 __global__ void __launch_bounds__(NT) norm_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ b, bf16_t* __restrict__ y, int8_t* __restrict__ yq,
-    float* __restrict__ ys, bf16_t* __restrict__ res_out, int H, float eps) {
+    float* __restrict__ ys, bf16_t* __restrict__ res_out, int H, float eps, const float* __restrict__ xpart,
+    int S) {
   __shared__ float red[NT / 64];
   const size_t row = blockIdx.x;
   // gamma (and beta) chunks are loaded up front with the row, so no global load sits between
@@ -88,7 +92,27 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     if constexpr (!RMS) bv[c] = b != nullptr ? *reinterpret_cast<const uint4*>(b + e) : make_uint4(0, 0, 0, 0);
   }
   float v[NCH][8];
-  load_row<NCH>(x + row * H, H, v);
+  if constexpr (PART) {
+    const size_t slice = (size_t)gridDim.x * H;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * NT + threadIdx.x) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      if (e < H) {
+        for (int k = 0; k < S; ++k) {
+          const float4* p = reinterpret_cast<const float4*>(xpart + k * slice + row * H + e);
+          const float4 p0 = p[0], p1 = p[1];
+          v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
+          v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
+        }
+        unpack8(pack8(v[c]), v[c]);                        // the GEMV output is bf16
+        if constexpr (!HAS_RES) *reinterpret_cast<uint4*>(res_out + row * H + e) = pack8(v[c]);
+      }
+    }
+  } else {
+    load_row<NCH>(x + row * H, H, v);
+  }
   if constexpr (HAS_RES) {
     float r[NCH][8];
     load_row<NCH>(res + row * H, H, r);
@@ -264,16 +288,24 @@ __global__ void __launch_bounds__(NT) max_prob_kernel(const void* __restrict__ l
 
 extern "C" int edge_norm(const void* x, const void* res, const void* w, const void* b, void* y, void* yq,
                          float* ys, void* res_out, int rows, int H, float eps, int rms, int quant,
-                         hipStream_t st) {
+                         const float* xpart, int S, hipStream_t st) {
   if (H % 8) return -2;
+  if (xpart != nullptr && (!rms || res_out == nullptr || S < 1)) return -2;
   if (rows == 0) return 0;
   const bf16_t *X = (const bf16_t*)x, *R = (const bf16_t*)res, *W = (const bf16_t*)w, *Bb = (const bf16_t*)b;
   bf16_t *Y = (bf16_t*)y, *RO = (bf16_t*)res_out;
   int8_t* Q = (int8_t*)yq;
 #define LAUNCH_NORM(RMS, HR, QU) \
-  hipLaunchKernelGGL((norm_kernel<NCH, RMS, HR, QU>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, eps)
+  hipLaunchKernelGGL((norm_kernel<NCH, RMS, HR, QU, false>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, \
+                     eps, nullptr, 0)
+#define LAUNCH_NORMP(HR, QU) \
+  hipLaunchKernelGGL((norm_kernel<NCH, true, HR, QU, true>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, \
+                     eps, xpart, S)
   NCH_DISPATCH(H, {
-    if (rms) {
+    if (xpart != nullptr) {
+      if (res) { if (quant) LAUNCH_NORMP(true, true); else LAUNCH_NORMP(true, false); }
+      else { if (quant) LAUNCH_NORMP(false, true); else LAUNCH_NORMP(false, false); }
+    } else if (rms) {
       if (res) { if (quant) LAUNCH_NORM(true, true, true); else LAUNCH_NORM(true, true, false); }
       else { if (quant) LAUNCH_NORM(true, false, true); else LAUNCH_NORM(true, false, false); }
     } else {
@@ -282,6 +314,7 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
     }
   });
 #undef LAUNCH_NORM
+#undef LAUNCH_NORMP
   return (int)hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops import _ref
-from ..models.layers import GroupQuantBF16, Linear, QAct
+from ..models.layers import GroupQuantBF16, Linear, PartialSum, QAct
 
 # Decode MLP policy (A/B on MI355X, Llama-2-7B, profiles/bench_ops_r1_gemv16.json): the gate_up
 # GEMV quantises silu(g) * u in its own epilogue (8 tiles = 64 features per workgroup) for every
@@ -58,6 +58,7 @@ class W8A8Linear(nn.Module):
         self._w_cpu = None
         self.out_dtype = dtype
         self.glu_blocked = False      # rows stored 16-blocked [gate(16) | up(16)] (fused decode GLU)
+        self.split_k_out = 0          # > 0: decode output as split-K PartialSum (consumer is an RMSNorm)
 
     @classmethod
     @torch.no_grad()
@@ -120,6 +121,9 @@ class W8A8Linear(nn.Module):
         K, N = self.in_features, self.out_features
         shp = x.q.shape[:-1]
         scale = x.scale if x.scale.dim() == 2 and x.q.dim() == 2 else x.scale.reshape(-1)
+        if self.split_k_out and x.q.is_cuda and ops.gpu_path(x.q) and K % 64 == 0 and 0 < x.q.numel() // K <= 64:
+            return PartialSum(ops.w8a8_linear_splitk(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale,
+                                                     self.bias, N, K, self.split_k_out if self.split_k_out > 1 else 0))
         out = ops.w8a8_linear(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale, self.bias,
                               N, K, w_ref=self._wref(x.q), out_dtype=self.out_dtype)
         return out.view(*shp, N)
@@ -228,12 +232,32 @@ def enable_fused_glu(model) -> int:
     as GEMV+SwiGLU -> down GEMV with in-kernel per-group quant (two launches instead of three).
     Returns the number of layers changed."""
     cfg = model.cfg
-    if not (cfg.is_glu and cfg.act == "silu_glu" and cfg.intermediate_size % 64 == 0):
+    n = 0
+    if cfg.is_glu and cfg.act == "silu_glu" and cfg.intermediate_size % 64 == 0:
+        for layer in model.layers:
+            up = layer.mlp.up
+            if isinstance(up, W8A8Linear) and isinstance(layer.mlp.down, W8A8Linear) and not up.glu_blocked:
+                up.block_glu_()
+                n += 1
+    enable_split_k_outputs(model)
+    return n
+
+
+# EDGELLM_SPLITK=0 turns the split-K decode outputs off (A/B runs)
+SPLIT_K = os.environ.get("EDGELLM_SPLITK", "1") != "0"
+
+
+def enable_split_k_outputs(model) -> int:
+    """Sequential-residual RMSNorm decoders (Llama): the o and down projections feed an RMSNorm
+    (or the stage exit), so on GPU their decode GEMVs emit split-K partial slices that the norm
+    kernel sums — each workgroup then reads 1/S of the activation matrix instead of all of it."""
+    cfg = model.cfg
+    if not SPLIT_K or cfg.parallel_residual or cfg.norm != "rms":
         return 0
     n = 0
     for layer in model.layers:
-        up = layer.mlp.up
-        if isinstance(up, W8A8Linear) and isinstance(layer.mlp.down, W8A8Linear) and not up.glu_blocked:
-            up.block_glu_()
-            n += 1
+        for lin in (layer.attn.o, layer.mlp.down):
+            if isinstance(lin, W8A8Linear) and lin.in_features % 64 == 0:
+                lin.split_k_out = 1
+                n += 1
     return n

@@ -181,3 +181,69 @@ def test_glu_forms_agree(cuda, M):
     deq = q.float().view(M, F // 64, 64) * step
     err = (deq - ref.float().view(M, F // 64, 64)).abs()
     assert (err <= 0.51 * step + 1e-2 * ref.float().view(M, F // 64, 64).abs() + 1e-3).all(), err.max().item()
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 32, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (2048, 8192), (1040, 1024)])
+@pytest.mark.parametrize("grouped", [False, True])
+def test_gemv_split_k_partials(cuda, M, N, K, grouped):
+    """Split-K partial slices: their in-order sum equals the unsplit GEMV (fp32 tolerance), and
+    the bf16 rounding of that sum equals the unsplit bf16 output to one ulp."""
+    C = ops.ext()
+    torch.manual_seed(M + N)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = (torch.rand(K // 64, (M + 15) // 16 * 16, device=cuda) if grouped else torch.rand(M, device=cuda)) * 0.02
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.02 + 1e-3
+    bias = torch.randn(N, device=cuda).bfloat16()
+    wp = ops.pack_int8_weight(w)
+    parts = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, 0)
+    assert parts.dim() == 3 and parts.shape[1:] == (M, N) and 1 <= parts.shape[0] <= 8
+    from edgellm.models.layers import PartialSum
+    y = PartialSum(parts).materialize()
+    ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
+    _close(parts.sum(0), ref, 1e-2, 1e-4)
+    _close(y, C.w8a8_gemm(qx, sx, wp, sw, bias, N, K), 1e-2, 1e-2)
+    assert torch.equal(C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, 0), parts)     # deterministic
+
+
+@pytest.mark.parametrize("M", [1, 16, 40])
+@pytest.mark.parametrize("with_res", [False, True])
+@pytest.mark.parametrize("quant", [False, True])
+def test_rms_norm_parts(cuda, M, with_res, quant):
+    """Norm over split-K slices == norm over the materialised bf16 sum (the same kernel math)."""
+    from edgellm.models.layers import PartialSum
+    H, S = 4096, 4
+    parts = torch.randn(S, M, H, device=cuda)
+    res = torch.randn(M, H, device=cuda).bfloat16() if with_res else None
+    w = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    y, s, h = ops.rms_norm_parts(parts, res, w, 1e-5, quant)
+    x = PartialSum(parts).materialize()
+    if quant:
+        q_ref, s_ref, h_ref = ops.rms_norm_quant(x, w, 1e-5, res)
+        assert torch.equal(y, q_ref) and torch.equal(s, s_ref)
+    else:
+        y_ref, h_ref = ops.rms_norm(x, w, 1e-5, res)
+        assert torch.equal(y, y_ref)
+    assert torch.equal(h, h_ref if with_res else x)
+
+
+def test_model_split_k_decode_matches_unsplit(cuda):
+    """W8A8 Llama decode with split-K o/down outputs summed inside the norms == the unsplit path
+    (greedy tokens; only float summation order differs)."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.quant import quantize_model
+    cfg = tiny("llama2", hidden_size=512, num_heads=4, num_kv_heads=4, intermediate_size=1024, num_layers=2)
+    model = quantize_model(build_model(cfg, device=cuda, seed=3), "w8a8_smoothquant")
+    lins = [l.attn.o for l in model.layers] + [l.mlp.down for l in model.layers]
+    assert all(lin.split_k_out for lin in lins)
+    prompts = [[5, 9, 100, 7, 3, 11, 42, 8]] * 4
+    sp = SamplingParams(max_new_tokens=12, do_sample=False)
+    outs = {}
+    for on in (1, 0):
+        for lin in lins:
+            lin.split_k_out = on
+        outs[on] = Generator(model, max_batch=4, max_seq=64).generate(prompts, sp, seed=0).tokens
+    same = sum(a == b for ra, rb in zip(outs[0], outs[1]) for a, b in zip(ra, rb))
+    assert same >= 0.9 * sum(len(r) for r in outs[0]), (outs[0], outs[1])

@@ -46,7 +46,7 @@ def timeit(fn, iters=50, warm=3, per_graph=20):
     return ts[len(ts) // 2] * 1e3 / per_graph  # median us per call
 
 
-def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True, grouped=False, shapes=None):
+def gemv_rows(C, dev, Ms=(1, 16, 32, 64), sweep=True, grouped=False, shapes=None):
     """Cache-cold INT8 GEMV sweep.  ``grouped``: per-(token, 64-column) activation scales (the
     decode o/down projections after the fused producers)."""
     shapes = shapes or {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
@@ -94,7 +94,7 @@ def gemv_rows(C, dev, Ms=(1, 16, 64), sweep=True, grouped=False, shapes=None):
     return out
 
 
-def glu_rows(C, dev, Ms=(1, 16, 33, 64)):
+def glu_rows(C, dev, Ms=(1, 16, 32, 64)):
     """Decode MLP front half (Llama-2-7B: F = 11008), cache-cold: gate_up GEMV + SwiGLU writing
     bf16 h (2 or 4 tiles per workgroup) followed by the group-quant kernel, vs the 8-tile form
     that quantises h in its own epilogue (4 or 8 waves)."""
