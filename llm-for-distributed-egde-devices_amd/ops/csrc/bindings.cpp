@@ -384,7 +384,8 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
   TORCH_CHECK(M <= 64, "split-K GEMV is a decode (M <= 64) kernel");
   const int64_t mpad = a_scale_mpad(sa, M, KT);
   if (S <= 0) {
-    const int64_t groups = ((N + 15) / 16 + 3) / 4;
+    const int64_t ntw = M <= 16 ? 2 : 4;                 // tiles per workgroup (gemm_i8.hip launcher)
+    const int64_t groups = ((N + 15) / 16 + ntw - 1) / ntw;
     S = std::max<int64_t>(1, std::min<int64_t>(8, (256 + groups / 2) / groups));
   }
   S = std::min<int64_t>(S, KT);

@@ -477,8 +477,13 @@ extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void*
   if (M <= 0 || M > 64 || K % 64 != 0 || K / 64 != KT || S < 1 || S > KT) return -2;
   const int mblocks = (M + 15) / 16;
   if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
-#define SK(MBV, KWV, AMV) return launch_one<MBV, 4, 1, KWV, 2, AMV, EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, \
-                                                                          KT, Mpad, st, S)
+  // 2 tiles per workgroup for one row block, 4 for more (the binding sizes S for ~256 workgroups;
+  // measured on Llama-2-7B o/down: S = 2 best at 16 rows, S = 4 at 32)
+#define SK(MBV, KWV, AMV)                                                                                          \
+  return mblocks > 1 ? launch_one<MBV, 4, 1, KWV, 2, AMV, EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, KT, Mpad, \
+                                                              st, S)                                               \
+                : launch_one<MBV, 2, 1, KWV, 2, AMV, EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, KT, Mpad, \
+                                                              st, S)
   if (a_mode == A_GROUP) {
     if (mblocks <= 1) SK(1, 16, A_GROUP);
     if (mblocks <= 2) SK(2, 8, A_GROUP);

@@ -243,8 +243,8 @@ def enable_fused_glu(model) -> int:
     return n
 
 
-# EDGELLM_SPLITK=0 turns the split-K decode outputs off (A/B runs)
-SPLIT_K = os.environ.get("EDGELLM_SPLITK", "1") != "0"
+# EDGELLM_SPLITK: 0 turns the split-K decode outputs off, 1 = automatic split count, N > 1 forces N
+SPLIT_K = int(os.environ.get("EDGELLM_SPLITK", "1"))
 
 
 def enable_split_k_outputs(model) -> int:
@@ -258,6 +258,6 @@ def enable_split_k_outputs(model) -> int:
     for layer in model.layers:
         for lin in (layer.attn.o, layer.mlp.down):
             if isinstance(lin, W8A8Linear) and lin.in_features % 64 == 0:
-                lin.split_k_out = 1
+                lin.split_k_out = SPLIT_K
                 n += 1
     return n
