@@ -31,6 +31,7 @@ import torch  # noqa: E402
 
 import edgellm  # noqa: E402,F401
 from edgellm.engine import Generator, SamplingParams  # noqa: E402
+from edgellm.engine.generate import LaneGenerator  # noqa: E402
 from edgellm.models import build_model, get_config, tiny  # noqa: E402
 from edgellm.quant import quantize_model, synthetic_calibration  # noqa: E402
 from edgellm.quant.smoothquant import smoothquant_stage  # noqa: E402
@@ -52,6 +53,8 @@ def parse(argv=None):
                     help="sequences per micro-batch (64: the throughput point; 16 and 32 trade tok/s for latency)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="1 GPU: micro-batches decoded concurrently on separate HIP streams (each its own graphs)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
@@ -104,29 +107,38 @@ def run_single(args):
     if args.headinfer_heads is not None and args.headinfer_heads < cfg.num_kv_heads:
         from edgellm.offload import HeadInferKV
         kv = HeadInferKV(cfg, B, max_seq, args.headinfer_heads, device, chunk_size=max(args.prompt_len, 1))
-    gen = Generator(model, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs, kv=kv)
+    L = max(1, args.lanes)
+    if L > 1:
+        assert kv is None, "HeadInfer offload runs one lane"
+        gen = LaneGenerator(model, lanes=L, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs)
+    else:
+        gen = Generator(model, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs, kv=kv)
     g = torch.Generator().manual_seed(args.seed)
-    prompts = torch.randint(0, cfg.vocab_size, (B, args.prompt_len), generator=g).tolist()
+    prompts = torch.randint(0, cfg.vocab_size, (B * L, args.prompt_len), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=total_new, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
     gen.start(prompts, sp, seed=args.seed)
-    prefill_s = gen._run["t_prefill"]
+    prefill_s = gen._t_prefill if L > 1 else gen._run["t_prefill"]
     gen.step(args.warmup, record_latency=False)
     gen.precapture(args.steps + 1)
     _sync(device)
-    n_ev = len(gen._run["events"])
+    lanes = gen.lanes if L > 1 else [gen]
+    n_ev = [len(x._run["events"]) for x in lanes]
     t0 = time.perf_counter()
     gen.step(args.steps, record_latency=device.type == "cuda")
     _sync(device)
     dt = time.perf_counter() - t0
-    ev = gen._run["events"][n_ev:]
-    lat = sorted(ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev)))
+    lat = []
+    for x, n0 in zip(lanes, n_ev):
+        ev = x._run["events"][n0:]
+        lat += [ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev))]
+    lat.sort()
     p50 = lat[len(lat) // 2] if lat else dt / args.steps * 1e3
     p90 = lat[int(len(lat) * 0.9)] if lat else p50
     lmax = lat[-1] if lat else p50
-    tokens = B * args.steps
+    tokens = B * L * args.steps
     mem = torch.cuda.max_memory_allocated() / 1e9 if device.type == "cuda" else 0.0
-    return dict(value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B,
-                prefill_tps=B * args.prompt_len / prefill_s, build_s=t_build, graphs=gen._run["graphs_ok"],
+    return dict(value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
+                prefill_tps=B * L * args.prompt_len / prefill_s, build_s=t_build, graphs=lanes[0]._run["graphs_ok"],
                 mem_gb=mem, partition=[0, cfg.num_layers])
 
 
@@ -162,7 +174,8 @@ def main(argv=None):
                 + "; random prompts)",
         "config": {"model": args.model, "global_batch": res["global_batch"], "seq_len": args.prompt_len,
                    "parallelism": f"pp{args.gpus}", "quant": args.quant, "micro_batch": args.micro_batch,
-                   "micro_batches_in_flight": max(1, args.gpus), "partition": res.get("partition"),
+                   "micro_batches_in_flight": max(1, args.gpus) if args.gpus > 1 else max(1, args.lanes),
+                   "lanes": args.lanes if args.gpus == 1 else 1, "partition": res.get("partition"),
                    "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1",
                    "headinfer_heads": args.headinfer_heads,
                    "compute": "W8A8 INT8 MFMA GEMMs, bf16 attention/norms, bf16 LM head"},

@@ -293,3 +293,68 @@ class Generator:
             if stop_at_eos and eos_token_id is not None and self.all_hit(eos_token_id):
                 break
         return self.collect(eos_token_id, stop_at_eos)
+
+
+class LaneGenerator:
+    """``lanes`` independent Generators on one GPU (own KV rows, decode state, graphs and graph
+    memory pools) whose decode steps are replayed on ``lanes`` HIP streams, so one lane's
+    latency-bound kernels (norms, attention tails, kernel boundaries) overlap another lane's
+    weight streaming.  Each step advances every lane by one token.  Prompts are dealt to the
+    lanes in contiguous chunks; lane i samples with seed + 7919 * i."""
+
+    def __init__(self, model: DecoderLM, lanes: int = 2, max_batch: int = 1, max_seq: Optional[int] = None,
+                 use_graphs: Optional[bool] = None, **kw):
+        assert lanes >= 1
+        self.lanes = [Generator(model, max_batch=max_batch, max_seq=max_seq, use_graphs=use_graphs, **kw)
+                      for _ in range(lanes)]
+        self.cuda = model.device.type == "cuda"
+        self.streams = [torch.cuda.Stream(model.device) for _ in range(lanes)] if self.cuda else [None] * lanes
+
+    def _on(self, i):
+        return torch.cuda.stream(self.streams[i]) if self.cuda else _null_ctx()
+
+    @torch.no_grad()
+    def start(self, prompts: Sequence[Sequence[int]], sampling: SamplingParams, seed: int = 0) -> None:
+        L = len(self.lanes)
+        per = (len(prompts) + L - 1) // L
+        for i, g in enumerate(self.lanes):
+            chunk = list(prompts[i * per:(i + 1) * per])
+            assert chunk, "fewer prompts than lanes"
+            g.start(chunk, sampling, seed + 7919 * i)
+        self._t_prefill = sum(g._run["t_prefill"] for g in self.lanes)
+
+    def precapture(self, n_steps: int) -> int:
+        return sum(g.precapture(n_steps) for g in self.lanes)
+
+    @torch.no_grad()
+    def step(self, n: int = 1, record_latency: bool = True) -> None:
+        if self.cuda:
+            cur = torch.cuda.current_stream()
+            for s in self.streams:
+                s.wait_stream(cur)
+        for _ in range(n):
+            for i, g in enumerate(self.lanes):
+                with self._on(i):
+                    g.step(1, record_latency)
+        if self.cuda:
+            for s in self.streams:
+                cur.wait_stream(s)
+
+    def step_latencies_ms(self) -> List[float]:
+        """Per-lane intervals between consecutive recorded steps (device events)."""
+        out: List[float] = []
+        for g in self.lanes:
+            ev = g._run["events"]
+            out += [ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev))]
+        return out
+
+    def collect(self, eos_token_id: Optional[int] = None, stop_at_eos: bool = True) -> List[GenerationResult]:
+        return [g.collect(eos_token_id, stop_at_eos) for g in self.lanes]
+
+
+class _null_ctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
