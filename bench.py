@@ -8,9 +8,10 @@ Llama-2-7B, SmoothQuant W8A8 INT8, layer-split across N GPUs of one node.
 
 Work per step: every in-flight sequence decodes one token, sampled with the reference's config
 (T=0.7, top-k 50, top-p 0.9, repetition penalty 1.1 — Code/others/config.yaml:3-7).
-N = 1 runs the graph-captured Generator on one GPU; N > 1 runs the RCCL pipeline with one
-stage (~32/N decoder layers) per GPU and N micro-batches in flight, so per-GPU work per step is
-constant (weak scaling: global batch = micro-batch x N).
+N = 1 runs graph-captured Generators on one GPU; N > 1 runs the RCCL pipeline with one stage
+(~32/N decoder layers) per GPU and N x lanes micro-batches in flight.  Every GPU decodes ``lanes``
+micro-batches concurrently on separate HIP streams (default 2 x 64 sequences), so per-GPU work
+per step is constant (weak scaling: global batch = micro-batch x lanes x N).
 Weights: random-init Llama-2-7B architecture; the FULL model is SmoothQuant-calibrated on
 synthetic tokens and smoothed once, then each rank keeps its layers, so every split runs
 bit-identical INT8 weights.  Data: random prompt ids.  ``--device cpu --model tiny:llama``
@@ -53,8 +54,8 @@ def parse(argv=None):
                     help="sequences per micro-batch (64: the throughput point; 16 and 32 trade tok/s for latency)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--lanes", type=int, default=1,
-                    help="1 GPU: micro-batches decoded concurrently on separate HIP streams (each its own graphs)")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="micro-batches each GPU decodes concurrently on separate HIP streams (own graphs/pools)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
@@ -149,6 +150,8 @@ def run_pipeline(args):
 
 def main(argv=None):
     args = parse(argv)
+    if args.headinfer_heads is not None:
+        args.lanes = 1          # the HeadInfer offload is host-orchestrated: one lane per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 or world > 1:
         assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun"
@@ -174,8 +177,8 @@ def main(argv=None):
                 + "; random prompts)",
         "config": {"model": args.model, "global_batch": res["global_batch"], "seq_len": args.prompt_len,
                    "parallelism": f"pp{args.gpus}", "quant": args.quant, "micro_batch": args.micro_batch,
-                   "micro_batches_in_flight": max(1, args.gpus) if args.gpus > 1 else max(1, args.lanes),
-                   "lanes": args.lanes if args.gpus == 1 else 1, "partition": res.get("partition"),
+                   "micro_batches_in_flight": max(1, args.gpus) * max(1, args.lanes),
+                   "lanes": max(1, args.lanes), "partition": res.get("partition"),
                    "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1",
                    "headinfer_heads": args.headinfer_heads,
                    "compute": "W8A8 INT8 MFMA GEMMs, bf16 attention/norms, bf16 LM head"},

@@ -1,9 +1,10 @@
 """Multi-GPU leg of bench.py: pipeline of N stages (one per GPU), N micro-batches in flight.
 
-Timed region = ticks [t_a, t_b) with the pipeline full: t_a = M + W*M + (P-1), t_b = t_a + K*M,
-i.e. exactly K decode steps of every sequence (K*M micro-batch items per stage), bracketed on
-every rank by device-synchronize + barrier; the reported time is the max over ranks.
-p50 per-token latency = median interval between consecutive tokens of one sequence (M ticks),
+M = N x lanes micro-batches; each tick a stage runs one group of ``lanes`` micro-batches
+concurrently on that many HIP streams.  Timed region = ticks [t_a, t_b) with the pipeline full:
+t_a = (M + W*M)/L + (P-1), t_b = t_a + K*M/L, i.e. exactly K decode steps of every sequence,
+bracketed on every rank by device-synchronize + barrier; the reported time is the max over ranks.
+p50 per-token latency = median interval between consecutive tokens of one sequence (M/L ticks),
 from device events on the last stage (host timestamps on CPU).
 Runs on CPU with gloo when no GPU is present (``--device cpu``), which is how the multi-process
 path is tested without GPUs.
@@ -38,20 +39,22 @@ def run_pipeline_bench(args, build, model_config):
     bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
                              weight_bytes=wbytes, explicit=explicit)
     _, model = build(args, device, first=bounds[rank], last=bounds[rank + 1])
-    M, P, b, T = world, world, args.micro_batch, args.prompt_len
+    L = max(1, getattr(args, "lanes", 1))
+    M, P, b, T = world * L, world, args.micro_batch, args.prompt_len
     W, K = args.warmup, args.steps
     S = W + K + 1
     g = torch.Generator().manual_seed(args.seed)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)] if rank == 0 else None
     stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs,
-                          headinfer_heads=getattr(args, "headinfer_heads", None))
+                          headinfer_heads=getattr(args, "headinfer_heads", None), lanes=L)
     # initialise the communicator with a collective every rank joins
     x = torch.ones(1, device=cdev)
     dist.all_reduce(x)
     if use_cuda:
         torch.cuda.synchronize()
-    t_a = M + W * M + (P - 1)
-    t_b = t_a + K * M
+    # ticks count item groups of L micro-batches (one per lane)
+    t_a = (M + W * M) // L + (P - 1)
+    t_b = t_a + K * M // L
     marks = {}
     stamps = []
 
@@ -63,7 +66,7 @@ def run_pipeline_bench(args, build, model_config):
             if use_cuda:
                 torch.cuda.synchronize()
             marks[t] = time.perf_counter()
-        if stage.is_last and t_a <= t <= t_b and (t - t_a) % M == 0:
+        if stage.is_last and t_a <= t <= t_b and (t - t_a) % (M // L) == 0:
             if use_cuda:
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()

@@ -42,11 +42,13 @@ class PipelineResult:
 
 class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
-                 group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None):
+                 group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None,
+                 lanes: int = 1):
         """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
         to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
         HeadInfer").  The offloaded path is host-orchestrated, so its decode steps run eagerly."""
-        assert n_micro >= world, "need at least as many micro-batches as stages to keep the ring full"
+        assert lanes >= 1 and n_micro % lanes == 0, "micro-batches must split evenly over lanes"
+        assert n_micro >= world * lanes, "need lanes x stages micro-batches to keep the ring full"
         self.model, self.cfg = model, model.cfg
         self.rank, self.world = rank, world
         self.b, self.M = micro_batch, n_micro
@@ -80,7 +82,12 @@ class PipelineStage:
         self.hin = [torch.zeros(b, H, dtype=model.dtype, device=dev) for _ in range(n_micro)]
         self.hout = [torch.zeros(b, H, dtype=model.dtype, device=dev) for _ in range(n_micro)]
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
-        self._pool = None
+        self._pools: Dict[int, object] = {}
+        # lanes: micro-batches m with equal m % lanes share a HIP stream and a graph memory pool;
+        # the lanes of a tick run concurrently (their graphs never share intermediate buffers)
+        self.L = lanes
+        self.streams = ([torch.cuda.Stream(self.device) for _ in range(lanes)]
+                        if cuda and lanes > 1 else None)
 
     # ------------------------------------------------------------------ p2p
     def _exchange(self, sends, recvs):
@@ -155,10 +162,11 @@ class PipelineStage:
             # no P2P in flight during capture, and a thread-local capture so the process group's
             # watchdog thread may keep querying its events meanwhile
             torch.cuda.synchronize()
-            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+            lane = m % self.L
+            with torch.cuda.graph(g, pool=self._pools.get(lane), capture_error_mode="thread_local"):
                 self._decode_body(m, bucket)
-            if self._pool is None:
-                self._pool = g.pool()
+            if lane not in self._pools:
+                self._pools[lane] = g.pool()
             self._graphs[key] = g
             return g.replay()
         g.replay()
@@ -181,7 +189,7 @@ class PipelineStage:
             getattr(self.kv, "graph_safe", True) and all(getattr(mm, "graph_safe", True) for mm in self.model.modules())
         self._warm: Dict[int, bool] = {}
         self._graphs.clear()
-        self._pool = None
+        self._pools.clear()
         dev = self.device
         if self.is_last:
             self.seen = [torch.zeros(b, V, dtype=torch.uint8, device=dev) for _ in range(M)]
@@ -217,8 +225,21 @@ class PipelineStage:
         def feeds_back(i):  # does item i's sampled token feed a later decode item?
             return (i < M and S >= 1) or (i >= M and (i - M) // M + 1 < S)
 
+        # tick t: rank r processes item group t - r (items [g L, (g + 1) L), one per lane, on the
+        # lanes' streams); every tick starts with ONE grouped exchange (the previous group's outputs
+        # out, this group's inputs in) ordered after all lanes' work and before any of the next
+        L = self.L
+        n_groups = n_items // L
+        cur_stream = torch.cuda.current_stream(dev) if self.streams else None
+
+        def group_valid(g):
+            return 0 <= g < n_groups
+
+        def lane_ctx(i):
+            return torch.cuda.stream(self.streams[i % L]) if self.streams else _nullctx()
+
         t_start = time.perf_counter()
-        n_ticks = n_items + P - 1
+        n_ticks = n_groups + P - 1
         for t in range(n_ticks):
             if hook is not None:
                 hook(t)
@@ -226,42 +247,60 @@ class PipelineStage:
                 watchdog.beat(f"rank {self.rank} tick {t}/{n_ticks}")
             if fault is not None:
                 fault(t)
-            cur, prv = t - self.rank, t - 1 - self.rank
+            cur_g, prv_g = t - self.rank, t - 1 - self.rank
             sends, recvs = [], []
             if P > 1:
-                if not self.is_last and valid(prv):
-                    sends.append((pre_out[prv] if prv < M else self.hout[(prv - M) % M], self.next))
-                if self.is_last and valid(prv) and feeds_back(prv):
-                    sends.append((self.tok[prv % M], 0))
-                if not self.is_first and valid(cur):
-                    if cur < M:
-                        pre_in[cur] = torch.empty(b * T, H, dtype=self.model.dtype, device=dev)
-                        recvs.append((pre_in[cur], self.prev))
-                    else:
-                        recvs.append((self.hin[(cur - M) % M], self.prev))
+                if group_valid(prv_g):
+                    for prv in range(prv_g * L, prv_g * L + L):
+                        if not self.is_last:
+                            sends.append((pre_out[prv] if prv < M else self.hout[(prv - M) % M], self.next))
+                        elif feeds_back(prv):
+                            sends.append((self.tok[prv % M], 0))
+                if not self.is_first and group_valid(cur_g):
+                    for cur in range(cur_g * L, cur_g * L + L):
+                        if cur < M:
+                            pre_in[cur] = torch.empty(b * T, H, dtype=self.model.dtype, device=dev)
+                            recvs.append((pre_in[cur], self.prev))
+                        else:
+                            recvs.append((self.hin[(cur - M) % M], self.prev))
                 if self.is_first:
-                    prod = t - P          # item the last stage finished at tick t-1
-                    if valid(prod) and feeds_back(prod):
-                        recvs.append((self.tok[prod % M], P - 1))
+                    prod_g = t - P        # group the last stage finished at tick t-1
+                    if group_valid(prod_g):
+                        for prod in range(prod_g * L, prod_g * L + L):
+                            if feeds_back(prod):
+                                recvs.append((self.tok[prod % M], P - 1))
+            if self.streams:
+                for st in self.streams:
+                    cur_stream.wait_stream(st)
             self._exchange(sends, recvs)
-            if not valid(cur):
+            if self.streams:
+                for st in self.streams:
+                    st.wait_stream(cur_stream)
+            if not group_valid(cur_g):
                 continue
-            if cur < M:                                   # prefill item
-                m = cur
-                ids = prompts[m].to(dev) if self.is_first else None
-                out = self._prefill(m, ids, T, pre_in[m])
-                pre_in[m] = None
-                if self.is_last:
-                    self._sample(m, out)
-                else:
-                    pre_out[m] = out
-                if cur - 1 >= 0 and not self.is_last:
-                    pass
-            else:
-                k, m = divmod(cur - M, M)
-                self._decode(m, T + k + 1)
-            if not self.is_last and prv >= 0 and prv < M:
-                pre_out[prv] = None                        # sent this tick
+            for cur in range(cur_g * L, cur_g * L + L):
+                with lane_ctx(cur):
+                    if cur < M:                           # prefill item
+                        m = cur
+                        if self.streams and pre_in[m] is not None:
+                            pre_in[m].record_stream(self.streams[m % L])   # received on the exchange stream
+                        ids = prompts[m].to(dev) if self.is_first else None
+                        out = self._prefill(m, ids, T, pre_in[m])
+                        pre_in[m] = None
+                        if self.is_last:
+                            self._sample(m, out)
+                        else:
+                            pre_out[m] = out
+                    else:
+                        k, m = divmod(cur - M, M)
+                        self._decode(m, T + k + 1)
+            if not self.is_last and group_valid(prv_g):
+                for prv in range(prv_g * L, prv_g * L + L):
+                    if prv < M:
+                        pre_out[prv] = None                # sent this tick
+        if self.streams:
+            for st in self.streams:
+                cur_stream.wait_stream(st)
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
@@ -271,6 +310,14 @@ class PipelineStage:
             for m in range(M):
                 toks.extend(self.out[m].tolist())
         return PipelineResult(toks, n_ticks, elapsed)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def init_distributed(backend: Optional[str] = None):

@@ -31,23 +31,27 @@ COMMON = ["--device", "cpu", "--model", "tiny:llama", "--micro-batch", "2", "--s
           "--prompt-len", "6"]
 
 
-def test_bench_single_cpu():
-    r = subprocess.run([sys.executable, "bench.py", *COMMON], cwd=ROOT, capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_bench_single_cpu(lanes):
+    r = subprocess.run([sys.executable, "bench.py", *COMMON, "--lanes", str(lanes)], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert REQUIRED <= set(d) and d["n_gpus"] == 1 and d["value"] > 0
-    assert d["config"]["global_batch"] == 2 and d["config"]["parallelism"] == "pp1"
+    assert d["config"]["global_batch"] == 2 * lanes and d["config"]["parallelism"] == "pp1"
+    assert d["config"]["lanes"] == lanes
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_pipeline_torchrun_cpu(n):
+@pytest.mark.parametrize("n,lanes", [(2, 1), (2, 2), (3, 2)])
+def test_bench_pipeline_torchrun_cpu(n, lanes):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *COMMON]
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *COMMON,
+           "--lanes", str(lanes)]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
-    assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n and d["value"] > 0
+    assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n * lanes and d["value"] > 0
     assert d["config"]["parallelism"] == f"pp{n}" and len(d["config"]["partition"]) == n + 1
 
 

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads=None):
+def _worker(rank, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads=None, lanes=1):
     import edgellm  # noqa: F401
     from edgellm.parallel.pipeline import PipelineStage
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -36,7 +36,7 @@ def _worker(rank, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads=N
     model = build_model(cfg, dtype=torch.float32, first=bounds[rank], last=bounds[rank + 1], seed=7)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
-    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, headinfer_heads=headinfer_heads)
+    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, headinfer_heads=headinfer_heads, lanes=lanes)
     sp = SamplingParams(max_new_tokens=S + 1, do_sample=do_sample, temperature=0.7, top_k=20, top_p=0.9,
                         repetition_penalty=1.1)
     res = st.run(prompts if rank == 0 else None, T, sp, S, seed=5)
@@ -60,14 +60,16 @@ def _reference(arch, M, b, T, S, do_sample):
     return out
 
 
-@pytest.mark.parametrize("world,M", [(2, 2), (2, 3), (3, 3)])
+@pytest.mark.parametrize("world,M,lanes", [(2, 2, 1), (2, 3, 1), (3, 3, 1), (2, 4, 2), (3, 6, 2)])
 @pytest.mark.parametrize("do_sample", [False, True])
-def test_pipeline_matches_unsplit(world, M, do_sample):
+def test_pipeline_matches_unsplit(world, M, lanes, do_sample):
+    """Split == unsplit token for token, also with 2 lanes (two micro-batches per tick)."""
     arch, b, T, S = "llama", 2, 5, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, M, b, T, S, do_sample, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, M, b, T, S, do_sample, q, None, lanes))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=180)

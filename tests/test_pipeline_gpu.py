@@ -42,7 +42,7 @@ def _sampling(S, do_sample):
                           repetition_penalty=1.1)
 
 
-def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q):
+def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q, lanes=1):
     import edgellm  # noqa: F401
     from edgellm.parallel.pipeline import PipelineStage
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -53,7 +53,7 @@ def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q):
     _, model = _model(arch, quant, bounds[rank], bounds[rank + 1])
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
-    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4)
+    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, lanes=lanes)
     assert st.host_staged and st.use_graphs
     res = st.run(prompts if rank == 0 else None, T, _sampling(S, do_sample), S, seed=5)
     if res.tokens is not None:
@@ -73,14 +73,16 @@ def _reference(arch, quant, M, b, T, S, do_sample):
     return out
 
 
-@pytest.mark.parametrize("quant", ["none", "w8a8"])
+@pytest.mark.parametrize("quant,lanes", [("none", 1), ("w8a8", 1), ("w8a8", 2)])
 @pytest.mark.parametrize("do_sample", [False, True])
-def test_pipeline_gpu_matches_unsplit(cuda, quant, do_sample):
-    arch, world, M, b, T, S = "llama", 2, 2, 4, 9, 12
+def test_pipeline_gpu_matches_unsplit(cuda, quant, lanes, do_sample):
+    """lanes = 2: two micro-batches per tick on two HIP streams (own graph pools) per stage."""
+    arch, world, b, T, S = "llama", 2, 4, 9, 12
+    M = world * lanes
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, quant, M, b, T, S, do_sample, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, quant, M, b, T, S, do_sample, q, lanes))
              for r in range(world)]
     for p in procs:
         p.start()
