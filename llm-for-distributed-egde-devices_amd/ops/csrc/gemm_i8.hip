@@ -183,19 +183,26 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
       }
     }
   } else {
-    // pair p = (gate tile 2p, up tile 2p+1) -> feature (nt0/2 + p) * 16 + (lane & 15)
+    // pair p = (gate tile 2p, up tile 2p+1) -> feature (nt0/2 + p) * 16 + (lane & 15); a wave owns
+    // pairs wave, wave + NW, ...  EPI_GLUQ: every owned pair's row maxima reach LDS before the
+    // single barrier, then each 64-feature group (4 pairs) is quantised with one scale per row
     const int Fo = N / 2;
     constexpr int NP = NTW / 2 * MB;
-    static_assert(EPI != EPI_GLUQ || OWN == 1, "quantising GLU: one pair per wave");
+    float h[OWN][4];
+    bool owner[OWN];
+    int pp[OWN], ii[OWN];
 #pragma unroll
     for (int o = 0; o < OWN; ++o) {
       const int pf = wave + o * NW;
       const bool live = pf < NP;
       const int p = live ? pf / MB : 0, i = live ? pf % MB : 0;
-      const bool owner = live && nt0 + 2 * p + 1 < NTt;
+      pp[o] = p;
+      ii[o] = i;
+      owner[o] = live && nt0 + 2 * p + 1 < NTt;
       const int feat = (nt0 / 2 + p) * 16 + (lane & 15);
-      float h[4] = {0.f, 0.f, 0.f, 0.f};
-      if (owner) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h[o][q] = 0.f;
+      if (owner[o]) {
         const v4i g4 = total((2 * p) * MB + i), u4 = total((2 * p + 1) * MB + i);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -205,33 +212,36 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
           float u = (float)u4[q] * s_a * pre.s1[o] + pre.b1[o];
           g = bf2f(f2bf(g));                // the unfused GEMM output is bf16
           u = bf2f(f2bf(u));
-          h[q] = g / (1.f + __expf(-g)) * u;
+          h[o][q] = g / (1.f + __expf(-g)) * u;
           if constexpr (EPI == EPI_GLU)
-            if (row < M) reinterpret_cast<bf16_t*>(outv)[(size_t)row * Fo + feat] = f2bf(h[q]);
+            if (row < M) reinterpret_cast<bf16_t*>(outv)[(size_t)row * Fo + feat] = f2bf(h[o][q]);
         }
-      }
-      if constexpr (EPI == EPI_GLUQ) {
-        // 4 pairs = 64 features share one scale per row
-        if (owner) {
+        if constexpr (EPI == EPI_GLUQ) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            float m = fabsf(h[q]);
+            float m = fabsf(h[o][q]);
 #pragma unroll
             for (int d = 1; d < 16; d <<= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
             if ((lane & 15) == 0) gmax[i][p][4 * (lane >> 4) + q] = m;
           }
         }
-        __syncthreads();
-        if (owner) {
-          int8_t* hq = reinterpret_cast<int8_t*>(outv);
-          const int grp = nt0 / 8;
+      }
+    }
+    if constexpr (EPI == EPI_GLUQ) {
+      __syncthreads();
+      int8_t* hq = reinterpret_cast<int8_t*>(outv);
+      const int grp = nt0 / 8;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int rr = 4 * (lane >> 4) + q, row = i * 16 + rr;
-            const float amax = fmaxf(fmaxf(fmaxf(gmax[i][0][rr], gmax[i][1][rr]), fmaxf(gmax[i][2][rr], gmax[i][3][rr])), 1e-8f);
-            if (row < M) hq[(size_t)row * Fo + feat] = quant_i8(h[q], 127.f / amax);
-            if (p == 0 && (lane & 15) == 0 && row < Mpad) os[(size_t)grp * Mpad + row] = row < M ? amax / 127.f : 0.f;
-          }
+      for (int o = 0; o < OWN; ++o) {
+        if (!owner[o]) continue;
+        const int p = pp[o], i = ii[o];
+        const int feat = (nt0 / 2 + p) * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rr = 4 * (lane >> 4) + q, row = i * 16 + rr;
+          const float amax = fmaxf(fmaxf(fmaxf(gmax[i][0][rr], gmax[i][1][rr]), fmaxf(gmax[i][2][rr], gmax[i][3][rr])), 1e-8f);
+          if (row < M) hq[(size_t)row * Fo + feat] = quant_i8(h[o][q], 127.f / amax);
+          if (p == 0 && (lane & 15) == 0 && row < Mpad) os[(size_t)grp * Mpad + row] = row < M ? amax / 127.f : 0.f;
         }
       }
     }
@@ -248,10 +258,13 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   static_assert(NTW % TG == 0, "tiles split evenly over tile groups");
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && TPW % 2 == 0),
                 "GLU: gate/up pairs per wave, per-token A");
-  static_assert(EPI != EPI_GLUQ || (NTW == 8 && NW >= 4 * MB), "quantising GLU: 64 features, one pair per wave");
-  static_assert(KW * NTW * MB * 1024 <= 131072, "LDS reduction budget");
+  static_assert(EPI != EPI_GLUQ || NTW == 8, "quantising GLU: 64 features per workgroup");
+  // LDS reduction buffer: one partial set per k-wave, or per pair of k-waves when that would
+  // exceed 128 KiB (the upper half adds into the lower half first)
+  constexpr int KR = KW * NTW * MB * 1024 <= 131072 ? KW : KW / 2;
+  static_assert(KR * NTW * MB * 1024 <= 131072 && KW % KR == 0 && KW / KR <= 2, "LDS reduction budget");
   constexpr bool SCALED = AMODE == A_GROUP;
-  __shared__ v4i red[KW][NTW * MB][64];
+  __shared__ v4i red[KR][NTW * MB][64];
   __shared__ float gmax[MB][4][16];
   // EPI_PART (split-K): workgroup (group, s) reduces k-tiles [KT*s/S, KT*(s+1)/S) of its tiles and
   // writes fp32 partial sums part[s][M][N]; the consumer (norm kernel) adds the S slices in order
@@ -330,13 +343,28 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     issue(st, kt);
     compute(st, kt);
   }
+  if (KR == KW || kw >= KR) {
 #pragma unroll
-  for (int j = 0; j < TPW; ++j)
+    for (int j = 0; j < TPW; ++j)
 #pragma unroll
-    for (int i = 0; i < MB; ++i)
-      red[kw][(t0 + j) * MB + i][lane] = SCALED ? __builtin_bit_cast(v4i, accf[j][i]) : acc[j][i];
+      for (int i = 0; i < MB; ++i)
+        red[kw - (KW - KR)][(t0 + j) * MB + i][lane] = SCALED ? __builtin_bit_cast(v4i, accf[j][i]) : acc[j][i];
+  }
   __syncthreads();
-  gemv_epilogue<MB, NTW, NW, KW, SCALED, EPI>(&red[0][0][0], sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane,
+  if constexpr (KR != KW) {
+    if (kw < KR) {
+#pragma unroll
+      for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+          v4i& r = red[kw][(t0 + j) * MB + i][lane];
+          if constexpr (SCALED) r = __builtin_bit_cast(v4i, __builtin_bit_cast(v4f, r) + accf[j][i]);
+          else r += acc[j][i];
+        }
+    }
+    __syncthreads();
+  }
+  gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI>(&red[0][0][0], sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane,
                                               ks);
 }
 
@@ -451,7 +479,7 @@ int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const vo
                                                                           KT, Mpad, st)
 #define BY_KW(NTWV, UV)                                                   \
   do {                                                                    \
-    if constexpr (16 * NTWV * MB > 128 || MB > 2 || (AM == A_GROUP && (NTWV >= 4 || (MB > 1 && NTWV > 2)))) L(NTWV, 8, UV); \
+    if constexpr ((AM == A_GROUP && (NTWV >= 4 || (MB > 1 && NTWV > 2) || MB > 2)) || (MB > 2 && NTWV >= 3)) L(NTWV, 8, UV); \
     else { if (kw <= 8) L(NTWV, 8, UV); else L(NTWV, 16, UV); }           \
   } while (0)
   if (ntw <= 1) {
@@ -511,9 +539,14 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     if (epi == EPI_GLUQ) {
       if (os == nullptr || Mpad < mblocks * 16) return -2;
       // 8 tiles = 64 features; 16 waves as (TG tile groups) x (KW k-waves) within the LDS budget
-      if (mblocks <= 1) return launch_one<1, 8, 2, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      // one tile group (TG = 1): every wave holds all 8 tiles, so each activation fragment is
+      // fetched once per workgroup (TG > 1 re-fetched it per group: 1 MB of L2 reads per CU at 64 rows)
+      if (mblocks <= 1) {
+        if (g_gemv_kw == 16) return launch_one<1, 8, 2, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+        return launch_one<1, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      }
       if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
-      return launch_one<4, 8, 4, 4, 1, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      return launch_one<4, 8, 1, 8, 1, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
     }
     if (mblocks <= 1) return launch_one<1, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
     if (mblocks <= 2) return launch_one<2, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
