@@ -482,6 +482,11 @@ int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const vo
     if constexpr ((AM == A_GROUP && (NTWV >= 4 || (MB > 1 && NTWV > 2) || MB > 2)) || (MB > 2 && NTWV >= 3)) L(NTWV, 8, UV); \
     else { if (kw <= 8) L(NTWV, 8, UV); else L(NTWV, 16, UV); }           \
   } while (0)
+  // four row blocks, A_TOKEN: 16 waves with one k-tile in flight each (U = 1) fit the 128-VGPR
+  // budget where U = 2 needs 8 waves; un == 2 selects the 8-wave form (A/B)
+  if constexpr (MB == 4 && AM == A_TOKEN) {
+    if (un != 2 && ntw == 3) L(3, 16, 1);
+  }
   if (ntw <= 1) {
     if constexpr (MB == 1) { if (un >= 4) BY_KW(1, 4); }
     BY_KW(1, 2);
@@ -570,7 +575,7 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   }
   // NTW tiles per workgroup so that the grid is ~256 workgroups (one 16-wave group per CU)
   int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : (NTt >= 512 ? min(4, (NTt + 128) / 256) : 1);
-  const int un = g_gemv_unroll > 0 ? g_gemv_unroll : (ntw == 1 && KT >= 128 ? 4 : 2);
+  const int un = g_gemv_unroll > 0 ? g_gemv_unroll : (ntw == 1 && KT >= 128 ? 4 : (mblocks > 2 ? 1 : 2));
   const int kw = g_gemv_kw > 0 ? g_gemv_kw : 16;
 #define OUT(MBV, AMV) return launch_out<MBV, AMV>(ntw, un, kw, A, sa, Wp, sw, bias, out, M, N, K, KT, Mpad, st)
   if (a_mode == A_GROUP) {
