@@ -49,7 +49,11 @@ class HeadInferKV:
     graph_safe = False   # host-orchestrated transfers: not capturable
 
     def __init__(self, cfg: ModelConfig, max_batch: int, max_seq: int, h_on: int, device=None, first: int = 0,
-                 last: Optional[int] = None, chunk_heads: int = 1, chunk_size: int = 4096, dtype=torch.bfloat16):
+                 last: Optional[int] = None, chunk_heads: Optional[int] = None, chunk_size: int = 4096,
+                 dtype=torch.bfloat16, stage_budget_bytes: float = 2e9):
+        """``chunk_heads``: offloaded heads staged per transfer; None = as many as fit
+        ``stage_budget_bytes`` across the two ping-pong K/V buffers (the paper stages one head at a
+        time to fit a 24 GB card; with 288 GB of HBM larger chunks cut the per-head launches)."""
         hk, D = cfg.num_kv_heads, cfg.head_dim
         assert 0 <= h_on <= hk, "h_on must be within [0, num_kv_heads]"
         self.cfg, self.first = cfg, first
@@ -60,6 +64,9 @@ class HeadInferKV:
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.cuda = self.device.type == "cuda"
         self.gpu = KVCache(cfg, max_batch, max_seq, first, self.last, dtype, device, num_kv_heads=h_on)
+        if chunk_heads is None:
+            per_head = 2 * 2 * max_batch * max_seq * D * torch.finfo(dtype).bits // 8   # 2 buffers x (k, v)
+            chunk_heads = int(max(1, stage_budget_bytes // max(per_head, 1)))
         self.c = max(1, min(chunk_heads, max(self.h_off, 1)))
         pin = self.cuda
         self.host_k = torch.zeros((L, max_batch, self.h_off, max_seq, D), dtype=dtype, pin_memory=pin)

@@ -23,7 +23,7 @@ def _run(device, h_on, chunk_heads, chunk_size, kvh=4, arch="llama", dtype=torch
     return ref, got, kv
 
 
-@pytest.mark.parametrize("h_on,chunk_heads,chunk_size", [(1, 1, 8), (0, 2, 64), (2, 1, 5), (3, 4, 16)])
+@pytest.mark.parametrize("h_on,chunk_heads,chunk_size", [(1, 1, 8), (0, 2, 64), (2, 1, 5), (3, 4, 16), (1, None, 8)])
 def test_headinfer_matches_resident_cpu(h_on, chunk_heads, chunk_size):
     ref, got, kv = _run("cpu", h_on, chunk_heads, chunk_size)
     assert got.tokens == ref.tokens
@@ -39,7 +39,7 @@ def test_budget_to_heads():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("h_on,chunk_heads,chunk_size", [(1, 1, 8), (0, 2, 64), (2, 1, 5)])
+@pytest.mark.parametrize("h_on,chunk_heads,chunk_size", [(1, 1, 8), (0, 2, 64), (2, 1, 5), (1, None, 8)])
 def test_headinfer_matches_resident_gpu(cuda, h_on, chunk_heads, chunk_size):
     ref, got, kv = _run(cuda, h_on, chunk_heads, chunk_size, dtype=torch.bfloat16)
     assert got.tokens == ref.tokens
