@@ -551,6 +551,7 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
         return launch_one<1, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
       }
       if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      // (4 waves with U = 2 / 4 and AGPR accumulators measured 45.6 / 41.4 us against 34.3 us here)
       return launch_one<4, 8, 1, 8, 1, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
     }
     if (mblocks <= 1) return launch_one<1, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);

@@ -23,6 +23,17 @@ import edgellm  # noqa: E402,F401
 from edgellm import ops  # noqa: E402
 
 
+GLOBAL_TUNE = []   # --tune settings; re-applied whenever a sweep resets a knob to automatic
+
+
+def tune(C, name, a, b=0):
+    """Set a tuning knob; (0, 0) means automatic unless --tune pinned that knob."""
+    for n, va, vb in GLOBAL_TUNE:
+        if n == name and a == 0 and b == 0:
+            a, b = va, vb
+    C.tune(name, a, b)
+
+
 def timeit(fn, iters=50, warm=3, per_graph=20):
     """Median per-call device time (us): ``per_graph`` calls captured in one HIP graph, replayed
     ``iters`` times — removes host launch overhead, keeps the in-graph kernel boundaries that the
@@ -77,12 +88,12 @@ def gemv_rows(C, dev, Ms=(1, 16, 32, 64), sweep=True, grouped=False, shapes=None
                 for nw, u, ntw in variants:
                     if u == 4 and (M > 16 or ntw > 1):
                         continue
-                    C.tune("gemv", nw, u)
-                    C.tune("gemv_ntw", ntw, 0)
+                    tune(C, "gemv", nw, u)
+                    tune(C, "gemv_ntw", ntw, 0)
                     t = timeit(call, iters=10, per_graph=ncopy)
                     res.setdefault((nw, u, ntw), []).append(t)
-            C.tune("gemv", 0, 0)
-            C.tune("gemv_ntw", 0, 0)
+            tune(C, "gemv", 0, 0)
+            tune(C, "gemv_ntw", 0, 0)
             best = min(res, key=lambda k: min(res[k]))
             auto = min(res[(0, 0, 0)])
             nbytes = N * K + M * K + M * N * 2
@@ -121,11 +132,11 @@ def glu_rows(C, dev, Ms=(1, 16, 32, 64)):
         res = {}
         for rnd in range(2):
             for name, fn, ntw, nw in variants:
-                C.tune("gemv_ntw", ntw, 0)
-                C.tune("gemv", nw, 0)
+                tune(C, "gemv_ntw", ntw, 0)
+                tune(C, "gemv", nw, 0)
                 res.setdefault((name, ntw, nw), []).append(timeit(fn, iters=10, per_graph=ncopy))
-        C.tune("gemv_ntw", 0, 0)
-        C.tune("gemv", 0, 0)
+        tune(C, "gemv_ntw", 0, 0)
+        tune(C, "gemv", 0, 0)
         nbytes = N * K + M * K + M * N // 2
         for (name, ntw, nw), ts in res.items():
             out.append(dict(op="w8a8_glu", form=name, M=M, N=N, K=K, ntw=ntw, nw=nw, us=round(min(ts), 2),
@@ -243,6 +254,7 @@ def main():
     for t in a.tune:
         name, vals = t.split("=")
         v = [int(x) for x in vals.split(",")] + [0]
+        GLOBAL_TUNE.append((name, v[0], v[1]))
         C.tune(name, v[0], v[1])
     rows = gemv_rows(C, dev, sweep=not a.no_sweep) if only is None or "gemv" in only else []
     if only is None or "grouped" in only:
