@@ -70,7 +70,9 @@ class Attention(nn.Module):
             attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
         elif ctx.mode == "decode":
             # one launch: RoPE + KV append + attention (+ per-group int8 output for a W8A8 o-proj)
-            quant = self.o.takes_quantized_input and cfg.head_dim % 64 == 0
+            # per-(token, 64) int8 output feeds the decode GEMV (<= 64 rows); larger batches take
+            # bf16 attention output and per-token quantisation
+            quant = self.o.takes_quantized_input and cfg.head_dim % 64 == 0 and ctx.B <= 64
             out, s = ops.decode_attention_fused(qkv.view(ctx.B, -1), ctx.start_pos, ctx.rope if rot else None,
                                                 k_cache, v_cache, ctx.seq_lens, cfg.num_heads, self.scale,
                                                 ctx.max_len, rot, quant)

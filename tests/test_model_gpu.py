@@ -63,3 +63,21 @@ def test_flagship_shape_smoke(cuda):
     gen = Generator(m, max_batch=4, max_seq=256)
     res = gen.generate([[1] + list(range(100, 163))] * 4, SamplingParams(max_new_tokens=16), seed=1)
     assert all(len(t) == 16 for t in res.tokens)
+
+
+@pytest.mark.parametrize("B", [64, 80])
+def test_w8a8_decode_beyond_gemv_rows(cuda, B):
+    """Decode batches above the 64-row GEMV limit take the tiled GEMM and per-token quantisation
+    (no per-group attention output): they must run and agree with the same prompts at B = 16."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.quant import quantize_model
+    cfg = tiny("llama2", hidden_size=256, num_heads=4, num_kv_heads=4, intermediate_size=512, num_layers=2)
+    model = quantize_model(build_model(cfg, device=cuda, seed=5), "w8a8_smoothquant")
+    g = torch.Generator().manual_seed(1)
+    prompts = torch.randint(0, cfg.vocab_size, (B, 12), generator=g).tolist()
+    sp = SamplingParams(max_new_tokens=6, do_sample=False)
+    big = Generator(model, max_batch=B, max_seq=32).generate(prompts, sp, seed=0).tokens
+    small = Generator(model, max_batch=16, max_seq=32).generate(prompts[:16], sp, seed=0).tokens
+    same = sum(a == b for ra, rb in zip(big[:16], small) for a, b in zip(ra, rb))
+    assert len(big) == B and same >= 0.85 * 16 * 6
