@@ -36,8 +36,11 @@ def run_pipeline_bench(args, build, model_config):
     cfg = model_config(args)
     wbytes = 1.0 if args.quant != "none" else 2.0
     explicit = args.partition if "," in args.partition else None
+    # decode-time cost model: LM head + sampler ~0.6 of a W8A8 decoder layer (0.4 of a bf16 one),
+    # measured on MI355X at 64 rows per lane (parallel/partition.py::layer_costs)
+    hcl = 0.6 if args.quant != "none" else 0.4
     bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
-                             weight_bytes=wbytes, explicit=explicit)
+                             weight_bytes=wbytes, explicit=explicit, head_cost_layers=hcl)
     _, model = build(args, device, first=bounds[rank], last=bounds[rank + 1])
     L = max(1, getattr(args, "lanes", 1))
     M, P, b, T = world * L, world, args.micro_batch, args.prompt_len
@@ -95,7 +98,7 @@ def run_pipeline_bench(args, build, model_config):
         tokens = K * M * b
         res = dict(value=tokens / elapsed, ms_per_step=elapsed / K * 1e3, p50=float(lat.item()), global_batch=M * b,
                    mem_gb=float(mem.item()), partition=bounds,
-                   stage_cost_mb=[round(c / 1e6, 1) for c in stage_costs(cfg, bounds, wbytes)])
+                   stage_cost_mb=[round(c / 1e6, 1) for c in stage_costs(cfg, bounds, wbytes, head_cost_layers=hcl)])
     dist.barrier()
     dist.destroy_process_group()
     return res

@@ -13,8 +13,15 @@ from typing import List, Optional, Sequence, Tuple
 from ..models.configs import ModelConfig
 
 
-def layer_costs(cfg: ModelConfig, weight_bytes: float = 1.0, head_bytes: float = 2.0) -> Tuple[List[float], float]:
+def layer_costs(cfg: ModelConfig, weight_bytes: float = 1.0, head_bytes: float = 2.0,
+                head_cost_layers: Optional[float] = None) -> Tuple[List[float], float]:
+    """Per-layer costs and the last stage's extra (LM head + sampler).  By default both are bytes
+    streamed per step; ``head_cost_layers`` instead prices the head in measured decoder-layer
+    times (MI355X W8A8 decode at 64 rows: a layer ~132 us per lane, bf16 head GEMM + fused
+    sampler ~80 us, so 0.6 — bytes alone would call the 262 MB bf16 head 1.3 layers)."""
     per = cfg.layer_bytes(weight_bytes)
+    if head_cost_layers is not None:
+        return [per] * cfg.num_layers, head_cost_layers * per
     head = head_bytes * cfg.hidden_size * cfg.vocab_size
     return [per] * cfg.num_layers, head
 
@@ -61,7 +68,8 @@ def uniform_partition(L: int, stages: int) -> List[int]:
 
 
 def partition_model(cfg: ModelConfig, stages: int, mode: str = "balanced", weight_bytes: float = 1.0,
-                    head_bytes: float = 2.0, explicit: Optional[str] = None) -> List[int]:
+                    head_bytes: float = 2.0, explicit: Optional[str] = None,
+                    head_cost_layers: Optional[float] = None) -> List[int]:
     """mode: balanced | uniform | explicit ("8,8,8,8" layers per stage)."""
     if explicit or mode not in ("balanced", "uniform"):
         spec = explicit or mode
@@ -73,12 +81,13 @@ def partition_model(cfg: ModelConfig, stages: int, mode: str = "balanced", weigh
         return out
     if mode == "uniform":
         return uniform_partition(cfg.num_layers, stages)
-    costs, head = layer_costs(cfg, weight_bytes, head_bytes)
+    costs, head = layer_costs(cfg, weight_bytes, head_bytes, head_cost_layers)
     return balanced_partition(costs, stages, head)
 
 
-def stage_costs(cfg: ModelConfig, bounds: Sequence[int], weight_bytes: float = 1.0, head_bytes: float = 2.0):
-    costs, head = layer_costs(cfg, weight_bytes, head_bytes)
+def stage_costs(cfg: ModelConfig, bounds: Sequence[int], weight_bytes: float = 1.0, head_bytes: float = 2.0,
+                head_cost_layers: Optional[float] = None):
+    costs, head = layer_costs(cfg, weight_bytes, head_bytes, head_cost_layers)
     out = []
     for s in range(len(bounds) - 1):
         c = sum(costs[bounds[s]:bounds[s + 1]])

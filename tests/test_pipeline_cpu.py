@@ -151,3 +151,8 @@ def test_balanced_partition():
         c = stage_costs(cfg, bounds)
         assert max(c) <= min(c) + cfg.layer_bytes(1.0) + 2 * cfg.hidden_size * cfg.vocab_size
     assert partition_model(cfg, 4, explicit="9,8,8,7") == [0, 9, 17, 25, 32]
+    # decode-time costs: the head + sampler is 0.6 of a layer, so 8 stages of 4 layers beat the
+    # byte model's 4,4,4,4,4,4,5,3 (which puts 5 layers on one stage)
+    assert partition_model(cfg, 8, head_cost_layers=0.6) == [0, 4, 8, 12, 16, 20, 24, 28, 32]
+    assert max(stage_costs(cfg, partition_model(cfg, 8, head_cost_layers=0.6), head_cost_layers=0.6)) \
+        < max(stage_costs(cfg, partition_model(cfg, 8), head_cost_layers=0.6))
