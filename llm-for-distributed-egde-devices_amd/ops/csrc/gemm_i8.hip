@@ -29,6 +29,7 @@
 //          global_load_lds (16 B/lane, lane-linear fragment-ordered LDS images -> conflict-free
 //          ds_read_b128), LDS double buffer.
 #include "common.h"
+#include <type_traits>
 
 namespace {
 constexpr int NT = 256;
@@ -90,6 +91,9 @@ __device__ __forceinline__ v4i load_a_i8(const int8_t* __restrict__ arow_p, bool
 // kernel start, so the tail of the kernel never waits on an HBM round trip.
 
 __device__ const bf16_t g_zero_bf16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifndef GEMV_UNROLL_FIXED
+#define GEMV_UNROLL_FIXED 1
+#endif
 
 // Epilogue operands preloaded per owned fragment (EPI_OUT) or gate/up pair (GLU).
 template <int OWN>
@@ -336,12 +340,33 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
       }
     }
   };
-  // one step of U k-tiles per iteration: all its loads in flight, then its MFMAs (16 waves per
-  // CU hide each other's latency; a two-buffer software pipeline measured slower here)
-  for (int kt = kbeg + kw; kt < kend; kt += KW * U) {
-    Step st;
-    issue(st, kt);
-    compute(st, kt);
+  // one step of U k-tiles per iteration: all its loads in flight, then its MFMAs.  The k range
+  // lengths of the decode shapes (64, 32, 16 k-tiles) get a compile-time trip count, fully
+  // unrolled, so the scheduler can hoist the next steps' loads above this step's MFMAs (a wave's
+  // time is otherwise about one memory latency per step); other lengths take the runtime loop.
+  auto fixed = [&](auto nk) {
+    constexpr int NK = decltype(nk)::value, STEPS = (NK + KW * U - 1) / (KW * U);
+    Step st[STEPS];
+    issue(st[0], kbeg + kw);
+#pragma unroll
+    for (int i = 0; i < STEPS; ++i) {                   // one step of lookahead, no register copies
+      if (i + 1 < STEPS) issue(st[i + 1], kbeg + kw + (i + 1) * KW * U);
+      compute(st[i], kbeg + kw + i * KW * U);
+    }
+  };
+  // only where two steps plus the accumulators fit the register budget (measured: larger forms spill)
+  constexpr int REG_EST = 2 * U * (TPW * 4 + MB * 4 * (SCALED ? 2 : 1)) + TPW * MB * 4;
+  constexpr bool FIXED_OK = GEMV_UNROLL_FIXED && REG_EST <= (NW >= 16 ? 80 : 180) && (!SCALED || MB == 1);
+  const int nk = kend - kbeg;
+  if (FIXED_OK && nk == 64 && KW * U <= 64) fixed(std::integral_constant<int, 64>{});
+  else if (FIXED_OK && nk == 32 && KW * U <= 32) fixed(std::integral_constant<int, 32>{});
+  else if (FIXED_OK && nk == 16 && KW * U <= 16) fixed(std::integral_constant<int, 16>{});
+  else {
+    for (int kt = kbeg + kw; kt < kend; kt += KW * U) {
+      Step st;
+      issue(st, kt);
+      compute(st, kt);
+    }
   }
   if (KR == KW || kw >= KR) {
 #pragma unroll
