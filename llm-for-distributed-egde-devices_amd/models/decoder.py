@@ -70,9 +70,10 @@ class Attention(nn.Module):
             attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
         elif ctx.mode == "decode":
             # one launch: RoPE + KV append + attention (+ per-group int8 output for a W8A8 o-proj)
-            # per-(token, 64) int8 output feeds the decode GEMV (<= 64 rows); larger batches take
-            # bf16 attention output and per-token quantisation
-            quant = self.o.takes_quantized_input and cfg.head_dim % 64 == 0 and ctx.B <= 64
+            # per-(token, 64) int8 output feeds the decode GEMV (<= 64 rows, <= 128 for the shapes
+            # with 128-row kernels); larger batches take bf16 attention output and per-token quant
+            quant = self.o.takes_quantized_input and cfg.head_dim % 64 == 0 and \
+                getattr(self.o, "group_scales_ok", lambda m: m <= 64)(ctx.B)
             out, s = ops.decode_attention_fused(qkv.view(ctx.B, -1), ctx.start_pos, ctx.rope if rot else None,
                                                 k_cache, v_cache, ctx.seq_lens, cfg.num_heads, self.scale,
                                                 ctx.max_len, rot, quant)
@@ -101,7 +102,8 @@ class MLP(nn.Module):
             # GEMV + SwiGLU epilogue (int8 h with per-group scales, or bf16 h that the down
             # projection quantises per group — W8A8Linear.glu); larger ones the blocked
             # activation kernel
-            if isinstance(x, QAct) and x.q.dim() == 2 and x.q.shape[0] <= 64 and x.scale.dim() == 1:
+            if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and self.up.glu_rows_ok(x.q.shape[0]) \
+                    and (x.q.shape[0] <= 64 or getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0])):
                 return self.down(self.up.glu(x))
             return self.down(act_fn(self.up(x), "silu_glu_blocked", True))
         h = self.up(x)

@@ -66,8 +66,20 @@ def rms_norm_parts(parts, residual, weight, eps, quant: bool):
     return ext().rms_norm_parts(parts, residual, weight, eps, quant)
 
 
+def decode_rows_ok(M: int, K: int, splits: int = 1) -> bool:
+    """Whether the decode GEMV family (grouped scales, split-K, quantising GLU) takes M rows at
+    this K: every K up to 64 rows; 65-128 rows (two micro-batches in one) for the k-tile counts
+    gemm_i8.hip instantiates (K = 4096 whole; 4096 / 11008 / 14336 in 4 slices)."""
+    if M <= 64:
+        return True
+    if M > 128 or not available():
+        return False
+    return bool(ext().rows128_ok(K, splits))
+
+
 def w8a8_linear_splitk(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, splits: int = 0):
-    """Split-K W8A8 GEMV (GPU, M <= 64, K % 64 == 0): fp32 partial slices [S, M, N]."""
+    """Split-K W8A8 GEMV (GPU, K % 64 == 0, M <= 64 or ``decode_rows_ok(M, K, 4)``): fp32 partial
+    slices [S, M, N]."""
     return ext().w8a8_gemm_splitk(qx, x_scale, w_packed, w_scale, bias, N, K, splits)
 
 

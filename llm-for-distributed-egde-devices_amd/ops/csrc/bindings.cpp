@@ -42,6 +42,7 @@ int edge_sample_timestamps(int enable, unsigned long long* host_out16);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
+int edge_w8a8_rows128_ok(int K, int S);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_decode_attn_config(int target_wg);
 }
@@ -334,13 +335,13 @@ at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at
 }
 
 // ---------------------------------------------------------------------------------- int8 gemm
-// Activation scales: per token (sa [M]) or per (token, 64-column group) (sa [KT, Mpad], M <= 64).
+// Activation scales: per token (sa [M]) or per (token, 64-column group) (sa [KT, Mpad], M <= 128).
 int64_t a_scale_mpad(const at::Tensor& sa, int64_t M, int64_t KT) {
   need(sa, at::kFloat, "a_scale");
   if (sa.dim() == 2) {
     TORCH_CHECK(sa.size(0) == KT && sa.size(1) >= (M + 15) / 16 * 16 && sa.size(1) % 16 == 0,
                 "grouped a_scale must be [K/64, Mpad]");
-    TORCH_CHECK(M <= 64, "grouped activation scales are a decode (M <= 64) feature");
+    TORCH_CHECK(M <= 128, "grouped activation scales are a decode (M <= 128) feature");
     return sa.size(1);
   }
   TORCH_CHECK(sa.numel() == M, "a_scale must have one entry per row");
@@ -373,16 +374,17 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
   return out;
 }
 
-// Split-K W8A8 GEMV (decode, M <= 64): fp32 partial slices [S, M, N] (w-scale and bias applied; bias
-// in slice 0) for a consumer that sums them (rms_norm_parts).  S = 0 picks the split count.
+// Split-K W8A8 GEMV (decode, M <= 64, or <= 128 where rows128_ok(K, S)): fp32 partial slices
+// [S, M, N] (w-scale and bias applied; bias in slice 0) for a consumer that sums them (rms_norm_parts).  S = 0 picks the split count.
 at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                             const std::optional<at::Tensor>& bias, int64_t N, int64_t K, int64_t S) {
   need(a, at::kChar, "a");
   TORCH_CHECK(a.size(-1) == K && K % 64 == 0, "split-K GEMV needs K % 64 == 0");
   check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = K / 64;
-  TORCH_CHECK(M <= 64, "split-K GEMV is a decode (M <= 64) kernel");
+  TORCH_CHECK(M <= 128, "split-K GEMV is a decode (M <= 128) kernel");
   const int64_t mpad = a_scale_mpad(sa, M, KT);
+  if (S <= 0 && M > 64) S = 4;                           // 65-128 rows: 4 slices (gemm_i8.hip rows128)
   if (S <= 0) {
     const int64_t ntw = M <= 16 ? 2 : 4;                 // tiles per workgroup (gemm_i8.hip launcher)
     const int64_t groups = ((N + 15) / 16 + ntw - 1) / ntw;
@@ -435,7 +437,8 @@ std::tuple<at::Tensor, at::Tensor> w8a8_gemm_gluq(const at::Tensor& a, const at:
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
   check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = (K + 63) / 64, Mpad = (M + 15) / 16 * 16;
-  TORCH_CHECK(M <= 64 && N % 128 == 0, "quantising GLU needs M <= 64 and N % 128 == 0");
+  TORCH_CHECK(M <= (K == 4096 ? 128 : 64) && N % 128 == 0,
+              "quantising GLU needs M <= 64 (128 at K = 4096) and N % 128 == 0");
   TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GLU takes per-token activation scales");
   auto q = at::empty({M, N / 2}, a.options());
   auto s = at::empty({N / 128, Mpad}, a.options().dtype(at::kFloat));
@@ -514,6 +517,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("group_quant", &group_quant);
   m.def("sample", &sample);
   m.def("sample_timestamps", &sample_timestamps);
+  m.def("rows128_ok", [](int64_t K, int64_t S) { return edge_w8a8_rows128_ok((int)K, (int)S) != 0; },
+        "whether the 65-128 row decode GEMV has a kernel for K (in S split-K slices)");
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);

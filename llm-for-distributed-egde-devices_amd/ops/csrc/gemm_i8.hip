@@ -25,6 +25,9 @@
 //          (2 or 4 tiles per workgroup; rowwise.hip::group_quant_kernel quantises it for the down
 //          projection); EPI_GLUQ (8 tiles = 64 features) also quantises h per (token, 64 features)
 //          in the epilogue and writes int8 h + scales [N/128][Mpad] directly.
+//   ldsa:  gemv with the activations staged through LDS once per workgroup and one tile per
+//          wave: the 33-128 row GLUQ at K = 4096, and every projection at 65-128 rows (two
+//          decode micro-batches in one) for the k-tile counts of 4096-hidden models.
 //   tiled: M > 64 (prefill). 128x128 block tile, BK=64, 4 waves in 2x2, A and B staged with
 //          global_load_lds (16 B/lane, lane-linear fragment-ordered LDS images -> conflict-free
 //          ds_read_b128), LDS double buffer.
@@ -393,6 +396,141 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
                                               ks);
 }
 
+// ------------------------------------------------------------------------ LDS-staged activations
+// At 64 decode rows the weight-stationary GEMV above holds 8 tiles x 4 row blocks of accumulators
+// per wave (128 VGPRs), so only 8 waves fit and each waits one memory latency per step.  Here the
+// workgroup stages each step's activation fragments (C k-tiles x MB row blocks) in LDS once
+// (register-staged: global load, ds_write, one barrier per step; two LDS buffers) and every wave
+// reads them from there.  Wave w owns TPW tiles for all MB row blocks and one k-slice of every
+// step (NTW / TPW tile groups x KH k-slices), so its accumulators are TPW x MB fragments and its
+// registers go to prefetch: D steps of weight and activation loads are in flight per wave.  K is
+// a compile-time 64 * KTC and the step loop unrolls fully, so every register set has a name and
+// the compiler waits with counted vmcnt.  Loads are issued per step as [weights, activations],
+// so the wait that retires a step's activations (before their LDS write) retires only loads the
+// next step needs anyway.  The reduction over the KH k-slices reuses the activation buffers.
+// Measured on gate_up at 64 rows (22016 x 4096, SwiGLU + int8 epilogue): 26.3 us against 33.9 us
+// for the weight-stationary kernel; TPW 1 / 2, D 1..6 and 8- or 16-wave register staging (tile
+// groups sharing one LDS image) all land at 26-29 us, the per-CU load rate of 172 busy CUs.
+// KTC (k-tiles per workgroup) need not be a multiple of the step: the last step's missing k-tiles
+// are skipped by wave-uniform branches.  EPI_PART: workgroup (group, ks) reduces k-tiles
+// [ks * KTC, (ks + 1) * KTC) and writes fp32 partials (KT == S * KTC).  SCALED (A_GROUP): each
+// step's per-(token, 64) scales are staged beside the activations and every k-tile's exact int32
+// MFMA sum is folded into a float accumulator with its scale.
+template <int MB, int NTW, int TPW, int KH, int KPW, int D, int KTC, bool SCALED, int EPI>
+__global__ void __launch_bounds__(NTW / TPW * KH * 64) w8a8_gemv_ldsa_kernel(
+    const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
+    const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
+    int M, int N, int K, int NTt, int Mpad, int S) {
+  constexpr int TG = NTW / TPW, NW = TG * KH, C = KH * KPW, STEPS = (KTC + C - 1) / C;
+  constexpr int DD = D < STEPS ? D : STEPS - 1;          // steps in flight ahead
+  constexpr int F = NTW * MB, NFRAG = C * MB, FPW = NFRAG / NW;
+  constexpr int ROWS = MB * 16, SCH = SCALED ? C * ROWS / 256 : 0;   // waves staging 64 x v4f scales
+  constexpr int ABYTES = 2 * NFRAG * 1024 + 2 * C * ROWS * 4 * (SCALED ? 1 : 0), RBYTES = KH * F * 1024;
+  static_assert(NTW % TPW == 0 && NFRAG % NW == 0 && DD >= 1 && SCH <= NW && (!SCALED || C * ROWS % 256 == 0), "shape");
+  static_assert(RBYTES <= 131072 && ABYTES <= 131072, "LDS budget");
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTW == 8 && !SCALED), "epilogues");
+  __shared__ __attribute__((aligned(16))) v4i lds[(ABYTES > RBYTES ? ABYTES : RBYTES) / 16];
+  __shared__ float gmax[MB][4][16];
+  float* lsc = reinterpret_cast<float*>(lds + 2 * NFRAG * 64);   // [2][C][ROWS] staged scales
+  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
+  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
+  const int kbeg = ks * KTC, KT = K / 64;
+  const int nt0 = grp * NTW;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t0 = (wave % TG) * TPW, h = wave / TG;
+  const int akc = 16 * (lane >> 4);
+  const v4i* wp[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+    wp[j] = reinterpret_cast<const v4i*>(Wp + ((size_t)min(nt0 + t0 + j, NTt - 1) * KT + kbeg) * 1024);
+  const int8_t* asrc[FPW];
+  int fid[FPW], fk[FPW];
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) {
+    const int f = wave + i * NW;                           // fragment (k-tile f / MB, rows f % MB)
+    fid[i] = f;
+    fk[i] = f / MB;
+    asrc[i] = A + (size_t)min((f % MB) * 16 + (lane & 15), M - 1) * K + (size_t)kbeg * 64 + akc;
+  }
+  // scale staging: wave w < SCH loads v4f e = w * 64 + lane of the step's [C][ROWS] block
+  const int se = (wave * 64 + lane) * 4, skk = se / ROWS, srow = min(se % ROWS, Mpad - 4);
+  const auto pre = epi_preload<MB, NTW, NW, EPI>(sw, bias, nt0, NTt, wave, lane);
+  v4i acc[TPW][MB];
+  v4f accf[TPW][MB];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int i = 0; i < MB; ++i) { acc[j][i] = v4i{0, 0, 0, 0}; accf[j][i] = v4f{0.f, 0.f, 0.f, 0.f}; }
+  v4i w[DD + 1][TPW][KPW], ast[DD][FPW];
+  v4f sst[DD];
+  // s is a compile-time value after unrolling; k-tiles past KTC are clamped (loads) or skipped
+  auto issue = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+      for (int u = 0; u < KPW; ++u)
+        w[s % (DD + 1)][j][u] = __builtin_nontemporal_load(wp[j] + min(s * C + h * KPW + u, KTC - 1) * 64 + lane);
+#pragma unroll
+    for (int i = 0; i < FPW; ++i)
+      ast[s % DD][i] = *reinterpret_cast<const v4i*>(asrc[i] + min(s * C + fk[i], KTC - 1) * 64);
+    if constexpr (SCALED)
+      if (wave < SCH)
+        sst[s % DD] = *reinterpret_cast<const v4f*>(sa + (size_t)(kbeg + min(s * C + skk, KTC - 1)) * Mpad + srow);
+  };
+  auto stage = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < FPW; ++i)
+      if ((s + 1) * C <= KTC || s * C + fk[i] < KTC) lds[((size_t)(s & 1) * NFRAG + fid[i]) * 64 + lane] = ast[s % DD][i];
+    if constexpr (SCALED)
+      if (wave < SCH) *reinterpret_cast<v4f*>(lsc + (s & 1) * C * ROWS + se) = sst[s % DD];
+  };
+#pragma unroll
+  for (int s = 0; s < DD; ++s) issue(s);
+  stage(0);
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) {
+    if (s + DD < STEPS) issue(s + DD);
+#pragma unroll
+    for (int u = 0; u < KPW; ++u) {
+      if ((s + 1) * C <= KTC || s * C + h * KPW + u < KTC) {   // wave-uniform: ragged last step
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+          const v4i a = lds[((size_t)(s & 1) * NFRAG + (h * KPW + u) * MB + i) * 64 + lane];
+          if constexpr (SCALED) {
+            const v4f sg = *reinterpret_cast<const v4f*>(lsc + (s & 1) * C * ROWS + (h * KPW + u) * ROWS + i * 16 +
+                                                         4 * (lane >> 4));
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) fold(accf[j][i], mfma_i8(a, w[s % (DD + 1)][j][u], v4i{0, 0, 0, 0}), sg);
+            // pin the folds every 4 row blocks: unpinned, the compiler sinks every step's cvt/fma
+            // chain to the epilogue and keeps all MFMA results alive (100+ spilled VGPRs)
+            if (i % 4 == 3)
+#pragma unroll
+              for (int ii = i - 3; ii <= i; ++ii)
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) asm volatile("" : "+v"(accf[j][ii]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) acc[j][i] = mfma_i8(a, w[s % (DD + 1)][j][u], acc[j][i]);
+          }
+        }
+      }
+    }
+    if (s + 1 < STEPS) {
+      stage(s + 1);
+      __syncthreads();
+    }
+  }
+  __syncthreads();                                         // activation buffers become the reduction buffer
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+      lds[((size_t)h * F + (t0 + j) * MB + i) * 64 + lane] = SCALED ? __builtin_bit_cast(v4i, accf[j][i]) : acc[j][i];
+  __syncthreads();
+  gemv_epilogue<MB, NTW, NW, KH, SCALED, EPI>(lds, sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane, ks);
+}
+
 // ------------------------------------------------------------------------------------ tiled
 // Block tile 128 x 128, BK = 64. LDS image per buffer: A 8 x 1 KiB fragments, B 8 x 1 KiB.
 constexpr int BM = 128, BN = 128;
@@ -496,6 +634,47 @@ int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, 
   return (int)hipGetLastError();
 }
 
+template <int MB, int NTW, int TPW, int KH, int KPW, int D, int KTC, bool SC, int EP>
+int launch_ldsa(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                float* os, int M, int N, int K, int Mpad, hipStream_t st, int S = 1) {
+  const int NTt = (N + 15) / 16;
+  hipLaunchKernelGGL((w8a8_gemv_ldsa_kernel<MB, NTW, TPW, KH, KPW, D, KTC, SC, EP>),
+                     dim3((NTt + NTW - 1) / NTW * S), dim3(NTW / TPW * KH * 64), 0, st, (const int8_t*)A, sa,
+                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);
+  return (int)hipGetLastError();
+}
+
+// 65-128 rows (two decode micro-batches in one): LDS-staged activations, one tile per wave, 8 row
+// blocks of accumulators.  Instantiated for the k-tile counts of the 4096-hidden models (K = 4096
+// whole, and K = 4096 / 11008 / 14336 in 4 split-K slices); -1 = no kernel for this shape.
+}  // namespace
+
+// k-tile counts launch_rows128 has kernels for: the whole K (S = 1) or each of S split-K slices
+extern "C" int edge_w8a8_rows128_ok(int K, int S) {
+  if (K <= 0 || S < 1 || K % 64 != 0 || (K / 64) % S != 0) return 0;
+  const int ktc = K / 64 / S;
+  return S > 1 ? (ktc == 16 || ktc == 43 || ktc == 56) : ktc == 64;
+}
+
+namespace {
+template <int EP>
+int launch_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                   float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
+  if (!edge_w8a8_rows128_ok(K, S) || (EP == EPI_PART) != (S > 1)) return -1;
+  const int ktc = K / 64 / S;
+#define R128(KTC)                                                                                                   \
+  if (ktc == KTC)                                                                                                   \
+    return scaled ? launch_ldsa<8, 4, 1, 4, 1, 2, KTC, true, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S) \
+                  : launch_ldsa<8, 4, 1, 4, 1, 2, KTC, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
+  if constexpr (EP == EPI_PART) {
+    R128(16) R128(43) R128(56)
+  } else {
+    R128(64)
+  }
+#undef R128
+  return -1;
+}
+
 // EPI_OUT: 16 waves; KW = 16 while the LDS reduction fits (KW x NTW x MB KiB <= 128 KiB), else 8
 template <int MB, int AM>
 int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const void* Wp, const float* sw,
@@ -532,9 +711,13 @@ int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const vo
 extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                                      float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S,
                                      hipStream_t st) {
-  if (M <= 0 || M > 64 || K % 64 != 0 || K / 64 != KT || S < 1 || S > KT) return -2;
+  if (M <= 0 || M > 128 || K % 64 != 0 || K / 64 != KT || S < 1 || S > KT) return -2;
   const int mblocks = (M + 15) / 16;
   if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
+  if (M > 64) {
+    const int r = launch_rows128<EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, S);
+    return r == -1 ? -2 : r;
+  }
   // 2 tiles per workgroup for one row block, 4 for more (the binding sizes S for ~256 workgroups;
   // measured on Llama-2-7B o/down: S = 2 best at 16 rows, S = 4 at 32)
 #define SK(MBV, KWV, AMV)                                                                                          \
@@ -563,9 +746,16 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   if (M == 0 || N == 0) return 0;
   const int NTt = (N + 15) / 16;
   const int mblocks = (M + 15) / 16;
-  if (a_mode != A_TOKEN && (M > 64 || (a_mode == A_GROUP && Mpad < mblocks * 16))) return -2;
+  if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
+  if (M > 64 && M <= 128 && epi == EPI_OUT && g_gemv_unroll != 1) {
+    const int r = launch_rows128<EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, 1);
+    if (r != -1) return r;
+  }
+  if (a_mode != A_TOKEN && M > 64) return -2;
   if (epi == EPI_GLU || epi == EPI_GLUQ) {
-    if (a_mode != A_TOKEN || M > 64 || N % (epi == EPI_GLUQ ? 128 : 32) != 0) return -2;
+    const bool ldsa = KT == 64 && K == 4096 && N % 128 == 0 && g_gemv_unroll != 1;
+    if (a_mode != A_TOKEN || M > (epi == EPI_GLUQ && ldsa ? 128 : 64) || N % (epi == EPI_GLUQ ? 128 : 32) != 0)
+      return -2;
     if (epi == EPI_GLUQ) {
       if (os == nullptr || Mpad < mblocks * 16) return -2;
       // 8 tiles = 64 features; 16 waves as (TG tile groups) x (KW k-waves) within the LDS budget
@@ -576,6 +766,12 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
         return launch_one<1, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
       }
       if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      // K = 4096: activations staged in LDS (unroll knob 1 = the weight-stationary form)
+      if (ldsa) {
+        if (mblocks > 4) return launch_ldsa<8, 8, 1, 2, 2, 2, 64, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st);
+        if (g_gemv_kw == 2) return launch_ldsa<4, 8, 2, 4, 1, 4, 64, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st);
+        return launch_ldsa<4, 8, 1, 2, 4, 2, 64, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st);
+      }
       // (4 waves with U = 2 / 4 and AGPR accumulators measured 45.6 / 41.4 us against 34.3 us here)
       return launch_one<4, 8, 1, 8, 1, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
     }

@@ -121,12 +121,23 @@ class W8A8Linear(nn.Module):
         K, N = self.in_features, self.out_features
         shp = x.q.shape[:-1]
         scale = x.scale if x.scale.dim() == 2 and x.q.dim() == 2 else x.scale.reshape(-1)
-        if self.split_k_out and x.q.is_cuda and ops.gpu_path(x.q) and K % 64 == 0 and 0 < x.q.numel() // K <= 64:
+        M = x.q.numel() // K
+        if self.split_k_out and x.q.is_cuda and ops.gpu_path(x.q) and K % 64 == 0 and 0 < M and \
+                ops.decode_rows_ok(M, K, 4 if M > 64 else 1):
             return PartialSum(ops.w8a8_linear_splitk(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale,
                                                      self.bias, N, K, self.split_k_out if self.split_k_out > 1 else 0))
         out = ops.w8a8_linear(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale, self.bias,
                               N, K, w_ref=self._wref(x.q), out_dtype=self.out_dtype)
         return out.view(*shp, N)
+
+    def group_scales_ok(self, M: int) -> bool:
+        """Whether this projection consumes per-(token, 64) activation scales at M rows."""
+        K = self.in_features
+        return ops.decode_rows_ok(M, K) or (bool(self.split_k_out) and ops.decode_rows_ok(M, K, 4))
+
+    def glu_rows_ok(self, M: int) -> bool:
+        """Whether the fused gate_up + SwiGLU kernel takes M rows (65-128: quantising form only)."""
+        return M <= 64 or (self.out_features % 128 == 0 and ops.decode_rows_ok(M, self.in_features))
 
     def glu(self, x: QAct):
         """Fused gate_up -> silu(g) * u (blocked layout, M <= 64) for the down projection: int8
@@ -134,7 +145,7 @@ class W8A8Linear(nn.Module):
         ``glu_quant_rows(M)``, else bf16 h that the down projection quantises per group."""
         K, N = self.in_features, self.out_features
         M = x.q.numel() // K
-        quant = N % 128 == 0 and glu_quant_rows(M)
+        quant = N % 128 == 0 and (glu_quant_rows(M) or M > 64)
         out = ops.w8a8_glu(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,
                            w_ref=self._wref(x.q), quant=quant)
         return QAct(*out) if quant else GroupQuantBF16(out)

@@ -183,6 +183,76 @@ def test_glu_forms_agree(cuda, M):
     assert (err <= 0.51 * step + 1e-2 * ref.float().view(M, F // 64, 64).abs() + 1e-3).all(), err.max().item()
 
 
+@pytest.mark.parametrize("M", [65, 100, 128])
+@pytest.mark.parametrize("grouped", [False, True])
+@pytest.mark.parametrize("N,K,S", [(12288, 4096, 1), (4096, 4096, 4), (4096, 11008, 4), (1024, 14336, 4)])
+def test_gemv_rows128(cuda, M, grouped, N, K, S):
+    """65-128 rows (LDS-staged kernel, 8 row blocks): whole-K outputs and split-K partial slices
+    against the fp32 reference, per-token and per-(token, 64) activation scales."""
+    C = ops.ext()
+    assert C.rows128_ok(K, S)
+    torch.manual_seed(M + K)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = (torch.rand(K // 64, (M + 15) // 16 * 16, device=cuda) if grouped else torch.rand(M, device=cuda)) * 0.01
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
+    if S == 1:
+        out = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+        _close(out, ref, 1e-2, 1e-2)
+    else:
+        parts = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
+        assert parts.shape == (S, M, N)
+        _close(parts.sum(0), ref, 1e-3, 1e-2)
+        assert torch.equal(parts, C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S))
+
+
+@pytest.mark.parametrize("M", [65, 100, 128])
+def test_gluq_beyond_64_rows(cuda, M):
+    """The quantising GLU epilogue at 5-8 row blocks (LDS-staged kernel, K = 4096)."""
+    C = ops.ext()
+    F, K = 11008, 4096
+    torch.manual_seed(M)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (2 * F, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
+    wb, swb = _ref.block_glu_rows(w), _ref.block_glu_rows(sw)
+    wp = ops.pack_int8_weight(wb)
+    ref = _ref.silu_mul(_ref.unblock_glu(_ref.w8a8_linear(qx, sx, wb, swb, None, torch.bfloat16)))
+    q, s = C.w8a8_gemm_gluq(qx, sx, wp, swb, None, 2 * F, K)
+    step = s[:, :M].t().unsqueeze(-1)
+    deq = q.float().view(M, F // 64, 64) * step
+    err = (deq - ref.float().view(M, F // 64, 64)).abs()
+    assert (err <= 0.51 * step + 1e-2 * ref.float().view(M, F // 64, 64).abs() + 1e-3).all(), err.max().item()
+
+
+@pytest.mark.parametrize("M", [33, 48, 64])
+@pytest.mark.parametrize("gate_up", [(22016, 4096), (1024, 4096)])
+def test_gluq_lds_staged_matches_weight_stationary(cuda, M, gate_up):
+    """The LDS-staged-activation GLUQ kernel (K = 4096, 3-4 row blocks) and the weight-stationary
+    kernel sum the same exact int32 products and share the epilogue: bit-identical outputs."""
+    C = ops.ext()
+    N, K = gate_up
+    torch.manual_seed(M)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.004 + 1e-4
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    q_new, s_new = C.w8a8_gemm_gluq(qx, sx, wp, sw, bias, N, K)
+    try:
+        C.tune("gemv", 0, 1)                         # unroll knob 1 = weight-stationary kernel
+        q_old, s_old = C.w8a8_gemm_gluq(qx, sx, wp, sw, bias, N, K)
+    finally:
+        C.tune("gemv", 0, 0)
+    assert torch.equal(q_new, q_old)
+    assert torch.equal(s_new, s_old)
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 32, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (2048, 8192), (1040, 1024)])
 @pytest.mark.parametrize("grouped", [False, True])

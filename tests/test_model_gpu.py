@@ -65,6 +65,27 @@ def test_flagship_shape_smoke(cuda):
     assert all(len(t) == 16 for t in res.tokens)
 
 
+@pytest.mark.parametrize("B", [96, 128])
+def test_w8a8_decode_128_rows_4096_hidden(cuda, B):
+    """At 4096 hidden (the k-tile counts with 65-128 row kernels) a decode batch of up to 128 keeps
+    the fused decode path: grouped-scale attention output, split-K o/down, quantising GLU.  The
+    tokens must agree with the same prompts decoded at B = 16."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.quant import quantize_model
+    from edgellm import ops as eops
+    cfg = tiny("llama2", hidden_size=4096, num_heads=32, num_kv_heads=32, intermediate_size=4096, num_layers=1)
+    model = quantize_model(build_model(cfg, device=cuda, seed=5), "w8a8_smoothquant")
+    assert eops.decode_rows_ok(B, 4096) and eops.decode_rows_ok(B, 4096, 4)
+    g = torch.Generator().manual_seed(1)
+    prompts = torch.randint(0, cfg.vocab_size, (B, 12), generator=g).tolist()
+    sp = SamplingParams(max_new_tokens=6, do_sample=False)
+    big = Generator(model, max_batch=B, max_seq=32).generate(prompts, sp, seed=0).tokens
+    small = Generator(model, max_batch=16, max_seq=32).generate(prompts[:16], sp, seed=0).tokens
+    same = sum(a == b for ra, rb in zip(big[:16], small) for a, b in zip(ra, rb))
+    assert len(big) == B and same >= 0.85 * 16 * 6
+
+
 @pytest.mark.parametrize("B", [64, 80])
 def test_w8a8_decode_beyond_gemv_rows(cuda, B):
     """Decode batches above the 64-row GEMV limit take the tiled GEMM and per-token quantisation

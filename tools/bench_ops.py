@@ -57,7 +57,7 @@ def timeit(fn, iters=50, warm=3, per_graph=20):
     return ts[len(ts) // 2] * 1e3 / per_graph  # median us per call
 
 
-def gemv_rows(C, dev, Ms=(1, 16, 32, 64), sweep=True, grouped=False, shapes=None):
+def gemv_rows(C, dev, Ms=(1, 16, 32, 64, 128), sweep=True, grouped=False, shapes=None):
     """Cache-cold INT8 GEMV sweep.  ``grouped``: per-(token, 64-column) activation scales (the
     decode o/down projections after the fused producers)."""
     shapes = shapes or {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
@@ -74,6 +74,8 @@ def gemv_rows(C, dev, Ms=(1, 16, 32, 64), sweep=True, grouped=False, shapes=None
         wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
         sw = torch.rand(N, device=dev) * 0.01
         for M in Ms:
+            if M > 64 and grouped and not C.rows128_ok(K, 1):
+                continue                                  # (65-128 grouped rows: split-K shapes only)
             qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
             sx = (torch.rand((K + 63) // 64, (M + 15) // 16 * 16, device=dev) if grouped
                   else torch.rand(M, device=dev)) * 0.01
@@ -86,7 +88,7 @@ def gemv_rows(C, dev, Ms=(1, 16, 32, 64), sweep=True, grouped=False, shapes=None
 
             for rnd in range(2):  # interleaved rounds
                 for nw, u, ntw in variants:
-                    if u == 4 and (M > 16 or ntw > 1):
+                    if (u == 4 and (M > 16 or ntw > 1)) or (M > 64 and (nw, u, ntw) != (0, 0, 0)):
                         continue
                     tune(C, "gemv", nw, u)
                     tune(C, "gemv_ntw", ntw, 0)
@@ -105,7 +107,7 @@ def gemv_rows(C, dev, Ms=(1, 16, 32, 64), sweep=True, grouped=False, shapes=None
     return out
 
 
-def glu_rows(C, dev, Ms=(1, 16, 32, 64)):
+def glu_rows(C, dev, Ms=(1, 16, 32, 64, 128)):
     """Decode MLP front half (Llama-2-7B: F = 11008), cache-cold: gate_up GEMV + SwiGLU writing
     bf16 h (2 or 4 tiles per workgroup) followed by the group-quant kernel, vs the 8-tile form
     that quantises h in its own epilogue (4 or 8 waves)."""
@@ -128,7 +130,8 @@ def glu_rows(C, dev, Ms=(1, 16, 32, 64)):
             ctr[0] = (ctr[0] + 1) % ncopy
             return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
 
-        variants = [("bf16+group_quant", bf16_then_quant, 0, 0), ("quant_epilogue", quant_epilogue, 0, 0)]
+        variants = [("bf16+group_quant", bf16_then_quant, 0, 0)] if M <= 64 else []
+        variants.append(("quant_epilogue", quant_epilogue, 0, 0))
         res = {}
         for rnd in range(2):
             for name, fn, ntw, nw in variants:
