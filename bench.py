@@ -10,7 +10,7 @@ Work per step: every in-flight sequence decodes one token, sampled with the refe
 (T=0.7, top-k 50, top-p 0.9, repetition penalty 1.1 — Code/others/config.yaml:3-7).
 N = 1 runs graph-captured Generators on one GPU; N > 1 runs the RCCL pipeline with one stage
 (~32/N decoder layers) per GPU and N x lanes micro-batches in flight.  Every GPU decodes ``lanes``
-micro-batches concurrently on separate HIP streams (default 2 x 64 sequences), so per-GPU work
+micro-batches concurrently on separate HIP streams (default 2 x 128 sequences), so per-GPU work
 per step is constant (weak scaling: global batch = micro-batch x lanes x N).
 Weights: random-init Llama-2-7B architecture; the FULL model is SmoothQuant-calibrated on
 synthetic tokens and smoothed once, then each rank keeps its layers, so every split runs
@@ -50,8 +50,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama-2-7b")
     ap.add_argument("--quant", default="w8a8_smoothquant", choices=["none", "w8a8_smoothquant", "w8a8"])
-    ap.add_argument("--micro-batch", type=int, default=64,
-                    help="sequences per micro-batch (64: the throughput point; 16 and 32 trade tok/s for latency)")
+    ap.add_argument("--micro-batch", type=int, default=128,
+                    help="sequences per micro-batch (128: the largest the fused decode GEMVs take; with --lanes 1 "
+                         "the latency point, 16-64 trade tok/s for latency)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--lanes", type=int, default=2,
