@@ -166,6 +166,18 @@ def other_rows(C, dev, only=None):
                             TBps=round(nbytes / t / 1e6, 2)))
             print(out[-1], flush=True)
         C.tune("decode_attn", 0, 0)
+    for Bf, L in (((64, 160), (128, 160), (128, 512)) if want("attn_fused") else ()):
+        # the model's decode attention: RoPE + KV append + attention + per-(token, 64) int8 output
+        S = L + 8
+        qkv = torch.randn(Bf, 3 * Hq * D, device=dev).bfloat16()
+        kc = torch.randn(Bf, Hq, S, D, device=dev).bfloat16()
+        vc = torch.randn_like(kc)
+        sl = torch.full((Bf,), L, dtype=torch.int32, device=dev)
+        rope = ops.rope_tables(D, S, 10000.0, device=dev)
+        t = timeit(lambda: C.decode_attn_fused(qkv, sl - 1, rope, kc, vc, sl, Hq, 1 / math.sqrt(D), L, D, True))
+        nbytes = 2 * Bf * Hq * L * D * 2
+        out.append(dict(op="decode_attn_fused_q", B=Bf, Hkv=Hq, ctx=L, us=round(t, 2), TBps=round(nbytes / t / 1e6, 2)))
+        print(out[-1], flush=True)
     if want("small"):
         out += small_rows(C, dev, B, H, Hq, D)
     if want("sample"):
@@ -249,7 +261,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--tune", action="append", default=[], help="name=a[,b] passed to ext().tune (repeatable)")
-    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,small,sample,prefill")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
