@@ -61,8 +61,11 @@ __device__ __forceinline__ void quant_group_store(float v, int8_t* q, float* s_s
 
 template <int D> struct Lanes { static constexpr int v = (D / 8 <= 8) ? 8 : ((D / 8 <= 16) ? 16 : 32); };
 
-template <int D, int G, bool DIRECT, bool FUSED, bool QOUT>
-__global__ void __launch_bounds__(NT) decode_attn_kernel(
+// OCC > 0: single-buffered key loop, nontemporal K/V loads and at least OCC waves per SIMD
+// (occupancy instead of a second register buffer), and FUSED keeps the new key in registers (no
+// append barrier); OCC = 0: two register buffers, no occupancy target.
+template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC>
+__global__ void __launch_bounds__(NT, OCC > 0 ? OCC : 1) decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     int64_t c_sb, int64_t c_sh, const int* __restrict__ seq_lens, float scale_log2, int CH, int nsplit,
     bf16_t* __restrict__ out, int64_t o_sb, float* __restrict__ part_acc, float* __restrict__ part_ml, Fuse fz) {
@@ -126,27 +129,53 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
     }
   }
 
+  // OCC > 0 keeps the new token's rotated k and v in wave 0's registers (lanes kl = 0 / 1 hold
+  // dims d0..d0+7) and adds that key to the softmax directly, so no barrier orders the append
+  // before the cache reads and the K/V loads start at once; the cache loop skips the new key.
+  float knew[8], vnew[8];
+  bool own = false;
   if constexpr (FUSED) {
     // append the new token's rotated k and its v (only the split that owns the position)
     const int pos = fz.pos[b];
-    if (pos >= start && pos < end) {
-      const int Hkv = gridDim.y;
-      const bf16_t* row = q + b * fz.qkv_sb;
-      const float2* csp = reinterpret_cast<const float2*>(fz.cs) + (size_t)pos * (fz.rot / 2);
-      for (int c = threadIdx.x; c < 2 * (D / 8); c += NT) {
-        const bool is_v = c >= D / 8;
-        const int e0 = (is_v ? c - D / 8 : c) * 8;
+    own = pos >= start && pos < end;
+    const int Hkv = gridDim.y;
+    const bf16_t* row = q + b * fz.qkv_sb;
+    const float2* csp = reinterpret_cast<const float2*>(fz.cs) + (size_t)pos * (fz.rot / 2);
+    if constexpr (OCC > 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { knew[j] = 0.f; vnew[j] = 0.f; }
+      if (own && wave == 0 && kl < 2 && dvalid) {
+        const bool is_v = kl == 1;
         const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + kvh) * D;
         float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(head + e0), v);
-        if (!is_v && e0 < fz.rot) rope8(head, e0, fz.rot, csp, v);
-        *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + e0) = pack8(v);
+        unpack8(*reinterpret_cast<const uint4*>(head + d0), v);
+        if (!is_v && d0 < fz.rot) rope8(head, d0, fz.rot, csp, v);
+        *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + d0) = pack8(v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {                // the cached bf16 value
+          const float r = bf2f(f2bf(v[j]));
+          knew[j] = is_v ? 0.f : r;
+          vnew[j] = is_v ? r : 0.f;
+        }
       }
+    } else {
+      if (own) {
+        for (int c = threadIdx.x; c < 2 * (D / 8); c += NT) {
+          const bool is_v = c >= D / 8;
+          const int e0 = (is_v ? c - D / 8 : c) * 8;
+          const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + kvh) * D;
+          float v[8];
+          unpack8(*reinterpret_cast<const uint4*>(head + e0), v);
+          if (!is_v && e0 < fz.rot) rope8(head, e0, fz.rot, csp, v);
+          *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + e0) = pack8(v);
+        }
+      }
+      // Only this workgroup reads the new row, so the barrier's workgroup-scope release/acquire is
+      // enough (an agent-scope __threadfence would write back L2 in every workgroup: 3x slower).
+      __syncthreads();
     }
-    // Only this workgroup reads the new row, so the barrier's workgroup-scope release/acquire is
-    // enough (an agent-scope __threadfence would write back L2 in every workgroup: 3x slower).
-    __syncthreads();
   }
+  const int nl = (OCC > 0 && FUSED && own) ? n - 1 : n;   // keys read from the cache
 
   // ---- one pass: each wave keeps an online softmax (m, l, acc) over its key slice; K and V rows
   // are loaded together and the next chunk is in flight while the current one is consumed
@@ -167,9 +196,14 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int k = base + kl + u * KPB;
-      const size_t off = (size_t)(k < n ? k : 0) * D + dc;
-      kr[u] = *reinterpret_cast<const uint4*>(kb + off);
-      vr[u] = *reinterpret_cast<const uint4*>(vb + off);
+      const size_t off = (size_t)(k < nl ? k : 0) * D + dc;
+      if constexpr (OCC > 0) {                   // read once per step: nontemporal
+        kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + off)));
+        vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + off)));
+      } else {
+        kr[u] = *reinterpret_cast<const uint4*>(kb + off);
+        vr[u] = *reinterpret_cast<const uint4*>(vb + off);
+      }
     }
   };
   auto consume = [&](int base, const uint4 (&kr)[UNROLL], const uint4 (&vr)[UNROLL]) {
@@ -194,7 +228,7 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
         for (int h = 0; h < G; ++h) s[u][h] += __shfl_xor(s[u][h], o, 64);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
-      if (base + kl + u * KPB >= n) {
+      if (base + kl + u * KPB >= nl) {
 #pragma unroll
         for (int h = 0; h < G; ++h) s[u][h] = -INFINITY;
       }
@@ -226,17 +260,43 @@ __global__ void __launch_bounds__(NT) decode_attn_kernel(
       }
     }
   };
-  {
+  if constexpr (OCC > 0 && FUSED) {
+    if (own && wave == 0) {                          // the new key first: m = its score, l = 1
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        float sp = 0.f;
+        if (kl == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sp += qf[h][j] * knew[j];
+        }
+#pragma unroll
+        for (int o = LPK / 2; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 64);
+        m[h] = __shfl(sp, dl, 64);                   // lane dl holds the kl = 0 group's sum
+        if (kl == 1) {
+          l[h] = 1.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[h][j] = vnew[j];
+        }
+      }
+    }
+  }
+  if constexpr (OCC > 0) {
+    uint4 ka[UNROLL], va[UNROLL];
+    for (int base = wave * KPW; base < nl; base += STEP) {  // wave-uniform trip count (shuffles inside)
+      load(base, ka, va);
+      consume(base, ka, va);
+    }
+  } else {
     uint4 ka[UNROLL], va[UNROLL], kb2[UNROLL], vb2[UNROLL];
     int base = wave * KPW;                           // wave-uniform trip count (shuffles inside)
-    if (base < n) load(base, ka, va);
-    while (base < n) {
+    if (base < nl) load(base, ka, va);
+    while (base < nl) {
       const int nb = base + STEP;
-      if (nb < n) load(nb, kb2, vb2);
+      if (nb < nl) load(nb, kb2, vb2);
       consume(base, ka, va);
-      if (nb >= n) break;
+      if (nb >= nl) break;
       const int nb2 = nb + STEP;
-      if (nb2 < n) load(nb2, ka, va);
+      if (nb2 < nl) load(nb2, ka, va);
       consume(nb, kb2, vb2);
       base = nb2;
     }
@@ -333,7 +393,28 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __rest
 
 // Workspace sizes (floats) for a given launch; the binding allocates them.
 static int g_target_wg = 512;   // >= 2 workgroups per CU before splitting K
+// fused kernels: 4 (default) / 5 = single-buffered, barrier-free, >= 4 / 5 waves per SIMD; 0 = the
+// double-buffered form with the append barrier (168 VGPRs, 3 waves per SIMD).  Measured at 128
+// sequences x 32 heads, context 160 (tools/bench_ops.py attn_fused): 57.7 / 60.4 / 66.6 us.
+static int g_attn_occ = 4;
 extern "C" void edge_decode_attn_config(int target_wg) { g_target_wg = target_wg > 0 ? target_wg : 512; }
+extern "C" void edge_decode_attn_occ(int occ) { g_attn_occ = occ == 0 || occ == 5 ? occ : 4; }
+
+namespace {
+template <int D, int G, bool DI, bool FU, bool QO>
+void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q_sb, void* k_cache, void* v_cache,
+                 int64_t c_sb, int64_t c_sh, const int* seq_lens, float sl2, int ch, int nsplit, void* out,
+                 int64_t o_sb, float* part_acc, float* part_ml, const Fuse& fz) {
+#define ATTN_ARGS grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, (bf16_t*)k_cache, (bf16_t*)v_cache, c_sb, c_sh, \
+                  seq_lens, sl2, ch, nsplit, (bf16_t*)out, o_sb, part_acc, part_ml, fz
+  if constexpr (FU) {                           // the model's decode step: occupancy variant selectable
+    if (g_attn_occ == 4) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 4>), ATTN_ARGS); return; }
+    if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 5>), ATTN_ARGS); return; }
+  }
+  hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 0>), ATTN_ARGS);
+#undef ATTN_ARGS
+}
+}  // namespace
 
 extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out) {
   const int target_wg = g_target_wg;
@@ -370,10 +451,9 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
   const size_t lds = (size_t)(NW * G * D + 2 * NW * G + 2 * G) * sizeof(float);
   const dim3 grid(nsplit, Hkv, B);
   const bool direct = nsplit == 1;
-#define DK(DD, GG, DI, FU, QO)                                                                                 \
-  hipLaunchKernelGGL((decode_attn_kernel<DD, GG, DI, FU, QO>), grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, \
-                     (bf16_t*)k_cache, (bf16_t*)v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, (bf16_t*)out, o_sb, \
-                     part_acc, part_ml, fz)
+#define DK(DD, GG, DI, FU, QO)                                                                                     \
+  launch_attn<DD, GG, DI, FU, QO>(grid, lds, st, q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, out, \
+                                  o_sb, part_acc, part_ml, fz)
 #define DLAUNCH(DD, GG)                                                     \
   do {                                                                      \
     if (direct) {                                                           \

@@ -45,6 +45,7 @@ void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_decode_attn_config(int target_wg);
+void edge_decode_attn_occ(int occ);
 }
 
 namespace {
@@ -523,6 +524,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
+    else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });
 }

@@ -29,10 +29,20 @@ def _close(a, b, atol, rtol=0.0):
                                           (8, 8, 256, 64), (12, 12, 64, 0)])
 @pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333)])
 @pytest.mark.parametrize("quant", [False, True])
-def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant):
+@pytest.mark.parametrize("occ", [0, 4, 5])
+def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant, occ):
     if quant and D % 64:
         pytest.skip("per-group output needs D % 64 == 0")
     C = ops.ext()
+    C.tune("decode_attn_occ", occ, 0)
+    try:
+        _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant)
+    finally:
+        C.tune("decode_attn_occ", 4, 0)
+
+
+def _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant):
+    cuda = torch.device("cuda")
     torch.manual_seed(3)
     B = len(lens)
     S = max(lens) + 5
