@@ -93,21 +93,38 @@ __global__ void __launch_bounds__(NT) norm_kernel(
   }
   float v[NCH][8];
   if constexpr (PART) {
+    // every slice's loads are issued before the first add (S <= 8: one memory round trip, not S)
     const size_t slice = (size_t)gridDim.x * H;
+    float4 pv[NCH][8][2];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = min((c * NT + (int)threadIdx.x) * 8, H - 8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < S) {
+          const float4* p = reinterpret_cast<const float4*>(xpart + k * slice + row * H + e);
+          pv[c][k][0] = p[0];
+          pv[c][k][1] = p[1];
+        }
+    }
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int e = (c * NT + threadIdx.x) * 8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
-      if (e < H) {
-        for (int k = 0; k < S; ++k) {
-          const float4* p = reinterpret_cast<const float4*>(xpart + k * slice + row * H + e);
-          const float4 p0 = p[0], p1 = p[1];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < S) {
+          const float4 p0 = pv[c][k][0], p1 = pv[c][k][1];
           v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
           v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
         }
+      if (e < H) {
         unpack8(pack8(v[c]), v[c]);                        // the GEMV output is bf16
         if constexpr (!HAS_RES) *reinterpret_cast<uint4*>(res_out + row * H + e) = pack8(v[c]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
       }
     }
   } else {
@@ -301,6 +318,7 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
 #define LAUNCH_NORMP(HR, QU) \
   hipLaunchKernelGGL((norm_kernel<NCH, true, HR, QU, true>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, \
                      eps, xpart, S)
+  if (xpart != nullptr && (S < 1 || S > 8 || H % 8 != 0)) return -2;   // partial slices: 1..8
   NCH_DISPATCH(H, {
     if (xpart != nullptr) {
       if (res) { if (quant) LAUNCH_NORMP(true, true); else LAUNCH_NORMP(true, false); }

@@ -203,6 +203,11 @@ def small_rows(C, dev, B, H, Hq, D):
         rr = torch.randn(rows, H, device=dev).bfloat16()
         t = timeit(lambda: C.norm(xx, rr, w, None, 1e-5, True, True))
         out.append(dict(op="rmsnorm_res_quant", rows=rows, H=H, us=round(t, 2)))
+    for rows, S in ((64, 4), (128, 4)):
+        parts = torch.randn(S, rows, H, device=dev)
+        rr = torch.randn(rows, H, device=dev).bfloat16()
+        t = timeit(lambda: C.rms_norm_parts(parts, rr, w, 1e-5, True))
+        out.append(dict(op="rmsnorm_parts_res_quant", rows=rows, S=S, H=H, us=round(t, 2)))
     gu = torch.randn(B, 2 * 11008, device=dev).bfloat16()
     out.append(dict(op="silu_mul_quant", rows=B, F=11008, us=round(timeit(lambda: C.act(gu, 0, True)), 2)))
     qkv = torch.randn(B, 3 * H, device=dev).bfloat16()
