@@ -92,3 +92,23 @@ def test_checkpoint_roundtrip(tmp_path, mode):
     # stage-sliced load gets the same layer weights
     st = load_quantized(str(tmp_path), first=1, last=2)
     assert st.layers[0].idx == 1 and isinstance(st.layers[0].attn.qkv, type(m.layers[1].attn.qkv))
+
+
+def test_decode_rows_capability_table():
+    """The 65-128 row decode GEMVs exist for the k-tile counts of the 4096-hidden models only: the
+    Python gates (grouped attention output, split-K, fused GLU) must agree with the kernel table."""
+    from edgellm import ops
+    if not ops.available():
+        pytest.skip("extension not built")
+    assert all(ops.decode_rows_ok(M, K) for M in (1, 17, 64) for K in (64, 1000, 11008))
+    assert ops.decode_rows_ok(128, 4096) and ops.decode_rows_ok(65, 4096)
+    assert not ops.decode_rows_ok(129, 4096) and not ops.decode_rows_ok(100, 11008)
+    for K in (4096, 11008, 14336):                      # o / down of Llama-2-7B, down of Llama-3-8B
+        assert ops.decode_rows_ok(128, K, 4)
+    assert not ops.decode_rows_ok(128, 2048, 4)
+    lin = W8A8Linear(11008, 4096, bias=False)
+    assert not lin.group_scales_ok(128)                 # whole-K 11008 at 128 rows: no kernel
+    lin.split_k_out = 4
+    assert lin.group_scales_ok(128) and lin.group_scales_ok(64)
+    up = W8A8Linear(4096, 22016, bias=False)
+    assert up.glu_rows_ok(128) and not W8A8Linear(2048, 11008, bias=False).glu_rows_ok(100)
