@@ -106,8 +106,13 @@ class MLP(nn.Module):
                     and (x.q.shape[0] <= 64 or getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0])):
                 return self.down(self.up.glu(x))
             return self.down(act_fn(self.up(x), "silu_glu_blocked", True))
+        down_q = getattr(self.down, "takes_quantized_input", False)
+        if self.act == "silu_glu" and type(self.up) is Linear and not down_q and not isinstance(x, QAct) \
+                and ops.bf16_gemv_ok(x, self.up.weight, glu=True):
+            # bf16 decode: gate_up GEMV with the SwiGLU epilogue (one launch, gemv_bf16.hip)
+            return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, glu=True))
         h = self.up(x)
-        h = act_fn(h, self.act, getattr(self.down, "takes_quantized_input", False))
+        h = act_fn(h, self.act, down_q)
         return self.down(h)
 
 

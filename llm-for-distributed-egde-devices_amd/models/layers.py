@@ -1,6 +1,7 @@
 """Building blocks shared by every decoder family.
 
-``Linear`` is the bf16 projection (a plain library GEMM: hipBLASLt through ``F.linear``);
+``Linear`` is the bf16 projection (decode rows: ``gemv_bf16.hip``; otherwise hipBLASLt through
+``F.linear`` — ``ops.linear_bf16``);
 quantised replacements live in ``edgellm.quant`` and expose the same interface:
 
     forward(x)                 -> y     x is bf16, or a QAct (int8 + per-token scale) when
@@ -14,7 +15,6 @@ from typing import NamedTuple, Optional
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import ops
 
@@ -58,7 +58,7 @@ class Linear(nn.Module):
     def forward(self, x):
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
-        return F.linear(x, self.weight, self.bias)
+        return ops.linear_bf16(x, self.weight, self.bias)     # decode rows: HIP GEMV; else hipBLASLt
 
     def extra_repr(self):
         return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, bf16"

@@ -213,6 +213,27 @@ def unpack_int8_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
     return w[:N, :K].contiguous()
 
 
+def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bool:
+    """Whether ``linear_bf16`` runs the HIP decode GEMV for this call (GPU, bf16, <= 16 rows,
+    K % 64 == 0, N % 16 == 0 (% 32 for the fused GLU))."""
+    K = x.shape[-1]
+    return (_gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_contiguous()
+            and 0 < x.numel() // max(K, 1) <= 16 and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0)
+
+
+def linear_bf16(x, weight, bias=None, glu: bool = False):
+    """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` (weights streamed once at
+    HBM rate; ``glu``: weight = [gate | up] and the result is silu(gate) * up); everything else is
+    ``F.linear`` (hipBLASLt on GPU)."""
+    if bf16_gemv_ok(x, weight, glu):
+        return ext().gemv_bf16(x, weight, bias, glu)
+    y = torch.nn.functional.linear(x, weight, bias)
+    if glu:
+        g, u = y.chunk(2, dim=-1)
+        return torch.nn.functional.silu(g.float()).mul(u.float()).to(y.dtype)
+    return y
+
+
 def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,
                 out_dtype=torch.bfloat16):
     """INT8 x INT8 -> int32 MFMA GEMM with per-channel weight dequant (+bias) -> bf16.

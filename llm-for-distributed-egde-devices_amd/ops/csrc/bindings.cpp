@@ -43,6 +43,8 @@ int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* 
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
 void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
+int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
+                   hipStream_t st);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_decode_attn_config(int target_wg);
 void edge_decode_attn_occ(int occ);
@@ -400,6 +402,23 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
   return part;
 }
 
+// bf16 decode GEMV (M <= 16, K % 64 == 0, N % 16 == 0): x [.., K] . w[N, K]^T (+ bias) -> bf16.
+// glu: w = [gate | up] (N = 2F) and the result is silu(gate) * up [.., F].
+at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& w, const std::optional<at::Tensor>& bias, bool glu) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "weight");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(-1), "weight must be [N, K] with K = x.size(-1)");
+  const int64_t K = x.size(-1), M = rows_of(x), N = w.size(0);
+  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+  auto os = x.sizes().vec();
+  os.back() = glu ? N / 2 : N;
+  auto out = at::empty(os, x.options());
+  check(edge_gemv_bf16(x.data_ptr(), w.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N,
+                       (int)K, glu ? 1 : 0, stream()),
+        "gemv_bf16");
+  return out;
+}
+
 // Per-(token, 64 columns) int8 quantisation: (q [M, K], scales [K/64, Mpad]).
 std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
   need(x, at::kBFloat16, "x");
@@ -510,6 +529,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_attn", &decode_attn);
   m.def("prefill_attn", &prefill_attn);
   m.def("w8a8_gemm", &w8a8_gemm);
+  m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]");
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
   m.def("w8a8_gemm_splitk", &w8a8_gemm_splitk);

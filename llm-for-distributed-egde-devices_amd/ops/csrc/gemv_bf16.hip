@@ -1,0 +1,145 @@
+// Decode GEMV for bf16 weights: y[M, N] = x[M, K] . W[N, K]^T (+ bias) -> bf16, M <= 16.
+// The fp16/bf16 evaluators (Phi-2, Pythia-1B, Llama-3.2-1B at batch 1) spend
+// most of a decode step here; hipBLASLt's small-M kernels stream the weights at about 2 TB/s.
+//
+// Weights stay in the Hugging Face [N, K] layout (the prefill GEMMs read the same tensor).  One
+// MFMA (v_mfma_f32_16x16x32_bf16) takes a 16-row x 32-k B fragment: lane l loads the 16 bytes
+// W[n0 + (l & 15)][k0 + 8 (l >> 4) ..].  A wave walks K in pairs of k-steps (64 elements), so
+// every weight row contributes one whole 128-byte line per pair.  A workgroup = 16 waves on NTW
+// 16-column tiles; wave w takes k-pairs w, w + 16, ..., keeping U pairs of weight loads in
+// flight (nontemporal: each weight byte is read once per step).  The 16 partial tiles are
+// reduced through LDS.  Rows >= M load a clamped row and are never stored.
+//   EPI_OUT: + bias, bf16 [M, N].
+//   EPI_GLU: W = [gate (F rows) | up (F rows)] (the natural gate_up concatenation); a workgroup's
+//            tiles are NTW/2 gate tiles and the matching up tiles, and it writes
+//            h = silu(gate) * up as bf16 [M, F] (gate and up rounded to bf16 first, as the
+//            unfused GEMM output is) — the separate SwiGLU launch disappears.
+#include "common.h"
+
+namespace {
+constexpr int EPI_OUT = 0, EPI_GLU = 1;
+constexpr int NW = 16;
+
+__device__ __forceinline__ v4f mfma_bf16(const v8s& a, const v8s& b, const v4f& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
+  return __builtin_bit_cast(v8s, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p)));
+}
+
+template <int NTW, int U, int EPI>
+__global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                            const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                            int M, int N, int K, int F) {
+  static_assert(EPI == EPI_OUT || NTW % 2 == 0, "GLU: gate/up tile pairs");
+  __shared__ v4f red[NW][NTW][64];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, kq = 8 * (lane >> 4);
+  // output column of tile j for this lane (EPI_GLU: gate tiles then the matching up tiles)
+  auto col_of = [&](int j) -> int {
+    if constexpr (EPI == EPI_GLU) {
+      const int f0 = blockIdx.x * (NTW / 2) * 16;
+      return j < NTW / 2 ? f0 + j * 16 + r : F + f0 + (j - NTW / 2) * 16 + r;
+    } else {
+      return (blockIdx.x * NTW + j) * 16 + r;
+    }
+  };
+  const bf16_t* wrow[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) wrow[j] = W + (size_t)min(col_of(j), N - 1) * K + kq;
+  const bf16_t* arow = A + (size_t)min(r, M - 1) * K + kq;
+  const int KP = K / 64;
+  v4f acc[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int kp = wave; kp < KP; kp += NW * U) {
+    v8s a[U][2], b[U][NTW][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = min(kp + u * NW, KP - 1) * 64;          // clamped: loads never branch
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        b[u][j][0] = ld_nt(wrow[j] + k);
+        b[u][j][1] = ld_nt(wrow[j] + k + 32);
+      }
+      a[u][0] = *reinterpret_cast<const v8s*>(arow + k);
+      a[u][1] = *reinterpret_cast<const v8s*>(arow + k + 32);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (kp + u * NW < KP) {                               // wave-uniform (scalar) guard
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          acc[j] = mfma_bf16(a[u][0], b[u][j][0], acc[j]);
+          acc[j] = mfma_bf16(a[u][1], b[u][j][1], acc[j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) red[wave][j][lane] = acc[j];
+  __syncthreads();
+  constexpr int OUTS = EPI == EPI_GLU ? NTW / 2 : NTW;      // output tiles; wave w < OUTS writes tile w
+  if (wave < OUTS) {
+    auto total = [&](int j) {                               // 4 LDS reads in flight (bounded registers)
+      v4f s = red[0][j][lane];
+#pragma unroll 4
+      for (int w = 1; w < NW; ++w) s += red[w][j][lane];
+      return s;
+    };
+    const int c0 = col_of(wave);
+    if constexpr (EPI == EPI_GLU) {
+      const int c1 = col_of(wave + NTW / 2);
+      const v4f g4 = total(wave), u4 = total(wave + NTW / 2);
+      const float bg = bias != nullptr ? bf2f(bias[c0]) : 0.f, bu = bias != nullptr ? bf2f(bias[c1]) : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 4 * (lane >> 4) + q;
+        const float g = bf2f(f2bf(g4[q] + bg)), u = bf2f(f2bf(u4[q] + bu));
+        if (row < M && c0 < F) out[(size_t)row * F + c0] = f2bf(g / (1.f + __expf(-g)) * u);
+      }
+    } else {
+      const v4f s4 = total(wave);
+      const float bv = bias != nullptr && c0 < N ? bf2f(bias[c0]) : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 4 * (lane >> 4) + q;
+        if (row < M && c0 < N) out[(size_t)row * N + c0] = f2bf(s4[q] + bv);
+      }
+    }
+  }
+}
+
+template <int NTW, int U, int EPI>
+int launch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
+           hipStream_t st) {
+  const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
+  hipLaunchKernelGGL((gemv_bf16_kernel<NTW, U, EPI>), dim3(groups), dim3(NW * 64), 0, st, (const bf16_t*)A,
+                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F);
+  return (int)hipGetLastError();
+}
+}  // namespace
+
+// epi 0: out bf16 [M, N]; epi 1 (GLU): W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F]
+// (F % 16 == 0).  M <= 16, K % 64 == 0, N % 16 == 0.  Returns -2 for shapes it does not take.
+extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
+                              hipStream_t st) {
+  if (M <= 0 || M > 16 || K % 64 != 0 || N % 16 != 0 || K <= 0) return -2;
+  const int KP = K / 64;
+  const int U = KP >= 64 ? 4 : 2;                            // k-pairs in flight per wave
+  if (epi == EPI_GLU) {
+    if (N % 32 != 0) return -2;
+    const int F = N / 2, ft = F / 16;
+    if (ft >= 512) return launch<4, 2, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st);
+    return U == 4 ? launch<2, 4, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st)
+                  : launch<2, 2, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st);
+  }
+  const int nt = N / 16;
+  // ~256 workgroups: one tile each below 512 tiles, then 2 or 4
+  if (nt >= 1024) return launch<4, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st);
+  if (nt >= 512) return U == 4 ? launch<2, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st)
+                               : launch<2, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st);
+  return U == 4 ? launch<1, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st)
+                : launch<1, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st);
+}

@@ -327,3 +327,48 @@ def test_model_split_k_decode_matches_unsplit(cuda):
         outs[on] = Generator(model, max_batch=4, max_seq=64).generate(prompts, sp, seed=0).tokens
     same = sum(a == b for ra, rb in zip(outs[0], outs[1]) for a, b in zip(ra, rb))
     assert same >= 0.9 * sum(len(r) for r in outs[0]), (outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 8192), (7680, 2560), (32000, 4096), (48, 64)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemv_bf16(cuda, M, N, K, bias):
+    """bf16 decode GEMV (gemv_bf16.hip) == fp32 reference of x . W^T (+ bias), rounded once."""
+    C = ops.ext()
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16() if bias else None
+    y = C.gemv_bf16(x, w, b, False)
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    _close(y, ref, 2e-2, 1e-2)
+    assert torch.equal(y, C.gemv_bf16(x, w, b, False))
+
+
+@pytest.mark.parametrize("M", [1, 7, 16])
+@pytest.mark.parametrize("F,K", [(8192, 2048), (5632, 2048), (64, 128)])
+def test_gemv_bf16_glu(cuda, M, F, K):
+    """Fused bf16 gate_up GEMV + SwiGLU over the natural [gate | up] rows == unfused reference
+    (gate and up rounded to bf16, as the GEMM output is)."""
+    C = ops.ext()
+    torch.manual_seed(F + M)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(2 * F, K, device=cuda) * 0.05).bfloat16()
+    h = C.gemv_bf16(x, w, None, True)
+    gu = (x.float() @ w.float().t()).bfloat16().float()
+    g, u = gu[:, :F], gu[:, F:]
+    ref = torch.nn.functional.silu(g) * u
+    assert h.shape == (M, F)
+    _close(h, ref, 2e-2, 2e-2)
+
+
+def test_linear_bf16_routes_decode_rows(cuda):
+    """ops.linear_bf16: <= 16 rows take the HIP GEMV, larger batches hipBLASLt; both agree."""
+    torch.manual_seed(0)
+    w = (torch.randn(4096, 2048, device=cuda) * 0.05).bfloat16()
+    x = torch.randn(16, 2048, device=cuda).bfloat16()
+    assert ops.bf16_gemv_ok(x, w) and not ops.bf16_gemv_ok(torch.cat([x, x]), w)
+    small = ops.linear_bf16(x, w)
+    big = ops.linear_bf16(torch.cat([x, x]), w)[:16]
+    _close(small, big, 2e-2, 1e-2)
