@@ -221,17 +221,20 @@ def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bo
             and 0 < x.numel() // max(K, 1) <= 16 and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0)
 
 
-def linear_bf16(x, weight, bias=None, glu: bool = False):
+_GEMV_EPI = {None: 0, "silu_glu": 1, "gelu_tanh": 2, "gelu": 3}
+
+
+def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = None):
     """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` (weights streamed once at
-    HBM rate; ``glu``: weight = [gate | up] and the result is silu(gate) * up); everything else is
-    ``F.linear`` (hipBLASLt on GPU)."""
-    if bf16_gemv_ok(x, weight, glu):
-        return ext().gemv_bf16(x, weight, bias, glu)
-    y = torch.nn.functional.linear(x, weight, bias)
+    HBM rate; ``glu``: weight = [gate | up] and the result is silu(gate) * up; ``act`` "gelu_tanh" /
+    "gelu": the activation of the bf16 output in the same kernel); everything else is
+    ``F.linear`` (hipBLASLt on GPU) followed by the activation op."""
     if glu:
-        g, u = y.chunk(2, dim=-1)
-        return torch.nn.functional.silu(g.float()).mul(u.float()).to(y.dtype)
-    return y
+        act = "silu_glu"
+    if bf16_gemv_ok(x, weight, glu):
+        return ext().gemv_bf16(x, weight, bias, _GEMV_EPI[act])
+    y = torch.nn.functional.linear(x, weight, bias)
+    return y if act is None else activation(y, act)
 
 
 def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,

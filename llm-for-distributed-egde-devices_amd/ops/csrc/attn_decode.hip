@@ -63,20 +63,20 @@ template <int D> struct Lanes { static constexpr int v = (D / 8 <= 8) ? 8 : ((D 
 
 // OCC > 0: single-buffered key loop, nontemporal K/V loads and at least OCC waves per SIMD
 // (occupancy instead of a second register buffer), and FUSED keeps the new key in registers (no
-// append barrier); OCC = 0: two register buffers, no occupancy target.
-template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC>
-__global__ void __launch_bounds__(NT, OCC > 0 ? OCC : 1) decode_attn_kernel(
+// append barrier); OCC = 0: two register buffers, no occupancy target.  NWV: waves per workgroup.
+template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC, int NWV = NW>
+__global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     int64_t c_sb, int64_t c_sh, const int* __restrict__ seq_lens, float scale_log2, int CH, int nsplit,
     bf16_t* __restrict__ out, int64_t o_sb, float* __restrict__ part_acc, float* __restrict__ part_ml, Fuse fz) {
   constexpr int LPK = Lanes<D>::v;        // lanes per key row
   constexpr int KPW = 64 / LPK;           // keys per wave-instruction
-  constexpr int KPB = KPW * NW;           // keys per workgroup step
+  constexpr int KPB = KPW * NWV;           // keys per workgroup step
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* red = smem;                      // [NW][G][D] per-wave rescaled accumulators
-  float* wm = red + NW * G * D;           // [NW][G] per-wave running max
-  float* wl = wm + NW * G;                // [NW][G] per-wave rescaled sums
-  float* mstat = wl + NW * G;             // [G]
+  float* red = smem;                      // [NWV][G][D] per-wave rescaled accumulators
+  float* wm = red + NWV * G * D;           // [NWV][G] per-wave running max
+  float* wl = wm + NWV * G;                // [NWV][G] per-wave rescaled sums
+  float* mstat = wl + NWV * G;             // [G]
   float* lstat = mstat + G;               // [G]
 
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(NT, OCC > 0 ? OCC : 1) decode_attn_kernel(
 
   if (n <= 0) {  // empty split (seq shorter than the grid's hint): publish an empty partial
     if (!DIRECT) {
-      for (int i = threadIdx.x; i < G * D; i += NT) {
+      for (int i = threadIdx.x; i < G * D; i += (NWV * 64)) {
         const int h = i / D, d = i - h * D;
         part_acc[(((size_t)b * Hq + kvh * G + h) * nsplit + split) * D + d] = 0.f;
       }
@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(NT, OCC > 0 ? OCC : 1) decode_attn_kernel(
       }
     } else {
       if (own) {
-        for (int c = threadIdx.x; c < 2 * (D / 8); c += NT) {
+        for (int c = threadIdx.x; c < 2 * (D / 8); c += (NWV * 64)) {
           const bool is_v = c >= D / 8;
           const int e0 = (is_v ? c - D / 8 : c) * 8;
           const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + kvh) * D;
@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(NT, OCC > 0 ? OCC : 1) decode_attn_kernel(
   for (int h = 0; h < G; ++h) {
     float M = wm[h];
 #pragma unroll
-    for (int w = 1; w < NW; ++w) M = fmaxf(M, wm[w * G + h]);
+    for (int w = 1; w < NWV; ++w) M = fmaxf(M, wm[w * G + h]);
     const float sc_w = m[h] == -INFINITY ? 0.f : exp2f(m[h] - M);   // wave without keys: 0
     if (kl == 0 && dvalid) {
 #pragma unroll
@@ -333,15 +333,15 @@ __global__ void __launch_bounds__(NT, OCC > 0 ? OCC : 1) decode_attn_kernel(
   if (threadIdx.x < G) {
     float L = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) L += wl[w * G + threadIdx.x];
+    for (int w = 0; w < NWV; ++w) L += wl[w * G + threadIdx.x];
     lstat[threadIdx.x] = L;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < G * D; i += NT) {
+  for (int i = threadIdx.x; i < G * D; i += (NWV * 64)) {
     const int h = i / D, d = i - h * D;
     float a = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) a += red[(w * G + h) * D + d];
+    for (int w = 0; w < NWV; ++w) a += red[(w * G + h) * D + d];
     const int hq = kvh * G + h;
     if (DIRECT) {
       if constexpr (QOUT) {     // D % 64 == 0: each 64-column group is one wave of this loop
@@ -407,25 +407,29 @@ void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q
                  int64_t o_sb, float* part_acc, float* part_ml, const Fuse& fz) {
 #define ATTN_ARGS grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, (bf16_t*)k_cache, (bf16_t*)v_cache, c_sb, c_sh, \
                   seq_lens, sl2, ch, nsplit, (bf16_t*)out, o_sb, part_acc, part_ml, fz
-  if constexpr (FU) {                           // the model's decode step: occupancy variant selectable
-    if (g_attn_occ == 4) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 4>), ATTN_ARGS); return; }
-    if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 5>), ATTN_ARGS); return; }
+  if constexpr (FU) {                           // the model's decode step: barrier-free form selectable
+    // occupancy target per GQA group size: the per-head q / accumulator registers grow with G, and
+    // a 4-waves-per-SIMD bound spills 250-900 B/lane at G >= 4 (ISA resource report)
+    constexpr int OCC4 = G <= 2 ? 4 : (G == 4 ? 2 : 1), OCC5 = G <= 2 ? 5 : OCC4;
+    if (g_attn_occ == 4) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4>), ATTN_ARGS); return; }
+    if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC5>), ATTN_ARGS); return; }
   }
   hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 0>), ATTN_ARGS);
 #undef ATTN_ARGS
 }
 }  // namespace
 
-extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out) {
+extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out) {
   const int target_wg = g_target_wg;
   int per = B * Hkv;
   int nsplit = (target_wg + per - 1) / per;
   int ch = (max_len + nsplit - 1) / nsplit;
   ch = ((ch + 63) / 64) * 64;
-  // at least 256 keys per split: below that the combine launch and the partial round trip cost
-  // more than the split saves (batch 1, Llama-3.2-1B, context <= 256: 15.7 + 4.8 us per layer with
-  // 4 splits of 64 keys)
-  if (ch < 256) ch = 256;
+  // at least 64 KiB of K+V per split (256 keys at D = 64, 128 at D = 128, 64 at D = 256): below
+  // that the combine launch and the partial round trip cost more than the split saves (batch 1,
+  // Llama-3.2-1B, context <= 256: 15.7 + 4.8 us per layer with 4 splits of 64 keys)
+  const int ch_min = D > 0 ? ((16384 / D + 63) / 64) * 64 : 64;
+  if (ch < ch_min) ch = ch_min;
   if (ch > 1024) ch = 1024;
   nsplit = (max_len + ch - 1) / ch;
   if (nsplit < 1) nsplit = 1;

@@ -24,7 +24,7 @@ int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, v
                        void* v_cache, int B, int T, int Hq, int Hkv, int D, int rot, int64_t c_sb, int64_t c_sh,
                        int S, void* k2, void* v2, int64_t c2_sb, int64_t c2_sh, int S2, int split_h,
                        const int* cpos2, hipStream_t st);
-int edge_decode_attn_plan(int B, int Hkv, int max_len, int* ch_out, int* nsplit_out);
+int edge_decode_attn_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out);
 int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb, int64_t c_sh,
                      const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch, int nsplit, void* out,
                      int64_t o_sb, float* part_acc, float* part_ml, const int* pos, const float* cs, int rot,
@@ -251,7 +251,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   const int64_t Hkv = k_cache.size(1);
   TORCH_CHECK(max_len_hint > 0 && max_len_hint <= k_cache.size(2), "max_len_hint out of range");
   int ch = 0, nsplit = 0;
-  edge_decode_attn_plan((int)B, (int)Hkv, (int)max_len_hint, &ch, &nsplit);
+  edge_decode_attn_plan((int)B, (int)Hkv, (int)max_len_hint, (int)D, &ch, &nsplit);
   auto out = at::empty({B, Hq, D}, q.options());
   at::Tensor pacc, pml;
   if (nsplit > 1) {
@@ -293,7 +293,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_fused(
     cs = rope->data_ptr<float>();
   }
   int ch = 0, nsplit = 0;
-  edge_decode_attn_plan((int)B, (int)Hkv, (int)max_len_hint, &ch, &nsplit);
+  edge_decode_attn_plan((int)B, (int)Hkv, (int)max_len_hint, (int)D, &ch, &nsplit);
   at::Tensor pacc, pml, out, oq;
   std::optional<at::Tensor> os;
   if (nsplit > 1) {
@@ -404,7 +404,9 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
 
 // bf16 decode GEMV (M <= 16, K % 64 == 0, N % 16 == 0): x [.., K] . w[N, K]^T (+ bias) -> bf16.
 // glu: w = [gate | up] (N = 2F) and the result is silu(gate) * up [.., F].
-at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& w, const std::optional<at::Tensor>& bias, bool glu) {
+// epi: 0 plain, 1 SwiGLU over [gate | up], 2 gelu-tanh, 3 gelu (erf).
+at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& w, const std::optional<at::Tensor>& bias, int64_t epi) {
+  const bool glu = epi == 1;
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "weight");
   TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(-1), "weight must be [N, K] with K = x.size(-1)");
@@ -414,7 +416,7 @@ at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& w, const std::option
   os.back() = glu ? N / 2 : N;
   auto out = at::empty(os, x.options());
   check(edge_gemv_bf16(x.data_ptr(), w.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N,
-                       (int)K, glu ? 1 : 0, stream()),
+                       (int)K, (int)epi, stream()),
         "gemv_bf16");
   return out;
 }

@@ -14,10 +14,12 @@
 //            tiles are NTW/2 gate tiles and the matching up tiles, and it writes
 //            h = silu(gate) * up as bf16 [M, F] (gate and up rounded to bf16 first, as the
 //            unfused GEMM output is) — the separate SwiGLU launch disappears.
+//   EPI_GELU_TANH / EPI_GELU: gelu(bf16(y + bias)) -> bf16 [M, N] (Phi-2 / Pythia MLP up
+//            projection; the same math as rowwise.hip::act_kernel modes 1 / 2).
 #include "common.h"
 
 namespace {
-constexpr int EPI_OUT = 0, EPI_GLU = 1;
+constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GELU_TANH = 2, EPI_GELU = 3;
 constexpr int NW = 16;
 
 __device__ __forceinline__ v4f mfma_bf16(const v8s& a, const v8s& b, const v4f& c) {
@@ -32,7 +34,7 @@ template <int NTW, int U, int EPI>
 __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                             int M, int N, int K, int F) {
-  static_assert(EPI == EPI_OUT || NTW % 2 == 0, "GLU: gate/up tile pairs");
+  static_assert(EPI != EPI_GLU || NTW % 2 == 0, "GLU: gate/up tile pairs");
   __shared__ v4f red[NW][NTW][64];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = 8 * (lane >> 4);
@@ -105,7 +107,15 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 4 * (lane >> 4) + q;
-        if (row < M && c0 < N) out[(size_t)row * N + c0] = f2bf(s4[q] + bv);
+        float v = s4[q] + bv;
+        if constexpr (EPI == EPI_GELU_TANH) {
+          const float a = bf2f(f2bf(v)), k0 = 0.7978845608028654f, k1 = 0.044715f;
+          v = 0.5f * a * (1.f + tanhf(k0 * (a + k1 * a * a * a)));
+        } else if constexpr (EPI == EPI_GELU) {
+          const float a = bf2f(f2bf(v));
+          v = 0.5f * a * (1.f + erff(a * 0.7071067811865476f));
+        }
+        if (row < M && c0 < N) out[(size_t)row * N + c0] = f2bf(v);
       }
     }
   }
@@ -122,7 +132,8 @@ int launch(const void* A, const void* W, const void* bias, void* out, int M, int
 }  // namespace
 
 // epi 0: out bf16 [M, N]; epi 1 (GLU): W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F]
-// (F % 16 == 0).  M <= 16, K % 64 == 0, N % 16 == 0.  Returns -2 for shapes it does not take.
+// (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 16, K % 64 == 0,
+// N % 16 == 0.  Returns -2 for shapes it does not take.
 extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                               hipStream_t st) {
   if (M <= 0 || M > 16 || K % 64 != 0 || N % 16 != 0 || K <= 0) return -2;
@@ -135,11 +146,17 @@ extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, vo
     return U == 4 ? launch<2, 4, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st)
                   : launch<2, 2, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st);
   }
+  if (epi != EPI_OUT && epi != EPI_GELU_TANH && epi != EPI_GELU) return -2;
   const int nt = N / 16;
   // ~256 workgroups: one tile each below 512 tiles, then 2 or 4
-  if (nt >= 1024) return launch<4, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st);
-  if (nt >= 512) return U == 4 ? launch<2, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st)
-                               : launch<2, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st);
-  return U == 4 ? launch<1, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st)
-                : launch<1, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st);
+#define PICK(EP)                                                                               \
+  if (nt >= 1024) return launch<4, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);                \
+  if (nt >= 512) return U == 4 ? launch<2, 4, EP>(A, W, bias, out, M, N, K, 0, nt, st)         \
+                               : launch<2, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);        \
+  return U == 4 ? launch<1, 4, EP>(A, W, bias, out, M, N, K, 0, nt, st)                        \
+                : launch<1, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);
+  if (epi == EPI_GELU_TANH) { PICK(EPI_GELU_TANH) }
+  if (epi == EPI_GELU) { PICK(EPI_GELU) }
+  PICK(EPI_OUT)
+#undef PICK
 }

@@ -125,7 +125,8 @@ class W8A8Linear(nn.Module):
         if self.split_k_out and x.q.is_cuda and ops.gpu_path(x.q) and K % 64 == 0 and 0 < M and \
                 ops.decode_rows_ok(M, K, 4 if M > 64 else 1):
             return PartialSum(ops.w8a8_linear_splitk(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale,
-                                                     self.bias, N, K, self.split_k_out if self.split_k_out > 1 else 0))
+                                                     self.bias, N, K,
+                                                     self.split_k_out if self.split_k_out > 1 and M <= 64 else 0))
         out = ops.w8a8_linear(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale, self.bias,
                               N, K, w_ref=self._wref(x.q), out_dtype=self.out_dtype)
         return out.view(*shp, N)

@@ -339,11 +339,11 @@ def test_gemv_bf16(cuda, M, N, K, bias):
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
     b = torch.randn(N, device=cuda).bfloat16() if bias else None
-    y = C.gemv_bf16(x, w, b, False)
+    y = C.gemv_bf16(x, w, b, 0)
     ref = x.float() @ w.float().t() + (b.float() if bias else 0)
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
     _close(y, ref, 2e-2, 1e-2)
-    assert torch.equal(y, C.gemv_bf16(x, w, b, False))
+    assert torch.equal(y, C.gemv_bf16(x, w, b, 0))
 
 
 @pytest.mark.parametrize("M", [1, 7, 16])
@@ -355,7 +355,7 @@ def test_gemv_bf16_glu(cuda, M, F, K):
     torch.manual_seed(F + M)
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(2 * F, K, device=cuda) * 0.05).bfloat16()
-    h = C.gemv_bf16(x, w, None, True)
+    h = C.gemv_bf16(x, w, None, 1)
     gu = (x.float() @ w.float().t()).bfloat16().float()
     g, u = gu[:, :F], gu[:, F:]
     ref = torch.nn.functional.silu(g) * u
@@ -372,3 +372,16 @@ def test_linear_bf16_routes_decode_rows(cuda):
     small = ops.linear_bf16(x, w)
     big = ops.linear_bf16(torch.cat([x, x]), w)[:16]
     _close(small, big, 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "gelu"])
+@pytest.mark.parametrize("M,N,K", [(1, 10240, 2560), (16, 8192, 2048)])
+def test_gemv_bf16_gelu(cuda, act, M, N, K):
+    """bf16 GEMV with the GELU epilogue == hipBLASLt GEMM -> act_kernel (Phi-2 / Pythia up-proj)."""
+    torch.manual_seed(N + M)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    fused = ops.linear_bf16(x, w, b, act=act)
+    ref = ops.activation(torch.nn.functional.linear(x, w, b), act)
+    _close(fused, ref, 2e-2, 2e-2)
