@@ -209,12 +209,18 @@ class Generator:
             torch.cuda.synchronize()
         self._run = dict(B=B, plens=plens, sampling=sampling, t0=t0, t_prefill=time.perf_counter() - t0,
                          produced=1, host_max=max(plens), events=[], cuda=cuda,
-                         graphs_ok=self.use_graphs and cuda and self.graph_safe and not needs_host_sampler(sampling, V))
+                         graphs_ok=self.use_graphs and cuda and self.graph_safe_for(B)
+                         and not needs_host_sampler(sampling, V))
 
     @property
     def graph_safe(self) -> bool:
         return getattr(self.kv, "graph_safe", True) and \
             all(getattr(m, "graph_safe", True) for m in self.model.modules())
+
+    def graph_safe_for(self, B: int) -> bool:
+        """graph_safe, counting modules that are capturable up to a batch size (``graph_safe_rows``)."""
+        return getattr(self.kv, "graph_safe", True) and \
+            all(getattr(m, "graph_safe", True) or getattr(m, "graph_safe_rows", 0) >= B for m in self.model.modules())
 
     @torch.no_grad()
     def step(self, n: int = 1, record_latency: bool = True) -> int:

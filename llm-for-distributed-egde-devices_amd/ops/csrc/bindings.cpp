@@ -45,6 +45,10 @@ void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st);
+int edge_llmint8_prep(const void* x, int M, int K, float thr, int cmax, void* q, float* sa, int* cols, float* xo,
+                      int* count, hipStream_t st);
+int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int* count, const void* wt,
+                         const float* scb, int M, int N, int cmax, hipStream_t st);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_decode_attn_config(int target_wg);
 void edge_decode_attn_occ(int occ);
@@ -421,6 +425,40 @@ at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& w, const std::option
   return out;
 }
 
+// LLM.int8 decode preparation (M <= 16): (q int8 [M, K] with the outlier columns zeroed, per-token
+// scales [M], outlier columns [cmax] (first `count`), outlier values [M, cmax], count [1]).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> llmint8_prep(const at::Tensor& x, double thr,
+                                                                                    int64_t cmax) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 2, "x must be [M, K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  auto q = at::empty({M, K}, x.options().dtype(at::kChar));
+  auto sa = at::empty({M}, x.options().dtype(at::kFloat));
+  auto cols = at::zeros({cmax}, x.options().dtype(at::kInt));
+  auto xo = at::zeros({M, cmax}, x.options().dtype(at::kFloat));
+  auto count = at::empty({1}, x.options().dtype(at::kInt));
+  check(edge_llmint8_prep(x.data_ptr(), (int)M, (int)K, (float)thr, (int)cmax, q.data_ptr(), sa.data_ptr<float>(),
+                          cols.data_ptr<int>(), xo.data_ptr<float>(), count.data_ptr<int>(), stream()),
+        "llmint8_prep");
+  return {q, sa, cols, xo, count};
+}
+
+// out bf16 [M, N] += xo[:, :count] . W^T[cols[:count]] * SCB / 127 (wt = int8 W^T [K, N]), in place.
+void llmint8_outlier(at::Tensor& out, const at::Tensor& xo, const at::Tensor& cols, const at::Tensor& count,
+                     const at::Tensor& wt, const at::Tensor& scb) {
+  need(out, at::kBFloat16, "out");
+  need(xo, at::kFloat, "xo");
+  need(cols, at::kInt, "cols");
+  need(count, at::kInt, "count");
+  need(wt, at::kChar, "weight_t");
+  need(scb, at::kFloat, "SCB");
+  const int64_t M = out.size(0), N = out.size(1);
+  TORCH_CHECK(out.dim() == 2 && wt.dim() == 2 && wt.size(1) == N && xo.size(0) == M && xo.size(1) == cols.numel());
+  check(edge_llmint8_outlier(out.data_ptr(), xo.data_ptr<float>(), cols.data_ptr<int>(), count.data_ptr<int>(),
+                             wt.data_ptr(), scb.data_ptr<float>(), (int)M, (int)N, (int)cols.numel(), stream()),
+        "llmint8_outlier");
+}
+
 // Per-(token, 64 columns) int8 quantisation: (q [M, K], scales [K/64, Mpad]).
 std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
   need(x, at::kBFloat16, "x");
@@ -531,6 +569,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_attn", &decode_attn);
   m.def("prefill_attn", &prefill_attn);
   m.def("w8a8_gemm", &w8a8_gemm);
+  m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
+  m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
   m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]");
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);

@@ -186,7 +186,8 @@ class PipelineStage:
         V = self.cfg.vocab_size
         self.sampling = sampling
         self.graphs_ok = self.use_graphs and not needs_host_sampler(sampling, V) and \
-            getattr(self.kv, "graph_safe", True) and all(getattr(mm, "graph_safe", True) for mm in self.model.modules())
+            getattr(self.kv, "graph_safe", True) and \
+            all(getattr(mm, "graph_safe", True) or getattr(mm, "graph_safe_rows", 0) >= b for mm in self.model.modules())
         self._warm: Dict[int, bool] = {}
         self._graphs.clear()
         self._pools.clear()

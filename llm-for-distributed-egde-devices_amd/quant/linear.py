@@ -157,7 +157,14 @@ class W8A8Linear(nn.Module):
 
 class LLMInt8Linear(nn.Module):
     takes_quantized_input = False
-    graph_safe = False   # outlier-column discovery is data dependent (host sync), like bnb
+    graph_safe = False   # outlier-column discovery is data dependent (host sync), like bnb ...
+    OUTLIER_CAP = 256    # ... except decode rows on GPU: ops/csrc/llmint8.hip finds them on the device
+
+    @property
+    def graph_safe_rows(self) -> int:
+        """Batch sizes up to which forward() runs without a host sync (graph-capturable)."""
+        K = self.in_features
+        return 16 if (ops.available() and self.w_packed.is_cuda and K % 8 == 0 and K <= 32768) else 0
 
     def __init__(self, in_features: int, out_features: int, bias: bool, threshold: float = 6.0, device=None,
                  dtype=torch.bfloat16):
@@ -168,6 +175,7 @@ class LLMInt8Linear(nn.Module):
         self.register_buffer("w_packed", torch.zeros(nt * kt * 1024, dtype=torch.int8, device=device))
         self.register_buffer("SCB", torch.ones(out_features, dtype=torch.float32, device=device))
         self.register_buffer("bias", torch.zeros(out_features, dtype=dtype, device=device) if bias else None)
+        self._weight_t = None          # int8 W^T for the device-side outlier path (built on first use)
 
     @classmethod
     @torch.no_grad()
@@ -181,7 +189,12 @@ class LLMInt8Linear(nn.Module):
         return m
 
     @torch.no_grad()
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._weight_t = None          # derived device copies follow the loaded weights
+        super()._load_from_state_dict(*args, **kwargs)
+
     def load_int8(self, q, scb, bias=None):
+        self._weight_t = None
         self.weight_i8.copy_(q)
         self.w_packed.copy_(ops.pack_int8_weight(q))
         self.SCB.copy_(scb.float())
@@ -194,6 +207,16 @@ class LLMInt8Linear(nn.Module):
         K, N = self.in_features, self.out_features
         shp = x.shape[:-1]
         x2 = x.reshape(-1, K)
+        if x2.is_cuda and ops.gpu_path(x2) and x2.shape[0] <= self.graph_safe_rows and x2.dtype == torch.bfloat16:
+            # decode: outlier columns found on the device (llmint8.hip), no host sync
+            C = ops.ext()
+            if self._weight_t is None or self._weight_t.device != x2.device:
+                self._weight_t = self.weight_i8.t().contiguous()          # W^T: outlier columns as rows
+                self._w_deq = self.SCB / 127.0
+            q, sa, cols, xo, count = C.llmint8_prep(x2.contiguous(), self.threshold, self.OUTLIER_CAP)
+            out = ops.w8a8_linear(q, sa, self.w_packed, self._w_deq, self.bias, N, K)
+            C.llmint8_outlier(out, xo, cols, count, self._weight_t, self.SCB)
+            return out.view(*shp, N)
         cols = (x2.abs() > self.threshold).any(0).nonzero().flatten()
         w_scale = self.SCB / 127.0
         if cols.numel() > 0:

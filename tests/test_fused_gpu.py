@@ -385,3 +385,35 @@ def test_gemv_bf16_gelu(cuda, act, M, N, K):
     fused = ops.linear_bf16(x, w, b, act=act)
     ref = ops.activation(torch.nn.functional.linear(x, w, b), act)
     _close(fused, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("K,N", [(2048, 3072), (2560, 10240), (8192, 2048)])
+@pytest.mark.parametrize("outliers", [0, 3, 300])
+def test_llmint8_device_outliers(cuda, M, K, N, outliers):
+    """LLM.int8 decode without a host sync (llmint8.hip) == the host-side outlier path: the same
+    columns go to the 16-bit part (300 > the 256-column cap: the overflow stays int8, so only the
+    first 256 columns may differ from bitsandbytes' split)."""
+    from edgellm.models.layers import Linear
+    from edgellm.quant import LLMInt8Linear
+    torch.manual_seed(M + K + outliers)
+    lin = Linear(K, N, bias=True, device=cuda)
+    lin.weight.data.copy_(torch.randn(N, K, device=cuda) * 0.02)
+    lin.bias.data.copy_(torch.randn(N, device=cuda) * 0.1)
+    m = LLMInt8Linear.from_float(lin)
+    x = torch.randn(M, K, device=cuda)
+    if outliers:
+        cols = torch.randperm(K, device=cuda)[:outliers]
+        x[0, cols] = 8.0 + torch.rand(outliers, device=cuda) * 4
+    x = x.bfloat16()
+    fast = m(x)                                         # device path (M <= 16)
+    m_slow = LLMInt8Linear.from_float(lin)
+    m_slow.OUTLIER_CAP = 10 ** 9
+    x_slow = x.float()
+    # host path: the same math with data-dependent indexing (force it with a 17th row of zeros)
+    slow = m_slow(torch.cat([x, torch.zeros(17 - M, K, device=cuda, dtype=x.dtype)]))[:M]
+    if outliers <= LLMInt8Linear.OUTLIER_CAP:
+        _close(fast, slow, 3e-2, 2e-2)
+    ref = x_slow @ lin.weight.float().t() + lin.bias.float()
+    rel = (fast.float() - ref).norm() / ref.norm()
+    assert rel < 2e-2, rel
