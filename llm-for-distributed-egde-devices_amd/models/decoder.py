@@ -110,11 +110,13 @@ class MLP(nn.Module):
         if self.act == "silu_glu" and type(self.up) is Linear and not down_q and not isinstance(x, QAct) \
                 and ops.bf16_gemv_ok(x, self.up.weight, glu=True):
             # bf16 decode: gate_up GEMV with the SwiGLU epilogue (one launch, gemv_bf16.hip)
-            return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, glu=True))
+            return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, glu=True,
+                                             packed=self.up.decode_weight(x)))
         if self.act in ("gelu_tanh", "gelu") and type(self.up) is Linear and not down_q \
                 and not isinstance(x, QAct) and ops.bf16_gemv_ok(x, self.up.weight):
             # bf16 decode (Phi-2, Pythia): up-projection GEMV with the GELU epilogue
-            return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, act=self.act))
+            return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, act=self.act,
+                                             packed=self.up.decode_weight(x)))
         h = self.up(x)
         h = act_fn(h, self.act, down_q)
         return self.down(h)

@@ -58,7 +58,18 @@ class Linear(nn.Module):
     def forward(self, x):
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
-        return ops.linear_bf16(x, self.weight, self.bias)     # decode rows: HIP GEMV; else hipBLASLt
+        return ops.linear_bf16(x, self.weight, self.bias, packed=self.decode_weight(x))
+
+    def decode_weight(self, x) -> "Optional[torch.Tensor]":
+        """Fragment-packed copy of the weight for the decode GEMV (``gemv_bf16.hip``), built on the
+        first decode-sized call (before any graph capture) and kept; None when not applicable."""
+        if not ops.bf16_gemv_ok(x, self.weight):
+            return None
+        wp, ver = getattr(self, "_wp", None), self.weight._version   # in-place weight edits repack
+        if wp is None or getattr(self, "_wp_ver", -1) != ver or wp.device != self.weight.device:
+            wp = self._wp = ops.pack_bf16_weight(self.weight.detach())
+            self._wp_ver = ver
+        return wp
 
     def extra_repr(self):
         return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, bf16"

@@ -221,18 +221,28 @@ def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bo
             and 0 < x.numel() // max(K, 1) <= 16 and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0)
 
 
+def pack_bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] bf16 -> MFMA-fragment order for ``gemv_bf16.hip``: 1 KiB tiles of 16 rows x 32 k,
+    lane l holding W[16 nt + (l & 15)][32 kt + 8 (l >> 4) .. +8] (N % 16 == 0, K % 32 == 0)."""
+    N, K = w.shape
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(-1)
+
+
 _GEMV_EPI = {None: 0, "silu_glu": 1, "gelu_tanh": 2, "gelu": 3}
 
 
-def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = None):
-    """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` (weights streamed once at
-    HBM rate; ``glu``: weight = [gate | up] and the result is silu(gate) * up; ``act`` "gelu_tanh" /
-    "gelu": the activation of the bf16 output in the same kernel); everything else is
-    ``F.linear`` (hipBLASLt on GPU) followed by the activation op."""
+def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = None,
+                packed: Optional[torch.Tensor] = None):
+    """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` on the fragment-packed
+    weight (``packed``: the layer's cached ``pack_bf16_weight(weight)``; packed per call when
+    absent); ``glu``: weight = [gate | up] and the result is silu(gate) * up; ``act``
+    "gelu_tanh" / "gelu": the activation of the bf16 output in the same kernel.  Everything else
+    is ``F.linear`` (hipBLASLt on GPU) followed by the activation op."""
     if glu:
         act = "silu_glu"
     if bf16_gemv_ok(x, weight, glu):
-        return ext().gemv_bf16(x, weight, bias, _GEMV_EPI[act])
+        wp = packed if packed is not None else pack_bf16_weight(weight)
+        return ext().gemv_bf16(x, wp, bias, weight.shape[0], _GEMV_EPI[act])
     y = torch.nn.functional.linear(x, weight, bias)
     return y if act is None else activation(y, act)
 

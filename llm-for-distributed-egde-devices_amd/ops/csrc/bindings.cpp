@@ -406,20 +406,20 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
   return part;
 }
 
-// bf16 decode GEMV (M <= 16, K % 64 == 0, N % 16 == 0): x [.., K] . w[N, K]^T (+ bias) -> bf16.
-// glu: w = [gate | up] (N = 2F) and the result is silu(gate) * up [.., F].
-// epi: 0 plain, 1 SwiGLU over [gate | up], 2 gelu-tanh, 3 gelu (erf).
-at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& w, const std::optional<at::Tensor>& bias, int64_t epi) {
-  const bool glu = epi == 1;
+// bf16 decode GEMV (M <= 16, K % 64 == 0, N % 16 == 0): x [.., K] . W[N, K]^T (+ bias) -> bf16, with
+// W fragment-packed (ops.pack_bf16_weight).  epi: 0 plain, 1 SwiGLU over [gate | up] (result
+// [.., N/2]), 2 gelu-tanh, 3 gelu (erf).
+at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
+                     int64_t epi) {
   need(x, at::kBFloat16, "x");
-  need(w, at::kBFloat16, "weight");
-  TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(-1), "weight must be [N, K] with K = x.size(-1)");
-  const int64_t K = x.size(-1), M = rows_of(x), N = w.size(0);
+  need(wp, at::kBFloat16, "weight (packed)");
+  const int64_t K = x.size(-1), M = rows_of(x);
+  TORCH_CHECK(wp.numel() == N * K, "packed weight must hold N * K elements");
   if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
   auto os = x.sizes().vec();
-  os.back() = glu ? N / 2 : N;
+  os.back() = epi == 1 ? N / 2 : N;
   auto out = at::empty(os, x.options());
-  check(edge_gemv_bf16(x.data_ptr(), w.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N,
+  check(edge_gemv_bf16(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N,
                        (int)K, (int)epi, stream()),
         "gemv_bf16");
   return out;

@@ -2,11 +2,13 @@
 // The fp16/bf16 evaluators (Phi-2, Pythia-1B, Llama-3.2-1B at batch 1) spend
 // most of a decode step here; hipBLASLt's small-M kernels stream the weights at about 2 TB/s.
 //
-// Weights stay in the Hugging Face [N, K] layout (the prefill GEMMs read the same tensor).  One
-// MFMA (v_mfma_f32_16x16x32_bf16) takes a 16-row x 32-k B fragment: lane l loads the 16 bytes
-// W[n0 + (l & 15)][k0 + 8 (l >> 4) ..].  A wave walks K in pairs of k-steps (64 elements), so
-// every weight row contributes one whole 128-byte line per pair.  A workgroup = 16 waves on NTW
-// 16-column tiles; wave w takes k-pairs w, w + 16, ..., keeping U pairs of weight loads in
+// Weights are read in MFMA fragment order (ops.pack_bf16_weight, a decode-only copy of the HF
+// [N, K] tensor that prefill keeps using): 1 KiB tiles of 16 rows x 32 k, tile (nt, kt) at
+// ((nt * K/32) + kt) * 512 elements, lane l's 8 elements = W[16 nt + (l & 15)][32 kt + 8 (l >> 4) ..]
+// — the B fragment of v_mfma_f32_16x16x32_bf16.  A wave walks K in pairs of k-steps, i.e. 2 KiB
+// of contiguous weights per tile per pair (the [N, K] layout gave each load instruction 16 rows x
+// 64 B: 36 % more bytes fetched and 2.3 TB/s on Llama-3.2-1B's gate_up).  A workgroup = 16 waves
+// on NTW 16-column tiles; wave w takes k-pairs w, w + 16, ..., keeping U pairs of weight loads in
 // flight (nontemporal: each weight byte is read once per step).  The 16 partial tiles are
 // reduced through LDS.  Rows >= M load a clamped row and are never stored.
 //   EPI_OUT: + bias, bf16 [M, N].
@@ -47,11 +49,11 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
       return (blockIdx.x * NTW + j) * 16 + r;
     }
   };
-  const bf16_t* wrow[NTW];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) wrow[j] = W + (size_t)min(col_of(j), N - 1) * K + kq;
-  const bf16_t* arow = A + (size_t)min(r, M - 1) * K + kq;
   const int KP = K / 64;
+  const bf16_t* wrow[NTW];                                  // tile row of this lane's fragments
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) wrow[j] = W + ((size_t)(min(col_of(j), N - 1) >> 4) * (2 * KP) * 64 + lane) * 8;
+  const bf16_t* arow = A + (size_t)min(r, M - 1) * K + kq;
   v4f acc[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -61,9 +63,9 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
     for (int u = 0; u < U; ++u) {
       const int k = min(kp + u * NW, KP - 1) * 64;          // clamped: loads never branch
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        b[u][j][0] = ld_nt(wrow[j] + k);
-        b[u][j][1] = ld_nt(wrow[j] + k + 32);
+      for (int j = 0; j < NTW; ++j) {                        // tiles 2 kp, 2 kp + 1: 2 KiB contiguous
+        b[u][j][0] = ld_nt(wrow[j] + (size_t)k * 16);
+        b[u][j][1] = ld_nt(wrow[j] + (size_t)k * 16 + 512);
       }
       a[u][0] = *reinterpret_cast<const v8s*>(arow + k);
       a[u][1] = *reinterpret_cast<const v8s*>(arow + k + 32);
@@ -131,7 +133,7 @@ int launch(const void* A, const void* W, const void* bias, void* out, int M, int
 }
 }  // namespace
 
-// epi 0: out bf16 [M, N]; epi 1 (GLU): W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F]
+// W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N]; epi 1 (GLU): W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F]
 // (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 16, K % 64 == 0,
 // N % 16 == 0.  Returns -2 for shapes it does not take.
 extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,

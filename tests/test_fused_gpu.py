@@ -339,11 +339,11 @@ def test_gemv_bf16(cuda, M, N, K, bias):
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
     b = torch.randn(N, device=cuda).bfloat16() if bias else None
-    y = C.gemv_bf16(x, w, b, 0)
+    y = C.gemv_bf16(x, ops.pack_bf16_weight(w), b, N, 0)
     ref = x.float() @ w.float().t() + (b.float() if bias else 0)
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
     _close(y, ref, 2e-2, 1e-2)
-    assert torch.equal(y, C.gemv_bf16(x, w, b, 0))
+    assert torch.equal(y, C.gemv_bf16(x, ops.pack_bf16_weight(w), b, N, 0))
 
 
 @pytest.mark.parametrize("M", [1, 7, 16])
@@ -355,7 +355,7 @@ def test_gemv_bf16_glu(cuda, M, F, K):
     torch.manual_seed(F + M)
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(2 * F, K, device=cuda) * 0.05).bfloat16()
-    h = C.gemv_bf16(x, w, None, 1)
+    h = C.gemv_bf16(x, ops.pack_bf16_weight(w), None, 2 * F, 1)
     gu = (x.float() @ w.float().t()).bfloat16().float()
     g, u = gu[:, :F], gu[:, F:]
     ref = torch.nn.functional.silu(g) * u
