@@ -19,6 +19,7 @@ the head if last == num_layers; it exchanges a single bf16 hidden tensor with it
 from __future__ import annotations
 
 import math
+import os
 import zlib
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -29,6 +30,10 @@ import torch.nn as nn
 from .. import ops
 from .configs import ModelConfig
 from .layers import Linear, Norm, PartialSum, QAct, act_fn, quant_if
+
+# split-K slices of the bf16 o / down decode GEMVs (0 = off); N = 2048-4096 outputs have only
+# 128-256 tiles, so two slices put every CU to work
+BF16_SPLIT_K = int(os.environ.get("EDGELLM_BF16_SPLITK", "2"))
 
 
 @dataclass
@@ -130,6 +135,10 @@ class DecoderLayer(nn.Module):
         self.norm2 = (None if cfg.shared_input_norm else Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device))
         self.attn = Attention(cfg, idx, dtype, device)
         self.mlp = MLP(cfg, dtype, device)
+        if cfg.norm == "rms" and not cfg.parallel_residual:
+            # o and down feed an RMSNorm (or the stage exit): bf16 decode GEMVs split K and the norm
+            # kernel sums the fp32 slices (quantised replacements set their own split)
+            self.attn.o.split_k_out = self.mlp.down.split_k_out = BF16_SPLIT_K
 
     def forward(self, x, residual, ctx: AttnCtx):
         cfg = self.cfg

@@ -45,6 +45,7 @@ class GroupQuantBF16(NamedTuple):
 
 class Linear(nn.Module):
     takes_quantized_input = False
+    split_k_out = 0     # > 0: decode calls return split-K fp32 partials (PartialSum) for the next norm
 
     def __init__(self, in_features: int, out_features: int, bias: bool = False, dtype=torch.bfloat16,
                  device=None):
@@ -58,7 +59,11 @@ class Linear(nn.Module):
     def forward(self, x):
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
-        return ops.linear_bf16(x, self.weight, self.bias, packed=self.decode_weight(x))
+        wp = self.decode_weight(x)
+        if self.split_k_out and wp is not None and x.shape[-1] // 64 >= self.split_k_out:
+            return PartialSum(ops.ext().gemv_bf16_splitk(x.reshape(-1, x.shape[-1]), wp, self.bias,
+                                                         self.out_features, self.split_k_out))
+        return ops.linear_bf16(x, self.weight, self.bias, packed=wp)
 
     def decode_weight(self, x) -> "Optional[torch.Tensor]":
         """Fragment-packed copy of the weight for the decode GEMV (``gemv_bf16.hip``), built on the

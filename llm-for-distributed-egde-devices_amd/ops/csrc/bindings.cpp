@@ -45,6 +45,8 @@ void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st);
+int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
+                          hipStream_t st);
 int edge_llmint8_prep(const void* x, int M, int K, float thr, int cmax, void* q, float* sa, int* cols, float* xo,
                       int* count, hipStream_t st);
 int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int* count, const void* wt,
@@ -425,6 +427,21 @@ at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optio
   return out;
 }
 
+// Split-K bf16 decode GEMV: fp32 partial slices [S, M, N] (bias in slice 0) for rms_norm_parts.
+at::Tensor gemv_bf16_splitk(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias,
+                            int64_t N, int64_t S) {
+  need(x, at::kBFloat16, "x");
+  need(wp, at::kBFloat16, "weight (packed)");
+  const int64_t K = x.size(-1), M = rows_of(x);
+  TORCH_CHECK(wp.numel() == N * K, "packed weight must hold N * K elements");
+  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+  auto part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  check(edge_gemv_bf16_splitk(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, part.data_ptr<float>(),
+                              (int)M, (int)N, (int)K, (int)S, stream()),
+        "gemv_bf16_splitk");
+  return part;
+}
+
 // LLM.int8 decode preparation (M <= 16): (q int8 [M, K] with the outlier columns zeroed, per-token
 // scales [M], outlier columns [cmax] (first `count`), outlier values [M, cmax], count [1]).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> llmint8_prep(const at::Tensor& x, double thr,
@@ -571,6 +588,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm", &w8a8_gemm);
   m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
+  m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");
   m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]");
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);

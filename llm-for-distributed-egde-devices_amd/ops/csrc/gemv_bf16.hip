@@ -18,10 +18,13 @@
 //            unfused GEMM output is) — the separate SwiGLU launch disappears.
 //   EPI_GELU_TANH / EPI_GELU: gelu(bf16(y + bias)) -> bf16 [M, N] (Phi-2 / Pythia MLP up
 //            projection; the same math as rowwise.hip::act_kernel modes 1 / 2).
+//   EPI_PART: split-K, workgroup (group, ks) reduces k-pairs [KP ks / S, KP (ks + 1) / S) and
+//            writes fp32 partials part[ks][M][N] (bias in slice 0) for a norm kernel that sums
+//            them (the o / down projections of RMSNorm decoders; N = 2048 has only 128 tiles).
 #include "common.h"
 
 namespace {
-constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GELU_TANH = 2, EPI_GELU = 3;
+constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GELU_TANH = 2, EPI_GELU = 3, EPI_PART = 4;
 constexpr int NW = 16;
 
 __device__ __forceinline__ v4f mfma_bf16(const v8s& a, const v8s& b, const v4f& c) {
@@ -35,21 +38,24 @@ __device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
 template <int NTW, int U, int EPI>
 __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                            int M, int N, int K, int F) {
+                                                            int M, int N, int K, int F, int S) {
   static_assert(EPI != EPI_GLU || NTW % 2 == 0, "GLU: gate/up tile pairs");
   __shared__ v4f red[NW][NTW][64];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = 8 * (lane >> 4);
   // output column of tile j for this lane (EPI_GLU: gate tiles then the matching up tiles)
+  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
+  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
   auto col_of = [&](int j) -> int {
     if constexpr (EPI == EPI_GLU) {
-      const int f0 = blockIdx.x * (NTW / 2) * 16;
+      const int f0 = grp * (NTW / 2) * 16;
       return j < NTW / 2 ? f0 + j * 16 + r : F + f0 + (j - NTW / 2) * 16 + r;
     } else {
-      return (blockIdx.x * NTW + j) * 16 + r;
+      return (grp * NTW + j) * 16 + r;
     }
   };
   const int KP = K / 64;
+  const int kbeg = EPI == EPI_PART ? KP * ks / S : 0, kend = EPI == EPI_PART ? KP * (ks + 1) / S : KP;
   const bf16_t* wrow[NTW];                                  // tile row of this lane's fragments
 #pragma unroll
   for (int j = 0; j < NTW; ++j) wrow[j] = W + ((size_t)(min(col_of(j), N - 1) >> 4) * (2 * KP) * 64 + lane) * 8;
@@ -57,11 +63,11 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   v4f acc[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
-  for (int kp = wave; kp < KP; kp += NW * U) {
+  for (int kp = kbeg + wave; kp < kend; kp += NW * U) {
     v8s a[U][2], b[U][NTW][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = min(kp + u * NW, KP - 1) * 64;          // clamped: loads never branch
+      const int k = min(kp + u * NW, kend - 1) * 64;        // clamped: loads never branch
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {                        // tiles 2 kp, 2 kp + 1: 2 KiB contiguous
         b[u][j][0] = ld_nt(wrow[j] + (size_t)k * 16);
@@ -72,7 +78,7 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (kp + u * NW < KP) {                               // wave-uniform (scalar) guard
+      if (kp + u * NW < kend) {                             // wave-uniform (scalar) guard
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
           acc[j] = mfma_bf16(a[u][0], b[u][j][0], acc[j]);
@@ -103,6 +109,15 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
         const float g = bf2f(f2bf(g4[q] + bg)), u = bf2f(f2bf(u4[q] + bu));
         if (row < M && c0 < F) out[(size_t)row * F + c0] = f2bf(g / (1.f + __expf(-g)) * u);
       }
+    } else if constexpr (EPI == EPI_PART) {
+      const v4f s4 = total(wave);
+      const float bv = bias != nullptr && c0 < N && ks == 0 ? bf2f(bias[c0]) : 0.f;
+      float* part = reinterpret_cast<float*>(out) + (size_t)ks * M * N;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 4 * (lane >> 4) + q;
+        if (row < M && c0 < N) part[(size_t)row * N + c0] = s4[q] + bv;
+      }
     } else {
       const v4f s4 = total(wave);
       const float bv = bias != nullptr && c0 < N ? bf2f(bias[c0]) : 0.f;
@@ -125,16 +140,16 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
 
 template <int NTW, int U, int EPI>
 int launch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
-           hipStream_t st) {
+           hipStream_t st, int S = 1) {
   const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
-  hipLaunchKernelGGL((gemv_bf16_kernel<NTW, U, EPI>), dim3(groups), dim3(NW * 64), 0, st, (const bf16_t*)A,
-                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F);
+  hipLaunchKernelGGL((gemv_bf16_kernel<NTW, U, EPI>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
+                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S);
   return (int)hipGetLastError();
 }
 }  // namespace
 
-// W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N]; epi 1 (GLU): W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F]
-// (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 16, K % 64 == 0,
+// W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N]; epi 1 (GLU):
+// W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F] (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 16, K % 64 == 0,
 // N % 16 == 0.  Returns -2 for shapes it does not take.
 extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                               hipStream_t st) {
@@ -161,4 +176,13 @@ extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, vo
   if (epi == EPI_GELU) { PICK(EPI_GELU) }
   PICK(EPI_OUT)
 #undef PICK
+}
+
+// Split-K form: fp32 partial slices part [S, M, N] (bias in slice 0), one 16-column tile per group.
+extern "C" int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K,
+                                     int S, hipStream_t st) {
+  if (M <= 0 || M > 16 || K % 64 != 0 || N % 16 != 0 || S < 1 || S > K / 64) return -2;
+  const int nt = N / 16, kps = K / 64 / S;
+  return kps >= 64 ? launch<1, 4, EPI_PART>(A, W, bias, part, M, N, K, 0, nt, st, S)
+                   : launch<1, 2, EPI_PART>(A, W, bias, part, M, N, K, 0, nt, st, S);
 }
