@@ -411,6 +411,8 @@ void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q
     // occupancy target per GQA group size: the per-head q / accumulator registers grow with G, and
     // a 4-waves-per-SIMD bound spills 250-900 B/lane at G >= 4 (ISA resource report)
     constexpr int OCC4 = G <= 2 ? 4 : (G == 4 ? 2 : 1), OCC5 = G <= 2 ? 5 : OCC4;
+    // (8- and 16-wave workgroups for batch-1 grids measured slower: Llama-3.2-1B decode step
+    // 1.08 -> 1.19 ms with 8 waves)
     if (g_attn_occ == 4) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4>), ATTN_ARGS); return; }
     if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC5>), ATTN_ARGS); return; }
   }
