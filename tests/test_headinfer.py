@@ -44,3 +44,24 @@ def test_headinfer_matches_resident_gpu(cuda, h_on, chunk_heads, chunk_size):
     ref, got, kv = _run(cuda, h_on, chunk_heads, chunk_size, dtype=torch.bfloat16)
     assert got.tokens == ref.tokens
     assert kv.host_k.is_pinned()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 37])
+def test_copy_head_block_kernel_both_directions(cuda, T):
+    """offload.hip::head_block_copy_kernel: strided [B, c, T, D] blocks between a pinned host pool
+    and a device buffer, against torch's copy of the same views (bit-exact)."""
+    from edgellm import ops
+    B, H, S, D, h0, c, p0 = 5, 8, 64, 128, 3, 4, 9
+    host = torch.randn(B, H, S, D, dtype=torch.bfloat16).pin_memory()
+    dev = torch.zeros(B, c, S, D, dtype=torch.bfloat16, device="cuda")
+    ops.copy_head_block(dev[:, :, p0:p0 + T], host[:, h0:h0 + c, p0:p0 + T])
+    torch.cuda.synchronize()
+    assert torch.equal(dev[:, :, p0:p0 + T].cpu(), host[:, h0:h0 + c, p0:p0 + T])
+    assert not dev[:, :, :p0].any() and not dev[:, :, p0 + T:].any()
+    src = torch.randn(B, c, T, D, dtype=torch.bfloat16, device="cuda")
+    before = host.clone()
+    ops.copy_head_block(host[:, h0:h0 + c, p0:p0 + T], src)
+    torch.cuda.synchronize()
+    before[:, h0:h0 + c, p0:p0 + T] = src.cpu()
+    assert torch.equal(host, before)
