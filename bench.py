@@ -60,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
+    ap.add_argument("--latency-point", default="auto", choices=["auto", "off", "int8", "both"],
+                    help="also report batch-1 p50 per-token latency (single GPU): int8 = the benchmark model at "
+                         "micro-batch 1, both = plus the bf16 model; auto = both on a GPU, off on CPU")
     ap.add_argument("--headinfer-heads", type=int, default=None,
                     help="HeadInfer: KV heads per layer kept on the GPU, the rest offloaded to pinned host memory")
     return ap.parse_args(argv)
@@ -67,7 +70,7 @@ def parse(argv=None):
 
 def model_config(args):
     if args.model.startswith("tiny:"):
-        return tiny(args.model.split(":", 1)[1], num_layers=4)
+        return tiny(args.model.split(":", 1)[1], num_layers=8)   # 8 layers: splits up to 8 stages
     return get_config(args.model)
 
 
@@ -102,6 +105,8 @@ def run_single(args):
     t_build = time.perf_counter()
     cfg, model = build(args, device)
     t_build = time.perf_counter() - t_build
+    if device.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(device)   # report the serving peak, not the build's
     B = args.micro_batch
     total_new = args.warmup + args.steps + 2
     max_seq = args.prompt_len + total_new + 8
@@ -120,6 +125,7 @@ def run_single(args):
     sp = SamplingParams(max_new_tokens=total_new, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
     gen.start(prompts, sp, seed=args.seed)
     prefill_s = gen._t_prefill if L > 1 else gen._run["t_prefill"]
+    ttft_ms = (gen.lanes[0] if L > 1 else gen)._run["t_prefill"] * 1e3   # prefill + first sampled token, lane 0
     gen.step(args.warmup, record_latency=False)
     gen.precapture(args.steps + 1)
     _sync(device)
@@ -139,9 +145,69 @@ def run_single(args):
     lmax = lat[-1] if lat else p50
     tokens = B * L * args.steps
     mem = torch.cuda.max_memory_allocated() / 1e9 if device.type == "cuda" else 0.0
-    return dict(value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
-                prefill_tps=B * L * args.prompt_len / prefill_s, build_s=t_build, graphs=lanes[0]._run["graphs_ok"],
-                mem_gb=mem, partition=[0, cfg.num_layers])
+    kv_gpu = (kv.gpu_bytes() if kv is not None else gen_kv_bytes(gen)) / 1e9
+    graphs = lanes[0]._run["graphs_ok"]
+    del gen, lanes
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    lat_pts = latency_points(args, device, model, cfg) if args.headinfer_heads is None else {}
+    return dict(latency_point=lat_pts,value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
+                prefill_tps=B * L * args.prompt_len / prefill_s, build_s=t_build, graphs=graphs,
+                mem_gb=mem, partition=[0, cfg.num_layers], ttft_ms=ttft_ms, world_size=1, kv_gpu_gb=kv_gpu,
+                kv_host_gb=(kv.host_bytes() / 1e9 if kv is not None else 0.0))
+
+
+@torch.no_grad()
+def batch1_p50(model, cfg, args, device, steps: int) -> dict:
+    """Batch-1 decode latency of ``model`` (graph-captured, same sampling config): p50 / p90 of
+    per-token device-event intervals over ``steps`` tokens after a warm-up."""
+    W = max(4, args.warmup)
+    max_seq = args.prompt_len + W + steps + 16
+    gen = Generator(model, max_batch=1, max_seq=max_seq, use_graphs=not args.no_graphs)
+    g = torch.Generator().manual_seed(args.seed + 1)
+    prompt = torch.randint(0, cfg.vocab_size, (1, args.prompt_len), generator=g).tolist()
+    sp = SamplingParams(max_new_tokens=W + steps + 2, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
+    gen.start(prompt, sp, seed=args.seed)
+    gen.step(W, record_latency=False)
+    gen.precapture(steps + 1)
+    _sync(device)
+    n0 = len(gen._run["events"])
+    t0 = time.perf_counter()
+    gen.step(steps, record_latency=device.type == "cuda")
+    _sync(device)
+    dt = time.perf_counter() - t0
+    ev = gen._run["events"][n0:]
+    lat = sorted(ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev))) or [dt / steps * 1e3]
+    out = dict(p50_ms=round(lat[len(lat) // 2], 4), p90_ms=round(lat[int(len(lat) * 0.9)], 4),
+               tokens_per_s=round(steps / dt, 1), ttft_ms=round(gen._run["t_prefill"] * 1e3, 3))
+    del gen
+    return out
+
+
+def latency_points(args, device, model, cfg) -> dict:
+    mode = args.latency_point
+    if mode == "auto":
+        mode = "both" if device.type == "cuda" else "off"
+    if mode == "off":
+        return {}
+    steps = max(32, args.steps)
+    pts = {"micro_batch": 1, "prompt_len": args.prompt_len, "steps": steps}
+    pts[args.quant if args.quant != "none" else "bf16"] = batch1_p50(model, cfg, args, device, steps)
+    if mode == "both" and args.quant != "none":
+        import copy
+        a2 = copy.copy(args)
+        a2.quant = "none"
+        _, m16 = build(a2, device)
+        pts["bf16"] = batch1_p50(m16, cfg, a2, device, steps)
+        del m16
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+    return pts
+
+
+def gen_kv_bytes(gen) -> int:
+    lanes = gen.lanes if hasattr(gen, "lanes") else [gen]
+    return sum(x.kv.nbytes() for x in lanes)
 
 
 def run_pipeline(args):
@@ -171,7 +237,11 @@ def main(argv=None):
         "ms_per_step": round(res["ms_per_step"], 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(res["value"] / BASELINE_TPS, 2),
+        # no published value exists for this metric (Llama-2-7B INT8 split 1/2/4/8)
+        "vs_baseline": None,
+        "closest_published": {"what": "single-stream INT8 decode tok/s, Llama-3.2-1B, bitsandbytes LLM.int8, "
+                                      "A100 (ACL.pdf p.7 Table 3) - different model size and batch",
+                              "value": BASELINE_TPS},
         "dtype": "int8" if args.quant != "none" else "bf16",
         "data": f"synthetic (random-init {args.model} weights"
                 + (", SmoothQuant-calibrated on random tokens" if args.quant == "w8a8_smoothquant" else "")
@@ -188,7 +258,18 @@ def main(argv=None):
         "max_token_latency_ms": round(res.get("lat_max", res["p50"]), 4),
         "prefill_tokens_per_s": round(res.get("prefill_tps", 0.0), 1),
         "peak_mem_gb": round(res.get("mem_gb", 0.0), 2),
+        "world_size": res.get("world_size", args.gpus),
     }
+    if res.get("ttft_ms") is not None:
+        out["ttft_ms"] = round(res["ttft_ms"], 3)
+    for k in ("kv_gpu_gb", "kv_host_gb"):
+        if k in res:
+            out[k] = round(res[k], 3)
+    if res.get("latency_point"):
+        out["latency_point"] = res["latency_point"]
+    if "per_rank" in res:
+        out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
+        out["per_rank"] = res["per_rank"]
     print(json.dumps(out), flush=True)
     return out
 

@@ -50,10 +50,12 @@ class HeadInferKV:
 
     def __init__(self, cfg: ModelConfig, max_batch: int, max_seq: int, h_on: int, device=None, first: int = 0,
                  last: Optional[int] = None, chunk_heads: Optional[int] = None, chunk_size: int = 4096,
-                 dtype=torch.bfloat16, stage_budget_bytes: float = 2e9):
+                 dtype=torch.bfloat16, stage_budget_bytes: float = 2e9, call_rows: Optional[int] = None):
         """``chunk_heads``: offloaded heads staged per transfer; None = as many as fit
         ``stage_budget_bytes`` across the two ping-pong K/V buffers (the paper stages one head at a
-        time to fit a 24 GB card; with 288 GB of HBM larger chunks cut the per-head launches)."""
+        time to fit a 24 GB card; with 288 GB of HBM larger chunks cut the per-head launches).
+        ``call_rows``: most cache rows one forward touches (a pipeline micro-batch); the staging
+        and new-row buffers are sized by it instead of by the whole cache (``max_batch``)."""
         hk, D = cfg.num_kv_heads, cfg.head_dim
         assert 0 <= h_on <= hk, "h_on must be within [0, num_kv_heads]"
         self.cfg, self.first = cfg, first
@@ -64,16 +66,17 @@ class HeadInferKV:
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.cuda = self.device.type == "cuda"
         self.gpu = KVCache(cfg, max_batch, max_seq, first, self.last, dtype, device, num_kv_heads=h_on)
+        R = self.call_rows = min(max_batch, call_rows or max_batch)
         if chunk_heads is None:
-            per_head = 2 * 2 * max_batch * max_seq * D * torch.finfo(dtype).bits // 8   # 2 buffers x (k, v)
+            per_head = 2 * 2 * R * max_seq * D * torch.finfo(dtype).bits // 8   # 2 buffers x (k, v)
             chunk_heads = int(max(1, stage_budget_bytes // max(per_head, 1)))
         self.c = max(1, min(chunk_heads, max(self.h_off, 1)))
         pin = self.cuda
         self.host_k = torch.zeros((L, max_batch, self.h_off, max_seq, D), dtype=dtype, pin_memory=pin)
         self.host_v = torch.zeros_like(self.host_k, pin_memory=pin)
         mk = lambda *s: torch.zeros(*s, dtype=dtype, device=device)  # noqa: E731
-        self.stage = [(mk(max_batch, self.c, max_seq, D), mk(max_batch, self.c, max_seq, D)) for _ in range(2)]
-        self.new = [(mk(max_batch, self.h_off, chunk_size, D), mk(max_batch, self.h_off, chunk_size, D))
+        self.stage = [(mk(R, self.c, max_seq, D), mk(R, self.c, max_seq, D)) for _ in range(2)]
+        self.new = [(mk(R, self.h_off, chunk_size, D), mk(R, self.h_off, chunk_size, D))
                     for _ in range(2)]
         self.zeros = torch.zeros(max_batch, dtype=torch.int32, device=device)
         if self.cuda:
@@ -129,6 +132,7 @@ class HeadInferKV:
         cfg = self.cfg
         B, T = ctx.B, ctx.T
         assert T <= self.chunk_size, "prefill must be chunked to <= chunk_size tokens"
+        assert B <= self.call_rows, "a forward may touch at most call_rows cache rows"
         hq, hk, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
         G = hq // hk
         r0, r1 = ctx.kv.r0, ctx.kv.r1

@@ -1,4 +1,4 @@
-"""Multi-GPU leg of bench.py: pipeline of N stages (one per GPU), N micro-batches in flight.
+"""Multi-GPU leg of bench.py: pipeline of N stages (one per GPU), N x lanes micro-batches in flight.
 
 M = N x lanes micro-batches; each tick a stage runs one group of ``lanes`` micro-batches
 concurrently on that many HIP streams.  Timed region = ticks [t_a, t_b) with the pipeline full:
@@ -6,12 +6,18 @@ t_a = (M + W*M)/L + (P-1), t_b = t_a + K*M/L, i.e. exactly K decode steps of eve
 bracketed on every rank by device-synchronize + barrier; the reported time is the max over ranks.
 p50 per-token latency = median interval between consecutive tokens of one sequence (M/L ticks),
 from device events on the last stage (host timestamps on CPU).
-Runs on CPU with gloo when no GPU is present (``--device cpu``), which is how the multi-process
-path is tested without GPUs.
+
+Failure handling: the process group carries a timeout (``EDGELLM_PG_TIMEOUT_S``),
+and a heartbeat ``Watchdog`` (``EDGELLM_WATCHDOG_S``, default 300 s) aborts a rank that makes no
+progress, naming its last tick, so torchrun tears the job down instead of hanging.
+Every rank reports its per-tick compute, P2P wait and bubble fraction over the timed window
+(``per_rank`` in the result).  Runs on CPU with gloo when no GPU is present (``--device cpu``),
+which is how the multi-process path is tested without GPUs.
 """
 from __future__ import annotations
 
 import os
+import sys
 import time
 
 import torch
@@ -20,11 +26,24 @@ import torch.distributed as dist
 from ..engine.generate import SamplingParams
 from .partition import partition_model, stage_costs
 from .pipeline import PipelineStage, init_distributed
+from .watchdog import Watchdog
+
+_STAT_KEYS = ("compute_ms_per_tick", "p2p_wait_ms_per_tick", "bubble_frac", "p2p_bytes_per_tick", "span_ms",
+              "ttft_ms")
+
+
+def _abort_rank(msg: str):
+    sys.stderr.write(f"[edgellm watchdog] rank {os.environ.get('RANK', '?')}: {msg}\n")
+    sys.stderr.flush()
+    os._exit(124)
 
 
 def run_pipeline_bench(args, build, model_config):
     """``build(args, device, first, last) -> (cfg, stage_model)``; ``model_config(args) -> cfg``."""
     use_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
+    wd = Watchdog(timeout_s=float(os.environ.get("EDGELLM_WATCHDOG_S", "300")), on_timeout=_abort_rank,
+                  name="bench_pipeline").start()
+    wd.beat("init_process_group")
     rank, world = init_distributed("nccl" if use_cuda else "gloo")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
@@ -41,6 +60,7 @@ def run_pipeline_bench(args, build, model_config):
     hcl = 0.6 if args.quant != "none" else 0.4
     bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
                              weight_bytes=wbytes, explicit=explicit, head_cost_layers=hcl)
+    wd.beat("build")
     _, model = build(args, device, first=bounds[rank], last=bounds[rank + 1])
     L = max(1, getattr(args, "lanes", 1))
     M, P, b, T = world * L, world, args.micro_batch, args.prompt_len
@@ -48,13 +68,13 @@ def run_pipeline_bench(args, build, model_config):
     S = W + K + 1
     g = torch.Generator().manual_seed(args.seed)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)] if rank == 0 else None
+    wd.beat("stage init (communicator warm-up)")
+    # the stage's constructor joins every rank in one collective (eager RCCL communicator)
     stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs,
                           headinfer_heads=getattr(args, "headinfer_heads", None), lanes=L)
-    # initialise the communicator with a collective every rank joins
-    x = torch.ones(1, device=cdev)
-    dist.all_reduce(x)
     if use_cuda:
         torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(device)
     # ticks count item groups of L micro-batches (one per lane)
     t_a = (M + W * M) // L + (P - 1)
     t_b = t_a + K * M // L
@@ -78,7 +98,9 @@ def run_pipeline_bench(args, build, model_config):
                 stamps.append(time.perf_counter())
 
     sp = SamplingParams(max_new_tokens=S + 1, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
-    stage.run(prompts, T, sp, S, seed=args.seed, hook=hook)
+    dist.barrier()
+    res_stage = stage.run(prompts, T, sp, S, seed=args.seed, hook=hook, watchdog=wd, stats_window=(t_a, t_b))
+    wd.beat("report")
     fdt = torch.float64
     dt = torch.tensor([marks[t_b] - marks[t_a]], device=cdev, dtype=fdt)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
@@ -92,13 +114,26 @@ def run_pipeline_bench(args, build, model_config):
     dist.all_reduce(lat, op=dist.ReduceOp.MAX)
     mem = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9 if use_cuda else 0.0], device=cdev, dtype=fdt)
     dist.all_reduce(mem, op=dist.ReduceOp.MAX)
+    # per-rank window statistics, gathered to every rank as one [world, k] tensor
+    mine = torch.tensor([[float(res_stage.stats.get(k, float("nan"))) for k in _STAT_KEYS]], device=cdev, dtype=fdt)
+    allst = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allst, mine)
     elapsed = float(dt.item())
     res = None
     if rank == 0:
         tokens = K * M * b
+        per_rank = []
+        for r, row in enumerate(allst):
+            d = {k: round(float(v), 4) for k, v in zip(_STAT_KEYS, row[0].tolist()) if v == v}
+            d.update(rank=r, layers=[bounds[r], bounds[r + 1]])
+            per_rank.append(d)
+        ttft = [d["ttft_ms"] for d in per_rank if "ttft_ms" in d]
         res = dict(value=tokens / elapsed, ms_per_step=elapsed / K * 1e3, p50=float(lat.item()), global_batch=M * b,
-                   mem_gb=float(mem.item()), partition=bounds,
+                   mem_gb=float(mem.item()), partition=bounds, world_size=world, per_rank=per_rank,
+                   bubble_frac_max=max(d.get("bubble_frac", 0.0) for d in per_rank),
+                   ttft_ms=ttft[0] if ttft else None,
                    stage_cost_mb=[round(c / 1e6, 1) for c in stage_costs(cfg, bounds, wbytes, head_cost_layers=hcl)])
     dist.barrier()
+    wd.stop()
     dist.destroy_process_group()
     return res

@@ -1,27 +1,37 @@
 """Layer-partitioned inference pipeline: one process per GPU ("edge device"), RCCL P2P over xGMI.
 
 The reference only ever splits a model implicitly through accelerate's ``device_map="auto"``
-(activations hop GPUs via ``tensor.to(next_device)``, no micro-batching — SURVEY §2.4, K16) and
-ships no tensors over its gRPC demo.  Here every stage is its own process; hidden states move
-rank r -> r+1 with RCCL point-to-point, and the tokens sampled on the last stage travel back to
-stage 0 (a token ring), so decode keeps every stage busy:
+(activations hop GPUs via ``tensor.to(next_device)``, no micro-batching — SURVEY §2.4, K16;
+Code/Base Models/Llama_bf16_updated.py:31) and ships no tensors over its gRPC demo.  Here every
+stage is its own process; hidden states move rank r -> r+1 with RCCL point-to-point, and the
+tokens sampled on the last stage travel back to stage 0 (a token ring), so decode keeps every
+stage busy:
 
   work items (same order on every rank):  prefill(m) for m < M, then decode(k, m) for k < S
   rank s processes item i at tick i + s (lockstep); with M >= P micro-batches the token of
   decode(k, m) reaches stage 0 exactly when decode(k+1, m) starts (M - P ticks of slack).
 
-Per tick each rank issues ONE grouped P2P exchange (send the previous tick's output, receive
-this tick's input — grouped, so no send/recv ordering deadlock), then runs its layers for the
-micro-batch.  The decode compute of each micro-batch is captured in a HIP graph (per KV-length
-bucket); the P2P ops stay outside the graph on RCCL's stream, ordered by stream waits, so the
-host never blocks on the device inside the loop.  Messages: decode b*H*2 bytes per hop
-(16 x 4096 bf16 = 128 KiB), prefill b*T*H*2.
+Per tick each rank issues ONE grouped P2P exchange through ``dist.batch_isend_irecv`` (send the
+previous tick's outputs, receive this tick's inputs — grouped, so no send/recv ordering deadlock;
+on RCCL one ncclGroupStart/End over the process group's communicator), then runs its layers for
+the micro-batches of the tick.  The same P2POp path runs under gloo on the CPU, which is how the
+multi-rank schedule is tested without GPUs.  The decode compute of each micro-batch is captured in
+a HIP graph per KV-length bucket (all buckets of a run are captured at the first capture, before
+any timed region); the P2P ops stay outside the graphs on RCCL's stream, ordered by stream waits,
+so the host never blocks on the device inside the loop.  Messages: decode b*H*2 bytes per hop
+(128 x 4096 bf16 = 1 MiB), prefill b*T*H*2.
+
+Communicator set-up is eager: ``init_distributed`` binds the rank's device (``device_id``) so
+RCCL builds the world communicator at init, and ``PipelineStage.__init__`` runs one all-ranks
+collective before any P2P (``batch_isend_irecv`` requires the first op on a communicator to be
+joined by every rank).  Per-tick device events give every rank's compute time, P2P wait and
+bubble fraction over a window of ticks (``run(stats_window=...)`` -> ``PipelineResult.stats``).
 """
 from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -30,6 +40,7 @@ from .. import ops
 from ..engine.generate import GRAPH_BUCKET, SamplingParams, needs_host_sampler
 from ..engine.kv_cache import KVCache
 from ..models.decoder import AttnCtx, DecoderLM
+from ..utils.tracing import debug_sync, trace_range
 
 
 @dataclass
@@ -38,17 +49,22 @@ class PipelineResult:
     ticks: int
     elapsed_s: float
     marks: Dict[str, float] = field(default_factory=dict)
+    stats: Dict[str, float] = field(default_factory=dict)   # this rank, over the stats window
 
 
 class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
                  group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None,
-                 lanes: int = 1):
+                 lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True):
         """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
         to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
-        HeadInfer").  The offloaded path is host-orchestrated, so its decode steps run eagerly."""
+        HeadInfer").  The offloaded path is host-orchestrated on one compute stream, so it runs one
+        lane and its decode steps run eagerly; its cache is built at ``run`` with prefill chunks
+        of min(prompt_len, ``prefill_chunk``) tokens and staging buffers of one micro-batch."""
         assert lanes >= 1 and n_micro % lanes == 0, "micro-batches must split evenly over lanes"
         assert n_micro >= world * lanes, "need lanes x stages micro-batches to keep the ring full"
+        offload = headinfer_heads is not None and headinfer_heads < model.cfg.num_kv_heads
+        assert not offload or lanes == 1, "HeadInfer offload orders its transfers on one stream: use lanes=1"
         self.model, self.cfg = model, model.cfg
         self.rank, self.world = rank, world
         self.b, self.M = micro_batch, n_micro
@@ -60,16 +76,14 @@ class PipelineStage:
         assert self.is_first == (rank == 0) and self.is_last == (rank == world - 1)
         self.prev = (rank - 1) % world
         self.next = (rank + 1) % world
-        if headinfer_heads is not None and headinfer_heads < self.cfg.num_kv_heads:
-            from ..offload import HeadInferKV
-            self.kv = HeadInferKV(self.cfg, micro_batch * n_micro, max_seq, headinfer_heads, self.device, self.first,
-                                  self.last, chunk_size=max_seq, dtype=model.dtype)
-        else:
-            self.kv = KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last, model.dtype,
-                              self.device)
-        self.attn_hook = getattr(self.kv, "attn_hook", None)
+        self.h_on = headinfer_heads if offload else None
+        self.prefill_chunk = max(1, prefill_chunk)
+        self.kv = None if offload else KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last,
+                                               model.dtype, self.device)
+        self.attn_hook = None
         self.rope = model.rope_table(self.device)
         cuda = self.device.type == "cuda"
+        self.cuda = cuda
         self.use_graphs = cuda if use_graphs is None else (use_graphs and cuda)
         self.nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
         # gloo with device tensors (several ranks sharing one GPU for a rehearsal): P2P is staged
@@ -88,40 +102,86 @@ class PipelineStage:
         self.L = lanes
         self.streams = ([torch.cuda.Stream(self.device) for _ in range(lanes)]
                         if cuda and lanes > 1 else None)
+        self.p2p_bytes = 0
+        if warm_comm and dist.is_initialized() and world > 1:
+            self.warm_communicator()
+
+    def warm_communicator(self):
+        """One collective every rank joins: creates RCCL's world communicator (and its xGMI peer
+        connections' first use) before the first grouped P2P, outside any timed region."""
+        x = torch.ones(1, device=self.device if self.nccl else "cpu")
+        dist.all_reduce(x, group=self.group)
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ p2p
     def _exchange(self, sends, recvs):
-        """sends/recvs: lists of (tensor, peer).  One grouped exchange."""
+        """sends/recvs: lists of (tensor, peer).  One grouped exchange (dist.P2POp batch)."""
         if not sends and not recvs:
             return
-        if self.nccl:
+        self.p2p_bytes += sum(t.numel() * t.element_size() for t, _ in sends)
+        if self.host_staged:
+            bufs = [torch.empty(t.shape, dtype=t.dtype) for t, _ in recvs]
+            p2p = [dist.P2POp(dist.isend, t.cpu(), p, self.group) for t, p in sends]
+            p2p += [dist.P2POp(dist.irecv, h, p, self.group) for h, (_, p) in zip(bufs, recvs)]
+        else:
+            bufs = None
             p2p = [dist.P2POp(dist.isend, t, p, self.group) for t, p in sends]
             p2p += [dist.P2POp(dist.irecv, t, p, self.group) for t, p in recvs]
+        with trace_range("pp.exchange"):
+            # RCCL: wait() makes the current stream wait on the communication (no host block)
             for w in dist.batch_isend_irecv(p2p):
                 w.wait()
-        elif self.host_staged:
-            works = [dist.isend(t.cpu(), p, self.group) for t, p in sends]
-            bufs = [torch.empty(t.shape, dtype=t.dtype) for t, _ in recvs]
-            works += [dist.irecv(h, p, self.group) for h, (_, p) in zip(bufs, recvs)]
-            for w in works:
-                w.wait()
+        if bufs is not None:
             for h, (t, _) in zip(bufs, recvs):
                 t.copy_(h)
-        else:
-            works = [dist.isend(t, p, self.group) for t, p in sends]
-            works += [dist.irecv(t, p, self.group) for t, p in recvs]
-            for w in works:
-                w.wait()
+        debug_sync("pp.exchange")
+
+    def _send_one(self, t: torch.Tensor, peer: int):
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, peer, self.group)]):
+            w.wait()
+
+    def _recv_one(self, t: torch.Tensor, peer: int):
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, peer, self.group)]):
+            w.wait()
 
     # ------------------------------------------------------------------ compute
     def _rows(self, m):
         return self.kv.rows(m * self.b, (m + 1) * self.b)
 
+    def _build_offload_kv(self, T: int):
+        from ..offload import HeadInferKV
+        chunk = min(T, self.prefill_chunk)
+        kv = self.kv
+        if kv is None or kv.chunk_size != chunk:
+            self.kv = None
+            if self.cuda:
+                torch.cuda.empty_cache()
+            self.kv = HeadInferKV(self.cfg, self.b * self.M, self.max_seq, self.h_on, self.device, self.first,
+                                  self.last, chunk_size=chunk, dtype=self.model.dtype, call_rows=self.b)
+        self.attn_hook = self.kv.attn_hook
+
     def _prefill(self, m: int, ids: Optional[torch.Tensor], T: int, hidden: Optional[torch.Tensor]):
-        b = self.b
-        sp = torch.zeros(b, dtype=torch.int32, device=self.device)
-        ctx = AttnCtx("prefill", b, T, sp, sp + T, T, self._rows(m), self.rope, attn_hook=self.attn_hook)
-        out = self.model(ids, ctx, hidden=hidden, logits="last")
+        """Prefill micro-batch m (prompt length T); chunked by ``prefill_chunk`` when the KV is
+        offloaded (HeadInfer bounds activation memory by the chunk, as in the paper)."""
+        b, H = self.b, self.cfg.hidden_size
+        C = getattr(self.kv, "chunk_size", T) if self.attn_hook is not None else T
+        outs = []
+        out = None
+        for c0 in range(0, T, C):
+            c1 = min(T, c0 + C)
+            sp = torch.full((b,), c0, dtype=torch.int32, device=self.device)
+            ctx = AttnCtx("prefill", b, c1 - c0, sp, sp + (c1 - c0), c1, self._rows(m), self.rope,
+                          attn_hook=self.attn_hook)
+            x_ids = ids[:, c0:c1] if ids is not None else None
+            x_h = None
+            if hidden is not None:
+                x_h = hidden.view(b, T, H)[:, c0:c1].reshape(b * (c1 - c0), H) if C < T else hidden
+            out = self.model(x_ids, ctx, hidden=x_h, logits="last")
+            if not self.is_last and C < T:
+                outs.append(out.view(b, c1 - c0, H))
+        if outs:
+            out = torch.cat(outs, 1).reshape(b * T, H)
         self.pos[m].fill_(T)
         self.lens[m].fill_(T + 1)
         return out
@@ -148,49 +208,69 @@ class PipelineStage:
         self.rng[m][1:].add_(1)
         self.step[m].add_(1)
 
+    def _bucket(self, max_len: int) -> int:
+        return min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
+
+    def _capture(self, m: int, bucket: int):
+        g = torch.cuda.CUDAGraph()
+        lane = m % self.L
+        # thread-local capture so the process group's watchdog thread may keep querying its
+        # events meanwhile; the caller guarantees no P2P of this rank is in flight
+        with torch.cuda.graph(g, pool=self._pools.get(lane), capture_error_mode="thread_local"):
+            self._decode_body(m, bucket)
+        if lane not in self._pools:
+            self._pools[lane] = g.pool()
+        self._graphs[(m, bucket)] = g
+        return g
+
     def _decode(self, m: int, max_len: int):
         if not self.graphs_ok:
             return self._decode_body(m, max_len)
-        bucket = min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
-        key = (m, bucket)
-        g = self._graphs.get(key)
+        bucket = self._bucket(max_len)
+        g = self._graphs.get((m, bucket))
         if g is None:
             if not self._warm.get(m):
                 self._warm[m] = True
                 return self._decode_body(m, bucket)     # first decode of m runs eagerly (warm-up)
-            g = torch.cuda.CUDAGraph()
-            # no P2P in flight during capture, and a thread-local capture so the process group's
-            # watchdog thread may keep querying its events meanwhile
-            torch.cuda.synchronize()
-            lane = m % self.L
-            with torch.cuda.graph(g, pool=self._pools.get(lane), capture_error_mode="thread_local"):
-                self._decode_body(m, bucket)
-            if lane not in self._pools:
-                self._pools[lane] = g.pool()
-            self._graphs[key] = g
-            return g.replay()
+            # capture every bucket this run will reach for m at once (capture records, it does
+            # not execute), so no capture — and no device synchronize — lands later in the run
+            torch.cuda.synchronize(self.device)
+            b = bucket
+            while True:
+                if (m, b) not in self._graphs:
+                    self._capture(m, b)
+                if b >= self._final_bucket:
+                    break
+                b = self._bucket(b + 1)
+            g = self._graphs[(m, bucket)]
         g.replay()
 
     # ------------------------------------------------------------------ schedule
     @torch.no_grad()
     def run(self, prompts: Optional[Sequence[torch.Tensor]], prompt_len: int, sampling: SamplingParams,
             decode_steps: int, seed: int = 0, hook: Optional[Callable[[int], None]] = None,
-            watchdog=None, fault: Optional[Callable[[int], None]] = None) -> PipelineResult:
+            watchdog=None, fault: Optional[Callable[[int], None]] = None,
+            stats_window: Optional[Tuple[int, int]] = None) -> PipelineResult:
         """prompts: M tensors [b, T] of token ids (needed on rank 0 only; T = prompt_len).
         decode_steps = tokens generated per sequence after the first (prefill-sampled) one.
         ``watchdog`` (parallel.watchdog.Watchdog) gets a heartbeat per tick; ``fault(tick)`` is a
-        test hook that may delay or raise before a tick's exchange (fault injection)."""
+        test hook that may delay or raise before a tick's exchange (fault injection).
+        ``stats_window=(t_a, t_b)``: ticks over which this rank's compute / P2P-wait / bubble
+        statistics are taken (``PipelineResult.stats``)."""
         M, P, b, T = self.M, self.world, self.b, prompt_len
         S = decode_steps
         assert T + S + 1 <= self.max_seq
         V = self.cfg.vocab_size
         self.sampling = sampling
+        if self.h_on is not None:
+            self._build_offload_kv(T)
         self.graphs_ok = self.use_graphs and not needs_host_sampler(sampling, V) and \
             getattr(self.kv, "graph_safe", True) and \
             all(getattr(mm, "graph_safe", True) or getattr(mm, "graph_safe_rows", 0) >= b for mm in self.model.modules())
         self._warm: Dict[int, bool] = {}
         self._graphs.clear()
         self._pools.clear()
+        self._final_bucket = self._bucket(T + S + 1)
         dev = self.device
         if self.is_last:
             self.seen = [torch.zeros(b, V, dtype=torch.uint8, device=dev) for _ in range(M)]
@@ -198,30 +278,25 @@ class PipelineStage:
                         for m in range(M)]
             self.step = [torch.zeros(1, dtype=torch.long, device=dev) for _ in range(M)]
             self.out = [torch.zeros(b, S + 1, dtype=torch.long, device=dev) for _ in range(M)]
-        if self.is_first and self.is_last is False:
-            pass
         # repetition-penalty history needs the prompt ids on the last stage
+        pdev = "cpu" if self.host_staged else dev
         if self.is_last:
             if self.is_first:
                 for m in range(M):
                     self.seen[m].scatter_(1, prompts[m].to(dev), 1)
             else:
-                pids = torch.zeros(M, b, T, dtype=torch.long, device="cpu" if self.host_staged else dev)
-                if dist.is_initialized():
-                    dist.recv(pids, 0, self.group)
+                pids = torch.zeros(M, b, T, dtype=torch.long, device=pdev)
+                self._recv_one(pids, 0)
                 pids = pids.to(dev)
                 for m in range(M):
                     self.seen[m].scatter_(1, pids[m], 1)
         elif self.is_first and P > 1:
-            dist.send(torch.stack([p.to("cpu" if self.host_staged else dev) for p in prompts]), P - 1, self.group)
+            self._send_one(torch.stack([p.to(pdev) for p in prompts]), P - 1)
 
         H = self.cfg.hidden_size
         pre_in = [None] * M
         pre_out = [None] * M
         n_items = M + S * M
-
-        def valid(i):
-            return 0 <= i < n_items
 
         def feeds_back(i):  # does item i's sampled token feed a later decode item?
             return (i < M and S >= 1) or (i >= M and (i - M) // M + 1 < S)
@@ -231,7 +306,7 @@ class PipelineStage:
         # out, this group's inputs in) ordered after all lanes' work and before any of the next
         L = self.L
         n_groups = n_items // L
-        cur_stream = torch.cuda.current_stream(dev) if self.streams else None
+        cur_stream = torch.cuda.current_stream(dev) if self.cuda else None
 
         def group_valid(g):
             return 0 <= g < n_groups
@@ -239,8 +314,24 @@ class PipelineStage:
         def lane_ctx(i):
             return torch.cuda.stream(self.streams[i % L]) if self.streams else _nullctx()
 
+        w_a, w_b = stats_window if stats_window is not None else (-1, -1)
+        ev_in: Dict[int, object] = {}      # tick -> inputs ready (exchange done)
+        ev_done: Dict[int, object] = {}    # tick -> all lanes' compute done
+        win_bytes = 0
+
+        def mark(store, t):
+            if self.cuda:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(cur_stream)
+                store[t] = e
+            else:
+                store[t] = time.perf_counter()
+
         t_start = time.perf_counter()
         n_ticks = n_groups + P - 1
+        t_first = P - 1 if self.is_last else -1     # tick whose prefill samples the first token
+        ev_first: Dict[int, object] = {}
+        mark(ev_first, -1)
         for t in range(n_ticks):
             if hook is not None:
                 hook(t)
@@ -273,28 +364,41 @@ class PipelineStage:
             if self.streams:
                 for st in self.streams:
                     cur_stream.wait_stream(st)
+            if w_a <= t - 1 < w_b:
+                mark(ev_done, t - 1)
+            if w_a <= t < w_b:
+                win_bytes += sum(x.numel() * x.element_size() for x, _ in sends)
             self._exchange(sends, recvs)
+            if w_a <= t < w_b:
+                mark(ev_in, t)
             if self.streams:
                 for st in self.streams:
                     st.wait_stream(cur_stream)
             if not group_valid(cur_g):
                 continue
-            for cur in range(cur_g * L, cur_g * L + L):
-                with lane_ctx(cur):
-                    if cur < M:                           # prefill item
-                        m = cur
-                        if self.streams and pre_in[m] is not None:
-                            pre_in[m].record_stream(self.streams[m % L])   # received on the exchange stream
-                        ids = prompts[m].to(dev) if self.is_first else None
-                        out = self._prefill(m, ids, T, pre_in[m])
-                        pre_in[m] = None
-                        if self.is_last:
-                            self._sample(m, out)
+            with trace_range(f"pp.tick{t}"):
+                for cur in range(cur_g * L, cur_g * L + L):
+                    with lane_ctx(cur):
+                        if cur < M:                           # prefill item
+                            m = cur
+                            if self.streams and pre_in[m] is not None:
+                                pre_in[m].record_stream(self.streams[m % L])   # received on the exchange stream
+                            ids = prompts[m].to(dev) if self.is_first else None
+                            out = self._prefill(m, ids, T, pre_in[m])
+                            pre_in[m] = None
+                            if self.is_last:
+                                self._sample(m, out)
+                            else:
+                                pre_out[m] = out
                         else:
-                            pre_out[m] = out
-                    else:
-                        k, m = divmod(cur - M, M)
-                        self._decode(m, T + k + 1)
+                            k, m = divmod(cur - M, M)
+                            self._decode(m, T + k + 1)
+            debug_sync(f"pp.tick{t}")
+            if t == t_first:
+                if self.streams:
+                    for st in self.streams:
+                        cur_stream.wait_stream(st)
+                mark(ev_first, t)
             if not self.is_last and group_valid(prv_g):
                 for prv in range(prv_g * L, prv_g * L + L):
                     if prv < M:
@@ -302,15 +406,43 @@ class PipelineStage:
         if self.streams:
             for st in self.streams:
                 cur_stream.wait_stream(st)
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
+        if w_a <= n_ticks - 1 < w_b:
+            mark(ev_done, n_ticks - 1)
+        if self.cuda:
+            torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t_start
+        stats = {}
+        if stats_window is not None and ev_in:
+            stats = self._window_stats(ev_in, ev_done, w_a, w_b, win_bytes)
+        if t_first >= 0 and t_first in ev_first:
+            a, z = ev_first[-1], ev_first[t_first]
+            stats["ttft_ms"] = a.elapsed_time(z) if self.cuda else (z - a) * 1e3
         toks = None
         if self.is_last:
             toks = []
             for m in range(M):
                 toks.extend(self.out[m].tolist())
-        return PipelineResult(toks, n_ticks, elapsed)
+        return PipelineResult(toks, n_ticks, elapsed, stats=stats)
+
+    def _window_stats(self, ev_in, ev_done, t_a, t_b, nbytes) -> Dict[str, float]:
+        """Per-tick compute (inputs ready -> all lanes done) and P2P wait (lanes done -> next
+        inputs ready) on this rank, milliseconds; bubble = 1 - compute / window span."""
+        ticks = [t for t in range(t_a, t_b) if t in ev_in and t in ev_done]
+        if not ticks:
+            return {}
+        if self.cuda:
+            dt = lambda a, b: a.elapsed_time(b)             # noqa: E731
+        else:
+            dt = lambda a, b: (b - a) * 1e3                 # noqa: E731
+        busy = [dt(ev_in[t], ev_done[t]) for t in ticks]
+        waits = [dt(ev_done[t - 1], ev_in[t]) for t in ticks if t - 1 in ev_done]
+        span = dt(ev_in[ticks[0]], ev_done[ticks[-1]])
+        busy_s = sorted(busy)
+        return dict(ticks=len(ticks), compute_ms_per_tick=sum(busy) / len(busy),
+                    compute_ms_p50=busy_s[len(busy_s) // 2],
+                    p2p_wait_ms_per_tick=(sum(waits) / len(waits)) if waits else 0.0,
+                    span_ms=span, bubble_frac=max(0.0, 1.0 - sum(busy) / span) if span > 0 else 0.0,
+                    p2p_bytes_per_tick=nbytes / max(1, t_b - t_a))
 
 
 class _nullctx:
@@ -321,15 +453,24 @@ class _nullctx:
         return False
 
 
-def init_distributed(backend: Optional[str] = None):
-    """torchrun-style init (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*). backend "nccl" is RCCL."""
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None):
+    """torchrun-style init (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*). backend "nccl" is RCCL.
+
+    With RCCL the rank's GPU is bound at init (``device_id``): the world communicator is created
+    eagerly, so the first grouped P2P does not build one lazily inside the decode loop.
+    ``timeout_s`` (default ``EDGELLM_PG_TIMEOUT_S`` or 600) bounds every collective / P2P wait."""
     import os
+    from .watchdog import init_pg_timeout
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     backend = os.environ.get("EDGELLM_DIST_BACKEND", backend)   # e.g. gloo: GPU ranks sharing one device
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+    timeout = init_pg_timeout(float(os.environ.get("EDGELLM_PG_TIMEOUT_S", timeout_s or 600.0)))
+    kw = {}
     if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    dist.init_process_group(backend=backend)
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        kw["device_id"] = dev
+    dist.init_process_group(backend=backend, timeout=timeout, **kw)
     return dist.get_rank(), dist.get_world_size()

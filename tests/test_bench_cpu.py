@@ -42,7 +42,7 @@ def test_bench_single_cpu(lanes):
     assert d["config"]["lanes"] == lanes
 
 
-@pytest.mark.parametrize("n,lanes", [(2, 1), (2, 2), (3, 2)])
+@pytest.mark.parametrize("n,lanes", [(2, 1), (2, 2), (3, 2), (4, 2), (8, 1), (8, 2)])
 def test_bench_pipeline_torchrun_cpu(n, lanes):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *COMMON,
@@ -53,6 +53,12 @@ def test_bench_pipeline_torchrun_cpu(n, lanes):
     d = _last_json(r.stdout)
     assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n * lanes and d["value"] > 0
     assert d["config"]["parallelism"] == f"pp{n}" and len(d["config"]["partition"]) == n + 1
+    # per-rank window statistics from every stage (compute / P2P wait / bubble / bytes per tick)
+    assert d["world_size"] == n and len(d["per_rank"]) == n
+    for r, st in enumerate(d["per_rank"]):
+        assert st["rank"] == r and st["compute_ms_per_tick"] > 0 and 0 <= st["bubble_frac"] <= 1
+        assert st["p2p_bytes_per_tick"] > 0
+    assert d["ttft_ms"] > 0
 
 
 @pytest.mark.parametrize("n", [1, 2])

@@ -1,4 +1,8 @@
-"""Pipeline runtime on CPU with the gloo backend (multi-process, world_size 2 and 3).
+"""Pipeline runtime on CPU with the gloo backend (multi-process, world_size 2, 3, 4 and 8).
+
+Every exchange goes through the same ``dist.P2POp`` / ``batch_isend_irecv`` code the RCCL run
+uses; world 4 and 8 rehearse the driver's 4- and 8-GPU splits (8 layers: one or two per stage,
+plus the head stage), with one and two lanes and with HeadInfer offload.
 
 Checks the split model's tokens are identical to the unsplit model's (greedy and seeded
 sampling) — the SURVEY §4 requirement "a split model's output is bit-identical (greedy) to the
@@ -25,29 +29,35 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads=None, lanes=1):
+def _worker(rank, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads=None, lanes=1, n_layers=4,
+            prefill_chunk=4096):
     import edgellm  # noqa: F401
     from edgellm.parallel.pipeline import PipelineStage
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
-    cfg = tiny(arch, num_layers=4)
+    cfg = tiny(arch, num_layers=n_layers)
     bounds = partition_model(cfg, world, "uniform")
     model = build_model(cfg, dtype=torch.float32, first=bounds[rank], last=bounds[rank + 1], seed=7)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
-    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, headinfer_heads=headinfer_heads, lanes=lanes)
+    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, headinfer_heads=headinfer_heads, lanes=lanes,
+                       prefill_chunk=prefill_chunk)
     sp = SamplingParams(max_new_tokens=S + 1, do_sample=do_sample, temperature=0.7, top_k=20, top_p=0.9,
                         repetition_penalty=1.1)
-    res = st.run(prompts if rank == 0 else None, T, sp, S, seed=5)
+    n_ticks = (M + S * M) // lanes + world - 1
+    res = st.run(prompts if rank == 0 else None, T, sp, S, seed=5, stats_window=(M // lanes + world - 1, n_ticks))
+    assert res.stats["ticks"] > 0 and 0.0 <= res.stats["bubble_frac"] <= 1.0, res.stats
+    if world > 1:
+        assert res.stats["p2p_bytes_per_tick"] > 0, res.stats
     if res.tokens is not None:
         q.put(res.tokens)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _reference(arch, M, b, T, S, do_sample):
-    cfg = tiny(arch, num_layers=4)
+def _reference(arch, M, b, T, S, do_sample, n_layers=4):
+    cfg = tiny(arch, num_layers=n_layers)
     model = build_model(cfg, dtype=torch.float32, seed=7)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
@@ -77,6 +87,52 @@ def test_pipeline_matches_unsplit(world, M, lanes, do_sample):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == _reference(arch, M, b, T, S, do_sample)
+
+
+def _run_world(world, M, lanes, do_sample, headinfer_heads=None, n_layers=8, T=5, S=6, prefill_chunk=4096):
+    arch, b = "llama", 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, M, b, T, S, do_sample, q, headinfer_heads,
+                                               lanes, n_layers, prefill_chunk))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    assert got == _reference(arch, M, b, T, S, do_sample, n_layers)
+
+
+@pytest.mark.parametrize("world,M,lanes", [(4, 4, 1), (4, 8, 2), (8, 8, 1), (8, 16, 2)])
+def test_pipeline_world_4_8_matches_unsplit(world, M, lanes):
+    """The driver's 4- and 8-stage splits (8 layers: 2 or 1 per stage, head on the last),
+    sampled decode, through the P2POp exchange: tokens equal the unsplit model's."""
+    torch.set_num_threads(1)
+    _run_world(world, M, lanes, True)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_pipeline_world_4_8_headinfer_chunked_prefill(world):
+    """BASELINE config 4 rehearsal: every stage offloads 1 of 2 KV heads, prefill runs in
+    3-token chunks across the stages; tokens equal the unsplit, fully resident model's."""
+    torch.set_num_threads(1)
+    _run_world(world, world, 1, True, headinfer_heads=1, T=7, prefill_chunk=3)
+
+
+def test_pipeline_headinfer_rejects_lanes():
+    cfg = tiny("llama", num_layers=2)
+    model = build_model(cfg, dtype=torch.float32, seed=7)
+    from edgellm.parallel.pipeline import PipelineStage
+    with pytest.raises(AssertionError, match="one stream"):
+        PipelineStage(model, 0, 1, 1, 2, max_seq=16, headinfer_heads=1, lanes=2)
 
 
 def test_pipeline_with_headinfer_offload_matches_unsplit():
