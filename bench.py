@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--lanes", type=int, default=2,
                     help="micro-batches each GPU decodes concurrently on separate HIP streams (own graphs/pools)")
+    ap.add_argument("--kv-dtype", default="int8", choices=["bf16", "int8"],
+                    help="KV cache: int8 with per-(token, head) scales (default; halves the attention bytes) or bf16")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
@@ -117,9 +119,11 @@ def run_single(args):
     L = max(1, args.lanes)
     if L > 1:
         assert kv is None, "HeadInfer offload runs one lane"
-        gen = LaneGenerator(model, lanes=L, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs)
+        gen = LaneGenerator(model, lanes=L, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs,
+                            kv_dtype=kv_dtype(args, cfg))
     else:
-        gen = Generator(model, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs, kv=kv)
+        gen = Generator(model, max_batch=B, max_seq=max_seq, use_graphs=not args.no_graphs, kv=kv,
+                        kv_dtype=kv_dtype(args, cfg))
     g = torch.Generator().manual_seed(args.seed)
     prompts = torch.randint(0, cfg.vocab_size, (B * L, args.prompt_len), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=total_new, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
@@ -157,13 +161,21 @@ def run_single(args):
                 kv_host_gb=(kv.host_bytes() / 1e9 if kv is not None else 0.0))
 
 
+def kv_dtype(args, cfg) -> str:
+    """The requested KV-cache dtype where the model and mode support it (int8 needs head_dim
+    64 / 128 / 256 and no HeadInfer offload)."""
+    if args.kv_dtype == "int8" and cfg.head_dim in (64, 128, 256) and args.headinfer_heads is None:
+        return "int8"
+    return "bf16"
+
+
 @torch.no_grad()
 def batch1_p50(model, cfg, args, device, steps: int) -> dict:
     """Batch-1 decode latency of ``model`` (graph-captured, same sampling config): p50 / p90 of
     per-token device-event intervals over ``steps`` tokens after a warm-up."""
     W = max(4, args.warmup)
     max_seq = args.prompt_len + W + steps + 16
-    gen = Generator(model, max_batch=1, max_seq=max_seq, use_graphs=not args.no_graphs)
+    gen = Generator(model, max_batch=1, max_seq=max_seq, use_graphs=not args.no_graphs, kv_dtype=kv_dtype(args, cfg))
     g = torch.Generator().manual_seed(args.seed + 1)
     prompt = torch.randint(0, cfg.vocab_size, (1, args.prompt_len), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=W + steps + 2, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
@@ -212,7 +224,7 @@ def gen_kv_bytes(gen) -> int:
 
 def run_pipeline(args):
     from edgellm.parallel.bench_pipeline import run_pipeline_bench
-    return run_pipeline_bench(args, build, model_config)
+    return run_pipeline_bench(args, build, model_config, kv_dtype)
 
 
 def main(argv=None):
@@ -252,7 +264,10 @@ def main(argv=None):
                    "lanes": max(1, args.lanes), "partition": res.get("partition"),
                    "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1",
                    "headinfer_heads": args.headinfer_heads,
-                   "compute": "W8A8 INT8 MFMA GEMMs, bf16 attention/norms, bf16 LM head"},
+                   "kv_cache": ("int8, one fp32 scale per (token, head)" if kv_dtype(args, model_config(args)) == "int8"
+                                else "bf16"),
+                   "compute": ("W8A8 INT8 MFMA GEMMs, bf16 norms / softmax, bf16 LM head" if args.quant != "none"
+                               else "bf16 GEMMs / attention / norms")},
         "p50_token_latency_ms": round(res["p50"], 4),
         "p90_token_latency_ms": round(res.get("p90", res["p50"]), 4),
         "max_token_latency_ms": round(res.get("lat_max", res["p50"]), 4),

@@ -98,7 +98,8 @@ class _DecodeState:
 class Generator:
     def __init__(self, model: DecoderLM, max_batch: int = 1, max_seq: Optional[int] = None,
                  use_graphs: Optional[bool] = None, eos_check_every: int = 8, kv: Optional[KVCache] = None,
-                 prefill_chunk: Optional[int] = None):
+                 prefill_chunk: Optional[int] = None, kv_dtype: str = "bf16"):
+        """``kv_dtype``: "bf16" or "int8" (per-(token, head) scaled int8 KV cache, engine.kv_cache)."""
         assert model.has_embed and model.has_head, "Generator needs a full model (use parallel.pipeline for stages)"
         self.model = model
         self.cfg = model.cfg
@@ -106,7 +107,7 @@ class Generator:
         max_seq = min(max_seq or self.cfg.max_position_embeddings, self.cfg.max_position_embeddings)
         self.max_seq = max_seq
         self.kv = kv if kv is not None else KVCache(self.cfg, max_batch, max_seq, device=self.device,
-                                                    dtype=model.dtype)
+                                                    dtype=model.dtype, kv_dtype=kv_dtype)
         self.rope = model.rope_table(self.device)
         # HeadInfer (edgellm.offload) caches carry an attention hook and a prefill chunk size
         self.attn_hook = getattr(self.kv, "attn_hook", None)

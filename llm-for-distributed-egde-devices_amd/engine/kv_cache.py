@@ -7,6 +7,11 @@ one contiguous ``S*D`` run, so
   * a micro-batch / request slot is a contiguous slice along B (``rows``).
 Sized up front (no per-token ``torch.cat`` as in HF DynamicCache): with 288 GB of
 HBM a Llama-2-7B bf16 cache of 64 sequences x 4096 tokens (128 GB) still fits beside the weights.
+
+``kv_dtype="int8"``: k / v are int8 with one fp32 scale per (token, head) (``ks`` / ``vs``
+[L, B, Hkv, S]); decode attention reads D + 4 bytes per row instead of 2 D (1.94x fewer at
+D = 128) and the quantising append is fused into the decode attention kernel
+(ops/csrc/attn_decode_i8.hip).  Needs head_dim 64 / 128 / 256.
 """
 from __future__ import annotations
 
@@ -20,15 +25,25 @@ from ..models.configs import ModelConfig
 class KVCache:
     def __init__(self, cfg: ModelConfig, max_batch: int, max_seq: int, first_layer: int = 0,
                  last_layer: Optional[int] = None, dtype=torch.bfloat16, device=None,
-                 num_kv_heads: Optional[int] = None):
+                 num_kv_heads: Optional[int] = None, kv_dtype: str = "bf16"):
+        assert kv_dtype in ("bf16", "int8"), kv_dtype
         self.cfg = cfg
         self.first = first_layer
         self.last = cfg.num_layers if last_layer is None else last_layer
         self.max_batch, self.max_seq = max_batch, max_seq
         hk = cfg.num_kv_heads if num_kv_heads is None else num_kv_heads
         shape = (self.last - self.first, max_batch, hk, max_seq, cfg.head_dim)
-        self.k = torch.zeros(shape, dtype=dtype, device=device)
-        self.v = torch.zeros(shape, dtype=dtype, device=device)
+        self.quantized = kv_dtype == "int8"
+        self.kv_dtype = kv_dtype
+        if self.quantized:
+            assert cfg.head_dim in (64, 128, 256), "int8 KV cache needs head_dim 64 / 128 / 256"
+            self.k = torch.zeros(shape, dtype=torch.int8, device=device)
+            self.v = torch.zeros(shape, dtype=torch.int8, device=device)
+            self.ks = torch.zeros(shape[:-1], dtype=torch.float32, device=device)
+            self.vs = torch.zeros(shape[:-1], dtype=torch.float32, device=device)
+        else:
+            self.k = torch.zeros(shape, dtype=dtype, device=device)
+            self.v = torch.zeros(shape, dtype=dtype, device=device)
 
     @staticmethod
     def bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2) -> int:
@@ -37,11 +52,17 @@ class KVCache:
     def layer(self, i: int):
         return self.k[i - self.first], self.v[i - self.first]
 
+    def layer_scales(self, i: int):
+        return self.ks[i - self.first], self.vs[i - self.first]
+
     def rows(self, r0: int, r1: int) -> "KVView":
         return KVView(self, r0, r1)
 
     def nbytes(self) -> int:
-        return self.k.numel() * self.k.element_size() * 2
+        n = self.k.numel() * self.k.element_size() * 2
+        if self.quantized:
+            n += self.ks.numel() * 4 * 2
+        return n
 
 
 class KVView:
@@ -49,7 +70,12 @@ class KVView:
 
     def __init__(self, cache: KVCache, r0: int, r1: int):
         self.cache, self.r0, self.r1 = cache, r0, r1
+        self.quantized = getattr(cache, "quantized", False)
 
     def layer(self, i: int):
         k, v = self.cache.layer(i)
         return k[self.r0:self.r1], v[self.r0:self.r1]
+
+    def layer_scales(self, i: int):
+        ks, vs = self.cache.layer_scales(i)
+        return ks[self.r0:self.r1], vs[self.r0:self.r1]

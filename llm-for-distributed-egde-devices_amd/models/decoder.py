@@ -73,6 +73,8 @@ class Attention(nn.Module):
         rot = cfg.rotary_dim if cfg.pos_emb == "rope" else 0
         if ctx.attn_hook is not None:
             attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
+        elif getattr(ctx.kv, "quantized", False):
+            return self._forward_kv8(qkv, ctx, k_cache, v_cache, rot)
         elif ctx.mode == "decode":
             # one launch: RoPE + KV append + attention (+ per-group int8 output for a W8A8 o-proj)
             # per-(token, 64) int8 output feeds the decode GEMV (<= 64 rows, <= 128 for the shapes
@@ -89,6 +91,38 @@ class Attention(nn.Module):
             q = ops.rope_kv_write(qkv, ctx.start_pos, ctx.rope if rot else None, k_cache, v_cache,
                                   cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, rot)  # [B,T,Hq,D]
             attn = ops.prefill_attention(q, k_cache, v_cache, ctx.start_pos, self.scale, ctx.causal)
+        attn = attn.reshape(ctx.B * ctx.T, cfg.q_size)
+        return self.o(quant_if(attn, self.o))
+
+
+    def _forward_kv8(self, qkv, ctx: AttnCtx, k_cache, v_cache, rot: int):
+        """int8 KV cache (engine.kv_cache, kv_dtype="int8").  Decode: one launch for RoPE +
+        quantising append + attention over the int8 cache.  Prefill: RoPE writes the rotated bf16
+        k / v of the new tokens (plus the dequantised history when start > 0) into a scratch the
+        prefill attention reads, and the new rows are quantised into the cache."""
+        cfg = self.cfg
+        ks, vs = ctx.kv.layer_scales(self.layer_idx)
+        if ctx.mode == "decode":
+            quant = self.o.takes_quantized_input and getattr(self.o, "group_scales_ok", lambda m: m <= 64)(ctx.B)
+            out, s = ops.decode_attention_fused_i8(qkv.view(ctx.B, -1), ctx.start_pos, ctx.rope if rot else None,
+                                                   k_cache, v_cache, ks, vs, ctx.seq_lens, cfg.num_heads, self.scale,
+                                                   ctx.max_len, rot, quant)
+            if quant:
+                return self.o(QAct(out, s))
+            attn = out
+        else:
+            B, T, S = ctx.B, ctx.T, ctx.max_len
+            hist = S - T                                  # host bound of the cached prefix
+            kb = torch.empty(B, cfg.num_kv_heads, S, cfg.head_dim, dtype=qkv.dtype, device=qkv.device)
+            vb = torch.empty_like(kb)
+            if hist > 0:
+                kb[:, :, :hist] = ops._ref.dequant_kv(k_cache[:, :, :hist], ks[:, :, :hist]).to(kb.dtype)
+                vb[:, :, :hist] = ops._ref.dequant_kv(v_cache[:, :, :hist], vs[:, :, :hist]).to(vb.dtype)
+            q = ops.rope_kv_write(qkv, ctx.start_pos, ctx.rope if rot else None, kb, vb, cfg.num_heads,
+                                  cfg.num_kv_heads, cfg.head_dim, rot)
+            ops.kv_quant_append(kb, ctx.start_pos, T, k_cache, ks)
+            ops.kv_quant_append(vb, ctx.start_pos, T, v_cache, vs)
+            attn = ops.prefill_attention(q, kb, vb, ctx.start_pos, self.scale, ctx.causal)
         attn = attn.reshape(ctx.B * ctx.T, cfg.q_size)
         return self.o(quant_if(attn, self.o))
 

@@ -187,6 +187,37 @@ def decode_attention_fused(qkv, start_pos, rope, k_cache, v_cache, seq_lens, num
     return out, None
 
 
+def decode_attention_fused_i8(qkv, start_pos, rope, k_cache, v_cache, k_scale, v_scale, seq_lens, num_heads: int,
+                              scale: float, max_len_hint: int, rotary_dim: int, quant_out: bool = False):
+    """``decode_attention_fused`` over an int8 KV cache (int8 [B, Hkv, S, D] + fp32 scales
+    [B, Hkv, S]): the new token is quantised per (token, head) in the same launch
+    (ops/csrc/attn_decode_i8.hip)."""
+    Hkv, D = k_cache.shape[1], k_cache.shape[3]
+    if _gpu(qkv):
+        return ext().decode_attn_i8(qkv, start_pos, rope if rotary_dim else None, k_cache, v_cache, k_scale, v_scale,
+                                    seq_lens, num_heads, scale, int(max_len_hint), rotary_dim, quant_out)
+    q = _ref.rope_kv_write_i8(qkv, start_pos, rope if rotary_dim else None, k_cache, v_cache, k_scale, v_scale,
+                              num_heads, Hkv, D, rotary_dim)
+    S = int(seq_lens.max().item())
+    kf = _ref.dequant_kv(k_cache[:, :, :S], k_scale[:, :, :S])
+    vf = _ref.dequant_kv(v_cache[:, :, :S], v_scale[:, :, :S])
+    out = _ref.decode_attention(q.view(qkv.shape[0], num_heads, D).float(), kf, vf, seq_lens, scale).to(qkv.dtype)
+    if quant_out:
+        return _ref.quant_per_group(out.reshape(qkv.shape[0], num_heads * D))
+    return out, None
+
+
+def kv_quant_append(src, start_pos, T: int, cache, scales):
+    """Quantise bf16 rows ``src[b, h, start_pos[b] + t]`` (t < T) into an int8 cache + scales."""
+    if _gpu(src):
+        return ext().kv_quant_append(src, start_pos, int(T), cache, scales)
+    for b in range(src.shape[0]):
+        p0 = int(start_pos[b])
+        q, s = _ref.quant_kv_rows(src[b, :, p0:p0 + T])
+        cache[b, :, p0:p0 + T] = q
+        scales[b, :, p0:p0 + T] = s
+
+
 def prefill_attention(q, k_cache, v_cache, start_pos, scale, causal=True):
     if _gpu(q):
         return ext().prefill_attn(q, k_cache, v_cache, start_pos, scale, causal)

@@ -194,6 +194,47 @@ def rope_kv_write(qkv: torch.Tensor, start_pos: torch.Tensor, rope: Optional[tor
     return q.to(qkv.dtype)
 
 
+def quant_kv_rows(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """int8 KV cache rows: per-(token, head) symmetric quantisation over the last dim
+    (ops/csrc/attn_decode_i8.hip::quant_row16): q = rint(x * 127 / amax), scale = amax / 127."""
+    x = x.float()
+    amax = x.abs().amax(-1).clamp_min(1e-8)
+    q = torch.round(x * (127.0 / amax)[..., None]).clamp(-127, 127).to(torch.int8)
+    return q, amax / 127.0
+
+
+def dequant_kv(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    return q.float() * s[..., None]
+
+
+def rope_kv_write_i8(qkv: torch.Tensor, start_pos: torch.Tensor, rope: Optional[torch.Tensor],
+                     k_cache: torch.Tensor, v_cache: torch.Tensor, k_scale: torch.Tensor, v_scale: torch.Tensor,
+                     num_heads: int, num_kv_heads: int, head_dim: int, rotary_dim: int) -> torch.Tensor:
+    """rope_kv_write into an int8 cache: the rotated k / v rows (rounded to the activation dtype,
+    as the bf16 cache stores them) are quantised per (token, head); returns q [B, T, Hq, D]."""
+    B = k_cache.shape[0]
+    T = qkv.shape[0] // B
+    hq, hk, d = num_heads, num_kv_heads, head_dim
+    x = qkv.view(B, T, -1).float()
+    q = x[..., :hq * d].view(B, T, hq, d)
+    k = x[..., hq * d:(hq + hk) * d].view(B, T, hk, d)
+    v = x[..., (hq + hk) * d:].view(B, T, hk, d)
+    pos = start_pos.long()[:, None] + torch.arange(T, device=qkv.device)[None]
+    if rope is not None and rotary_dim > 0:
+        cs = rope[pos][:, :, None]
+        q = _rotate(q, cs, rotary_dim)
+        k = _rotate(k, cs, rotary_dim)
+    kq, ks = quant_kv_rows(k.to(qkv.dtype))
+    vq, vs = quant_kv_rows(v.to(qkv.dtype))
+    for b in range(B):
+        p = pos[b]
+        k_cache[b, :, p] = kq[b].transpose(0, 1)
+        v_cache[b, :, p] = vq[b].transpose(0, 1)
+        k_scale[b, :, p] = ks[b].transpose(0, 1)
+        v_scale[b, :, p] = vs[b].transpose(0, 1)
+    return q.to(qkv.dtype)
+
+
 # --------------------------------------------------------------------------- attention (K5, K6)
 
 

@@ -53,6 +53,15 @@ int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int*
                          const float* scb, int M, int N, int cmax, hipStream_t st);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_decode_attn_config(int target_wg);
+int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, void* vc, float* ks, float* vs, int64_t c_sb,
+                        int64_t c_sh, int64_t s_sb, int64_t s_sh, const int* seq_lens, int B, int Hq, int Hkv, int D,
+                        float scale, int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
+                        const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
+                        hipStream_t st);
+int edge_decode_attn_i8_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out);
+int edge_kv_quant_append(const void* src, int64_t x_sb, int64_t x_sh, const int* start_pos, void* dst, int64_t c_sb,
+                         int64_t c_sh, float* sc, int64_t s_sb, int64_t s_sh, int B, int Hkv, int T, int D, int S,
+                         hipStream_t st);
 void edge_decode_attn_occ(int occ);
 }
 
@@ -325,6 +334,82 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_fused(
   return {out, std::nullopt};
 }
 
+// ---------------------------------------------------------------------------- int8 KV cache
+void check_cache8(const at::Tensor& c, const at::Tensor& s, const char* name, int64_t D) {
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kChar, name, " must be an int8 GPU tensor");
+  TORCH_CHECK(c.dim() == 4 && c.size(3) == D && c.stride(3) == 1 && c.stride(2) == D,
+              name, " must be [B, Hkv, S, D] with contiguous rows");
+  TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kFloat && s.dim() == 3 && s.stride(2) == 1 &&
+                  s.size(0) == c.size(0) && s.size(1) == c.size(1) && s.size(2) == c.size(2),
+              name, " scales must be fp32 [B, Hkv, S]");
+}
+
+std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_i8(
+    const at::Tensor& qkv, const at::Tensor& start_pos, const std::optional<at::Tensor>& rope, at::Tensor& k_cache,
+    at::Tensor& v_cache, at::Tensor& k_scale, at::Tensor& v_scale, const at::Tensor& seq_lens, int64_t Hq,
+    double scale, int64_t max_len_hint, int64_t rot, bool quant_out) {
+  need(qkv, at::kBFloat16, "qkv");
+  TORCH_CHECK(qkv.dim() == 2, "qkv must be [B, (Hq + 2 Hkv) * D]");
+  const int64_t B = qkv.size(0), D = k_cache.size(3), Hkv = k_cache.size(1);
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width does not match the cache geometry");
+  TORCH_CHECK(D == 64 || D == 128 || D == 256, "int8 KV cache needs head_dim 64 / 128 / 256");
+  check_cache8(k_cache, k_scale, "k_cache", D);
+  check_cache8(v_cache, v_scale, "v_cache", D);
+  TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_scale.strides() == v_scale.strides() && k_cache.size(0) == B);
+  need(start_pos, at::kInt, "start_pos");
+  need(seq_lens, at::kInt, "seq_lens");
+  TORCH_CHECK(start_pos.numel() == B && seq_lens.numel() == B);
+  TORCH_CHECK(max_len_hint > 0 && max_len_hint <= k_cache.size(2), "max_len_hint out of range");
+  const float* cs = nullptr;
+  if (rot > 0) {
+    TORCH_CHECK(rope.has_value(), "rope table required for rot > 0");
+    need(*rope, at::kFloat, "rope");
+    TORCH_CHECK(rope->size(-2) * 2 == rot, "rope table width must be rot/2");
+    cs = rope->data_ptr<float>();
+  }
+  int ch = 0, nsplit = 0;
+  edge_decode_attn_i8_plan((int)B, (int)Hkv, (int)max_len_hint, (int)D, &ch, &nsplit);
+  at::Tensor pacc, pml, out, oq;
+  std::optional<at::Tensor> os;
+  if (nsplit > 1) {
+    pacc = at::empty({B, Hq, nsplit, D}, qkv.options().dtype(at::kFloat));
+    pml = at::empty({B, Hq, nsplit, 2}, qkv.options().dtype(at::kFloat));
+  }
+  const int64_t Mpad = (B + 15) / 16 * 16;
+  if (quant_out) {
+    oq = at::empty({B, Hq * D}, qkv.options().dtype(at::kChar));
+    os = at::empty({Hq * D / 64, Mpad}, qkv.options().dtype(at::kFloat));
+  } else {
+    out = at::empty({B, Hq, D}, qkv.options());
+  }
+  check(edge_decode_attn_i8(qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                            k_scale.data_ptr<float>(), v_scale.data_ptr<float>(), k_cache.stride(0), k_cache.stride(1),
+                            k_scale.stride(0), k_scale.stride(1), seq_lens.data_ptr<int>(), (int)B, (int)Hq, (int)Hkv,
+                            (int)D, (float)scale, ch, nsplit, quant_out ? nullptr : out.data_ptr(),
+                            quant_out ? 0 : out.stride(0), nsplit > 1 ? pacc.data_ptr<float>() : nullptr,
+                            nsplit > 1 ? pml.data_ptr<float>() : nullptr, start_pos.data_ptr<int>(), cs, (int)rot,
+                            quant_out ? oq.data_ptr() : nullptr, quant_out ? os->data_ptr<float>() : nullptr,
+                            (int)Mpad, stream()),
+        "decode_attn_i8");
+  if (quant_out) return {oq, os};
+  return {out, std::nullopt};
+}
+
+// src: bf16 [B, Hkv, >= start + T, D] rows (rotated k or v); writes rows [start_pos[b], +T) quantised
+void kv_quant_append(const at::Tensor& src, const at::Tensor& start_pos, int64_t T, at::Tensor& cache,
+                     at::Tensor& scales) {
+  const int64_t D = cache.size(3), B = cache.size(0), Hkv = cache.size(1);
+  check_cache(src, "src", D);
+  check_cache8(cache, scales, "cache", D);
+  TORCH_CHECK(src.size(0) == B && src.size(1) == Hkv, "src geometry");
+  need(start_pos, at::kInt, "start_pos");
+  TORCH_CHECK(start_pos.numel() == B);
+  check(edge_kv_quant_append(src.data_ptr(), src.stride(0), src.stride(1), start_pos.data_ptr<int>(), cache.data_ptr(),
+                             cache.stride(0), cache.stride(1), scales.data_ptr<float>(), scales.stride(0),
+                             scales.stride(1), (int)B, (int)Hkv, (int)T, (int)D, (int)cache.size(2), stream()),
+        "kv_quant_append");
+}
+
 at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& start_pos, double scale, bool causal) {
   need(q, at::kBFloat16, "q");
@@ -591,6 +676,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");
   m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]");
   m.def("decode_attn_fused", &decode_attn_fused);
+  m.def("decode_attn_i8", &decode_attn_i8, "decode attention over an int8 KV cache, fused RoPE + quantising append");
+  m.def("kv_quant_append", &kv_quant_append, "quantise bf16 K/V rows into an int8 KV cache (prefill append)");
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
   m.def("w8a8_gemm_splitk", &w8a8_gemm_splitk);
   m.def("rms_norm_parts", &rms_norm_parts);

@@ -38,8 +38,9 @@ def _abort_rank(msg: str):
     os._exit(124)
 
 
-def run_pipeline_bench(args, build, model_config):
-    """``build(args, device, first, last) -> (cfg, stage_model)``; ``model_config(args) -> cfg``."""
+def run_pipeline_bench(args, build, model_config, kv_dtype=None):
+    """``build(args, device, first, last) -> (cfg, stage_model)``; ``model_config(args) -> cfg``;
+    ``kv_dtype(args, cfg) -> "bf16" | "int8"`` picks the KV-cache dtype (bf16 when absent)."""
     use_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
     wd = Watchdog(timeout_s=float(os.environ.get("EDGELLM_WATCHDOG_S", "300")), on_timeout=_abort_rank,
                   name="bench_pipeline").start()
@@ -71,7 +72,8 @@ def run_pipeline_bench(args, build, model_config):
     wd.beat("stage init (communicator warm-up)")
     # the stage's constructor joins every rank in one collective (eager RCCL communicator)
     stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs,
-                          headinfer_heads=getattr(args, "headinfer_heads", None), lanes=L)
+                          headinfer_heads=getattr(args, "headinfer_heads", None), lanes=L,
+                          kv_dtype=kv_dtype(args, cfg) if kv_dtype is not None else "bf16")
     if use_cuda:
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats(device)

@@ -55,7 +55,7 @@ class PipelineResult:
 class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
                  group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None,
-                 lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True):
+                 lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True, kv_dtype: str = "bf16"):
         """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
         to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
         HeadInfer").  The offloaded path is host-orchestrated on one compute stream, so it runs one
@@ -78,8 +78,9 @@ class PipelineStage:
         self.next = (rank + 1) % world
         self.h_on = headinfer_heads if offload else None
         self.prefill_chunk = max(1, prefill_chunk)
+        assert not offload or kv_dtype == "bf16", "HeadInfer offload keeps a bf16 KV cache"
         self.kv = None if offload else KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last,
-                                               model.dtype, self.device)
+                                               model.dtype, self.device, kv_dtype=kv_dtype)
         self.attn_hook = None
         self.rope = model.rope_table(self.device)
         cuda = self.device.type == "cuda"
@@ -176,7 +177,7 @@ class PipelineStage:
             x_ids = ids[:, c0:c1] if ids is not None else None
             x_h = None
             if hidden is not None:
-                x_h = hidden.view(b, T, H)[:, c0:c1].reshape(b * (c1 - c0), H) if C < T else hidden
+                x_h = hidden.view(b, T, H)[:, c0:c1].contiguous().view(b * (c1 - c0), H) if C < T else hidden
             out = self.model(x_ids, ctx, hidden=x_h, logits="last")
             if not self.is_last and C < T:
                 outs.append(out.view(b, c1 - c0, H))

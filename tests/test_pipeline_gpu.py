@@ -42,56 +42,76 @@ def _sampling(S, do_sample):
                           repetition_penalty=1.1)
 
 
-def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q, lanes=1):
+def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q, lanes=1, headinfer_heads=None,
+            prefill_chunk=4096):
     import edgellm  # noqa: F401
     from edgellm.parallel.pipeline import PipelineStage
+    from datetime import timedelta
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rank that dies must not leave its peer blocked in a gloo recv for gloo's 30-min default
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
     torch.cuda.set_device(0)
     cfg = tiny(arch, num_layers=4)
     bounds = partition_model(cfg, world, "uniform")
     _, model = _model(arch, quant, bounds[rank], bounds[rank + 1])
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
-    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, lanes=lanes)
+    st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, lanes=lanes, headinfer_heads=headinfer_heads,
+                       prefill_chunk=prefill_chunk)
     assert st.host_staged and st.use_graphs
-    res = st.run(prompts if rank == 0 else None, T, _sampling(S, do_sample), S, seed=5)
+    n_ticks = (M + S * M) // lanes + world - 1
+    res = st.run(prompts if rank == 0 else None, T, _sampling(S, do_sample), S, seed=5,
+                 stats_window=(M // lanes + world - 1, n_ticks))
+    assert res.stats["compute_ms_per_tick"] > 0 and 0 <= res.stats["bubble_frac"] <= 1
     if res.tokens is not None:
         q.put(res.tokens)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _reference(arch, quant, M, b, T, S, do_sample):
+def _reference(arch, quant, M, b, T, S, do_sample, prefill_chunk=None):
     cfg, model = _model(arch, quant)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
     out = []
-    gen = Generator(model, max_batch=b, max_seq=T + S + 4)
+    gen = Generator(model, max_batch=b, max_seq=T + S + 4, prefill_chunk=prefill_chunk)
     for m in range(M):
         out.extend(gen.generate(prompts[m].tolist(), _sampling(S, do_sample), seed=(5 + 7919 * m) & 0x7FFFFFFF).tokens)
     return out
 
 
-@pytest.mark.parametrize("quant,lanes", [("none", 1), ("w8a8", 1), ("w8a8", 2)])
+@pytest.mark.parametrize("quant,lanes,world", [("none", 1, 2), ("w8a8", 1, 2), ("w8a8", 2, 2), ("w8a8", 2, 4)])
 @pytest.mark.parametrize("do_sample", [False, True])
-def test_pipeline_gpu_matches_unsplit(cuda, quant, lanes, do_sample):
-    """lanes = 2: two micro-batches per tick on two HIP streams (own graph pools) per stage."""
-    arch, world, b, T, S = "llama", 2, 4, 9, 12
+def test_pipeline_gpu_matches_unsplit(cuda, quant, lanes, world, do_sample):
+    """lanes = 2: two micro-batches per tick on two HIP streams (own graph pools) per stage;
+    world 4: one layer per stage, the driver's 4-way split shape."""
+    _run(quant, lanes, world, do_sample)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_pipeline_gpu_headinfer_chunked(cuda, world):
+    """Pipeline + HeadInfer on the device: 1 of 2 KV heads per layer offloaded to pinned host
+    memory, prefill in 4-token chunks; tokens equal the resident unsplit model's."""
+    _run("w8a8", 1, world, True, headinfer_heads=1, prefill_chunk=4)
+
+
+def _run(quant, lanes, world, do_sample, headinfer_heads=None, prefill_chunk=4096):
+    arch, b, T, S = "llama", 4, 9, 12
     M = world * lanes
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, quant, M, b, T, S, do_sample, q, lanes))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, arch, quant, M, b, T, S, do_sample, q, lanes,
+                                               headinfer_heads, prefill_chunk))
              for r in range(world)]
     for p in procs:
         p.start()
     try:
-        got = q.get(timeout=300)
+        got = q.get(timeout=150)
     finally:
         for p in procs:
             p.join(timeout=120)
             if p.exitcode is None:
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
-    assert got == _reference(arch, quant, M, b, T, S, do_sample)
+    assert got == _reference(arch, quant, M, b, T, S, do_sample, prefill_chunk if headinfer_heads else None)
