@@ -57,8 +57,8 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--lanes", type=int, default=2,
                     help="micro-batches each GPU decodes concurrently on separate HIP streams (own graphs/pools)")
-    ap.add_argument("--kv-dtype", default="int8", choices=["bf16", "int8"],
-                    help="KV cache: int8 with per-(token, head) scales (default; halves the attention bytes) or bf16")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"],
+                    help="KV cache: bf16 (default) or int8 with per-(token, head) scales (half the KV bytes: 1.6x faster attention at >= 512 keys, neutral at the 128-token bench context)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")

@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import sys
+import time
 from typing import List, Optional
 
 import torch
@@ -22,11 +23,12 @@ import torch
 from ..config import add_reference_args, apply_overrides, load_config, RunConfig
 from ..data import load_qa
 from ..engine import Generator, SamplingParams
-from ..eval import Embedder, MetricSuite, ProgressLog, Results
+from ..eval import EfficiencyMeter, Embedder, MetricSuite, ProgressLog, Results
 from ..models.registry import load_model
 from ..orchestrator import Agent, Orchestrator, RefineMerge, VoteMerge
-from ..utils.log import format_final_report, get_logger
-from .common import add_runtime_args, pick_devices, pop_runtime
+from ..parallel.split import agent_devices, split_model
+from ..utils.log import format_efficiency_report, format_final_report, get_logger
+from .common import add_runtime_args, build_generator, pick_devices, pop_runtime, resolve_runtime
 
 logger = get_logger("combine")
 
@@ -47,14 +49,24 @@ def build_embedder(name: Optional[str], base_dir: Optional[str], device) -> Embe
 
 
 def make_agent(name: str, model_id: str, precision: str, quant: str, device, sampling: SamplingParams, rt: dict,
-               cpu_prompt: bool = False) -> Agent:
-    model, tok, source = load_model(model_id, precision, quant, device, rt.get("base_model_path"))
-    logger.info(f"{name}: {source} on {device} ({quant})")
-    gen = Generator(model, max_batch=1, max_seq=rt.get("max_seq", 2048))
+               cpu_prompt: bool = False, gpus=None) -> Agent:
+    """One agent: the model on ``device``, or split layer-wise over its GPU group (``gpus``, the
+    YAML ``agents[].gpus``; else ``pp_size`` devices from ``device``) — the reference's
+    ``device_map="auto"`` placement (combine_model_fp_updated.py:40)."""
+    devs = agent_devices(gpus, torch.device(device), int(rt.get("pp_size") or 1))
+    model, tok, source = load_model(model_id, precision, quant, devs[0], rt.get("base_model_path"))
+    if len(devs) > 1:
+        model = split_model(model, devs)
+        logger.info(f"{name}: {source} split over {[str(d) for d in devs]} at layers {model.bounds} ({quant})")
+    else:
+        logger.info(f"{name}: {source} on {devs[0]} ({quant})")
+    gen = build_generator(model, rt, max_batch=int(rt.get("batch_size") or 1))
     return Agent(name, gen, tok, sampling, cpu_prompt)
 
 
 def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: bool = False) -> dict:
+    """qa_specs: (name, model, precision[, quant[, gpus]]) per QA agent."""
+    rt = resolve_runtime(cfg, rt)
     quant = rt.get("quant") or cfg.quant.mode
     devices = pick_devices(rt.get("devices"))
     s = cfg.sampling
@@ -62,8 +74,12 @@ def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: 
     logger.info("Loading dataset...")
     rows = load_qa(cfg.dataset_name, cfg.dataset_split, cfg.dataset_path, rt.get("num_samples"))
     logger.info("Loading models...")
-    agents = [make_agent(n, mid, prec, quant, devices[i % len(devices)], sampling, rt, cpu_variant)
-              for i, (n, mid, prec) in enumerate(qa_specs)]
+    agents = []
+    for i, spec in enumerate(qa_specs):
+        n, mid, prec = spec[:3]
+        aq = spec[3] if len(spec) > 3 and spec[3] not in (None, "none") else quant
+        gpus = spec[4] if len(spec) > 4 else None
+        agents.append(make_agent(n, mid, prec, aq, devices[i % len(devices)], sampling, rt, cpu_variant, gpus))
     merge_kind = rt.get("merge") or cfg.merge
     refiner = None
     if merge_kind == "refine" or refiner_spec is not None:
@@ -83,31 +99,45 @@ def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: 
     progress = ProgressLog(rt.get("progress"))
     done = progress.done()
     results = Results()
-    logger.info("Starting evaluation loop...")
-    for i, sample in enumerate(rows):
-        if i in done:
-            results.add({k: done[i][k] for k in done[i] if k not in ("index",)})
-            continue
-        q, ref = sample["query"], sample["answer"]
-        logger.info(f"Processing question: {q}")
-        res = orch.answer(q, ref, seed=rt.get("seed", 0) + i)
-        for name, ans in res.answers.items():
-            logger.info(f"Answer from {name}: {ans[:100]}...")
+    eff = EfficiencyMeter([a.device for a in agents] + ([refiner.device] if refiner else []))
+    bs = max(1, int(rt.get("batch_size") or 1))
+    logger.info("Starting evaluation loop..." + (f" ({bs} questions per batch)" if bs > 1 else ""))
+    todo = [i for i in range(len(rows)) if i not in done]
+    for i in done:
+        results.add({k: done[i][k] for k in done[i] if k not in ("index",)})
+    for j0 in range(0, len(todo), bs):
+        idx = todo[j0:j0 + bs]
+        qs, refs = [rows[i]["query"] for i in idx], [rows[i]["answer"] for i in idx]
+        for q in qs:
+            logger.info(f"Processing question: {q}")
+        t0 = time.perf_counter()
+        if bs == 1:
+            outs = [orch.answer(qs[0], refs[0], seed=rt.get("seed", 0) + idx[0])]
+        else:
+            outs = orch.answer_batch(qs, refs, seed=rt.get("seed", 0) + idx[0])
+        for i, q, ref, res in zip(idx, qs, refs, outs):
+            for name, ans in res.answers.items():
+                logger.info(f"Answer from {name}: {ans[:100]}...")
+                if cpu_variant:
+                    logger.info(f"[Q{i + 1}] {name} TPS: {res.tps[name]:.2f} tokens/sec")
+            logger.info(f"Refined response: {res.final[:100]}...")
+            m = suite.score(res.final, ref, scorer.generator.model, scorer.tokenizer, tps=res.combo_tps)
+            if m["rouge1"] == 0.0 and m["tps"] == 0.0:
+                logger.error("Error in evaluation: metrics zeroed for this sample")
+            results.add(m)
+            progress.append(i, m)
+            if rt.get("metrics_jsonl"):
+                with open(rt["metrics_jsonl"], "a") as f:
+                    f.write(json.dumps({"index": i, **m, "agent_tps": res.tps, "wall_s": res.wall_s}) + "\n")
             if cpu_variant:
-                logger.info(f"[Q{i + 1}] {name} TPS: {res.tps[name]:.2f} tokens/sec")
-        logger.info(f"Refined response: {res.final[:100]}...")
-        m = suite.score(res.final, ref, scorer.generator.model, scorer.tokenizer, tps=res.combo_tps)
-        if m["rouge1"] == 0.0 and m["tps"] == 0.0:
-            logger.error("Error in evaluation: metrics zeroed for this sample")
-        results.add(m)
-        progress.append(i, m)
-        if rt.get("metrics_jsonl"):
-            with open(rt["metrics_jsonl"], "a") as f:
-                f.write(json.dumps({"index": i, **m, "agent_tps": res.tps, "wall_s": res.wall_s}) + "\n")
-        if cpu_variant:
-            logger.info(f"[Q{i + 1}] Total time: {res.wall_s:.2f} sec\n")
+                logger.info(f"[Q{i + 1}] Total time: {res.wall_s:.2f} sec\n")
+        # QA agents' generated tokens of this batch (each result holds every row of the batch)
+        eff.add(time.perf_counter() - t0, len(idx), sum(len(t) for g in outs[0].results.values() for t in g.tokens))
     means = results.means()
     for line in format_final_report(means):
+        logger.info(line)
+    means.update(eff.summary())
+    for line in format_efficiency_report(means):
         logger.info(line)
     return means
 
@@ -121,7 +151,7 @@ def main(argv: Optional[List[str]] = None) -> dict:
         sys.exit(1)
     cfg = apply_overrides(load_config(args.config), args)
     if cfg.agents:
-        qa = [(a.name, a.model, a.precision) for a in cfg.agents]
+        qa = [(a.name, a.model, a.precision, a.quant, a.gpus) for a in cfg.agents]
     else:  # the reference's three fixed roles (combine_model_fp_updated.py:174-176)
         qa = [("phi_model", cfg.phi_model or "microsoft/phi-2", "fp16"),
               ("pythia_model", cfg.pythia_model or "EleutherAI/pythia-1b", "fp16")]

@@ -24,7 +24,15 @@ def add_runtime_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
                    help="do not leak the gold answer into the refiner prompt")
     g.add_argument("--merge", default=None, choices=["refine", "vote"], help="ensemble merge (default refine)")
     g.add_argument("--serial", action="store_true", help="run agents one after another (reference behaviour)")
-    g.add_argument("--headinfer_heads", type=int, default=None, help="KV heads resident on GPU (HeadInfer)")
+    g.add_argument("--headinfer_heads", type=int, default=None,
+                   help="HeadInfer: KV heads per layer resident on the GPU, the rest in pinned host memory "
+                        "(default: YAML offload.gpu_kv_budget_heads when offload.headinfer is true)")
+    g.add_argument("--prefill_chunk", type=int, default=None, help="chunked prefill size (YAML offload.chunk_size)")
+    g.add_argument("--pp_size", type=int, default=None,
+                   help="split each model's layers over this many GPUs (YAML parallel.pp_size; agents[].gpus wins)")
+    g.add_argument("--batch_size", type=int, default=None,
+                   help="questions decoded together per agent (YAML parallel.microbatches; 1 = the reference)")
+    g.add_argument("--kv_dtype", default=None, choices=["bf16", "int8"], help="KV-cache dtype (default bf16)")
     g.add_argument("--metrics_jsonl", default=None, help="append structured per-sample metrics here")
     return p
 
@@ -40,5 +48,42 @@ def pick_devices(spec: str = None) -> List[torch.device]:
 def pop_runtime(args: argparse.Namespace) -> dict:
     """Remove runtime-only keys so the remaining namespace is the reference's flag set."""
     keys = ["quant", "precision", "devices", "num_samples", "seed", "max_seq", "progress", "base_model_path",
-            "no_legacy_decode", "no_reference_in_refiner", "merge", "serial", "headinfer_heads", "metrics_jsonl"]
+            "no_legacy_decode", "no_reference_in_refiner", "merge", "serial", "headinfer_heads", "metrics_jsonl",
+            "prefill_chunk", "pp_size", "batch_size", "kv_dtype"]
     return {k: args.__dict__.pop(k) for k in keys if k in args.__dict__}
+
+
+def resolve_runtime(cfg, rt: dict) -> dict:
+    """Fold the YAML sections the CLIs act on (``parallel``, ``offload``) into the runtime dict;
+    an explicit flag wins.  Returns rt with: pp_size, batch_size, headinfer_heads, prefill_chunk."""
+    rt = dict(rt)
+    if rt.get("pp_size") is None:
+        rt["pp_size"] = max(1, int(cfg.parallel.pp_size or 1))
+    if rt.get("batch_size") is None:
+        rt["batch_size"] = max(1, int(cfg.parallel.microbatches or 1))
+    if rt.get("headinfer_heads") is None and cfg.offload.headinfer:
+        rt["headinfer_heads"] = cfg.offload.gpu_kv_budget_heads if cfg.offload.gpu_kv_budget_heads is not None else 0
+    if rt.get("prefill_chunk") is None:
+        rt["prefill_chunk"] = cfg.offload.chunk_size
+    rt.setdefault("kv_dtype", None)
+    rt["kv_dtype"] = rt["kv_dtype"] or "bf16"
+    return rt
+
+
+def build_generator(model, rt: dict, max_batch: int = 1):
+    """The decode engine for one agent / model as the runtime options ask: HeadInfer KV offload
+    (``headinfer_heads``, chunked prefill), int8 KV cache, or the resident bf16 cache."""
+    from ..engine import Generator
+    max_seq = rt.get("max_seq", 2048)
+    h_on = rt.get("headinfer_heads")
+    if h_on is not None and h_on < model.cfg.num_kv_heads:
+        assert not hasattr(model, "make_kv"), "HeadInfer offload runs on a single-device model"
+        from ..offload import HeadInferKV
+        chunk = min(int(rt.get("prefill_chunk") or 4096), max_seq)
+        kv = HeadInferKV(model.cfg, max_batch, max_seq, int(h_on), model.device, chunk_size=chunk, dtype=model.dtype)
+        return Generator(model, max_batch=max_batch, max_seq=max_seq, kv=kv)
+    kvd = rt.get("kv_dtype") or "bf16"
+    if kvd == "int8" and model.cfg.head_dim not in (64, 128, 256):
+        kvd = "bf16"
+    return Generator(model, max_batch=max_batch, max_seq=max_seq, kv_dtype=kvd,
+                     prefill_chunk=rt.get("prefill_chunk") if h_on is not None else None)

@@ -13,42 +13,64 @@ from __future__ import annotations
 
 import argparse
 import os
+import time
 from typing import List, Optional
 
 from ..config import add_reference_args, apply_overrides, load_config
 from ..data import load_qa
-from ..engine import Generator, SamplingParams
-from ..eval import MetricSuite, Results
+from ..engine import SamplingParams
+from ..eval import EfficiencyMeter, MetricSuite, Results
 from ..models.registry import load_model
 from ..orchestrator.prompts import qa_prompt
-from ..utils.log import format_single_model_report, get_logger
+from ..parallel.split import agent_devices, split_model
+from ..utils.log import format_efficiency_report, format_single_model_report, get_logger
 from .combine import build_embedder
-from .common import add_runtime_args, pick_devices, pop_runtime
+from .common import add_runtime_args, build_generator, pick_devices, pop_runtime, resolve_runtime
 
 logger = get_logger("evaluate")
 
 
 def evaluate_model(model_id: str, rows, cfg, rt) -> dict:
+    """The reference's per-model loop (Llama_bf16_updated.py:96-134).  ``pp_size`` > 1 splits the
+    model's layers over that many GPUs (its ``device_map="auto"``, :31); ``batch_size`` > 1
+    decodes that many questions together (TPS per sample = its tokens incl. prompt / the batch's
+    wall time)."""
     logger.info(f"\n--- Evaluating Model: {model_id} ---")
+    rt = resolve_runtime(cfg, rt)
     dev = pick_devices(rt.get("devices"))[0]
+    devs = agent_devices(None, dev, int(rt.get("pp_size") or 1))
     quant = rt.get("quant") or cfg.quant.mode
     precision = rt.get("precision") or "bf16"
-    model, tok, source = load_model(model_id, precision, quant, dev, rt.get("base_model_path"))
-    logger.info(f"{model_id}: {source} ({quant})")
-    gen = Generator(model, max_batch=1, max_seq=rt.get("max_seq", 2048))
+    model, tok, source = load_model(model_id, precision, quant, devs[0], rt.get("base_model_path"))
+    if len(devs) > 1:
+        model = split_model(model, devs)
+        logger.info(f"{model_id}: {source} split over {[str(d) for d in devs]} at layers {model.bounds} ({quant})")
+    else:
+        logger.info(f"{model_id}: {source} ({quant})")
+    bs = max(1, int(rt.get("batch_size") or 1))
+    gen = build_generator(model, rt, max_batch=bs)
     s = cfg.sampling
     sp = SamplingParams(s.max_new_tokens, s.temperature, s.top_k, s.top_p, s.repetition_penalty, s.do_sample)
     suite = MetricSuite(build_embedder(cfg.embedder_model, rt.get("base_model_path"), dev))
     res_all = Results()
-    for i, sample in enumerate(rows):
-        ids = tok.encode(qa_prompt(sample["query"]))
-        ids = ids[-(gen.max_seq - sp.max_new_tokens):]
-        r = gen.generate([ids], sp, seed=rt.get("seed", 0) + i, eos_token_id=getattr(tok, "eos_token_id", None))
-        text = tok.decode((ids + r.tokens[0]) if not rt.get("no_legacy_decode") else r.tokens[0],
-                          skip_special_tokens=True).strip()
-        res_all.add(suite.score(text, sample["answer"], model, tok, tps=r.tps_incl_prompt()))
+    eff = EfficiencyMeter(devs)
+    eos = getattr(tok, "eos_token_id", None)
+    for j0 in range(0, len(rows), bs):
+        batch = rows[j0:j0 + bs]
+        t0 = time.perf_counter()
+        ids = [tok.encode(qa_prompt(smp["query"]))[-(gen.max_seq - sp.max_new_tokens):] for smp in batch]
+        r = gen.generate(ids, sp, seed=rt.get("seed", 0) + j0, eos_token_id=eos)
+        for i, (smp, pid, out) in enumerate(zip(batch, ids, r.tokens)):
+            text = tok.decode((pid + out) if not rt.get("no_legacy_decode") else out, skip_special_tokens=True).strip()
+            # prompt + generated tokens / generate wall time (Llama_bf16_updated.py:89-90)
+            tps = (len(pid) + len(out)) / r.elapsed_s if r.elapsed_s > 0 else 0.0
+            res_all.add(suite.score(text, smp["answer"], model, tok, tps=tps))
+        eff.add(time.perf_counter() - t0, len(batch), r.num_generated)
     means = res_all.means()
     for line in format_single_model_report(means):
+        logger.info(line)
+    means.update(eff.summary())
+    for line in format_efficiency_report(means):
         logger.info(line)
     return means
 

@@ -32,6 +32,11 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--max-batch", type=int, default=8)
     ap.add_argument("--max-seq", type=int, default=2048)
     ap.add_argument("--stage", default=None, help="first:last — serve these layers as a gRPC pipeline stage")
+    ap.add_argument("--pp-size", type=int, default=1, help="split the engine's layers over this many GPUs")
+    ap.add_argument("--gpus", default=None, help="comma list of GPU ids for the engine (overrides --pp-size)")
+    ap.add_argument("--headinfer-heads", type=int, default=None, help="HeadInfer: KV heads per layer kept on the GPU")
+    ap.add_argument("--prefill-chunk", type=int, default=4096, help="chunked prefill size (HeadInfer)")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"])
     return ap.parse_args(argv)
 
 
@@ -52,12 +57,19 @@ def build(args: argparse.Namespace):
         extra.append(StageServer(model, max_seq=args.max_seq).handler())
         log.info(f"stage layers [{a}, {b}) of {src}")
     elif args.model:
-        from ..engine import Generator
         from ..models.registry import load_model
+        from ..parallel.split import agent_devices, split_model
         from ..serve.server import ServingEngine
-        model, tok, src = load_model(args.model, args.precision, args.quant, device, base_dir=args.base_model_path)
-        engine = ServingEngine(Generator(model, max_batch=args.max_batch, max_seq=args.max_seq), tok, args.max_batch)
-        log.info(f"generation engine: {src}")
+        from .common import build_generator
+        gpus = [int(g) for g in args.gpus.split(",")] if args.gpus else None
+        devs = agent_devices(gpus, torch.device(device), args.pp_size)
+        model, tok, src = load_model(args.model, args.precision, args.quant, devs[0], base_dir=args.base_model_path)
+        if len(devs) > 1:
+            model = split_model(model, devs)
+        rt = dict(max_seq=args.max_seq, headinfer_heads=args.headinfer_heads, prefill_chunk=args.prefill_chunk,
+                  kv_dtype=args.kv_dtype)
+        engine = ServingEngine(build_generator(model, rt, max_batch=args.max_batch), tok, args.max_batch)
+        log.info(f"generation engine: {src} on {[str(d) for d in devs]}")
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=10),           # server.py:14
                          options=[("grpc.max_receive_message_length", 256 << 20),
                                   ("grpc.max_send_message_length", 256 << 20)])

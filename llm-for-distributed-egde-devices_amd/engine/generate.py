@@ -106,8 +106,11 @@ class Generator:
         self.device = model.device
         max_seq = min(max_seq or self.cfg.max_position_embeddings, self.cfg.max_position_embeddings)
         self.max_seq = max_seq
-        self.kv = kv if kv is not None else KVCache(self.cfg, max_batch, max_seq, device=self.device,
-                                                    dtype=model.dtype, kv_dtype=kv_dtype)
+        if kv is None:
+            # a model split over several devices (parallel.split.SplitLM) brings per-stage caches
+            kv = (model.make_kv(max_batch, max_seq, kv_dtype) if hasattr(model, "make_kv") else
+                  KVCache(self.cfg, max_batch, max_seq, device=self.device, dtype=model.dtype, kv_dtype=kv_dtype))
+        self.kv = kv
         self.rope = model.rope_table(self.device)
         # HeadInfer (edgellm.offload) caches carry an attention hook and a prefill chunk size
         self.attn_hook = getattr(self.kv, "attn_hook", None)

@@ -131,3 +131,35 @@ class ProgressLog:
             return
         with open(self.path, "a") as f:
             f.write(json.dumps({"index": index, **rec}) + "\n")
+
+
+class EfficiencyMeter:
+    """Table-3 efficiency columns (ACL.pdf p.7) measured by the harness itself:
+    "Time Taken" = wall time per sample of the whole loop, metrics included (the reference reads
+    tqdm's s/it, Llama_bf16_updated.py:103-124), aggregate generated tok/s of the QA agents, and
+    peak device memory (the reference read nvidia-smi by hand; here max_memory_allocated summed
+    over the agents' distinct GPUs)."""
+
+    def __init__(self, devices=()):
+        import time as _t
+        self.devices = sorted({str(d) for d in devices if str(d).startswith("cuda")})
+        self.wall = 0.0
+        self.n = 0
+        self.tokens = 0
+        self._t0 = _t.perf_counter()
+
+    def add(self, wall_s: float, n_samples: int, gen_tokens: int):
+        self.wall += wall_s
+        self.n += n_samples
+        self.tokens += gen_tokens
+
+    def peak_gb(self) -> float:
+        import torch
+        if not self.devices or not torch.cuda.is_available():
+            return 0.0
+        return sum(torch.cuda.max_memory_allocated(torch.device(d)) for d in self.devices) / 1e9
+
+    def summary(self) -> dict:
+        return {"time_per_sample_s": self.wall / max(self.n, 1), "total_time_s": self.wall,
+                "agg_tokens_per_s": self.tokens / self.wall if self.wall > 0 else 0.0,
+                "peak_mem_gb": self.peak_gb(), "samples": self.n}

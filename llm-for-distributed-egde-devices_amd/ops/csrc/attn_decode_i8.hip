@@ -32,6 +32,7 @@ struct Fuse8 {
   int8_t* out_q;        // QOUT: [B, Hq*D] int8
   float* out_s;         // QOUT: [(Hq*D)/64][Mpad]
   int Mpad;
+  int S;                // cache capacity (positions): loads below it are in bounds before seq_lens is known
 };
 
 __device__ __forceinline__ void rope8i(const bf16_t* __restrict__ head, int e0, int rot, const float2* csp,
@@ -56,6 +57,17 @@ __device__ __forceinline__ void unpack16i(const uint4& u, float* f) {
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) f[4 * i + j] = (float)(int8_t)((w[i] >> (8 * j)) & 0xff);
+  }
+}
+
+// 16 int8 as OFFSET bytes: u = q + 128 in [1, 255], one v_cvt_f32_ubyteN per element (the XOR flips
+// the sign bit of all 4 bytes of a dword in one op); the caller subtracts 128 * sum(weights).
+__device__ __forceinline__ void unpack16u(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x ^ 0x80808080u, u.y ^ 0x80808080u, u.z ^ 0x80808080u, u.w ^ 0x80808080u};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[4 * i + j] = (float)((w[i] >> (8 * j)) & 0xffu);
   }
 }
 
@@ -109,7 +121,7 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
   constexpr int LPK = D / 16;             // lanes per key row (16 int8 each)
   constexpr int KPW = 64 / LPK;           // keys per wave-instruction
   constexpr int KPB = KPW * NW;           // keys per workgroup step
-  constexpr int UNROLL = G >= 4 ? 2 : 4;  // key rows in flight per lane (registers: q / acc grow with G)
+  constexpr int UNROLL = G >= 4 ? 2 : 4;  // key rows per lane per chunk (q / acc grow with G)
   static_assert(D % 64 == 0 && LPK >= 4 && LPK <= 16, "D in {64, 128, 256}");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* red = smem;                      // [NW][G][D]
@@ -146,6 +158,26 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
   const int8_t* vb = vc + b * c_sb + kvh * c_sh + (size_t)start * D;
   const float* ksb = ksc + b * s_sb + kvh * s_sh + start;
   const float* vsb = vsc + b * s_sb + kvh * s_sh + start;
+  // The first chunk's K/V rows are requested before anything else (they depend only on the grid
+  // position, clamped to the cache capacity, not on seq_lens): at decode contexts of a few
+  // hundred keys that is the whole split, so the kernel pays one HBM round trip, overlapped with
+  // the q / RoPE / append work, instead of one after it.
+  constexpr int STEP = KPB * UNROLL;
+  const int lim = min(CH, fz.S - start) - 1;              // last in-bounds key of this split
+  uint4 kr[UNROLL], vr[UNROLL];
+  float ks[UNROLL], vs[UNROLL];
+  auto load = [&](int base, int bound) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = base + kl + u * KPB;
+      const int kk = k <= bound ? k : 0;
+      kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + (size_t)kk * D + d0)));
+      vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + (size_t)kk * D + d0)));
+      ks[u] = ksb[kk];
+      vs[u] = vsb[kk];
+    }
+  };
+  load(wave * KPW, lim);
 
   // q (rotated, rounded to bf16 as the unfused path would store it, pre-scaled by log2e/sqrt(D))
   const bf16_t* row = qkv + b * fz.qkv_sb;
@@ -167,6 +199,13 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[h][8 * c + j] = v[j] * scale_log2;
     }
+  }
+  float qsum[G];                                           // offset-byte keys: score -= 128 * qsum
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    qsum[h] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) qsum[h] += qf[h][j];
   }
 
   // append: lane groups kl = 0 (k) / 1 (v) of wave 0 in the owning split
@@ -193,11 +232,12 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
   }
   const int nl = own ? n - 1 : n;                  // keys read from the cache (the new one is last)
 
-  float m[G], l[G], acc[G][16];
+  float m[G], l[G], acc[G][16], vbias[G];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
     m[h] = -INFINITY;
     l[h] = 0.f;
+    vbias[h] = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[h][j] = 0.f;
   }
@@ -219,27 +259,16 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
     }
   }
 
-  constexpr int STEP = KPB * UNROLL;
   for (int base = wave * KPW; base < nl; base += STEP) {     // wave-uniform trip count
-    uint4 kr[UNROLL], vr[UNROLL];
-    float ks[UNROLL], vs[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = base + kl + u * KPB;
-      const int kk = k < nl ? k : 0;
-      kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + (size_t)kk * D + d0)));
-      vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + (size_t)kk * D + d0)));
-      ks[u] = ksb[kk];
-      vs[u] = vsb[kk];
-    }
+    if (base != wave * KPW) load(base, lim);                   // later chunks (long contexts)
     float s[UNROLL][G];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       float kf[16];
-      unpack16i(kr[u], kf);
+      unpack16u(kr[u], kf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
-        float a = 0.f;
+        float a = -128.f * qsum[h];
 #pragma unroll
         for (int j = 0; j < 16; ++j) a += qf[h][j] * kf[j];
         s[u][h] = a;
@@ -266,23 +295,29 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
       const float alpha = exp2f(m[h] - mn);
       m[h] = mn;
       l[h] *= alpha;
+      vbias[h] *= alpha;
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[h][j] *= alpha;
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       float vf[16];
-      unpack16i(vr[u], vf);
+      unpack16u(vr[u], vf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         const float p = exp2f(s[u][h] - m[h]);
         l[h] += p;
         const float pv = p * vs[u];
+        vbias[h] += pv;
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[h][j] += pv * vf[j];
       }
     }
   }
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[h][j] -= 128.f * vbias[h];
   // reduce over the KPW key groups of this wave: the group totals of l; acc per dim lane
 #pragma unroll
   for (int o = LPK; o < 64; o <<= 1)
@@ -342,6 +377,179 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
     float* ml = part_ml + (((size_t)b * Hq + kvh * G + threadIdx.x) * nsplit + split) * 2;
     ml[0] = mstat[threadIdx.x];
     ml[1] = lstat[threadIdx.x];
+  }
+}
+
+// Wave-per-(sequence, head) form for MHA at large batch and short contexts (the Llama-2-7B decode
+// step at 128 rows x 32 heads x ~160 keys): the workgroup-per-head kernel above runs its 4096
+// workgroups in 4 rounds per CU, each paying the whole dependent-load chain (sequence length ->
+// q / RoPE -> K/V chunks -> LDS merge behind 3 barriers), and is latency-bound at ~2.6 TB/s.  Here
+// every wave owns one (b, h) pair and walks all its keys itself — 4 pairs per 256-thread
+// workgroup, so all B*H waves are resident in ONE round (16 per CU at 4 waves/SIMD), the online
+// softmax never leaves the wave (no LDS, no barrier) and the next chunk's K/V rows are in flight
+// while the current chunk is consumed (two register buffers).  Offset-byte conversion
+// (unpack16u) halves the int8 -> float cost; the -128 bias is folded into one FMA per key
+// (scores) and one running sum (values).
+template <int D, bool QOUT>
+__global__ void __launch_bounds__(NT, 4) decode_attn_i8_wave_kernel(
+    const bf16_t* __restrict__ qkv, int8_t* __restrict__ kc, int8_t* __restrict__ vc, float* __restrict__ ksc,
+    float* __restrict__ vsc, int64_t c_sb, int64_t c_sh, int64_t s_sb, int64_t s_sh, const int* __restrict__ seq_lens,
+    float scale_log2, int Hkv, int npairs, bf16_t* __restrict__ out, int64_t o_sb, Fuse8 fz) {
+  constexpr int LPK = D / 16, KPW = 64 / LPK, U = 2;     // U key rows per lane per buffer
+  constexpr int CHUNK = KPW * U;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pair = blockIdx.x * NW + wave;
+  if (pair >= npairs) return;                           // whole wave exits (no barriers below)
+  const int b = pair / Hkv, h = pair - b * Hkv;
+  const int Hq = Hkv;
+  const int dl = lane % LPK, kl = lane / LPK, d0 = dl * 16;
+  const int8_t* kb = kc + b * c_sb + h * c_sh;
+  const int8_t* vb = vc + b * c_sb + h * c_sh;
+  const float* ksb = ksc + b * s_sb + h * s_sh;
+  const float* vsb = vsc + b * s_sb + h * s_sh;
+  const int lim = fz.S - 1;                             // loads clamp to the cache, masks use nl
+
+  uint4 kr[2][U], vr[2][U];
+  float ks[2][U], vs[2][U];
+  auto load = [&](int buf, int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + kl + u * KPW;
+      const int kk = k <= lim ? k : 0;
+      kr[buf][u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + (size_t)kk * D + d0)));
+      vr[buf][u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + (size_t)kk * D + d0)));
+      ks[buf][u] = ksb[kk];
+      vs[buf][u] = vsb[kk];
+    }
+  };
+  load(0, 0);                                           // first chunk in flight before seq_lens is read
+  const int len = seq_lens[b];
+  const int pos = fz.pos[b];
+  const int nl = len - 1;                               // cached keys [0, pos); the new one is at pos
+
+  const bf16_t* row = qkv + b * fz.qkv_sb;
+  const float2* csp = reinterpret_cast<const float2*>(fz.cs) + (size_t)pos * (fz.rot / 2);
+  float qf[16], qsum = 0.f;
+  {
+    const bf16_t* qh = row + (size_t)h * D;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(qh + d0 + 8 * c), v);
+      if (d0 + 8 * c < fz.rot) {
+        rope8i(qh, d0 + 8 * c, fz.rot, csp, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { qf[8 * c + j] = v[j] * scale_log2; qsum += qf[8 * c + j]; }
+    }
+  }
+  // the new token: key groups kl = 0 (k) and 1 (v) rotate / quantise / store it
+  float xnew[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) xnew[j] = 0.f;
+  if (kl < 2) {
+    const bool is_v = kl == 1;
+    const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + h) * D;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(head + d0 + 8 * c), v);
+      if (!is_v && d0 + 8 * c < fz.rot) rope8i(head, d0 + 8 * c, fz.rot, csp, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xnew[8 * c + j] = bf2f(f2bf(v[j]));
+    }
+    float sc;
+    const uint4 qv = quant_row16<LPK>(xnew, sc);
+    *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + h * c_sh + (size_t)pos * D + d0) = qv;
+    if (dl == 0) (is_v ? vsc : ksc)[b * s_sb + h * s_sh + pos] = sc;
+  }
+  // online softmax state, uniform across the wave; the new key seeds it (m = its score, l = 1)
+  float sp = 0.f;
+  if (kl == 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sp += qf[j] * xnew[j];
+  }
+  sp = group_sum<LPK>(sp);
+  float m = __shfl(sp, dl, 64), l = kl == 1 ? 1.f : 0.f, vbias = 0.f;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = kl == 1 ? xnew[j] : 0.f;
+  // acc holds sum p * vs * u (offset bytes) + the new value; vbias = sum p * vs (for the -128 term)
+
+  int buf = 0;
+  for (int base = 0; base < nl; base += CHUNK) {        // wave-uniform
+    if (base + CHUNK < nl) load(buf ^ 1, base + CHUNK);
+    float s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float kf[16];
+      unpack16u(kr[buf][u], kf);
+      float a = -128.f * qsum;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a += qf[j] * kf[j];
+      s[u] = group_sum<LPK>(a) * ks[buf][u];
+      if (base + kl + u * KPW >= nl) s[u] = -INFINITY;
+    }
+    float cm = s[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) cm = fmaxf(cm, s[u]);
+#pragma unroll
+    for (int o = LPK; o < 64; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+    const float mn = fmaxf(m, cm);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+    vbias *= alpha;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] *= alpha;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float vf[16];
+      unpack16u(vr[buf][u], vf);
+      const float p = exp2f(s[u] - m);
+      l += p;
+      const float pv = p * vs[buf][u];
+      vbias += pv;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] += pv * vf[j];
+    }
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] -= 128.f * vbias;
+#pragma unroll
+  for (int o = LPK; o < 64; o <<= 1) {
+    l += __shfl_xor(l, o, 64);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] += __shfl_xor(acc[j], o, 64);
+  }
+  const float inv = 1.f / l;
+  float o[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) o[j] = bf2f(f2bf(acc[j] * inv));
+  if constexpr (QOUT) {
+    // per (token, 64 columns): 4 lanes x 16 dims; every key group holds the same values
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a = fmaxf(a, fabsf(o[j]));
+    a = fmaxf(group_max<4>(a), 1e-8f);
+    const float iv = 127.f / a;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j >> 2] |= ((uint32_t)(uint8_t)quant_i8(o[j], iv)) << (8 * (j & 3));
+    const int col = h * D + d0;
+    if (kl == 0) {
+      *reinterpret_cast<uint4*>(fz.out_q + (size_t)b * Hq * D + col) = uint4{w[0], w[1], w[2], w[3]};
+      if ((dl & 3) == 0) fz.out_s[(size_t)(col >> 6) * fz.Mpad + b] = a / 127.f;
+    }
+  } else {
+    if (kl == 0) {
+      bf16_t* op = out + b * o_sb + (size_t)h * D + d0;
+      *reinterpret_cast<uint4*>(op) = pack8(o);
+      *reinterpret_cast<uint4*>(op + 8) = pack8(o + 8);
+    }
   }
 }
 
@@ -414,8 +622,24 @@ extern "C" int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, vo
   const bool qout = out_q != nullptr;
   if (qout && (D % 64 != 0 || Mpad < B)) return -2;
   if (rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
-  const Fuse8 fz{pos, cs, rot, qkv_sb, (int8_t*)out_q, out_s, Mpad};
+  const Fuse8 fz{pos, cs, rot, qkv_sb, (int8_t*)out_q, out_s, Mpad, (int)(c_sh / D)};
   const float sl2 = scale * 1.4426950408889634f;
+  if (G == 1 && ch < 0) {                 // wave-per-(sequence, head) form (edge_decode_attn_i8_plan)
+    const int npairs = B * Hkv, blocks = (npairs + NW - 1) / NW;
+#define WV(DD, QO) hipLaunchKernelGGL((decode_attn_i8_wave_kernel<DD, QO>), dim3(blocks), dim3(NT), 0, st,       \
+                                      (const bf16_t*)qkv, (int8_t*)kc, (int8_t*)vc, ks, vs, c_sb, c_sh, s_sb, s_sh, \
+                                      seq_lens, sl2, Hkv, npairs, (bf16_t*)out, o_sb, fz)
+#define WVQ(DD) do { if (qout) WV(DD, true); else WV(DD, false); } while (0)
+    switch (D) {
+      case 64: WVQ(64); break;
+      case 128: WVQ(128); break;
+      case 256: WVQ(256); break;
+      default: return -4;
+    }
+#undef WVQ
+#undef WV
+    return (int)hipGetLastError();
+  }
   const size_t lds = (size_t)(NW * G * D + 2 * NW * G + 2 * G) * sizeof(float);
   const dim3 grid(nsplit, Hkv, B);
   const bool direct = nsplit == 1;
@@ -456,8 +680,19 @@ extern "C" int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, vo
 }
 
 // Split plan for the int8 cache: the bf16 plan's rule on bytes (>= 64 KiB of K+V per split).
-extern "C" int edge_decode_attn_i8_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out) {
+// ch = -1 selects the wave-per-(sequence, head) kernel: MHA with enough pairs to put every CU to
+// work with one round of resident waves (B * Hkv >= 2048) and contexts a single wave walks in a
+// few chunks (<= g_attn8_wave_max keys).
+static int g_attn8_wave_max = 0;     // wave form off by default (measured slower at 128 x 160; tune "attn8_wave_max")
+extern "C" void edge_decode_attn_i8_wave_max(int v) { g_attn8_wave_max = v; }
+extern "C" int edge_decode_attn_i8_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out,
+                                        int G) {
   const int per = B * Hkv;
+  if (G == 1 && per >= 2048 && max_len <= g_attn8_wave_max) {
+    *ch_out = -1;
+    *nsplit_out = 1;
+    return 0;
+  }
   int nsplit = (g_attn8_target_wg + per - 1) / per;
   int ch = (max_len + nsplit - 1) / nsplit;
   ch = ((ch + 63) / 64) * 64;

@@ -58,7 +58,8 @@ int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, void* vc, flo
                         float scale, int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
                         const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
                         hipStream_t st);
-int edge_decode_attn_i8_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out);
+int edge_decode_attn_i8_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out, int G);
+void edge_decode_attn_i8_wave_max(int v);
 int edge_kv_quant_append(const void* src, int64_t x_sb, int64_t x_sh, const int* start_pos, void* dst, int64_t c_sb,
                          int64_t c_sh, float* sc, int64_t s_sb, int64_t s_sh, int B, int Hkv, int T, int D, int S,
                          hipStream_t st);
@@ -368,7 +369,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_i8(
     cs = rope->data_ptr<float>();
   }
   int ch = 0, nsplit = 0;
-  edge_decode_attn_i8_plan((int)B, (int)Hkv, (int)max_len_hint, (int)D, &ch, &nsplit);
+  edge_decode_attn_i8_plan((int)B, (int)Hkv, (int)max_len_hint, (int)D, &ch, &nsplit, (int)(Hq / Hkv));
   at::Tensor pacc, pml, out, oq;
   std::optional<at::Tensor> os;
   if (nsplit > 1) {
@@ -692,6 +693,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
+    else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });
 }

@@ -56,6 +56,26 @@ class Agent:
         text = self.tokenizer.decode((ids + toks) if legacy_decode else toks, skip_special_tokens=True).strip()
         return text, res
 
+    def run_batch(self, prompt_texts: Sequence[str], seed: int, legacy_decode: bool = True,
+                  sampling: Optional[SamplingParams] = None):
+        """Decode several prompts together (one batched generate: per-sequence prefill, one
+        graph-replayed decode step for all rows).  Returns (texts, GenerationResult)."""
+        sp = sampling or self.sampling
+        max_seq = self.generator.max_seq
+        ids_list = []
+        for t in prompt_texts:
+            ids = self.tokenizer.encode(t)
+            if len(ids) + sp.max_new_tokens > max_seq:
+                ids = ids[-(max_seq - sp.max_new_tokens):]
+            ids_list.append(ids)
+        eos = getattr(self.tokenizer, "eos_token_id", None)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        res = self.generator.generate(ids_list, sp, seed=seed, eos_token_id=eos)
+        texts = [self.tokenizer.decode((ids + toks) if legacy_decode else toks, skip_special_tokens=True).strip()
+                 for ids, toks in zip(ids_list, res.tokens)]
+        return texts, res
+
 
 @dataclass
 class EnsembleResult:
@@ -96,11 +116,18 @@ class RefineMerge:
     def __init__(self, refiner: Agent, include_reference: bool = True, legacy_decode: bool = True):
         self.refiner, self.include_reference, self.legacy_decode = refiner, include_reference, legacy_decode
 
+    def _sampling(self):
+        return SamplingParams(max_new_tokens=self.refiner.sampling.max_new_tokens, **REFINER_SAMPLING)
+
     def __call__(self, answers: Dict[str, str], question: str, reference: Optional[str], seed: int):
         prompt = refine_prompt(list(answers.values()), reference, self.include_reference)
-        sp = SamplingParams(max_new_tokens=self.refiner.sampling.max_new_tokens, **REFINER_SAMPLING)
-        text, res = self.refiner.run(prompt, seed, self.legacy_decode, sp)
+        text, res = self.refiner.run(prompt, seed, self.legacy_decode, self._sampling())
         return text, res
+
+    def batch(self, answers: List[Dict[str, str]], questions, references, seed: int):
+        prompts = [refine_prompt(list(a.values()), r, self.include_reference) for a, r in zip(answers, references)]
+        texts, res = self.refiner.run_batch(prompts, seed, self.legacy_decode, self._sampling())
+        return texts, res
 
 
 class Orchestrator:
@@ -147,3 +174,53 @@ class Orchestrator:
                 vals.append(tps["merger"])
         return EnsembleResult(question, ordered, final, results, tps, sum(vals) / len(vals), time.perf_counter() - t0,
                               getattr(self.merge, "name", "custom"))
+
+    def answer_batch(self, questions: Sequence[str], references: Sequence[Optional[str]], seed: int = 0
+                     ) -> List[EnsembleResult]:
+        """Batched ``answer``: every agent decodes all questions of the batch together (agents on
+        distinct devices concurrently), then the merge runs batched (refiner) or per question
+        (vote).  Per-sample TPS = the sample's generated tokens / its agent's batch wall time (a
+        per-stream rate, comparable with the reference's batch-1 TPS); the batch's aggregate
+        throughput is ``sum(generated) / wall``."""
+        t0 = time.perf_counter()
+        outs: Dict[str, tuple] = {}
+        errors: List[BaseException] = []
+
+        def work(i, agent):
+            try:
+                prompts = [qa_prompt(q, agent.cpu_prompt) for q in questions]
+                outs[agent.name] = agent.run_batch(prompts, seed + 1000 * i, self.legacy_decode)
+            except BaseException as e:  # surfaced after join
+                errors.append(e)
+
+        devices = {a.device for a in self.agents}
+        if self.concurrent and len(self.agents) > 1 and len(devices) > 1:
+            threads = [threading.Thread(target=work, args=(i, a)) for i, a in enumerate(self.agents)]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+        else:
+            for i, a in enumerate(self.agents):
+                work(i, a)
+        if errors:
+            raise errors[0]
+        n = len(questions)
+        answers = [{a.name: outs[a.name][0][j] for a in self.agents} for j in range(n)]
+        per_tps = [{a.name: len(outs[a.name][1].tokens[j]) / max(outs[a.name][1].elapsed_s, 1e-9) for a in self.agents}
+                   for j in range(n)]
+        if hasattr(self.merge, "batch"):
+            finals, mres = self.merge.batch(answers, questions, references, seed)
+            for j in range(n):
+                per_tps[j]["merger"] = len(mres.tokens[j]) / max(mres.elapsed_s, 1e-9)
+        else:
+            finals = [self.merge(answers[j], questions[j], references[j], seed)[0] for j in range(n)]
+        wall = time.perf_counter() - t0
+        out = []
+        for j in range(n):
+            tps = per_tps[j]
+            vals = [v for k, v in tps.items() if k != "merger" or self.tps_includes_merger]
+            out.append(EnsembleResult(questions[j], answers[j], finals[j],
+                                      {a.name: outs[a.name][1] for a in self.agents}, tps, sum(vals) / len(vals),
+                                      wall / n, getattr(self.merge, "name", "custom")))
+        return out

@@ -46,6 +46,19 @@ def format_final_report(means: dict) -> list:
     ]
 
 
+def format_efficiency_report(means: dict) -> list:
+    """Efficiency lines in the layout of the paper's Table 3 (memory, time, tokens/sec), after
+    the reference's nine lines: time = whole-loop wall per sample (tqdm s/it), metrics included."""
+    t = means.get("total_time_s", 0.0)
+    h, rem = divmod(int(round(t)), 3600)
+    m, s = divmod(rem, 60)
+    return [
+        f"Time Taken     → {h}:{m:02d}:{s:02d} ({means.get('time_per_sample_s', 0.0):.2f} s/it)",
+        f"Memory (GB)    → {means.get('peak_mem_gb', 0.0):.2f}",
+        f"Agg. Tok/Sec   → {means.get('agg_tokens_per_s', 0.0):.2f}",
+    ]
+
+
 def format_single_model_report(means: dict) -> list:
     """Final lines of the single-model evaluators (Llama_bf16_updated.py:126-134)."""
     r1, r2, rl = means["rouge1"], means["rouge2"], means["rougeL"]

@@ -46,7 +46,8 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--copies", type=int, default=0, help="cache copies rotated (0: enough for > 512 MB)")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--only", default="bf16,int8")
+    ap.add_argument("--only", default="bf16,int8,int8wave",
+                    help="bf16 | int8 (workgroup-per-head split form) | int8wave (wave-per-head form)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv = (int(x) for x in a.heads.split("x"))
@@ -62,17 +63,18 @@ def main():
         pos = sl - 1
         rope = ops.rope_tables(D, S, 10000.0, device=dev)
         for kind in a.only.split(","):
+            ops.ext().tune("attn8_wave_max", 1024 if kind == "int8wave" else 0, 0)
             caches = []
             for _ in range(n):
                 k = torch.randn(B, Hkv, S, D, device=dev).bfloat16()
                 v = torch.randn_like(k)
-                if kind == "int8":
+                if kind.startswith("int8"):
                     kq, ks = _ref.quant_kv_rows(k)
                     vq, vs = _ref.quant_kv_rows(v)
                     caches.append((kq, vq, ks.contiguous(), vs.contiguous()))
                 else:
                     caches.append((k, v))
-            if kind == "int8":
+            if kind.startswith("int8"):
                 fns = [lambda c=c: ops.decode_attention_fused_i8(qkv, pos, rope, c[0], c[1], c[2], c[3], sl, Hq,
                                                                  1 / math.sqrt(D), L, D, True) for c in caches]
                 nbytes = 2 * B * Hkv * L * (D + 4)
