@@ -616,12 +616,229 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
       }
     }
 }
+
+// ------------------------------------------------------------------------------------- ring
+// 65-128 decode rows (two micro-batches or one 128-row micro-batch) on an LDS-DMA ring.
+// The ldsa kernel above stages activations through VGPRs (global load -> ds_write -> barrier) with
+// two steps in flight, ~96 KiB per CU: at 128 rows every CU also re-reads the whole 512 KiB
+// activation matrix from L2, and with ~2-3 us of loaded memory latency that in-flight budget caps
+// a CU at ~30 GB/s (qkv 25.8 us for 50 MB).  Here BOTH operands go global -> LDS by
+// global_load_lds (no VGPR round trip, no ds_write) into a ring of R stages of C k-tiles, R - 1
+// stages (~110 KiB) in flight per CU, one barrier per stage:
+//   wait own DMA of stage s (counted vmcnt) -> barrier (stage s landed everywhere, slot of s - 1
+//   free) -> DMA stage s + R - 1 into that slot -> MFMA over stage s.
+// A stage holds the 8 row blocks x C activation fragments, the NTW x C weight tiles and (SCALED)
+// the C k-tiles' per-(token, 64) scales.  4 waves; wave w owns row blocks {2w, 2w + 1} for all NTW
+// tiles (2 NTW accumulators), reading 2 activation + NTW weight fragments per k-tile from LDS —
+// no k-split inside the workgroup, so no LDS reduction; everything the epilogue needs from
+// global memory is loaded at kernel start.  EPI_PART: blockIdx = group * S + slice (fp32 partial
+// slices for the next RMSNorm); EPI_GLUQ: NTW = 8 (64 features), the row maxima are wave-local.
+// LDS reads of DMA-filled ring slots go through inline asm: the compiler cannot tell ring slots
+// apart, and for a plain LDS load (or a fenced __syncthreads) it would wait for EVERY outstanding
+// LDS-DMA (vmcnt(0)), draining the ring each stage.  Ordering is explicit instead: counted vmcnt
+// for this wave's own DMA, a bare s_barrier for the other waves', lgkmcnt(0) before the MFMAs.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
+}
+__device__ __forceinline__ v4i lds_read16(uint32_t addr) {
+  v4i r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
+template <int NTW, int C, int R, bool SCALED, int EPI>
+__global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
+    const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
+    const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
+    int M, int N, int K, int NTt, int Mpad, int S, int KTC) {
+  constexpr int MB = 8, NWV = 4;
+  constexpr int APC = MB * C, WPC = NTW * C, SPC = SCALED ? (C + 1) / 2 : 0;
+  constexpr int PIECES = APC + WPC + SPC, STAGE = PIECES * 1024;
+  constexpr int PPW = PIECES / NWV, PEXTRA = PIECES % NWV;   // waves < PEXTRA issue PPW + 1 pieces
+  static_assert(R * STAGE <= 150 * 1024, "LDS ring budget");
+  static_assert(EPI != EPI_GLUQ || NTW == 8, "GLUQ: 8 tiles = 64 features per workgroup");
+  __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
+  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
+  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
+  const int kbeg = ks * KTC, KT = K / 64;
+  const int nt0 = grp * NTW;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int STEPS = (KTC + C - 1) / C;
+
+  // per-lane DMA sources of this wave's pieces (p = wave + i * NWV), advanced by k-tile
+  constexpr int PMAX = PPW + (PEXTRA ? 1 : 0);
+  const int8_t* src[PMAX];
+  int stride[PMAX], klocal[PMAX];
+#pragma unroll
+  for (int i = 0; i < PMAX; ++i) {
+    const int p = min(wave + i * NWV, PIECES - 1);
+    if (p < APC) {                                   // activation fragment: row block p % MB
+      const int row = min((p % MB) * 16 + (lane & 15), M - 1);
+      src[i] = A + (size_t)row * K + (size_t)kbeg * 64 + 16 * (lane >> 4);
+      stride[i] = 64;
+      klocal[i] = p / MB;
+    } else if (p < APC + WPC) {                      // weight tile nt0 + q % NTW
+      const int q = p - APC;
+      src[i] = Wp + ((size_t)min(nt0 + q % NTW, NTt - 1) * KT + kbeg) * 1024 + lane * 16;
+      stride[i] = 1024;
+      klocal[i] = q / NTW;
+    } else {                                         // scales of k-tiles 2q, 2q + 1 (rows 4 x lane)
+      const int q = p - APC - WPC;
+      src[i] = reinterpret_cast<const int8_t*>(sa + (size_t)kbeg * Mpad + min(4 * (lane & 31), Mpad - 4));
+      stride[i] = Mpad * 4;
+      klocal[i] = 2 * q + (lane >> 5);
+    }
+  }
+  auto issue = [&](int st) {
+#pragma unroll
+    for (int i = 0; i < PMAX; ++i) {
+      if (i < PPW || wave < PEXTRA) {
+        const int p = wave + i * NWV;
+        const int kt = min(st * C + klocal[i], KTC - 1);       // past the slice: a valid, unused tile
+        glds16(src[i] + (size_t)kt * stride[i], ring + (st % R) * STAGE + p * 1024);
+      }
+    }
+  };
+  auto wait_ahead = [&](bool steady) {               // own DMA of the oldest stage landed
+    constexpr int NA = (R - 2) * (PPW + 1), NB = (R - 2) * PPW;
+    static_assert(NA < 64, "vmcnt range");
+    if (steady) {
+      if (wave < PEXTRA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+
+  // epilogue operands, loaded now (the tail of the kernel never waits on memory)
+  float sw_t[NTW], b_t[NTW], sa_r[2][4];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int col = min((nt0 + t) * 16 + (lane & 15), N - 1);
+    sw_t[t] = sw[col];
+    b_t[t] = bias != nullptr ? bf2f(bias[col]) : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sa_r[j][q] = SCALED ? 1.f : sa[min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, M - 1)];
+
+  v4i acc[2][NTW];
+  v4f accf[2][NTW];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) { acc[j][t] = v4i{0, 0, 0, 0}; accf[j][t] = v4f{0.f, 0.f, 0.f, 0.f}; }
+
+#pragma unroll
+  for (int st = 0; st < R - 1; ++st)
+    if (st < STEPS) issue(st);
+  const uint32_t ring0 = lds_off(ring);
+  for (int s = 0; s < STEPS; ++s) {
+    wait_ahead(s + R - 2 < STEPS);
+    __builtin_amdgcn_s_barrier();
+    if (s + R - 1 < STEPS) issue(s + R - 1);
+    const uint32_t base = ring0 + (s % R) * STAGE;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (s * C + c < KTC) {                          // wave-uniform
+        v4i a[2], b[NTW];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) a[j] = lds_read16(base + (c * MB + 2 * wave + j) * 1024 + lane * 16);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) b[t] = lds_read16(base + (APC + c * NTW + t) * 1024 + lane * 16);
+        v4f sgv[2];
+        if constexpr (SCALED) {
+          const uint32_t scl = base + (APC + WPC + c / 2) * 1024 + (c & 1) * 512;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            sgv[j] = __builtin_bit_cast(v4f, lds_read16(scl + ((2 * wave + j) * 16 + 4 * (lane >> 4)) * 4));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // the fragments' values are defined only after the wait: pin them behind it
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(a[j]));
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(b[t]));
+        if constexpr (SCALED) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(sgv[j]));
+        }
+        if constexpr (SCALED) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const v4f sg = sgv[j];
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) fold(accf[j][t], mfma_i8(a[j], b[t], v4i{0, 0, 0, 0}), sg);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) acc[j][t] = mfma_i8(a[j], b[t], acc[j][t]);
+        }
+      }
+    }
+  }
+
+  // epilogue: lane holds col (lane & 15) of each tile, rows 4 (lane >> 4) + q of its 2 row blocks
+  auto value = [&](int j, int t, int q) -> float {
+    return SCALED ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j][q];
+  };
+  if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      const int col = (nt0 + t) * 16 + (lane & 15);
+      if (nt0 + t >= NTt || col >= N) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+          if (row >= M) continue;
+          if constexpr (EPI == EPI_PART) {
+            reinterpret_cast<float*>(outv)[((size_t)ks * M + row) * N + col] =
+                value(j, t, q) * sw_t[t] + (ks == 0 ? b_t[t] : 0.f);
+          } else {
+            reinterpret_cast<bf16_t*>(outv)[(size_t)row * N + col] = f2bf(value(j, t, q) * sw_t[t] + b_t[t]);
+          }
+        }
+    }
+  } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
+    const int Fo = N / 2, grp64 = nt0 / 8;
+    int8_t* hq = reinterpret_cast<int8_t*>(outv);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+        float h[4], amax = 0.f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          float g = bf2f(f2bf(value(j, 2 * p, q) * sw_t[2 * p] + b_t[2 * p]));     // the unfused GEMM output is bf16
+          float u = bf2f(f2bf(value(j, 2 * p + 1, q) * sw_t[2 * p + 1] + b_t[2 * p + 1]));
+          h[p] = g / (1.f + __expf(-g)) * u;
+          amax = fmaxf(amax, fabsf(h[p]));
+        }
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) amax = fmaxf(amax, __shfl_xor(amax, d, 64));
+        amax = fmaxf(amax, 1e-8f);
+        const bool live = nt0 + 7 < NTt;
+        if (live && row < M) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) hq[(size_t)row * Fo + (nt0 / 2 + p) * 16 + (lane & 15)] = quant_i8(h[p], 127.f / amax);
+        }
+        if (live && (lane & 15) == 0 && row < Mpad) os[(size_t)grp64 * Mpad + row] = row < M ? amax / 127.f : 0.f;
+      }
+  }
+}
 }  // namespace
 
-static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0;
+static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 1;
 // tuning hooks (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int kw, int unroll) { g_gemv_kw = kw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
+extern "C" void edge_w8a8_gemv_ring(int on) { g_gemv_ring = on; }
 
 namespace {
 template <int MB, int NTW, int TG, int KW, int U, int AM, int EP>
@@ -644,6 +861,38 @@ int launch_ldsa(const void* A, const float* sa, const void* Wp, const float* sw,
   return (int)hipGetLastError();
 }
 
+template <int NTW, int C, int R, bool SC, int EP>
+int launch_ring(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                float* os, int M, int N, int K, int Mpad, hipStream_t st, int S, int KTC) {
+  const int NTt = (N + 15) / 16;
+  hipLaunchKernelGGL((w8a8_gemv_ring_kernel<NTW, C, R, SC, EP>), dim3((NTt + NTW - 1) / NTW * S), dim3(256), 0, st,
+                     (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S,
+                     KTC);
+  return (int)hipGetLastError();
+}
+
+// Ring kernel for 65-128 rows: NTW sized for ~256 workgroups (one per CU), k-tiles per stage and
+// ring depth for ~110-130 KiB of LDS-DMA in flight.  -1: no ring kernel for this call.
+template <int EP>
+int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                        float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
+  if (!g_gemv_ring || M <= 64 || M > 128 || K % 64 != 0 || (K / 64) % S != 0 || (EP == EPI_PART) != (S > 1)) return -1;
+  // per-(token, 64) scales (o / down): the per-k-tile fold serialises the MFMAs and the ring form
+  // measured slower than the LDS-staged kernel (o + down 24.8 us avg vs 12.1 / 22.3): off
+  if (scaled) return -1;
+  const int KTC = K / 64 / S, NTt = (N + 15) / 16;
+  if constexpr (EP == EPI_GLUQ) {
+    if (scaled || N % 128 != 0) return -1;
+    return launch_ring<8, 1, 8, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+  } else {
+    const int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : max(1, min(4, (NTt * S + 128) / 256));
+#define RG(NTWV)                                                                                                      if (ntw == NTWV)                                                                                                      return scaled ? launch_ring<NTWV, 2, 5, true, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC)                        : launch_ring<NTWV, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+    RG(1) RG(2) RG(3) RG(4)
+#undef RG
+  }
+  return -1;
+}
+
 // 65-128 rows (two decode micro-batches in one): LDS-staged activations, one tile per wave, 8 row
 // blocks of accumulators.  Instantiated for the k-tile counts of the 4096-hidden models (K = 4096
 // whole, and K = 4096 / 11008 / 14336 in 4 split-K slices); -1 = no kernel for this shape.
@@ -660,6 +909,10 @@ namespace {
 template <int EP>
 int launch_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                    float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
+  {
+    const int r = launch_ring_rows128<EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, scaled, st, S);
+    if (r != -1) return r;
+  }
   if (!edge_w8a8_rows128_ok(K, S) || (EP == EPI_PART) != (S > 1)) return -1;
   const int ktc = K / 64 / S;
 #define R128(KTC)                                                                                                   \
@@ -766,6 +1019,10 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
         return launch_one<1, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
       }
       if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+      if (mblocks > 4) {
+        const int r = launch_ring_rows128<EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, false, st, 1);
+        if (r != -1) return r;
+      }
       // K = 4096: activations staged in LDS (unroll knob 1 = the weight-stationary form)
       if (ldsa) {
         // 128 rows: 2 steps of prefetch (4 steps: 37.7 us, 4 k-tiles per wave-step: 40.9 us, against 35.8)

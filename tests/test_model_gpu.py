@@ -81,9 +81,31 @@ def test_w8a8_decode_128_rows_4096_hidden(cuda, B):
     prompts = torch.randint(0, cfg.vocab_size, (B, 12), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=6, do_sample=False)
     big = Generator(model, max_batch=B, max_seq=32).generate(prompts, sp, seed=0).tokens
-    small = Generator(model, max_batch=16, max_seq=32).generate(prompts[:16], sp, seed=0).tokens
-    same = sum(a == b for ra, rb in zip(big[:16], small) for a, b in zip(ra, rb))
-    assert len(big) == B and same >= 0.85 * 16 * 6
+    assert len(big) == B and all(len(t) == 6 for t in big)
+    _rows_match_small_batch(model, prompts, B, cuda)
+
+
+def _rows_match_small_batch(model, prompts, B, cuda, tol=3e-2):
+    """Decode-step logits of the first 16 rows at batch B (its kernel family) against the same
+    rows decoded at batch 16: rows are independent, so only kernel rounding may differ — bounded
+    per row on relative logit error (a wrong row block cannot hide behind token agreement)."""
+    from edgellm.models import AttnCtx
+    cfg = model.cfg
+    outs = {}
+    for b in (B, 16):
+        ids = torch.tensor(prompts[:b], device=cuda)
+        T = ids.shape[1]
+        kv = KVCache(cfg, b, T + 4, dtype=model.dtype, device=cuda)
+        sp = torch.zeros(b, dtype=torch.int32, device=cuda)
+        with torch.no_grad():
+            last = model(ids, AttnCtx("prefill", b, T, sp, sp + T, T, kv.rows(0, b), model.rope_table(cuda)),
+                         logits="last")
+            tok = last.argmax(-1)
+            pos = torch.full((b,), T, dtype=torch.int32, device=cuda)
+            outs[b] = model(tok.view(b, 1), AttnCtx("decode", b, 1, pos, pos + 1, T + 1, kv.rows(0, b),
+                                                    model.rope_table(cuda))).float()[:16]
+    rel = (outs[B] - outs[16]).norm(dim=-1) / outs[16].norm(dim=-1)
+    assert rel.max().item() < tol, rel.max().item()
 
 
 @pytest.mark.parametrize("B", [64, 80])
@@ -99,6 +121,5 @@ def test_w8a8_decode_beyond_gemv_rows(cuda, B):
     prompts = torch.randint(0, cfg.vocab_size, (B, 12), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=6, do_sample=False)
     big = Generator(model, max_batch=B, max_seq=32).generate(prompts, sp, seed=0).tokens
-    small = Generator(model, max_batch=16, max_seq=32).generate(prompts[:16], sp, seed=0).tokens
-    same = sum(a == b for ra, rb in zip(big[:16], small) for a, b in zip(ra, rb))
-    assert len(big) == B and same >= 0.85 * 16 * 6
+    assert len(big) == B and all(len(t) == 6 for t in big)
+    _rows_match_small_batch(model, prompts, B, cuda)
