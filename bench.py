@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--latency-point", default="auto", choices=["auto", "off", "int8", "both"],
                     help="also report batch-1 p50 per-token latency (single GPU): int8 = the benchmark model at "
                          "micro-batch 1, both = plus the bf16 model; auto = both on a GPU, off on CPU")
+    ap.add_argument("--prefill-chunk", type=int, default=None,
+                    help="chunked prefill size with HeadInfer (default: the whole prompt in one chunk)")
     ap.add_argument("--headinfer-heads", type=int, default=None,
                     help="HeadInfer: KV heads per layer kept on the GPU, the rest offloaded to pinned host memory")
     return ap.parse_args(argv)
@@ -72,8 +74,13 @@ def parse(argv=None):
 
 def model_config(args):
     if args.model.startswith("tiny:"):
-        return tiny(args.model.split(":", 1)[1], num_layers=8)   # 8 layers: splits up to 8 stages
-    return get_config(args.model)
+        cfg = tiny(args.model.split(":", 1)[1], num_layers=8)   # 8 layers: splits up to 8 stages
+    else:
+        cfg = get_config(args.model)
+    need = args.prompt_len + args.warmup + args.steps + 16
+    if need > cfg.max_position_embeddings:      # long-context runs (HeadInfer): extend the RoPE table
+        cfg = cfg.replace(max_position_embeddings=need)
+    return cfg
 
 
 def build(args, device, first=0, last=None):
@@ -115,7 +122,8 @@ def run_single(args):
     kv = None
     if args.headinfer_heads is not None and args.headinfer_heads < cfg.num_kv_heads:
         from edgellm.offload import HeadInferKV
-        kv = HeadInferKV(cfg, B, max_seq, args.headinfer_heads, device, chunk_size=max(args.prompt_len, 1))
+        kv = HeadInferKV(cfg, B, max_seq, args.headinfer_heads, device,
+                         chunk_size=max(1, min(args.prompt_len, args.prefill_chunk or args.prompt_len)))
     L = max(1, args.lanes)
     if L > 1:
         assert kv is None, "HeadInfer offload runs one lane"
@@ -155,7 +163,11 @@ def run_single(args):
     if device.type == "cuda":
         torch.cuda.empty_cache()
     lat_pts = latency_points(args, device, model, cfg) if args.headinfer_heads is None else {}
-    return dict(latency_point=lat_pts,value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
+    offload = {}
+    if kv is not None:
+        offload = dict(h_on=kv.h_on, h_off=kv.h_off, chunk_size=kv.chunk_size, h2d_gb=round(kv.bytes_h2d / 1e9, 3),
+                       d2h_gb=round(kv.bytes_d2h / 1e9, 3), transports=dict(kv.transports))
+    return dict(latency_point=lat_pts, offload=offload,value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
                 prefill_tps=B * L * args.prompt_len / prefill_s, build_s=t_build, graphs=graphs,
                 mem_gb=mem, partition=[0, cfg.num_layers], ttft_ms=ttft_ms, world_size=1, kv_gpu_gb=kv_gpu,
                 kv_host_gb=(kv.host_bytes() / 1e9 if kv is not None else 0.0))
@@ -280,6 +292,8 @@ def main(argv=None):
     for k in ("kv_gpu_gb", "kv_host_gb"):
         if k in res:
             out[k] = round(res[k], 3)
+    if res.get("offload"):
+        out["offload"] = res["offload"]
     if res.get("latency_point"):
         out["latency_point"] = res["latency_point"]
     if "per_rank" in res:

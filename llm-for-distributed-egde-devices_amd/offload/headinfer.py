@@ -87,6 +87,8 @@ class HeadInferKV:
         self.tags = [None, None]
         self.bytes_h2d = 0
         self.bytes_d2h = 0
+        self.transports = {}              # transport name -> copies (offload statistics, tests)
+        self.copy_mode = int(os.environ.get("EDGELLM_HEADINFER_COPY_MODE", "0"))   # 0 auto, 1 kernel, 2 dma
         self.attn_hook = self
 
     # -------------------------------------------------------------- KV-cache interface
@@ -105,7 +107,8 @@ class HeadInferKV:
 
     # -------------------------------------------------------------- transfers
     def _copy(self, dst, src):
-        ops.copy_head_block(dst, src)
+        t = ops.copy_head_block(dst, src, self.copy_mode)
+        self.transports[t] = self.transports.get(t, 0) + 1
         if _SYNC and self.cuda:
             torch.cuda.synchronize()
 

@@ -155,12 +155,18 @@ def rope_kv_write(qkv, start_pos, rope, k_cache, v_cache, num_heads, num_kv_head
                               k2, v2, split, cpos2)
 
 
-def copy_head_block(dst, src):
+COPY_TRANSPORTS = {0: "none", 1: "kernel", 2: "dma", 3: "torch"}
+
+
+def copy_head_block(dst, src, mode: int = 0) -> str:
     """Async strided copy of a [B, c, L, D] KV head block (pinned host <-> device) on the
-    current stream (native hipMemcpy2DAsync on GPU)."""
+    current stream.  ``mode`` 0 = auto (rows >= 64 KiB on the copy engines, shorter rows by the
+    copy kernel over mapped pinned memory), 1 = kernel, 2 = copy engines.  Returns the transport
+    used ("kernel" | "dma" | "torch" on CPU)."""
     if (dst.is_cuda or src.is_cuda) and not _REF_ON_GPU:
-        return ext().copy_head_block(dst, src)
+        return COPY_TRANSPORTS[int(ext().copy_head_block(dst, src, int(mode)))]
     dst.copy_(src)
+    return "torch"
 
 
 def decode_attention(q, k_cache, v_cache, seq_lens, scale, max_len_hint: Optional[int] = None):

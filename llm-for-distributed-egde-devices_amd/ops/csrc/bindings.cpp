@@ -40,7 +40,7 @@ int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, fl
 size_t edge_sample_workspace(int B, int V);
 int edge_sample_timestamps(int enable, unsigned long long* host_out16);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
-                         int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st);
+                         int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st, int mode, int* used);
 void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
@@ -643,7 +643,7 @@ std::vector<int64_t> sample_timestamps(bool enable) {
 // ---------------------------------------------------------------------------------- offload
 // dst/src: [B, c, L, D] views of head-major caches (last two dims contiguous), any mix of pinned
 // host and device memory; async on the current stream.
-void copy_head_block(at::Tensor& dst, const at::Tensor& src) {
+int64_t copy_head_block(at::Tensor& dst, const at::Tensor& src, int64_t mode) {
   TORCH_CHECK(dst.dim() == 4 && src.dim() == 4 && dst.sizes() == src.sizes(), "head blocks must match [B,c,L,D]");
   TORCH_CHECK(dst.scalar_type() == src.scalar_type());
   const int64_t D = dst.size(3), L = dst.size(2);
@@ -652,15 +652,18 @@ void copy_head_block(at::Tensor& dst, const at::Tensor& src) {
   TORCH_CHECK(dst.is_cuda() || dst.is_pinned(), "host side must be pinned");
   TORCH_CHECK(src.is_cuda() || src.is_pinned(), "host side must be pinned");
   const int es = (int)dst.element_size();
+  int used = 0;
   check(edge_copy_head_block(dst.data_ptr(), dst.stride(0), dst.stride(1), src.data_ptr(), src.stride(0),
-                             src.stride(1), (int)dst.size(0), (int)dst.size(1), L * D * es, es, stream()),
+                             src.stride(1), (int)dst.size(0), (int)dst.size(1), L * D * es, es, stream(), (int)mode,
+                             &used),
         "copy_head_block");
+  return used;          // 1: copy kernel over mapped memory, 2: copy engines (hipMemcpy2DAsync)
 }
 
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.def("copy_head_block", &copy_head_block);
+  m.def("copy_head_block", &copy_head_block, py::arg("dst"), py::arg("src"), py::arg("mode") = 0);
   m.doc() = "edgellm CDNA4 (gfx950) HIP kernels";
   m.def("norm", &norm);
   m.def("act", &act);

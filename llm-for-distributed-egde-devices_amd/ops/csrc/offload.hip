@@ -13,6 +13,11 @@
 //    the step.  Measured: see docs/BENCHMARKS.md (HeadInfer row).
 //  * dma (EDGE_HEADINFER_COPY=dma, or when a pointer is not device-mapped / not 16B aligned):
 //    one hipMemcpy2DAsync per batch row on the copy engines.
+// Auto choice (mode 0): rows of >= 64 KiB (the history prefetches of long contexts: a 32K-token
+// head row is 8 MiB) go to the copy engines (SDMA), so the CUs keep computing attention over the
+// resident heads while the next chunk streams in; short rows (the decode write-back of one new
+// token per head) take the one-launch kernel.  The return value reports the transport used
+// (1 kernel, 2 dma) so tests and the offload statistics can tell them apart.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -53,11 +58,13 @@ bool use_kernel() {
 
 extern "C" int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb,
                                     int64_t src_sh, int B, int heads, int64_t row_bytes, int elem_bytes,
-                                    hipStream_t st) {
+                                    hipStream_t st, int mode, int* used) {
+  *used = 0;
   if (B == 0 || heads == 0 || row_bytes == 0) return 0;
   const int64_t sb_d = dst_sb * elem_bytes, sh_d = dst_sh * elem_bytes;
   const int64_t sb_s = src_sb * elem_bytes, sh_s = src_sh * elem_bytes;
-  if (use_kernel() && (row_bytes | sb_d | sh_d | sb_s | sh_s) % 16 == 0) {
+  const bool want_kernel = mode == 1 || (mode == 0 && use_kernel() && row_bytes < (64 << 10));
+  if (want_kernel && (row_bytes | sb_d | sh_d | sb_s | sh_s) % 16 == 0) {
     void* dd = device_alias(dst);
     const void* ds = device_alias(src);
     if (dd && ds && (((uintptr_t)dd | (uintptr_t)ds) & 15) == 0 && (int64_t)B * heads <= INT32_MAX) {
@@ -65,6 +72,7 @@ extern "C" int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, c
       const int threads = row_vec >= 256 ? 256 : (row_vec >= 64 ? 64 : (int)((row_vec + 63) / 64) * 64);
       hipLaunchKernelGGL(head_block_copy_kernel, dim3((unsigned)(B * heads)), dim3(threads), 0, st, (uint4*)dd,
                          sb_d / 16, sh_d / 16, (const uint4*)ds, sb_s / 16, sh_s / 16, heads, row_vec);
+      *used = 1;
       return (int)hipGetLastError();
     }
   }
@@ -75,5 +83,6 @@ extern "C" int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, c
                                     hipMemcpyDefault, st);
     if (e != hipSuccess) return (int)e;
   }
+  *used = 2;
   return 0;
 }

@@ -53,15 +53,49 @@ def test_copy_head_block_kernel_both_directions(cuda, T):
     and a device buffer, against torch's copy of the same views (bit-exact)."""
     from edgellm import ops
     B, H, S, D, h0, c, p0 = 5, 8, 64, 128, 3, 4, 9
+    for mode, want in ((0, "kernel"), (1, "kernel"), (2, "dma")):
+        host = torch.randn(B, H, S, D, dtype=torch.bfloat16).pin_memory()
+        dev = torch.zeros(B, c, S, D, dtype=torch.bfloat16, device="cuda")
+        # short rows: auto picks the one-launch kernel; mode 2 forces the copy engines
+        assert ops.copy_head_block(dev[:, :, p0:p0 + T], host[:, h0:h0 + c, p0:p0 + T], mode) == want
+        torch.cuda.synchronize()
+        assert torch.equal(dev[:, :, p0:p0 + T].cpu(), host[:, h0:h0 + c, p0:p0 + T])
+        assert not dev[:, :, :p0].any() and not dev[:, :, p0 + T:].any()
+        src = torch.randn(B, c, T, D, dtype=torch.bfloat16, device="cuda")
+        before = host.clone()
+        assert ops.copy_head_block(host[:, h0:h0 + c, p0:p0 + T], src, mode) == want
+        torch.cuda.synchronize()
+        before[:, h0:h0 + c, p0:p0 + T] = src.cpu()
+        assert torch.equal(host, before)
+
+
+@pytest.mark.gpu
+def test_copy_head_block_long_rows_use_copy_engines(cuda):
+    """History rows >= 64 KiB (long contexts) go to the SDMA engines in auto mode, bit-exact."""
+    from edgellm import ops
+    B, H, S, D = 1, 4, 1024, 128                 # 1024 positions x 256 B = 256 KiB per head row
     host = torch.randn(B, H, S, D, dtype=torch.bfloat16).pin_memory()
-    dev = torch.zeros(B, c, S, D, dtype=torch.bfloat16, device="cuda")
-    ops.copy_head_block(dev[:, :, p0:p0 + T], host[:, h0:h0 + c, p0:p0 + T])
+    dev = torch.zeros(B, 2, S, D, dtype=torch.bfloat16, device="cuda")
+    assert ops.copy_head_block(dev, host[:, 1:3]) == "dma"
     torch.cuda.synchronize()
-    assert torch.equal(dev[:, :, p0:p0 + T].cpu(), host[:, h0:h0 + c, p0:p0 + T])
-    assert not dev[:, :, :p0].any() and not dev[:, :, p0 + T:].any()
-    src = torch.randn(B, c, T, D, dtype=torch.bfloat16, device="cuda")
-    before = host.clone()
-    ops.copy_head_block(host[:, h0:h0 + c, p0:p0 + T], src)
-    torch.cuda.synchronize()
-    before[:, h0:h0 + c, p0:p0 + T] = src.cpu()
-    assert torch.equal(host, before)
+    assert torch.equal(dev.cpu(), host[:, 1:3])
+
+
+@pytest.mark.gpu
+def test_headinfer_long_context_matches_resident(cuda):
+    """HeadInfer as a long-context mechanism: a 9K-token prompt prefilled in 2K chunks with ONE of
+    two KV heads per layer on the GPU (history prefetched from pinned host memory each chunk and
+    each decode step, SDMA for the long rows) decodes exactly the resident model's tokens."""
+    cfg = tiny("llama2", hidden_size=256, num_heads=2, num_kv_heads=2, num_layers=2, intermediate_size=512,
+               max_position_embeddings=16384)
+    m = build_model(cfg, device=cuda, seed=3)
+    T, new, chunk = 9000, 12, 2048
+    g = torch.Generator().manual_seed(0)
+    prompt = [torch.randint(0, cfg.vocab_size, (T,), generator=g).tolist()]
+    sp = SamplingParams(max_new_tokens=new, do_sample=False)
+    ref = Generator(m, max_batch=1, max_seq=T + new + 8, use_graphs=False, prefill_chunk=chunk).generate(prompt, sp)
+    kv = HeadInferKV(cfg, 1, T + new + 8, h_on=1, device=cuda, chunk_size=chunk)
+    got = Generator(m, max_batch=1, max_seq=T + new + 8, kv=kv).generate(prompt, sp)
+    assert got.tokens == ref.tokens
+    assert kv.transports.get("dma", 0) > 0 and kv.transports.get("kernel", 0) > 0
+    assert kv.host_bytes() > 0 and kv.gpu.nbytes() == kv.host_bytes()      # 1 of 2 heads resident
