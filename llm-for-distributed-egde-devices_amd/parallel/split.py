@@ -169,7 +169,16 @@ def agent_devices(gpus: Optional[List[int]], fallback: torch.device, pp_size: in
     if gpus:
         if not torch.cuda.is_available():
             return [torch.device("cpu")]
-        return [torch.device("cuda", int(g)) for g in gpus]
+        n = torch.cuda.device_count()
+        if max(int(g) for g in gpus) >= n:
+            from ..utils.log import get_logger
+            get_logger("split").warning(f"gpus {list(gpus)} on a {n}-GPU host: folded modulo {n}")
+        out: List[torch.device] = []
+        for g in gpus:                       # fold onto the visible GPUs, drop repeats in order
+            d = torch.device("cuda", int(g) % n)
+            if d not in out:
+                out.append(d)
+        return out
     if pp_size > 1 and fallback.type == "cuda":
         n = torch.cuda.device_count()
         return [torch.device("cuda", ((fallback.index or 0) + i) % n) for i in range(pp_size)]
