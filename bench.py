@@ -36,6 +36,7 @@ from edgellm.engine.generate import LaneGenerator  # noqa: E402
 from edgellm.models import build_model, get_config, tiny  # noqa: E402
 from edgellm.quant import quantize_model, synthetic_calibration  # noqa: E402
 from edgellm.quant.smoothquant import smoothquant_stage  # noqa: E402
+from edgellm.utils.tracing import MetricsWriter, trace_range  # noqa: E402
 
 METRIC = "tokens/sec (whole node) + p50 per-token latency, Llama-2-7B INT8 split 1/2/4/8"
 # no published value for this metric; the closest published point is the reference's
@@ -69,6 +70,8 @@ def parse(argv=None):
                     help="chunked prefill size with HeadInfer (default: the whole prompt in one chunk)")
     ap.add_argument("--headinfer-heads", type=int, default=None,
                     help="HeadInfer: KV heads per layer kept on the GPU, the rest offloaded to pinned host memory")
+    ap.add_argument("--metrics-out", default=os.environ.get("EDGELLM_METRICS"),
+                    help="append the result record (plus HBM peak) to this JSONL file")
     return ap.parse_args(argv)
 
 
@@ -144,8 +147,9 @@ def run_single(args):
     lanes = gen.lanes if L > 1 else [gen]
     n_ev = [len(x._run["events"]) for x in lanes]
     t0 = time.perf_counter()
-    gen.step(args.steps, record_latency=device.type == "cuda")
-    _sync(device)
+    with trace_range("bench.timed"):
+        gen.step(args.steps, record_latency=device.type == "cuda")
+        _sync(device)
     dt = time.perf_counter() - t0
     lat = []
     for x, n0 in zip(lanes, n_ev):
@@ -300,6 +304,7 @@ def main(argv=None):
         out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
         out["per_rank"] = res["per_rank"]
     print(json.dumps(out), flush=True)
+    MetricsWriter(args.metrics_out).write(event="bench", **out)
     return out
 
 

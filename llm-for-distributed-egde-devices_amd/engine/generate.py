@@ -18,6 +18,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 
 from .. import ops
+from ..utils.tracing import debug_sync, trace_range
 from ..models.decoder import AttnCtx, DecoderLM
 from .kv_cache import KVCache
 
@@ -137,7 +138,10 @@ class Generator:
         sp = torch.full((B,), start, dtype=torch.int32, device=self.device)
         ctx = AttnCtx("prefill", B, T, sp, sp + T, start + T, self.kv.rows(row0, row0 + B), self.rope,
                       attn_hook=self.attn_hook)
-        return self.model(ids, ctx)
+        with trace_range(f"prefill.B{B}.T{T}"):
+            out = self.model(ids, ctx)
+        debug_sync("prefill")
+        return out
 
     def _decode_step(self, st: _DecodeState, B: int, max_len: int, sp: SamplingParams):
         ctx = AttnCtx("decode", B, 1, st.pos, st.seq_lens, max_len, self.kv.rows(0, B), self.rope,
@@ -235,14 +239,16 @@ class Generator:
             if r["produced"] >= sampling.max_new_tokens:
                 break
             max_len = r["host_max"] + 1
-            if r["graphs_ok"]:
-                bucket = min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
-                if not self._graphs:
-                    self._decode_step(st, B, bucket, sampling)      # warm-up step (a real step)
+            with trace_range(f"decode.B{B}"):
+                if r["graphs_ok"]:
+                    bucket = min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
+                    if not self._graphs:
+                        self._decode_step(st, B, bucket, sampling)      # warm-up step (a real step)
+                    else:
+                        self._graph_for(st, B, bucket, sampling).replay()
                 else:
-                    self._graph_for(st, B, bucket, sampling).replay()
-            else:
-                self._decode_step(st, B, max_len, sampling)
+                    self._decode_step(st, B, max_len, sampling)
+            debug_sync("decode step")
             if record_latency and r["cuda"]:
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()

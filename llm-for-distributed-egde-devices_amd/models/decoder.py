@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..utils import tracing
 from .configs import ModelConfig
 from .layers import Linear, Norm, PartialSum, QAct, act_fn, quant_if
 
@@ -253,6 +254,11 @@ class DecoderLM(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward_layers(self, x: torch.Tensor, ctx: AttnCtx, residual: Optional[torch.Tensor] = None):
+        if tracing.TRACE:                      # roctx range per layer (rocprofv3 --marker-trace)
+            for layer in self.layers:
+                with tracing.trace_range(f"{ctx.mode}.layer{layer.idx}"):
+                    x, residual = layer(x, residual, ctx)
+            return x, residual
         for layer in self.layers:
             x, residual = layer(x, residual, ctx)
         return x, residual

@@ -9,6 +9,7 @@ through ``metrics()``.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -16,12 +17,15 @@ from concurrent.futures import Future
 from typing import Dict, List, Optional
 
 from ..engine.generate import Generator, SamplingParams
-from ..utils.tracing import LatencyHistogram
+from ..utils.tracing import LatencyHistogram, MetricsWriter, trace_range
 
 
 class ServingEngine:
-    def __init__(self, generator: Generator, tokenizer, max_batch: int = 8, batch_wait_s: float = 0.005):
+    def __init__(self, generator: Generator, tokenizer, max_batch: int = 8, batch_wait_s: float = 0.005,
+                 metrics_path: Optional[str] = None):
         self.gen, self.tok = generator, tokenizer
+        # one JSONL record per served batch (EDGELLM_METRICS=<path> or metrics_path)
+        self.writer = MetricsWriter(metrics_path or os.environ.get("EDGELLM_METRICS"))
         self.max_batch = min(max_batch, generator.kv.max_batch)
         self.batch_wait_s = batch_wait_s
         self.q: "queue.Queue[tuple]" = queue.Queue()
@@ -86,7 +90,9 @@ class ServingEngine:
         prompts = [b[0] for b in batch]
         sp = batch[0][1]
         try:
-            res = self.gen.generate(prompts, sp, seed=batch[0][2], eos_token_id=getattr(self.tok, "eos_token_id", None))
+            with trace_range(f"serve.batch{len(batch)}"):
+                res = self.gen.generate(prompts, sp, seed=batch[0][2],
+                                        eos_token_id=getattr(self.tok, "eos_token_id", None))
         except Exception as e:  # report to every caller, keep serving
             self.stats["errors"] += 1
             for b in batch:
@@ -95,6 +101,11 @@ class ServingEngine:
         self.stats["batches"] += 1
         steps = max((len(t) for t in res.tokens), default=0)
         self.lat.extend(res.step_ms or ([res.elapsed_s * 1e3 / steps] if steps else []))
+        step = sorted(res.step_ms)
+        self.writer.write(event="batch", batch_size=len(batch), prompt_tokens=sum(len(p) for p in prompts),
+                          generated_tokens=sum(len(t) for t in res.tokens), ttft_ms=res.prefill_s * 1e3,
+                          elapsed_s=res.elapsed_s, p50_step_ms=step[len(step) // 2] if step else None,
+                          max_queue_ms=max((time.perf_counter() - b[4]) * 1e3 for b in batch))
         for i, b in enumerate(batch):
             toks = res.tokens[i]
             self.stats["requests"] += 1

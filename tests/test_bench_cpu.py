@@ -42,6 +42,18 @@ def test_bench_single_cpu(lanes):
     assert d["config"]["lanes"] == lanes
 
 
+def test_bench_metrics_out_and_tracing_cpu(tmp_path):
+    """--metrics-out appends the result record; EDGELLM_TRACE / EDGELLM_SYNC_DEBUG paths run."""
+    path = tmp_path / "m.jsonl"
+    env = dict(os.environ, EDGELLM_TRACE="1", EDGELLM_SYNC_DEBUG="1")
+    r = subprocess.run([sys.executable, "bench.py", *COMMON, "--lanes", "1", "--metrics-out", str(path)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    rec = json.loads(path.read_text().splitlines()[-1])
+    assert rec["event"] == "bench" and rec["value"] == d["value"] and rec["metric"] == d["metric"]
+
+
 @pytest.mark.parametrize("n,lanes", [(2, 1), (2, 2), (3, 2), (4, 2), (8, 1), (8, 2)])
 def test_bench_pipeline_torchrun_cpu(n, lanes):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",

@@ -1,6 +1,7 @@
 """Serving / comm layer on CPU: TimeService + REST compatibility with the reference demo
 (Code/gRPC/*), and the BASELINE.json CPU config — a GPT-2 2-stage layer split over localhost
 gRPC — checked token-for-token against the single-process engine, with injected drops."""
+import json
 import re
 
 import pytest
@@ -86,7 +87,7 @@ def test_gpt2_two_stage_grpc_matches_single_process(do_sample, faults):
         server.stop(0)
 
 
-def test_serving_engine_batches_concurrent_requests():
+def test_serving_engine_batches_concurrent_requests(tmp_path):
     import threading
     from fastapi.testclient import TestClient
     from edgellm.serve.rest import make_app
@@ -94,8 +95,9 @@ def test_serving_engine_batches_concurrent_requests():
     from edgellm.utils.tokenizer import ByteTokenizer
     cfg = tiny("llama")
     m = build_model(cfg, dtype=torch.float32, seed=2)
+    mpath = tmp_path / "serve_metrics.jsonl"
     eng = ServingEngine(Generator(m, max_batch=4, max_seq=128), ByteTokenizer(cfg.vocab_size), max_batch=4,
-                        batch_wait_s=0.05)
+                        batch_wait_s=0.05, metrics_path=str(mpath))
     try:
         sp = SamplingParams(max_new_tokens=5, do_sample=False)
         futs = [eng.submit([1, 2, 3 + i], sp) for i in range(4)]
@@ -109,6 +111,9 @@ def test_serving_engine_batches_concurrent_requests():
         r = c.post("/generate", json={"prompt": "hello", "max_new_tokens": 3, "do_sample": False})
         assert r.status_code == 200 and len(r.json()["tokens"]) == 3
         assert c.get("/metrics").json()["requests"] == 5
+        recs = [json.loads(l) for l in mpath.read_text().splitlines()]     # one JSONL record per batch
+        assert len(recs) == eng.metrics()["batches"] and sum(r["batch_size"] for r in recs) == 5
+        assert all(r["event"] == "batch" and r["ttft_ms"] > 0 and r["generated_tokens"] > 0 for r in recs)
     finally:
         eng.close()
 
