@@ -617,6 +617,188 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
     }
 }
 
+// LDS byte address of a __shared__ pointer, and a ds_read_b128 the compiler does not track (callers
+// order it with explicit lgkmcnt waits; see the ring kernel below)
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
+}
+__device__ __forceinline__ v4i lds_read16(uint32_t addr) {
+  v4i r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
+// ------------------------------------------------------------------------------------ big
+// Prefill GEMM (M > 128, K % 64 == 0, N % 8 == 0): BM x 256 block tile (BM = 256, or 128 when
+// 256-row tiles would leave CUs idle), 8 waves as 2 (M) x 4 (N), BK = 64, one block per CU.
+//  * Both operands go global -> LDS by global_load_lds into a ring of R = 4 stages (BM/16 + 16 KiB
+//    each; 128 KiB at BM = 256): 3 stages of DMA stay in flight across every barrier (counted
+//    vmcnt, bare s_barrier, LDS reads by inline asm so the compiler never drains the ring with a
+//    vmcnt(0) — the structure of the 128-row decode ring kernel below).
+//  * Fragments are double-buffered in registers: iteration s reads stage s + 1's fragments while
+//    the MFMAs consume stage s's, so LDS latency hides under 32 MFMAs per wave.
+//  * Operands are swapped in the MFMA (W tile as the A operand, activations as B), so the
+//    accumulator of a lane holds 4 consecutive output COLUMNS of one row: the epilogue scales,
+//    packs 4 bf16 into 8 bytes, and restages the wave's tile through LDS (XOR-swizzled 16-B
+//    chunks) to write full 128-B row segments with 16-B stores.
+//  * blockIdx -> tile: bijective XCD remap (each XCD gets a contiguous range), then groups of 4
+//    row tiles walked column-major, so an XCD's ~32 resident blocks share 4 A panels and 8 W panels
+//    in its L2.
+template <int BMV>
+__global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                              const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                              const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                              int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
+  constexpr int R = 4, BNV = 256, NWV = 8;
+  constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
+  constexpr int MI = BMV / 32, NJ = 4;                        // row blocks / column tiles per wave
+  static_assert(PIECES % NWV == 0, "pieces per wave");
+  static_assert(R * STAGE <= 160 * 1024 && NWV * (BMV / 2) * 128 <= R * STAGE, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  constexpr int GM = 4;
+  const int per_group = GM * grid_n;
+  const int grp = wgid / per_group, gm0 = grp * GM, gsz = min(GM, grid_m - gm0);
+  const int inr = wgid - grp * per_group;
+  const int bm = gm0 + inr % gsz, bn = inr / gsz;
+
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // this wave's DMA pieces p = wave + 8 i: A row block p (p < AP) or W tile p - AP
+  const int8_t* src[PPW];
+  int stride[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int p = wave + NWV * i;
+    if (p < AP) {
+      const int row = min(bm * BMV + p * 16 + (lane & 15), M - 1);
+      src[i] = A + (size_t)row * K + 16 * (lane >> 4);
+      stride[i] = 64;
+    } else {
+      const int t = min(bn * BP + (p - AP), NTt - 1);
+      src[i] = Wp + (size_t)t * KT * 1024 + lane * 16;
+      stride[i] = 1024;
+    }
+  }
+  auto issue = [&](int st) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+      glds16(src[i] + (size_t)st * stride[i], ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
+  };
+  // own DMA of stage `st` landed, `ahead` younger stages may stay in flight
+  auto wait_stage = [&](int ahead) {
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  const uint32_t ring0 = lds_off(ring) + lane * 16;
+  auto read_frags = [&](int st, v4i (&fw)[NJ], v4i (&fa)[MI]) {
+    const uint32_t base = ring0 + (st % R) * STAGE;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) fw[j] = lds_read16(base + (AP + wn * NJ + j) * 1024);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = lds_read16(base + (wm * MI + i) * 1024);
+  };
+  auto pin = [&](v4i (&fw)[NJ], v4i (&fa)[MI]) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(fw[j]));
+#pragma unroll
+    for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(fa[i]));
+  };
+
+  v4i acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  auto mma = [&](const v4i (&fw)[NJ], const v4i (&fa)[MI]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_i8(fw[j], fa[i], acc[i][j]);
+  };
+
+  // prologue: R stages in flight, stage 0's fragments in registers
+#pragma unroll
+  for (int st = 0; st < R; ++st)
+    if (st < KT) issue(st);
+  v4i w0[NJ], a0[MI], w1[NJ], a1[MI];
+  {
+    const int ahead = min(R - 1, KT - 1);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
+    else wait_stage(ahead);
+  }
+  __builtin_amdgcn_s_barrier();
+  read_frags(0, w0, a0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pin(w0, a0);
+
+  // iteration s: stage s + 1 -> (w_nxt, a_nxt) while the MFMAs consume (w_cur, a_cur)
+  auto step = [&](int s, v4i (&wc)[NJ], v4i (&ac)[MI], v4i (&wx)[NJ], v4i (&ax)[MI]) {
+    const bool more = s + 1 < KT;                     // wave-uniform
+    if (more) {
+      wait_stage(min(R - 2, KT - 2 - s));
+      __builtin_amdgcn_s_barrier();                   // stage s + 1 landed everywhere; slot of s free
+      if (s + R < KT) issue(s + R);
+      read_frags(s + 1, wx, ax);
+    }
+    mma(wc, ac);
+    if (more) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pin(wx, ax);
+    }
+  };
+  int s = 0;
+  for (; s + 1 < KT; s += 2) {
+    step(s, w0, a0, w1, a1);
+    step(s + 1, w1, a1, w0, a0);
+  }
+  if (s < KT) step(s, w0, a0, w1, a1);
+
+  // epilogue: lane holds out[row = rb*16 + (lane & 15)][col = tile*16 + 4 (lane >> 4) + r]
+  const int g4 = lane >> 4, r16 = lane & 15;
+  float swv[NJ][4], bv[NJ][4], sav[MI];
+  const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = min(bn * BNV + (wn * NJ + j) * 16 + 4 * g4 + r, N - 1);
+      swv[j][r] = sw[col];
+      bv[j][r] = bf2f(bp[bias != nullptr ? col : 0]);   // absent bias: a zero word, no branch
+    }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) sav[i] = sa[min(bm * BMV + (wm * MI + i) * 16 + r16, M - 1)];
+  __syncthreads();                                    // every wave is done with the ring
+  // wave tile [MI*16 rows][64 cols] bf16, 128-B rows, 16-B chunk c of row m at c ^ (m & 7)
+  int8_t* wt = ring + wave * (MI * 16 * 128);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = i * 16 + r16;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (float)acc[i][j][r] * sav[i] * swv[j][r] + bv[j][r];
+      const int c16 = 2 * j + (g4 >> 1);
+      uint2 pk{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+      *reinterpret_cast<uint2*>(wt + m * 128 + ((c16 ^ (m & 7)) << 4) + (g4 & 1) * 8) = pk;
+    }
+  }
+  // (a wave's LDS operations complete in issue order: no wait between its writes and reads)
+#pragma unroll
+  for (int it = 0; it < MI * 2; ++it) {
+    const int m = it * 8 + (lane >> 3), c = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(wt + m * 128 + ((c ^ (m & 7)) << 4));
+    const int row = bm * BMV + wm * MI * 16 + m, col = bn * BNV + wn * 64 + c * 8;
+    if (row < M && col < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col) = v;   // N % 8 == 0
+  }
+}
+
 // ------------------------------------------------------------------------------------- ring
 // 65-128 decode rows (two micro-batches or one 128-row micro-batch) on an LDS-DMA ring.
 // The ldsa kernel above stages activations through VGPRs (global load -> ds_write -> barrier) with
@@ -637,14 +819,6 @@ __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __res
 // apart, and for a plain LDS load (or a fenced __syncthreads) it would wait for EVERY outstanding
 // LDS-DMA (vmcnt(0)), draining the ring each stage.  Ordering is explicit instead: counted vmcnt
 // for this wave's own DMA, a bare s_barrier for the other waves', lgkmcnt(0) before the MFMAs.
-__device__ __forceinline__ uint32_t lds_off(const void* p) {
-  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
-}
-__device__ __forceinline__ v4i lds_read16(uint32_t addr) {
-  v4i r;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
 
 template <int NTW, int C, int R, bool SCALED, int EPI>
 __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
@@ -835,6 +1009,9 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 }  // namespace
 
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 1;
+// prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
+static int g_prefill_gemm = 0;
+extern "C" void edge_w8a8_prefill_gemm(int v) { g_prefill_gemm = v; }
 // tuning hooks (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int kw, int unroll) { g_gemv_kw = kw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
@@ -1036,6 +1213,20 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     if (mblocks <= 1) return launch_one<1, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
     if (mblocks <= 2) return launch_one<2, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
     return launch_one<4, 4, 2, 4, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
+  }
+  if (M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1) {
+    // 256 x 256 tiles when they fill the chip (>= 256 blocks), else 128 x 256
+    const int grid_n = (NTt * 16 + 255) / 256;
+    const int g256 = (M + 255) / 256, g128 = (M + 127) / 128;
+    const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && g256 * grid_n >= 256);
+    const int grid_m = big ? g256 : g128;
+    if (big)
+      hipLaunchKernelGGL(w8a8_gemm_big_kernel<256>, dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n);
+    else
+      hipLaunchKernelGGL(w8a8_gemm_big_kernel<128>, dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n);
+    return (int)hipGetLastError();
   }
   if (M > 64 && K % 64 == 0 && K / 64 == KT) {
     const int grid_n = (NTt * 16 + BN - 1) / BN;

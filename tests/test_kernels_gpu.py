@@ -171,6 +171,50 @@ def test_w8a8_gemm(cuda, M, N, K):
     _close(out, ref, 1e-2, 1e-2)
 
 
+PREFILL_FORMS = {"auto": 0, "tiled128": 1, "ring256": 2, "ring128": 3}
+
+
+@pytest.mark.parametrize("form", list(PREFILL_FORMS))
+@pytest.mark.parametrize("M,N,K", [(300, 272, 64), (129, 1040, 192), (1000, 520, 128), (640, 4096, 256)])
+def test_w8a8_prefill_layout_exact(cuda, form, M, N, K):
+    """Exact integers through every prefill GEMM form: row m of A selects column (7m mod K), so
+    out[m] must equal that column of an asymmetric W — catches swapped operands, a wrong
+    LDS-restaged store, ring slots read early (1..4 k-tiles: every prologue/tail wait) and
+    ragged M / N tiles."""
+    C = ops.ext()
+    a = torch.zeros(M, K, dtype=torch.int8, device=cuda)
+    sel = (torch.arange(M, device=cuda) * 7) % K
+    a[torch.arange(M, device=cuda), sel] = 1
+    w = (torch.arange(N * K, device=cuda).view(N, K) % 113 - 56).to(torch.int8)
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("prefill_gemm", PREFILL_FORMS[form], 0)
+        out = C.w8a8_gemm(a, torch.ones(M, device=cuda), wp, torch.ones(N, device=cuda), None, N, K)
+    finally:
+        C.tune("prefill_gemm", 0, 0)
+    assert torch.equal(out.float(), w[:, sel].t().float())
+
+
+@pytest.mark.parametrize("form", list(PREFILL_FORMS))
+@pytest.mark.parametrize("M,N,K", [(2100, 4096, 4096), (777, 11008, 4096), (520, 4096, 11008)])
+def test_w8a8_prefill_gemm(cuda, form, M, N, K):
+    """Random int8 operands, per-token / per-channel scales and bias vs the fp32 reference."""
+    C = ops.ext()
+    g = torch.Generator(device=cuda).manual_seed(M + N)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda, generator=g)
+    sx = torch.rand(M, device=cuda, generator=g) * 0.02 + 1e-3
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda, generator=g)
+    sw = torch.rand(N, device=cuda, generator=g) * 0.02 + 1e-3
+    bias = torch.randn(N, device=cuda, generator=g).bfloat16()
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("prefill_gemm", PREFILL_FORMS[form], 0)
+        out = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+    finally:
+        C.tune("prefill_gemm", 0, 0)
+    _close(out, _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32), 1e-2, 1e-2)
+
+
 @pytest.mark.parametrize("ntw,nw,u", [(2, 4, 2), (4, 8, 4), (4, 16, 2), (2, 16, 4)])
 @pytest.mark.parametrize("M,N,K", [(16, 160, 96), (7, 22016, 4096), (16, 4096, 11008), (3, 1040, 128),
                                    (33, 4096, 4096), (64, 12288, 4096), (50, 1040, 128)])

@@ -253,15 +253,38 @@ def prefill_rows(C, dev, Hq, D):
         t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=20)
         flops = 4 * T * T * D * Hq / 2
         out.append(dict(op="prefill_attn_causal", T=T, H=Hq, D=D, us=round(t, 2), TFLOPs=round(flops / t / 1e6, 1)))
-    # tiled int8 GEMM (prefill)
-    for M in (512, 2048):
-        N, K = 12288, 4096
-        a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+    out += prefill_gemm_rows(C, dev)
+    return out
+
+
+def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
+    """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
+    interleaved in one process (0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the LDS-DMA
+    ring kernel at 256 / 128 rows per block)."""
+    out = []
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
+    forms = {"auto": 0, "tiled128": 1, "ring256": 2, "ring128": 3}
+    for name, (N, K) in shapes.items():
         w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
         wp = ops.pack_int8_weight(w)
-        s1, s2 = torch.rand(M, device=dev), torch.rand(N, device=dev)
-        t = timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K), iters=20)
-        out.append(dict(op="w8a8_gemm_tiled", M=M, N=N, K=K, us=round(t, 2), TOPs=round(2 * M * N * K / t / 1e6, 1)))
+        s2 = torch.rand(N, device=dev) * 0.01
+        for M in Ms:
+            a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            s1 = torch.rand(M, device=dev) * 0.01
+            res = {}
+            for rnd in range(2):
+                for form, v in forms.items():
+                    C.tune("prefill_gemm", v, 0)
+                    per = max(2, min(20, int(4e11 // (M * N * K))))
+                    res.setdefault(form, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K),
+                                                           iters=5, per_graph=per))
+            C.tune("prefill_gemm", 0, 0)
+            row = dict(op="w8a8_gemm_prefill", shape=name, M=M, N=N, K=K)
+            for form, ts in res.items():
+                row[form + "_us"] = round(min(ts), 1)
+                row[form + "_TOPs"] = round(2 * M * N * K / min(ts) / 1e6, 1)
+            out.append(row)
+            print(row, flush=True)
     return out
 
 
@@ -270,7 +293,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--tune", action="append", default=[], help="name=a[,b] passed to ext().tune (repeatable)")
-    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill,pgemm")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
@@ -287,6 +310,8 @@ def main():
     if only is None or "glu" in only:
         rows += glu_rows(C, dev)
     rows += other_rows(C, dev, only)
+    if only is not None and "pgemm" in only:
+        rows += prefill_gemm_rows(C, dev)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
