@@ -28,9 +28,11 @@
 //   ldsa:  gemv with the activations staged through LDS once per workgroup and one tile per
 //          wave: the 33-128 row GLUQ at K = 4096, and every projection at 65-128 rows (two
 //          decode micro-batches in one) for the k-tile counts of 4096-hidden models.
-//   tiled: M > 64 (prefill). 128x128 block tile, BK=64, 4 waves in 2x2, A and B staged with
-//          global_load_lds (16 B/lane, lane-linear fragment-ordered LDS images -> conflict-free
-//          ds_read_b128), LDS double buffer.
+//   big:   M > 128 (prefill). 128x256 / 256x256 block tile, 8 waves, BK=64, a 4-stage
+//          global_load_lds ring (counted vmcnt, bare barriers), register-double-buffered
+//          fragments, LDS-restaged 16-B store epilogue (see the kernel).
+//   tiled: 65-128 rows without a decode kernel, ragged shapes. 128x128 block tile, 4 waves in
+//          2x2, both operands staged with global_load_lds, LDS double buffer.
 #include "common.h"
 #include <type_traits>
 
@@ -628,6 +630,17 @@ __device__ __forceinline__ v4i lds_read16(uint32_t addr) {
   return r;
 }
 
+// n ds_read_b128 at addr + 1024 i (immediate offsets: no address VALU, no extra VGPRs)
+template <int I, int N>
+__device__ __forceinline__ void lds_read_row_(uint32_t addr, v4i (&f)[N]) {
+  if constexpr (I < N) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[I]) : "v"(addr), "n"(I * 1024));
+    lds_read_row_<I + 1, N>(addr, f);
+  }
+}
+template <int N>
+__device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_read_row_<0, N>(addr, f); }
+
 // ------------------------------------------------------------------------------------ big
 // Prefill GEMM (M > 128, K % 64 == 0, N % 8 == 0): BM x 256 block tile (BM = 256, or 128 when
 // 256-row tiles would leave CUs idle), 8 waves as 2 (M) x 4 (N), BK = 64, one block per CU.
@@ -653,7 +666,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
   constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
   constexpr int MI = BMV / 32, NJ = 4;                        // row blocks / column tiles per wave
   static_assert(PIECES % NWV == 0, "pieces per wave");
-  static_assert(R * STAGE <= 160 * 1024 && NWV * (BMV / 2) * 128 <= R * STAGE, "LDS budget");
+  static_assert(R * STAGE <= 160 * 1024 && NWV * (BMV / 4) * 256 <= R * STAGE, "LDS budget");
   __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
 
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -668,40 +681,42 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // this wave's DMA pieces p = wave + 8 i: A row block p (p < AP) or W tile p - AP
-  const int8_t* src[PPW];
-  int stride[PPW];
+  // this wave's DMA pieces p = wave + 8 i: A row block p (p < AP) or W tile p - AP.  Per-lane
+  // 32-bit offsets from the (wave-uniform) operand base: one VGPR per piece, SGPR base + VGPR
+  // offset addressing (M * K and the packed W stay below 4 GiB)
+  uint32_t off[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int p = wave + NWV * i;
     if (p < AP) {
       const int row = min(bm * BMV + p * 16 + (lane & 15), M - 1);
-      src[i] = A + (size_t)row * K + 16 * (lane >> 4);
-      stride[i] = 64;
+      off[i] = (uint32_t)row * (uint32_t)K + 16 * (lane >> 4);
     } else {
       const int t = min(bn * BP + (p - AP), NTt - 1);
-      src[i] = Wp + (size_t)t * KT * 1024 + lane * 16;
-      stride[i] = 1024;
+      off[i] = (uint32_t)t * (uint32_t)KT * 1024u + lane * 16;
     }
   }
+  // DMA of stage st into slot st % R.  Stages past the last k-tile re-load the last k-tile into
+  // their slot (never read again: every stage still to be read sits in another slot), so every
+  // stage is PPW pieces per wave, the loop is branch-free and the vmcnt counts are constants.
   auto issue = [&](int st) {
+    const int kt = min(st, KT - 1);
+    const int8_t* ab = A + (size_t)kt * 64;
+    const int8_t* wb = Wp + (size_t)kt * 1024;
 #pragma unroll
-    for (int i = 0; i < PPW; ++i)
-      glds16(src[i] + (size_t)st * stride[i], ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
+    for (int i = 0; i < PPW; ++i) {
+      const bool isa = wave + NWV * i < AP;             // compile-time per i when AP % 8 == 0
+      glds16((isa ? ab : wb) + off[i], ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
+    }
   };
-  // own DMA of stage `st` landed, `ahead` younger stages may stay in flight
-  auto wait_stage = [&](int ahead) {
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
+  // fragment reads: one VGPR base per operand and slot, immediate offsets
   const uint32_t ring0 = lds_off(ring) + lane * 16;
+  const uint32_t wbase = ring0 + (AP + wn * NJ) * 1024, abase = ring0 + wm * MI * 1024;
   auto read_frags = [&](int st, v4i (&fw)[NJ], v4i (&fa)[MI]) {
-    const uint32_t base = ring0 + (st % R) * STAGE;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) fw[j] = lds_read16(base + (AP + wn * NJ + j) * 1024);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = lds_read16(base + (wm * MI + i) * 1024);
+    const uint32_t so = (st % R) * STAGE;
+    const uint32_t wb = wbase + so, ab = abase + so;
+    lds_read_row<NJ>(wb, fw);
+    lds_read_row<MI>(ab, fa);
   };
   auto pin = [&](v4i (&fw)[NJ], v4i (&fa)[MI]) {
 #pragma unroll
@@ -715,87 +730,100 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
-  auto mma = [&](const v4i (&fw)[NJ], const v4i (&fa)[MI]) {
+  // fragments pinned after the reads that precede this call, accumulators pinned after the
+  // MFMAs: the MFMAs sit between the fragment reads and the next lgkmcnt wait (left alone,
+  // hipcc hoists the wait above them and the LDS latency is exposed every k-tile)
+  auto mma = [&](v4i (&fw)[NJ], v4i (&fa)[MI]) {
+    pin(fw, fa);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_i8(fw[j], fa[i], acc[i][j]);
   };
+  auto pin_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(acc[i][j]));
+  };
 
   // prologue: R stages in flight, stage 0's fragments in registers
 #pragma unroll
-  for (int st = 0; st < R; ++st)
-    if (st < KT) issue(st);
+  for (int st = 0; st < R; ++st) issue(st);
   v4i w0[NJ], a0[MI], w1[NJ], a1[MI];
-  {
-    const int ahead = min(R - 1, KT - 1);
-    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
-    else wait_stage(ahead);
-  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 1) * PPW) : "memory");
   __builtin_amdgcn_s_barrier();
   read_frags(0, w0, a0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  pin(w0, a0);
 
-  // iteration s: stage s + 1 -> (w_nxt, a_nxt) while the MFMAs consume (w_cur, a_cur)
-  auto step = [&](int s, v4i (&wc)[NJ], v4i (&ac)[MI], v4i (&wx)[NJ], v4i (&ax)[MI]) {
-    const bool more = s + 1 < KT;                     // wave-uniform
-    if (more) {
-      wait_stage(min(R - 2, KT - 2 - s));
-      __builtin_amdgcn_s_barrier();                   // stage s + 1 landed everywhere; slot of s free
-      if (s + R < KT) issue(s + R);
-      read_frags(s + 1, wx, ax);
-    }
+  // k-tile s < KT - 1: stage s + 1's fragments -> (wx, ax) while the MFMAs consume (wc, ac):
+  // reads -> MFMAs -> lgkmcnt(0), the wave's own MFMAs cover the LDS latency (measured 3-8 %
+  // faster than reads -> lgkmcnt(0) -> MFMAs, where only the SIMD's other wave covers it)
+  auto full = [&](int s, v4i (&wc)[NJ], v4i (&ac)[MI], v4i (&wx)[NJ], v4i (&ax)[MI]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 2) * PPW) : "memory");   // own DMA of s + 1
+    __builtin_amdgcn_s_barrier();                     // stage s + 1 landed everywhere; slot of s free
+    issue(s + R);
+    read_frags(s + 1, wx, ax);
     mma(wc, ac);
-    if (more) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      pin(wx, ax);
-    }
+    pin_acc();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   int s = 0;
-  for (; s + 1 < KT; s += 2) {
-    step(s, w0, a0, w1, a1);
-    step(s + 1, w1, a1, w0, a0);
+  for (; s + 2 < KT; s += 2) {
+    full(s, w0, a0, w1, a1);
+    full(s + 1, w1, a1, w0, a0);
   }
-  if (s < KT) step(s, w0, a0, w1, a1);
+  if (s + 1 < KT) {
+    full(s, w0, a0, w1, a1);
+    mma(w1, a1);
+  } else {
+    mma(w0, a0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-load stages past the end
 
-  // epilogue: lane holds out[row = rb*16 + (lane & 15)][col = tile*16 + 4 (lane >> 4) + r]
-  const int g4 = lane >> 4, r16 = lane & 15;
-  float swv[NJ][4], bv[NJ][4], sav[MI];
+  // epilogue: lane holds int32 out[row = rb*16 + (lane & 15)][col = tile*16 + 4 (lane >> 4) + r].
+  // The raw accumulators go to LDS first (one 16-B write per tile, freeing their registers), in
+  // halves of MI/2 row blocks per wave ([MI*8 rows][64 cols] int32, 256-B rows, 16-B chunk c of
+  // row m at c ^ (m & 15): conflict-free); each lane then owns 8 consecutive columns (its scales
+  // and bias loaded once), scales, packs bf16 and writes 16 B.
+  const int r16 = lane & 15, g4 = lane >> 4, c8 = lane & 7;
+  const int col0 = bn * BNV + wn * 64 + c8 * 8;
   const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
+  float swv[8], bv[8];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int col = min(bn * BNV + (wn * NJ + j) * 16 + 4 * g4 + r, N - 1);
-      swv[j][r] = sw[col];
-      bv[j][r] = bf2f(bp[bias != nullptr ? col : 0]);   // absent bias: a zero word, no branch
-    }
-#pragma unroll
-  for (int i = 0; i < MI; ++i) sav[i] = sa[min(bm * BMV + (wm * MI + i) * 16 + r16, M - 1)];
-  __syncthreads();                                    // every wave is done with the ring
-  // wave tile [MI*16 rows][64 cols] bf16, 128-B rows, 16-B chunk c of row m at c ^ (m & 7)
-  int8_t* wt = ring + wave * (MI * 16 * 128);
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = i * 16 + r16;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (float)acc[i][j][r] * sav[i] * swv[j][r] + bv[j][r];
-      const int c16 = 2 * j + (g4 >> 1);
-      uint2 pk{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
-      *reinterpret_cast<uint2*>(wt + m * 128 + ((c16 ^ (m & 7)) << 4) + (g4 & 1) * 8) = pk;
-    }
+  for (int e = 0; e < 8; ++e) {
+    const int col = min(col0 + e, N - 1);
+    swv[e] = sw[col];
+    bv[e] = bf2f(bp[bias != nullptr ? col : 0]);        // absent bias: a zero word, no branch
   }
-  // (a wave's LDS operations complete in issue order: no wait between its writes and reads)
+  __syncthreads();                                    // every wave is done with the ring
+  int8_t* wt = ring + wave * (MI * 8 * 256);
+  constexpr int HALF = MI / 2;
 #pragma unroll
-  for (int it = 0; it < MI * 2; ++it) {
-    const int m = it * 8 + (lane >> 3), c = lane & 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(wt + m * 128 + ((c ^ (m & 7)) << 4));
-    const int row = bm * BMV + wm * MI * 16 + m, col = bn * BNV + wn * 64 + c * 8;
-    if (row < M && col < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col) = v;   // N % 8 == 0
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+      const int m = i * 16 + r16;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        *reinterpret_cast<v4i*>(wt + m * 256 + (((4 * j + g4) ^ (m & 15)) << 4)) = acc[h * HALF + i][j];
+    }
+    // (a wave's LDS operations complete in issue order: no wait between its writes and reads)
+#pragma unroll
+    for (int it = 0; it < HALF * 2; ++it) {
+      const int m = it * 8 + (lane >> 3);
+      const int row = bm * BMV + wm * MI * 16 + h * HALF * 16 + m;
+      const float sr = sa[min(row, M - 1)];
+      const v4i lo = *reinterpret_cast<const v4i*>(wt + m * 256 + (((2 * c8) ^ (m & 15)) << 4));
+      const v4i hi = *reinterpret_cast<const v4i*>(wt + m * 256 + (((2 * c8 + 1) ^ (m & 15)) << 4));
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (float)lo[e] * sr * swv[e] + bv[e];
+        v[e + 4] = (float)hi[e] * sr * swv[e + 4] + bv[e + 4];
+      }
+      if (row < M && col0 < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col0) = pack8(v);   // N % 8 == 0
+    }
   }
 }
 
@@ -1215,17 +1243,19 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     return launch_one<4, 4, 2, 4, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
   }
   if (M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1) {
-    // 256 x 256 tiles when they fill the chip (>= 256 blocks), else 128 x 256
+    // 128 x 256 tiles, except 256 x 256 for the long-K down projection when those still fill the
+    // chip (tools/bench_ops.py pgemm, Llama-2-7B shapes at M = 512 / 2048 / 16384: 128-row tiles
+    // 1.5-2.1 POPS, equal or ahead everywhere but K = 11008 at M = 16384, 2.21 vs 2.11)
     const int grid_n = (NTt * 16 + 255) / 256;
     const int g256 = (M + 255) / 256, g128 = (M + 127) / 128;
-    const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && g256 * grid_n >= 256);
+    const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && K > 8192 && g256 * grid_n >= 256);
     const int grid_m = big ? g256 : g128;
-    if (big)
-      hipLaunchKernelGGL(w8a8_gemm_big_kernel<256>, dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n);
-    else
-      hipLaunchKernelGGL(w8a8_gemm_big_kernel<128>, dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n);
+#define BIGK(BMV)                                                                                                \
+  hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,     \
+                     (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
+    if (big) BIGK(256);
+    else BIGK(128);
+#undef BIGK
     return (int)hipGetLastError();
   }
   if (M > 64 && K % 64 == 0 && K / 64 == KT) {

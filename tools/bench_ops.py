@@ -257,6 +257,56 @@ def prefill_rows(C, dev, Hq, D):
     return out
 
 
+def batch1_rows(C, dev, M=1):
+    """Batch-1 decode GEMVs at Llama-2-7B shapes, cache-cold: the quantising gate_up GEMV (8- vs
+    16-wave workgroups) and the split-K o / down GEMVs over S slices (grouped activation scales)."""
+    out = []
+    N, K = 2 * 11008, 4096
+    ncopy = max(2, (1 << 30) // (N * K) + 1)
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+    wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+    sw = torch.rand(N, device=dev) * 0.01
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+    sx = torch.rand(M, device=dev) * 0.01
+    ctr = [0]
+
+    def gluq():
+        ctr[0] = (ctr[0] + 1) % ncopy
+        return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
+
+    res = {}
+    for rnd in range(3):
+        for kw in (0, 16):
+            tune(C, "gemv", kw, 0)
+            res.setdefault(kw, []).append(timeit(gluq, iters=10, per_graph=ncopy))
+    tune(C, "gemv", 0, 0)
+    for kw, ts in res.items():
+        out.append(dict(op="w8a8_gluq_m1", M=M, kw=kw, us=round(min(ts), 2), TBps=round(N * K / min(ts) / 1e6, 2)))
+        print(out[-1], flush=True)
+    del wps
+    for name, (N, K) in {"o": (4096, 4096), "down": (4096, 11008)}.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+        sw = torch.rand(N, device=dev) * 0.01
+        qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        sx = torch.rand(K // 64, 16, device=dev) * 0.01
+        res = {}
+        for rnd in range(3):
+            for S in (0, 1, 2, 4, 8):
+                def call():
+                    ctr[0] = (ctr[0] + 1) % ncopy
+                    return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, S)
+                res.setdefault(S, []).append(timeit(call, iters=10, per_graph=ncopy))
+        for S, ts in res.items():
+            out.append(dict(op="w8a8_splitk_m1", shape=name, M=M, S=S, us=round(min(ts), 2),
+                            TBps=round(N * K / min(ts) / 1e6, 2)))
+            print(out[-1], flush=True)
+        del wps
+    out += gemv_rows(C, dev, Ms=(M,), sweep=True, shapes={"qkv": (12288, 4096)})
+    return out
+
+
 def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
     interleaved in one process (0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the LDS-DMA
@@ -293,7 +343,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--tune", action="append", default=[], help="name=a[,b] passed to ext().tune (repeatable)")
-    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill,pgemm")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill,pgemm,m1")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
@@ -312,6 +362,8 @@ def main():
     rows += other_rows(C, dev, only)
     if only is not None and "pgemm" in only:
         rows += prefill_gemm_rows(C, dev)
+    if only is not None and "m1" in only:
+        rows += batch1_rows(C, dev)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
