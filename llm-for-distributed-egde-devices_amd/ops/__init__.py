@@ -28,7 +28,18 @@ def _load():
             _C = importlib.import_module(__name__ + "._C")
         except BaseException as e:  # noqa: BLE001 - re-raised on first GPU use
             _C_ERR = e
+        else:
+            apply_tune(os.environ.get("EDGELLM_TUNE", ""))
     return _C
+
+
+def apply_tune(spec: str) -> None:
+    """Kernel tuning knobs from ``name=a[,b];name=a`` (``EDGELLM_TUNE``): A/B a launcher choice
+    at model level without a rebuild (names: the extension's ``tune`` table)."""
+    for item in filter(None, (t.strip() for t in spec.replace(";", " ").split())):
+        name, _, vals = item.partition("=")
+        v = [int(x) for x in vals.split(",") if x] + [0, 0]
+        _C.tune(name, v[0], v[1])
 
 
 def ext():

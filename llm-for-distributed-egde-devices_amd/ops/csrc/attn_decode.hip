@@ -34,6 +34,7 @@ struct Fuse {
   int8_t* out_q;        // QOUT: [B, Hq*D] int8
   float* out_s;         // QOUT: [(Hq*D)/64][Mpad] scales
   int Mpad;
+  int gs;               // query heads of one KV head split over gs workgroups (G = 1 in the kernel)
 };
 
 // Rotate the 8 values at head offset e0 (HF rotate_half convention), x/partner read from `head`.
@@ -79,7 +80,9 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   float* mstat = wl + NWV * G;             // [G]
   float* lstat = mstat + G;               // [G]
 
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  // head split (fz.gs > 1, G = 1): workgroup y serves query head y of KV head y / gs; every
+  // such workgroup rebuilds the new key / value in registers, only the first one stores it
+  const int split = blockIdx.x, kvh = blockIdx.y / fz.gs, qh0 = blockIdx.y * G, b = blockIdx.z;
   const int Hq = gridDim.y * G;
   const int len = seq_lens[b];
   const int start = split * CH;
@@ -94,10 +97,10 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     if (!DIRECT) {
       for (int i = threadIdx.x; i < G * D; i += (NWV * 64)) {
         const int h = i / D, d = i - h * D;
-        part_acc[(((size_t)b * Hq + kvh * G + h) * nsplit + split) * D + d] = 0.f;
+        part_acc[(((size_t)b * Hq + qh0 + h) * nsplit + split) * D + d] = 0.f;
       }
       if (threadIdx.x < G) {
-        float* ml = part_ml + (((size_t)b * Hq + kvh * G + threadIdx.x) * nsplit + split) * 2;
+        float* ml = part_ml + (((size_t)b * Hq + qh0 + threadIdx.x) * nsplit + split) * 2;
         ml[0] = -INFINITY; ml[1] = 0.f;
       }
     }
@@ -112,7 +115,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
 #pragma unroll
   for (int h = 0; h < G; ++h) {
     if (dvalid) {
-      const bf16_t* qh = q + b * q_sb + (size_t)(kvh * G + h) * D;
+      const bf16_t* qh = q + b * q_sb + (size_t)(qh0 + h) * D;
       unpack8(*reinterpret_cast<const uint4*>(qh + d0), qf[h]);
       if constexpr (FUSED) {
         if (d0 < fz.rot) {
@@ -138,7 +141,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     // append the new token's rotated k and its v (only the split that owns the position)
     const int pos = fz.pos[b];
     own = pos >= start && pos < end;
-    const int Hkv = gridDim.y;
+    const int Hkv = gridDim.y / fz.gs;
     const bf16_t* row = q + b * fz.qkv_sb;
     const float2* csp = reinterpret_cast<const float2*>(fz.cs) + (size_t)pos * (fz.rot / 2);
     if constexpr (OCC > 0) {
@@ -150,7 +153,8 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
         float v[8];
         unpack8(*reinterpret_cast<const uint4*>(head + d0), v);
         if (!is_v && d0 < fz.rot) rope8(head, d0, fz.rot, csp, v);
-        *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + d0) = pack8(v);
+        if (blockIdx.y % fz.gs == 0)
+          *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + d0) = pack8(v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {                // the cached bf16 value
           const float r = bf2f(f2bf(v[j]));
@@ -342,7 +346,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     float a = 0.f;
 #pragma unroll
     for (int w = 0; w < NWV; ++w) a += red[(w * G + h) * D + d];
-    const int hq = kvh * G + h;
+    const int hq = qh0 + h;
     if (DIRECT) {
       if constexpr (QOUT) {     // D % 64 == 0: each 64-column group is one wave of this loop
         const float vq = bf2f(f2bf(a / lstat[h]));
@@ -357,7 +361,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     }
   }
   if (!DIRECT && threadIdx.x < G) {
-    float* ml = part_ml + (((size_t)b * Hq + kvh * G + threadIdx.x) * nsplit + split) * 2;
+    float* ml = part_ml + (((size_t)b * Hq + qh0 + threadIdx.x) * nsplit + split) * 2;
     ml[0] = mstat[threadIdx.x];
     ml[1] = lstat[threadIdx.x];
   }
@@ -397,6 +401,9 @@ static int g_target_wg = 512;   // >= 2 workgroups per CU before splitting K
 // double-buffered form with the append barrier (168 VGPRs, 3 waves per SIMD).  Measured at 128
 // sequences x 32 heads, context 160 (tools/bench_ops.py attn_fused): 57.7 / 60.4 / 66.6 us.
 static int g_attn_occ = 4;
+// query-head split for small grids (tune "decode_attn_gsplit"): 0 automatic, 1 off, 2 always (GQA)
+static int g_attn_gsplit = 0;
+extern "C" void edge_decode_attn_gsplit(int v) { g_attn_gsplit = v; }
 extern "C" void edge_decode_attn_config(int target_wg) { g_target_wg = target_wg > 0 ? target_wg : 512; }
 extern "C" void edge_decode_attn_occ(int occ) { g_attn_occ = occ == 0 || occ == 5 ? occ : 4; }
 
@@ -427,10 +434,11 @@ extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int D, int* ch
   int nsplit = (target_wg + per - 1) / per;
   int ch = (max_len + nsplit - 1) / nsplit;
   ch = ((ch + 63) / 64) * 64;
-  // at least 64 KiB of K+V per split (256 keys at D = 64, 128 at D = 128, 64 at D = 256): below
-  // that the combine launch and the partial round trip cost more than the split saves (batch 1,
-  // Llama-3.2-1B, context <= 256: 15.7 + 4.8 us per layer with 4 splits of 64 keys)
-  const int ch_min = D > 0 ? ((16384 / D + 63) / 64) * 64 : 64;
+  // at least 256 keys per split: below that the combine launch and the partial round trip cost
+  // more than the split saves (batch 1, Llama-3.2-1B, context <= 256: 15.7 + 4.8 us per layer with
+  // 4 splits of 64 keys; Llama-2-7B W8A8 batch 1 at context ~200: 2.16 ms/token direct against
+  // 2.33-2.42 ms with 2 splits of 128 keys + combine)
+  const int ch_min = 256;
   if (ch < ch_min) ch = ch_min;
   if (ch > 1024) ch = 1024;
   nsplit = (max_len + ch - 1) / ch;
@@ -450,15 +458,22 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
                                 const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
                                 hipStream_t st) {
   if (B == 0) return 0;
-  const int G = Hq / Hkv;
-  if (G * Hkv != Hq) return -2;
+  const int G0 = Hq / Hkv;
+  if (G0 * Hkv != Hq) return -2;
   const bool fused = pos != nullptr, qout = out_q != nullptr;
   if (qout && (D % 64 != 0 || Mpad < B)) return -2;
   if (fused && rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
-  const Fuse fz{pos, cs, fused ? rot : 0, q_sb, (int8_t*)out_q, out_s, Mpad};
+  // grids of a few dozen workgroups (batch 1-4 on a GQA model: 8 KV heads) are bound by each
+  // workgroup's serial chain over its keys x G query heads: give every query head its own
+  // workgroup instead (K/V rows re-read G times, from L2).  Needs the barrier-free fused form
+  // (the new key in registers) or the plain kernel: no workgroup reads a row another one appends.
+  const bool gs_ok = G0 > 1 && (!fused || g_attn_occ != 0);
+  const int gs = gs_ok && (g_attn_gsplit == 2 || (g_attn_gsplit == 0 && B * Hkv * nsplit < 128)) ? G0 : 1;
+  const int G = G0 / gs;
+  const Fuse fz{pos, cs, fused ? rot : 0, q_sb, (int8_t*)out_q, out_s, Mpad, gs};
   const float sl2 = scale * 1.4426950408889634f;
   const size_t lds = (size_t)(NW * G * D + 2 * NW * G + 2 * G) * sizeof(float);
-  const dim3 grid(nsplit, Hkv, B);
+  const dim3 grid(nsplit, Hkv * gs, B);
   const bool direct = nsplit == 1;
 #define DK(DD, GG, DI, FU, QO)                                                                                     \
   launch_attn<DD, GG, DI, FU, QO>(grid, lds, st, q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, out, \

@@ -657,7 +657,7 @@ __device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_r
 //  * blockIdx -> tile: bijective XCD remap (each XCD gets a contiguous range), then groups of 4
 //    row tiles walked column-major, so an XCD's ~32 resident blocks share 4 A panels and 8 W panels
 //    in its L2.
-template <int BMV>
+template <int BMV, int ISS>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
@@ -699,15 +699,15 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
   // DMA of stage st into slot st % R.  Stages past the last k-tile re-load the last k-tile into
   // their slot (never read again: every stage still to be read sits in another slot), so every
   // stage is PPW pieces per wave, the loop is branch-free and the vmcnt counts are constants.
-  auto issue = [&](int st) {
+  auto issue_piece = [&](int st, int i) {
     const int kt = min(st, KT - 1);
-    const int8_t* ab = A + (size_t)kt * 64;
-    const int8_t* wb = Wp + (size_t)kt * 1024;
+    const bool isa = wave + NWV * i < AP;
+    glds16((isa ? A + (size_t)kt * 64 : Wp + (size_t)kt * 1024) + off[i],
+           ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
+  };
+  auto issue = [&](int st) {
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const bool isa = wave + NWV * i < AP;             // compile-time per i when AP % 8 == 0
-      glds16((isa ? ab : wb) + off[i], ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
-    }
+    for (int i = 0; i < PPW; ++i) issue_piece(st, i);
   };
   // fragment reads: one VGPR base per operand and slot, immediate offsets
   const uint32_t ring0 = lds_off(ring) + lane * 16;
@@ -762,10 +762,30 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
   auto full = [&](int s, v4i (&wc)[NJ], v4i (&ac)[MI], v4i (&wx)[NJ], v4i (&ax)[MI]) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 2) * PPW) : "memory");   // own DMA of s + 1
     __builtin_amdgcn_s_barrier();                     // stage s + 1 landed everywhere; slot of s free
-    issue(s + R);
+    if constexpr (ISS == 0) issue(s + R);
     read_frags(s + 1, wx, ax);
-    mma(wc, ac);
+    if constexpr (ISS == 2) {
+      // DMA pieces interleaved into the MFMA stream: piece g after MFMA group g (a glds that
+      // stalls on a full memory queue then holds back only the MFMAs behind it)
+      pin(wc, ac);
+      constexpr int TOT = MI * NJ, GRP = TOT / (PPW + 1);
+#pragma unroll
+      for (int f = 0; f < TOT; ++f) {
+        const int i = f / NJ, j = f % NJ;
+        acc[i][j] = mfma_i8(wc[j], ac[i], acc[i][j]);
+        if ((f + 1) % GRP == 0 && (f + 1) / GRP <= PPW) {
+          asm volatile("" : "+v"(acc[i][j])::"memory");   // this MFMA issued before the piece
+          issue_piece(s + R, (f + 1) / GRP - 1);
+        }
+      }
+    } else {
+      mma(wc, ac);
+    }
     pin_acc();
+    if constexpr (ISS == 1) {
+      asm volatile("" ::: "memory");                  // the pieces after every MFMA of the k-tile
+      issue(s + R);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   int s = 0;
@@ -1038,8 +1058,10 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 1;
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
-static int g_prefill_gemm = 0;
-extern "C" void edge_w8a8_prefill_gemm(int v) { g_prefill_gemm = v; }
+static int g_prefill_gemm = 0, g_prefill_iss = 2;
+// b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
+// MFMAs, 2 interleaved into them: the default, 1-3 % ahead of 0 on the Llama-2-7B shapes)
+extern "C" void edge_w8a8_prefill_gemm(int v, int b) { g_prefill_gemm = v; g_prefill_iss = b; }
 // tuning hooks (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int kw, int unroll) { g_gemv_kw = kw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
@@ -1220,8 +1242,10 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
       // one tile group (TG = 1): every wave holds all 8 tiles, so each activation fragment is
       // fetched once per workgroup (TG > 1 re-fetched it per group: 1 MB of L2 reads per CU at 64 rows)
       if (mblocks <= 1) {
-        if (g_gemv_kw == 16) return launch_one<1, 8, 2, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
-        return launch_one<1, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+        // 16 waves as 2 tile groups x 8 k-waves (batch 1, Llama-2-7B gate_up: 19.1 us against 21.1 us
+        // for 8 waves holding all 8 tiles; the re-fetched activation row is 4 KiB); kw = 8 selects the latter
+        if (g_gemv_kw == 8) return launch_one<1, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
+        return launch_one<1, 8, 2, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
       }
       if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
       if (mblocks > 4) {
@@ -1250,11 +1274,12 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     const int g256 = (M + 255) / 256, g128 = (M + 127) / 128;
     const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && K > 8192 && g256 * grid_n >= 256);
     const int grid_m = big ? g256 : g128;
-#define BIGK(BMV)                                                                                                \
-  hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,     \
+#define BIGK(BMV, ISS)                                                                                           \
+  hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
-    if (big) BIGK(256);
-    else BIGK(128);
+    const int iss = g_prefill_iss;
+    if (big) { if (iss == 1) BIGK(256, 1); else if (iss == 2) BIGK(256, 2); else BIGK(256, 0); }
+    else { if (iss == 1) BIGK(128, 1); else if (iss == 2) BIGK(128, 2); else BIGK(128, 0); }
 #undef BIGK
     return (int)hipGetLastError();
   }

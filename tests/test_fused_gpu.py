@@ -41,6 +41,30 @@ def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant, occ):
         C.tune("decode_attn_occ", 4, 0)
 
 
+@pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 8, 64, 64), (32, 8, 128, 128), (16, 2, 128, 64), (8, 4, 256, 64)])
+@pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333), (300,)])
+@pytest.mark.parametrize("gsplit", [1, 2])
+@pytest.mark.parametrize("quant", [False, True])
+def test_decode_attention_gsplit(cuda, Hq, Hkv, D, rot, lens, gsplit, quant):
+    """Query-head split (one workgroup per query head, the new key rebuilt in every workgroup of a
+    KV head, stored by the first): forced on (2) and off (1), fused append + output quant, and the
+    plain kernel."""
+    C = ops.ext()
+    C.tune("decode_attn_gsplit", gsplit, 0)
+    try:
+        _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant)
+        B = len(lens)
+        S = max(lens) + 5
+        q = torch.randn(B, Hq, D, device=cuda).bfloat16()
+        kc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+        vc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+        sl = torch.tensor(lens, device=cuda, dtype=torch.int32)
+        _close(C.decode_attn(q, kc, vc, sl, 1 / math.sqrt(D), S), _ref.decode_attention(q, kc, vc, sl, 1 / math.sqrt(D)),
+               2e-2, 2e-2)
+    finally:
+        C.tune("decode_attn_gsplit", 0, 0)
+
+
 def _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant):
     cuda = torch.device("cuda")
     torch.manual_seed(3)

@@ -276,7 +276,7 @@ def batch1_rows(C, dev, M=1):
 
     res = {}
     for rnd in range(3):
-        for kw in (0, 16):
+        for kw in (0, 8):
             tune(C, "gemv", kw, 0)
             res.setdefault(kw, []).append(timeit(gluq, iters=10, per_graph=ncopy))
     tune(C, "gemv", 0, 0)
@@ -309,11 +309,13 @@ def batch1_rows(C, dev, M=1):
 
 def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
-    interleaved in one process (0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the LDS-DMA
-    ring kernel at 256 / 128 rows per block)."""
+    interleaved in one process ((form, issue): form 0 automatic, 2 / 3 the LDS-DMA ring kernel at
+    256 / 128 rows per block; issue 0 / 1 / 2 = DMA pieces before the fragment reads / after the
+    MFMAs / interleaved into them)."""
     out = []
     shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
-    forms = {"auto": 0, "tiled128": 1, "ring256": 2, "ring128": 3}
+    forms = {"auto": (0, 2), "ring256": (2, 0), "ring128": (3, 0), "ring256_late": (2, 1), "ring128_late": (3, 1),
+             "ring256_ilv": (2, 2), "ring128_ilv": (3, 2)}
     for name, (N, K) in shapes.items():
         w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
         wp = ops.pack_int8_weight(w)
@@ -324,11 +326,11 @@ def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
             res = {}
             for rnd in range(2):
                 for form, v in forms.items():
-                    C.tune("prefill_gemm", v, 0)
+                    C.tune("prefill_gemm", *v)
                     per = max(2, min(20, int(4e11 // (M * N * K))))
                     res.setdefault(form, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K),
                                                            iters=5, per_graph=per))
-            C.tune("prefill_gemm", 0, 0)
+            C.tune("prefill_gemm", 0, 2)
             row = dict(op="w8a8_gemm_prefill", shape=name, M=M, N=N, K=K)
             for form, ts in res.items():
                 row[form + "_us"] = round(min(ts), 1)

@@ -20,6 +20,7 @@ from edgellm import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--form", type=int, default=0)
+    ap.add_argument("--iss", type=int, default=2)
     ap.add_argument("--M", type=int, default=16384)
     ap.add_argument("--N", type=int, default=12288)
     ap.add_argument("--K", type=int, default=4096)
@@ -33,7 +34,7 @@ def main():
     w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
     wp = ops.pack_int8_weight(w)
     sx, sw = torch.rand(M, device=dev) * 0.01, torch.rand(N, device=dev) * 0.01
-    C.tune("prefill_gemm", a.form, 0)
+    C.tune("prefill_gemm", a.form, a.iss)
     fns = {"edge": lambda: C.w8a8_gemm(x, sx, wp, sw, None, N, K)}
     if a.intmm:
         wt = w.t()                           # [K, N] column-major view of the [N, K] weight
