@@ -54,6 +54,7 @@ int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int*
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_gemv_ring(int on);
 void edge_w8a8_prefill_gemm(int v, int b);
+void edge_w8a8_ring2_cfg(int v, int rot);
 void edge_decode_attn_config(int target_wg);
 int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, void* vc, float* ks, float* vs, int64_t c_sb,
                         int64_t c_sh, int64_t s_sb, int64_t s_sh, const int* seq_lens, int B, int Hq, int Hkv, int D,
@@ -698,6 +699,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
+    else if (what == "ring2_cfg") edge_w8a8_ring2_cfg((int)a, (int)b);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);

@@ -540,6 +540,11 @@ constexpr int BM = 128, BN = 128;
 __device__ __forceinline__ void glds16(const void* g, void* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
+// streaming form (cache policy nt): weight bytes read once per step, kept out of the way of the
+// L2-resident activation panel every workgroup re-reads
+__device__ __forceinline__ void glds16_nt(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2);
+}
 
 __global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                              const int8_t* __restrict__ Wp, const float* __restrict__ sw,
@@ -868,7 +873,14 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
 // LDS-DMA (vmcnt(0)), draining the ring each stage.  Ordering is explicit instead: counted vmcnt
 // for this wave's own DMA, a bare s_barrier for the other waves', lgkmcnt(0) before the MFMAs.
 
-template <int NTW, int C, int R, bool SCALED, int EPI>
+// LN (whole lines, C == 2): an activation piece is 8 rows x 128 B (two k-tiles) instead of one
+// fragment's 16 rows x 64 B.  Measured (tools/ingest_bw.hip), L2 -> LDS by LDS-DMA moves 1 KiB
+// pieces of whole 128-B lines at ~60 B/clk/CU but the 16-row x 64-B fragment pattern at ~18: at 128
+// rows the activation re-reads are 2.7x the weight bytes, so their access pattern, not HBM, set
+// the GEMV's rate.  Within a piece, lane l loads row l >> 3, 16-B chunk (l & 7) ^ (l >> 3) to LDS
+// position l: logical chunk c of row r sits at c ^ (r & 7), and the fragment reads (16 rows x
+// one chunk) hit 8 distinct 16-B bank groups per 8 rows.
+template <int NTW, int C, int R, bool SCALED, int EPI, bool LN = false>
 __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
@@ -879,6 +891,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
   constexpr int PPW = PIECES / NWV, PEXTRA = PIECES % NWV;   // waves < PEXTRA issue PPW + 1 pieces
   static_assert(R * STAGE <= 150 * 1024, "LDS ring budget");
   static_assert(EPI != EPI_GLUQ || NTW == 8, "GLUQ: 8 tiles = 64 features per workgroup");
+  static_assert(!LN || C == 2, "whole-line activation pieces cover two k-tiles");
   __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
   const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
   const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
@@ -894,7 +907,12 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 #pragma unroll
   for (int i = 0; i < PMAX; ++i) {
     const int p = min(wave + i * NWV, PIECES - 1);
-    if (p < APC) {                                   // activation fragment: row block p % MB
+    if (p < APC && LN) {                             // activation lines: rows 8p .. 8p + 7, two k-tiles
+      const int row = min(p * 8 + (lane >> 3), M - 1);
+      src[i] = A + (size_t)row * K + (size_t)kbeg * 64 + 16 * ((lane & 7) ^ (lane >> 3));
+      stride[i] = 64;
+      klocal[i] = 0;
+    } else if (p < APC) {                            // activation fragment: row block p % MB
       const int row = min((p % MB) * 16 + (lane & 15), M - 1);
       src[i] = A + (size_t)row * K + (size_t)kbeg * 64 + 16 * (lane >> 4);
       stride[i] = 64;
@@ -916,7 +934,8 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
     for (int i = 0; i < PMAX; ++i) {
       if (i < PPW || wave < PEXTRA) {
         const int p = wave + i * NWV;
-        const int kt = min(st * C + klocal[i], KTC - 1);       // past the slice: a valid, unused tile
+        // past the slice: a valid, unused tile (line pieces: a valid pair, KTC % 2 == 0)
+        const int kt = LN && p < APC ? min(st * C, KTC - C) : min(st * C + klocal[i], KTC - 1);
         glds16(src[i] + (size_t)kt * stride[i], ring + (st % R) * STAGE + p * 1024);
       }
     }
@@ -966,7 +985,13 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
       if (s * C + c < KTC) {                          // wave-uniform
         v4i a[2], b[NTW];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) a[j] = lds_read16(base + (c * MB + 2 * wave + j) * 1024 + lane * 16);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (LN)   // row block rb = 2 wave + j: pieces 2 rb, 2 rb + 1; chunk 4 c + (lane >> 4)
+            a[j] = lds_read16(base + (2 * (2 * wave + j) + ((lane & 15) >> 3)) * 1024 + (lane & 7) * 128 +
+                              (((4 * c + (lane >> 4)) ^ (lane & 7)) << 4));
+          else
+            a[j] = lds_read16(base + (c * MB + 2 * wave + j) * 1024 + lane * 16);
+        }
 #pragma unroll
         for (int t = 0; t < NTW; ++t) b[t] = lds_read16(base + (APC + c * NTW + t) * 1024 + lane * 16);
         v4f sgv[2];
@@ -1054,9 +1079,193 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
       }
   }
 }
+
+// ------------------------------------------------------------------------------------ ring2
+// 65-128 decode rows with DECOUPLED prefetch depths for the two operands.  Streaming weights from
+// HBM at full rate needs ~2.5-4 us of loaded latency covered, while the activation re-reads are
+// L2 hits.  In the one-ring kernel above most of the ~110 KiB in flight per CU is activation
+// pieces, so only ~30 KiB of weights are in flight.  vmcnt retires a wave's loads in issue order,
+// so one wave cannot keep a deep weight queue behind a shallow activation queue — separate waves
+// can:
+//   * NWL loader waves issue only weight tiles, DW = RW - 1 stages ahead (RW slots);
+//   * 4 compute waves issue only activation pieces (whole lines, as the ring kernel's LN form),
+//     DA = RA - 1 stages ahead, and own 2 row blocks x NTW tiles of accumulators each.
+// A stage is two k-tiles.  One bare barrier per stage: every wave first waits (counted vmcnt) for
+// its own DMA of stage s, then the barrier makes slot s visible to all and frees slot s - 1,
+// which the next issue reuses.  Stages past the end re-load the last one (never read).
+// Epilogues as the ring kernel (EPI_OUT bf16, EPI_GLUQ SwiGLU + per-64 int8), no split-K; K % 128 == 0.
+template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true>
+__global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
+    const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
+    const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
+    int M, int N, int K, int NTt, int Mpad) {
+  constexpr int MB = 8, NCW = 4, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
+  static_assert(WST % NWL == 0, "weight pieces split evenly over the loader waves");
+  static_assert(DW * WPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
+  static_assert(EPI == EPI_OUT || (EPI == EPI_GLUQ && NTW == 8), "GLUQ: 8 tiles = 64 features");
+  static_assert((RW * WST + RA * 16) * 1024 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) int8_t lds[(RW * WST + RA * 16) * 1024];
+  int8_t* const wring = lds;
+  int8_t* const aring = lds + RW * WST * 1024;
+  const int KT = K / 64, NS = KT / 2;
+  const int nt0 = blockIdx.x * NTW;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // k order rotated per workgroup (int32 sums: exact in any order): the ~256 workgroups do not all
+  // request the same activation lines at the same moment
+  const int rot = ROT ? (int)((blockIdx.x * 5u) % (unsigned)NS) : 0;
+  auto phys = [&](int st) { const int k = min(st, NS - 1) + rot; return k >= NS ? k - NS : k; };
+
+  if (wave >= NCW) {                                  // ---- weight loader: pieces (k-tile c, tile t)
+    const int lw = wave - NCW;
+    uint32_t woff[WPW];
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int q = lw * WPW + i, c = q / NTW, t = q % NTW;
+      woff[i] = ((uint32_t)min(nt0 + t, NTt - 1) * (uint32_t)KT + c) * 1024u + lane * 16;
+    }
+    auto issue = [&](int st) {
+      const int8_t* wb = Wp + (size_t)phys(st) * 2048;
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
+    };
+    for (int st = 0; st < DW; ++st) issue(st);
+    for (int s = 0; s < NS; ++s) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DW - 1) * WPW) : "memory");   // own pieces of stage s
+      __builtin_amdgcn_s_barrier();
+      issue(s + DW);                                  // into the slot of stage s - 1
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the workgroup
+    return;
+  }
+
+  // ---- compute waves: activation line pieces 4 wave .. 4 wave + 3 (rows 8p .. 8p + 7, 128 B)
+  uint32_t aoff[APW];
+#pragma unroll
+  for (int i = 0; i < APW; ++i)
+    aoff[i] = (uint32_t)min((APW * wave + i) * 8 + (lane >> 3), M - 1) * (uint32_t)K + 16 * ((lane & 7) ^ (lane >> 3));
+  auto issue = [&](int st) {
+    const int8_t* ab = A + (size_t)phys(st) * 128;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
+  };
+  // epilogue operands first (the tail never waits on memory; retired by the first vmcnt wait)
+  float sw_t[NTW], b_t[NTW], sa_r[2][4];
+  const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int col = min((nt0 + t) * 16 + (lane & 15), N - 1);
+    sw_t[t] = sw[col];
+    b_t[t] = bf2f(bp[bias != nullptr ? col : 0]);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sa_r[j][q] = sa[min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, M - 1)];
+  v4i acc[2][NTW];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[j][t] = v4i{0, 0, 0, 0};
+
+  for (int st = 0; st < DA; ++st) issue(st);
+  // row block rb = 2 wave + j lives in line pieces 2 rb, 2 rb + 1; k-tile c's chunk is 4 c + (lane >> 4)
+  const uint32_t a0 = lds_off(aring) + (4 * wave + ((lane & 15) >> 3)) * 1024 + (lane & 7) * 128;
+  const uint32_t ax[2] = {(uint32_t)(((lane >> 4) ^ (lane & 7)) << 4), (uint32_t)(((4 + (lane >> 4)) ^ (lane & 7)) << 4)};
+  const uint32_t w0 = lds_off(wring) + lane * 16;
+  // one k-tile's fragments: [2 row blocks | NTW tiles], double-buffered by k-tile, so the MFMAs
+  // of one k-tile run while the next one's LDS reads are in flight (across the stage barrier too)
+  constexpr int NF = 2 + NTW;
+  auto read_kt = [&](int st, int c, v4i (&f)[NF]) {
+    const uint32_t ab = a0 + (st % RA) * 16 * 1024, wb = w0 + (st % RW) * WST * 1024;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) f[j] = lds_read16(ab + j * 2048 + ax[c]);
+    v4i b[NTW];
+    lds_read_row<NTW>(wb + c * NTW * 1024, b);
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) f[2 + t] = b[t];
+  };
+  auto mma = [&](v4i (&f)[NF]) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(f[i]));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) acc[j][t] = mfma_i8(f[j], f[2 + t], acc[j][t]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(acc[j][t]));
+  };
+  // barrier k certifies stage k (both operands) and frees the slots of stage k - 1
+  auto sync_stage = [&](int st) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * APW) : "memory");    // own pieces of stage st
+    __builtin_amdgcn_s_barrier();
+    issue(st + DA);
+  };
+  v4i x[NF], y[NF];
+  sync_stage(0);
+  read_kt(0, 0, x);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int s = 0; s < NS; ++s) {                     // x holds k-tile (s, 0)
+    read_kt(s, 1, y);
+    mma(x);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (s + 1 < NS) {                                 // wave-uniform
+      sync_stage(s + 1);
+      read_kt(s + 1, 0, x);
+    }
+    mma(y);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue: lane holds col (lane & 15) of each tile, rows 4 (lane >> 4) + q of its 2 row blocks
+  if constexpr (EPI == EPI_OUT) {
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      const int col = (nt0 + t) * 16 + (lane & 15);
+      if (nt0 + t >= NTt || col >= N) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+          if (row < M)
+            reinterpret_cast<bf16_t*>(outv)[(size_t)row * N + col] = f2bf((float)acc[j][t][q] * sa_r[j][q] * sw_t[t] + b_t[t]);
+        }
+    }
+  } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
+    const int Fo = N / 2, grp64 = nt0 / 8;
+    int8_t* hq = reinterpret_cast<int8_t*>(outv);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+        float h[4], amax = 0.f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const float g = bf2f(f2bf((float)acc[j][2 * p][q] * sa_r[j][q] * sw_t[2 * p] + b_t[2 * p]));
+          const float u = bf2f(f2bf((float)acc[j][2 * p + 1][q] * sa_r[j][q] * sw_t[2 * p + 1] + b_t[2 * p + 1]));
+          h[p] = g / (1.f + __expf(-g)) * u;
+          amax = fmaxf(amax, fabsf(h[p]));
+        }
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) amax = fmaxf(amax, __shfl_xor(amax, d, 64));
+        amax = fmaxf(amax, 1e-8f);
+        const bool live = nt0 + 7 < NTt;
+        if (live && row < M) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) hq[(size_t)row * Fo + (nt0 / 2 + p) * 16 + (lane & 15)] = quant_i8(h[p], 127.f / amax);
+        }
+        if (live && (lane & 15) == 0 && row < Mpad) os[(size_t)grp64 * Mpad + row] = row < M ? amax / 127.f : 0.f;
+      }
+  }
+}
 }  // namespace
 
-static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 1;
+static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 1, g_ring2_cfg = 0, g_ring2_rot = 1;
+extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
 static int g_prefill_gemm = 0, g_prefill_iss = 2;
 // b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
@@ -1088,11 +1297,11 @@ int launch_ldsa(const void* A, const float* sa, const void* Wp, const float* sw,
   return (int)hipGetLastError();
 }
 
-template <int NTW, int C, int R, bool SC, int EP>
+template <int NTW, int C, int R, bool SC, int EP, bool LN = false>
 int launch_ring(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                 float* os, int M, int N, int K, int Mpad, hipStream_t st, int S, int KTC) {
   const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_ring_kernel<NTW, C, R, SC, EP>), dim3((NTt + NTW - 1) / NTW * S), dim3(256), 0, st,
+  hipLaunchKernelGGL((w8a8_gemv_ring_kernel<NTW, C, R, SC, EP, LN>), dim3((NTt + NTW - 1) / NTW * S), dim3(256), 0, st,
                      (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S,
                      KTC);
   return (int)hipGetLastError();
@@ -1104,10 +1313,52 @@ template <int EP>
 int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                         float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
   if (!g_gemv_ring || M <= 64 || M > 128 || K % 64 != 0 || (K / 64) % S != 0 || (EP == EPI_PART) != (S > 1)) return -1;
+  // decoupled-depth form (ring2): qkv-like EPI_OUT with 3 tiles per workgroup, quantising GLU
+  if (g_gemv_ring == 2 && !scaled && S == 1 && K % 128 == 0) {
+    const int NTt = (N + 15) / 16;
+#define R2(NTWV, NWLV, RWV, RAV, EPV)                                                                            \
+  do {                                                                                                           \
+    if (g_ring2_rot == 0) {                                                                                    \
+      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false>), dim3((NTt + NTWV - 1) / NTWV), \
+                         dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,            \
+                         (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad);                                    \
+      return (int)hipGetLastError();                                                                           \
+    }                                                                                                          \
+    hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV>), dim3((NTt + NTWV - 1) / NTWV),     \
+                       dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,              \
+                       (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad);                                      \
+    return (int)hipGetLastError();                                                                             \
+  } while (0)
+    if constexpr (EP == EPI_GLUQ) {
+      if (N % 128 == 0) {
+        if (g_ring2_cfg == 1) R2(8, 4, 5, 4, EPI_GLUQ);
+        if (g_ring2_cfg == 2) R2(8, 4, 4, 5, EPI_GLUQ);
+        R2(8, 4, 6, 3, EPI_GLUQ);
+      }
+    } else if constexpr (EP == EPI_OUT) {
+      if (g_ring2_cfg == 1) R2(3, 3, 14, 4, EPI_OUT);
+      if (g_ring2_cfg == 2) R2(3, 6, 16, 3, EPI_OUT);
+      if (g_ring2_cfg == 3) R2(4, 4, 12, 4, EPI_OUT);
+      R2(3, 3, 16, 3, EPI_OUT);
+    }
+#undef R2
+  }
   // per-(token, 64) scales (o / down): the per-k-tile fold serialises the MFMAs and the ring form
   // measured slower than the LDS-staged kernel (o + down 24.8 us avg vs 12.1 / 22.3): off
   if (scaled) return -1;
   const int KTC = K / 64 / S, NTt = (N + 15) / 16;
+  if (g_gemv_ring == 3 && KTC % 2 == 0) {            // whole-line activation pieces
+    if constexpr (EP == EPI_GLUQ) {
+      if (N % 128 != 0) return -1;
+      return launch_ring<8, 2, 4, false, EPI_GLUQ, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+    } else {
+      const int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : max(1, min(4, (NTt * S + 128) / 256));
+      if (ntw == 1) return launch_ring<1, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+      if (ntw == 2) return launch_ring<2, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+      if (ntw == 3) return launch_ring<3, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+      return launch_ring<4, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+    }
+  }
   if constexpr (EP == EPI_GLUQ) {
     if (scaled || N % 128 != 0) return -1;
     return launch_ring<8, 1, 8, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);

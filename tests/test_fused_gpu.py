@@ -488,12 +488,19 @@ def test_bf16_model_split_k_decode_matches_unsplit(cuda):
     assert outs[0] == outs[1]
 
 
+RING_DEFAULT = 1     # gemm_i8.hip g_gemv_ring
+
+
+@pytest.mark.parametrize("ring", [1, 2, 3])
 @pytest.mark.parametrize("M", [65, 100, 128])
-@pytest.mark.parametrize("N,K,S", [(12288, 4096, 1), (6144, 4096, 1), (4096, 4096, 4), (4096, 11008, 4)])
-def test_gemv_ring_matches_ldsa(cuda, M, N, K, S):
-    """The LDS-DMA ring kernel (65-128 rows) and the LDS-staged kernel sum the same exact int32
-    products per output (per-token scales): bit-identical outputs / partial slices."""
+@pytest.mark.parametrize("N,K,S", [(12288, 4096, 1), (6144, 4096, 1), (4096, 4096, 4), (4096, 11008, 4),
+                                   (12304, 4096, 1)])
+def test_gemv_ring_matches_ldsa(cuda, ring, M, N, K, S):
+    """The LDS-DMA ring kernels (65-128 rows; 2 = decoupled weight / activation depths) and the
+    LDS-staged kernel sum the same exact int32 products per output (per-token scales):
+    bit-identical outputs / partial slices."""
     C = ops.ext()
+    C.tune("gemv_ring", ring, 0)
     torch.manual_seed(M + N)
     qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
     sx = torch.rand(M, device=cuda) * 0.01
@@ -503,19 +510,20 @@ def test_gemv_ring_matches_ldsa(cuda, M, N, K, S):
     wp = ops.pack_int8_weight(w)
     run = (lambda: C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)) if S == 1 else \
         (lambda: C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S))
-    ring = run()
     try:
+        ring_out = run()
         C.tune("gemv_ring", 0, 0)
         old = run()
     finally:
-        C.tune("gemv_ring", 1, 0)
+        C.tune("gemv_ring", RING_DEFAULT, 0)
     if S == 1 and K // 64 != 64:
         return
-    assert torch.equal(ring, old)
+    assert torch.equal(ring_out, old)
 
 
+@pytest.mark.parametrize("ring", [1, 2, 3])
 @pytest.mark.parametrize("M", [65, 128])
-def test_gluq_ring_matches_ldsa(cuda, M):
+def test_gluq_ring_matches_ldsa(cuda, ring, M):
     """gate_up + SwiGLU + int8 quantisation on the ring kernel vs the LDS-staged kernel: the
     int32 sums and the epilogue arithmetic are the same, so outputs and scales are identical."""
     C = ops.ext()
@@ -527,11 +535,12 @@ def test_gluq_ring_matches_ldsa(cuda, M):
     sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
     wp = ops.pack_int8_weight(_ref.block_glu_rows(w))
     swb = _ref.block_glu_rows(sw)
-    q1, s1 = C.w8a8_gemm_gluq(qx, sx, wp, swb, None, 2 * F, K)
     try:
+        C.tune("gemv_ring", ring, 0)
+        q1, s1 = C.w8a8_gemm_gluq(qx, sx, wp, swb, None, 2 * F, K)
         C.tune("gemv_ring", 0, 0)
         q0, s0 = C.w8a8_gemm_gluq(qx, sx, wp, swb, None, 2 * F, K)
     finally:
-        C.tune("gemv_ring", 1, 0)
+        C.tune("gemv_ring", RING_DEFAULT, 0)
     assert torch.equal(s1, s0)
     assert (q1.int() - q0.int()).abs().max() <= 1      # __expf in both; identical but for fma contraction

@@ -307,6 +307,47 @@ def batch1_rows(C, dev, M=1):
     return out
 
 
+def ring_rows(C, dev, Ms=(128, 96)):
+    """65-128-row decode GEMVs, cache-cold, per kernel form (tune gemv_ring: 0 LDS-staged,
+    1 one-ring LDS-DMA, 2 decoupled weight / activation depths): qkv and the quantising gate_up."""
+    out = []
+    for name, (N, K) in {"qkv": (12288, 4096), "gate_up": (22016, 4096)}.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+        sw = torch.rand(N, device=dev) * 0.01
+        for M in Ms:
+            qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            sx = torch.rand(M, device=dev) * 0.01
+            ctr = [0]
+
+            def call():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                if name == "gate_up":
+                    return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
+                return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
+
+            res = {}
+            # (form, ring2 config, k rotation): form 0 LDS-staged, 1 one-ring, 3 one-ring + whole
+            # activation lines, 2 decoupled depths + whole lines (ring2)
+            forms = [(0, 0, 1), (1, 0, 1), (3, 0, 1), (2, 0, 0), (2, 0, 1), (2, 1, 0), (2, 1, 1), (2, 2, 1)]
+            for rnd in range(3):
+                for form, cfg, rot in forms:
+                    C.tune("gemv_ring", form, 0)
+                    C.tune("ring2_cfg", cfg, rot)
+                    res.setdefault(form * 100 + cfg * 10 + rot, []).append(timeit(call, iters=10, per_graph=ncopy))
+            C.tune("gemv_ring", 1, 0)
+            C.tune("ring2_cfg", 0, 1)
+            row = dict(op="w8a8_rows128", shape=name, M=M, N=N, K=K)
+            for form, ts in res.items():
+                row[f"ring{form}_us"] = round(min(ts), 2)
+                row[f"ring{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
+            out.append(row)
+            print(row, flush=True)
+        del wps
+    return out
+
+
 def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
     interleaved in one process ((form, issue): form 0 automatic, 2 / 3 the LDS-DMA ring kernel at
@@ -345,7 +386,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--tune", action="append", default=[], help="name=a[,b] passed to ext().tune (repeatable)")
-    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill,pgemm,m1")
+    ap.add_argument("--only", default=None, help="comma list of: gemv,grouped,glu,attn,attn_fused,small,sample,prefill,pgemm,m1,ring")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     dev = torch.device("cuda:0")
@@ -366,6 +407,8 @@ def main():
         rows += prefill_gemm_rows(C, dev)
     if only is not None and "m1" in only:
         rows += batch1_rows(C, dev)
+    if only is not None and "ring" in only:
+        rows += ring_rows(C, dev)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
