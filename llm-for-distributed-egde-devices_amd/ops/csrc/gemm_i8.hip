@@ -1093,27 +1093,38 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // A stage is two k-tiles.  One bare barrier per stage: every wave first waits (counted vmcnt) for
 // its own DMA of stage s, then the barrier makes slot s visible to all and frees slot s - 1,
 // which the next issue reuses.  Stages past the end re-load the last one (never read).
-// Epilogues as the ring kernel (EPI_OUT bf16, EPI_GLUQ SwiGLU + per-64 int8), no split-K; K % 128 == 0.
-template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true>
+// Epilogues as the ring kernel (EPI_OUT bf16, EPI_GLUQ SwiGLU + per-64 int8, EPI_PART fp32 split-K
+// slices); K % 128 == 0.  SC (per-(token, 64) activation scales, the o / down inputs): the loader
+// waves also DMA each stage's scales (one 1 KiB piece: 2 k-tiles x Mpad rows, lanes split over the
+// loader waves) into a third ring, and every k-tile's int32 MFMA result is folded in fp32.
+// EPI_PART: blockIdx = group * S + slice; slice ks reduces stages [NS ks / S, NS (ks + 1) / S).
+template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false>
 __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
-    int M, int N, int K, int NTt, int Mpad) {
+    int M, int N, int K, int NTt, int Mpad, int S = 1) {
   constexpr int MB = 8, NCW = 4, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
+  constexpr int LPW = WPW + (SC ? 1 : 0);             // loader pieces per stage (+ the scale piece)
   static_assert(WST % NWL == 0, "weight pieces split evenly over the loader waves");
-  static_assert(DW * WPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
-  static_assert(EPI == EPI_OUT || (EPI == EPI_GLUQ && NTW == 8), "GLUQ: 8 tiles = 64 features");
-  static_assert((RW * WST + RA * 16) * 1024 <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(1024))) int8_t lds[(RW * WST + RA * 16) * 1024];
+  static_assert(DW * LPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTW == 8 && !SC), "epilogues");
+  constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0);
+  static_assert(LDS_KB * 1024 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_KB * 1024];
   int8_t* const wring = lds;
   int8_t* const aring = lds + RW * WST * 1024;
-  const int KT = K / 64, NS = KT / 2;
-  const int nt0 = blockIdx.x * NTW;
+  int8_t* const sring = aring + RA * 16 * 1024;       // SC only
+  const int KT = K / 64, NSA = KT / 2;
+  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
+  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
+  const int sbeg = EPI == EPI_PART ? (int)((int64_t)NSA * ks / S) : 0;
+  const int NS = EPI == EPI_PART ? (int)((int64_t)NSA * (ks + 1) / S) - sbeg : NSA;
+  const int nt0 = grp * NTW;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // k order rotated per workgroup (int32 sums: exact in any order): the ~256 workgroups do not all
-  // request the same activation lines at the same moment
-  const int rot = ROT ? (int)((blockIdx.x * 5u) % (unsigned)NS) : 0;
-  auto phys = [&](int st) { const int k = min(st, NS - 1) + rot; return k >= NS ? k - NS : k; };
+  // k order rotated per workgroup (int32 sums: exact in any order; SC: a fixed per-workgroup fp32
+  // order): the ~256 workgroups do not all request the same activation lines at the same moment
+  const int rot = ROT ? (int)((grp * 5u) % (unsigned)NS) : 0;
+  auto phys = [&](int st) { const int k = min(st, NS - 1) + rot; return sbeg + (k >= NS ? k - NS : k); };
 
   if (wave >= NCW) {                                  // ---- weight loader: pieces (k-tile c, tile t)
     const int lw = wave - NCW;
@@ -1123,14 +1134,21 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
       const int q = lw * WPW + i, c = q / NTW, t = q % NTW;
       woff[i] = ((uint32_t)min(nt0 + t, NTt - 1) * (uint32_t)KT + c) * 1024u + lane * 16;
     }
+    // scale piece: lanes 0-31 the rows of k-tile 2 p, lanes 32-63 of 2 p + 1 (4 rows per lane)
+    const uint32_t soff = (uint32_t)((lane >> 5) * Mpad + min(4 * (lane & 31), Mpad - 4));
+    const bool smine = (lane % NWL) == lw;
     auto issue = [&](int st) {
-      const int8_t* wb = Wp + (size_t)phys(st) * 2048;
+      const int p = phys(st);
+      const int8_t* wb = Wp + (size_t)p * 2048;
 #pragma unroll
       for (int i = 0; i < WPW; ++i) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
+      if constexpr (SC) {
+        if (smine) glds16(sa + (size_t)(2 * p) * Mpad + soff, sring + (st % RW) * 1024);
+      }
     };
     for (int st = 0; st < DW; ++st) issue(st);
     for (int s = 0; s < NS; ++s) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DW - 1) * WPW) : "memory");   // own pieces of stage s
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DW - 1) * LPW) : "memory");   // own pieces of stage s
       __builtin_amdgcn_s_barrier();
       issue(s + DW);                                  // into the slot of stage s - 1
     }
@@ -1160,21 +1178,24 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sa_r[j][q] = sa[min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, M - 1)];
+    for (int q = 0; q < 4; ++q) sa_r[j][q] = SC ? 1.f : sa[min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, M - 1)];
   v4i acc[2][NTW];
+  v4f accf[2][NTW];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) acc[j][t] = v4i{0, 0, 0, 0};
+    for (int t = 0; t < NTW; ++t) { acc[j][t] = v4i{0, 0, 0, 0}; accf[j][t] = v4f{0.f, 0.f, 0.f, 0.f}; }
 
   for (int st = 0; st < DA; ++st) issue(st);
   // row block rb = 2 wave + j lives in line pieces 2 rb, 2 rb + 1; k-tile c's chunk is 4 c + (lane >> 4)
   const uint32_t a0 = lds_off(aring) + (4 * wave + ((lane & 15) >> 3)) * 1024 + (lane & 7) * 128;
   const uint32_t ax[2] = {(uint32_t)(((lane >> 4) ^ (lane & 7)) << 4), (uint32_t)(((4 + (lane >> 4)) ^ (lane & 7)) << 4)};
   const uint32_t w0 = lds_off(wring) + lane * 16;
-  // one k-tile's fragments: [2 row blocks | NTW tiles], double-buffered by k-tile, so the MFMAs
-  // of one k-tile run while the next one's LDS reads are in flight (across the stage barrier too)
-  constexpr int NF = 2 + NTW;
+  const uint32_t s0 = lds_off(sring) + ((2 * wave) * 16 + 4 * (lane >> 4)) * 4;
+  // one k-tile's fragments: [2 row blocks | NTW tiles | SC: 2 row blocks' scales], double-buffered
+  // by k-tile, so the MFMAs of one k-tile run while the next one's LDS reads are in flight (across
+  // the stage barrier too)
+  constexpr int NF = 2 + NTW + (SC ? 2 : 0);
   auto read_kt = [&](int st, int c, v4i (&f)[NF]) {
     const uint32_t ab = a0 + (st % RA) * 16 * 1024, wb = w0 + (st % RW) * WST * 1024;
 #pragma unroll
@@ -1183,18 +1204,35 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
     lds_read_row<NTW>(wb + c * NTW * 1024, b);
 #pragma unroll
     for (int t = 0; t < NTW; ++t) f[2 + t] = b[t];
+    if constexpr (SC) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) f[2 + NTW + j] = lds_read16(s0 + (st % RW) * 1024 + c * 512 + j * 64);
+    }
   };
   auto mma = [&](v4i (&f)[NF]) {
 #pragma unroll
     for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(f[i]));
+    if constexpr (SC) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        const v4f sg = __builtin_bit_cast(v4f, f[2 + NTW + j]);
 #pragma unroll
-      for (int t = 0; t < NTW; ++t) acc[j][t] = mfma_i8(f[j], f[2 + t], acc[j][t]);
+        for (int t = 0; t < NTW; ++t) fold(accf[j][t], mfma_i8(f[j], f[2 + t], v4i{0, 0, 0, 0}), sg);
+      }
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(acc[j][t]));
+        for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(accf[j][t]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[j][t] = mfma_i8(f[j], f[2 + t], acc[j][t]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(acc[j][t]));
+    }
   };
   // barrier k certifies stage k (both operands) and frees the slots of stage k - 1
   auto sync_stage = [&](int st) {
@@ -1220,7 +1258,7 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // epilogue: lane holds col (lane & 15) of each tile, rows 4 (lane >> 4) + q of its 2 row blocks
-  if constexpr (EPI == EPI_OUT) {
+  if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
       const int col = (nt0 + t) * 16 + (lane & 15);
@@ -1230,8 +1268,12 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
-          if (row < M)
-            reinterpret_cast<bf16_t*>(outv)[(size_t)row * N + col] = f2bf((float)acc[j][t][q] * sa_r[j][q] * sw_t[t] + b_t[t]);
+          if (row >= M) continue;
+          const float v = SC ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j][q];
+          if constexpr (EPI == EPI_PART)
+            reinterpret_cast<float*>(outv)[((size_t)ks * M + row) * N + col] = v * sw_t[t] + (ks == 0 ? b_t[t] : 0.f);
+          else
+            reinterpret_cast<bf16_t*>(outv)[(size_t)row * N + col] = f2bf(v * sw_t[t] + b_t[t]);
         }
     }
   } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
@@ -1264,7 +1306,7 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 }
 }  // namespace
 
-static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 1, g_ring2_cfg = 0, g_ring2_rot = 1;
+static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_ring2_cfg = 0, g_ring2_rot = 1;
 extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
 static int g_prefill_gemm = 0, g_prefill_iss = 2;
@@ -1313,6 +1355,27 @@ template <int EP>
 int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                         float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
   if (!g_gemv_ring || M <= 64 || M > 128 || K % 64 != 0 || (K / 64) % S != 0 || (EP == EPI_PART) != (S > 1)) return -1;
+  // decoupled-depth form, grouped-scale split-K (o / down): >= 4 stages per slice
+  if constexpr (EP == EPI_PART) {
+    if (g_gemv_ring == 2 && scaled && K % 128 == 0 && K / 128 >= 4 * S && Mpad >= 4 && Mpad % 4 == 0) {
+      const int NTt = (N + 15) / 16;
+#define R2S(NTWV, NWLV, RWV, RAV)                                                                                    \
+  do {                                                                                                           \
+    hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPI_PART, true, true>),                     \
+                       dim3((NTt + NTWV - 1) / NTWV * S), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa,   \
+                       (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);            \
+    return (int)hipGetLastError();                                                                             \
+  } while (0)
+      // measured at M = 128 (tools/bench_ops.py --only ring): down (K = 11008) 22.4 -> 20.1 us with
+      // (4, 4, 8, 4); o (K = 4096, 8 stages per slice) stays on the LDS-staged kernel (11.5 us vs
+      // 12.0-15.4 for every ring2 geometry)
+      if (g_ring2_cfg == 1 || (g_ring2_cfg == 0 && K >= 8192)) R2S(4, 4, 8, 4);
+      if (g_ring2_cfg == 2) R2S(4, 2, 12, 3);
+      if (g_ring2_cfg == 3) R2S(2, 2, 16, 4);
+      if (g_ring2_cfg == 4) R2S(4, 4, 12, 3);
+#undef R2S
+    }
+  }
   // decoupled-depth form (ring2): qkv-like EPI_OUT with 3 tiles per workgroup, quantising GLU
   if (g_gemv_ring == 2 && !scaled && S == 1 && K % 128 == 0) {
     const int NTt = (N + 15) / 16;
@@ -1321,12 +1384,12 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
     if (g_ring2_rot == 0) {                                                                                    \
       hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false>), dim3((NTt + NTWV - 1) / NTWV), \
                          dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,            \
-                         (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad);                                    \
+                         (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, 1);                                 \
       return (int)hipGetLastError();                                                                           \
     }                                                                                                          \
     hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV>), dim3((NTt + NTWV - 1) / NTWV),     \
                        dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,              \
-                       (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad);                                      \
+                       (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, 1);                                   \
     return (int)hipGetLastError();                                                                             \
   } while (0)
     if constexpr (EP == EPI_GLUQ) {

@@ -488,7 +488,7 @@ def test_bf16_model_split_k_decode_matches_unsplit(cuda):
     assert outs[0] == outs[1]
 
 
-RING_DEFAULT = 1     # gemm_i8.hip g_gemv_ring
+RING_DEFAULT = 2     # gemm_i8.hip g_gemv_ring
 
 
 @pytest.mark.parametrize("ring", [1, 2, 3])
@@ -544,3 +544,36 @@ def test_gluq_ring_matches_ldsa(cuda, ring, M):
         C.tune("gemv_ring", RING_DEFAULT, 0)
     assert torch.equal(s1, s0)
     assert (q1.int() - q0.int()).abs().max() <= 1      # __expf in both; identical but for fma contraction
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M", [65, 100, 128])
+@pytest.mark.parametrize("N,K,S", [(4096, 4096, 4), (4096, 11008, 4), (1024, 14336, 4)])
+def test_ring2_grouped_splitk(cuda, cfg, M, N, K, S):
+    """o / down at 65-128 rows: the decoupled-depth ring kernel with per-(token, 64) scales folded
+    per k-tile and split-K slices on stage boundaries, vs the LDS-staged kernel (slices on k-tile
+    boundaries: the slice sums agree to fp32 rounding) and the fp32 reference."""
+    C = ops.ext()
+    torch.manual_seed(M * 7 + K)
+    Mpad = (M + 15) // 16 * 16
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(K // 64, Mpad, device=cuda) * 0.01
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("gemv_ring", 2, 0)
+        C.tune("ring2_cfg", cfg, 1)
+        p2 = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
+        again = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
+        C.tune("gemv_ring", 0, 0)
+        p0 = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
+    finally:
+        C.tune("gemv_ring", RING_DEFAULT, 0)
+        C.tune("ring2_cfg", 0, 1)
+    assert torch.equal(p2, again)                      # deterministic
+    s2, s0 = p2.sum(0), p0.sum(0)
+    assert (s2 - s0).abs().max().item() <= 1e-4 * s0.abs().max().item() + 1e-5
+    ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
+    _close(s2, ref, 1e-3, 1e-2)

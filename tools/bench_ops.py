@@ -336,9 +336,40 @@ def ring_rows(C, dev, Ms=(128, 96)):
                     C.tune("gemv_ring", form, 0)
                     C.tune("ring2_cfg", cfg, rot)
                     res.setdefault(form * 100 + cfg * 10 + rot, []).append(timeit(call, iters=10, per_graph=ncopy))
-            C.tune("gemv_ring", 1, 0)
+            C.tune("gemv_ring", 2, 0)
             C.tune("ring2_cfg", 0, 1)
             row = dict(op="w8a8_rows128", shape=name, M=M, N=N, K=K)
+            for form, ts in res.items():
+                row[f"ring{form}_us"] = round(min(ts), 2)
+                row[f"ring{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
+            out.append(row)
+            print(row, flush=True)
+        del wps
+    # o / down: per-(token, 64) activation scales, split-K S = 4 fp32 slices (form 0 LDS-staged,
+    # form 2 ring2 with the scale ring, configs 0-3)
+    for name, (N, K) in {"o": (4096, 4096), "down": (4096, 11008)}.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+        sw = torch.rand(N, device=dev) * 0.01
+        for M in Ms:
+            qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            sx = torch.rand(K // 64, (M + 15) // 16 * 16, device=dev) * 0.01
+            ctr = [0]
+
+            def call():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, 4)
+
+            res = {}
+            for rnd in range(3):
+                for form, cfg in [(0, 0), (2, 0), (2, 1), (2, 2), (2, 3), (2, 4)]:
+                    C.tune("gemv_ring", form, 0)
+                    C.tune("ring2_cfg", cfg, 1)
+                    res.setdefault(form * 100 + cfg * 10 + 1, []).append(timeit(call, iters=10, per_graph=ncopy))
+            C.tune("gemv_ring", 2, 0)
+            C.tune("ring2_cfg", 0, 1)
+            row = dict(op="w8a8_rows128_grouped_splitk4", shape=name, M=M, N=N, K=K)
             for form, ts in res.items():
                 row[f"ring{form}_us"] = round(min(ts), 2)
                 row[f"ring{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
