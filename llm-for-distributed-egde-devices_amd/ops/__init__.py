@@ -261,12 +261,17 @@ def unpack_int8_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
     return w[:N, :K].contiguous()
 
 
+# rows the bf16 decode GEMV takes (gemv_bf16.hip handles up to 64: 4 row blocks per weight read)
+BF16_GEMV_MAX_ROWS = int(os.environ.get("EDGELLM_BF16_GEMV_ROWS", "16"))
+
+
 def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bool:
-    """Whether ``linear_bf16`` runs the HIP decode GEMV for this call (GPU, bf16, <= 16 rows,
-    K % 64 == 0, N % 16 == 0 (% 32 for the fused GLU))."""
+    """Whether ``linear_bf16`` runs the HIP decode GEMV for this call (GPU, bf16, <=
+    ``BF16_GEMV_MAX_ROWS`` rows, K % 64 == 0, N % 16 == 0 (% 32 for the fused GLU))."""
     K = x.shape[-1]
     return (_gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_contiguous()
-            and 0 < x.numel() // max(K, 1) <= 16 and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0)
+            and 0 < x.numel() // max(K, 1) <= BF16_GEMV_MAX_ROWS and K % 64 == 0
+            and weight.shape[0] % (32 if glu else 16) == 0)
 
 
 def pack_bf16_weight(w: torch.Tensor) -> torch.Tensor:

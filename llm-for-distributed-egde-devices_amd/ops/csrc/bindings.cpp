@@ -498,7 +498,7 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
   return part;
 }
 
-// bf16 decode GEMV (M <= 16, K % 64 == 0, N % 16 == 0): x [.., K] . W[N, K]^T (+ bias) -> bf16, with
+// bf16 decode GEMV (M <= 64, K % 64 == 0, N % 16 == 0): x [.., K] . W[N, K]^T (+ bias) -> bf16, with
 // W fragment-packed (ops.pack_bf16_weight).  epi: 0 plain, 1 SwiGLU over [gate | up] (result
 // [.., N/2]), 2 gelu-tanh, 3 gelu (erf).
 at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,

@@ -1,4 +1,6 @@
-// Decode GEMV for bf16 weights: y[M, N] = x[M, K] . W[N, K]^T (+ bias) -> bf16, M <= 16.
+// Decode GEMV for bf16 weights: y[M, N] = x[M, K] . W[N, K]^T (+ bias) -> bf16, M <= 64
+// (MB = 1..4 row blocks of 16: every weight fragment feeds MB MFMAs, so 17-64 decode rows read the
+// weights once instead of hipBLASLt's small-M kernels).
 // The fp16/bf16 evaluators (Phi-2, Pythia-1B, Llama-3.2-1B at batch 1) spend
 // most of a decode step here; hipBLASLt's small-M kernels stream the weights at about 2 TB/s.
 //
@@ -35,12 +37,13 @@ __device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
   return __builtin_bit_cast(v8s, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p)));
 }
 
-template <int NTW, int U, int EPI>
+template <int MB, int NTW, int U, int EPI>
 __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                             int M, int N, int K, int F, int S) {
   static_assert(EPI != EPI_GLU || NTW % 2 == 0, "GLU: gate/up tile pairs");
-  __shared__ v4f red[NW][NTW][64];
+  static_assert(MB * NTW <= 8 && MB * (EPI == EPI_GLU ? NTW / 2 : NTW) <= NW, "LDS reduction / output waves");
+  __shared__ v4f red[NW][MB * NTW][64];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = 8 * (lane >> 4);
   // output column of tile j for this lane (EPI_GLU: gate tiles then the matching up tiles)
@@ -59,12 +62,16 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   const bf16_t* wrow[NTW];                                  // tile row of this lane's fragments
 #pragma unroll
   for (int j = 0; j < NTW; ++j) wrow[j] = W + ((size_t)(min(col_of(j), N - 1) >> 4) * (2 * KP) * 64 + lane) * 8;
-  const bf16_t* arow = A + (size_t)min(r, M - 1) * K + kq;
-  v4f acc[NTW];
+  const bf16_t* arow[MB];
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int mb = 0; mb < MB; ++mb) arow[mb] = A + (size_t)min(16 * mb + r, M - 1) * K + kq;
+  v4f acc[MB][NTW];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[mb][j] = v4f{0.f, 0.f, 0.f, 0.f};
   for (int kp = kbeg + wave; kp < kend; kp += NW * U) {
-    v8s a[U][2], b[U][NTW][2];
+    v8s a[U][MB][2], b[U][NTW][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = min(kp + u * NW, kend - 1) * 64;        // clamped: loads never branch
@@ -73,57 +80,66 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
         b[u][j][0] = ld_nt(wrow[j] + (size_t)k * 16);
         b[u][j][1] = ld_nt(wrow[j] + (size_t)k * 16 + 512);
       }
-      a[u][0] = *reinterpret_cast<const v8s*>(arow + k);
-      a[u][1] = *reinterpret_cast<const v8s*>(arow + k + 32);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        a[u][mb][0] = *reinterpret_cast<const v8s*>(arow[mb] + k);
+        a[u][mb][1] = *reinterpret_cast<const v8s*>(arow[mb] + k + 32);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (kp + u * NW < kend) {                             // wave-uniform (scalar) guard
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          acc[j] = mfma_bf16(a[u][0], b[u][j][0], acc[j]);
-          acc[j] = mfma_bf16(a[u][1], b[u][j][1], acc[j]);
-        }
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) {
+            acc[mb][j] = mfma_bf16(a[u][mb][0], b[u][j][0], acc[mb][j]);
+            acc[mb][j] = mfma_bf16(a[u][mb][1], b[u][j][1], acc[mb][j]);
+          }
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) red[wave][j][lane] = acc[j];
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) red[wave][mb * NTW + j][lane] = acc[mb][j];
   __syncthreads();
-  constexpr int OUTS = EPI == EPI_GLU ? NTW / 2 : NTW;      // output tiles; wave w < OUTS writes tile w
-  if (wave < OUTS) {
+  // output units (row block, tile): wave w < MB * OUTS writes tile w % OUTS of row block w / OUTS
+  constexpr int OUTS = EPI == EPI_GLU ? NTW / 2 : NTW;
+  if (wave < MB * OUTS) {
+    const int mb = wave / OUTS, tw = wave - mb * OUTS;
     auto total = [&](int j) {                               // 4 LDS reads in flight (bounded registers)
-      v4f s = red[0][j][lane];
+      v4f s = red[0][mb * NTW + j][lane];
 #pragma unroll 4
-      for (int w = 1; w < NW; ++w) s += red[w][j][lane];
+      for (int w = 1; w < NW; ++w) s += red[w][mb * NTW + j][lane];
       return s;
     };
-    const int c0 = col_of(wave);
+    const int c0 = col_of(tw);
     if constexpr (EPI == EPI_GLU) {
-      const int c1 = col_of(wave + NTW / 2);
-      const v4f g4 = total(wave), u4 = total(wave + NTW / 2);
+      const int c1 = col_of(tw + NTW / 2);
+      const v4f g4 = total(tw), u4 = total(tw + NTW / 2);
       const float bg = bias != nullptr ? bf2f(bias[c0]) : 0.f, bu = bias != nullptr ? bf2f(bias[c1]) : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 4 * (lane >> 4) + q;
+        const int row = 16 * mb + 4 * (lane >> 4) + q;
         const float g = bf2f(f2bf(g4[q] + bg)), u = bf2f(f2bf(u4[q] + bu));
         if (row < M && c0 < F) out[(size_t)row * F + c0] = f2bf(g / (1.f + __expf(-g)) * u);
       }
     } else if constexpr (EPI == EPI_PART) {
-      const v4f s4 = total(wave);
+      const v4f s4 = total(tw);
       const float bv = bias != nullptr && c0 < N && ks == 0 ? bf2f(bias[c0]) : 0.f;
       float* part = reinterpret_cast<float*>(out) + (size_t)ks * M * N;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 4 * (lane >> 4) + q;
+        const int row = 16 * mb + 4 * (lane >> 4) + q;
         if (row < M && c0 < N) part[(size_t)row * N + c0] = s4[q] + bv;
       }
     } else {
-      const v4f s4 = total(wave);
+      const v4f s4 = total(tw);
       const float bv = bias != nullptr && c0 < N ? bf2f(bias[c0]) : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 4 * (lane >> 4) + q;
+        const int row = 16 * mb + 4 * (lane >> 4) + q;
         float v = s4[q] + bv;
         if constexpr (EPI == EPI_GELU_TANH) {
           const float a = bf2f(f2bf(v)), k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -138,22 +154,36 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   }
 }
 
+template <int MB, int NTW, int U, int EPI>
+int launch_mb(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
+              hipStream_t st, int S) {
+  const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
+  hipLaunchKernelGGL((gemv_bf16_kernel<MB, NTW, U, EPI>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
+                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S);
+  return (int)hipGetLastError();
+}
+
+// NTW / U chosen for one row block; more row blocks keep U = 2 (registers) and at most 8 / MB
+// tiles (the LDS reduction holds MB x NTW tiles of 16 waves)
 template <int NTW, int U, int EPI>
 int launch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
            hipStream_t st, int S = 1) {
-  const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
-  hipLaunchKernelGGL((gemv_bf16_kernel<NTW, U, EPI>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
-                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S);
-  return (int)hipGetLastError();
+  constexpr int G = EPI == EPI_GLU ? 2 : 1;                 // GLU keeps gate / up pairs
+  constexpr int N2 = NTW > 4 ? 4 : (NTW < G ? G : NTW), N34 = NTW > 2 ? 2 : (NTW < G ? G : NTW);
+  const int mb = (M + 15) / 16;
+  if (mb <= 1) return launch_mb<1, NTW, U, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
+  if (mb == 2) return launch_mb<2, N2, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
+  if (mb == 3) return launch_mb<3, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
+  return launch_mb<4, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
 }
 }  // namespace
 
 // W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N]; epi 1 (GLU):
-// W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F] (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 16, K % 64 == 0,
+// W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F] (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 64, K % 64 == 0,
 // N % 16 == 0.  Returns -2 for shapes it does not take.
 extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                               hipStream_t st) {
-  if (M <= 0 || M > 16 || K % 64 != 0 || N % 16 != 0 || K <= 0) return -2;
+  if (M <= 0 || M > 64 || K % 64 != 0 || N % 16 != 0 || K <= 0) return -2;
   const int KP = K / 64;
   const int U = KP >= 64 ? 4 : 2;                            // k-pairs in flight per wave
   if (epi == EPI_GLU) {
@@ -181,7 +211,7 @@ extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, vo
 // Split-K form: fp32 partial slices part [S, M, N] (bias in slice 0), one 16-column tile per group.
 extern "C" int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K,
                                      int S, hipStream_t st) {
-  if (M <= 0 || M > 16 || K % 64 != 0 || N % 16 != 0 || S < 1 || S > K / 64) return -2;
+  if (M <= 0 || M > 64 || K % 64 != 0 || N % 16 != 0 || S < 1 || S > K / 64) return -2;
   const int nt = N / 16, kps = K / 64 / S;
   return kps >= 64 ? launch<1, 4, EPI_PART>(A, W, bias, part, M, N, K, 0, nt, st, S)
                    : launch<1, 2, EPI_PART>(A, W, bias, part, M, N, K, 0, nt, st, S);

@@ -91,6 +91,14 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     wv[c] = *reinterpret_cast<const uint4*>(w + e);
     if constexpr (!RMS) bv[c] = b != nullptr ? *reinterpret_cast<const uint4*>(b + e) : make_uint4(0, 0, 0, 0);
   }
+  // the residual row too: its loads are in flight with the input's (partial slices'), so the
+  // kernel pays one memory round trip, not two (decode at 1-128 rows is latency-bound here)
+  uint4 rv[NCH];
+  if constexpr (HAS_RES) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      rv[c] = *reinterpret_cast<const uint4*>(res + row * H + min((c * NT + (int)threadIdx.x) * 8, H - 8));
+  }
   float v[NCH][8];
   if constexpr (PART) {
     // every slice's loads are issued before the first add (S <= 8: one memory round trip, not S)
@@ -131,12 +139,14 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     load_row<NCH>(x + row * H, H, v);
   }
   if constexpr (HAS_RES) {
-    float r[NCH][8];
-    load_row<NCH>(res + row * H, H, r);
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
+    for (int c = 0; c < NCH; ++c) {
+      if ((c * NT + (int)threadIdx.x) * 8 >= H) continue;    // clamped load: not this row's data
+      float r[8];
+      unpack8(rv[c], r);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] += r[c][j];
+      for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+    }
     // the residual stream is kept in bf16 (as HF does); normalise the rounded value
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {

@@ -365,7 +365,7 @@ def test_model_split_k_decode_matches_unsplit(cuda):
     assert all(len(t) == 12 for t in out)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 33, 48, 64])
 @pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 8192), (7680, 2560), (32000, 4096), (48, 64)])
 @pytest.mark.parametrize("bias", [False, True])
 def test_gemv_bf16(cuda, M, N, K, bias):
@@ -382,7 +382,7 @@ def test_gemv_bf16(cuda, M, N, K, bias):
     assert torch.equal(y, C.gemv_bf16(x, ops.pack_bf16_weight(w), b, N, 0))
 
 
-@pytest.mark.parametrize("M", [1, 7, 16])
+@pytest.mark.parametrize("M", [1, 7, 16, 31, 64])
 @pytest.mark.parametrize("F,K", [(8192, 2048), (5632, 2048), (64, 128)])
 def test_gemv_bf16_glu(cuda, M, F, K):
     """Fused bf16 gate_up GEMV + SwiGLU over the natural [gate | up] rows == unfused reference
@@ -400,18 +400,20 @@ def test_gemv_bf16_glu(cuda, M, F, K):
 
 
 def test_linear_bf16_routes_decode_rows(cuda):
-    """ops.linear_bf16: <= 16 rows take the HIP GEMV, larger batches hipBLASLt; both agree."""
+    """ops.linear_bf16: <= BF16_GEMV_MAX_ROWS rows take the HIP GEMV, larger batches hipBLASLt;
+    both agree."""
     torch.manual_seed(0)
+    n = ops.BF16_GEMV_MAX_ROWS
     w = (torch.randn(4096, 2048, device=cuda) * 0.05).bfloat16()
-    x = torch.randn(16, 2048, device=cuda).bfloat16()
-    assert ops.bf16_gemv_ok(x, w) and not ops.bf16_gemv_ok(torch.cat([x, x]), w)
+    x = torch.randn(n, 2048, device=cuda).bfloat16()
+    assert ops.bf16_gemv_ok(x, w) and not ops.bf16_gemv_ok(torch.cat([x, x[:1]]), w)
     small = ops.linear_bf16(x, w)
-    big = ops.linear_bf16(torch.cat([x, x]), w)[:16]
+    big = ops.linear_bf16(torch.cat([x, x[:1]]), w)[:n]
     _close(small, big, 2e-2, 1e-2)
 
 
 @pytest.mark.parametrize("act", ["gelu_tanh", "gelu"])
-@pytest.mark.parametrize("M,N,K", [(1, 10240, 2560), (16, 8192, 2048)])
+@pytest.mark.parametrize("M,N,K", [(1, 10240, 2560), (16, 8192, 2048), (50, 10240, 2560)])
 def test_gemv_bf16_gelu(cuda, act, M, N, K):
     """bf16 GEMV with the GELU epilogue == hipBLASLt GEMM -> act_kernel (Phi-2 / Pythia up-proj)."""
     torch.manual_seed(N + M)
@@ -455,7 +457,7 @@ def test_llmint8_device_outliers(cuda, M, K, N, outliers):
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("M", [1, 16])
+@pytest.mark.parametrize("M", [1, 16, 40, 64])
 @pytest.mark.parametrize("N,K,S", [(2048, 8192, 2), (2048, 2048, 2), (4096, 4096, 3)])
 def test_gemv_bf16_split_k(cuda, M, N, K, S):
     """bf16 split-K partial slices sum to the unsplit GEMV (fp32 tolerance), bias in slice 0."""

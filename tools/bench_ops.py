@@ -379,6 +379,37 @@ def ring_rows(C, dev, Ms=(128, 96)):
     return out
 
 
+def bf16_rows(C, dev, Ms=(8, 16, 32, 48, 64)):
+    """bf16 decode projections at 1-64 rows (Llama-2-7B shapes), cache-cold: gemv_bf16.hip
+    (1-4 row blocks of 16 per weight read) vs hipBLASLt through torch.nn.functional.linear."""
+    out = []
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
+              "lm_head": (32000, 4096)}
+    for name, (N, K) in shapes.items():
+        ncopy = max(2, (1 << 30) // (2 * N * K) + 1)
+        ws = [(torch.randn(N, K, device=dev) * 0.02).bfloat16() for _ in range(ncopy)]
+        wps = [ops.pack_bf16_weight(w) for w in ws]
+        for M in Ms:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            ctr = [0]
+
+            def ours():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.gemv_bf16(x, wps[ctr[0]], None, N, 0)
+
+            def blas():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return torch.nn.functional.linear(x, ws[ctr[0]])
+
+            t_o = min(timeit(ours, iters=10, per_graph=ncopy) for _ in range(2))
+            t_b = min(timeit(blas, iters=10, per_graph=ncopy) for _ in range(2))
+            out.append(dict(op="bf16_rows", shape=name, M=M, N=N, K=K, gemv_us=round(t_o, 2), hipblaslt_us=round(t_b, 2),
+                            gemv_TBps=round(2 * N * K / t_o / 1e6, 2), hipblaslt_TBps=round(2 * N * K / t_b / 1e6, 2)))
+            print(out[-1], flush=True)
+        del ws, wps
+    return out
+
+
 def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
     interleaved in one process ((form, issue): form 0 automatic, 2 / 3 the LDS-DMA ring kernel at
@@ -440,6 +471,8 @@ def main():
         rows += batch1_rows(C, dev)
     if only is not None and "ring" in only:
         rows += ring_rows(C, dev)
+    if only is not None and "bf16rows" in only:
+        rows += bf16_rows(C, dev)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
