@@ -55,6 +55,10 @@ void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_gemv_ring(int on);
 void edge_w8a8_prefill_gemm(int v, int b);
 void edge_w8a8_ring2_cfg(int v, int rot);
+void edge_w8a8_prefill_apack(int v);
+int edge_w8a8_apack_ok(int M, int N, int K, int KT);
+int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
+                       void* out, int M, int N, int K, int KT, hipStream_t st);
 void edge_decode_attn_config(int target_wg);
 int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, void* vc, float* ks, float* vs, int64_t c_sb,
                         int64_t c_sh, int64_t s_sb, int64_t s_sh, const int* seq_lens, int B, int Hq, int Hkv, int D,
@@ -466,6 +470,15 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
   auto os = a.sizes().vec();
   os.back() = N;
   auto out = at::empty(os, a.options().dtype(at::kBFloat16));
+  if (mpad == 0 && a.is_contiguous() && edge_w8a8_apack_ok((int)M, (int)N, (int)K, (int)KT)) {
+    // prefill: A fragment-packed into a stream-ordered scratch, then the ring GEMM on contiguous pieces
+    auto ap = at::empty({(M + 15) / 16 * 16 * K}, a.options());
+    check(edge_w8a8_gemm_apk(a.data_ptr(), ap.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                             bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N, (int)K, (int)KT,
+                             stream()),
+          "w8a8_gemm_apk");
+    return out;
+  }
   check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
                        bias ? bias->data_ptr() : nullptr, out.data_ptr(), nullptr, (int)M, (int)N, (int)K, (int)KT,
                        mpad > 0 ? 1 : 0, (int)mpad, 0, stream()),
@@ -701,6 +714,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
     else if (what == "ring2_cfg") edge_w8a8_ring2_cfg((int)a, (int)b);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
+    else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
     else if (what == "decode_attn_gsplit") edge_decode_attn_gsplit((int)a);

@@ -662,7 +662,11 @@ __device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_r
 //  * blockIdx -> tile: bijective XCD remap (each XCD gets a contiguous range), then groups of 4
 //    row tiles walked column-major, so an XCD's ~32 resident blocks share 4 A panels and 8 W panels
 //    in its L2.
-template <int BMV, int ISS>
+//  * APK: A arrives fragment-packed (pack_a_kernel: 1 KiB = 16 rows x 64 k per (row block, k-tile),
+//    the layout of the packed weights), so an A piece is 1 KiB of contiguous bytes instead of 16
+//    rows x 64 B — the pattern tools/ingest_bw.hip measured at ~18 B/clk/CU L2 -> LDS against
+//    ~60 for contiguous pieces.  The LDS image is identical, only the DMA source offsets change.
+template <int BMV, int ISS, bool APK = false>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
@@ -693,7 +697,10 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int p = wave + NWV * i;
-    if (p < AP) {
+    if (p < AP && APK) {
+      const int rb = min(bm * (BMV / 16) + p, (M + 15) / 16 - 1);
+      off[i] = (uint32_t)rb * (uint32_t)KT * 1024u + lane * 16;
+    } else if (p < AP) {
       const int row = min(bm * BMV + p * 16 + (lane & 15), M - 1);
       off[i] = (uint32_t)row * (uint32_t)K + 16 * (lane >> 4);
     } else {
@@ -707,7 +714,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
   auto issue_piece = [&](int st, int i) {
     const int kt = min(st, KT - 1);
     const bool isa = wave + NWV * i < AP;
-    glds16((isa ? A + (size_t)kt * 64 : Wp + (size_t)kt * 1024) + off[i],
+    glds16((isa ? A + (size_t)kt * (APK ? 1024 : 64) : Wp + (size_t)kt * 1024) + off[i],
            ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
   };
   auto issue = [&](int st) {
@@ -850,6 +857,21 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
       if (row < M && col0 < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col0) = pack8(v);   // N % 8 == 0
     }
   }
+}
+
+// Fragment-pack A [M, K] int8 for the APK prefill GEMM: piece (rb, kt) = 1 KiB at
+// (rb * KT + kt) * 1024, lane l's 16 B = A[16 rb + (l & 15)][64 kt + 16 (l >> 4) ..] (rows past M
+// repeat row M - 1; the GEMM never stores them).  One thread per 16 B; writes are contiguous.
+__global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ A, int8_t* __restrict__ Ap, int M, int K,
+                                                     int KT, int64_t total) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int64_t piece = t >> 6;
+  const int lane = (int)(t & 63);
+  const int rb = (int)(piece / KT), kt = (int)(piece - (int64_t)rb * KT);
+  const int row = min(rb * 16 + (lane & 15), M - 1);
+  *reinterpret_cast<uint4*>(Ap + t * 16) =
+      *reinterpret_cast<const uint4*>(A + (size_t)row * K + (size_t)kt * 64 + 16 * (lane >> 4));
 }
 
 // ------------------------------------------------------------------------------------- ring
@@ -1309,7 +1331,8 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_ring2_cfg = 0, g_ring2_rot = 1;
 extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
-static int g_prefill_gemm = 0, g_prefill_iss = 2;
+static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1;
+extern "C" void edge_w8a8_prefill_apack(int v) { g_prefill_apack = v; }
 // b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
 // MFMAs, 2 interleaved into them: the default, 1-3 % ahead of 0 on the Llama-2-7B shapes)
 extern "C" void edge_w8a8_prefill_gemm(int v, int b) { g_prefill_gemm = v; g_prefill_iss = b; }
@@ -1580,7 +1603,7 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     if (mblocks <= 2) return launch_one<2, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
     return launch_one<4, 4, 2, 4, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
   }
-  if (M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1) {
+  if (M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1) {   // (see edge_w8a8_gemm_apk)
     // 128 x 256 tiles, except 256 x 256 for the long-K down projection when those still fill the
     // chip (tools/bench_ops.py pgemm, Llama-2-7B shapes at M = 512 / 2048 / 16384: 128-row tiles
     // 1.5-2.1 POPS, equal or ahead everywhere but K = 11008 at M = 16384, 2.21 vs 2.11)
@@ -1627,4 +1650,38 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   if (mblocks <= 2) OUT(2, A_TOKEN);
   OUT(4, A_TOKEN);
 #undef OUT
+}
+
+// Prefill GEMM with A fragment-packed first (APK form of w8a8_gemm_big_kernel).  Ap: scratch of
+// (M + 15) / 16 * 16 * K bytes from the caller's (stream-ordered) allocator.  Returns -2 when the
+// shape does not take the ring GEMM (the caller then runs edge_w8a8_gemm).
+// g_prefill_apack: 0 off, 1 automatic, 2 always.  Automatic = wide N at >= 2048 rows, where every A
+// panel is re-read by >= 32 column blocks (tools/bench_ops.py pgemm, Llama-2-7B shapes: gate_up
+// 1.91 -> 2.10 POPS and qkv 1.96 -> 2.04 at M = 16384; at N = 4096 or M = 512 the extra pass over
+// A costs more than the contiguous pieces save, o at M = 2048 1.85 -> 1.69)
+extern "C" int edge_w8a8_apack_ok(int M, int N, int K, int KT) {
+  const bool want = g_prefill_apack == 2 || (g_prefill_apack == 1 && N >= 8192 && M >= 2048);
+  return want && M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1 &&
+         (int64_t)((M + 15) / 16) * KT * 1024 < (int64_t)1 << 32;
+}
+
+extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw,
+                                  const void* bias, void* out, int M, int N, int K, int KT, hipStream_t st) {
+  if (!edge_w8a8_apack_ok(M, N, K, KT)) return -2;
+  const int64_t total = (int64_t)((M + 15) / 16) * KT * 64;
+  hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const int8_t*)A,
+                     (int8_t*)Ap, M, K, KT, total);
+  const int NTt = (N + 15) / 16;
+  const int grid_n = (NTt * 16 + 255) / 256;
+  const int g256 = (M + 255) / 256, g128 = (M + 127) / 128;
+  const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && K > 8192 && g256 * grid_n >= 256);
+  const int grid_m = big ? g256 : g128;
+#define BIGP(BMV, ISS)                                                                                            \
+  hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS, true>), dim3(grid_m * grid_n), dim3(512), 0, st,            \
+                     (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, \
+                     grid_m, grid_n)
+  if (big) BIGP(256, 2);
+  else BIGP(128, 2);
+#undef BIGP
+  return (int)hipGetLastError();
 }

@@ -175,9 +175,10 @@ PREFILL_FORMS = {"auto": (0, 2), "tiled128": (1, 0), "ring256": (2, 0), "ring128
                  "ring128_late": (3, 1), "ring256_ilv": (2, 2), "ring128_ilv": (3, 2)}
 
 
+@pytest.mark.parametrize("apack", [0, 2])
 @pytest.mark.parametrize("form", list(PREFILL_FORMS))
 @pytest.mark.parametrize("M,N,K", [(300, 272, 64), (129, 1040, 192), (1000, 520, 128), (640, 4096, 256)])
-def test_w8a8_prefill_layout_exact(cuda, form, M, N, K):
+def test_w8a8_prefill_layout_exact(cuda, apack, form, M, N, K):
     """Exact integers through every prefill GEMM form: row m of A selects column (7m mod K), so
     out[m] must equal that column of an asymmetric W — catches swapped operands, a wrong
     LDS-restaged store, ring slots read early (1..4 k-tiles: every prologue/tail wait) and
@@ -190,15 +191,18 @@ def test_w8a8_prefill_layout_exact(cuda, form, M, N, K):
     wp = ops.pack_int8_weight(w)
     try:
         C.tune("prefill_gemm", *PREFILL_FORMS[form])
+        C.tune("prefill_apack", apack, 0)
         out = C.w8a8_gemm(a, torch.ones(M, device=cuda), wp, torch.ones(N, device=cuda), None, N, K)
     finally:
         C.tune("prefill_gemm", 0, 2)
+        C.tune("prefill_apack", 1, 0)
     assert torch.equal(out.float(), w[:, sel].t().float())
 
 
+@pytest.mark.parametrize("apack", [0, 2])
 @pytest.mark.parametrize("form", list(PREFILL_FORMS))
 @pytest.mark.parametrize("M,N,K", [(2100, 4096, 4096), (777, 11008, 4096), (520, 4096, 11008)])
-def test_w8a8_prefill_gemm(cuda, form, M, N, K):
+def test_w8a8_prefill_gemm(cuda, apack, form, M, N, K):
     """Random int8 operands, per-token / per-channel scales and bias vs the fp32 reference."""
     C = ops.ext()
     g = torch.Generator(device=cuda).manual_seed(M + N)
@@ -210,10 +214,33 @@ def test_w8a8_prefill_gemm(cuda, form, M, N, K):
     wp = ops.pack_int8_weight(w)
     try:
         C.tune("prefill_gemm", *PREFILL_FORMS[form])
+        C.tune("prefill_apack", apack, 0)
         out = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
     finally:
         C.tune("prefill_gemm", 0, 2)
+        C.tune("prefill_apack", 1, 0)
     _close(out, _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32), 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(2100, 4096, 4096), (131, 12288, 4096), (1000, 4096, 11008)])
+def test_w8a8_prefill_apack_bit_exact(cuda, M, N, K):
+    """Fragment-packed A (pack_a_kernel + contiguous DMA pieces) loads the same LDS image as the
+    row-major A pieces: identical outputs, bit for bit."""
+    C = ops.ext()
+    g = torch.Generator(device=cuda).manual_seed(M)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda, generator=g)
+    sx = torch.rand(M, device=cuda, generator=g) * 0.02 + 1e-3
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda, generator=g)
+    sw = torch.rand(N, device=cuda, generator=g) * 0.02 + 1e-3
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("prefill_apack", 0, 0)
+        row_major = C.w8a8_gemm(qx, sx, wp, sw, None, N, K)
+        C.tune("prefill_apack", 2, 0)
+        packed = C.w8a8_gemm(qx, sx, wp, sw, None, N, K)
+    finally:
+        C.tune("prefill_apack", 1, 0)
+    assert torch.equal(row_major, packed)
 
 
 @pytest.mark.parametrize("ntw,nw,u", [(2, 4, 2), (4, 8, 4), (4, 16, 2), (2, 16, 4)])

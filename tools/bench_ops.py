@@ -417,8 +417,9 @@ def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     MFMAs / interleaved into them)."""
     out = []
     shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
-    forms = {"auto": (0, 2), "ring256": (2, 0), "ring128": (3, 0), "ring256_late": (2, 1), "ring128_late": (3, 1),
-             "ring256_ilv": (2, 2), "ring128_ilv": (3, 2)}
+    # (prefill_gemm form, DMA issue point, A fragment-packed first)
+    forms = {"auto": (0, 2, 1), "auto_rowmajorA": (0, 2, 0), "ring256_apack": (2, 2, 2), "ring128_apack": (3, 2, 2),
+             "ring256_ilv": (2, 2, 0), "ring128_ilv": (3, 2, 0)}
     for name, (N, K) in shapes.items():
         w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
         wp = ops.pack_int8_weight(w)
@@ -429,11 +430,13 @@ def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
             res = {}
             for rnd in range(2):
                 for form, v in forms.items():
-                    C.tune("prefill_gemm", *v)
+                    C.tune("prefill_gemm", v[0], v[1])
+                    C.tune("prefill_apack", v[2], 0)
                     per = max(2, min(20, int(4e11 // (M * N * K))))
                     res.setdefault(form, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K),
                                                            iters=5, per_graph=per))
             C.tune("prefill_gemm", 0, 2)
+            C.tune("prefill_apack", 1, 0)
             row = dict(op="w8a8_gemm_prefill", shape=name, M=M, N=N, K=K)
             for form, ts in res.items():
                 row[form + "_us"] = round(min(ts), 1)
