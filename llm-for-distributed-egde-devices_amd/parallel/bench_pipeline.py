@@ -80,11 +80,14 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     # ticks count item groups of L micro-batches (one per lane)
     t_a = (M + W * M) // L + (P - 1)
     t_b = t_a + K * M // L
+    # prefill window: tick 0 to the first tick after every prefill group left the last stage
+    # (synchronised like the timed window; it ends before the warm-up decodes are timed)
+    t_p = M // L + (P - 1)
     marks = {}
     stamps = []
 
     def hook(t):
-        if t in (t_a, t_b):
+        if t in (0, t_p, t_a, t_b):
             if use_cuda:
                 torch.cuda.synchronize()
             dist.barrier()
@@ -104,7 +107,7 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     res_stage = stage.run(prompts, T, sp, S, seed=args.seed, hook=hook, watchdog=wd, stats_window=(t_a, t_b))
     wd.beat("report")
     fdt = torch.float64
-    dt = torch.tensor([marks[t_b] - marks[t_a]], device=cdev, dtype=fdt)
+    dt = torch.tensor([marks[t_b] - marks[t_a], marks[t_p] - marks[0]], device=cdev, dtype=fdt)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     lat = torch.zeros(1, device=cdev, dtype=fdt)
     if stage.is_last and len(stamps) > 1:
@@ -120,7 +123,7 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     mine = torch.tensor([[float(res_stage.stats.get(k, float("nan"))) for k in _STAT_KEYS]], device=cdev, dtype=fdt)
     allst = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allst, mine)
-    elapsed = float(dt.item())
+    elapsed, prefill_s = float(dt[0].item()), float(dt[1].item())
     res = None
     if rank == 0:
         tokens = K * M * b
@@ -131,6 +134,7 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
             per_rank.append(d)
         ttft = [d["ttft_ms"] for d in per_rank if "ttft_ms" in d]
         res = dict(value=tokens / elapsed, ms_per_step=elapsed / K * 1e3, p50=float(lat.item()), global_batch=M * b,
+                   prefill_tps=M * b * T / prefill_s if prefill_s > 0 else 0.0,
                    mem_gb=float(mem.item()), partition=bounds, world_size=world, per_rank=per_rank,
                    bubble_frac_max=max(d.get("bubble_frac", 0.0) for d in per_rank),
                    ttft_ms=ttft[0] if ttft else None,
