@@ -1396,6 +1396,8 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
       if (g_ring2_cfg == 2) R2S(4, 2, 12, 3);
       if (g_ring2_cfg == 3) R2S(2, 2, 16, 4);
       if (g_ring2_cfg == 4) R2S(4, 4, 12, 3);
+      if (g_ring2_cfg == 5) R2S(4, 4, 6, 6);            // deeper activation ring (short o slices)
+      if (g_ring2_cfg == 6) R2S(4, 4, 5, 7);
 #undef R2S
     }
   }

@@ -548,7 +548,7 @@ def test_gluq_ring_matches_ldsa(cuda, ring, M):
     assert (q1.int() - q0.int()).abs().max() <= 1      # __expf in both; identical but for fma contraction
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M", [65, 100, 128])
 @pytest.mark.parametrize("N,K,S", [(4096, 4096, 4), (4096, 11008, 4), (1024, 14336, 4)])
 def test_ring2_grouped_splitk(cuda, cfg, M, N, K, S):

@@ -41,7 +41,7 @@ if os.environ.get("O_PROBE_TIME"):
         sw = torch.rand(N, device=dev) * 0.01
         qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
         sx = torch.rand(K // 64, M, device=dev) * 0.01
-        for ring, cfg, S in [(0, 0, 4), (2, 1, 4), (2, 1, 2), (2, 3, 2), (2, 3, 4), (2, 2, 2)]:
+        for ring, cfg, S in [(0, 0, 4), (2, 1, 4), (2, 5, 4), (2, 6, 4), (2, 4, 4)]:
             if ring == 0 and S != 4:
                 continue
             C.tune("gemv_ring", ring, 0)
