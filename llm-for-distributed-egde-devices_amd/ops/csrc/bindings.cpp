@@ -56,6 +56,7 @@ void edge_w8a8_gemv_ring(int on);
 void edge_w8a8_prefill_gemm(int v, int b);
 void edge_w8a8_ring2_cfg(int v, int rot);
 void edge_w8a8_prefill_apack(int v);
+void edge_w8a8_weight_nt(int v);
 int edge_w8a8_apack_ok(int M, int N, int K, int KT);
 int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
                        void* out, int M, int N, int K, int KT, hipStream_t st);
@@ -715,6 +716,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "ring2_cfg") edge_w8a8_ring2_cfg((int)a, (int)b);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);
+    else if (what == "weight_nt") edge_w8a8_weight_nt((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
     else if (what == "decode_attn_gsplit") edge_decode_attn_gsplit((int)a);

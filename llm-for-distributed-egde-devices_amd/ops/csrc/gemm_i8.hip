@@ -1120,7 +1120,9 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // waves also DMA each stage's scales (one 1 KiB piece: 2 k-tiles x Mpad rows, lanes split over the
 // loader waves) into a third ring, and every k-tile's int32 MFMA result is folded in fp32.
 // EPI_PART: blockIdx = group * S + slice; slice ks reduces stages [NS ks / S, NS (ks + 1) / S).
-template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false>
+// WNT: weight DMA with the nontemporal cache policy (default); false = normal allocation, so the
+// other lane's read of the same layer can hit the memory-side cache (A/B knob "weight_nt")
+template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true>
 __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
@@ -1163,7 +1165,10 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
       const int p = phys(st);
       const int8_t* wb = Wp + (size_t)p * 2048;
 #pragma unroll
-      for (int i = 0; i < WPW; ++i) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
+      for (int i = 0; i < WPW; ++i) {
+        if constexpr (WNT) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
+        else glds16(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
+      }
       if constexpr (SC) {
         if (smine) glds16(sa + (size_t)(2 * p) * Mpad + soff, sring + (st % RW) * 1024);
       }
@@ -1330,6 +1335,8 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_ring2_cfg = 0, g_ring2_rot = 1;
 extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
+static int g_w_nt = 1;
+extern "C" void edge_w8a8_weight_nt(int v) { g_w_nt = v; }
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
 static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1;
 extern "C" void edge_w8a8_prefill_apack(int v) { g_prefill_apack = v; }
@@ -1384,6 +1391,12 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
       const int NTt = (N + 15) / 16;
 #define R2S(NTWV, NWLV, RWV, RAV)                                                                                    \
   do {                                                                                                           \
+    if (!g_w_nt) {                                                                                             \
+      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPI_PART, true, true, false>),          \
+                         dim3((NTt + NTWV - 1) / NTWV * S), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, \
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);          \
+      return (int)hipGetLastError();                                                                           \
+    }                                                                                                          \
     hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPI_PART, true, true>),                     \
                        dim3((NTt + NTWV - 1) / NTWV * S), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa,   \
                        (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);            \
@@ -1406,6 +1419,12 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
     const int NTt = (N + 15) / 16;
 #define R2(NTWV, NWLV, RWV, RAV, EPV)                                                                            \
   do {                                                                                                           \
+    if (!g_w_nt) {                                                                                             \
+      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, true, false, false>),              \
+                         dim3((NTt + NTWV - 1) / NTWV), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa,    \
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, 1);          \
+      return (int)hipGetLastError();                                                                           \
+    }                                                                                                          \
     if (g_ring2_rot == 0) {                                                                                    \
       hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false>), dim3((NTt + NTWV - 1) / NTWV), \
                          dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,            \
