@@ -53,5 +53,17 @@ if os.environ.get("O_PROBE_TIME"):
                 return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, S)
             t = min(timeit(call, iters=10, per_graph=ncopy) for _ in range(3))
             print(dict(shape=sh, ring=ring, cfg=cfg, S=S, us=round(t, 2)), flush=True)
+        # unsplit (EPI_OUT, bf16 out) on the same grouped-scale input: isolates the fp32 slice writes
+        C.tune("gemv_ring", 0, 0)
+        ctr = [0]
+
+        def call_out():
+            ctr[0] = (ctr[0] + 1) % ncopy
+            return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
+        try:
+            t = min(timeit(call_out, iters=10, per_graph=ncopy) for _ in range(3))
+            print(dict(shape=sh, ring=0, cfg=0, S=1, epi="out_bf16", us=round(t, 2)), flush=True)
+        except RuntimeError as e:      # no unsplit 128-row kernel for this K (down: 172 k-tiles)
+            print(dict(shape=sh, S=1, epi="out_bf16", skipped=str(e)[:80]), flush=True)
     C.tune("gemv_ring", 2, 0)
     C.tune("ring2_cfg", 0, 1)
