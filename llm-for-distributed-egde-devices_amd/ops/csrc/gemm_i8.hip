@@ -1333,7 +1333,7 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 }
 }  // namespace
 
-static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_ring2_cfg = 0, g_ring2_rot = 1;
+static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_ring2_cfg = 0, g_ring2_rot = 0;
 extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
 static int g_w_nt = 1;
 extern "C" void edge_w8a8_weight_nt(int v) { g_w_nt = v; }
@@ -1403,9 +1403,11 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
     return (int)hipGetLastError();                                                                             \
   } while (0)
       // measured at M = 128 (tools/bench_ops.py --only ring): down (K = 11008) 22.4 -> 20.1 us with
-      // (4, 4, 8, 4); o (K = 4096, 8 stages per slice) stays on the LDS-staged kernel (11.5 us vs
-      // 12.0-15.4 for every ring2 geometry)
-      if (g_ring2_cfg == 1 || (g_ring2_cfg == 0 && K >= 8192)) R2S(4, 4, 8, 4);
+      // (4, 4, 8, 4).  o (K = 4096, 8 stages per slice) is 11.6 us LDS-staged and 12.0 here alone,
+      // but the 2-lane bench with o / down / qkv / gate_up all on ring2 (this geometry, no k
+      // rotation for qkv / gate_up) measured 32.9-33.4k against 32.2-32.4k tok/s (interleaved
+      // A/B, profiles/bench_ring2_cfg_ab_r2.jsonl).  cfg 7: o back on the LDS-staged kernel.
+      if (g_ring2_cfg == 0 || g_ring2_cfg == 1 || (g_ring2_cfg == 7 && K >= 8192)) R2S(4, 4, 8, 4);
       if (g_ring2_cfg == 2) R2S(4, 2, 12, 3);
       if (g_ring2_cfg == 3) R2S(2, 2, 16, 4);
       if (g_ring2_cfg == 4) R2S(4, 4, 12, 3);
@@ -1438,15 +1440,15 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
   } while (0)
     if constexpr (EP == EPI_GLUQ) {
       if (N % 128 == 0) {
-        if (g_ring2_cfg == 1) R2(8, 4, 5, 4, EPI_GLUQ);
+        if (g_ring2_cfg == 3) R2(8, 4, 6, 3, EPI_GLUQ);       // the first default (27.6 us)
         if (g_ring2_cfg == 2) R2(8, 4, 4, 5, EPI_GLUQ);
-        R2(8, 4, 6, 3, EPI_GLUQ);
+        R2(8, 4, 5, 4, EPI_GLUQ);
       }
     } else if constexpr (EP == EPI_OUT) {
-      if (g_ring2_cfg == 1) R2(3, 3, 14, 4, EPI_OUT);
+      if (g_ring2_cfg == 4) R2(3, 3, 16, 3, EPI_OUT);      // the first default (18.3-19.0 us)
       if (g_ring2_cfg == 2) R2(3, 6, 16, 3, EPI_OUT);
       if (g_ring2_cfg == 3) R2(4, 4, 12, 4, EPI_OUT);
-      R2(3, 3, 16, 3, EPI_OUT);
+      R2(3, 3, 14, 4, EPI_OUT);
     }
 #undef R2
   }

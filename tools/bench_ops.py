@@ -337,7 +337,7 @@ def ring_rows(C, dev, Ms=(128, 96)):
                     C.tune("ring2_cfg", cfg, rot)
                     res.setdefault(form * 100 + cfg * 10 + rot, []).append(timeit(call, iters=10, per_graph=ncopy))
             C.tune("gemv_ring", 2, 0)
-            C.tune("ring2_cfg", 0, 1)
+            C.tune("ring2_cfg", 0, 0)
             row = dict(op="w8a8_rows128", shape=name, M=M, N=N, K=K)
             for form, ts in res.items():
                 row[f"ring{form}_us"] = round(min(ts), 2)
@@ -368,7 +368,7 @@ def ring_rows(C, dev, Ms=(128, 96)):
                     C.tune("ring2_cfg", cfg, 1)
                     res.setdefault(form * 100 + cfg * 10 + 1, []).append(timeit(call, iters=10, per_graph=ncopy))
             C.tune("gemv_ring", 2, 0)
-            C.tune("ring2_cfg", 0, 1)
+            C.tune("ring2_cfg", 0, 0)
             row = dict(op="w8a8_rows128_grouped_splitk4", shape=name, M=M, N=N, K=K)
             for form, ts in res.items():
                 row[f"ring{form}_us"] = round(min(ts), 2)

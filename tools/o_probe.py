@@ -66,4 +66,4 @@ if os.environ.get("O_PROBE_TIME"):
         except RuntimeError as e:      # no unsplit 128-row kernel for this K (down: 172 k-tiles)
             print(dict(shape=sh, S=1, epi="out_bf16", skipped=str(e)[:80]), flush=True)
     C.tune("gemv_ring", 2, 0)
-    C.tune("ring2_cfg", 0, 1)
+    C.tune("ring2_cfg", 0, 0)
