@@ -80,12 +80,27 @@ def rms_norm_parts(parts, residual, weight, eps, quant: bool):
 def decode_rows_ok(M: int, K: int, splits: int = 1) -> bool:
     """Whether the decode GEMV family (grouped scales, split-K, quantising GLU) takes M rows at
     this K: every K up to 64 rows; 65-128 rows (two micro-batches in one) for the k-tile counts
-    gemm_i8.hip instantiates (K = 4096 whole; 4096 / 11008 / 14336 in 4 slices)."""
+    gemm_i8.hip instantiates (K = 4096 whole; 4096 / 11008 / 14336 in 4 slices); 129-256 rows
+    (one 256-row micro-batch: the row-split ring2 kernels, split-K count fixed per K) for
+    K % 128 == 0."""
     if M <= 64:
         return True
-    if M > 128 or not available():
+    if M > 256 or not available():
         return False
+    if M > 128:
+        return bool(ext().rows256_ok(K))
     return bool(ext().rows128_ok(K, splits))
+
+
+# Activation scales of the o / down inputs at 129-256 decode rows: "group" = per (token, 64) from
+# the fused producers (attention epilogue, quantising SwiGLU GEMM), folded per k-tile in the GEMM;
+# "token" = bf16 producer output + a per-token quant launch, no fold in the GEMM (A/B knob)
+DEC256_GROUP = os.environ.get("EDGELLM_DEC256_SCALES", "group") == "group"
+
+
+def group_scale_rows_ok(M: int) -> bool:
+    """Whether decode producers emit per-(token, 64) scales at M rows (always up to 128)."""
+    return M <= 128 or DEC256_GROUP
 
 
 def w8a8_linear_splitk(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, splits: int = 0):

@@ -4,6 +4,7 @@
 // torch's caching allocator (graph-capture safe) and launches on torch's current HIP stream.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 #include <optional>
@@ -43,6 +44,9 @@ int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* 
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st, int mode, int* used);
 void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
+int edge_w8a8_rows256_ok(int K);
+int edge_w8a8_rows256_splits(int K);
+void edge_w8a8_rows256_cfg(int cfg, int nt);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st);
 int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
@@ -78,6 +82,10 @@ void edge_decode_attn_gsplit(int v);
 namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// Every entry point runs on the device of its first tensor argument: the kernels launch on the
+// current device's current stream, so a caller whose current device differs (a layer of another
+// pipeline stage, parallel/split.py) still gets its kernels on the owning GPU and stream.
+#define DEVICE_GUARD(t) const c10::hip::OptionalHIPGuardMasqueradingAsCUDA device_guard_((t).is_cuda() ? std::optional<c10::Device>((t).device()) : std::nullopt)
 
 void check(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "edgellm HIP kernel '", what, "' failed with code ", rc,
@@ -98,6 +106,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
                                                                     const at::Tensor& w,
                                                                     const std::optional<at::Tensor>& b, double eps,
                                                                     bool rms, bool quant) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "weight");
   const int64_t H = x.size(-1), R = rows_of(x);
@@ -131,6 +140,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
 std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(const at::Tensor& parts,
                                                                               const std::optional<at::Tensor>& residual,
                                                                               const at::Tensor& w, double eps, bool quant) {
+  DEVICE_GUARD(parts);
   need(parts, at::kFloat, "parts");
   need(w, at::kBFloat16, "weight");
   TORCH_CHECK(parts.dim() == 3, "parts must be [S, M, H]");
@@ -159,6 +169,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(con
 
 // ---------------------------------------------------------------------------------- activations
 std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64_t mode, bool quant) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   const int64_t W = x.size(-1), R = rows_of(x);
   const int64_t F = (mode == 0 || mode == 3) ? W / 2 : W;
@@ -181,6 +192,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64
 }
 
 std::tuple<at::Tensor, at::Tensor> quant(const at::Tensor& x) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   const int64_t H = x.size(-1), R = rows_of(x);
   auto q = at::empty(x.sizes(), x.options().dtype(at::kChar));
@@ -192,6 +204,7 @@ std::tuple<at::Tensor, at::Tensor> quant(const at::Tensor& x) {
 }
 
 at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
+  DEVICE_GUARD(ids);
   need(ids, at::kLong, "ids");
   need(table, at::kBFloat16, "table");
   auto os = ids.sizes().vec();
@@ -204,6 +217,7 @@ at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
 }
 
 at::Tensor max_prob(const at::Tensor& logits) {
+  DEVICE_GUARD(logits);
   TORCH_CHECK(logits.is_cuda() && logits.is_contiguous());
   const bool bf = logits.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
@@ -226,6 +240,7 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
                          at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot,
                          const std::optional<at::Tensor>& k2, const std::optional<at::Tensor>& v2, int64_t split,
                          const std::optional<at::Tensor>& cpos2) {
+  DEVICE_GUARD(qkv);
   need(qkv, at::kBFloat16, "qkv");
   need(start_pos, at::kInt, "start_pos");
   check_cache(k_cache, "k_cache", D);
@@ -265,6 +280,7 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
 // ---------------------------------------------------------------------------------- attention
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                        const at::Tensor& seq_lens, double scale, int64_t max_len_hint) {
+  DEVICE_GUARD(q);
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && q.dim() == 3, "q must be bf16 [B, Hq, D]");
   TORCH_CHECK(q.stride(2) == 1 && q.stride(1) == q.size(2), "q heads must be contiguous");
   const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
@@ -299,6 +315,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_fused(
     const at::Tensor& qkv, const at::Tensor& start_pos, const std::optional<at::Tensor>& rope, at::Tensor& k_cache,
     at::Tensor& v_cache, const at::Tensor& seq_lens, int64_t Hq, double scale, int64_t max_len_hint, int64_t rot,
     bool quant_out) {
+  DEVICE_GUARD(qkv);
   need(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(qkv.dim() == 2, "qkv must be [B, (Hq + 2 Hkv) * D]");
   const int64_t B = qkv.size(0), D = k_cache.size(3), Hkv = k_cache.size(1);
@@ -358,6 +375,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_i8(
     const at::Tensor& qkv, const at::Tensor& start_pos, const std::optional<at::Tensor>& rope, at::Tensor& k_cache,
     at::Tensor& v_cache, at::Tensor& k_scale, at::Tensor& v_scale, const at::Tensor& seq_lens, int64_t Hq,
     double scale, int64_t max_len_hint, int64_t rot, bool quant_out) {
+  DEVICE_GUARD(qkv);
   need(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(qkv.dim() == 2, "qkv must be [B, (Hq + 2 Hkv) * D]");
   const int64_t B = qkv.size(0), D = k_cache.size(3), Hkv = k_cache.size(1);
@@ -408,6 +426,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_i8(
 // src: bf16 [B, Hkv, >= start + T, D] rows (rotated k or v); writes rows [start_pos[b], +T) quantised
 void kv_quant_append(const at::Tensor& src, const at::Tensor& start_pos, int64_t T, at::Tensor& cache,
                      at::Tensor& scales) {
+  DEVICE_GUARD(src);
   const int64_t D = cache.size(3), B = cache.size(0), Hkv = cache.size(1);
   check_cache(src, "src", D);
   check_cache8(cache, scales, "cache", D);
@@ -422,6 +441,7 @@ void kv_quant_append(const at::Tensor& src, const at::Tensor& start_pos, int64_t
 
 at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& start_pos, double scale, bool causal) {
+  DEVICE_GUARD(q);
   need(q, at::kBFloat16, "q");
   TORCH_CHECK(q.dim() == 4, "q must be [B, T, Hq, D]");
   const int64_t B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3);
@@ -439,13 +459,13 @@ at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at
 }
 
 // ---------------------------------------------------------------------------------- int8 gemm
-// Activation scales: per token (sa [M]) or per (token, 64-column group) (sa [KT, Mpad], M <= 128).
+// Activation scales: per token (sa [M]) or per (token, 64-column group) (sa [KT, Mpad], M <= 256).
 int64_t a_scale_mpad(const at::Tensor& sa, int64_t M, int64_t KT) {
   need(sa, at::kFloat, "a_scale");
   if (sa.dim() == 2) {
     TORCH_CHECK(sa.size(0) == KT && sa.size(1) >= (M + 15) / 16 * 16 && sa.size(1) % 16 == 0,
                 "grouped a_scale must be [K/64, Mpad]");
-    TORCH_CHECK(M <= 128, "grouped activation scales are a decode (M <= 128) feature");
+    TORCH_CHECK(M <= 256, "grouped activation scales are a decode (M <= 256) feature");
     return sa.size(1);
   }
   TORCH_CHECK(sa.numel() == M, "a_scale must have one entry per row");
@@ -463,6 +483,7 @@ void check_w8a8_operands(const at::Tensor& wp, const at::Tensor& sw, const std::
 
 at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                      const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  DEVICE_GUARD(a);
   need(a, at::kChar, "a");
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
   check_w8a8_operands(wp, sw, bias, N, K);
@@ -487,16 +508,19 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
   return out;
 }
 
-// Split-K W8A8 GEMV (decode, M <= 64, or <= 128 where rows128_ok(K, S)): fp32 partial slices
+// Split-K W8A8 GEMV (decode, M <= 64, <= 128 where rows128_ok(K, S), <= 256 where rows256_ok(K)): fp32 partial slices
 // [S, M, N] (w-scale and bias applied; bias in slice 0) for a consumer that sums them (rms_norm_parts).  S = 0 picks the split count.
 at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                             const std::optional<at::Tensor>& bias, int64_t N, int64_t K, int64_t S) {
+  DEVICE_GUARD(a);
   need(a, at::kChar, "a");
   TORCH_CHECK(a.size(-1) == K && K % 64 == 0, "split-K GEMV needs K % 64 == 0");
   check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = K / 64;
-  TORCH_CHECK(M <= 128, "split-K GEMV is a decode (M <= 128) kernel");
+  TORCH_CHECK(M <= 256, "split-K GEMV is a decode (M <= 256) kernel");
   const int64_t mpad = a_scale_mpad(sa, M, KT);
+  if (M > 128) S = edge_w8a8_rows256_splits((int)K);     // 129-256 rows: fixed per K (gemm_i8.hip rows256)
+  TORCH_CHECK(M <= 128 || S > 1, "no 129-256-row split-K kernel for this K");
   if (S <= 0 && M > 64) S = 4;                           // 65-128 rows: 4 slices (gemm_i8.hip rows128)
   if (S <= 0) {
     const int64_t ntw = M <= 16 ? 2 : 4;                 // tiles per workgroup (gemm_i8.hip launcher)
@@ -517,6 +541,7 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
 // [.., N/2]), 2 gelu-tanh, 3 gelu (erf).
 at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
                      int64_t epi) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(wp, at::kBFloat16, "weight (packed)");
   const int64_t K = x.size(-1), M = rows_of(x);
@@ -534,6 +559,7 @@ at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optio
 // Split-K bf16 decode GEMV: fp32 partial slices [S, M, N] (bias in slice 0) for rms_norm_parts.
 at::Tensor gemv_bf16_splitk(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias,
                             int64_t N, int64_t S) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(wp, at::kBFloat16, "weight (packed)");
   const int64_t K = x.size(-1), M = rows_of(x);
@@ -550,6 +576,7 @@ at::Tensor gemv_bf16_splitk(const at::Tensor& x, const at::Tensor& wp, const std
 // scales [M], outlier columns [cmax] (first `count`), outlier values [M, cmax], count [1]).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> llmint8_prep(const at::Tensor& x, double thr,
                                                                                     int64_t cmax) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 2, "x must be [M, K]");
   const int64_t M = x.size(0), K = x.size(1);
@@ -567,6 +594,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> llmint8_p
 // out bf16 [M, N] += xo[:, :count] . W^T[cols[:count]] * SCB / 127 (wt = int8 W^T [K, N]), in place.
 void llmint8_outlier(at::Tensor& out, const at::Tensor& xo, const at::Tensor& cols, const at::Tensor& count,
                      const at::Tensor& wt, const at::Tensor& scb) {
+  DEVICE_GUARD(out);
   need(out, at::kBFloat16, "out");
   need(xo, at::kFloat, "xo");
   need(cols, at::kInt, "cols");
@@ -582,6 +610,7 @@ void llmint8_outlier(at::Tensor& out, const at::Tensor& xo, const at::Tensor& co
 
 // Per-(token, 64 columns) int8 quantisation: (q [M, K], scales [K/64, Mpad]).
 std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
+  DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 64 == 0, "group_quant needs [M, K] with K % 64 == 0");
   const int64_t M = x.size(0), K = x.size(1), Mpad = (M + 15) / 16 * 16;
@@ -595,6 +624,7 @@ std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
 // gate_up projection (16-blocked rows) fused with silu(g) * u: returns bf16 h [M, N/2].
 at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                          const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  DEVICE_GUARD(a);
   need(a, at::kChar, "a");
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
   check_w8a8_operands(wp, sw, bias, N, K);
@@ -614,12 +644,13 @@ at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Te
 std::tuple<at::Tensor, at::Tensor> w8a8_gemm_gluq(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp,
                                                   const at::Tensor& sw, const std::optional<at::Tensor>& bias,
                                                   int64_t N, int64_t K) {
+  DEVICE_GUARD(a);
   need(a, at::kChar, "a");
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
   check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = (K + 63) / 64, Mpad = (M + 15) / 16 * 16;
-  TORCH_CHECK(M <= (K == 4096 ? 128 : 64) && N % 128 == 0,
-              "quantising GLU needs M <= 64 (128 at K = 4096) and N % 128 == 0");
+  TORCH_CHECK((M <= (K == 4096 ? 128 : 64) || (M <= 256 && edge_w8a8_rows256_ok((int)K))) && N % 128 == 0,
+              "quantising GLU needs M <= 64 (128 at K = 4096, 256 where rows256_ok(K)) and N % 128 == 0");
   TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GLU takes per-token activation scales");
   auto q = at::empty({M, N / 2}, a.options());
   auto s = at::empty({N / 128, Mpad}, a.options().dtype(at::kFloat));
@@ -634,6 +665,7 @@ std::tuple<at::Tensor, at::Tensor> w8a8_gemm_gluq(const at::Tensor& a, const at:
 // Returns an empty tensor when the configuration needs the host fallback.
 at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& seen, double temperature,
                   int64_t top_k, double top_p, double penalty, bool do_sample, const at::Tensor& rng) {
+  DEVICE_GUARD(logits);
   TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
   const bool bf = logits.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == at::kFloat);
@@ -661,6 +693,7 @@ std::vector<int64_t> sample_timestamps(bool enable) {
 // dst/src: [B, c, L, D] views of head-major caches (last two dims contiguous), any mix of pinned
 // host and device memory; async on the current stream.
 int64_t copy_head_block(at::Tensor& dst, const at::Tensor& src, int64_t mode) {
+  DEVICE_GUARD((dst.is_cuda() ? dst : src));
   TORCH_CHECK(dst.dim() == 4 && src.dim() == 4 && dst.sizes() == src.sizes(), "head blocks must match [B,c,L,D]");
   TORCH_CHECK(dst.scalar_type() == src.scalar_type());
   const int64_t D = dst.size(3), L = dst.size(2);
@@ -709,11 +742,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_timestamps", &sample_timestamps);
   m.def("rows128_ok", [](int64_t K, int64_t S) { return edge_w8a8_rows128_ok((int)K, (int)S) != 0; },
         "whether the 65-128 row decode GEMV has a kernel for K (in S split-K slices)");
+  m.def("rows256_ok", [](int64_t K) { return edge_w8a8_rows256_ok((int)K) != 0; },
+        "whether the 129-256 row decode GEMMs (row-split ring2) take this K");
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
     else if (what == "ring2_cfg") edge_w8a8_ring2_cfg((int)a, (int)b);
+    else if (what == "ring2_256") edge_w8a8_rows256_cfg((int)a, (int)b);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);
     else if (what == "weight_nt") edge_w8a8_weight_nt((int)a);

@@ -1122,25 +1122,46 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // EPI_PART: blockIdx = group * S + slice; slice ks reduces stages [NS ks / S, NS (ks + 1) / S).
 // WNT: weight DMA with the nontemporal cache policy (default); false = normal allocation, so the
 // other lane's read of the same layer can hit the memory-side cache (A/B knob "weight_nt")
-template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true>
-__global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
+// MS == 2 (129-256 rows, one 256-row decode micro-batch): the rows are cut into two halves of at
+// most 128 and each logical workgroup runs once per half.  Block b computes half (b >> 3) & 1 of
+// logical workgroup (b & 7) | (b >> 4) << 3, so the two halves of one weight panel are blocks b and
+// b + 8: under the observed round-robin dispatch they share an XCD, and the second reader of a
+// weight line finds it in that XCD's L2 (speed only: each half is a complete, independent
+// computation).  Launch 16 * ceil(G / 8) blocks for G logical workgroups; surplus blocks exit.
+// NAL > 0: NAL dedicated activation-loader waves issue every activation piece (DA stages ahead) and
+// the compute waves only read LDS and run MFMAs.  With NAL == 0 the compute waves issue their own
+// activation DMA, and at 128 rows x 6 tiles that DMA issue (the CU's texture path is busy with
+// 28 KiB per stage) serialised with their MFMAs: ~1400 cycles per stage against ~470 of DMA and ~400
+// of MFMA (tools/bench_ops.py --only rows256, qkv 22 us at M = 256).
+template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true, int MS = 1,
+          int NAL = 0>
+__global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
-    int M, int N, int K, int NTt, int Mpad, int S = 1) {
+    int M, int N, int K, int NTt, int Mpad, int S = 1, int G = 0) {
   constexpr int MB = 8, NCW = 4, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
   constexpr int LPW = WPW + (SC ? 1 : 0);             // loader pieces per stage (+ the scale piece)
   static_assert(WST % NWL == 0, "weight pieces split evenly over the loader waves");
   static_assert(DW * LPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTW == 8 && !SC), "epilogues");
+  static_assert(MS == 1 || MS == 2, "row split");
+  static_assert(NAL == 0 || (16 % NAL == 0 && DA * (16 / NAL) <= 63), "activation loaders");
   constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0);
   static_assert(LDS_KB * 1024 <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_KB * 1024];
   int8_t* const wring = lds;
   int8_t* const aring = lds + RW * WST * 1024;
   int8_t* const sring = aring + RA * 16 * 1024;       // SC only
+  int lbid = (int)blockIdx.x, row0 = 0;
+  if constexpr (MS == 2) {
+    row0 = (((int)blockIdx.x >> 3) & 1) * 128;
+    lbid = ((int)blockIdx.x & 7) | (((int)blockIdx.x >> 4) << 3);
+    if (lbid >= G) return;                            // whole workgroup: no barrier is left waiting
+  }
+  const int Ml = min(128, M - row0);                  // rows of this half (>= 1: MS == 2 only for M > 128)
   const int KT = K / 64, NSA = KT / 2;
-  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
-  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
+  const int grp = EPI == EPI_PART ? lbid / S : lbid;
+  const int ks = EPI == EPI_PART ? lbid % S : 0;
   const int sbeg = EPI == EPI_PART ? (int)((int64_t)NSA * ks / S) : 0;
   const int NS = EPI == EPI_PART ? (int)((int64_t)NSA * (ks + 1) / S) - sbeg : NSA;
   const int nt0 = grp * NTW;
@@ -1150,6 +1171,30 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
   const int rot = ROT ? (int)((grp * 5u) % (unsigned)NS) : 0;
   auto phys = [&](int st) { const int k = min(st, NS - 1) + rot; return sbeg + (k >= NS ? k - NS : k); };
 
+  const int8_t* const Ah = A + (size_t)row0 * K;
+  if constexpr (NAL > 0) {
+    if (wave >= NCW + NWL) {                          // ---- activation loader: line pieces al * APL ..
+      constexpr int APL = 16 / NAL;
+      const int al = wave - NCW - NWL;
+      uint32_t aoff[APL];
+#pragma unroll
+      for (int i = 0; i < APL; ++i)
+        aoff[i] = (uint32_t)min((al * APL + i) * 8 + (lane >> 3), Ml - 1) * (uint32_t)K + 16 * ((lane & 7) ^ (lane >> 3));
+      auto issue = [&](int st) {
+        const int8_t* ab = Ah + (size_t)phys(st) * 128;
+#pragma unroll
+        for (int i = 0; i < APL; ++i) glds16(ab + aoff[i], aring + ((st % RA) * 16 + al * APL + i) * 1024);
+      };
+      for (int st = 0; st < DA; ++st) issue(st);
+      for (int s = 0; s < NS; ++s) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * APL) : "memory");   // own pieces of stage s
+        __builtin_amdgcn_s_barrier();
+        issue(s + DA);                                  // into the slot of stage s - 1
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
+  }
   if (wave >= NCW) {                                  // ---- weight loader: pieces (k-tile c, tile t)
     const int lw = wave - NCW;
     uint32_t woff[WPW];
@@ -1159,7 +1204,7 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
       woff[i] = ((uint32_t)min(nt0 + t, NTt - 1) * (uint32_t)KT + c) * 1024u + lane * 16;
     }
     // scale piece: lanes 0-31 the rows of k-tile 2 p, lanes 32-63 of 2 p + 1 (4 rows per lane)
-    const uint32_t soff = (uint32_t)((lane >> 5) * Mpad + min(4 * (lane & 31), Mpad - 4));
+    const uint32_t soff = (uint32_t)((lane >> 5) * Mpad + row0 + min(4 * (lane & 31), Mpad - row0 - 4));
     const bool smine = (lane % NWL) == lw;
     auto issue = [&](int st) {
       const int p = phys(st);
@@ -1187,11 +1232,13 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
   uint32_t aoff[APW];
 #pragma unroll
   for (int i = 0; i < APW; ++i)
-    aoff[i] = (uint32_t)min((APW * wave + i) * 8 + (lane >> 3), M - 1) * (uint32_t)K + 16 * ((lane & 7) ^ (lane >> 3));
+    aoff[i] = (uint32_t)min((APW * wave + i) * 8 + (lane >> 3), Ml - 1) * (uint32_t)K + 16 * ((lane & 7) ^ (lane >> 3));
   auto issue = [&](int st) {
-    const int8_t* ab = A + (size_t)phys(st) * 128;
+    if constexpr (NAL == 0) {
+      const int8_t* ab = Ah + (size_t)phys(st) * 128;
 #pragma unroll
-    for (int i = 0; i < APW; ++i) glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
+      for (int i = 0; i < APW; ++i) glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
+    }
   };
   // epilogue operands first (the tail never waits on memory; retired by the first vmcnt wait)
   float sw_t[NTW], b_t[NTW], sa_r[2][4];
@@ -1205,7 +1252,7 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sa_r[j][q] = SC ? 1.f : sa[min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, M - 1)];
+    for (int q = 0; q < 4; ++q) sa_r[j][q] = SC ? 1.f : sa[row0 + min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, Ml - 1)];
   v4i acc[2][NTW];
   v4f accf[2][NTW];
 #pragma unroll
@@ -1263,7 +1310,7 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
   };
   // barrier k certifies stage k (both operands) and frees the slots of stage k - 1
   auto sync_stage = [&](int st) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * APW) : "memory");    // own pieces of stage st
+    if constexpr (NAL == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * APW) : "memory");    // own pieces of stage st
     __builtin_amdgcn_s_barrier();
     issue(st + DA);
   };
@@ -1294,8 +1341,9 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
-          if (row >= M) continue;
+          const int lrow = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+          if (lrow >= Ml) continue;
+          const int row = row0 + lrow;
           const float v = SC ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j][q];
           if constexpr (EPI == EPI_PART)
             reinterpret_cast<float*>(outv)[((size_t)ks * M + row) * N + col] = v * sw_t[t] + (ks == 0 ? b_t[t] : 0.f);
@@ -1310,7 +1358,8 @@ __global__ void __launch_bounds__((4 + NWL) * 64, 1) w8a8_gemv_ring2_kernel(
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+        const int lrow = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
+        const int row = row0 + lrow;
         float h[4], amax = 0.f;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
@@ -1480,10 +1529,89 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
   return -1;
 }
 
+// 129-256 rows (one 256-row decode micro-batch): ring2 with the rows cut in two halves that stream
+// the same weight panel on one XCD (MS = 2), so a decode step reads every weight from HBM once for
+// all 256 sequences instead of once per 128-row lane, and with dedicated activation-loader waves.
+// Tiles per workgroup are chosen for ~256 launched workgroups (the logical grid doubles).
+// cfg (EDGELLM_TUNE=ring2_256=c[,nt]): A/B geometries; nt = 0 (cfg 0 only) selects normal weight
+// allocation instead of nontemporal (1-4 % slower at M = 256).  -1: no kernel for this call.
+static int g_r256_cfg = 0, g_r256_nt = 1;
+template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV>
+int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
+                int M, int N, int K, int Mpad, hipStream_t st, int S) {
+  const int NTt = (N + 15) / 16, G = (NTt + NTWV - 1) / NTWV * S;
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV>),
+                     dim3((G + 7) / 8 * 16), dim3((4 + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
+                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G);
+  return (int)hipGetLastError();
+}
+
+template <int EP>
+int launch_rows256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                   float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
+  if (M <= 128 || M > 256 || K % 128 != 0 || (EP == EPI_PART) != (S > 1) || (scaled && EP != EPI_PART)) return -1;
+  const int NTt = (N + 15) / 16;
+  // (tiles, weight loaders, weight slots, activation slots, activation loaders); cfg 0 may flip the
+  // weight cache policy (nt knob), the A/B configs run nontemporal
+#define R256(NTWV, NWLV, RWV, RAV, NALV, SCV)                                                                    \
+  return g_r256_nt || g_r256_cfg ? launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, SCV, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S) \
+                                 : launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, SCV, false>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S)
+  // 8 waves (4 compute, 2 weight loaders, 2 activation loaders) keep 256 VGPRs per wave: the
+  // 10-wave form (4 weight loaders) spilled 236 B/lane at 8 tiles with grouped scales, and the
+  // spill traffic broke the loader waves' counted vmcnt (non-deterministic slices)
+  const int c = g_r256_cfg;
+  if constexpr (EP == EPI_PART) {
+    // split-K (o / down; grouped scales from the fused producers, or per token): >= 4 stages per slice
+    if (K / 128 < 4 * S || (scaled && (Mpad < M || Mpad % 16 != 0))) return -1;
+    const bool narrow = (NTt + 3) / 4 * S <= 160;     // o (N 4096, 2 slices): 128 logical at 4 tiles
+#define R256S(NTWV, NWLV, RWV, RAV, NALV) \
+  do { if (scaled) R256(NTWV, NWLV, RWV, RAV, NALV, true); R256(NTWV, NWLV, RWV, RAV, NALV, false); } while (0)
+    if (narrow) {
+      if (c == 1) R256S(4, 2, 8, 4, 1);
+      if (c == 2) R256S(4, 4, 8, 4, 0);
+      if (c == 3) R256S(4, 2, 6, 6, 2);
+      R256S(4, 2, 8, 4, 2);
+    }
+    if (c == 1) R256S(8, 2, 5, 4, 1);                 // down (N 4096, 4 slices): 128 logical at 8 tiles
+    if (c == 2) R256S(8, 4, 5, 4, 0);
+    if (c == 3) R256S(8, 2, 4, 5, 2);
+    R256S(8, 2, 5, 4, 2);
+#undef R256S
+  } else if constexpr (EP == EPI_GLUQ) {
+    if (N % 128 != 0 || scaled) return -1;
+    if (c == 1) R256(8, 2, 5, 4, 1, false);
+    if (c == 2) R256(8, 4, 5, 4, 0, false);
+    if (c == 3) R256(8, 2, 4, 5, 2, false);
+    R256(8, 2, 5, 4, 2, false);
+  } else {
+    if (scaled || S != 1) return -1;
+    // ~128 logical workgroups (256 launched): 3 tiles for N <= 6144, 6 for qkv-sized N
+    if (NTt <= 512) {
+      if (c == 2) R256(3, 3, 14, 4, 0, false);
+      R256(3, 2, 14, 4, 2, false);
+    }
+    if (NTt <= 1024) {
+      if (c == 1) R256(6, 2, 7, 4, 1, false);
+      if (c == 2) R256(6, 4, 7, 4, 0, false);
+      if (c == 3) R256(6, 2, 6, 5, 2, false);
+      R256(6, 2, 7, 4, 2, false);
+    }
+    R256(8, 2, 5, 4, 2, false);
+  }
+#undef R256
+  return -1;
+}
+
 // 65-128 rows (two decode micro-batches in one): LDS-staged activations, one tile per wave, 8 row
 // blocks of accumulators.  Instantiated for the k-tile counts of the 4096-hidden models (K = 4096
 // whole, and K = 4096 / 11008 / 14336 in 4 split-K slices); -1 = no kernel for this shape.
 }  // namespace
+
+extern "C" void edge_w8a8_rows256_cfg(int cfg, int nt) { g_r256_cfg = cfg; g_r256_nt = nt; }
+// split-K slices the 129-256-row kernels use for a K (0: none)
+extern "C" int edge_w8a8_rows256_splits(int K) { return K % 128 != 0 ? 0 : (K / 128 >= 64 ? 4 : 2); }
+// whether the 129-256-row decode kernels take this K (whole K; split-K at rows256_splits(K))
+extern "C" int edge_w8a8_rows256_ok(int K) { return K % 128 == 0 && K / 128 >= 8; }
 
 // k-tile counts launch_rows128 has kernels for: the whole K (S = 1) or each of S split-K slices
 extern "C" int edge_w8a8_rows128_ok(int K, int S) {
@@ -1551,9 +1679,13 @@ int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const vo
 extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                                      float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S,
                                      hipStream_t st) {
-  if (M <= 0 || M > 128 || K % 64 != 0 || K / 64 != KT || S < 1 || S > KT) return -2;
+  if (M <= 0 || M > 256 || K % 64 != 0 || K / 64 != KT || S < 1 || S > KT) return -2;
   const int mblocks = (M + 15) / 16;
   if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
+  if (M > 128) {
+    const int r = launch_rows256<EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, S);
+    return r == -1 ? -2 : r;
+  }
   if (M > 64) {
     const int r = launch_rows128<EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, S);
     return r == -1 ? -2 : r;
@@ -1589,6 +1721,14 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
   if (M > 64 && M <= 128 && epi == EPI_OUT && g_gemv_unroll != 1) {
     const int r = launch_rows128<EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, 1);
+    if (r != -1) return r;
+  }
+  if (M > 128 && M <= 256 && (epi == EPI_OUT || epi == EPI_GLUQ) && a_mode == A_TOKEN && g_gemv_ring) {
+    const int r = epi == EPI_OUT
+                      ? launch_rows256<EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, Mpad, false, st, 1)
+                      : (os == nullptr || Mpad < mblocks * 16
+                             ? -1
+                             : launch_rows256<EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, false, st, 1));
     if (r != -1) return r;
   }
   if (a_mode != A_TOKEN && M > 64) return -2;

@@ -134,11 +134,13 @@ class W8A8Linear(nn.Module):
     def group_scales_ok(self, M: int) -> bool:
         """Whether this projection consumes per-(token, 64) activation scales at M rows."""
         K = self.in_features
-        return ops.decode_rows_ok(M, K) or (bool(self.split_k_out) and ops.decode_rows_ok(M, K, 4))
+        return ops.group_scale_rows_ok(M) and \
+            (ops.decode_rows_ok(M, K) or (bool(self.split_k_out) and ops.decode_rows_ok(M, K, 4)))
 
     def glu_rows_ok(self, M: int) -> bool:
         """Whether the fused gate_up + SwiGLU kernel takes M rows (65-128: quantising form only)."""
-        return M <= 64 or (self.out_features % 128 == 0 and ops.decode_rows_ok(M, self.in_features))
+        return M <= 64 or (self.out_features % 128 == 0 and ops.decode_rows_ok(M, self.in_features)
+                           and ops.group_scale_rows_ok(M))
 
     def glu(self, x: QAct):
         """Fused gate_up -> silu(g) * u (blocked layout, M <= 64) for the down projection: int8

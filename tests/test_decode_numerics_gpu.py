@@ -4,7 +4,7 @@ split-K o / down, quantising GLU, 65-128-row kernels, bf16 GEMVs) against the fp
 
 Bounded on the relative error of the decode-step logits, at micro-batch
 sizes that select every decode kernel family: 1 (GEMV), 16 / 64 (grouped-scale GEMVs), 128 (the
-LDS-staged / ring kernels).
+LDS-staged / ring kernels), 200 / 256 (the row-split ring2 kernels of one 256-row micro-batch).
 """
 import pytest
 import torch
@@ -37,7 +37,7 @@ def _decode_logits(model, kv, tok, pos, dev):
     return model(tok.view(B, 1), ctx).float()
 
 
-@pytest.mark.parametrize("B", [1, 16, 64, 128])
+@pytest.mark.parametrize("B", [1, 16, 64, 128, 200, 256])
 @pytest.mark.parametrize("quant", ["none", "w8a8_smoothquant"])
 def test_decode_step_logits_match_fp32_reference(cuda, B, quant, monkeypatch):
     model = _model(cuda, quant)

@@ -102,7 +102,10 @@ def test_decode_rows_capability_table():
         pytest.skip("extension not built")
     assert all(ops.decode_rows_ok(M, K) for M in (1, 17, 64) for K in (64, 1000, 11008))
     assert ops.decode_rows_ok(128, 4096) and ops.decode_rows_ok(65, 4096)
-    assert not ops.decode_rows_ok(129, 4096) and not ops.decode_rows_ok(100, 11008)
+    assert not ops.decode_rows_ok(100, 11008)
+    # 129-256 rows: the row-split ring2 kernels, any K % 128 == 0 with >= 8 stages
+    assert ops.decode_rows_ok(129, 4096) and ops.decode_rows_ok(256, 11008, 4) and ops.decode_rows_ok(256, 1024)
+    assert not ops.decode_rows_ok(257, 4096) and not ops.decode_rows_ok(200, 1000) and not ops.decode_rows_ok(200, 896)
     for K in (4096, 11008, 14336):                      # o / down of Llama-2-7B, down of Llama-3-8B
         assert ops.decode_rows_ok(128, K, 4)
     assert not ops.decode_rows_ok(128, 2048, 4)

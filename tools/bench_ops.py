@@ -379,6 +379,55 @@ def ring_rows(C, dev, Ms=(128, 96)):
     return out
 
 
+def rows256_rows(C, dev, M=256):
+    """One 256-row decode micro-batch (row-split ring2, weights read once) against two 128-row
+    launches (the 2-lane form, weights read twice), cache-cold, every launcher geometry
+    (tune ring2_256 = cfg, nt) timed interleaved: qkv, o / down (grouped scales, split-K) and the
+    quantising gate_up."""
+    out = []
+    shapes = {"qkv": (12288, 4096, "out"), "o": (4096, 4096, "part"), "gate_up": (22016, 4096, "gluq"),
+              "down": (4096, 11008, "part"), "o_token": (4096, 4096, "part_tok"),
+              "down_token": (4096, 11008, "part_tok"), "gate_up_bf16out": (22016, 4096, "out")}
+    for name, (N, K, kind) in shapes.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+        sw = torch.rand(N, device=dev) * 0.01
+        ctr = [0]
+
+        def make(rows):
+            qx = torch.randint(-127, 128, (rows, K), dtype=torch.int8, device=dev)
+            sx = (torch.rand(K // 64, (rows + 15) // 16 * 16, device=dev) if kind == "part"
+                  else torch.rand(rows, device=dev)) * 0.01
+
+            def call():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                if kind == "gluq":
+                    return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
+                if kind in ("part", "part_tok"):
+                    return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, 0)
+                return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
+            return call
+
+        c256, c128 = make(M), make(M // 2)
+        forms = [(0, 1), (0, 0), (1, 1), (2, 1), (3, 1)]
+        res = {}
+        for rnd in range(3):
+            for cfg, nt in forms:
+                C.tune("ring2_256", cfg, nt)
+                res.setdefault(f"r256_c{cfg}_nt{nt}", []).append(timeit(c256, iters=10, per_graph=ncopy))
+            C.tune("ring2_256", 0, 1)
+            res.setdefault("two_x128", []).append(2 * timeit(c128, iters=10, per_graph=ncopy))
+        row = dict(op="w8a8_rows256", shape=name, M=M, N=N, K=K, weight_MB=round(N * K / 1e6, 1))
+        for form, ts in res.items():
+            row[f"{form}_us"] = round(min(ts), 2)
+            row[f"{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
+        out.append(row)
+        print(row, flush=True)
+        del wps
+    return out
+
+
 def bf16_rows(C, dev, Ms=(8, 16, 32, 48, 64)):
     """bf16 decode projections at 1-64 rows (Llama-2-7B shapes), cache-cold: gemv_bf16.hip
     (1-4 row blocks of 16 per weight read) vs hipBLASLt through torch.nn.functional.linear."""
@@ -474,6 +523,8 @@ def main():
         rows += batch1_rows(C, dev)
     if only is not None and "ring" in only:
         rows += ring_rows(C, dev)
+    if only is not None and "rows256" in only:
+        rows += rows256_rows(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
     if a.out:
