@@ -28,7 +28,8 @@ from ..models.registry import load_model
 from ..orchestrator import Agent, Orchestrator, RefineMerge, VoteMerge
 from ..parallel.split import agent_devices, split_model
 from ..utils.log import format_efficiency_report, format_final_report, get_logger
-from .common import add_runtime_args, build_generator, pick_devices, pop_runtime, resolve_runtime
+from .common import (add_runtime_args, build_generator, build_pp_engine, pick_devices, pop_runtime, pp_launch,
+                     resolve_runtime)
 
 logger = get_logger("combine")
 
@@ -49,10 +50,16 @@ def build_embedder(name: Optional[str], base_dir: Optional[str], device) -> Embe
 
 
 def make_agent(name: str, model_id: str, precision: str, quant: str, device, sampling: SamplingParams, rt: dict,
-               cpu_prompt: bool = False, gpus=None) -> Agent:
+               cpu_prompt: bool = False, gpus=None, launch=None, tag: int = 0) -> Agent:
     """One agent: the model on ``device``, or split layer-wise over its GPU group (``gpus``, the
     YAML ``agents[].gpus``; else ``pp_size`` devices from ``device``) — the reference's
-    ``device_map="auto"`` placement (combine_model_fp_updated.py:40)."""
+    ``device_map="auto"`` placement (combine_model_fp_updated.py:40).  Under torchrun
+    (``launch``) this rank's pipeline stage behind a PipelineGenerator (parallel/pp_engine.py)."""
+    if launch is not None:
+        eng, tok, source, bounds = build_pp_engine(model_id, precision, quant, rt, launch, tag,
+                                                   max_batch=int(rt.get("batch_size") or 1))
+        logger.info(f"{name}: {source} pipelined over {launch[1]} ranks at layers {bounds} ({quant})")
+        return Agent(name, eng, tok, sampling, cpu_prompt)
     devs = agent_devices(gpus, torch.device(device), int(rt.get("pp_size") or 1))
     model, tok, source = load_model(model_id, precision, quant, devs[0], rt.get("base_model_path"))
     if len(devs) > 1:
@@ -68,7 +75,8 @@ def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: 
     """qa_specs: (name, model, precision[, quant[, gpus]]) per QA agent."""
     rt = resolve_runtime(cfg, rt)
     quant = rt.get("quant") or cfg.quant.mode
-    devices = pick_devices(rt.get("devices"))
+    launch = pp_launch(rt)                        # torchrun: every model pipelined over the ranks
+    devices = [launch[2]] if launch is not None else pick_devices(rt.get("devices"))
     s = cfg.sampling
     sampling = SamplingParams(s.max_new_tokens, s.temperature, s.top_k, s.top_p, s.repetition_penalty, s.do_sample)
     logger.info("Loading dataset...")
@@ -79,12 +87,28 @@ def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: 
         n, mid, prec = spec[:3]
         aq = spec[3] if len(spec) > 3 and spec[3] not in (None, "none") else quant
         gpus = spec[4] if len(spec) > 4 else None
-        agents.append(make_agent(n, mid, prec, aq, devices[i % len(devices)], sampling, rt, cpu_variant, gpus))
+        agents.append(make_agent(n, mid, prec, aq, devices[i % len(devices)], sampling, rt, cpu_variant, gpus,
+                                 launch=launch, tag=i))
     merge_kind = rt.get("merge") or cfg.merge
     refiner = None
     if merge_kind == "refine" or refiner_spec is not None:
         rn, rid, rprec = refiner_spec
-        refiner = make_agent(rn, rid, rprec, quant, devices[len(agents) % len(devices)], sampling, rt)
+        refiner = make_agent(rn, rid, rprec, quant, devices[len(agents) % len(devices)], sampling, rt,
+                             launch=launch, tag=len(agents))
+    if launch is not None:
+        from ..parallel.pp_engine import serve_workers, stop_workers
+        if launch[0] != 0:                        # workers: serve the driver's commands until STOP
+            serve_workers({a.generator.tag: a.generator for a in agents + ([refiner] if refiner else [])})
+            return {}
+        # no STOP on an exception: the driver's exit makes torchrun tear the workers down (a STOP
+        # broadcast could meet a worker blocked inside a pipeline exchange)
+        out = _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_variant)
+        stop_workers(agents[0].generator)
+        return out
+    return _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_variant)
+
+
+def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_variant) -> dict:
     legacy = not rt.get("no_legacy_decode", False)
     if merge_kind == "vote":
         merge = VoteMerge()
@@ -128,7 +152,8 @@ def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: 
             progress.append(i, m)
             if rt.get("metrics_jsonl"):
                 with open(rt["metrics_jsonl"], "a") as f:
-                    f.write(json.dumps({"index": i, **m, "agent_tps": res.tps, "wall_s": res.wall_s}) + "\n")
+                    f.write(json.dumps({"index": i, **m, "agent_tps": res.tps, "wall_s": res.wall_s,
+                                        "answers": res.answers, "final": res.final}) + "\n")
             if cpu_variant:
                 logger.info(f"[Q{i + 1}] Total time: {res.wall_s:.2f} sec\n")
         # QA agents' generated tokens of this batch (each result holds every row of the batch)

@@ -87,3 +87,41 @@ def build_generator(model, rt: dict, max_batch: int = 1):
         kvd = "bf16"
     return Generator(model, max_batch=max_batch, max_seq=max_seq, kv_dtype=kvd,
                      prefill_chunk=rt.get("prefill_chunk") if h_on is not None else None)
+
+
+def pp_launch(rt: dict):
+    """Under ``torchrun`` (WORLD_SIZE > 1) every model runs as a pipeline over the ranks, one
+    process per GPU (parallel/pp_engine.py): returns (rank, world, device) after initialising the
+    process group (RCCL with a GPU per rank, gloo on CPU); None for a single-process run.
+    ``pp_size`` must then equal the world size (or be left unset)."""
+    from ..parallel.pp_engine import distributed_world
+    world = distributed_world()
+    if world <= 1:
+        return None
+    import os
+    from ..parallel.pipeline import init_distributed
+    pp = int(rt.get("pp_size") or 1)
+    assert pp in (1, world), f"--pp_size {pp} under a {world}-rank torchrun launch"
+    want_cpu = (rt.get("devices") or "").startswith("cpu") or not torch.cuda.is_available()
+    rank, world = init_distributed("gloo" if want_cpu else "nccl")
+    import atexit
+    import torch.distributed as dist
+    # tear the process group down before interpreter exit (a live group's threads abort the
+    # process at exit, which torchrun reports as a failed rank)
+    atexit.register(lambda: dist.is_initialized() and dist.destroy_process_group())
+    dev = torch.device("cpu") if want_cpu else torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    return rank, world, dev
+
+
+def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch, tag: int, max_batch: int = 1):
+    """This rank's stage of ``model_id`` behind a ``PipelineGenerator`` (the Generator interface
+    on the driver, rank 0).  Returns (engine, tokenizer, source, bounds)."""
+    from ..parallel.pp_engine import PipelineGenerator, load_stage
+    rank, world, dev = launch
+    stage, tok, source, bounds = load_stage(model_id, precision, quant, dev, rt.get("base_model_path"), rank, world)
+    kvd = rt.get("kv_dtype") or "bf16"
+    if kvd == "int8" and stage.cfg.head_dim not in (64, 128, 256):
+        kvd = "bf16"
+    eng = PipelineGenerator(stage, rank, world, max_batch=max_batch, max_seq=rt.get("max_seq", 2048), tag=tag,
+                            kv_dtype=kvd)
+    return eng, tok, source, bounds

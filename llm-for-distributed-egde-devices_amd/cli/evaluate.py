@@ -25,7 +25,8 @@ from ..orchestrator.prompts import qa_prompt
 from ..parallel.split import agent_devices, split_model
 from ..utils.log import format_efficiency_report, format_single_model_report, get_logger
 from .combine import build_embedder
-from .common import add_runtime_args, build_generator, pick_devices, pop_runtime, resolve_runtime
+from .common import (add_runtime_args, build_generator, build_pp_engine, pick_devices, pop_runtime, pp_launch,
+                     resolve_runtime)
 
 logger = get_logger("evaluate")
 
@@ -37,18 +38,37 @@ def evaluate_model(model_id: str, rows, cfg, rt) -> dict:
     wall time)."""
     logger.info(f"\n--- Evaluating Model: {model_id} ---")
     rt = resolve_runtime(cfg, rt)
-    dev = pick_devices(rt.get("devices"))[0]
-    devs = agent_devices(None, dev, int(rt.get("pp_size") or 1))
     quant = rt.get("quant") or cfg.quant.mode
     precision = rt.get("precision") or "bf16"
+    bs = max(1, int(rt.get("batch_size") or 1))
+    launch = pp_launch(rt)
+    if launch is not None:
+        # torchrun: one pipeline stage per rank; rank 0 drives the loop, the others serve it
+        from ..parallel.pp_engine import serve_workers, stop_workers
+        gen, tok, source, bounds = build_pp_engine(model_id, precision, quant, rt, launch, tag=0, max_batch=bs)
+        if launch[0] != 0:
+            serve_workers({0: gen})
+            return {}
+        logger.info(f"{model_id}: {source} pipelined over {launch[1]} ranks at layers {bounds} ({quant})")
+        dev = launch[2]
+        devs = [dev]
+        model = gen.model                    # confidence scored through the pipeline
+        out = _evaluate_loop(model_id, rows, cfg, rt, gen, model, tok, dev, devs, bs)
+        stop_workers(gen)                    # (not on an exception: torchrun tears the workers down)
+        return out
+    dev = pick_devices(rt.get("devices"))[0]
+    devs = agent_devices(None, dev, int(rt.get("pp_size") or 1))
     model, tok, source = load_model(model_id, precision, quant, devs[0], rt.get("base_model_path"))
     if len(devs) > 1:
         model = split_model(model, devs)
         logger.info(f"{model_id}: {source} split over {[str(d) for d in devs]} at layers {model.bounds} ({quant})")
     else:
         logger.info(f"{model_id}: {source} ({quant})")
-    bs = max(1, int(rt.get("batch_size") or 1))
     gen = build_generator(model, rt, max_batch=bs)
+    return _evaluate_loop(model_id, rows, cfg, rt, gen, model, tok, dev, devs, bs)
+
+
+def _evaluate_loop(model_id, rows, cfg, rt, gen, model, tok, dev, devs, bs) -> dict:
     s = cfg.sampling
     sp = SamplingParams(s.max_new_tokens, s.temperature, s.top_k, s.top_p, s.repetition_penalty, s.do_sample)
     suite = MetricSuite(build_embedder(cfg.embedder_model, rt.get("base_model_path"), dev))

@@ -125,19 +125,25 @@ class Generator:
 
     # ------------------------------------------------------------------ forward pieces
     @torch.no_grad()
-    def prefill(self, ids: torch.Tensor, row0: int = 0, start: int = 0) -> torch.Tensor:
-        """ids [B, T] (equal lengths) into cache rows [row0, row0+B) at positions start.. ;
-        returns last-position logits [B, V]."""
+    def prefill(self, ids: torch.Tensor, row0: int = 0, start: int = 0,
+                lens: Optional[Sequence[int]] = None) -> torch.Tensor:
+        """ids [B, T] into cache rows [row0, row0+B) at positions start.. ; returns the logits of
+        each row's last real token [B, V].  ``lens``: ragged prompts right-padded to T (one pass
+        for the whole batch; AttnCtx.last_pos)."""
         B, T = ids.shape
         assert start + T <= self.max_seq, "prompt exceeds the KV cache"
         if self.prefill_chunk and T > self.prefill_chunk:     # chunked prefill (HeadInfer)
+            assert lens is None or len(set(lens)) == 1, "chunked prefill takes equal-length prompts"
             out = None
             for c0 in range(0, T, self.prefill_chunk):
                 out = self.prefill(ids[:, c0:c0 + self.prefill_chunk], row0, start + c0)
             return out
         sp = torch.full((B,), start, dtype=torch.int32, device=self.device)
+        last = None
+        if lens is not None and len(set(lens)) > 1:
+            last = torch.tensor([n - 1 for n in lens], dtype=torch.long, device=self.device)
         ctx = AttnCtx("prefill", B, T, sp, sp + T, start + T, self.kv.rows(row0, row0 + B), self.rope,
-                      attn_hook=self.attn_hook)
+                      attn_hook=self.attn_hook, last_pos=last)
         with trace_range(f"prefill.B{B}.T{T}"):
             out = self.model(ids, ctx)
         debug_sync("prefill")
@@ -197,9 +203,14 @@ class Generator:
         if cuda:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        # equal lengths: one batched pass; otherwise one pass per sequence (own cache row)
+        # one batched pass; ragged prompts are right-padded to the longest (AttnCtx.last_pos), except
+        # under HeadInfer's chunked prefill, which takes one pass per sequence (own cache row)
         if len(set(plens)) == 1:
             logits = self.prefill(torch.tensor(prompts, dtype=torch.long, device=self.device), 0, 0)
+        elif not self.prefill_chunk:
+            T = max(plens)
+            pad = [list(p) + [0] * (T - len(p)) for p in prompts]
+            logits = self.prefill(torch.tensor(pad, dtype=torch.long, device=self.device), 0, 0, lens=plens)
         else:
             logits = torch.cat([self.prefill(torch.tensor([p], dtype=torch.long, device=self.device), b, 0)
                                 for b, p in enumerate(prompts)], 0)

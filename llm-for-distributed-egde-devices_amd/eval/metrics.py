@@ -29,9 +29,12 @@ METRIC_KEYS = ("rouge1", "rouge2", "rougeL", "bertscore", "bleu", "cosine", "con
 
 @torch.no_grad()
 def confidence_score(model: DecoderLM, ids: List[int]) -> float:
-    """mean_t max_v softmax(logits[t])  over the text's own tokens (one prefill pass)."""
+    """mean_t max_v softmax(logits[t])  over the text's own tokens (one prefill pass).  A
+    pipeline-parallel scorer (parallel/pp_engine.py) runs that pass through its stages."""
     if not ids:
         return 0.0
+    if hasattr(model, "confidence"):
+        return float(model.confidence(ids))
     dev = model.device
     T = len(ids)
     kv = KVCache(model.cfg, 1, T, dtype=model.dtype, device=dev)

@@ -57,6 +57,15 @@ class AttnCtx:
     rope: Optional[torch.Tensor] = None
     causal: bool = True
     attn_hook: Optional[object] = None   # HeadInfer offload manager (edgellm.offload)
+    # ragged prefill: int64 [B] index (within the T new tokens) of each row's last real token; rows
+    # are right-padded to T, so a real token never attends to a pad (causal) and the pads' cache
+    # entries lie past the row's length, where decode overwrites them before any read
+    last_pos: Optional[torch.Tensor] = None
+
+    def last_rows(self, device) -> torch.Tensor:
+        """Flat row indices [B] of each sequence's last real token in a [B*T, H] activation."""
+        last = self.last_pos.to(device) if self.last_pos is not None else self.T - 1
+        return torch.arange(self.B, device=device) * self.T + last
 
 
 class Attention(nn.Module):
@@ -269,7 +278,7 @@ class DecoderLM(nn.Module):
         if isinstance(x, PartialSum) and logits == "last" and ctx.T > 1:
             x = x.materialize()
         if logits == "last" and ctx.T > 1:
-            idx = torch.arange(ctx.B, device=x.device) * ctx.T + (ctx.T - 1)
+            idx = ctx.last_rows(x.device)
             x = x.index_select(0, idx)
             residual = residual.index_select(0, idx) if residual is not None else None
         h, _ = self.final_norm(x, residual)

@@ -104,6 +104,7 @@ class PipelineStage:
         self.streams = ([torch.cuda.Stream(self.device) for _ in range(lanes)]
                         if cuda and lanes > 1 else None)
         self.p2p_bytes = 0
+        self._plen, self._eos = None, None            # per-run: ragged prompt lengths, EOS id (last rank)
         if warm_comm and dist.is_initialized() and world > 1:
             self.warm_communicator()
 
@@ -164,16 +165,19 @@ class PipelineStage:
 
     def _prefill(self, m: int, ids: Optional[torch.Tensor], T: int, hidden: Optional[torch.Tensor]):
         """Prefill micro-batch m (prompt length T); chunked by ``prefill_chunk`` when the KV is
-        offloaded (HeadInfer bounds activation memory by the chunk, as in the paper)."""
+        offloaded (HeadInfer bounds activation memory by the chunk, as in the paper).  Ragged
+        prompts (``self._plen[m]``, right-padded to T) take one pass with per-row last positions."""
         b, H = self.b, self.cfg.hidden_size
+        plen = self._plen[m] if self._plen is not None else None
         C = getattr(self.kv, "chunk_size", T) if self.attn_hook is not None else T
+        assert plen is None or C >= T, "HeadInfer's chunked prefill takes equal-length prompts"
         outs = []
         out = None
         for c0 in range(0, T, C):
             c1 = min(T, c0 + C)
             sp = torch.full((b,), c0, dtype=torch.int32, device=self.device)
             ctx = AttnCtx("prefill", b, c1 - c0, sp, sp + (c1 - c0), c1, self._rows(m), self.rope,
-                          attn_hook=self.attn_hook)
+                          attn_hook=self.attn_hook, last_pos=(plen - 1) if plen is not None else None)
             x_ids = ids[:, c0:c1] if ids is not None else None
             x_h = None
             if hidden is not None:
@@ -183,8 +187,12 @@ class PipelineStage:
                 outs.append(out.view(b, c1 - c0, H))
         if outs:
             out = torch.cat(outs, 1).reshape(b * T, H)
-        self.pos[m].fill_(T)
-        self.lens[m].fill_(T + 1)
+        if plen is not None:
+            self.pos[m].copy_(plen)
+            self.lens[m].copy_(plen + 1)
+        else:
+            self.pos[m].fill_(T)
+            self.lens[m].fill_(T + 1)
         return out
 
     def _decode_body(self, m: int, max_len: int):
@@ -208,6 +216,8 @@ class PipelineStage:
         self.out[m].scatter_(1, self.step[m].view(1, 1).expand(self.b, 1), nxt.view(self.b, 1))
         self.rng[m][1:].add_(1)
         self.step[m].add_(1)
+        if self._eos is not None:                     # device-side EOS flags (graph-capturable)
+            self.hit[m].logical_or_(nxt.eq(self._eos))
 
     def _bucket(self, max_len: int) -> int:
         return min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
@@ -251,18 +261,34 @@ class PipelineStage:
     def run(self, prompts: Optional[Sequence[torch.Tensor]], prompt_len: int, sampling: SamplingParams,
             decode_steps: int, seed: int = 0, hook: Optional[Callable[[int], None]] = None,
             watchdog=None, fault: Optional[Callable[[int], None]] = None,
-            stats_window: Optional[Tuple[int, int]] = None) -> PipelineResult:
+            stats_window: Optional[Tuple[int, int]] = None, prompt_lens: Optional[torch.Tensor] = None,
+            eos_token_id: Optional[int] = None, eos_every: int = 8) -> PipelineResult:
         """prompts: M tensors [b, T] of token ids (needed on rank 0 only; T = prompt_len).
         decode_steps = tokens generated per sequence after the first (prefill-sampled) one.
         ``watchdog`` (parallel.watchdog.Watchdog) gets a heartbeat per tick; ``fault(tick)`` is a
         test hook that may delay or raise before a tick's exchange (fault injection).
         ``stats_window=(t_a, t_b)``: ticks over which this rank's compute / P2P-wait / bubble
-        statistics are taken (``PipelineResult.stats``)."""
+        statistics are taken (``PipelineResult.stats``).
+        ``prompt_lens`` [M, b] (every rank): ragged prompts right-padded to T; the last rank then
+        needs ``prompts`` too (repetition-penalty history without the pads).
+        ``eos_token_id``: every ``eos_every`` decode rounds all ranks agree (one all-reduce) whether
+        every sequence has produced EOS, and stop together at that tick."""
         M, P, b, T = self.M, self.world, self.b, prompt_len
         S = decode_steps
         assert T + S + 1 <= self.max_seq
         V = self.cfg.vocab_size
         self.sampling = sampling
+        dev = self.device
+        self._plen = None
+        if prompt_lens is not None:
+            pl = prompt_lens.to(dev, torch.int32).view(M, b)
+            assert int(pl.max()) <= T and int(pl.min()) >= 1
+            if int(pl.min()) < T:
+                self._plen = [pl[m].clone() for m in range(M)]
+        self._eos = (torch.tensor(int(eos_token_id), dtype=torch.long, device=dev)
+                     if eos_token_id is not None and self.is_last else None)
+        if self.is_last:
+            self.hit = [torch.zeros(b, dtype=torch.bool, device=dev) for _ in range(M)]
         if self.h_on is not None:
             self._build_offload_kv(T)
         self.graphs_ok = self.use_graphs and not needs_host_sampler(sampling, V) and \
@@ -272,7 +298,6 @@ class PipelineStage:
         self._graphs.clear()
         self._pools.clear()
         self._final_bucket = self._bucket(T + S + 1)
-        dev = self.device
         if self.is_last:
             self.seen = [torch.zeros(b, V, dtype=torch.uint8, device=dev) for _ in range(M)]
             self.rng = [torch.tensor([(seed + 7919 * m) & 0x7FFFFFFF, 0], dtype=torch.int32, device=dev)
@@ -282,16 +307,20 @@ class PipelineStage:
         # repetition-penalty history needs the prompt ids on the last stage
         pdev = "cpu" if self.host_staged else dev
         if self.is_last:
-            if self.is_first:
+            if self.is_first or (prompts is not None and prompt_lens is not None):
                 for m in range(M):
-                    self.seen[m].scatter_(1, prompts[m].to(dev), 1)
+                    ids = prompts[m].to(dev)
+                    if self._plen is not None:          # pads repeat the row's first token
+                        pos = torch.arange(T, device=dev)[None, :]
+                        ids = torch.where(pos < self._plen[m][:, None], ids, ids[:, :1])
+                    self.seen[m].scatter_(1, ids, 1)
             else:
                 pids = torch.zeros(M, b, T, dtype=torch.long, device=pdev)
                 self._recv_one(pids, 0)
                 pids = pids.to(dev)
                 for m in range(M):
                     self.seen[m].scatter_(1, pids[m], 1)
-        elif self.is_first and P > 1:
+        elif self.is_first and P > 1 and prompt_lens is None:
             self._send_one(torch.stack([p.to(pdev) for p in prompts]), P - 1)
 
         H = self.cfg.hidden_size
@@ -330,6 +359,11 @@ class PipelineStage:
 
         t_start = time.perf_counter()
         n_ticks = n_groups + P - 1
+        # EOS agreement: from the tick after which the last stage has sampled every micro-batch's
+        # first token, once per eos_every decode rounds (M / L ticks per round)
+        eos_on = eos_token_id is not None and (P == 1 or dist.is_initialized())
+        eos_from, eos_period = (M // L) + P - 1, max(1, eos_every) * max(1, M // L)
+        stopped_at = None
         t_first = P - 1 if self.is_last else -1     # tick whose prefill samples the first token
         ev_first: Dict[int, object] = {}
         mark(ev_first, -1)
@@ -404,6 +438,10 @@ class PipelineStage:
                 for prv in range(prv_g * L, prv_g * L + L):
                     if prv < M:
                         pre_out[prv] = None                # sent this tick
+            if eos_on and t >= eos_from and (t - eos_from) % eos_period == 0 and t < n_ticks - 1:
+                if self._all_hit():
+                    stopped_at = t
+                    break
         if self.streams:
             for st in self.streams:
                 cur_stream.wait_stream(st)
@@ -423,7 +461,26 @@ class PipelineStage:
             toks = []
             for m in range(M):
                 toks.extend(self.out[m].tolist())
-        return PipelineResult(toks, n_ticks, elapsed, stats=stats)
+        if stopped_at is not None:
+            stats["eos_stop_tick"] = stopped_at
+        return PipelineResult(toks, n_ticks if stopped_at is None else stopped_at + 1, elapsed, stats=stats)
+
+    def _all_hit(self) -> bool:
+        """Every rank joins: True when the last stage has seen EOS in every row (one all-reduce
+        of a device flag; the host waits for it, once per check period)."""
+        if self.is_last:
+            if self.streams:
+                cur = torch.cuda.current_stream(self.device)
+                for st in self.streams:
+                    cur.wait_stream(st)
+            flag = torch.stack([h.all() for h in self.hit]).all().to(torch.int32).view(1)
+        else:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if self.world > 1:
+            f = flag if self.nccl else flag.cpu()
+            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            flag = f
+        return bool(flag.item())
 
     def _window_stats(self, ev_in, ev_done, t_a, t_b, nbytes) -> Dict[str, float]:
         """Per-tick compute (inputs ready -> all lanes done) and P2P wait (lanes done -> next

@@ -1,0 +1,259 @@
+"""Pipeline-parallel serving engine: the micro-batched RCCL ``PipelineStage`` behind the
+``Generator`` interface, so the CLIs (evaluate / combine / serve) run a model split over
+``pp_size`` GPUs as one process per GPU instead of the eager in-process ``SplitLM``.
+
+The reference's only multi-device mechanism is accelerate's ``device_map="auto"`` layer split,
+which hops the hidden state GPU to GPU with no micro-batching
+(Code/Base Models/combine_model_fp_updated.py:40, Llama_bf16_updated.py:31).  Here, under
+``torchrun --nproc-per-node P``:
+
+* every rank holds stage ``rank`` of every agent's model (``load_stage``: bit-identical weights
+  to the unsplit model for a layer, SmoothQuant calibrated on the full model once);
+* rank 0 is the DRIVER: it runs the evaluation loop, and each ``generate`` / ``confidence``
+  call broadcasts one command (a small int64 header + float sampling parameters + the padded
+  prompt ids and lengths) to all ranks;
+* every other rank is a WORKER in ``serve_workers``: it executes the same commands on its stage
+  until the driver sends STOP;
+* a command runs ``PipelineStage.run`` on every rank (ragged prompts right-padded, one prefill
+  pass per micro-batch, EOS agreement every few decode rounds) and the last stage returns the
+  tokens (and timings) to the driver with one P2P message.
+
+Prompts are spread over the stage's M micro-batches of b rows; unused rows repeat prompt 0 and
+are discarded.  Works on gloo (CPU, tests) and on RCCL (one GPU per rank).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..engine.generate import GenerationResult, SamplingParams
+from ..models.decoder import AttnCtx, DecoderLM
+from .pipeline import PipelineStage
+
+CMD_GENERATE, CMD_SCORE, CMD_STOP = 1, 2, 3
+_HDR = 12
+
+
+def distributed_world() -> int:
+    """WORLD_SIZE of a torchrun launch (1 when not launched by torchrun)."""
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def load_stage(model_id: str, precision: str, quant: str, device, base_dir: Optional[str], rank: int, world: int,
+               bounds: Optional[Sequence[int]] = None):
+    """This rank's pipeline stage of ``model_id``: layers [bounds[rank], bounds[rank+1]) (balanced
+    partition by default), the embedding on rank 0, the head on the last rank.  Weights equal the
+    unsplit model's (random-init weights are seeded by global parameter name; SmoothQuant calibrates
+    and smooths the FULL model, then cuts the stage).  Returns (stage, tokenizer, source, bounds)."""
+    from ..models.registry import load_model
+    from .partition import partition_model
+    full_needed = quant == "w8a8_smoothquant"
+    if full_needed:
+        full, tok, source = load_model(model_id, precision, "none", device, base_dir)
+        cfg = full.cfg
+    else:
+        full = None
+        cfg, tok, source = _cfg_of(model_id, precision, device, base_dir)
+    if bounds is None:
+        wb = 1.0 if quant not in (None, "none") else 2.0
+        bounds = partition_model(cfg, world, "balanced", weight_bytes=wb)
+    first, last = int(bounds[rank]), int(bounds[rank + 1])
+    if full_needed:
+        from ..quant.smoothquant import smoothquant_stage
+        text = ("Question: when did the first world war begin and which countries fought in it? Answer: "
+                "The First World War began in 1914 after the assassination of Archduke Franz Ferdinand.")
+        ids = tok.encode(text)[:64]
+        calib = torch.tensor([[i % full.cfg.vocab_size for i in ids]], device=full.device)
+        stage = smoothquant_stage(full, first, last, calib, device=device)
+        del full
+    else:
+        stage, tok, source = load_model(model_id, precision, quant, device, base_dir, first=first, last=last)
+    return stage, tok, source, list(bounds)
+
+
+def _cfg_of(model_id, precision, device, base_dir):
+    """Config + tokenizer of a model without materialising its layers (an embedding-only stage)."""
+    from ..models.registry import load_model
+    m, tok, source = load_model(model_id, precision, "none", device, base_dir, first=0, last=0)
+    return m.cfg, tok, source
+
+
+class _Scorer:
+    """What MetricSuite's confidence metric needs from a scoring model (``confidence``)."""
+
+    def __init__(self, engine: "PipelineGenerator"):
+        self.engine = engine
+
+    @property
+    def device(self):
+        return self.engine.device
+
+    def confidence(self, ids: List[int]) -> float:
+        return self.engine.confidence(ids)
+
+
+class PipelineGenerator:
+    """Generator-compatible front end of one model's pipeline stage on this rank."""
+
+    def __init__(self, stage_model: DecoderLM, rank: int, world: int, max_batch: int = 1, max_seq: int = 2048,
+                 tag: int = 0, lanes: int = 1, n_micro: Optional[int] = None, kv_dtype: str = "bf16",
+                 eos_every: int = 8, group=None, use_graphs: Optional[bool] = None):
+        self.rank, self.world, self.tag, self.group = rank, world, tag, group
+        M = max(n_micro or 0, world * lanes)
+        b = max(1, math.ceil(max_batch / M))
+        self.stage = PipelineStage(stage_model, rank, world, b, M, min(max_seq, stage_model.cfg.max_position_embeddings),
+                                   group=group, lanes=lanes, kv_dtype=kv_dtype, use_graphs=use_graphs)
+        self.cfg, self.eos_every = stage_model.cfg, eos_every
+        self.max_seq = min(max_seq, stage_model.cfg.max_position_embeddings)   # as Generator
+        self.device = stage_model.device
+        self.nccl = self.stage.nccl
+        self.cdev = self.device if self.nccl else torch.device("cpu")
+        self.model = _Scorer(self)          # Agent / MetricSuite read generator.model
+        self.last_rank = world - 1
+
+    # ------------------------------------------------------------------ comm helpers
+    def _bcast(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, 0, group=self.group)
+        return t
+
+    def _to_driver(self, t: torch.Tensor) -> torch.Tensor:
+        """Last rank -> rank 0 (in place on rank 0's buffer)."""
+        if self.world == 1:
+            return t
+        if self.rank == self.last_rank:
+            dist.send(t, 0, group=self.group)
+        elif self.rank == 0:
+            dist.recv(t, self.last_rank, group=self.group)
+        return t
+
+    # ------------------------------------------------------------------ driver API
+    @torch.no_grad()
+    def generate(self, prompts: Sequence[Sequence[int]], sampling: SamplingParams, seed: int = 0,
+                 eos_token_id: Optional[int] = None, stop_at_eos: bool = True,
+                 record_step_latency: bool = False) -> GenerationResult:
+        assert self.rank == 0, "the driver (rank 0) issues commands; workers run serve_workers()"
+        st = self.stage
+        n = len(prompts)
+        assert 0 < n <= st.M * st.b, f"{n} prompts > {st.M} micro-batches x {st.b} rows"
+        plens = [len(p) for p in prompts]
+        T = max(plens)
+        assert T + sampling.max_new_tokens <= self.max_seq, "prompt + max_new_tokens exceeds max_seq"
+        rows = list(prompts) + [prompts[0]] * (st.M * st.b - n)
+        ids = torch.zeros(len(rows), T, dtype=torch.long, device=self.cdev)
+        for i, p in enumerate(rows):
+            ids[i, :len(p)] = torch.tensor(p, dtype=torch.long)
+        lens = torch.tensor([len(p) for p in rows], dtype=torch.long, device=self.cdev)
+        hdr = torch.tensor([CMD_GENERATE, self.tag, n, T, sampling.max_new_tokens, seed,
+                            -1 if eos_token_id is None or not stop_at_eos else int(eos_token_id),
+                            int(sampling.do_sample), int(sampling.top_k or 0), 0, 0, 0],
+                           dtype=torch.long, device=self.cdev)
+        fl = torch.tensor([sampling.temperature, sampling.top_p if sampling.top_p is not None else 1.0,
+                           sampling.repetition_penalty, 0.0], dtype=torch.float64, device=self.cdev)
+        self._bcast(hdr)
+        self._bcast(fl)
+        self._bcast(ids)
+        self._bcast(lens)
+        toks, elapsed, ttft = self._run_generate(hdr, fl, ids, lens)
+        out = []
+        for r in toks[:n]:
+            if eos_token_id is not None and stop_at_eos and eos_token_id in r:
+                r = r[:r.index(eos_token_id) + 1]
+            out.append(r)
+        return GenerationResult(out, plens, elapsed, ttft, max(0.0, elapsed - ttft))
+
+    @torch.no_grad()
+    def confidence(self, ids: List[int]) -> float:
+        """mean over positions of max softmax(logits): one pipelined prefill of ``ids`` (K13)."""
+        assert self.rank == 0
+        if not ids:
+            return 0.0
+        hdr = torch.zeros(_HDR, dtype=torch.long, device=self.cdev)
+        hdr[0], hdr[1], hdr[2] = CMD_SCORE, self.tag, len(ids)
+        self._bcast(hdr)
+        t = self._bcast(torch.tensor(ids, dtype=torch.long, device=self.cdev))
+        return self._run_score(t)
+
+    # ------------------------------------------------------------------ every rank
+    def _run_generate(self, hdr, fl, ids, lens):
+        st = self.stage
+        n, T, max_new, seed, eos = (int(hdr[i]) for i in (2, 3, 4, 5, 6))
+        sp = SamplingParams(max_new_tokens=max_new, temperature=float(fl[0]), top_k=int(hdr[8]),
+                            top_p=float(fl[1]), repetition_penalty=float(fl[2]), do_sample=bool(int(hdr[7])))
+        M, b = st.M, st.b
+        dev = self.device
+        ids_d = ids.to(dev)
+        prompts = [ids_d[m * b:(m + 1) * b] for m in range(M)]
+        res = st.run(prompts, T, sp, max_new - 1, seed=seed, prompt_lens=lens.view(M, b),
+                     eos_token_id=None if eos < 0 else eos, eos_every=self.eos_every)
+        out = torch.zeros(M * b, max_new, dtype=torch.long, device=self.cdev)
+        timing = torch.zeros(3, dtype=torch.float64, device=self.cdev)
+        if self.rank == self.last_rank:
+            out.copy_(torch.tensor(res.tokens, dtype=torch.long))
+            timing[0] = res.elapsed_s
+            timing[1] = res.stats.get("ttft_ms", 0.0) / 1e3
+            timing[2] = res.ticks
+        self._to_driver(out)
+        self._to_driver(timing)
+        self.last_ticks = int(timing[2])                # ticks run (fewer when EOS ended the run)
+        return out.tolist(), float(timing[0]), float(timing[1])
+
+    def _run_score(self, ids: torch.Tensor) -> float:
+        """One prefill of [1, T] through the stages (micro-batch 0's cache row 0)."""
+        st, dev = self.stage, self.device
+        T = ids.numel()
+        assert T <= self.max_seq
+        H = self.cfg.hidden_size
+        sp = torch.zeros(1, dtype=torch.int32, device=dev)
+        ctx = AttnCtx("prefill", 1, T, sp, sp + T, T, st.kv.rows(0, 1), st.rope)
+        hidden = None
+        if not st.is_first:
+            hidden = torch.empty(T, H, dtype=st.model.dtype, device=dev if self.nccl else "cpu")
+            dist.recv(hidden, st.prev, group=self.group)
+            hidden = hidden.to(dev)
+        out = st.model(ids.to(dev).view(1, T) if st.is_first else None, ctx, hidden=hidden, logits="all")
+        val = torch.zeros(1, dtype=torch.float64, device=self.cdev)
+        if st.is_last:
+            val[0] = float(ops.max_softmax_prob(out).mean())
+        else:
+            dist.send(out.contiguous() if self.nccl else out.contiguous().cpu(), st.next, group=self.group)
+        self._to_driver(val)
+        return float(val[0])
+
+
+def serve_workers(engines: Dict[int, PipelineGenerator]) -> int:
+    """Worker loop of ranks > 0: execute the driver's commands on the stage of the addressed model
+    (``tag``) until STOP.  Returns the number of commands served."""
+    any_eng = next(iter(engines.values()))
+    served = 0
+    while True:
+        hdr = any_eng._bcast(torch.zeros(_HDR, dtype=torch.long, device=any_eng.cdev))
+        cmd, tag = int(hdr[0]), int(hdr[1])
+        if cmd == CMD_STOP:
+            return served
+        eng = engines[tag]
+        if cmd == CMD_GENERATE:
+            fl = eng._bcast(torch.zeros(4, dtype=torch.float64, device=eng.cdev))
+            n_rows, T = eng.stage.M * eng.stage.b, int(hdr[3])
+            ids = eng._bcast(torch.zeros(n_rows, T, dtype=torch.long, device=eng.cdev))
+            lens = eng._bcast(torch.zeros(n_rows, dtype=torch.long, device=eng.cdev))
+            eng._run_generate(hdr, fl, ids, lens)
+        elif cmd == CMD_SCORE:
+            ids = eng._bcast(torch.zeros(int(hdr[2]), dtype=torch.long, device=eng.cdev))
+            eng._run_score(ids)
+        else:
+            raise RuntimeError(f"unknown pipeline command {cmd}")
+        served += 1
+
+
+def stop_workers(engine: PipelineGenerator) -> None:
+    """Driver: release the workers' serve loop."""
+    if engine.world > 1 and engine.rank == 0:
+        hdr = torch.zeros(_HDR, dtype=torch.long, device=engine.cdev)
+        hdr[0] = CMD_STOP
+        engine._bcast(hdr)

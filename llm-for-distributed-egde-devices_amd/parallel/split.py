@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from ..engine.kv_cache import KVCache
 from ..models.decoder import AttnCtx, DecoderLM
+from ..models.layers import PartialSum
 from .partition import partition_model
 
 
@@ -121,7 +122,9 @@ class SplitLM(nn.Module):
             rope = self._ropes.get(dev)
             if rope is None:
                 rope = self._ropes[dev] = ctx.rope.to(dev)
-        return dataclasses.replace(ctx, start_pos=ctx.start_pos.to(dev), seq_lens=ctx.seq_lens.to(dev), rope=rope)
+        last = ctx.last_pos.to(dev) if ctx.last_pos is not None else None
+        return dataclasses.replace(ctx, start_pos=ctx.start_pos.to(dev), seq_lens=ctx.seq_lens.to(dev), rope=rope,
+                                   last_pos=last)
 
     @torch.no_grad()
     def forward(self, ids: Optional[torch.Tensor], ctx: AttnCtx, hidden: Optional[torch.Tensor] = None,
@@ -131,8 +134,8 @@ class SplitLM(nn.Module):
         residual = None
         for s, dev in enumerate(self.devices):
             c = self._ctx_on(ctx, dev)
-            if x.device != dev:                              # the inter-stage hop (xGMI peer copy)
-                from ..models.layers import PartialSum
+            xd = x.parts.device if isinstance(x, PartialSum) else x.device   # split-K slices (o / down)
+            if xd != dev:                                    # the inter-stage hop (xGMI peer copy)
                 if isinstance(x, PartialSum):
                     x = x.materialize()
                 x = x.to(dev, non_blocking=True)
@@ -141,11 +144,10 @@ class SplitLM(nn.Module):
                 x, residual = layer(x, residual, c)
         c = self._ctx_on(ctx, self.devices[-1])
         if self._head_embed is not None:
-            from ..models.layers import PartialSum
             if isinstance(x, PartialSum):
                 x = x.materialize()
             if logits == "last" and c.T > 1:
-                idx = torch.arange(c.B, device=x.device) * c.T + (c.T - 1)
+                idx = c.last_rows(x.device)
                 x = x.index_select(0, idx)
                 residual = residual.index_select(0, idx) if residual is not None else None
             h, _ = m.final_norm(x, residual)

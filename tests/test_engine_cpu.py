@@ -66,3 +66,21 @@ def test_lane_generator_matches_independent_generators():
     for i in range(2):
         ref = Generator(m, max_batch=2, max_seq=32).generate(prompts[2 * i:2 * i + 2], sp, seed=11 + 7919 * i)
         assert got[i] == ref.tokens
+
+
+def test_ragged_batched_prefill_matches_one_at_a_time():
+    """Unequal prompts prefill in ONE right-padded pass (AttnCtx.last_pos): greedy tokens and the
+    sampled stream equal each prompt generated alone, for every decoder family."""
+    prompts = [[3, 14, 15, 92, 65, 35, 89], [7, 1], [22, 4, 9, 9, 31], [5]]
+    for arch in ("llama", "gpt_neox", "phi", "gpt2"):
+        m = build_model(tiny(arch), dtype=torch.float32, seed=7)
+        sp = SamplingParams(max_new_tokens=8, do_sample=False, repetition_penalty=1.1)
+        batched = Generator(m, max_batch=4, max_seq=64)
+        calls = []
+        orig = batched.prefill
+        batched.prefill = lambda *a, **k: calls.append(a[0].shape) or orig(*a, **k)
+        res = batched.generate(prompts, sp)
+        assert len(calls) == 1 and tuple(calls[0]) == (4, 7), calls     # one pass, padded to the longest
+        for p, toks in zip(prompts, res.tokens):
+            alone = Generator(m, max_batch=1, max_seq=64).generate([p], sp)
+            assert toks == alone.tokens[0], arch
