@@ -10,8 +10,9 @@ Work per step: every in-flight sequence decodes one token, sampled with the refe
 (T=0.7, top-k 50, top-p 0.9, repetition penalty 1.1 — Code/others/config.yaml:3-7).
 N = 1 runs graph-captured Generators on one GPU; N > 1 runs the RCCL pipeline with one stage
 (~32/N decoder layers) per GPU and N x lanes micro-batches in flight.  Every GPU decodes ``lanes``
-micro-batches concurrently on separate HIP streams (default 2 x 128 sequences), so per-GPU work
-per step is constant (weak scaling: global batch = micro-batch x lanes x N).
+micro-batches concurrently on separate HIP streams (default 1 x 256 sequences: one micro-batch
+whose decode GEMMs read each weight once per step), so per-GPU work per step is constant (weak
+scaling: global batch = micro-batch x lanes x N).
 Weights: random-init Llama-2-7B architecture; the FULL model is SmoothQuant-calibrated on
 synthetic tokens and smoothed once, then each rank keeps its layers, so every split runs
 bit-identical INT8 weights.  Data: random prompt ids.  ``--device cpu --model tiny:llama``
@@ -51,13 +52,14 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama-2-7b")
     ap.add_argument("--quant", default="w8a8_smoothquant", choices=["none", "w8a8_smoothquant", "w8a8"])
-    ap.add_argument("--micro-batch", type=int, default=128,
-                    help="sequences per micro-batch (128: the largest the fused decode GEMVs take; with --lanes 1 "
-                         "the latency point, 16-64 trade tok/s for latency)")
+    ap.add_argument("--micro-batch", type=int, default=256,
+                    help="sequences per micro-batch (256: the largest the fused decode GEMMs take — the 129-256-row "
+                         "kernels stream every weight once for all 256 sequences; 16-128 trade tok/s for latency)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--lanes", type=int, default=2,
-                    help="micro-batches each GPU decodes concurrently on separate HIP streams (own graphs/pools)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="micro-batches each GPU decodes concurrently on separate HIP streams (own graphs/pools); "
+                         "1 x 256 reads each weight once per step (2 x 128 reads it twice: 33.2k vs 34.8k tok/s)")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"],
                     help="KV cache: bf16 (default) or int8 with per-(token, head) scales (half the KV bytes: 1.6x faster attention at >= 512 keys, neutral at the 128-token bench context)")
     ap.add_argument("--no-graphs", action="store_true")
@@ -65,7 +67,8 @@ def parse(argv=None):
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
     ap.add_argument("--latency-point", default="auto", choices=["auto", "off", "int8", "both"],
                     help="also report batch-1 p50 per-token latency (single GPU): int8 = the benchmark model at "
-                         "micro-batch 1, both = plus the bf16 model; auto = both on a GPU, off on CPU")
+                         "micro-batch 1, both = plus a bf16 copy of the model (13.5 GB more, built for this only); "
+                         "auto = int8 on a GPU, off on CPU")
     ap.add_argument("--prefill-chunk", type=int, default=None,
                     help="chunked prefill size with HeadInfer (default: the whole prompt in one chunk)")
     ap.add_argument("--headinfer-heads", type=int, default=None,
@@ -215,7 +218,7 @@ def batch1_p50(model, cfg, args, device, steps: int) -> dict:
 def latency_points(args, device, model, cfg) -> dict:
     mode = args.latency_point
     if mode == "auto":
-        mode = "both" if device.type == "cuda" else "off"
+        mode = "int8" if device.type == "cuda" else "off"
     if mode == "off":
         return {}
     steps = max(32, args.steps)

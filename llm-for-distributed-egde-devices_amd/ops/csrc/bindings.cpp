@@ -47,6 +47,7 @@ int edge_w8a8_rows128_ok(int K, int S);
 int edge_w8a8_rows256_ok(int K);
 int edge_w8a8_rows256_splits(int K);
 void edge_w8a8_rows256_cfg(int cfg, int nt);
+void edge_w8a8_rows256_diag(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st);
 int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
@@ -750,6 +751,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
     else if (what == "ring2_cfg") edge_w8a8_ring2_cfg((int)a, (int)b);
     else if (what == "ring2_256") edge_w8a8_rows256_cfg((int)a, (int)b);
+    else if (what == "ring2_256_diag") edge_w8a8_rows256_diag((int)a);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);
     else if (what == "weight_nt") edge_w8a8_weight_nt((int)a);

@@ -68,6 +68,10 @@ __device__ __forceinline__ void fold(v4f& accf, const v4i& t, const v4f& s) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) accf[q] += (float)t[q] * s[q];
 }
+__device__ __forceinline__ void fold1(v4f& accf, const v4i& t, float s) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) accf[q] += (float)t[q] * s;
+}
 
 // int8 A fragment of k-tile k for this lane's row (ragged K: byte-wise, zero padded)
 __device__ __forceinline__ v4i load_a_i8(const int8_t* __restrict__ arow_p, bool aval, int k, int kend, int akc,
@@ -634,6 +638,11 @@ __device__ __forceinline__ v4i lds_read16(uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
   return r;
 }
+__device__ __forceinline__ int lds_read4(uint32_t addr) {
+  int r;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
 
 // n ds_read_b128 at addr + 1024 i (immediate offsets: no address VALU, no extra VGPRs)
 template <int I, int N>
@@ -1123,42 +1132,63 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // WNT: weight DMA with the nontemporal cache policy (default); false = normal allocation, so the
 // other lane's read of the same layer can hit the memory-side cache (A/B knob "weight_nt")
 // MS == 2 (129-256 rows, one 256-row decode micro-batch): the rows are cut into two halves of at
-// most 128 and each logical workgroup runs once per half.  Block b computes half (b >> 3) & 1 of
-// logical workgroup (b & 7) | (b >> 4) << 3, so the two halves of one weight panel are blocks b and
-// b + 8: under the observed round-robin dispatch they share an XCD, and the second reader of a
-// weight line finds it in that XCD's L2 (speed only: each half is a complete, independent
-// computation).  Launch 16 * ceil(G / 8) blocks for G logical workgroups; surplus blocks exit.
+// most 128 and each logical workgroup runs once per half.  The two halves of one weight panel are
+// blocks b and b + 8: under the observed round-robin dispatch they share an XCD, and the second
+// reader of a weight line finds it in that XCD's L2 (speed only: each half is a complete,
+// independent computation).  Launch 16 * ceil(G / 8) blocks for G logical workgroups; surplus
+// blocks exit.
 // NAL > 0: NAL dedicated activation-loader waves issue every activation piece (DA stages ahead) and
 // the compute waves only read LDS and run MFMAs.  With NAL == 0 the compute waves issue their own
 // activation DMA, and at 128 rows x 6 tiles that DMA issue (the CU's texture path is busy with
 // 28 KiB per stage) serialised with their MFMAs: ~1400 cycles per stage against ~470 of DMA and ~400
 // of MFMA (tools/bench_ops.py --only rows256, qkv 22 us at M = 256).
+// NCW == 8: eight compute waves (two per SIMD) as 4 (rows) x 2 (tiles), each with 2 row blocks x
+// NTW / 2 tiles: the per-k-tile fold of the grouped scales (8 VALU per MFMA) then issues from two
+// waves per SIMD beside the other wave's MFMAs instead of serialising behind one wave's own.
 template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true, int MS = 1,
-          int NAL = 0>
-__global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
+          int NAL = 0, int NCW = 4>
+__global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
-    int M, int N, int K, int NTt, int Mpad, int S = 1, int G = 0) {
-  constexpr int MB = 8, NCW = 4, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
+    int M, int N, int K, int NTt, int Mpad, int S = 1, int G = 0, int diag = 0) {
+  // diag (speed diagnostics only, results are garbage): 1 no activation DMA, 2 no weight DMA,
+  // 4 no MFMAs, 8 no LDS fragment reads and no MFMAs, 16 no epilogue, 32 exit at once, 64 the weight
+  // loaders re-read two k-tiles (weights L2-resident), 128 epilogue without its global stores
+  constexpr int MB = 8, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
+  constexpr int NTH = NCW == 8 ? NTW / 2 : NTW;       // tiles per compute wave
+  static_assert(NCW == 4 || (NCW == 8 && NTW % 2 == 0 && EPI != EPI_GLUQ), "compute waves");
   constexpr int LPW = WPW + (SC ? 1 : 0);             // loader pieces per stage (+ the scale piece)
   static_assert(WST % NWL == 0, "weight pieces split evenly over the loader waves");
   static_assert(DW * LPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTW == 8 && !SC), "epilogues");
   static_assert(MS == 1 || MS == 2, "row split");
   static_assert(NAL == 0 || (16 % NAL == 0 && DA * (16 / NAL) <= 63), "activation loaders");
-  constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0);
+  // + 1 KiB: the workgroup's weight scales and bias (fp32, <= 128 columns), staged once for the epilogue
+  constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0) + 1;
   static_assert(LDS_KB * 1024 <= 160 * 1024, "LDS budget");
+  static_assert(NTW * 16 <= 128, "epilogue operand area");
   __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_KB * 1024];
   int8_t* const wring = lds;
   int8_t* const aring = lds + RW * WST * 1024;
   int8_t* const sring = aring + RA * 16 * 1024;       // SC only
+  float* const epi_sw = reinterpret_cast<float*>(lds + (LDS_KB - 1) * 1024);
+  float* const epi_b = epi_sw + 128;
   int lbid = (int)blockIdx.x, row0 = 0;
   if constexpr (MS == 2) {
-    row0 = (((int)blockIdx.x >> 3) & 1) * 128;
-    lbid = ((int)blockIdx.x & 7) | (((int)blockIdx.x >> 4) << 3);
-    if (lbid >= G) return;                            // whole workgroup: no barrier is left waiting
+    // XCD-contiguous logical order: blocks b = 8 j + x (x = b & 7 labels the blocks that share an
+    // XCD under round-robin dispatch) take logical workgroup x * ceil(G / 8) + (j >> 1), half j & 1,
+    // so both halves of a panel AND neighbouring column groups (whose output rows meet inside one
+    // 128-B line) share an XCD's L2 — partial lines merge there instead of in HBM (speed only)
+    // EPI_PART keeps the round-robin order: an XCD then holds a fixed subset of the K slices, and
+    // the activation bytes of those slices stay in its L2 (measured: o 14.9 vs 17.0 us, down 31.3
+    // vs 34.9 at M = 256 against the contiguous order)
+    const int x = (int)blockIdx.x & 7, j = (int)blockIdx.x >> 3, gx = (G + 7) >> 3;
+    row0 = (j & 1) * 128;
+    lbid = EPI == EPI_PART ? x | ((j >> 1) << 3) : x * gx + (j >> 1);
+    if ((j >> 1) >= gx || lbid >= G) return;          // whole workgroup: no barrier is left waiting
   }
   const int Ml = min(128, M - row0);                  // rows of this half (>= 1: MS == 2 only for M > 128)
+  if (diag & 32) return;                              // (diagnostic: launch + dispatch only)
   const int KT = K / 64, NSA = KT / 2;
   const int grp = EPI == EPI_PART ? lbid / S : lbid;
   const int ks = EPI == EPI_PART ? lbid % S : 0;
@@ -1166,6 +1196,7 @@ __global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kerne
   const int NS = EPI == EPI_PART ? (int)((int64_t)NSA * (ks + 1) / S) - sbeg : NSA;
   const int nt0 = grp * NTW;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mw = NCW == 8 ? (wave & 3) : wave, tb = NCW == 8 ? (wave >> 2) * NTH : 0;   // compute waves
   // k order rotated per workgroup (int32 sums: exact in any order; SC: a fixed per-workgroup fp32
   // order): the ~256 workgroups do not all request the same activation lines at the same moment
   const int rot = ROT ? (int)((grp * 5u) % (unsigned)NS) : 0;
@@ -1183,7 +1214,8 @@ __global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kerne
       auto issue = [&](int st) {
         const int8_t* ab = Ah + (size_t)phys(st) * 128;
 #pragma unroll
-        for (int i = 0; i < APL; ++i) glds16(ab + aoff[i], aring + ((st % RA) * 16 + al * APL + i) * 1024);
+        for (int i = 0; i < APL; ++i)
+          if (!(diag & 1)) glds16(ab + aoff[i], aring + ((st % RA) * 16 + al * APL + i) * 1024);
       };
       for (int st = 0; st < DA; ++st) issue(st);
       for (int s = 0; s < NS; ++s) {
@@ -1207,10 +1239,11 @@ __global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kerne
     const uint32_t soff = (uint32_t)((lane >> 5) * Mpad + row0 + min(4 * (lane & 31), Mpad - row0 - 4));
     const bool smine = (lane % NWL) == lw;
     auto issue = [&](int st) {
-      const int p = phys(st);
+      const int p = (diag & 64) ? (phys(st) & 1) : phys(st);   // (diagnostic 64: L2-resident weights)
       const int8_t* wb = Wp + (size_t)p * 2048;
 #pragma unroll
       for (int i = 0; i < WPW; ++i) {
+        if (diag & 2) continue;
         if constexpr (WNT) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
         else glds16(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
       }
@@ -1237,50 +1270,55 @@ __global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kerne
     if constexpr (NAL == 0) {
       const int8_t* ab = Ah + (size_t)phys(st) * 128;
 #pragma unroll
-      for (int i = 0; i < APW; ++i) glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
+      for (int i = 0; i < APW; ++i)
+        if (!(diag & 1)) glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
     }
   };
-  // epilogue operands first (the tail never waits on memory; retired by the first vmcnt wait)
-  float sw_t[NTW], b_t[NTW], sa_r[2][4];
-  const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
-#pragma unroll
-  for (int t = 0; t < NTW; ++t) {
-    const int col = min((nt0 + t) * 16 + (lane & 15), N - 1);
-    sw_t[t] = sw[col];
-    b_t[t] = bf2f(bp[bias != nullptr ? col : 0]);
+  // The MFMA operands are swapped (weight tile = A operand, activations = B): a lane's accumulator
+  // holds 4 CONSECUTIVE output columns (4 (lane >> 4) + q of tile t) of ONE row ((lane & 15) of row
+  // block j), so the epilogue stores 8 B (bf16) / 16 B (fp32) per lane instead of 2 / 4 B, and a
+  // row's activation scale is one value per lane.  The workgroup's weight scales and bias go to
+  // LDS once now (ordered for the epilogue by the stage barriers); the tail never waits on memory.
+  {
+    const int c = threadIdx.x;                        // compute waves: 256 threads, <= 128 columns
+    if (c < NTW * 16) {
+      const int col = min(nt0 * 16 + c, N - 1);
+      epi_sw[c] = sw[col];
+      epi_b[c] = bias != nullptr ? bf2f(bias[col]) : 0.f;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   }
+  float sa_r[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) sa_r[j] = SC ? 1.f : sa[row0 + min((2 * mw + j) * 16 + (lane & 15), Ml - 1)];
+  v4i acc[2][NTH];
+  v4f accf[2][NTH];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sa_r[j][q] = SC ? 1.f : sa[row0 + min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, Ml - 1)];
-  v4i acc[2][NTW];
-  v4f accf[2][NTW];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) { acc[j][t] = v4i{0, 0, 0, 0}; accf[j][t] = v4f{0.f, 0.f, 0.f, 0.f}; }
+    for (int t = 0; t < NTH; ++t) { acc[j][t] = v4i{0, 0, 0, 0}; accf[j][t] = v4f{0.f, 0.f, 0.f, 0.f}; }
 
   for (int st = 0; st < DA; ++st) issue(st);
   // row block rb = 2 wave + j lives in line pieces 2 rb, 2 rb + 1; k-tile c's chunk is 4 c + (lane >> 4)
-  const uint32_t a0 = lds_off(aring) + (4 * wave + ((lane & 15) >> 3)) * 1024 + (lane & 7) * 128;
+  const uint32_t a0 = lds_off(aring) + (4 * mw + ((lane & 15) >> 3)) * 1024 + (lane & 7) * 128;
   const uint32_t ax[2] = {(uint32_t)(((lane >> 4) ^ (lane & 7)) << 4), (uint32_t)(((4 + (lane >> 4)) ^ (lane & 7)) << 4)};
-  const uint32_t w0 = lds_off(wring) + lane * 16;
-  const uint32_t s0 = lds_off(sring) + ((2 * wave) * 16 + 4 * (lane >> 4)) * 4;
-  // one k-tile's fragments: [2 row blocks | NTW tiles | SC: 2 row blocks' scales], double-buffered
-  // by k-tile, so the MFMAs of one k-tile run while the next one's LDS reads are in flight (across
-  // the stage barrier too)
-  constexpr int NF = 2 + NTW + (SC ? 2 : 0);
+  const uint32_t w0 = lds_off(wring) + lane * 16 + tb * 1024;
+  const uint32_t s0 = lds_off(sring) + ((2 * mw) * 16 + (lane & 15)) * 4;
+  // one k-tile's fragments: [2 row blocks | NTW tiles | SC: 2 row blocks' scales (lane's row, in
+  // element 0)], double-buffered by k-tile, so the MFMAs of one k-tile run while the next one's LDS
+  // reads are in flight (across the stage barrier too)
+  constexpr int NF = 2 + NTH + (SC ? 2 : 0);
   auto read_kt = [&](int st, int c, v4i (&f)[NF]) {
     const uint32_t ab = a0 + (st % RA) * 16 * 1024, wb = w0 + (st % RW) * WST * 1024;
 #pragma unroll
     for (int j = 0; j < 2; ++j) f[j] = lds_read16(ab + j * 2048 + ax[c]);
-    v4i b[NTW];
-    lds_read_row<NTW>(wb + c * NTW * 1024, b);
+    v4i b[NTH];
+    lds_read_row<NTH>(wb + c * NTW * 1024, b);
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) f[2 + t] = b[t];
+    for (int t = 0; t < NTH; ++t) f[2 + t] = b[t];
     if constexpr (SC) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) f[2 + NTW + j] = lds_read16(s0 + (st % RW) * 1024 + c * 512 + j * 64);
+      for (int j = 0; j < 2; ++j) f[2 + NTH + j][0] = lds_read4(s0 + (st % RW) * 1024 + c * 512 + j * 64);
     }
   };
   auto mma = [&](v4i (&f)[NF]) {
@@ -1289,23 +1327,23 @@ __global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kerne
     if constexpr (SC) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const v4f sg = __builtin_bit_cast(v4f, f[2 + NTW + j]);
+        const float sg = __builtin_bit_cast(float, f[2 + NTH + j][0]);
 #pragma unroll
-        for (int t = 0; t < NTW; ++t) fold(accf[j][t], mfma_i8(f[j], f[2 + t], v4i{0, 0, 0, 0}), sg);
+        for (int t = 0; t < NTH; ++t) fold1(accf[j][t], mfma_i8(f[2 + t], f[j], v4i{0, 0, 0, 0}), sg);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(accf[j][t]));
+        for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(accf[j][t]));
     } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int t = 0; t < NTW; ++t) acc[j][t] = mfma_i8(f[j], f[2 + t], acc[j][t]);
+        for (int t = 0; t < NTH; ++t) acc[j][t] = mfma_i8(f[2 + t], f[j], acc[j][t]);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(acc[j][t]));
+        for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(acc[j][t]));
     }
   };
   // barrier k certifies stage k (both operands) and frees the slots of stage k - 1
@@ -1315,69 +1353,88 @@ __global__ void __launch_bounds__((4 + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kerne
     issue(st + DA);
   };
   v4i x[NF], y[NF];
+  const bool rd = !(diag & 8), mm = !(diag & 12);
   sync_stage(0);
-  read_kt(0, 0, x);
+  if (rd) read_kt(0, 0, x);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   for (int s = 0; s < NS; ++s) {                     // x holds k-tile (s, 0)
-    read_kt(s, 1, y);
-    mma(x);
+    if (rd) read_kt(s, 1, y);
+    if (mm) mma(x);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (s + 1 < NS) {                                 // wave-uniform
       sync_stage(s + 1);
-      read_kt(s + 1, 0, x);
+      if (rd) read_kt(s + 1, 0, x);
     }
-    mma(y);
+    if (mm) mma(y);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // epilogue: lane holds col (lane & 15) of each tile, rows 4 (lane >> 4) + q of its 2 row blocks
+  if (diag & 16) return;                            // (diagnostic: no epilogue)
+  // epilogue: lane holds row (2 wave + j) * 16 + (lane & 15), columns 4 (lane >> 4) .. + 3 of tile t
+  const int g4 = 4 * (lane >> 4);
   if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      const int col = (nt0 + t) * 16 + (lane & 15);
-      if (nt0 + t >= NTt || col >= N) continue;
+    for (int j = 0; j < 2; ++j) {
+      const int lrow = (2 * mw + j) * 16 + (lane & 15);
+      if (lrow >= Ml) continue;
+      const int row = row0 + lrow;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int t = 0; t < NTH; ++t) {
+        const int cl = (tb + t) * 16 + g4, col = nt0 * 16 + cl;
+        if (col >= N) continue;
+        float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int lrow = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
-          if (lrow >= Ml) continue;
-          const int row = row0 + lrow;
-          const float v = SC ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j][q];
-          if constexpr (EPI == EPI_PART)
-            reinterpret_cast<float*>(outv)[((size_t)ks * M + row) * N + col] = v * sw_t[t] + (ks == 0 ? b_t[t] : 0.f);
-          else
-            reinterpret_cast<bf16_t*>(outv)[(size_t)row * N + col] = f2bf(v * sw_t[t] + b_t[t]);
+          const float a = SC ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j];
+          v[q] = a * epi_sw[cl + q] + ((EPI == EPI_OUT || ks == 0) ? epi_b[cl + q] : 0.f);
         }
+        if (diag & 128) { asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])); continue; }
+        if constexpr (EPI == EPI_PART) {
+          float* o = reinterpret_cast<float*>(outv) + ((size_t)ks * M + row) * N + col;
+          if (col + 3 < N && (N & 3) == 0) *reinterpret_cast<v4f*>(o) = v4f{v[0], v[1], v[2], v[3]};
+          else for (int q = 0; q < 4 && col + q < N; ++q) o[q] = v[q];
+        } else {
+          bf16_t* o = reinterpret_cast<bf16_t*>(outv) + (size_t)row * N + col;
+          if (col + 3 < N && (N & 3) == 0) *reinterpret_cast<uint2*>(o) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+          else for (int q = 0; q < 4 && col + q < N; ++q) o[q] = f2bf(v[q]);
+        }
+      }
     }
   } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
     const int Fo = N / 2, grp64 = nt0 / 8;
     int8_t* hq = reinterpret_cast<int8_t*>(outv);
+    const bool live = nt0 + 7 < NTt;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      const int lrow = (2 * wave + j) * 16 + (lane & 15);
+      const int row = row0 + lrow;
+      float h[4][4], amax = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int lrow = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
-        const int row = row0 + lrow;
-        float h[4], amax = 0.f;
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cg = 2 * p * 16 + g4 + q, cu = cg + 16;
+          const float g = bf2f(f2bf((float)acc[j][2 * p][q] * sa_r[j] * epi_sw[cg] + epi_b[cg]));     // the unfused GEMM output is bf16
+          const float u = bf2f(f2bf((float)acc[j][2 * p + 1][q] * sa_r[j] * epi_sw[cu] + epi_b[cu]));
+          h[p][q] = g / (1.f + __expf(-g)) * u;
+          amax = fmaxf(amax, fabsf(h[p][q]));
+        }
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));   // the row's 64 features sit in lanes l, l ^ 16, l ^ 32, l ^ 48
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      amax = fmaxf(amax, 1e-8f);
+      const float inv = 127.f / amax;
+      if (live && lrow < Ml) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          const float g = bf2f(f2bf((float)acc[j][2 * p][q] * sa_r[j][q] * sw_t[2 * p] + b_t[2 * p]));
-          const float u = bf2f(f2bf((float)acc[j][2 * p + 1][q] * sa_r[j][q] * sw_t[2 * p + 1] + b_t[2 * p + 1]));
-          h[p] = g / (1.f + __expf(-g)) * u;
-          amax = fmaxf(amax, fabsf(h[p]));
-        }
+          uint32_t w = 0;
 #pragma unroll
-        for (int d = 1; d < 16; d <<= 1) amax = fmaxf(amax, __shfl_xor(amax, d, 64));
-        amax = fmaxf(amax, 1e-8f);
-        const bool live = nt0 + 7 < NTt;
-        if (live && row < M) {
-#pragma unroll
-          for (int p = 0; p < 4; ++p) hq[(size_t)row * Fo + (nt0 / 2 + p) * 16 + (lane & 15)] = quant_i8(h[p], 127.f / amax);
+          for (int q = 0; q < 4; ++q) w |= (uint32_t)(uint8_t)quant_i8(h[p][q], inv) << (8 * q);
+          *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + (nt0 / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
         }
-        if (live && (lane & 15) == 0 && row < Mpad) os[(size_t)grp64 * Mpad + row] = row < M ? amax / 127.f : 0.f;
       }
+      if (live && lane < 16 && row < Mpad) os[(size_t)grp64 * Mpad + row] = lrow < Ml ? amax / 127.f : 0.f;
+    }
   }
 }
 }  // namespace
@@ -1456,6 +1513,14 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
       // but the 2-lane bench with o / down / qkv / gate_up all on ring2 (this geometry, no k
       // rotation for qkv / gate_up) measured 32.9-33.4k against 32.2-32.4k tok/s (interleaved
       // A/B, profiles/bench_ring2_cfg_ab_r2.jsonl).  cfg 7: o back on the LDS-staged kernel.
+      // cfg 0: 8 compute waves (two per SIMD) with 2 weight + 2 activation loader waves, the form
+      // that measured fastest at 256 rows (the fold issues beside the partner wave's MFMAs)
+      if (g_ring2_cfg == 0 && g_w_nt) {
+        hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<4, 2, 8, 4, EPI_PART, true, true, true, 1, 2, 8>),
+                           dim3((NTt + 3) / 4 * S), dim3(12 * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,
+                           (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);
+        return (int)hipGetLastError();
+      }
       if (g_ring2_cfg == 0 || g_ring2_cfg == 1 || (g_ring2_cfg == 7 && K >= 8192)) R2S(4, 4, 8, 4);
       if (g_ring2_cfg == 2) R2S(4, 2, 12, 3);
       if (g_ring2_cfg == 3) R2S(2, 2, 16, 4);
@@ -1496,7 +1561,7 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
     } else if constexpr (EP == EPI_OUT) {
       if (g_ring2_cfg == 4) R2(3, 3, 16, 3, EPI_OUT);      // the first default (18.3-19.0 us)
       if (g_ring2_cfg == 2) R2(3, 6, 16, 3, EPI_OUT);
-      if (g_ring2_cfg == 3) R2(4, 4, 12, 4, EPI_OUT);
+      if (g_ring2_cfg == 3) R2(4, 4, 11, 4, EPI_OUT);
       R2(3, 3, 14, 4, EPI_OUT);
     }
 #undef R2
@@ -1535,14 +1600,14 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
 // Tiles per workgroup are chosen for ~256 launched workgroups (the logical grid doubles).
 // cfg (EDGELLM_TUNE=ring2_256=c[,nt]): A/B geometries; nt = 0 (cfg 0 only) selects normal weight
 // allocation instead of nontemporal (1-4 % slower at M = 256).  -1: no kernel for this call.
-static int g_r256_cfg = 0, g_r256_nt = 1;
-template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV>
+static int g_r256_cfg = 0, g_r256_nt = 1, g_r256_diag = 0;
+template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV, int NCWV = 4>
 int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
                 int M, int N, int K, int Mpad, hipStream_t st, int S) {
   const int NTt = (N + 15) / 16, G = (NTt + NTWV - 1) / NTWV * S;
-  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV>),
-                     dim3((G + 7) / 8 * 16), dim3((4 + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
-                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G);
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV>),
+                     dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
+                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
   return (int)hipGetLastError();
 }
 
@@ -1566,16 +1631,24 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
     const bool narrow = (NTt + 3) / 4 * S <= 160;     // o (N 4096, 2 slices): 128 logical at 4 tiles
 #define R256S(NTWV, NWLV, RWV, RAV, NALV) \
   do { if (scaled) R256(NTWV, NWLV, RWV, RAV, NALV, true); R256(NTWV, NWLV, RWV, RAV, NALV, false); } while (0)
+#define R256S8(NTWV, NWLV, RWV, RAV, NALV)                                                                       \
+  do {                                                                                                        \
+    if (scaled) return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, true, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
+    return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
+  } while (0)
+    // 8 compute waves (two per SIMD): the grouped-scale fold issues beside the partner's MFMAs
+    // (tools/bench_ops.py --only rows256, M = 256: o 17.4 -> 14.9 us, down 34.8 -> 28.9 us)
     if (narrow) {
-      if (c == 1) R256S(4, 2, 8, 4, 1);
+      if (c == 1) R256S(4, 2, 8, 4, 2);              // 4 compute waves
       if (c == 2) R256S(4, 4, 8, 4, 0);
       if (c == 3) R256S(4, 2, 6, 6, 2);
-      R256S(4, 2, 8, 4, 2);
+      R256S8(4, 2, 8, 4, 2);
     }
-    if (c == 1) R256S(8, 2, 5, 4, 1);                 // down (N 4096, 4 slices): 128 logical at 8 tiles
+    if (c == 1) R256S(8, 2, 5, 4, 2);                 // down (N 4096, 4 slices): 128 logical at 8 tiles
     if (c == 2) R256S(8, 4, 5, 4, 0);
     if (c == 3) R256S(8, 2, 4, 5, 2);
-    R256S(8, 2, 5, 4, 2);
+    R256S8(8, 2, 5, 4, 2);
+#undef R256S8
 #undef R256S
   } else if constexpr (EP == EPI_GLUQ) {
     if (N % 128 != 0 || scaled) return -1;
@@ -1590,8 +1663,9 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
       if (c == 2) R256(3, 3, 14, 4, 0, false);
       R256(3, 2, 14, 4, 2, false);
     }
+    if (c == 4) R256(8, 2, 5, 4, 2, false);
     if (NTt <= 1024) {
-      if (c == 1) R256(6, 2, 7, 4, 1, false);
+      if (c == 1) return launch_r256<6, 2, 7, 4, 2, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
       if (c == 2) R256(6, 4, 7, 4, 0, false);
       if (c == 3) R256(6, 2, 6, 5, 2, false);
       R256(6, 2, 7, 4, 2, false);
@@ -1608,6 +1682,7 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
 }  // namespace
 
 extern "C" void edge_w8a8_rows256_cfg(int cfg, int nt) { g_r256_cfg = cfg; g_r256_nt = nt; }
+extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
 // split-K slices the 129-256-row kernels use for a K (0: none)
 extern "C" int edge_w8a8_rows256_splits(int K) { return K % 128 != 0 ? 0 : (K / 128 >= 64 ? 4 : 2); }
 // whether the 129-256-row decode kernels take this K (whole K; split-K at rows256_splits(K))

@@ -410,7 +410,7 @@ def rows256_rows(C, dev, M=256):
             return call
 
         c256, c128 = make(M), make(M // 2)
-        forms = [(0, 1), (0, 0), (1, 1), (2, 1), (3, 1)]
+        forms = [(0, 1), (0, 0), (1, 1), (2, 1), (3, 1), (4, 1)]
         res = {}
         for rnd in range(3):
             for cfg, nt in forms:
@@ -422,6 +422,44 @@ def rows256_rows(C, dev, M=256):
         for form, ts in res.items():
             row[f"{form}_us"] = round(min(ts), 2)
             row[f"{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
+        out.append(row)
+        print(row, flush=True)
+        del wps
+    return out
+
+
+def rows256_diag(C, dev, M=256):
+    """Where a 256-row decode GEMM's time goes: the same launch with parts of the ring switched off
+    (tune ring2_256_diag: 1 no activation DMA, 2 no weight DMA, 4 no MFMAs, 8 no LDS reads or
+    MFMAs; results garbage, timing only), cache-cold weights."""
+    out = []
+    shapes = {"qkv": (12288, 4096, "out"), "o": (4096, 4096, "part"), "down": (4096, 11008, "part")}
+    for name, (N, K, kind) in shapes.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+        sw = torch.rand(N, device=dev) * 0.01
+        qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        sx = (torch.rand(K // 64, M, device=dev) if kind == "part" else torch.rand(M, device=dev)) * 0.01
+        ctr = [0]
+
+        def call():
+            ctr[0] = (ctr[0] + 1) % ncopy
+            if kind == "gluq":
+                return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
+            if kind == "part":
+                return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, 0)
+            return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
+
+        res = {}
+        for rnd in range(3):
+            for d in (0, 3, 11, 16, 27, 128, 128 + 11, 128 + 3):
+                C.tune("ring2_256_diag", d, 0)
+                res.setdefault(d, []).append(timeit(call, iters=10, per_graph=ncopy))
+        C.tune("ring2_256_diag", 0, 0)
+        row = dict(op="w8a8_rows256_diag", shape=name, M=M, N=N, K=K)
+        for d, ts in res.items():
+            row[f"diag{d}_us"] = round(min(ts), 2)
         out.append(row)
         print(row, flush=True)
         del wps
@@ -525,6 +563,8 @@ def main():
         rows += ring_rows(C, dev)
     if only is not None and "rows256" in only:
         rows += rows256_rows(C, dev)
+    if only is not None and "r256diag" in only:
+        rows += rows256_diag(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
     if a.out:
