@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"],
                     help="KV cache: bf16 (default) or int8 with per-(token, head) scales (half the KV bytes: 1.6x faster attention at >= 512 keys, neutral at the 128-token bench context)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--force-pipeline", action="store_true",
+                    help="N = 1: time the RCCL PipelineStage engine (world-1 process group, device bound) "
+                         "instead of the Generator, same config")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
     ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
     ap.add_argument("--latency-point", default="auto", choices=["auto", "off", "int8", "both"],
@@ -246,12 +249,28 @@ def run_pipeline(args):
     return run_pipeline_bench(args, build, model_config, kv_dtype)
 
 
+def _world1_env():
+    """torchrun-style env for a one-rank process group (``--force-pipeline`` at N = 1)."""
+    import socket
+    if "MASTER_PORT" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    for k, v in (("RANK", "0"), ("LOCAL_RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1")):
+        os.environ.setdefault(k, v)
+
+
 def main(argv=None):
     args = parse(argv)
     if args.headinfer_heads is not None:
         args.lanes = 1          # the HeadInfer offload is host-orchestrated: one lane per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 or world > 1:
+    if args.force_pipeline and world == 1 and args.gpus == 1:
+        _world1_env()
+        world = 1
+        res = run_pipeline(args)
+    elif args.gpus > 1 or world > 1:
         assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun"
         res = run_pipeline(args)
     else:
@@ -293,6 +312,7 @@ def main(argv=None):
         "prefill_tokens_per_s": round(res.get("prefill_tps", 0.0), 1),
         "peak_mem_gb": round(res.get("mem_gb", 0.0), 2),
         "world_size": res.get("world_size", args.gpus),
+        "engine": "PipelineStage" if (args.force_pipeline or args.gpus > 1) else "Generator",
     }
     if res.get("ttft_ms") is not None:
         out["ttft_ms"] = round(res["ttft_ms"], 3)

@@ -88,6 +88,7 @@ __device__ __forceinline__ void wave_argmax(float& v, int& idx) {
   }
 }
 
+template <int NTT = NT>
 __device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int* ri) {
   wave_argmax(v, idx);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -97,12 +98,14 @@ __device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int*
   v = rv[0];
   idx = ri[0];
 #pragma unroll
-  for (int i = 1; i < NW; ++i)
+  for (int i = 1; i < NTT / 64; ++i)
     if (better(rv[i], ri[i], v, idx)) { v = rv[i]; idx = ri[i]; }
 }
 
-// Block-wide (min, max) of u32 keys; `scratch` holds >= 2*NW words.
+// Block-wide (min, max) of u32 keys; `scratch` holds >= 2*(NTT/64) words.
+template <int NTT = NT>
 __device__ __forceinline__ void block_minmax_u32(uint32_t& mn, uint32_t& mx, uint32_t* scratch) {
+  constexpr int W = NTT / 64;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
@@ -110,10 +113,10 @@ __device__ __forceinline__ void block_minmax_u32(uint32_t& mn, uint32_t& mx, uin
   }
   const int w = threadIdx.x >> 6;
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) { scratch[w] = mn; scratch[NW + w] = mx; }
+  if ((threadIdx.x & 63) == 0) { scratch[w] = mn; scratch[W + w] = mx; }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < NW; ++i) { mn = min(mn, scratch[i]); mx = max(mx, scratch[NW + i]); }
+  for (int i = 0; i < W; ++i) { mn = min(mn, scratch[i]); mx = max(mx, scratch[W + i]); }
 }
 
 __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t* scratch) {
@@ -134,13 +137,15 @@ __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* scratch)
   return r;
 }
 
-// Block sum of a wave-uniform count with one barrier: `scr` is [2][NW], alternated by `parity`.
+// Block sum of a wave-uniform count with one barrier: `scr` is [2][NTT/64], alternated by `parity`.
+template <int NTT = NT>
 __device__ __forceinline__ int block_count(int wave_cnt, int* scr, int& parity) {
-  if ((threadIdx.x & 63) == 0) scr[parity * NW + (threadIdx.x >> 6)] = wave_cnt;
+  constexpr int W = NTT / 64;
+  if ((threadIdx.x & 63) == 0) scr[parity * W + (threadIdx.x >> 6)] = wave_cnt;
   __syncthreads();
   int s = 0;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) s += scr[parity * NW + i];
+  for (int i = 0; i < W; ++i) s += scr[parity * W + i];
   parity ^= 1;
   return s;
 }
@@ -169,26 +174,26 @@ __device__ __forceinline__ int wave_alloc(bool pred, int* counter) {
 // length.  One pass gives each candidate its rank and the softmax mass of the strictly better
 // candidates (those all sit at or above the k-th value, so no k-th cut is needed in the pass);
 // the reads are unrolled x8 so the broadcast LDS loads overlap.  Result on every thread.
-template <int PER>
+template <int PER, int NTT = NT>
 __device__ __forceinline__ void rank_and_sample(const uint64_t* fc, float* fe, int n, int top_k, float top_p,
                                                 uint32_t seed, uint32_t row, uint32_t step, float* sh,
                                                 uint32_t* red, float* rv, int* ri, float& bv, int& bi) {
-  // sh: [0] k-th value, [1..1+NW) partial sums
+  // sh: [0] k-th value, [1..1+NTT/64) partial sums
   const int tid = threadIdx.x;
   uint64_t my[PER];
   uint32_t kmax = 0u, kmin_unused = 0xffffffffu;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int c = tid + q * NT;
+    const int c = tid + q * NTT;
     my[q] = c < n ? fc[c] : 0ull;
     kmax = max(kmax, (uint32_t)(my[q] >> 32));
   }
-  block_minmax_u32(kmin_unused, kmax, red);
+  block_minmax_u32<NTT>(kmin_unused, kmax, red);
   const float vmax = key2f(kmax);
   float e[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int c = tid + q * NT;
+    const int c = tid + q * NTT;
     e[q] = c < n ? __expf(cval(my[q]) - vmax) : 0.f;
     if (c < ((n + 7) & ~7)) fe[c] = e[q];
   }
@@ -211,33 +216,33 @@ __device__ __forceinline__ void rank_and_sample(const uint64_t* fc, float* fe, i
   const int kk = min(top_k, n);
 #pragma unroll
   for (int q = 0; q < PER; ++q)
-    if (tid + q * NT < n && rank[q] == kk - 1) sh[0] = cval(my[q]);
+    if (tid + q * NTT < n && rank[q] == kk - 1) sh[0] = cval(my[q]);
   __syncthreads();
   const float kth = sh[0];
   float tot = 0.f;
 #pragma unroll
   for (int q = 0; q < PER; ++q)
-    if (tid + q * NT < n && cval(my[q]) >= kth) tot += e[q];
+    if (tid + q * NTT < n && cval(my[q]) >= kth) tot += e[q];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
   if ((tid & 63) == 0) sh[1 + (tid >> 6)] = tot;
   __syncthreads();
   tot = 0.f;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) tot += sh[1 + i];
+  for (int i = 0; i < NTT / 64; ++i) tot += sh[1 + i];
   bv = -INFINITY;
   bi = 0x7fffffff;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const float v = cval(my[q]);
-    if (tid + q * NT >= n || v < kth) continue;
+    if (tid + q * NTT >= n || v < kth) continue;
     if (rank[q] == 0 || top_p >= 1.f || excl[q] / tot < top_p) {
       const int id = cidx(my[q]);
       const float g = v + gumbel(seed, row, step, id);
       if (better(g, id, bv, bi)) { bv = g; bi = id; }
     }
   }
-  block_argmax(bv, bi, rv, ri);
+  block_argmax<NTT>(bv, bi, rv, ri);
 }
 
 // Zero-pad fc[n .. round_up(n, 8)) (0 ranks below every real candidate).
@@ -545,7 +550,118 @@ __global__ void __launch_bounds__(NT) topk_row_kernel(const void* __restrict__ l
     if (seen != nullptr) seen[base + bi] = 1;
   }
 }
+
+// ---------------------------------------------------------------- whole-row form (large batches)
+// One 1024-thread workgroup per row, ONE launch: at B >= ~128 rows the split form's two launches,
+// its 1 KiB zero-padded candidate list per 2K chunk and the merge's cross-XCD reload cost more than
+// they spread.  Each thread holds NS x 8 consecutive scores as u32 keys in registers (one 16-byte
+// logits load + one 8-byte `seen` load per 8), the threshold search runs on the whole row
+// (count(key >= t) in [top_k, RCAP]), the survivors go straight to LDS and rank_and_sample runs
+// on them — same processor order, same Gumbel noise, same ties as the split form and _ref.sample.
+constexpr int NTR = 1024, NWR = NTR / 64;
+constexpr int RCAP = 256;                  // candidates ranked exactly (== FCAP)
+
+template <bool BF16, int NS>
+__global__ void __launch_bounds__(NTR) topk_rowwide_kernel(const void* __restrict__ logits,
+                                                           uint8_t* __restrict__ seen, int V, float inv_t, float pen,
+                                                           int top_k, float top_p, const int* __restrict__ rng,
+                                                           int64_t* __restrict__ out_tok) {
+  __shared__ uint32_t red[2 * NWR];
+  __shared__ int scr[2 * NWR];
+  __shared__ uint64_t fc[RCAP];
+  __shared__ float fe[RCAP];
+  __shared__ int ncand;
+  __shared__ float sh[1 + NWR], rv[NWR];
+  __shared__ int ri[NWR];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const size_t base = (size_t)row * V;
+  const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
+  uint32_t kr[NS][8];
+  uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int e0 = (q * NTR + tid) * 8;
+    if (e0 < V) {
+      float v[8];
+      if constexpr (BF16) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(logits) + base + e0);
+        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[2 * u] = __uint_as_float(w[u] << 16);
+          v[2 * u + 1] = __uint_as_float(w[u] & 0xffff0000u);
+        }
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(logits) + base + e0);
+        const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(logits) + base + e0 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      uint64_t sn = 0;
+      if (seen != nullptr) sn = *reinterpret_cast<const uint64_t*>(seen + base + e0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float x = v[u];
+        if ((sn >> (8 * u)) & 0xffu) x = x < 0.f ? x * pen : x / pen;
+        kr[q][u] = f2key(x * inv_t);
+        kmin = min(kmin, kr[q][u]);
+        kmax = max(kmax, kr[q][u]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) kr[q][u] = 0u;
+    }
+  }
+  if (tid == 0) ncand = 0;
+  uint32_t thr = 1u;
+  if (V > top_k) {
+    block_minmax_u32<NTR>(kmin, kmax, red);
+    uint32_t lo = kmin, hi = kmax;         // invariant: count(key >= lo) >= top_k
+    int parity = 0;
+    for (int it = 0; it < 48 && lo < hi; ++it) {
+      const uint32_t mid = probe(lo, hi, it);
+      int wc = 0;
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wc += ballot_count(kr[q][u] >= mid);   // invalid keys are 0 < mid
+      const int n = block_count<NTR>(wc, scr, parity);
+      if (n >= top_k) {
+        lo = mid;
+        if (n <= RCAP) break;
+      } else {
+        hi = mid - 1;
+      }
+    }
+    thr = max(lo, 1u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = kr[q][u] >= thr;
+      const int slot = wave_alloc(ok, &ncand);
+      if (ok && slot < RCAP) fc[slot] = ((uint64_t)kr[q][u] << 32) | (uint32_t)(~((q * NTR + tid) * 8 + u));
+    }
+  __syncthreads();
+  const int nf = min(ncand, RCAP);
+  pad8(fc, nf);
+  __syncthreads();
+  float bv;
+  int bi;
+  rank_and_sample<1, NTR>(fc, fe, nf, top_k, top_p, seed, row, step, sh, red, rv, ri, bv, bi);
+  if (tid == 0) {
+    out_tok[row] = bi;
+    if (seen != nullptr) seen[base + bi] = 1;
+  }
+}
 }  // namespace
+
+// Rows at or above which the whole-row sampler form runs (V % 8 == 0, V <= 32K: 32 keys per
+// thread stay in registers, 64 spill; top_k <= 128);
+// tune key "sample_rowwide" (0 = never).
+static int g_sample_rowwide_min = 128;
+extern "C" void edge_sample_rowwide_min(int v) { g_sample_rowwide_min = v; }
 
 // Debug: enable/read the merge-phase timestamps (ticks of the 100 MHz wall clock).
 extern "C" int edge_sample_timestamps(int enable, unsigned long long* host_out16) {
@@ -584,6 +700,13 @@ extern "C" int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B
                                     top_k, top_p, rng, out_tok);
     else hipLaunchKernelGGL(topk_row_kernel<false>, dim3(B), dim3(NT), 0, st, logits, seen, V, inv_t, penalty, top_k,
                             top_p, rng, out_tok);
+  } else if (mode == 2 && g_sample_rowwide_min > 0 && B >= g_sample_rowwide_min && V % 8 == 0 && V <= 32768) {
+    const int ns = (V + NTR * 8 - 1) / (NTR * 8);
+#define RW(BF, N) hipLaunchKernelGGL((topk_rowwide_kernel<BF, N>), dim3(B), dim3(NTR), 0, st, logits, seen, V, inv_t, \
+                                     penalty, top_k, top_p, rng, out_tok)
+    if (is_bf16) { if (ns <= 2) RW(true, 2); else RW(true, 4); }
+    else { if (ns <= 2) RW(false, 2); else RW(false, 4); }
+#undef RW
   } else if (mode == 2) {
 #define TC(BF, E) hipLaunchKernelGGL((topk_chunk_kernel<BF, E>), g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, \
                                      penalty, top_k, pc, pthr)

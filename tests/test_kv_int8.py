@@ -71,7 +71,7 @@ def test_kv_int8_rejects_head_dim():
 
 
 # --------------------------------------------------------------------------- GPU kernels
-def _decode_case(dev, B, Hq, Hkv, D, S, lens, quant_out, seed=0):
+def _decode_case(dev, B, Hq, Hkv, D, S, lens, quant_out, seed=0, wave=False):
     g = torch.Generator().manual_seed(seed)
     qkv = (torch.randn(B, (Hq + 2 * Hkv) * D, generator=g)).to(torch.bfloat16)
     k = torch.randn(B, Hkv, S, D, generator=g)
@@ -84,22 +84,31 @@ def _decode_case(dev, B, Hq, Hkv, D, S, lens, quant_out, seed=0):
     args_cpu = [qkv, pos, rope, kq.clone(), vq.clone(), ks.clone(), vs.clone(), seq_lens]
     args_gpu = [t.to(dev) for t in args_cpu]
     ref = ops.decode_attention_fused_i8(*args_cpu, Hq, D ** -0.5, S, D, quant_out)
-    got = ops.decode_attention_fused_i8(*args_gpu, Hq, D ** -0.5, S, D, quant_out)
-    torch.cuda.synchronize()
+    # wave=True: enable the wave-per-(sequence, head) kernel (off by default; tune key
+    # attn8_wave_max = longest cache it takes) for this call only
+    if wave:
+        ops.ext().tune("attn8_wave_max", S, 0)
+    try:
+        got = ops.decode_attention_fused_i8(*args_gpu, Hq, D ** -0.5, S, D, quant_out)
+        torch.cuda.synchronize()
+    finally:
+        if wave:
+            ops.ext().tune("attn8_wave_max", 0, 0)
     return args_cpu, args_gpu, ref, got
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,Hq,Hkv,D,S,lens", [
-    (3, 4, 4, 128, 160, [160, 97, 1]),         # MHA (Llama-2-7B heads), one split
-    (2, 8, 2, 128, 3000, [3000, 1500]),        # GQA 4:1, split-K + combine
-    (2, 4, 1, 64, 700, [700, 65]),             # D = 64, GQA 4:1
-    (1, 2, 2, 256, 300, [300]),                # D = 256
-    (64, 32, 32, 128, 200, [200 - 3 * i for i in range(64)]),   # wave-per-head form (B*H >= 2048)
-    (128, 16, 16, 64, 90, [90 - (i % 89) for i in range(128)]),  # wave form, D = 64, lens down to 2
+@pytest.mark.parametrize("B,Hq,Hkv,D,S,lens,wave", [
+    (3, 4, 4, 128, 160, [160, 97, 1], False),         # MHA (Llama-2-7B heads), one split
+    (2, 8, 2, 128, 3000, [3000, 1500], False),        # GQA 4:1, split-K + combine
+    (2, 4, 1, 64, 700, [700, 65], False),             # D = 64, GQA 4:1
+    (1, 2, 2, 256, 300, [300], False),                # D = 256
+    (64, 32, 32, 128, 200, [200 - 3 * i for i in range(64)], False),   # workgroup form at B*H >= 2048
+    (64, 32, 32, 128, 200, [200 - 3 * i for i in range(64)], True),    # wave-per-head form
+    (128, 16, 16, 64, 90, [90 - (i % 89) for i in range(128)], True),  # wave form, D = 64, lens down to 2
 ])
-def test_decode_attn_i8_kernel_vs_ref(cuda, B, Hq, Hkv, D, S, lens):
-    cpu, gpu, ref, got = _decode_case(cuda, B, Hq, Hkv, D, S, lens, False)
+def test_decode_attn_i8_kernel_vs_ref(cuda, B, Hq, Hkv, D, S, lens, wave):
+    cpu, gpu, ref, got = _decode_case(cuda, B, Hq, Hkv, D, S, lens, False, wave=wave)
     out_r, out_g = ref[0].float(), got[0].float().cpu()
     err = (out_g - out_r).abs().max().item()
     assert err < 2e-2, err
@@ -117,6 +126,18 @@ def test_decode_attn_i8_quant_out(cuda):
     cpu, gpu, ref, got = _decode_case(cuda, 4, 8, 8, 128, 200, [200, 150, 90, 3], True, seed=1)
     deq_r = ref[0].float().view(4, -1, 64) * ref[1][:, :4].t().reshape(4, -1, 1)
     deq_g = got[0].float().cpu().view(4, -1, 64) * got[1][:, :4].cpu().t().reshape(4, -1, 1)
+    assert (deq_g - deq_r).abs().max() < 3e-2
+
+
+@pytest.mark.gpu
+def test_decode_attn_i8_quant_out_wave(cuda):
+    """The wave-per-(sequence, head) kernel's quantised-output branch (per-(token, 64) o input)."""
+    B = 64
+    lens = [200 - 3 * i for i in range(B)]
+    cpu, gpu, ref, got = _decode_case(cuda, B, 32, 32, 128, 200, lens, True, seed=2, wave=True)
+    G = ref[0].shape[1] // 64
+    deq_r = ref[0].float().view(B, G, 64) * ref[1][:, :B].t().reshape(B, G, 1)
+    deq_g = got[0].float().cpu().view(B, G, 64) * got[1][:, :B].cpu().t().reshape(B, G, 1)
     assert (deq_g - deq_r).abs().max() < 3e-2
 
 

@@ -222,13 +222,18 @@ def small_rows(C, dev, B, H, Hq, D):
 def sample_rows(C, dev):
     out = []
     rng = torch.tensor([1, 0], dtype=torch.int32, device=dev)
-    for B, V in ((16, 32000), (64, 32000), (16, 128256)):
+    for B, V in ((1, 32000), (16, 32000), (64, 32000), (128, 32000), (256, 32000), (16, 128256)):
         logits = (torch.randn(B, V, device=dev) * 3).bfloat16()
         seen = (torch.rand(B, V, device=dev) < 0.005).to(torch.uint8)
         for name, args in (("topk50_topp0.9", (0.7, 50, 0.9, 1.1, True)), ("greedy", (0.0, 0, 1.0, 1.1, False)),
                            ("full", (1.0, 0, 1.0, 1.0, True))):
             out.append(dict(op=f"sample_{name}", rows=B, V=V,
                             us=round(timeit(lambda: C.sample(logits, seen, *args, rng)), 2)))
+            if name.startswith("topk"):       # split vs whole-row form (tune key sample_rowwide)
+                for form, v in (("split", 0), ("rowwide", 1)):
+                    C.tune("sample_rowwide", v, 0)
+                    out[-1][f"{form}_us"] = round(timeit(lambda: C.sample(logits, seen, *args, rng)), 2)
+                C.tune("sample_rowwide", 128, 0)
             if name.startswith("topk"):       # merge-kernel phase split (100 MHz wall clock)
                 C.sample_timestamps(True)
                 C.sample(logits, seen, *args, rng)
