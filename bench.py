@@ -132,7 +132,8 @@ def run_single(args):
     if args.headinfer_heads is not None and args.headinfer_heads < cfg.num_kv_heads:
         from edgellm.offload import HeadInferKV
         kv = HeadInferKV(cfg, B, max_seq, args.headinfer_heads, device,
-                         chunk_size=max(1, min(args.prompt_len, args.prefill_chunk or args.prompt_len)))
+                         chunk_size=max(1, min(args.prompt_len, args.prefill_chunk or args.prompt_len)),
+                         kv_dtype=kv_dtype(args, cfg))
     L = max(1, args.lanes)
     if L > 1:
         assert kv is None, "HeadInfer offload runs one lane"
@@ -184,9 +185,9 @@ def run_single(args):
 
 
 def kv_dtype(args, cfg) -> str:
-    """The requested KV-cache dtype where the model and mode support it (int8 needs head_dim
-    64 / 128 / 256 and no HeadInfer offload)."""
-    if args.kv_dtype == "int8" and cfg.head_dim in (64, 128, 256) and args.headinfer_heads is None:
+    """The requested KV-cache dtype where the model supports it (int8 needs head_dim 64 / 128 /
+    256; with HeadInfer it applies to every tier: resident, host pool and staging)."""
+    if args.kv_dtype == "int8" and cfg.head_dim in (64, 128, 256):
         return "int8"
     return "bf16"
 

@@ -227,7 +227,7 @@ class Generator:
         if cuda:
             torch.cuda.synchronize()
         self._run = dict(B=B, plens=plens, sampling=sampling, t0=t0, t_prefill=time.perf_counter() - t0,
-                         produced=1, host_max=max(plens), events=[], cuda=cuda,
+                         prefill_logits=logits, produced=1, host_max=max(plens), events=[], cuda=cuda,
                          graphs_ok=self.use_graphs and cuda and self.graph_safe_for(B)
                          and not needs_host_sampler(sampling, V))
 
@@ -377,6 +377,47 @@ class LaneGenerator:
 
     def collect(self, eos_token_id: Optional[int] = None, stop_at_eos: bool = True) -> List[GenerationResult]:
         return [g.collect(eos_token_id, stop_at_eos) for g in self.lanes]
+
+
+@torch.no_grad()
+def co_generate(jobs: Sequence[tuple], eos_check_every: int = 8) -> List[GenerationResult]:
+    """Run several Generators that share one GPU CONCURRENTLY: ``jobs`` = [(generator, prompts,
+    sampling, seed, eos_token_id)].  Every generator gets its own HIP stream; the prefills run
+    one after another, each generator's decode graphs are captured up front (single host thread,
+    so no capture overlaps another stream's launches), then one host loop issues ``eos_check_every``
+    graph replays per generator round-robin — while the host waits on one generator's EOS flag the
+    others' queued steps keep the GPU busy, and their weight streams overlap each other's latency-
+    bound kernels.  This is how ensemble agents placed on the same device decode side by side
+    (orchestrator.ensemble) instead of one after another."""
+    if not jobs:
+        return []
+    gens = [j[0] for j in jobs]
+    cuda = gens[0].device.type == "cuda"
+    streams = [torch.cuda.Stream(g.device) for g in gens] if cuda else [None] * len(gens)
+    on = (lambda i: torch.cuda.stream(streams[i])) if cuda else (lambda i: _null_ctx())
+    for g, prompts, sp, seed, _ in jobs:
+        g.start(prompts, sp, seed)
+    if cuda:
+        cur = torch.cuda.current_stream()
+        for st in streams:
+            st.wait_stream(cur)
+    for i, (g, _, sp, _, _) in enumerate(jobs):
+        with on(i):
+            g.step(2)                      # eager warm-up step + first capture, then every bucket
+            g.precapture(sp.max_new_tokens)
+    active = list(range(len(jobs)))
+    while active:
+        for i in list(active):
+            g, _, sp, _, eos = jobs[i]
+            with on(i):
+                g.step(eos_check_every)
+                done = g._run["produced"] >= sp.max_new_tokens or (eos is not None and g.all_hit(eos))
+            if done:
+                active.remove(i)
+    if cuda:
+        for st in streams:
+            cur.wait_stream(st)
+    return [g.collect(j[4]) for g, j in zip(gens, jobs)]
 
 
 class _null_ctx:

@@ -82,7 +82,14 @@ class Attention(nn.Module):
         k_cache, v_cache = ctx.kv.layer(self.layer_idx)
         rot = cfg.rotary_dim if cfg.pos_emb == "rope" else 0
         if ctx.attn_hook is not None:
-            attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
+            # int8 offload (HeadInferKV kv_dtype="int8") hands decode output to a W8A8 o-proj as
+            # per-(token, 64) int8, like the resident int8 path
+            quant = ctx.mode == "decode" and getattr(ctx.attn_hook, "q8", False) and self.o.takes_quantized_input \
+                and cfg.head_dim % 64 == 0 and getattr(self.o, "group_scales_ok", lambda m: m <= 64)(ctx.B)
+            attn = ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot, quant) if quant else \
+                ctx.attn_hook.attention(self.layer_idx, qkv, ctx, self.scale, rot)
+            if isinstance(attn, QAct):
+                return self.o(attn)
         elif getattr(ctx.kv, "quantized", False):
             return self._forward_kv8(qkv, ctx, k_cache, v_cache, rot)
         elif ctx.mode == "decode":

@@ -2,9 +2,10 @@
 
 Reference flow (combine_model_fp_updated.py:188-221): Phi-2 answers, then Pythia-1B answers,
 then Llama-3.2-1B-Instruct "refines" both answers — strictly in series in one process.
-Here agents are independent engines on their own devices and run CONCURRENTLY (one host thread
-per agent; the decode loops are graph replays, so the GIL is not the bottleneck); the merge
-waits for all of them.  Merges:
+Here agents are independent engines and run CONCURRENTLY: agents on different devices in their
+own host threads (the decode loops are graph replays, so the GIL is not the bottleneck), agents
+sharing a GPU on their own HIP streams from one thread (``run_agents`` -> engine co_generate);
+the merge waits for all of them.  Merges:
   * ``RefineMerge`` — the reference's LLM refiner (prompt with every answer + optional gold
     reference, fixed sampling T=0.5, top-k 30, top-p 0.9, rep 1.1: combine_model_fp_updated.py:128-132)
   * ``VoteMerge``   — majority vote (north star): the answer most agents agree on (normalised
@@ -25,7 +26,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 import torch
 
 from ..config import REFINER_SAMPLING
-from ..engine.generate import GenerationResult, Generator, SamplingParams
+from ..engine.generate import GenerationResult, Generator, SamplingParams, co_generate
 from ..eval.text_metrics import rouge_scores
 from .prompts import qa_prompt, refine_prompt
 
@@ -56,10 +57,8 @@ class Agent:
         text = self.tokenizer.decode((ids + toks) if legacy_decode else toks, skip_special_tokens=True).strip()
         return text, res
 
-    def run_batch(self, prompt_texts: Sequence[str], seed: int, legacy_decode: bool = True,
-                  sampling: Optional[SamplingParams] = None):
-        """Decode several prompts together (one batched generate: per-sequence prefill, one
-        graph-replayed decode step for all rows).  Returns (texts, GenerationResult)."""
+    def encode_batch(self, prompt_texts: Sequence[str], sampling: Optional[SamplingParams] = None):
+        """Token ids of each prompt, left-truncated so prompt + max_new_tokens fits the cache."""
         sp = sampling or self.sampling
         max_seq = self.generator.max_seq
         ids_list = []
@@ -68,13 +67,82 @@ class Agent:
             if len(ids) + sp.max_new_tokens > max_seq:
                 ids = ids[-(max_seq - sp.max_new_tokens):]
             ids_list.append(ids)
+        return ids_list
+
+    def decode_batch(self, ids_list, res: GenerationResult, legacy_decode: bool = True) -> List[str]:
+        return [self.tokenizer.decode((ids + toks) if legacy_decode else toks, skip_special_tokens=True).strip()
+                for ids, toks in zip(ids_list, res.tokens)]
+
+    def run_batch(self, prompt_texts: Sequence[str], seed: int, legacy_decode: bool = True,
+                  sampling: Optional[SamplingParams] = None):
+        """Decode several prompts together (one batched generate: per-sequence prefill, one
+        graph-replayed decode step for all rows).  Returns (texts, GenerationResult)."""
+        sp = sampling or self.sampling
+        ids_list = self.encode_batch(prompt_texts, sp)
         eos = getattr(self.tokenizer, "eos_token_id", None)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         res = self.generator.generate(ids_list, sp, seed=seed, eos_token_id=eos)
-        texts = [self.tokenizer.decode((ids + toks) if legacy_decode else toks, skip_special_tokens=True).strip()
-                 for ids, toks in zip(ids_list, res.tokens)]
-        return texts, res
+        return self.decode_batch(ids_list, res, legacy_decode), res
+
+
+def run_agents(agents: Sequence[Agent], prompts: Sequence[Sequence[str]], seeds: Sequence[int],
+               legacy_decode: bool = True, concurrent: bool = True, single: bool = False) -> List[tuple]:
+    """Run agent i on ``prompts[i]`` (a batch of texts) with ``seeds[i]``; returns [(texts, result)].
+    Agents on DIFFERENT devices run in parallel host threads; agents sharing a GPU decode side by
+    side on their own HIP streams (engine.generate.co_generate) — not one after another.
+    ``single``: one prompt per agent through ``Agent.run`` (the batch-1 reference flow)."""
+    out: List[Optional[tuple]] = [None] * len(agents)
+    errors: List[BaseException] = []
+    units: List[List[int]] = []
+    shared: Dict[object, List[int]] = {}
+    for i, a in enumerate(agents):
+        dev = getattr(a, "device", None)
+        if concurrent and isinstance(dev, torch.device) and dev.type == "cuda":
+            if dev not in shared:
+                shared[dev] = []
+                units.append(shared[dev])
+            shared[dev].append(i)
+        else:
+            units.append([i])
+
+    def work(idx):
+        try:
+            dev = agents[idx[0]].device
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
+            if len(idx) > 1:
+                jobs, enc = [], []
+                for i in idx:
+                    a = agents[i]
+                    ids = a.encode_batch(prompts[i])
+                    enc.append(ids)
+                    jobs.append((a.generator, ids, a.sampling, seeds[i], getattr(a.tokenizer, "eos_token_id", None)))
+                for i, ids, res in zip(idx, enc, co_generate(jobs)):
+                    out[i] = (agents[i].decode_batch(ids, res, legacy_decode), res)
+            else:
+                for i in idx:
+                    if single:
+                        text, res = agents[i].run(prompts[i][0], seeds[i], legacy_decode)
+                        out[i] = ([text], res)
+                    else:
+                        out[i] = agents[i].run_batch(prompts[i], seeds[i], legacy_decode)
+        except BaseException as e:  # surfaced after join
+            errors.append(e)
+
+    devices = {getattr(a, "device", None) for a in agents}
+    if concurrent and len(units) > 1 and len(devices) > 1:
+        threads = [threading.Thread(target=work, args=(idx,)) for idx in units]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    else:
+        for idx in units:
+            work(idx)
+    if errors:
+        raise errors[0]
+    return out
 
 
 @dataclass
@@ -141,29 +209,11 @@ class Orchestrator:
 
     def answer(self, question: str, reference: Optional[str] = None, seed: int = 0) -> EnsembleResult:
         t0 = time.perf_counter()
-        answers: Dict[str, str] = {}
-        results: Dict[str, GenerationResult] = {}
-        errors: List[BaseException] = []
-
-        def work(i, agent):
-            try:
-                text, res = agent.run(qa_prompt(question, agent.cpu_prompt), seed + 1000 * i, self.legacy_decode)
-                answers[agent.name], results[agent.name] = text, res
-            except BaseException as e:  # surfaced after join
-                errors.append(e)
-
-        devices = {a.device for a in self.agents}
-        if self.concurrent and len(self.agents) > 1 and len(devices) > 1:
-            threads = [threading.Thread(target=work, args=(i, a)) for i, a in enumerate(self.agents)]
-            for t in threads:
-                t.start()
-            for t in threads:
-                t.join()
-        else:
-            for i, a in enumerate(self.agents):
-                work(i, a)
-        if errors:
-            raise errors[0]
+        outs = run_agents(self.agents, [[qa_prompt(question, a.cpu_prompt)] for a in self.agents],
+                          [seed + 1000 * i for i in range(len(self.agents))], self.legacy_decode, self.concurrent,
+                          single=True)
+        answers = {a.name: o[0][0] for a, o in zip(self.agents, outs)}
+        results = {a.name: o[1] for a, o in zip(self.agents, outs)}
         ordered = {a.name: answers[a.name] for a in self.agents}
         final, mres = self.merge(ordered, question, reference, seed)
         tps = {n: r.tps_generated() for n, r in results.items()}
@@ -183,28 +233,9 @@ class Orchestrator:
         per-stream rate, comparable with the reference's batch-1 TPS); the batch's aggregate
         throughput is ``sum(generated) / wall``."""
         t0 = time.perf_counter()
-        outs: Dict[str, tuple] = {}
-        errors: List[BaseException] = []
-
-        def work(i, agent):
-            try:
-                prompts = [qa_prompt(q, agent.cpu_prompt) for q in questions]
-                outs[agent.name] = agent.run_batch(prompts, seed + 1000 * i, self.legacy_decode)
-            except BaseException as e:  # surfaced after join
-                errors.append(e)
-
-        devices = {a.device for a in self.agents}
-        if self.concurrent and len(self.agents) > 1 and len(devices) > 1:
-            threads = [threading.Thread(target=work, args=(i, a)) for i, a in enumerate(self.agents)]
-            for t in threads:
-                t.start()
-            for t in threads:
-                t.join()
-        else:
-            for i, a in enumerate(self.agents):
-                work(i, a)
-        if errors:
-            raise errors[0]
+        res = run_agents(self.agents, [[qa_prompt(q, a.cpu_prompt) for q in questions] for a in self.agents],
+                         [seed + 1000 * i for i in range(len(self.agents))], self.legacy_decode, self.concurrent)
+        outs: Dict[str, tuple] = {a.name: o for a, o in zip(self.agents, res)}
         n = len(questions)
         answers = [{a.name: outs[a.name][0][j] for a in self.agents} for j in range(n)]
         per_tps = [{a.name: len(outs[a.name][1].tokens[j]) / max(outs[a.name][1].elapsed_s, 1e-9) for a in self.agents}

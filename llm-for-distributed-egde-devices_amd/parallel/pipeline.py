@@ -78,7 +78,7 @@ class PipelineStage:
         self.next = (rank + 1) % world
         self.h_on = headinfer_heads if offload else None
         self.prefill_chunk = max(1, prefill_chunk)
-        assert not offload or kv_dtype == "bf16", "HeadInfer offload keeps a bf16 KV cache"
+        self.kv_dtype = kv_dtype
         self.kv = None if offload else KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last,
                                                model.dtype, self.device, kv_dtype=kv_dtype)
         self.attn_hook = None
@@ -160,7 +160,8 @@ class PipelineStage:
             if self.cuda:
                 torch.cuda.empty_cache()
             self.kv = HeadInferKV(self.cfg, self.b * self.M, self.max_seq, self.h_on, self.device, self.first,
-                                  self.last, chunk_size=chunk, dtype=self.model.dtype, call_rows=self.b)
+                                  self.last, chunk_size=chunk, dtype=self.model.dtype, call_rows=self.b,
+                                  kv_dtype=self.kv_dtype)
         self.attn_hook = self.kv.attn_hook
 
     def _prefill(self, m: int, ids: Optional[torch.Tensor], T: int, hidden: Optional[torch.Tensor]):

@@ -99,3 +99,72 @@ def test_headinfer_long_context_matches_resident(cuda):
     assert got.tokens == ref.tokens
     assert kv.transports.get("dma", 0) > 0 and kv.transports.get("kernel", 0) > 0
     assert kv.host_bytes() > 0 and kv.gpu.nbytes() == kv.host_bytes()      # 1 of 2 heads resident
+
+
+# --------------------------------------------------------------------------- int8 offload
+def _run_q8(device, h_on, chunk_heads, chunk_size, quant="none", T=23, new=9, dtype=torch.float32, seed=9):
+    """int8 KV on every tier (HeadInferKV kv_dtype="int8") against the resident int8 cache."""
+    from edgellm.quant import quantize_model
+    cfg = tiny("llama", hidden_size=256, num_heads=8, num_kv_heads=4, intermediate_size=512, num_layers=2)
+    m = build_model(cfg, dtype=dtype, device=device, seed=seed)
+    if quant != "none":
+        m = quantize_model(m, quant)
+    prompts = [[(7 * i + 3 * b) % cfg.vocab_size for i in range(T)] for b in range(2)]
+    sp = SamplingParams(max_new_tokens=new, temperature=0.8, top_k=20, top_p=0.95, repetition_penalty=1.1)
+    ref = Generator(m, max_batch=2, max_seq=T + new + 8, use_graphs=False, prefill_chunk=chunk_size,
+                    kv_dtype="int8").generate(prompts, sp, seed=4)
+    kv = HeadInferKV(cfg, 2, T + new + 8, h_on=h_on, device=device, chunk_heads=chunk_heads, chunk_size=chunk_size,
+                     dtype=dtype, kv_dtype="int8")
+    got = Generator(m, max_batch=2, max_seq=T + new + 8, kv=kv).generate(prompts, sp, seed=4)
+    return ref, got, kv
+
+
+@pytest.mark.parametrize("h_on,chunk_heads,chunk_size", [(1, 1, 8), (0, 2, 64), (2, 1, 5), (3, None, 16)])
+def test_headinfer_int8_matches_resident_int8_cpu(h_on, chunk_heads, chunk_size):
+    ref, got, kv = _run_q8("cpu", h_on, chunk_heads, chunk_size)
+    assert got.tokens == ref.tokens
+    assert kv.host_k.dtype == torch.int8 and kv.host_ks.dtype == torch.float32
+    # PCIe bytes per (token, head): D + 4 (int8 row + fp32 scale), not 2 D
+    assert kv.bytes_d2h > 0 and kv.bytes_h2d > 0
+    assert kv.host_bytes() == 2 * kv.host_k.numel() + 2 * 4 * kv.host_ks.numel()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h_on,chunk_heads,chunk_size", [(1, 1, 8), (0, 2, 64), (2, None, 16)])
+def test_headinfer_int8_matches_resident_int8_gpu(cuda, h_on, chunk_heads, chunk_size):
+    ref, got, kv = _run_q8(cuda, h_on, chunk_heads, chunk_size, quant="w8a8", dtype=torch.bfloat16)
+    assert got.tokens == ref.tokens
+    assert kv.host_k.is_pinned() and kv.host_ks.is_pinned()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kv_dtype", ["bf16", "int8"])
+def test_headinfer_w8a8_long_context_logits_vs_resident(cuda, kv_dtype):
+    """W8A8 model, 4.5K-token prompt prefilled in 1K chunks, 3 of 4 KV heads per layer offloaded
+    (int8 or bf16 on every tier): the last prefill chunk's logits stay within tolerance of the same
+    model over a fully resident cache of the same dtype, and 8 greedy decode tokens agree."""
+    from edgellm.quant import quantize_model
+    cfg = tiny("llama2", hidden_size=512, num_heads=4, num_kv_heads=4, num_layers=2, intermediate_size=1024,
+               max_position_embeddings=8192)
+    m = quantize_model(build_model(cfg, device=cuda, seed=5), "w8a8_smoothquant")
+    T, new, chunk = 4500, 8, 1024
+    g = torch.Generator().manual_seed(1)
+    prompt = [torch.randint(0, cfg.vocab_size, (T,), generator=g).tolist()]
+    sp = SamplingParams(max_new_tokens=new, do_sample=False)
+    S = T + new + 8
+    res = Generator(m, max_batch=1, max_seq=S, use_graphs=False, prefill_chunk=chunk, kv_dtype=kv_dtype)
+    kv = HeadInferKV(cfg, 1, S, h_on=1, device=cuda, chunk_size=chunk, kv_dtype=kv_dtype)
+    off = Generator(m, max_batch=1, max_seq=S, kv=kv)
+    logits = []
+    for gen in (res, off):
+        gen.start(prompt, sp, seed=0)
+        row = [gen._run["prefill_logits"].float().cpu()]
+        gen.step(new - 1, record_latency=False)
+        logits.append((gen.collect().tokens, row))
+    (t_res, l_res), (t_off, l_off) = logits
+    assert t_off == t_res
+    for a, b in zip(l_off, l_res):
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < 2e-2, rel
+    if kv_dtype == "int8":
+        assert kv.bytes_h2d > 0 and kv.host_k.dtype == torch.int8

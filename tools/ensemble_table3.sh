@@ -21,3 +21,8 @@ run combo_base_b16     $C --config configs/ensemble.yaml $D --num_samples 64 --b
 run combo_llmint8_b1   $C --config configs/ensemble_int8.yaml $D --num_samples 12
 run combo_w8a8_b16     $C --config configs/ensemble.yaml $D --num_samples 64 --batch_size 16 --quant w8a8_smoothquant
 run north_star_vote    $C --config configs/north_star.yaml $D --num_samples 32 --batch_size 16
+# agents sharing the GPU decode side by side on their own streams (orchestrator run_agents ->
+# engine co_generate), 128 questions per batch
+run north_star_vote_b128 $C --config configs/north_star.yaml $D --num_samples 256 --batch_size 128
+run combo_base_b128    $C --config configs/ensemble.yaml $D --num_samples 256 --batch_size 128
+run combo_w8a8_b128    $C --config configs/ensemble.yaml $D --num_samples 256 --batch_size 128 --quant w8a8_smoothquant
