@@ -35,7 +35,7 @@ import edgellm  # noqa: E402,F401
 from edgellm.engine import Generator, SamplingParams  # noqa: E402
 from edgellm.engine.generate import LaneGenerator  # noqa: E402
 from edgellm.models import build_model, get_config, tiny  # noqa: E402
-from edgellm.quant import quantize_model, synthetic_calibration  # noqa: E402
+from edgellm.quant import quantize_head, quantize_model, synthetic_calibration  # noqa: E402
 from edgellm.quant.smoothquant import smoothquant_stage  # noqa: E402
 from edgellm.utils.tracing import MetricsWriter, trace_range  # noqa: E402
 
@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"],
                     help="KV cache: bf16 (default) or int8 with per-(token, head) scales (half the KV bytes: 1.6x faster attention at >= 512 keys, neutral at the 128-token bench context)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--lm-head", default="bf16", choices=["bf16", "int8"],
+                    help="int8: W8A8 LM head (per-channel weights, per-token activations); default bf16 "
+                         "like the reference")
     ap.add_argument("--force-pipeline", action="store_true",
                     help="N = 1: time the RCCL PipelineStage engine (world-1 process group, device bound) "
                          "instead of the Generator, same config")
@@ -105,6 +108,8 @@ def build(args, device, first=0, last=None):
         model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=args.seed)
         if args.quant != "none":
             model = quantize_model(model, args.quant)
+    if getattr(args, "lm_head", "bf16") == "int8" and model.has_head:
+        model = quantize_head(model)
     if device.type == "cuda":
         torch.cuda.empty_cache()
         torch.cuda.synchronize()
@@ -305,8 +310,9 @@ def main(argv=None):
                    "headinfer_heads": args.headinfer_heads,
                    "kv_cache": ("int8, one fp32 scale per (token, head)" if kv_dtype(args, model_config(args)) == "int8"
                                 else "bf16"),
-                   "compute": ("W8A8 INT8 MFMA GEMMs, bf16 norms / softmax, bf16 LM head" if args.quant != "none"
-                               else "bf16 GEMMs / attention / norms")},
+                   "compute": ("W8A8 INT8 MFMA GEMMs, bf16 norms / softmax, "
+                               + ("W8A8 int8 LM head" if args.lm_head == "int8" else "bf16 LM head")
+                               if args.quant != "none" else "bf16 GEMMs / attention / norms")},
         "p50_token_latency_ms": round(res["p50"], 4),
         "p90_token_latency_ms": round(res.get("p90", res["p50"]), 4),
         "max_token_latency_ms": round(res.get("lat_max", res["p50"]), 4),

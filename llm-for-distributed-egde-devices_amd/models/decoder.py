@@ -288,7 +288,8 @@ class DecoderLM(nn.Module):
             idx = ctx.last_rows(x.device)
             x = x.index_select(0, idx)
             residual = residual.index_select(0, idx) if residual is not None else None
-        h, _ = self.final_norm(x, residual)
+        qh = getattr(self.lm_head, "takes_quantized_input", False)     # int8 LM head (quant.quantize_head)
+        h, _ = self.final_norm(x, residual, quant=qh)
         return self.lm_head(h) if self.lm_head is not None else self._tied_head(h)
 
     def _tied_head(self, h: torch.Tensor) -> torch.Tensor:

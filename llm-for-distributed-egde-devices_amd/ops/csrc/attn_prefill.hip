@@ -28,6 +28,10 @@ __device__ __forceinline__ v4f mfma_bf16(const v8s& a, const v8s& b, const v4f& 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ void glds16_fa(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
 template <int D>
 struct Geo {
   static constexpr int DP = (D + 31) / 32 * 32;       // reduction-padded head dim
@@ -222,7 +226,214 @@ __global__ void __launch_bounds__(NT) prefill_attn_kernel(
     }
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// fa_kernel: the D = 64 / 128 flash-attention forward (Llama-2 / -3 / -3.2 / Mistral heads), rebuilt for
+// CDNA4 around three choices the 16-row kernel above lacks:
+//  * 256 query rows per workgroup, 8 waves x 32 rows on v_mfma_f32_32x32x16_bf16, computed
+//    TRANSPOSED: S^T = K Q^T (A = K rows from LDS by ds_read_b128, B = Q^T resident in VGPRs) puts
+//    one query per lane (32 of the 64 keys of a tile in the lane, the other 32 in lane ^ 32), so
+//    the row max / sum are in-lane reductions plus ONE cross-half shuffle, the rescale of O is a
+//    per-lane multiply, and the S^T accumulator converts to the B operand (P^T) of O^T = V^T P^T
+//    in place — no P round trip through LDS.  V^T comes from the row-major V tile by
+//    ds_read_b64_tr_b16 (the key order inside a 16-key step is permuted identically on both
+//    operands, which leaves the sum unchanged).
+//  * K/V tiles (64 keys, 8 / 16 KiB each) move global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//    no VGPR staging) into a 3-slot ring: tile t + 2 is issued right after the one barrier of
+//    tile t, which also retires tile t - 1's slot — one s_barrier per tile, two tiles in flight.
+//  * XOR-swizzled 16-byte chunks (slot = chunk ^ f(key)) chosen so both the K reads (16 keys x
+//    one chunk per lane group) and the transposed V reads (4 keys x 4 chunks) are conflict-free;
+//    the DMA realises the swizzle by choosing each lane's global source address.
+// Causal tiles above a wave's last query are skipped by that wave (it still joins the barrier);
+// workgroups are dispatched longest-first.  Keys past the cache end are clamped to a valid row
+// and masked, so a tile never reads outside the cache.
+constexpr int FA_W = 8, FA_NT = FA_W * 64, FA_QT = FA_W * 32, FA_KT = 64, FA_RING = 3;
+template <int D>
+struct FaGeo {
+  static constexpr int ROWB = D * 2;                     // bytes per key row
+  static constexpr int CH = D / 8;                       // 16-byte chunks per row
+  static constexpr int KK = D / 16;                      // S^T k-steps
+  static constexpr int DB = D / 32;                      // O^T 32-row blocks
+  static constexpr int TILE = FA_KT * ROWB;              // one K (or V) tile
+  static constexpr int SLOT = 2 * TILE;
+  static constexpr int LDS = FA_RING * SLOT;             // 96 KiB (D 128) / 48 KiB (D 64)
+  static constexpr int RPP = 1024 / ROWB;                // key rows per 1 KiB DMA piece
+  static constexpr int PIECES = TILE / 1024;             // per K (or V) tile
+  static constexpr int PPW = 2 * PIECES / FA_W;          // pieces per wave per tile
+  // chunk swizzle: K reads (16 keys, one chunk) and transposed V reads (4 keys x 4 chunks) hit
+  // distinct banks.  D 128: one row = all 64 banks, 16 chunks; D 64: two rows per bank window
+  __device__ static __forceinline__ int swz(int kr) {
+    if constexpr (D == 128) return ((kr & 3) << 2) | ((kr >> 2) & 3);
+    else { const int v = (kr >> 1) & 7; return ((v & 1) << 2) | (v >> 1); }
+  }
+};
+
+__device__ __forceinline__ v16f mfma32_bf16(const v8s& a, const v8s& b, const v16f& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc, int64_t c_sb,
+    int64_t c_sh, const int* __restrict__ start_pos, bf16_t* __restrict__ out, int T, int Hq, int Hkv,
+    float scale_log2) {
+  using G = FaGeo<D>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int qtile = gridDim.x - 1 - blockIdx.x;                // longest (causal) first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kvh = h / (Hq / Hkv);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ql = lane & 31, hf = lane >> 5;                    // query column / half of the wave
+  const int s0 = start_pos[b];
+  const int nkeys = s0 + T;
+  const int q0 = qtile * FA_QT;
+  const int wq0 = q0 + wave * 32;
+  const int tq = wq0 + ql;                                     // this lane's query row (within T)
+  const int qpos = s0 + tq;
+  const int last_q = min(q0 + FA_QT, T) - 1;
+  const int kend = CAUSAL ? min(nkeys, s0 + last_q + 1) : nkeys;
+  const int ntiles = (kend + FA_KT - 1) / FA_KT;
+  const bf16_t* kbase = kc + b * c_sb + kvh * c_sh;
+  const bf16_t* vbase = vc + b * c_sb + kvh * c_sh;
+
+  // ---- Q^T fragments (B operand): lane <- Q[tq][16 kk + 8 hf .. +8]
+  v8s qf[G::KK];
+#pragma unroll
+  for (int kk = 0; kk < G::KK; ++kk)
+    qf[kk] = tq < T ? *reinterpret_cast<const v8s*>(q + (((size_t)b * T + tq) * Hq + h) * D + kk * 16 + hf * 8)
+                    : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+
+  // ---- LDS-DMA of tile t into ring slot t % 3: 1 KiB pieces of RPP key rows, PPW per wave
+  auto issue = [&](int t) {
+    char* slot = smem + (t % FA_RING) * G::SLOT;
+#pragma unroll
+    for (int j = 0; j < G::PPW; ++j) {
+      const int p = wave * G::PPW + j;                         // [0, PIECES) K, then V
+      const bool isv = p >= G::PIECES;
+      const int pp = isv ? p - G::PIECES : p;
+      const int kr = pp * G::RPP + lane / G::CH;               // tile-relative key row
+      const int key = min(t * FA_KT + kr, kend - 1);
+      const int ch = (lane % G::CH) ^ G::swz(kr);              // source chunk for this LDS slot
+      const bf16_t* src = (isv ? vbase : kbase) + (size_t)key * D + ch * 8;
+      glds16_fa(src, slot + (isv ? G::TILE : 0) + pp * 1024);
+    }
+  };
+
+  v16f o[G::DB];
+#pragma unroll
+  for (int i = 0; i < G::DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;
+
+  if (ntiles > 0) issue(0);
+  if (ntiles > 1) issue(1);
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                              // tile t landed; slot of t - 1 free
+    if (t + 2 < ntiles) issue(t + 2);
+    const int k0 = t * FA_KT;
+    if (wq0 >= T || (CAUSAL && k0 > s0 + wq0 + 31)) continue;  // nothing visible for this wave
+    const char* kl = smem + (t % FA_RING) * G::SLOT;
+    const char* vl = kl + G::TILE;
+
+    // ---- S^T = K Q^T for the two 32-key blocks
+    v16f sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+      const int kr = kb * 32 + ql;
+#pragma unroll
+      for (int kk = 0; kk < G::KK; ++kk) {
+        const v8s kf = *reinterpret_cast<const v8s*>(kl + kr * G::ROWB + (((2 * kk + hf) ^ G::swz(kr)) << 4));
+        sacc[kb] = mfma32_bf16(kf, qf[kk], sacc[kb]);
+      }
+      asm volatile("" ::: "memory");                           // K fragments: one 32-key block in flight
+    }
+    // ---- scale, mask, online softmax (one query per lane)
+    const bool full = (k0 + FA_KT <= kend) && (!CAUSAL || k0 + FA_KT - 1 <= s0 + wq0);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = sacc[kb][r] * scale_log2;
+        if (!full) {
+          const int key = k0 + kb * 32 + 8 * (r >> 2) + 4 * hf + (r & 3);
+          if (key >= kend || (CAUSAL && key > qpos)) v = -INFINITY;
+        }
+        sacc[kb][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m_i, mx);
+    const float msafe = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = exp2f(m_i - msafe);
+    float rs = 0.f;
+    v8s pb[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pv = exp2f(sacc[kb][8 * ks + j] - msafe);
+          rs += pv;
+          pb[kb][ks][j] = (short)f2bf(pv);
+        }
+    rs += __shfl_xor(rs, 32, 64);
+    l_i = l_i * alpha + rs;
+    m_i = mnew;
+#pragma unroll
+    for (int i = 0; i < G::DB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+
+    // ---- O^T += V^T P^T: per 16-key step, lane group g reads keys {4 hf .. +3} and {8 + 4 hf .. +3}
+    const int c16 = lane & 15, qq = c16 >> 2, pq = c16 & 3, g2 = (lane >> 4) & 1;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kr1 = kb * 32 + ks * 16 + 4 * hf + qq, kr2 = kr1 + 8;
+#pragma unroll
+        for (int db = 0; db < G::DB; ++db) {
+          const int d0 = db * 32 + g2 * 16 + 4 * pq;
+          const char* a1 = vl + kr1 * G::ROWB + (((d0 >> 3) ^ G::swz(kr1)) << 4) + (d0 & 7) * 2;
+          const char* a2 = vl + kr2 * G::ROWB + (((d0 >> 3) ^ G::swz(kr2)) << 4) + (d0 & 7) * 2;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
+          const v8s vf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[db] = mfma32_bf16(vf, pb[kb][ks], o[db]);
+        }
+        // bound the V fragments the compiler keeps in flight to one 16-key step (register budget:
+        // 2 waves / SIMD = 256 VGPRs, and a spill would join this kernel's counted vmcnt)
+        asm volatile("" ::: "memory");
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // no DMA outlives the workgroup
+
+  // ---- epilogue: lane holds O^T[d = 32 db + 8 j + 4 hf + 0..3][tq]
+  if (tq < T) {
+    const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    bf16_t* orow = out + (((size_t)b * T + tq) * Hq + h) * D;
+#pragma unroll
+    for (int db = 0; db < G::DB; ++db)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 w;
+        w.x = pack_bf2(o[db][4 * j] * inv, o[db][4 * j + 1] * inv);
+        w.y = pack_bf2(o[db][4 * j + 2] * inv, o[db][4 * j + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * j + 4 * hf) = w;
+      }
+  }
+}
 }  // namespace
+
+static int g_prefill_fa = 1;           // tune key "prefill_fa": 0 = the 16-row kernel for D = 64 / 128 too
+extern "C" void edge_prefill_fa(int v) { g_prefill_fa = v; }
 
 extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
                                  const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
@@ -230,6 +441,32 @@ extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void*
   if (B * T == 0) return 0;
   if (Hq % Hkv) return -2;
   const float sl2 = scale * 1.4426950408889634f;
+  if ((D == 128 || D == 64) && g_prefill_fa) {
+#define FA(DD)                                                                                                     \
+  do {                                                                                                             \
+    static bool fa_attr = false;                                                                                   \
+    if (!fa_attr) {                                                                                                \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, true>, hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                FaGeo<DD>::LDS);                                                                   \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                FaGeo<DD>::LDS);                                                                   \
+      fa_attr = true;                                                                                              \
+    }                                                                                                              \
+    const dim3 g((T + FA_QT - 1) / FA_QT, Hq, B);                                                                  \
+    if (causal)                                                                                                    \
+      hipLaunchKernelGGL((fa_kernel<DD, true>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, (const bf16_t*)q,              \
+                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \
+                         Hkv, sl2);                                                                                \
+    else                                                                                                           \
+      hipLaunchKernelGGL((fa_kernel<DD, false>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, (const bf16_t*)q,             \
+                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \
+                         Hkv, sl2);                                                                                \
+  } while (0)
+    if (D == 128) FA(128);
+    else FA(64);
+#undef FA
+    return (int)hipGetLastError();
+  }
   const dim3 grid((T + QT - 1) / QT, Hq, B);
 #define PL(DD)                                                                                                    \
   do {                                                                                                            \

@@ -56,9 +56,11 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     cfg = model_config(args)
     wbytes = 1.0 if args.quant != "none" else 2.0
     explicit = args.partition if "," in args.partition else None
-    # decode-time cost model: LM head + sampler ~0.6 of a W8A8 decoder layer (0.4 of a bf16 one),
-    # measured on MI355X at 64 rows per lane (parallel/partition.py::layer_costs)
-    hcl = 0.6 if args.quant != "none" else 0.4
+    # decode-time cost model, LM head + final norm + sampler in decoder-layer units, measured on
+    # MI355X at 256 rows (profiles/rocprof_bench_default_r3_kernel_stats.csv: layer ~227 us; bf16
+    # head GEMM 82 us + sampler 25 us + norm/embed ~10 us) -> 0.52; int8 head ~0.35 (estimate,
+    # parallel/partition.py::layer_costs); bf16 models 0.4
+    hcl = (0.35 if getattr(args, "lm_head", "bf16") == "int8" else 0.52) if args.quant != "none" else 0.4
     bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
                              weight_bytes=wbytes, explicit=explicit, head_cost_layers=hcl)
     wd.beat("build")

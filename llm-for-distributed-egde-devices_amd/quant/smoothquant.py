@@ -166,6 +166,19 @@ def quantize_model(model: DecoderLM, mode: str, calib_ids: Optional[torch.Tensor
 
 
 @torch.no_grad()
+def quantize_head(model: DecoderLM) -> DecoderLM:
+    """Optional W8A8 LM head (per-output-channel int8 weights, per-token int8 activations fused
+    into the final norm): halves the head's 2 V H bytes, the largest single GEMM of a decode step
+    (262 MB bf16 at Llama-2-7B), which is what the pipeline's last stage carries on top of its
+    layers.  Off by default — the reference, like bitsandbytes and SmoothQuant, keeps the head in
+    16 bits.  Untied heads only (a tied head shares the embedding matrix)."""
+    if model.lm_head is not None and not isinstance(model.lm_head, W8A8Linear):
+        model.lm_head = W8A8Linear.from_float(model.lm_head, None)
+        model.head_quant = "w8a8"
+    return model
+
+
+@torch.no_grad()
 def smoothquant_stage(full: DecoderLM, first: int, last: int, calib_ids: torch.Tensor, alpha: float = 0.5,
                       device=None) -> DecoderLM:
     """Calibrate + smooth the FULL model once, then cut layers [first, last) into a W8A8 stage.

@@ -1,11 +1,16 @@
 """Request-serving engine: a queue of generation requests batched onto one Generator.
 
 The reference serves only a time string (Code/gRPC/server.py, 10 worker threads, stateless).
-Here concurrent clients (REST ``POST /generate`` or in-process callers) enqueue requests; one
-worker thread drains the queue, groups requests with identical sampling settings into batches
-of up to ``max_batch`` (the fused sampler takes one configuration per launch) and runs them
-through the graph-captured decode loop.  Counters and per-token latency percentiles are exposed
-through ``metrics()``.
+Here concurrent clients (REST ``POST /generate`` or in-process callers) enqueue requests and one
+worker thread serves them, in one of two modes:
+  * ``continuous=True`` (default): iteration-level batching (engine.continuous.SlotDecoder) — a
+    request is admitted into a free cache slot between decode steps, every step advances all
+    occupied slots, a finished request frees its slot at once.  One sampling configuration per
+    session (the fused sampler takes one per launch); a request needing another configuration
+    waits until the running session drains.
+  * ``continuous=False``: static batches — requests with identical sampling settings are grouped
+    into batches of up to ``max_batch`` and each batch runs to completion.
+Counters and per-token latency percentiles are exposed through ``metrics()``.
 """
 from __future__ import annotations
 
@@ -16,13 +21,14 @@ import time
 from concurrent.futures import Future
 from typing import Dict, List, Optional
 
+from ..engine.continuous import SlotDecoder
 from ..engine.generate import Generator, SamplingParams
 from ..utils.tracing import LatencyHistogram, MetricsWriter, trace_range
 
 
 class ServingEngine:
     def __init__(self, generator: Generator, tokenizer, max_batch: int = 8, batch_wait_s: float = 0.005,
-                 metrics_path: Optional[str] = None):
+                 metrics_path: Optional[str] = None, continuous: Optional[bool] = None, steps_per_poll: int = 4):
         self.gen, self.tok = generator, tokenizer
         # one JSONL record per served batch (EDGELLM_METRICS=<path> or metrics_path)
         self.writer = MetricsWriter(metrics_path or os.environ.get("EDGELLM_METRICS"))
@@ -30,9 +36,13 @@ class ServingEngine:
         self.batch_wait_s = batch_wait_s
         self.q: "queue.Queue[tuple]" = queue.Queue()
         self.lat = LatencyHistogram()
-        self.stats = {"requests": 0, "batches": 0, "generated_tokens": 0, "errors": 0}
+        self.stats = {"requests": 0, "batches": 0, "generated_tokens": 0, "errors": 0, "sessions": 0,
+                      "decode_steps": 0, "max_concurrent": 0}
+        # continuous batching needs per-row cache lengths: not with a HeadInfer-offloaded cache
+        self.continuous = (generator.attn_hook is None) if continuous is None else continuous
+        self.steps_per_poll = max(1, steps_per_poll)
         self._stop = threading.Event()
-        self._worker = threading.Thread(target=self._loop, daemon=True)
+        self._worker = threading.Thread(target=self._loop_continuous if self.continuous else self._loop, daemon=True)
         self._worker.start()
 
     # ------------------------------------------------------------------ API
@@ -57,7 +67,75 @@ class ServingEngine:
         self.q.put(None)
         self._worker.join(timeout=10)
 
-    # ------------------------------------------------------------------ worker
+    # ------------------------------------------------------------------ continuous worker
+    def _loop_continuous(self):
+        pending: List[tuple] = []
+        dec: Optional[SlotDecoder] = None
+        eos = getattr(self.tok, "eos_token_id", None)
+        while True:
+            stop = self._stop.is_set()
+            try:                                   # block only when there is nothing to decode
+                item = self.q.get(timeout=0.1) if (not pending and (dec is None or not dec.busy())) \
+                    and not stop else self.q.get_nowait()
+                if item is None:
+                    self._stop.set()
+                else:
+                    pending.append(item)
+                while True:
+                    item = self.q.get_nowait()
+                    if item is None:
+                        self._stop.set()
+                    else:
+                        pending.append(item)
+            except queue.Empty:
+                pass
+            if self._stop.is_set() and not pending and (dec is None or not dec.busy()):
+                break
+            try:
+                if dec is not None and not dec.busy() and (not pending or pending[0][1].key() != dec.sp.key()
+                                                           or dec.col * 2 > dec.width):
+                    dec = None                     # session drained: the queue head picks the next one
+                if dec is None and pending:
+                    dec = SlotDecoder(self.gen, pending[0][1], seed=pending[0][2])
+                    self.stats["sessions"] += 1
+                if dec is None:
+                    continue
+                # admit every waiting request of this session's sampling configuration that fits
+                keep = []
+                for it in pending:
+                    ids, sp, _, fut, t_sub = it
+                    if sp.key() == dec.sp.key() and dec.can_admit(len(ids), sp.max_new_tokens):
+                        dec.admit(ids, sp.max_new_tokens, eos, tag=it)
+                    else:
+                        keep.append(it)
+                pending = keep
+                occ = sum(s is not None for s in dec.slots)
+                self.stats["max_concurrent"] = max(self.stats["max_concurrent"], occ)
+                n = dec.step(self.steps_per_poll)
+                self.stats["decode_steps"] += n
+                for it, res in dec.poll():
+                    self._finish(it, res, occ)
+            except Exception as e:  # fail the requests in flight, keep serving
+                self.stats["errors"] += 1
+                for s in (dec.slots if dec is not None else []):
+                    if s is not None and not s.tag[3].done():
+                        s.tag[3].set_exception(e)
+                dec = None
+
+    def _finish(self, it: tuple, res, occ: int):
+        toks = res.tokens[0]
+        self.stats["requests"] += 1
+        self.stats["generated_tokens"] += len(toks)
+        if len(toks) > 1 and res.decode_s > 0:
+            self.lat.extend([res.decode_s * 1e3 / (len(toks) - 1)])
+        self.writer.write(event="request", mode="continuous", prompt_tokens=len(it[0]), generated_tokens=len(toks),
+                          ttft_ms=res.prefill_s * 1e3, elapsed_s=res.elapsed_s, slots_busy=occ,
+                          queue_ms=(time.perf_counter() - it[4]) * 1e3)
+        it[3].set_result({"tokens": toks, "text": self.tok.decode(toks, skip_special_tokens=True),
+                          "tokens_per_s": len(toks) / res.elapsed_s if res.elapsed_s > 0 else 0.0,
+                          "queue_ms": (time.perf_counter() - it[4]) * 1e3, "batch_size": occ})
+
+    # ------------------------------------------------------------------ static-batch worker
     def _loop(self):
         pending: List[tuple] = []
         while not self._stop.is_set():

@@ -132,6 +132,31 @@ def test_prefill_attention(cuda, Hq, Hkv, D, T, starts):
     _close(out, ref, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("Hq,Hkv,T,starts", [(8, 2, 600, (0, 300)), (4, 4, 1100, (0,)), (8, 8, 257, (0, 64)),
+                                            (4, 1, 40, (1000, 3))])
+def test_prefill_attention_fa128(cuda, causal, Hq, Hkv, T, starts):
+    """The D = 128 LDS-DMA ring kernel (fa128) over many key tiles (ring wrap), partial query
+    tiles, chunked prefill offsets, GQA, against the fp32 reference and the 16-row kernel."""
+    C = ops.ext()
+    D, B = 128, len(starts)
+    S = max(starts) + T + 3
+    q = torch.randn(B, T, Hq, D, device=cuda).bfloat16()
+    kc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    vc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    sp = torch.tensor(starts, device=cuda, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = _ref.prefill_attention(q, kc, vc, sp, scale, causal)
+    out = C.prefill_attn(q, kc, vc, sp, scale, causal)
+    _close(out, ref, 2e-2, 2e-2)
+    C.tune("prefill_fa", 0, 0)
+    try:
+        old = C.prefill_attn(q, kc, vc, sp, scale, causal)
+    finally:
+        C.tune("prefill_fa", 1, 0)
+    _close(out, old, 2e-2, 2e-2)
+
+
 def test_prefill_attention_noncausal(cuda):
     C = ops.ext()
     q = torch.randn(2, 70, 4, 64, device=cuda).bfloat16()

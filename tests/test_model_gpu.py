@@ -123,3 +123,25 @@ def test_w8a8_decode_beyond_gemv_rows(cuda, B):
     big = Generator(model, max_batch=B, max_seq=32).generate(prompts, sp, seed=0).tokens
     assert len(big) == B and all(len(t) == 6 for t in big)
     _rows_match_small_batch(model, prompts, B, cuda)
+
+
+@pytest.mark.parametrize("B", [4, 256])
+def test_int8_lm_head_close_to_bf16(cuda, B):
+    """quantize_head: W8A8 LM head (final norm emits int8 + scales, 16-blocked int8 GEMM) against
+    the bf16 head of the same W8A8 model: decode logits within 3 % relative, top-1 mostly equal."""
+    from edgellm.quant import quantize_head
+    cfg = tiny("llama2", hidden_size=512, num_heads=4, num_kv_heads=4, intermediate_size=1024, num_layers=2,
+               vocab_size=4096)
+    base = quantize_model(build_model(cfg, device=cuda, seed=4), "w8a8")
+    q8 = quantize_head(copy.deepcopy(base))
+    assert q8.lm_head.takes_quantized_input
+    ids = torch.randint(0, cfg.vocab_size, (B, 9), generator=torch.Generator().manual_seed(2)).to(cuda)
+    outs = []
+    for m in (base, q8):
+        g = Generator(m, max_batch=B, max_seq=32)
+        g.prefill(ids[:, :8])
+        outs.append(g.prefill(ids[:, 8:], 0, 8).float())
+    a, b = outs
+    rel = ((b - a).norm() / a.norm()).item()
+    assert rel < 3e-2, rel
+    assert (a.argmax(-1) == b.argmax(-1)).float().mean() > 0.9

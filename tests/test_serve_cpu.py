@@ -97,7 +97,7 @@ def test_serving_engine_batches_concurrent_requests(tmp_path):
     m = build_model(cfg, dtype=torch.float32, seed=2)
     mpath = tmp_path / "serve_metrics.jsonl"
     eng = ServingEngine(Generator(m, max_batch=4, max_seq=128), ByteTokenizer(cfg.vocab_size), max_batch=4,
-                        batch_wait_s=0.05, metrics_path=str(mpath))
+                        batch_wait_s=0.05, metrics_path=str(mpath), continuous=False)
     try:
         sp = SamplingParams(max_new_tokens=5, do_sample=False)
         futs = [eng.submit([1, 2, 3 + i], sp) for i in range(4)]
@@ -114,6 +114,40 @@ def test_serving_engine_batches_concurrent_requests(tmp_path):
         recs = [json.loads(l) for l in mpath.read_text().splitlines()]     # one JSONL record per batch
         assert len(recs) == eng.metrics()["batches"] and sum(r["batch_size"] for r in recs) == 5
         assert all(r["event"] == "batch" and r["ttft_ms"] > 0 and r["generated_tokens"] > 0 for r in recs)
+    finally:
+        eng.close()
+
+
+def test_serving_engine_continuous_batching(tmp_path):
+    """Iteration-level batching: requests of different lengths / budgets arriving while others
+    decode are admitted into free slots between steps, finished slots are reused at once, and every
+    greedy result equals the request run alone."""
+    import time as _time
+    from edgellm.serve.server import ServingEngine
+    from edgellm.utils.tokenizer import ByteTokenizer
+    cfg = tiny("llama")
+    m = build_model(cfg, dtype=torch.float32, seed=2)
+    eng = ServingEngine(Generator(m, max_batch=3, max_seq=128), ByteTokenizer(cfg.vocab_size), steps_per_poll=2,
+                        metrics_path=str(tmp_path / "m.jsonl"))
+    assert eng.continuous
+    reqs = [([1, 2, 3], 9), ([5, 6, 7, 8, 9, 10], 4), ([11], 12), ([4, 4, 2, 7], 6), ([9, 8], 3), ([3] * 20, 7)]
+    try:
+        futs = []
+        for i, (ids, n) in enumerate(reqs):
+            futs.append(eng.submit(ids, SamplingParams(max_new_tokens=n, do_sample=False, repetition_penalty=1.1)))
+            if i == 2:
+                _time.sleep(0.05)             # the rest arrive while the first three decode
+        outs = [f.result(timeout=120) for f in futs]
+        for (ids, n), o in zip(reqs, outs):
+            sp = SamplingParams(max_new_tokens=n, do_sample=False, repetition_penalty=1.1)
+            assert o["tokens"] == Generator(m, max_batch=1, max_seq=128).generate([ids], sp).tokens[0]
+        st = eng.metrics()
+        assert st["requests"] == 6 and st["sessions"] == 1 and st["max_concurrent"] == 3
+        # 6 requests, 41 tokens, 3 slots: far fewer steps than running them one after another
+        assert st["decode_steps"] < sum(n - 1 for _, n in reqs)
+        # a sampling configuration change opens a new session once the running one drains
+        o = eng.submit([1, 2], SamplingParams(max_new_tokens=5, temperature=0.8, top_k=10)).result(timeout=60)
+        assert len(o["tokens"]) == 5 and eng.metrics()["sessions"] == 2
     finally:
         eng.close()
 

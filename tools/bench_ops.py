@@ -250,14 +250,22 @@ def sample_rows(C, dev):
 def prefill_rows(C, dev, Hq, D):
     out = []
     # prefill attention (MFMA)
-    for T in (512, 2048):
+    D0 = D
+    for T, Hkv, s0, D in ((512, Hq, 0, D0), (1024, Hq, 0, D0), (2048, Hq, 0, D0), (8192, Hq // 4, 0, D0),
+                          (4096, Hq // 4, 28672, D0), (1024, 8, 0, 64)):
         q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
-        kc = torch.randn(1, Hq, T, D, device=dev).bfloat16()
+        kc = torch.randn(1, Hkv, s0 + T, D, device=dev).bfloat16()
         vc = torch.randn_like(kc)
-        sp0 = torch.zeros(1, dtype=torch.int32, device=dev)
-        t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=20)
-        flops = 4 * T * T * D * Hq / 2
-        out.append(dict(op="prefill_attn_causal", T=T, H=Hq, D=D, us=round(t, 2), TFLOPs=round(flops / t / 1e6, 1)))
+        sp0 = torch.full((1,), s0, dtype=torch.int32, device=dev)
+        flops = 4 * T * (s0 + T / 2) * D * Hq
+        row = dict(op="prefill_attn_causal", T=T, start=s0, H=Hq, Hkv=Hkv, D=D)
+        for name, v in (("fa", 1), ("old", 0)):
+            C.tune("prefill_fa", v, 0)
+            t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=10)
+            row[f"{name}_us"], row[f"{name}_TFLOPs"] = round(t, 2), round(flops / t / 1e6, 1)
+        C.tune("prefill_fa", 1, 0)
+        out.append(row)
+        print(row, flush=True)
     out += prefill_gemm_rows(C, dev)
     return out
 
