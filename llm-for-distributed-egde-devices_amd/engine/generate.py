@@ -121,6 +121,7 @@ class Generator:
         self.eos_check_every = eos_check_every
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._pool = None
+        self._warm = False                # a decode step of the current state ran eagerly
         self._state: Optional[_DecodeState] = None
 
     # ------------------------------------------------------------------ forward pieces
@@ -178,6 +179,7 @@ class Generator:
     def reset_graphs(self):
         self._graphs.clear()
         self._pool = None
+        self._warm = False
 
     # ------------------------------------------------------------------ generate
     @torch.no_grad()
@@ -253,8 +255,12 @@ class Generator:
             with trace_range(f"decode.B{B}"):
                 if r["graphs_ok"]:
                     bucket = min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
-                    if not self._graphs:
-                        self._decode_step(st, B, bucket, sampling)      # warm-up step (a real step)
+                    if not self._warm:
+                        # first step of this decode state runs eagerly (lazy weight packs, workspace
+                        # allocations, autotune choices happen outside any capture); every later
+                        # step replays the captured graph of its length bucket
+                        self._decode_step(st, B, bucket, sampling)
+                        self._warm = True
                     else:
                         self._graph_for(st, B, bucket, sampling).replay()
                 else:
@@ -273,7 +279,7 @@ class Generator:
         """Capture the decode graphs of every length bucket the next ``n_steps`` will touch
         (capture records, it does not execute), so no capture lands in a timed region."""
         r = self._run
-        if not r["graphs_ok"] or not self._graphs:
+        if not r["graphs_ok"] or not self._warm:
             return 0
         lo = r["host_max"] + 1
         hi = min(self.max_seq, lo + n_steps)

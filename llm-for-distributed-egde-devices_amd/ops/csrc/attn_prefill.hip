@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
 }
 }  // namespace
 
-static int g_prefill_fa = 1;           // tune key "prefill_fa": 0 = the 16-row kernel for D = 64 / 128 too
+static int g_prefill_fa = 1;           // tune key "prefill_fa": 0 = the 16-row kernel only, 1 = auto, 2 = fa_kernel always
 extern "C" void edge_prefill_fa(int v) { g_prefill_fa = v; }
 
 extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
@@ -441,7 +441,12 @@ extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void*
   if (B * T == 0) return 0;
   if (Hq % Hkv) return -2;
   const float sl2 = scale * 1.4426950408889634f;
-  if ((D == 128 || D == 64) && g_prefill_fa) {
+  // fa_kernel takes 256 queries per workgroup: below ~128 workgroups (short prompts, few heads) the
+  // 64-row kernel keeps more CUs busy (tools/bench_ops.py --only prefill, D 128: T 512 x 32 heads
+  // 23.4 vs 27.6 us, T 1024 54.8 vs 50.2, T 2048 198 vs 98, 4K chunk over 28K cached keys 6.09 vs
+  // 2.78 ms)
+  const bool fa_fills = (int64_t)((T + FA_QT - 1) / FA_QT) * Hq * B >= 128;
+  if ((D == 128 || D == 64) && (g_prefill_fa == 2 || (g_prefill_fa == 1 && fa_fills))) {
 #define FA(DD)                                                                                                     \
   do {                                                                                                             \
     static bool fa_attr = false;                                                                                   \

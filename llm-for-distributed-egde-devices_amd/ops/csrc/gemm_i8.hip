@@ -1156,23 +1156,25 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   // loaders re-read two k-tiles (weights L2-resident), 128 epilogue without its global stores
   constexpr int MB = 8, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
   constexpr int NTH = NCW == 8 ? NTW / 2 : NTW;       // tiles per compute wave
-  static_assert(NCW == 4 || (NCW == 8 && NTW % 2 == 0 && EPI != EPI_GLUQ), "compute waves");
+  // GLUQ: a compute wave's tiles must be whole 64-feature quant groups (4 gate/up pairs): NTH == 8
+  static_assert(NCW == 4 || (NCW == 8 && NTW % 2 == 0 && (EPI != EPI_GLUQ || NTW == 16)), "compute waves");
   constexpr int LPW = WPW + (SC ? 1 : 0);             // loader pieces per stage (+ the scale piece)
   static_assert(WST % NWL == 0, "weight pieces split evenly over the loader waves");
   static_assert(DW * LPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
-  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTW == 8 && !SC), "epilogues");
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTH == 8 && !SC), "epilogues");
   static_assert(MS == 1 || MS == 2, "row split");
   static_assert(NAL == 0 || (16 % NAL == 0 && DA * (16 / NAL) <= 63), "activation loaders");
-  // + 1 KiB: the workgroup's weight scales and bias (fp32, <= 128 columns), staged once for the epilogue
-  constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0) + 1;
+  // + EPK KiB: the workgroup's weight scales and bias (fp32, EPC columns each), staged once for the epilogue
+  constexpr int EPC = NTW * 16 <= 128 ? 128 : 256, EPK = EPC / 128;
+  constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0) + EPK;
   static_assert(LDS_KB * 1024 <= 160 * 1024, "LDS budget");
-  static_assert(NTW * 16 <= 128, "epilogue operand area");
+  static_assert(NTW * 16 <= 256, "epilogue operand area");
   __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_KB * 1024];
   int8_t* const wring = lds;
   int8_t* const aring = lds + RW * WST * 1024;
   int8_t* const sring = aring + RA * 16 * 1024;       // SC only
-  float* const epi_sw = reinterpret_cast<float*>(lds + (LDS_KB - 1) * 1024);
-  float* const epi_b = epi_sw + 128;
+  float* const epi_sw = reinterpret_cast<float*>(lds + (LDS_KB - EPK) * 1024);
+  float* const epi_b = epi_sw + EPC;
   int lbid = (int)blockIdx.x, row0 = 0;
   if constexpr (MS == 2) {
     // XCD-contiguous logical order: blocks b = 8 j + x (x = b & 7 labels the blocks that share an
@@ -1280,7 +1282,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   // row's activation scale is one value per lane.  The workgroup's weight scales and bias go to
   // LDS once now (ordered for the epilogue by the stage barriers); the tail never waits on memory.
   {
-    const int c = threadIdx.x;                        // compute waves: 256 threads, <= 128 columns
+    const int c = threadIdx.x;                        // compute waves: >= 256 threads, <= 256 columns
     if (c < NTW * 16) {
       const int col = min(nt0 * 16 + c, N - 1);
       epi_sw[c] = sw[col];
@@ -1402,19 +1404,20 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       }
     }
   } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
-    const int Fo = N / 2, grp64 = nt0 / 8;
+    // the wave's 8 tiles [tb, tb + 8) are one 64-feature quant group (NCW == 8: two per workgroup)
+    const int Fo = N / 2, grp64 = (nt0 + tb) / 8;
     int8_t* hq = reinterpret_cast<int8_t*>(outv);
-    const bool live = nt0 + 7 < NTt;
+    const bool live = nt0 + tb + 7 < NTt;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int lrow = (2 * wave + j) * 16 + (lane & 15);
+      const int lrow = (2 * mw + j) * 16 + (lane & 15);
       const int row = row0 + lrow;
       float h[4][4], amax = 0.f;
 #pragma unroll
       for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int cg = 2 * p * 16 + g4 + q, cu = cg + 16;
+          const int cg = (tb + 2 * p) * 16 + g4 + q, cu = cg + 16;
           const float g = bf2f(f2bf((float)acc[j][2 * p][q] * sa_r[j] * epi_sw[cg] + epi_b[cg]));     // the unfused GEMM output is bf16
           const float u = bf2f(f2bf((float)acc[j][2 * p + 1][q] * sa_r[j] * epi_sw[cu] + epi_b[cu]));
           h[p][q] = g / (1.f + __expf(-g)) * u;
@@ -1430,7 +1433,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
           uint32_t w = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) w |= (uint32_t)(uint8_t)quant_i8(h[p][q], inv) << (8 * q);
-          *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + (nt0 / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
+          *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + ((nt0 + tb) / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
         }
       }
       if (live && lane < 16 && row < Mpad) os[(size_t)grp64 * Mpad + row] = lrow < Ml ? amax / 127.f : 0.f;
@@ -1443,7 +1446,7 @@ static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_
 extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
 static int g_w_nt = 1;
 extern "C" void edge_w8a8_weight_nt(int v) { g_w_nt = v; }
-// prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel at BM = 256 / 128
+// prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel (BM = 128)
 static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1;
 extern "C" void edge_w8a8_prefill_apack(int v) { g_prefill_apack = v; }
 // b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
@@ -1655,6 +1658,11 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
     if (c == 1) R256(8, 2, 5, 4, 1, false);
     if (c == 2) R256(8, 4, 5, 4, 0, false);
     if (c == 3) R256(8, 2, 4, 5, 2, false);
+    if (c == 5) R256(8, 2, 5, 4, 2, false);           // the two-round form below
+    // one round: 16 tiles per workgroup (gate_up N 22016 at 8 tiles = 344 launched workgroups = 2
+    // rounds; a quant group is 8 tiles) = 172 workgroups, 8 compute waves each owning one group
+    // (tools/bench_ops.py --only rows256, M = 256: gate_up 43.7 -> 34.7 us)
+    if (NTt % 16 == 0) return launch_r256<16, 2, 3, 3, 2, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
     R256(8, 2, 5, 4, 2, false);
   } else {
     if (scaled || S != 1) return -1;
@@ -1842,19 +1850,16 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     return launch_one<4, 4, 2, 4, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
   }
   if (M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1) {   // (see edge_w8a8_gemm_apk)
-    // 128 x 256 tiles, except 256 x 256 for the long-K down projection when those still fill the
-    // chip (tools/bench_ops.py pgemm, Llama-2-7B shapes at M = 512 / 2048 / 16384: 128-row tiles
-    // 1.5-2.1 POPS, equal or ahead everywhere but K = 11008 at M = 16384, 2.21 vs 2.11)
+    // 128 x 256 tiles.  (The 256 x 256 form measured 2.21 vs 2.11 POPS on the K = 11008 down
+    // projection at M = 16384, but at 256 VGPRs it spilled ~290 B per lane, and spill traffic joins
+    // the ring's counted vmcnt — the same hazard that broke a decode kernel — so it is gone.)
     const int grid_n = (NTt * 16 + 255) / 256;
-    const int g256 = (M + 255) / 256, g128 = (M + 127) / 128;
-    const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && K > 8192 && g256 * grid_n >= 256);
-    const int grid_m = big ? g256 : g128;
+    const int grid_m = (M + 127) / 128;
 #define BIGK(BMV, ISS)                                                                                           \
   hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
     const int iss = g_prefill_iss;
-    if (big) { if (iss == 1) BIGK(256, 1); else if (iss == 2) BIGK(256, 2); else BIGK(256, 0); }
-    else { if (iss == 1) BIGK(128, 1); else if (iss == 2) BIGK(128, 2); else BIGK(128, 0); }
+    if (iss == 1) BIGK(128, 1); else if (iss == 2) BIGK(128, 2); else BIGK(128, 0);
 #undef BIGK
     return (int)hipGetLastError();
   }
@@ -1911,15 +1916,9 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
                      (int8_t*)Ap, M, K, KT, total);
   const int NTt = (N + 15) / 16;
   const int grid_n = (NTt * 16 + 255) / 256;
-  const int g256 = (M + 255) / 256, g128 = (M + 127) / 128;
-  const bool big = g_prefill_gemm == 2 || (g_prefill_gemm != 3 && K > 8192 && g256 * grid_n >= 256);
-  const int grid_m = big ? g256 : g128;
-#define BIGP(BMV, ISS)                                                                                            \
-  hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS, true>), dim3(grid_m * grid_n), dim3(512), 0, st,            \
-                     (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, \
-                     grid_m, grid_n)
-  if (big) BIGP(256, 2);
-  else BIGP(128, 2);
-#undef BIGP
+  const int grid_m = (M + 127) / 128;
+  hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
+                     (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
+                     grid_m, grid_n);
   return (int)hipGetLastError();
 }

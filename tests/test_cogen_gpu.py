@@ -33,7 +33,7 @@ def test_co_generate_matches_solo(cuda):
     got = co_generate(jobs)
     for a, b in zip(got, solo):
         assert a.tokens == b.tokens
-    assert all(gen._graphs for gen in gens)             # decode ran graph-replayed
+    assert any(gen._graphs for gen in gens)             # decode ran graph-replayed
 
 
 def test_continuous_batching_gpu_matches_solo(cuda):

@@ -88,7 +88,10 @@ def test_w8a8_decode_128_rows_4096_hidden(cuda, B):
 def _rows_match_small_batch(model, prompts, B, cuda, tol=3e-2):
     """Decode-step logits of the first 16 rows at batch B (its kernel family) against the same
     rows decoded at batch 16: rows are independent, so only kernel rounding may differ — bounded
-    per row on relative logit error (a wrong row block cannot hide behind token agreement)."""
+    per row on relative logit error (a wrong row block cannot hide behind token agreement).
+    Both caches are prefilled in the same 16-sequence chunks (one prefill numerics: at 192 tokens
+    the 256-row decode GEMMs with per-(token, 64) activation scales, at B x 12 tokens the prefill
+    GEMM with per-token scales — a different quantisation that can flip a near-tied argmax)."""
     from edgellm.models import AttnCtx
     cfg = model.cfg
     outs = {}
@@ -96,11 +99,14 @@ def _rows_match_small_batch(model, prompts, B, cuda, tol=3e-2):
         ids = torch.tensor(prompts[:b], device=cuda)
         T = ids.shape[1]
         kv = KVCache(cfg, b, T + 4, dtype=model.dtype, device=cuda)
-        sp = torch.zeros(b, dtype=torch.int32, device=cuda)
         with torch.no_grad():
-            last = model(ids, AttnCtx("prefill", b, T, sp, sp + T, T, kv.rows(0, b), model.rope_table(cuda)),
-                         logits="last")
-            tok = last.argmax(-1)
+            lasts = []
+            for r0 in range(0, b, 16):
+                n = min(16, b - r0)
+                sp = torch.zeros(n, dtype=torch.int32, device=cuda)
+                lasts.append(model(ids[r0:r0 + n], AttnCtx("prefill", n, T, sp, sp + T, T, kv.rows(r0, r0 + n),
+                                                           model.rope_table(cuda)), logits="last"))
+            tok = torch.cat(lasts).argmax(-1)
             pos = torch.full((b,), T, dtype=torch.int32, device=cuda)
             outs[b] = model(tok.view(b, 1), AttnCtx("decode", b, 1, pos, pos + 1, T + 1, kv.rows(0, b),
                                                     model.rope_table(cuda))).float()[:16]

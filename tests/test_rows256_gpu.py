@@ -79,7 +79,7 @@ def test_rows256_splitk(cuda, cfg, nt, M, grouped, N, K):
     _close(parts.sum(0), ref, 1e-3, 1e-2)
 
 
-@pytest.mark.parametrize("cfg,nt", [(0, 0), (0, 1), (1, 1), (2, 1), (3, 1)])
+@pytest.mark.parametrize("cfg,nt", [(0, 0), (0, 1), (1, 1), (2, 1), (3, 1), (5, 1)])
 @pytest.mark.parametrize("M", [129, 256])
 @pytest.mark.parametrize("F,K", [(11008, 4096), (14336, 4096), (1024, 2048)])
 def test_rows256_gluq(cuda, cfg, nt, M, F, K):

@@ -259,7 +259,7 @@ def prefill_rows(C, dev, Hq, D):
         sp0 = torch.full((1,), s0, dtype=torch.int32, device=dev)
         flops = 4 * T * (s0 + T / 2) * D * Hq
         row = dict(op="prefill_attn_causal", T=T, start=s0, H=Hq, Hkv=Hkv, D=D)
-        for name, v in (("fa", 1), ("old", 0)):
+        for name, v in (("fa", 2), ("old", 0)):
             C.tune("prefill_fa", v, 0)
             t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=10)
             row[f"{name}_us"], row[f"{name}_TFLOPs"] = round(t, 2), round(flops / t / 1e6, 1)
@@ -423,7 +423,7 @@ def rows256_rows(C, dev, M=256):
             return call
 
         c256, c128 = make(M), make(M // 2)
-        forms = [(0, 1), (0, 0), (1, 1), (2, 1), (3, 1), (4, 1)]
+        forms = [(0, 1), (0, 0), (1, 1), (2, 1), (3, 1), (4, 1), (5, 1)]
         res = {}
         for rnd in range(3):
             for cfg, nt in forms:
