@@ -96,18 +96,25 @@ class HeadInferKV:
             chunk_heads = int(max(1, stage_budget_bytes // max(per_head, 1)))
         self.c = max(1, min(chunk_heads, max(self.h_off, 1)))
         pin = self.cuda
-        self.host_k = torch.zeros((L, max_batch, self.h_off, max_seq, D), dtype=edt, pin_memory=pin)
-        self.host_v = torch.zeros_like(self.host_k, pin_memory=pin)
         mk = lambda *s, dt=edt: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
-        self.stage = [(mk(R, self.c, max_seq, D), mk(R, self.c, max_seq, D)) for _ in range(2)]
         if self.q8:
-            # fp32 scales [.., S] moved as [.., S, 1] head blocks alongside the int8 rows
-            self.host_ks = torch.zeros((L, max_batch, self.h_off, max_seq), dtype=torch.float32, pin_memory=pin)
-            self.host_vs = torch.zeros_like(self.host_ks, pin_memory=pin)
-            self.stage_s = [(mk(R, self.c, max_seq, dt=torch.float32), mk(R, self.c, max_seq, dt=torch.float32))
-                            for _ in range(2)]
+            # K and V of a head interleaved as [.., head, {k, v}, S, D] (and their fp32 scales as
+            # [.., head, {k, v}, S]) on the host and in the staging buffers: one head-block copy
+            # moves both (a [B, 2 c, rows, D] block), halving the per-layer transfers whose fixed
+            # cost adds to the PCIe time; k / v are strided views for the kernels
+            self.host_kv = torch.zeros((L, max_batch, self.h_off, 2, max_seq, D), dtype=edt, pin_memory=pin)
+            self.host_s = torch.zeros((L, max_batch, self.h_off, 2, max_seq), dtype=torch.float32, pin_memory=pin)
+            self.host_k, self.host_v = self.host_kv[:, :, :, 0], self.host_kv[:, :, :, 1]
+            self.host_ks, self.host_vs = self.host_s[:, :, :, 0], self.host_s[:, :, :, 1]
+            self.stage_kv = [mk(R, self.c, 2, max_seq, D) for _ in range(2)]
+            self.stage_ss = [mk(R, self.c, 2, max_seq, dt=torch.float32) for _ in range(2)]
+            self.stage = [(t[:, :, 0], t[:, :, 1]) for t in self.stage_kv]
+            self.stage_s = [(t[:, :, 0], t[:, :, 1]) for t in self.stage_ss]
             self.new = []
         else:
+            self.host_k = torch.zeros((L, max_batch, self.h_off, max_seq, D), dtype=edt, pin_memory=pin)
+            self.host_v = torch.zeros_like(self.host_k, pin_memory=pin)
+            self.stage = [(mk(R, self.c, max_seq, D), mk(R, self.c, max_seq, D)) for _ in range(2)]
             self.new = [(mk(R, self.h_off, chunk_size, D), mk(R, self.h_off, chunk_size, D))
                         for _ in range(2)]
         self.zeros = torch.zeros(max_batch, dtype=torch.int32, device=device)
@@ -135,14 +142,15 @@ class HeadInferKV:
         return self.gpu.layer_scales(i)
 
     def gpu_bytes(self) -> int:
-        bufs = self.stage + self.new + (self.stage_s if self.q8 else [])
-        return self.gpu.nbytes() + sum(t.numel() * t.element_size() for p in bufs for t in p)
+        if self.q8:
+            bufs = self.stage_kv + self.stage_ss
+            return self.gpu.nbytes() + sum(t.numel() * t.element_size() for t in bufs)
+        return self.gpu.nbytes() + sum(t.numel() * t.element_size() for p in self.stage + self.new for t in p)
 
     def host_bytes(self) -> int:
-        n = 2 * self.host_k.numel() * self.host_k.element_size()
         if self.q8:
-            n += 2 * self.host_ks.numel() * 4
-        return n
+            return self.host_kv.numel() + self.host_s.numel() * 4
+        return 2 * self.host_k.numel() * self.host_k.element_size()
 
     # -------------------------------------------------------------- transfers
     def _copy(self, dst, src):
@@ -168,26 +176,28 @@ class HeadInferKV:
         self.bytes_h2d += 2 * (r1 - r0) * cc * hist * (self.cfg.head_dim * sk.element_size() + (4 if self.q8 else 0))
 
     def _h2d(self, buf, li, r0, r1, h0, cc, hist):
+        if self.q8:                                  # k + v in one block, their scales in another
+            B = r1 - r0
+            self._copy(self.stage_kv[buf][:B, :cc, :, :hist].flatten(1, 2),
+                       self.host_kv[li, r0:r1, h0:h0 + cc, :, :hist].flatten(1, 2))
+            self._copy(self.stage_ss[buf][:B, :cc, :, :hist].flatten(1, 2)[..., None],
+                       self.host_s[li, r0:r1, h0:h0 + cc, :, :hist].flatten(1, 2)[..., None])
+            return
         sk, sv = self.stage[buf]
         self._copy(sk[: r1 - r0, :cc, :hist], self.host_k[li, r0:r1, h0:h0 + cc, :hist])
         self._copy(sv[: r1 - r0, :cc, :hist], self.host_v[li, r0:r1, h0:h0 + cc, :hist])
-        if self.q8:
-            sks, svs = self.stage_s[buf]
-            self._copy(sks[: r1 - r0, :cc, :hist, None], self.host_ks[li, r0:r1, h0:h0 + cc, :hist, None])
-            self._copy(svs[: r1 - r0, :cc, :hist, None], self.host_vs[li, r0:r1, h0:h0 + cc, :hist, None])
+
 
     def _writeback_q8(self, buf, li, r0, r1, h0, cc, p0, n, cs):
         """int8 rows [p0, p0 + n) that a kernel appended to staging buffer ``buf`` -> the host
         pool (copy stream, after the compute stream's work so far); frees the buffer after."""
-        sk, sv = self.stage[buf]
-        sks, svs = self.stage_s[buf]
         B = r1 - r0
 
         def go():
-            self._copy(self.host_k[li, r0:r1, h0:h0 + cc, p0:p0 + n], sk[:B, :cc, p0:p0 + n])
-            self._copy(self.host_v[li, r0:r1, h0:h0 + cc, p0:p0 + n], sv[:B, :cc, p0:p0 + n])
-            self._copy(self.host_ks[li, r0:r1, h0:h0 + cc, p0:p0 + n, None], sks[:B, :cc, p0:p0 + n, None])
-            self._copy(self.host_vs[li, r0:r1, h0:h0 + cc, p0:p0 + n, None], svs[:B, :cc, p0:p0 + n, None])
+            self._copy(self.host_kv[li, r0:r1, h0:h0 + cc, :, p0:p0 + n].flatten(1, 2),
+                       self.stage_kv[buf][:B, :cc, :, p0:p0 + n].flatten(1, 2))
+            self._copy(self.host_s[li, r0:r1, h0:h0 + cc, :, p0:p0 + n].flatten(1, 2)[..., None],
+                       self.stage_ss[buf][:B, :cc, :, p0:p0 + n].flatten(1, 2)[..., None])
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(cs)

@@ -615,14 +615,16 @@ extern "C" int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, vo
                                    int64_t c_sb, int64_t c_sh, int64_t s_sb, int64_t s_sh, const int* seq_lens,
                                    int B, int Hq, int Hkv, int D, float scale, int ch, int nsplit, void* out,
                                    int64_t o_sb, float* part_acc, float* part_ml, const int* pos, const float* cs,
-                                   int rot, void* out_q, float* out_s, int Mpad, hipStream_t st) {
+                                   int rot, void* out_q, float* out_s, int Mpad, int S, hipStream_t st) {
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -2;
   const bool qout = out_q != nullptr;
   if (qout && (D % 64 != 0 || Mpad < B)) return -2;
   if (rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
-  const Fuse8 fz{pos, cs, rot, qkv_sb, (int8_t*)out_q, out_s, Mpad, (int)(c_sh / D)};
+  // S = the cache's positions per head (not c_sh / D: a head pitch may exceed S * D, e.g. HeadInfer's
+  // staging buffers interleave each head's K and V blocks)
+  const Fuse8 fz{pos, cs, rot, qkv_sb, (int8_t*)out_q, out_s, Mpad, S};
   const float sl2 = scale * 1.4426950408889634f;
   if (G == 1 && ch < 0) {                 // wave-per-(sequence, head) form (edge_decode_attn_i8_plan)
     const int npairs = B * Hkv, blocks = (npairs + NW - 1) / NW;

@@ -71,7 +71,7 @@ void edge_decode_attn_config(int target_wg);
 int edge_decode_attn_i8(const void* qkv, int64_t qkv_sb, void* kc, void* vc, float* ks, float* vs, int64_t c_sb,
                         int64_t c_sh, int64_t s_sb, int64_t s_sh, const int* seq_lens, int B, int Hq, int Hkv, int D,
                         float scale, int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
-                        const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
+                        const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad, int S,
                         hipStream_t st);
 int edge_decode_attn_i8_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out, int G);
 void edge_decode_attn_i8_wave_max(int v);
@@ -420,7 +420,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_i8(
                             quant_out ? 0 : out.stride(0), nsplit > 1 ? pacc.data_ptr<float>() : nullptr,
                             nsplit > 1 ? pml.data_ptr<float>() : nullptr, start_pos.data_ptr<int>(), cs, (int)rot,
                             quant_out ? oq.data_ptr() : nullptr, quant_out ? os->data_ptr<float>() : nullptr,
-                            (int)Mpad, stream()),
+                            (int)Mpad, (int)k_cache.size(2), stream()),
         "decode_attn_i8");
   if (quant_out) return {oq, os};
   return {out, std::nullopt};

@@ -126,7 +126,7 @@ def test_headinfer_int8_matches_resident_int8_cpu(h_on, chunk_heads, chunk_size)
     assert kv.host_k.dtype == torch.int8 and kv.host_ks.dtype == torch.float32
     # PCIe bytes per (token, head): D + 4 (int8 row + fp32 scale), not 2 D
     assert kv.bytes_d2h > 0 and kv.bytes_h2d > 0
-    assert kv.host_bytes() == 2 * kv.host_k.numel() + 2 * 4 * kv.host_ks.numel()
+    assert kv.host_bytes() == kv.host_kv.numel() + 4 * kv.host_s.numel()
 
 
 @pytest.mark.gpu
