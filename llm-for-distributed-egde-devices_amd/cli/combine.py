@@ -24,6 +24,7 @@ from ..config import add_reference_args, apply_overrides, load_config, RunConfig
 from ..data import load_qa
 from ..engine import Generator, SamplingParams
 from ..eval import EfficiencyMeter, Embedder, MetricSuite, ProgressLog, Results
+from ..eval.metrics import confidence_scores
 from ..models.registry import load_model
 from ..orchestrator import Agent, Orchestrator, RefineMerge, VoteMerge
 from ..parallel.split import agent_devices, split_model
@@ -139,13 +140,20 @@ def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_vari
             outs = [orch.answer(qs[0], refs[0], seed=rt.get("seed", 0) + idx[0])]
         else:
             outs = orch.answer_batch(qs, refs, seed=rt.get("seed", 0) + idx[0])
-        for i, q, ref, res in zip(idx, qs, refs, outs):
+        confs = [None] * len(outs)
+        if bs > 1 and scorer is not None:          # one padded scorer pass per 32 answers
+            try:
+                confs = confidence_scores(scorer.generator.model, [scorer.tokenizer.encode(r.final) for r in outs])
+            except Exception:
+                confs = [None] * len(outs)
+        for i, q, ref, res, conf in zip(idx, qs, refs, outs, confs):
             for name, ans in res.answers.items():
                 logger.info(f"Answer from {name}: {ans[:100]}...")
                 if cpu_variant:
                     logger.info(f"[Q{i + 1}] {name} TPS: {res.tps[name]:.2f} tokens/sec")
             logger.info(f"Refined response: {res.final[:100]}...")
-            m = suite.score(res.final, ref, scorer.generator.model, scorer.tokenizer, tps=res.combo_tps)
+            m = suite.score(res.final, ref, scorer.generator.model, scorer.tokenizer, tps=res.combo_tps,
+                            confidence=conf)
             if m["rouge1"] == 0.0 and m["tps"] == 0.0:
                 logger.error("Error in evaluation: metrics zeroed for this sample")
             results.add(m)

@@ -44,6 +44,32 @@ def confidence_score(model: DecoderLM, ids: List[int]) -> float:
     return float(ops.max_softmax_prob(logits).mean())
 
 
+@torch.no_grad()
+def confidence_scores(model: DecoderLM, ids_list: List[List[int]], rows_per_pass: int = 32) -> List[float]:
+    """``confidence_score`` of several texts with one right-padded prefill pass per
+    ``rows_per_pass`` texts (causal attention: a real token never sees the pads, so each row's
+    per-token logits are its own pass's); pads are excluded from each row's mean."""
+    if hasattr(model, "confidence") or not ids_list:
+        return [confidence_score(model, ids) for ids in ids_list]
+    out: List[float] = [0.0] * len(ids_list)
+    dev = model.device
+    live = [i for i, ids in enumerate(ids_list) if ids]
+    for c0 in range(0, len(live), rows_per_pass):
+        idx = live[c0:c0 + rows_per_pass]
+        B, T = len(idx), max(len(ids_list[i]) for i in idx)
+        x = torch.zeros(B, T, dtype=torch.long)
+        for r, i in enumerate(idx):
+            x[r, :len(ids_list[i])] = torch.tensor(ids_list[i])
+        kv = KVCache(model.cfg, B, T, dtype=model.dtype, device=dev)
+        sp = torch.zeros(B, dtype=torch.int32, device=dev)
+        ctx = AttnCtx("prefill", B, T, sp, sp + T, T, kv, model.rope_table(dev))
+        logits = model(x.to(dev), ctx, logits="all")
+        p = ops.max_softmax_prob(logits).float().view(B, T).cpu()
+        for r, i in enumerate(idx):
+            out[i] = float(p[r, :len(ids_list[i])].mean())
+    return out
+
+
 class Embedder:
     """Sentence embeddings + contextual token embeddings from a BERT-style encoder."""
 
@@ -87,13 +113,15 @@ class MetricSuite:
     strict: bool = False
 
     def score(self, pred: str, ref: str, scorer: Optional[DecoderLM] = None, scorer_tok=None,
-              tps: float = 0.0) -> Dict[str, float]:
+              tps: float = 0.0, confidence: Optional[float] = None) -> Dict[str, float]:
+        """``confidence``: precomputed (``confidence_scores`` over a batch), else one scorer pass."""
         try:
             r1, r2, rl = evaluate_rouge(pred, ref)
             bs = bertscore_f1(pred, ref, self.bert_embedder or self.embedder) if (self.bert_embedder or self.embedder) else 0.0
             bl = evaluate_bleu(pred, ref)
             cs = cosine_similarity(pred, ref, self.embedder) if self.embedder else 0.0
-            conf = confidence_score(scorer, scorer_tok.encode(pred)) if scorer is not None else 0.0
+            conf = confidence if confidence is not None else \
+                (confidence_score(scorer, scorer_tok.encode(pred)) if scorer is not None else 0.0)
             return dict(rouge1=r1, rouge2=r2, rougeL=rl, bertscore=bs, bleu=bl, cosine=cs, confidence=conf, tps=tps)
         except Exception:
             if self.strict:

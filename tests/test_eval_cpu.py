@@ -104,3 +104,14 @@ def test_orchestrator_runs_agents_concurrently_on_distinct_devices():
     agents[1].device = torch.device("meta")           # distinct "device groups" -> threads
     out = Orchestrator(agents, VoteMerge(), concurrent=True).answer("q")
     assert out.final == "same" and out.merge == "vote"
+
+
+def test_confidence_scores_batched_equals_per_text():
+    """One right-padded scorer pass per group of texts gives each text's own confidence."""
+    from edgellm.eval.metrics import confidence_score, confidence_scores
+    from edgellm.models import build_model, tiny
+    m = build_model(tiny("llama"), dtype=torch.float32, seed=3)
+    texts = [[5, 9, 2, 7], [1], [], [3, 3, 8, 1, 4, 4, 2, 9, 9], [6, 2]]
+    got = confidence_scores(m, texts, rows_per_pass=3)
+    want = [confidence_score(m, t) for t in texts]
+    assert got == pytest.approx(want, abs=1e-5)

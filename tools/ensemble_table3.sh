@@ -23,6 +23,6 @@ run combo_w8a8_b16     $C --config configs/ensemble.yaml $D --num_samples 64 --b
 run north_star_vote    $C --config configs/north_star.yaml $D --num_samples 32 --batch_size 16
 # agents sharing the GPU decode side by side on their own streams (orchestrator run_agents ->
 # engine co_generate), 128 questions per batch
-run north_star_vote_b128 $C --config configs/north_star.yaml $D --num_samples 256 --batch_size 128
+run north_star_vote_b256 $C --config configs/north_star.yaml $D --num_samples 512 --batch_size 256 --max_seq 512
 run combo_base_b128    $C --config configs/ensemble.yaml $D --num_samples 256 --batch_size 128
 run combo_w8a8_b128    $C --config configs/ensemble.yaml $D --num_samples 256 --batch_size 128 --quant w8a8_smoothquant
