@@ -58,6 +58,19 @@ class KVCache:
     def rows(self, r0: int, r1: int) -> "KVView":
         return KVView(self, r0, r1)
 
+    def prefill_scratch(self, B: int, S: int, dtype, device):
+        """bf16 (k, v) scratch [B, Hkv, S, D] for int8-cache prefill (rotated new rows + the
+        dequantised history), one grow-only buffer per stream shared by every layer: the layers of a
+        forward run in stream order, so layer i + 1 rewrites it only after layer i's attention."""
+        hk, D = self.k.shape[2], self.k.shape[4]
+        n = B * hk * S * D
+        key = (torch.cuda.current_stream(device).cuda_stream if torch.device(device).type == "cuda" else 0)
+        bufs = self.__dict__.setdefault("_scratch", {})
+        buf = bufs.get(key)
+        if buf is None or buf.numel() < 2 * n or buf.dtype != dtype or buf.device != torch.device(device):
+            buf = bufs[key] = torch.empty(2 * n, dtype=dtype, device=device)
+        return buf[:n].view(B, hk, S, D), buf[n:2 * n].view(B, hk, S, D)
+
     def nbytes(self) -> int:
         n = self.k.numel() * self.k.element_size() * 2
         if self.quantized:
@@ -79,3 +92,6 @@ class KVView:
     def layer_scales(self, i: int):
         ks, vs = self.cache.layer_scales(i)
         return ks[self.r0:self.r1], vs[self.r0:self.r1]
+
+    def prefill_scratch(self, B: int, S: int, dtype, device):
+        return self.cache.prefill_scratch(B, S, dtype, device)

@@ -115,8 +115,12 @@ class Attention(nn.Module):
     def _forward_kv8(self, qkv, ctx: AttnCtx, k_cache, v_cache, rot: int):
         """int8 KV cache (engine.kv_cache, kv_dtype="int8").  Decode: one launch for RoPE +
         quantising append + attention over the int8 cache.  Prefill: RoPE writes the rotated bf16
-        k / v of the new tokens (plus the dequantised history when start > 0) into a scratch the
-        prefill attention reads, and the new rows are quantised into the cache."""
+        k / v of the new tokens (plus, when start > 0, the history dequantised by one kernel) into a
+        per-stream scratch shared by all layers, the prefill attention reads it, and the new rows are
+        quantised into the cache.
+
+        Precision: the prompt's own tokens attend to their unquantised bf16 k / v during prefill;
+        every later read (decode steps, the next chunk's history) sees the int8-rounded values."""
         cfg = self.cfg
         ks, vs = ctx.kv.layer_scales(self.layer_idx)
         if ctx.mode == "decode":
@@ -130,11 +134,14 @@ class Attention(nn.Module):
         else:
             B, T, S = ctx.B, ctx.T, ctx.max_len
             hist = S - T                                  # host bound of the cached prefix
-            kb = torch.empty(B, cfg.num_kv_heads, S, cfg.head_dim, dtype=qkv.dtype, device=qkv.device)
-            vb = torch.empty_like(kb)
+            if hasattr(ctx.kv, "prefill_scratch"):
+                kb, vb = ctx.kv.prefill_scratch(B, S, qkv.dtype, qkv.device)
+            else:
+                kb = torch.empty(B, cfg.num_kv_heads, S, cfg.head_dim, dtype=qkv.dtype, device=qkv.device)
+                vb = torch.empty_like(kb)
             if hist > 0:
-                kb[:, :, :hist] = ops._ref.dequant_kv(k_cache[:, :, :hist], ks[:, :, :hist]).to(kb.dtype)
-                vb[:, :, :hist] = ops._ref.dequant_kv(v_cache[:, :, :hist], vs[:, :, :hist]).to(vb.dtype)
+                ops.kv_dequant(k_cache, ks, kb, hist)
+                ops.kv_dequant(v_cache, vs, vb, hist)
             q = ops.rope_kv_write(qkv, ctx.start_pos, ctx.rope if rot else None, kb, vb, cfg.num_heads,
                                   cfg.num_kv_heads, cfg.head_dim, rot)
             ops.kv_quant_append(kb, ctx.start_pos, T, k_cache, ks)

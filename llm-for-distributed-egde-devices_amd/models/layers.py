@@ -1,7 +1,7 @@
 """Building blocks shared by every decoder family.
 
-``Linear`` is the bf16 projection (decode rows: ``gemv_bf16.hip``; otherwise hipBLASLt through
-``F.linear`` — ``ops.linear_bf16``);
+``Linear`` is the bf16 projection (decode rows: ``gemv_bf16.hip`` up to 16, the bf16 ring GEMM
+up to 256; otherwise hipBLASLt through ``F.linear`` — ``ops.linear_bf16``);
 quantised replacements live in ``edgellm.quant`` and expose the same interface:
 
     forward(x)                 -> y     x is bf16, or a QAct (int8 + per-token scale) when
@@ -60,9 +60,17 @@ class Linear(nn.Module):
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
         wp = self.decode_weight(x)
-        if self.split_k_out and wp is not None and x.shape[-1] // 64 >= self.split_k_out:
-            return PartialSum(ops.ext().gemv_bf16_splitk(x.reshape(-1, x.shape[-1]), wp, self.bias,
-                                                         self.out_features, self.split_k_out))
+        if self.split_k_out and wp is not None:
+            K = x.shape[-1]
+            if ops.bf16_decode_mode(x, self.weight) == 2:
+                # 17-256 rows: the ring GEMM's split-K slices (the launcher picks S for the shape)
+                S = int(ops.ext().bf16_ring_splits(self.out_features, K))
+                if S > 1:
+                    return PartialSum(ops.ext().gemm_bf16_ring(x.reshape(-1, K), wp, self.bias,
+                                                               self.out_features, 3, S))
+            elif K // 64 >= self.split_k_out:
+                return PartialSum(ops.ext().gemv_bf16_splitk(x.reshape(-1, K), wp, self.bias,
+                                                             self.out_features, self.split_k_out))
         return ops.linear_bf16(x, self.weight, self.bias, packed=wp)
 
     def decode_weight(self, x) -> "Optional[torch.Tensor]":

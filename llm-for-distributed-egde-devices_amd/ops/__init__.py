@@ -250,6 +250,16 @@ def kv_quant_append(src, start_pos, T: int, cache, scales):
         scales[b, :, p0:p0 + T] = s
 
 
+def kv_dequant(cache, scales, dst, T: int):
+    """``dst[:, :, :T] = cache[:, :, :T] * scales[:, :, :T, None]`` (int8 KV rows -> bf16 scratch),
+    one kernel on GPU (no fp32 temporaries)."""
+    if T <= 0:
+        return
+    if _gpu(cache):
+        return ext().kv_dequant(cache, scales, dst, int(T))
+    dst[:, :, :T] = _ref.dequant_kv(cache[:, :, :T], scales[:, :, :T]).to(dst.dtype)
+
+
 def prefill_attention(q, k_cache, v_cache, start_pos, scale, causal=True):
     if _gpu(q):
         return ext().prefill_attn(q, k_cache, v_cache, start_pos, scale, causal)
@@ -280,13 +290,30 @@ def unpack_int8_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
 BF16_GEMV_MAX_ROWS = int(os.environ.get("EDGELLM_BF16_GEMV_ROWS", "16"))
 
 
-def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bool:
-    """Whether ``linear_bf16`` runs the HIP decode GEMV for this call (GPU, bf16, <=
-    ``BF16_GEMV_MAX_ROWS`` rows, K % 64 == 0, N % 16 == 0 (% 32 for the fused GLU))."""
+# rows the bf16 ring GEMM (gemm_i8.hip ring2 kernel, bf16 MFMA) takes above the GEMV
+BF16_RING_MAX_ROWS = 256
+
+
+def bf16_decode_mode(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> int:
+    """Which HIP decode kernel ``linear_bf16`` runs for this call: 1 = ``gemv_bf16.hip`` (<=
+    ``BF16_GEMV_MAX_ROWS`` rows), 2 = the bf16 ring GEMM (up to 256 rows, from the extension's
+    ``bf16_ring_min_rows``), 0 = none (hipBLASLt).  GPU, bf16, K % 64 == 0, N % 16 == 0 (% 32 for
+    the fused GLU)."""
     K = x.shape[-1]
-    return (_gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_contiguous()
-            and 0 < x.numel() // max(K, 1) <= BF16_GEMV_MAX_ROWS and K % 64 == 0
-            and weight.shape[0] % (32 if glu else 16) == 0)
+    if not (_gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_contiguous()
+            and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0):
+        return 0
+    M = x.numel() // max(K, 1)
+    if 0 < M <= BF16_GEMV_MAX_ROWS:
+        return 1
+    if M <= BF16_RING_MAX_ROWS and M >= ext().bf16_ring_min_rows():
+        return 2
+    return 0
+
+
+def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bool:
+    """Whether ``linear_bf16`` runs a HIP decode kernel for this call (``bf16_decode_mode``)."""
+    return bf16_decode_mode(x, weight, glu) != 0
 
 
 def pack_bf16_weight(w: torch.Tensor) -> torch.Tensor:
@@ -308,9 +335,15 @@ def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = No
     is ``F.linear`` (hipBLASLt on GPU) followed by the activation op."""
     if glu:
         act = "silu_glu"
-    if bf16_gemv_ok(x, weight, glu):
+    mode = bf16_decode_mode(x, weight, glu)
+    if mode == 1 or (mode == 2 and act in (None, "silu_glu")):
         wp = packed if packed is not None else pack_bf16_weight(weight)
-        return ext().gemv_bf16(x, wp, bias, weight.shape[0], _GEMV_EPI[act])
+        if mode == 1:
+            return ext().gemv_bf16(x, wp, bias, weight.shape[0], _GEMV_EPI[act])
+        return ext().gemm_bf16_ring(x, wp, bias, weight.shape[0], 1 if glu else 0, 0)
+    if mode == 2:           # GELU MLPs: ring GEMM, then the activation kernel
+        wp = packed if packed is not None else pack_bf16_weight(weight)
+        return activation(ext().gemm_bf16_ring(x, wp, bias, weight.shape[0], 0, 0), act)
     y = torch.nn.functional.linear(x, weight, bias)
     return y if act is None else activation(y, act)
 

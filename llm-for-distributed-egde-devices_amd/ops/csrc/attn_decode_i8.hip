@@ -607,7 +607,50 @@ __global__ void __launch_bounds__(256) kv_quant_append_kernel(const bf16_t* __re
     if (dl == 0) sc[b * s_sb + h * s_sh + pos] = s;
   }
 }
+
+// Prefill history: dequantise int8 cache rows [b, h, t < T] (+ their per-(token, head) scales)
+// straight into a bf16 [B, Hkv, *, D] scratch (one 16-B int8 chunk -> 32 B of bf16 per lane) — the
+// rows chunked prefill attends to beside the new tokens, without fp32 temporaries.
+template <int D>
+__global__ void __launch_bounds__(256) kv_dequant_kernel(const int8_t* __restrict__ src, int64_t c_sb, int64_t c_sh,
+                                                         const float* __restrict__ sc, int64_t s_sb, int64_t s_sh,
+                                                         bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_sh, int Hkv,
+                                                         int T, int nrows) {
+  constexpr int LPK = D / 16, RPW = 64 / LPK;
+  const int lane = threadIdx.x & 63;
+  const int r = ((blockIdx.x * 256 + threadIdx.x) >> 6) * RPW + lane / LPK;
+  if (r >= nrows) return;
+  const int dl = lane % LPK;
+  const int t = r % T, bh = r / T, h = bh % Hkv, b = bh / Hkv;
+  const uint4 q = *reinterpret_cast<const uint4*>(src + b * c_sb + h * c_sh + (size_t)t * D + dl * 16);
+  const float s = sc[b * s_sb + h * s_sh + t];
+  const int8_t* qb = reinterpret_cast<const int8_t*>(&q);
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = (float)qb[i] * s;
+  bf16_t* o = dst + b * d_sb + h * d_sh + (size_t)t * D + dl * 16;
+  *reinterpret_cast<uint4*>(o) = pack8(v);
+  *reinterpret_cast<uint4*>(o + 8) = pack8(v + 8);
+}
 }  // namespace
+
+extern "C" int edge_kv_dequant(const void* src, int64_t c_sb, int64_t c_sh, const float* sc, int64_t s_sb,
+                               int64_t s_sh, void* dst, int64_t d_sb, int64_t d_sh, int B, int Hkv, int T, int D,
+                               hipStream_t st) {
+  const int nrows = B * Hkv * T;
+  if (nrows == 0) return 0;
+  const int rpw = 64 / (D / 16), waves = (nrows + rpw - 1) / rpw, blocks = (waves + 3) / 4;
+#define DQ(DD) hipLaunchKernelGGL(kv_dequant_kernel<DD>, dim3(blocks), dim3(256), 0, st, (const int8_t*)src, c_sb, c_sh, \
+                                  sc, s_sb, s_sh, (bf16_t*)dst, d_sb, d_sh, Hkv, T, nrows)
+  switch (D) {
+    case 64: DQ(64); break;
+    case 128: DQ(128); break;
+    case 256: DQ(256); break;
+    default: return -4;
+  }
+#undef DQ
+  return (int)hipGetLastError();
+}
 
 static int g_attn8_target_wg = 512;
 

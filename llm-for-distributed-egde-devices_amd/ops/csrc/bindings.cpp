@@ -79,6 +79,13 @@ int edge_kv_quant_append(const void* src, int64_t x_sb, int64_t x_sh, const int*
                          int64_t c_sh, float* sc, int64_t s_sb, int64_t s_sh, int B, int Hkv, int T, int D, int S,
                          hipStream_t st);
 void edge_decode_attn_occ(int occ);
+int edge_kv_dequant(const void* src, int64_t c_sb, int64_t c_sh, const float* sc, int64_t s_sb, int64_t s_sh, void* dst,
+                    int64_t d_sb, int64_t d_sh, int B, int Hkv, int T, int D, hipStream_t st);
+int edge_gemm_bf16_ring(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi, int S,
+                        hipStream_t st);
+int edge_bf16_ring_splits(int N, int K);
+void edge_bf16_ring_cfg(int cfg, int min_rows);
+int edge_bf16_ring_min_rows();
 void edge_decode_attn_gsplit(int v);
 }
 
@@ -442,6 +449,19 @@ void kv_quant_append(const at::Tensor& src, const at::Tensor& start_pos, int64_t
         "kv_quant_append");
 }
 
+// dst bf16 [B, Hkv, >= T, D] <- the first T int8 rows of cache (+ scales) of every (b, h)
+void kv_dequant(const at::Tensor& cache, const at::Tensor& scales, at::Tensor& dst, int64_t T) {
+  DEVICE_GUARD(cache);
+  const int64_t D = cache.size(3), B = cache.size(0), Hkv = cache.size(1);
+  check_cache8(cache, scales, "cache", D);
+  check_cache(dst, "dst", D);
+  TORCH_CHECK(dst.size(0) == B && dst.size(1) == Hkv && dst.size(2) >= T && cache.size(2) >= T, "dst geometry");
+  check(edge_kv_dequant(cache.data_ptr(), cache.stride(0), cache.stride(1), scales.data_ptr<float>(), scales.stride(0),
+                        scales.stride(1), dst.data_ptr(), dst.stride(0), dst.stride(1), (int)B, (int)Hkv, (int)T, (int)D,
+                        stream()),
+        "kv_dequant");
+}
+
 at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& start_pos, double scale, bool causal) {
   DEVICE_GUARD(q);
@@ -573,6 +593,35 @@ at::Tensor gemv_bf16_splitk(const at::Tensor& x, const at::Tensor& wp, const std
                               (int)M, (int)N, (int)K, (int)S, stream()),
         "gemv_bf16_splitk");
   return part;
+}
+
+// bf16 decode projection at 17-256 rows on the ring2 kernel (gemm_i8.hip, bf16 operand mode) over
+// the same fragment-packed weight as gemv_bf16.  epi 0: bf16 [.., N]; 1: SwiGLU over [gate | up]
+// -> bf16 [.., N / 2]; 3: split-K fp32 partial slices [S, M, N] (S = 0: the launcher's choice).
+at::Tensor gemm_bf16_ring(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
+                          int64_t epi, int64_t S) {
+  DEVICE_GUARD(x);
+  need(x, at::kBFloat16, "x");
+  need(wp, at::kBFloat16, "weight (packed)");
+  const int64_t K = x.size(-1), M = rows_of(x);
+  TORCH_CHECK(wp.numel() == N * K, "packed weight must hold N * K elements");
+  TORCH_CHECK(M >= 1 && M <= 256, "bf16 ring GEMM takes 1-256 rows");
+  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+  at::Tensor out;
+  if (epi == 3) {
+    if (S <= 0) S = edge_bf16_ring_splits((int)N, (int)K);
+    TORCH_CHECK(S > 1, "split-K bf16 ring needs >= 2 slices at this shape");
+    out = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  } else {
+    auto os = x.sizes().vec();
+    os.back() = epi == 1 ? N / 2 : N;
+    out = at::empty(os, x.options());
+    S = 1;
+  }
+  check(edge_gemm_bf16_ring(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M,
+                            (int)N, (int)K, (int)epi, (int)S, stream()),
+        "gemm_bf16_ring");
+  return out;
 }
 
 // LLM.int8 decode preparation (M <= 16): (q int8 [M, K] with the outlier columns zeroed, per-token
@@ -732,9 +781,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");
+  m.def("gemm_bf16_ring", &gemm_bf16_ring, "bf16 decode GEMM, 17-256 rows (ring2 kernel, bf16 MFMA)");
+  m.def("bf16_ring_splits", [](int64_t N, int64_t K) { return (int64_t)edge_bf16_ring_splits((int)N, (int)K); });
+  m.def("bf16_ring_min_rows", []() { return (int64_t)edge_bf16_ring_min_rows(); });
   m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]");
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("decode_attn_i8", &decode_attn_i8, "decode attention over an int8 KV cache, fused RoPE + quantising append");
+  m.def("kv_dequant", &kv_dequant, "dequantise the first T rows of an int8 KV cache into a bf16 scratch");
   m.def("kv_quant_append", &kv_quant_append, "quantise bf16 K/V rows into an int8 KV cache (prefill append)");
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
   m.def("w8a8_gemm_splitk", &w8a8_gemm_splitk);
@@ -763,6 +816,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);
     else if (what == "sample_rowwide") edge_sample_rowwide_min((int)a);
     else if (what == "prefill_fa") edge_prefill_fa((int)a);
+    else if (what == "bf16_ring") edge_bf16_ring_cfg((int)a, (int)b);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });
 }

@@ -1146,7 +1146,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // NTW / 2 tiles: the per-k-tile fold of the grouped scales (8 VALU per MFMA) then issues from two
 // waves per SIMD beside the other wave's MFMAs instead of serialising behind one wave's own.
 template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true, int MS = 1,
-          int NAL = 0, int NCW = 4>
+          int NAL = 0, int NCW = 4, int DT = 0>
 __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
@@ -1161,7 +1161,9 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   constexpr int LPW = WPW + (SC ? 1 : 0);             // loader pieces per stage (+ the scale piece)
   static_assert(WST % NWL == 0, "weight pieces split evenly over the loader waves");
   static_assert(DW * LPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
-  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTH == 8 && !SC), "epilogues");
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTH == 8 && !SC && DT == 0) ||
+                (EPI == EPI_GLU && NTH % 2 == 0 && DT == 1), "epilogues");
+  static_assert(DT == 0 || !SC, "bf16 operands carry no activation scales");
   static_assert(MS == 1 || MS == 2, "row split");
   static_assert(NAL == 0 || (16 % NAL == 0 && DA * (16 / NAL) <= 63), "activation loaders");
   // + EPK KiB: the workgroup's weight scales and bias (fp32, EPC columns each), staged once for the epilogue
@@ -1197,6 +1199,17 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   const int sbeg = EPI == EPI_PART ? (int)((int64_t)NSA * ks / S) : 0;
   const int NS = EPI == EPI_PART ? (int)((int64_t)NSA * (ks + 1) / S) - sbeg : NSA;
   const int nt0 = grp * NTW;
+  // physical weight tile of the workgroup's logical tile t.  EPI_GLU (bf16): W = [gate | up] in
+  // natural order (F = N / 2 rows each); logical tiles (2p, 2p + 1) = (gate, up) of feature tile
+  // nt0 / 2 + p, so the GLU epilogue pairs them as the blocked int8 layout does
+  auto phys_tile = [&](int t) -> int {
+    if constexpr (EPI == EPI_GLU) {
+      const int F16 = NTt >> 1, ft = min(nt0 / 2 + (t >> 1), F16 - 1);
+      return (t & 1) ? F16 + ft : ft;
+    } else {
+      return min(nt0 + t, NTt - 1);
+    }
+  };
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int mw = NCW == 8 ? (wave & 3) : wave, tb = NCW == 8 ? (wave >> 2) * NTH : 0;   // compute waves
   // k order rotated per workgroup (int32 sums: exact in any order; SC: a fixed per-workgroup fp32
@@ -1235,7 +1248,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
       const int q = lw * WPW + i, c = q / NTW, t = q % NTW;
-      woff[i] = ((uint32_t)min(nt0 + t, NTt - 1) * (uint32_t)KT + c) * 1024u + lane * 16;
+      woff[i] = ((uint32_t)phys_tile(t) * (uint32_t)KT + c) * 1024u + lane * 16;
     }
     // scale piece: lanes 0-31 the rows of k-tile 2 p, lanes 32-63 of 2 p + 1 (4 rows per lane)
     const uint32_t soff = (uint32_t)((lane >> 5) * Mpad + row0 + min(4 * (lane & 31), Mpad - row0 - 4));
@@ -1284,15 +1297,15 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   {
     const int c = threadIdx.x;                        // compute waves: >= 256 threads, <= 256 columns
     if (c < NTW * 16) {
-      const int col = min(nt0 * 16 + c, N - 1);
-      epi_sw[c] = sw[col];
+      const int col = min(phys_tile(c >> 4) * 16 + (c & 15), N - 1);
+      epi_sw[c] = sw != nullptr ? sw[col] : 1.f;
       epi_b[c] = bias != nullptr ? bf2f(bias[col]) : 0.f;
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   }
   float sa_r[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) sa_r[j] = SC ? 1.f : sa[row0 + min((2 * mw + j) * 16 + (lane & 15), Ml - 1)];
+  for (int j = 0; j < 2; ++j) sa_r[j] = SC || DT ? 1.f : sa[row0 + min((2 * mw + j) * 16 + (lane & 15), Ml - 1)];
   v4i acc[2][NTH];
   v4f accf[2][NTH];
 #pragma unroll
@@ -1333,6 +1346,17 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
 #pragma unroll
         for (int t = 0; t < NTH; ++t) fold1(accf[j][t], mfma_i8(f[2 + t], f[j], v4i{0, 0, 0, 0}), sg);
       }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(accf[j][t]));
+    } else if constexpr (DT == 1) {                   // bf16 x bf16 -> fp32, 32 k per 64 B
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < NTH; ++t)
+          accf[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8s, f[2 + t]),
+                                                              __builtin_bit_cast(v8s, f[j]), accf[j][t], 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1388,7 +1412,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float a = SC ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j];
+          const float a = SC || DT ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j];
           v[q] = a * epi_sw[cl + q] + ((EPI == EPI_OUT || ks == 0) ? epi_b[cl + q] : 0.f);
         }
         if (diag & 128) { asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])); continue; }
@@ -1401,6 +1425,29 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
           if (col + 3 < N && (N & 3) == 0) *reinterpret_cast<uint2*>(o) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
           else for (int q = 0; q < 4 && col + q < N; ++q) o[q] = f2bf(v[q]);
         }
+      }
+    }
+  } else if constexpr (EPI == EPI_GLU) {             // bf16: h = silu(gate) * up -> bf16 [M, N / 2]
+    const int Fo = N / 2, F16 = NTt >> 1;
+    bf16_t* h = reinterpret_cast<bf16_t*>(outv);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lrow = (2 * mw + j) * 16 + (lane & 15);
+      if (lrow >= Ml) continue;
+      const int row = row0 + lrow;
+#pragma unroll
+      for (int p = 0; p < NTH / 2; ++p) {
+        const int ft = (nt0 + tb) / 2 + p;
+        if (ft >= F16) continue;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cg = (tb + 2 * p) * 16 + g4 + q, cu = cg + 16;
+          const float g = bf2f(f2bf(accf[j][2 * p][q] * epi_sw[cg] + epi_b[cg]));     // the unfused GEMM output is bf16
+          const float u = bf2f(f2bf(accf[j][2 * p + 1][q] * epi_sw[cu] + epi_b[cu]));
+          v[q] = g / (1.f + __expf(-g)) * u;
+        }
+        *reinterpret_cast<uint2*>(h + (size_t)row * Fo + ft * 16 + g4) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
       }
     }
   } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
@@ -1921,4 +1968,85 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
                      (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
                      grid_m, grid_n);
   return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ bf16 ring2
+// bf16 decode projections at 17-256 rows on the ring2 kernel (DT = 1).  The bf16 fragment-packed
+// weight (ops.pack_bf16_weight: 1 KiB tiles of 16 rows x 32 k) and a row-major bf16 activation
+// have, BYTE for byte, the layout of the int8 operands (a 64-B k-tile = 32 bf16, lane l's 16 B =
+// k 8 (l >> 4) .. + 8 of row l & 15), so the kernel streams them unchanged with K counted in bytes
+// and swaps the MFMA for v_mfma_f32_16x16x32_bf16 (same 16 cycles per 64 B of k as the i8 form).
+// Rows 129-256 run as two 128-row halves that share each weight panel through one XCD's L2
+// (MS = 2), so a 256-row decode step reads the bf16 weights from HBM once.
+// cfg (EDGELLM_TUNE=bf16_ring=c[,max_rows]): 0 automatic, 1-3 alternative geometries (A/B);
+// max_rows: the bf16 ring path takes 17..max_rows rows (0 -> 256).
+static int g_bfr_cfg = 0, g_bfr_min = 17;
+extern "C" void edge_bf16_ring_cfg(int cfg, int min_rows) { g_bfr_cfg = cfg; g_bfr_min = min_rows > 0 ? min_rows : 17; }
+extern "C" int edge_bf16_ring_min_rows() { return g_bfr_min; }
+
+namespace {
+template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int NCWV, int EPV, int MSV>
+int launch_bfr(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int S, hipStream_t st) {
+  const int NTt = N / 16, G = (NTt + NTWV - 1) / NTWV * S;
+  const dim3 grid(MSV == 2 ? (G + 7) / 8 * 16 : G);
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, false, true, MSV, NALV, NCWV, 1>), grid,
+                     dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, nullptr, (const int8_t*)W, nullptr,
+                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G, 0);
+  return (int)hipGetLastError();
+}
+
+template <int MSV>
+int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi, int S,
+                 hipStream_t st) {
+  const int NTt = N / 16, c = g_bfr_cfg;
+  // logical workgroups wanted: ~256 launched blocks (MS = 2 launches each logical workgroup twice)
+  const int want = MSV == 2 ? 128 : 256;
+#define BFR(NTWV, NWLV, RWV, RAV, NALV, NCWV, EPV) \
+  return launch_bfr<NTWV, NWLV, RWV, RAV, NALV, NCWV, EPV, MSV>(A, W, bias, out, M, N, K, S, st)
+  if (epi == EPI_GLU) {                               // gate_up: NTW / 2 feature tiles per workgroup
+    const int ft = NTt / 2;
+    if (c == 1) BFR(4, 2, 10, 4, 2, 4, EPI_GLU);
+    if (c == 2) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
+    if (ft >= want * 6) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
+    if (ft >= want * 3) BFR(8, 2, 5, 4, 2, 4, EPI_GLU);
+    BFR(4, 2, 10, 4, 2, 4, EPI_GLU);
+  }
+  if (epi == EPI_PART) {                              // split-K slices (o / down before the norm)
+    const int per = NTt * S / want;
+    if (c == 1) BFR(2, 2, 14, 4, 2, 4, EPI_PART);
+    if (per >= 3) BFR(4, 2, 10, 4, 2, 4, EPI_PART);
+    if (per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_PART);
+    BFR(1, 2, 16, 4, 2, 4, EPI_PART);
+  }
+  const int per = (NTt + want / 2) / want;            // EPI_OUT
+  if (c == 1 && per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_OUT);
+  if (per >= 7) BFR(8, 2, 5, 4, 2, 4, EPI_OUT);
+  if (per >= 5) BFR(6, 2, 7, 4, 2, 4, EPI_OUT);
+  if (per >= 4) BFR(4, 2, 10, 4, 2, 4, EPI_OUT);
+  if (per >= 3) BFR(3, 2, 14, 4, 2, 4, EPI_OUT);
+  if (per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_OUT);
+  BFR(1, 2, 16, 4, 2, 4, EPI_OUT);
+#undef BFR
+}
+}  // namespace
+
+// Split-K slices S for the bf16 ring path's EPI_PART at this (N, K): >= 4 stages of 64 k per slice
+extern "C" int edge_bf16_ring_splits(int N, int K) {
+  const int stages = K / 64;                           // 128-B stages of bf16 k
+  const int NTt = N / 16;
+  int S = max(1, min(8, (256 + NTt / 2) / max(NTt, 1)));
+  while (S > 1 && stages < 4 * S) --S;
+  return S;
+}
+
+// y = x . W^T (+ bias) for bf16 x [M, K] and fragment-packed bf16 W (17 <= M <= 256, K % 64 == 0,
+// N % 16 == 0; GLU: N % 32 == 0).  epi 0: bf16 [M, N]; 1: silu(gate) * up bf16 [M, N / 2] over
+// W = [gate | up]; 3 (EPI_PART): fp32 partial slices [S, M, N] (bias in slice 0).  -2: not taken.
+extern "C" int edge_gemm_bf16_ring(const void* A, const void* W, const void* bias, void* out, int M, int N, int K,
+                                   int epi, int S, hipStream_t st) {
+  if (M < 1 || M > 256 || K % 64 != 0 || K <= 0 || N % 16 != 0 || (epi == EPI_GLU && N % 32 != 0)) return -2;
+  if (epi != EPI_OUT && epi != EPI_GLU && epi != EPI_PART) return -2;
+  if ((epi == EPI_PART) != (S > 1) || S < 1 || K / 64 < 4 * S) return -2;
+  return M > 128 ? bfr_dispatch<2>(A, W, bias, out, M, N, K, epi, S, st)
+                 : bfr_dispatch<1>(A, W, bias, out, M, N, K, epi, S, st);
 }

@@ -182,3 +182,32 @@ def test_generate_int8_kv_gpu_close_to_bf16(cuda):
     assert all(len(t) == 12 for t in r8.tokens)
     agree = sum(a == b for x, y in zip(r16.tokens, r8.tokens) for a, b in zip(x, y)) / 48
     assert agree >= 0.7, agree
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [64, 128, 256])
+def test_kv_dequant_kernel(cuda, D):
+    """int8 cache rows -> bf16 scratch (chunked-prefill history) == the fp32 reference rounded once."""
+    B, Hkv, S, T = 3, 2, 40, 29
+    g = torch.Generator().manual_seed(D + 1)
+    c = torch.randint(-127, 128, (B, Hkv, S, D), generator=g, dtype=torch.int8)
+    s = torch.rand(B, Hkv, S, generator=g) * 0.05
+    ref = (c[:, :, :T].float() * s[:, :, :T, None]).to(torch.bfloat16)
+    dst = torch.zeros(B, Hkv, S + 3, D, dtype=torch.bfloat16, device=cuda)
+    ops.kv_dequant(c.to(cuda), s.to(cuda), dst, T)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:, :, :T].cpu(), ref)
+    assert (dst[:, :, T:] == 0).all()
+
+
+def test_prefill_scratch_reused_across_layers():
+    """KVCache.prefill_scratch: one grow-only buffer per stream, views of the requested shape."""
+    from edgellm.engine import KVCache
+    cfg = tiny("llama2", hidden_size=256, num_heads=2, num_kv_heads=2, num_layers=2, intermediate_size=512)
+    kv = KVCache(cfg, 4, 64, kv_dtype="int8")
+    k1, v1 = kv.rows(0, 2).prefill_scratch(2, 30, torch.bfloat16, "cpu")
+    assert k1.shape == (2, 2, 30, cfg.head_dim) and k1.is_contiguous() and v1.is_contiguous()
+    k2, _ = kv.prefill_scratch(2, 20, torch.bfloat16, "cpu")
+    assert k2.data_ptr() == k1.data_ptr()                    # smaller request: same storage
+    k3, _ = kv.prefill_scratch(4, 64, torch.bfloat16, "cpu")
+    assert k3.shape == (4, 2, 64, cfg.head_dim)

@@ -510,6 +510,55 @@ def bf16_rows(C, dev, Ms=(8, 16, 32, 48, 64)):
     return out
 
 
+def bf16_ring_rows(C, dev, Ms=(32, 64, 128, 256)):
+    """bf16 decode projections at 17-256 rows (Llama-2-7B shapes), cache-cold: the bf16 ring GEMM
+    (gemm_i8.hip ring2 kernel in bf16 operand mode; geometry cfg 0 / 1 / 2 interleaved) against
+    hipBLASLt (torch.nn.functional.linear; gate_up + the SwiGLU kernel) and, up to 64 rows, the
+    gemv_bf16.hip GEMV.  o / down are timed in their split-K form (fp32 slices for the norm)."""
+    out = []
+    shapes = {"qkv": (12288, 4096, 0), "o": (4096, 4096, 3), "gate_up": (22016, 4096, 1), "down": (4096, 11008, 3),
+              "lm_head": (32000, 4096, 0)}
+    for name, (N, K, epi) in shapes.items():
+        ncopy = max(2, (1 << 30) // (2 * N * K) + 1)
+        ws = [(torch.randn(N, K, device=dev) * 0.02).bfloat16() for _ in range(ncopy)]
+        wps = [ops.pack_bf16_weight(w) for w in ws]
+        S = int(C.bf16_ring_splits(N, K)) if epi == 3 else 0
+        for M in Ms:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            ctr = [0]
+
+            def ring():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.gemm_bf16_ring(x, wps[ctr[0]], None, N, epi, S)
+
+            def blas():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                y = torch.nn.functional.linear(x, ws[ctr[0]])
+                return ops.activation(y, "silu_glu") if epi == 1 else y
+
+            def gemv():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.gemv_bf16(x, wps[ctr[0]], None, N, 1 if epi == 1 else 0)
+
+            res = {}
+            for _ in range(2):
+                for cfg in (0, 1, 2):
+                    C.tune("bf16_ring", cfg, 0)
+                    res.setdefault(f"ring_c{cfg}", []).append(timeit(ring, iters=10, per_graph=ncopy))
+                C.tune("bf16_ring", 0, 0)
+                res.setdefault("hipblaslt", []).append(timeit(blas, iters=10, per_graph=ncopy))
+                if M <= 64:
+                    res.setdefault("gemv", []).append(timeit(gemv, iters=10, per_graph=ncopy))
+            row = dict(op="bf16_ring", shape=name, M=M, N=N, K=K, S=S)
+            for k, ts in res.items():
+                row[k + "_us"] = round(min(ts), 2)
+                row[k + "_TBps"] = round(2 * N * K / min(ts) / 1e6, 2)
+            out.append(row)
+            print(row, flush=True)
+        del ws, wps
+    return out
+
+
 def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
     interleaved in one process ((form, issue): form 0 automatic, 2 / 3 the LDS-DMA ring kernel at
@@ -580,6 +629,8 @@ def main():
         rows += rows256_diag(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
+    if only is not None and "bf16ring" in only:
+        rows += bf16_ring_rows(C, dev)
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
