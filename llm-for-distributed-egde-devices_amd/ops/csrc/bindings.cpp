@@ -50,6 +50,7 @@ int edge_w8a8_rows256_ok(int K);
 int edge_w8a8_rows256_splits(int K);
 void edge_w8a8_rows256_cfg(int cfg, int nt);
 void edge_w8a8_rows256_diag(int v);
+void edge_w8a8_rows256_magic(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st);
 int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
@@ -63,6 +64,7 @@ void edge_w8a8_gemv_ring(int on);
 void edge_w8a8_prefill_gemm(int v, int b);
 void edge_w8a8_ring2_cfg(int v, int rot);
 void edge_w8a8_prefill_apack(int v);
+void edge_w8a8_prefill_prio(int v);
 void edge_w8a8_weight_nt(int v);
 int edge_w8a8_apack_ok(int M, int N, int K, int KT);
 int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
@@ -807,8 +809,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "ring2_cfg") edge_w8a8_ring2_cfg((int)a, (int)b);
     else if (what == "ring2_256") edge_w8a8_rows256_cfg((int)a, (int)b);
     else if (what == "ring2_256_diag") edge_w8a8_rows256_diag((int)a);
+    else if (what == "ring2_256_magic") edge_w8a8_rows256_magic((int)a);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);
+    else if (what == "prefill_prio") edge_w8a8_prefill_prio((int)a);
     else if (what == "weight_nt") edge_w8a8_weight_nt((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);

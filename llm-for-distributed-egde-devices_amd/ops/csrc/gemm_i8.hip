@@ -675,7 +675,9 @@ __device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_r
 //    the layout of the packed weights), so an A piece is 1 KiB of contiguous bytes instead of 16
 //    rows x 64 B — the pattern tools/ingest_bw.hip measured at ~18 B/clk/CU L2 -> LDS against
 //    ~60 for contiguous pieces.  The LDS image is identical, only the DMA source offsets change.
-template <int BMV, int ISS, bool APK = false>
+// PRIO: s_setprio(1) around each k-tile's MFMA cluster (cdna guide T5: keeps hipcc from moving the
+// MFMAs across the barriers into the fragment reads / DMA issue; A/B knob prefill_prio)
+template <int BMV, int ISS, bool APK = false, bool PRIO = false>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
@@ -785,6 +787,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
     __builtin_amdgcn_s_barrier();                     // stage s + 1 landed everywhere; slot of s free
     if constexpr (ISS == 0) issue(s + R);
     read_frags(s + 1, wx, ax);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     if constexpr (ISS == 2) {
       // DMA pieces interleaved into the MFMA stream: piece g after MFMA group g (a glds that
       // stalls on a full memory queue then holds back only the MFMAs behind it)
@@ -803,6 +806,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __r
       mma(wc, ac);
     }
     pin_acc();
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (ISS == 1) {
       asm volatile("" ::: "memory");                  // the pieces after every MFMA of the k-tile
       issue(s + R);
@@ -1153,7 +1157,9 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     int M, int N, int K, int NTt, int Mpad, int S = 1, int G = 0, int diag = 0) {
   // diag (speed diagnostics only, results are garbage): 1 no activation DMA, 2 no weight DMA,
   // 4 no MFMAs, 8 no LDS fragment reads and no MFMAs, 16 no epilogue, 32 exit at once, 64 the weight
-  // loaders re-read two k-tiles (weights L2-resident), 128 epilogue without its global stores
+  // loaders re-read two k-tiles (weights L2-resident), 128 epilogue without its global stores.
+  // Scheduling A/B bits (results exact): 256 compute waves at s_setprio 1 for the whole loop, 512
+  // loader waves at s_setprio 1, 1024 s_setprio 1 around each k-tile's MFMA cluster
   constexpr int MB = 8, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
   constexpr int NTH = NCW == 8 ? NTW / 2 : NTW;       // tiles per compute wave
   // GLUQ: a compute wave's tiles must be whole 64-feature quant groups (4 gate/up pairs): NTH == 8
@@ -1163,7 +1169,8 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   static_assert(DW * LPW <= 63 && DA * APW <= 63 && DA >= 1, "vmcnt range");
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTH == 8 && !SC && DT == 0) ||
                 (EPI == EPI_GLU && NTH % 2 == 0 && DT == 1), "epilogues");
-  static_assert(DT == 0 || !SC, "bf16 operands carry no activation scales");
+  static_assert(DT != 1 || !SC, "bf16 operands carry no activation scales");
+  static_assert(DT != 2 || SC, "the magic-number fold is a grouped-scale (SC) form");
   static_assert(MS == 1 || MS == 2, "row split");
   static_assert(NAL == 0 || (16 % NAL == 0 && DA * (16 / NAL) <= 63), "activation loaders");
   // + EPK KiB: the workgroup's weight scales and bias (fp32, EPC columns each), staged once for the epilogue
@@ -1232,6 +1239,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         for (int i = 0; i < APL; ++i)
           if (!(diag & 1)) glds16(ab + aoff[i], aring + ((st % RA) * 16 + al * APL + i) * 1024);
       };
+      if (diag & 512) __builtin_amdgcn_s_setprio(1);
       for (int st = 0; st < DA; ++st) issue(st);
       for (int s = 0; s < NS; ++s) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * APL) : "memory");   // own pieces of stage s
@@ -1266,6 +1274,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         if (smine) glds16(sa + (size_t)(2 * p) * Mpad + soff, sring + (st % RW) * 1024);
       }
     };
+    if (diag & 512) __builtin_amdgcn_s_setprio(1);
     for (int st = 0; st < DW; ++st) issue(st);
     for (int s = 0; s < NS; ++s) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DW - 1) * LPW) : "memory");   // own pieces of stage s
@@ -1336,10 +1345,51 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       for (int j = 0; j < 2; ++j) f[2 + NTH + j][0] = lds_read4(s0 + (st % RW) * 1024 + c * 512 + j * 64);
     }
   };
+  const bool pflip = (diag & 1024) != 0;
+  if (diag & 256) __builtin_amdgcn_s_setprio(1);
+  // DT == 2, the one-VALU fold: each k-tile's MFMA starts from the bit pattern of 1.5 * 2^23
+  // (0x4B400000) instead of 0, so the int32 sum (|sum| <= 64 * 127^2 < 2^22) lands in the low
+  // mantissa bits and the result, read as a float, is exactly 12582912 + sum: one v_fmac per
+  // element replaces cvt + fma.  The 12582912 * scale terms are taken out every 8 k-tiles from a
+  // per-row running scale sum (ssum), which keeps the accumulator's magnitude, and so its
+  // rounding, within 8 such terms.
+  constexpr float MAGIC_F = 12582912.f;
+  const v4i MAGIC_I = v4i{0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
+  float ssum[2] = {0.f, 0.f};
+  auto unbias = [&]() {
+    if constexpr (DT == 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float c = -MAGIC_F * ssum[j];
+#pragma unroll
+        for (int t = 0; t < NTH; ++t)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) accf[j][t][q] += c;
+        ssum[j] = 0.f;
+      }
+    }
+  };
   auto mma = [&](v4i (&f)[NF]) {
 #pragma unroll
     for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(f[i]));
-    if constexpr (SC) {
+    if (pflip) __builtin_amdgcn_s_setprio(1);
+    if constexpr (SC && DT == 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float sg = __builtin_bit_cast(float, f[2 + NTH + j][0]);
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) {
+          const v4i r = mfma_i8(f[2 + t], f[j], MAGIC_I);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) accf[j][t][q] = __builtin_fmaf(__builtin_bit_cast(float, r[q]), sg, accf[j][t][q]);
+        }
+        ssum[j] += sg;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(accf[j][t]));
+    } else if constexpr (SC) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float sg = __builtin_bit_cast(float, f[2 + NTH + j][0]);
@@ -1371,6 +1421,10 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
 #pragma unroll
         for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(acc[j][t]));
     }
+    if (pflip) {
+      if (diag & 256) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
   };
   // barrier k certifies stage k (both operands) and frees the slots of stage k - 1
   auto sync_stage = [&](int st) {
@@ -1392,6 +1446,9 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       if (rd) read_kt(s + 1, 0, x);
     }
     if (mm) mma(y);
+    if constexpr (DT == 2) {
+      if ((s & 3) == 3 || s + 1 == NS) unbias();     // wave-uniform; the last stage always
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1494,7 +1551,8 @@ extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_r
 static int g_w_nt = 1;
 extern "C" void edge_w8a8_weight_nt(int v) { g_w_nt = v; }
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel (BM = 128)
-static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1;
+static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0;
+extern "C" void edge_w8a8_prefill_prio(int v) { g_prefill_prio = v; }
 extern "C" void edge_w8a8_prefill_apack(int v) { g_prefill_apack = v; }
 // b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
 // MFMAs, 2 interleaved into them: the default, 1-3 % ahead of 0 on the Llama-2-7B shapes)
@@ -1650,12 +1708,12 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
 // Tiles per workgroup are chosen for ~256 launched workgroups (the logical grid doubles).
 // cfg (EDGELLM_TUNE=ring2_256=c[,nt]): A/B geometries; nt = 0 (cfg 0 only) selects normal weight
 // allocation instead of nontemporal (1-4 % slower at M = 256).  -1: no kernel for this call.
-static int g_r256_cfg = 0, g_r256_nt = 1, g_r256_diag = 0;
-template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV, int NCWV = 4>
+static int g_r256_cfg = 0, g_r256_nt = 1, g_r256_diag = 0, g_r256_magic = 1;
+template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV, int NCWV = 4, int DTV = 0>
 int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
                 int M, int N, int K, int Mpad, hipStream_t st, int S) {
   const int NTt = (N + 15) / 16, G = (NTt + NTWV - 1) / NTWV * S;
-  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV>),
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV, DTV>),
                      dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
   return (int)hipGetLastError();
@@ -1683,6 +1741,7 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
   do { if (scaled) R256(NTWV, NWLV, RWV, RAV, NALV, true); R256(NTWV, NWLV, RWV, RAV, NALV, false); } while (0)
 #define R256S8(NTWV, NWLV, RWV, RAV, NALV)                                                                       \
   do {                                                                                                        \
+    if (scaled && g_r256_magic) return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, true, true, 8, 2>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
     if (scaled) return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, true, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
     return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
   } while (0)
@@ -1738,6 +1797,8 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
 
 extern "C" void edge_w8a8_rows256_cfg(int cfg, int nt) { g_r256_cfg = cfg; g_r256_nt = nt; }
 extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
+// grouped-scale fold of the 256-row split-K kernels: 1 = one-VALU magic-number form, 0 = cvt + fma
+extern "C" void edge_w8a8_rows256_magic(int v) { g_r256_magic = v; }
 // split-K slices the 129-256-row kernels use for a K (0: none)
 extern "C" int edge_w8a8_rows256_splits(int K) { return K % 128 != 0 ? 0 : (K / 128 >= 64 ? 4 : 2); }
 // whether the 129-256-row decode kernels take this K (whole K; split-K at rows256_splits(K))
@@ -1906,6 +1967,12 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
     const int iss = g_prefill_iss;
+    if (g_prefill_prio && iss == 2) {
+      hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, false, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
+                         (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
+                         grid_m, grid_n);
+      return (int)hipGetLastError();
+    }
     if (iss == 1) BIGK(128, 1); else if (iss == 2) BIGK(128, 2); else BIGK(128, 0);
 #undef BIGK
     return (int)hipGetLastError();
@@ -1964,9 +2031,14 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
   const int NTt = (N + 15) / 16;
   const int grid_n = (NTt * 16 + 255) / 256;
   const int grid_m = (M + 127) / 128;
-  hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
-                     (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
-                     grid_m, grid_n);
+  if (g_prefill_prio)
+    hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
+                       (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
+                       grid_m, grid_n);
+  else
+    hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
+                       (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
+                       grid_m, grid_n);
   return (int)hipGetLastError();
 }
 
@@ -1980,8 +2052,11 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
 // (MS = 2), so a 256-row decode step reads the bf16 weights from HBM once.
 // cfg (EDGELLM_TUNE=bf16_ring=c[,max_rows]): 0 automatic, 1-3 alternative geometries (A/B);
 // max_rows: the bf16 ring path takes 17..max_rows rows (0 -> 256).
-static int g_bfr_cfg = 0, g_bfr_min = 17;
-extern "C" void edge_bf16_ring_cfg(int cfg, int min_rows) { g_bfr_cfg = cfg; g_bfr_min = min_rows > 0 ? min_rows : 17; }
+// Default row floor 65: at 17-64 rows the ring kernel still computes 128-row tiles and re-reads
+// the (clamped) activation lines, and hipBLASLt is ahead on qkv / gate_up (LM-head-wide N excepted:
+// edge_bf16_ring_min_rows_for)
+static int g_bfr_cfg = 0, g_bfr_min = 65;
+extern "C" void edge_bf16_ring_cfg(int cfg, int min_rows) { g_bfr_cfg = cfg; g_bfr_min = min_rows > 0 ? min_rows : 65; }
 extern "C" int edge_bf16_ring_min_rows() { return g_bfr_min; }
 
 namespace {
@@ -1991,7 +2066,7 @@ int launch_bfr(const void* A, const void* W, const void* bias, void* out, int M,
   const dim3 grid(MSV == 2 ? (G + 7) / 8 * 16 : G);
   hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, false, true, MSV, NALV, NCWV, 1>), grid,
                      dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, nullptr, (const int8_t*)W, nullptr,
-                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G, 0);
+                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G, g_r256_diag & ~255);
   return (int)hipGetLastError();
 }
 
@@ -2004,22 +2079,29 @@ int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int 
 #define BFR(NTWV, NWLV, RWV, RAV, NALV, NCWV, EPV) \
   return launch_bfr<NTWV, NWLV, RWV, RAV, NALV, NCWV, EPV, MSV>(A, W, bias, out, M, N, K, S, st)
   if (epi == EPI_GLU) {                               // gate_up: NTW / 2 feature tiles per workgroup
+    // one round of fat workgroups beats two rounds of thin ones (tools/bench_ops.py --only
+    // bf16ring, Llama-2-7B gate_up at 256 rows: 16 tiles / 172 blocks 64.4 us, 8 tiles / 344
+    // blocks 80.6 us)
     const int ft = NTt / 2;
     if (c == 1) BFR(4, 2, 10, 4, 2, 4, EPI_GLU);
     if (c == 2) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
-    if (ft >= want * 6) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
-    if (ft >= want * 3) BFR(8, 2, 5, 4, 2, 4, EPI_GLU);
+    if (c == 3) BFR(8, 2, 5, 4, 2, 4, EPI_GLU);
+    if (MSV == 2 && ft >= 8 * 64) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
+    if (ft >= 4 * 128) BFR(8, 2, 5, 4, 2, 4, EPI_GLU);
     BFR(4, 2, 10, 4, 2, 4, EPI_GLU);
   }
   if (epi == EPI_PART) {                              // split-K slices (o / down before the norm)
     const int per = NTt * S / want;
     if (c == 1) BFR(2, 2, 14, 4, 2, 4, EPI_PART);
+    if (per >= 6) BFR(8, 2, 5, 4, 2, 4, EPI_PART);
     if (per >= 3) BFR(4, 2, 10, 4, 2, 4, EPI_PART);
     if (per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_PART);
     BFR(1, 2, 16, 4, 2, 4, EPI_PART);
   }
   const int per = (NTt + want / 2) / want;            // EPI_OUT
   if (c == 1 && per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_OUT);
+  if (c == 3 && per >= 7) BFR(8, 2, 5, 4, 2, 4, EPI_OUT);
+  if (per >= 12) BFR(16, 2, 3, 3, 2, 8, EPI_OUT);     // LM heads: one round (32000 x 4096 at 256 rows)
   if (per >= 7) BFR(8, 2, 5, 4, 2, 4, EPI_OUT);
   if (per >= 5) BFR(6, 2, 7, 4, 2, 4, EPI_OUT);
   if (per >= 4) BFR(4, 2, 10, 4, 2, 4, EPI_OUT);
@@ -2033,8 +2115,9 @@ int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int 
 // Split-K slices S for the bf16 ring path's EPI_PART at this (N, K): >= 4 stages of 64 k per slice
 extern "C" int edge_bf16_ring_splits(int N, int K) {
   const int stages = K / 64;                           // 128-B stages of bf16 k
+  // two slices halve each workgroup's activation re-reads; narrow N takes more to fill the chip
   const int NTt = N / 16;
-  int S = max(1, min(8, (256 + NTt / 2) / max(NTt, 1)));
+  int S = NTt >= 192 ? 2 : (NTt >= 64 ? 4 : 8);
   while (S > 1 && stages < 4 * S) --S;
   return S;
 }
@@ -2046,7 +2129,7 @@ extern "C" int edge_gemm_bf16_ring(const void* A, const void* W, const void* bia
                                    int epi, int S, hipStream_t st) {
   if (M < 1 || M > 256 || K % 64 != 0 || K <= 0 || N % 16 != 0 || (epi == EPI_GLU && N % 32 != 0)) return -2;
   if (epi != EPI_OUT && epi != EPI_GLU && epi != EPI_PART) return -2;
-  if ((epi == EPI_PART) != (S > 1) || S < 1 || K / 64 < 4 * S) return -2;
+  if ((epi == EPI_PART) != (S > 1) || S < 1 || (S > 1 && K / 64 < 4 * S)) return -2;
   return M > 128 ? bfr_dispatch<2>(A, W, bias, out, M, N, K, epi, S, st)
                  : bfr_dispatch<1>(A, W, bias, out, M, N, K, epi, S, st);
 }

@@ -400,14 +400,16 @@ def test_gemv_bf16_glu(cuda, M, F, K):
 
 
 def test_linear_bf16_routes_decode_rows(cuda):
-    """ops.linear_bf16: <= BF16_GEMV_MAX_ROWS rows take the HIP GEMV, 17-256 the bf16 ring GEMM,
-    larger batches hipBLASLt; all three agree."""
+    """ops.linear_bf16: <= BF16_GEMV_MAX_ROWS rows take the HIP GEMV, bf16_ring_min_rows..256 the
+    bf16 ring GEMM, the rest hipBLASLt; all three agree."""
     torch.manual_seed(0)
     n = ops.BF16_GEMV_MAX_ROWS
     w = (torch.randn(4096, 2048, device=cuda) * 0.05).bfloat16()
     x = torch.randn(300, 2048, device=cuda).bfloat16()
-    assert ops.bf16_decode_mode(x[:n], w) == 1 and ops.bf16_decode_mode(x[:n + 1], w) == 2
+    lo = int(ops.ext().bf16_ring_min_rows())
+    assert ops.bf16_decode_mode(x[:n], w) == 1 and ops.bf16_decode_mode(x[:lo], w) == 2
     assert ops.bf16_decode_mode(x[:256], w) == 2 and ops.bf16_decode_mode(x, w) == 0
+    assert lo == n + 1 or ops.bf16_decode_mode(x[:n + 1], w) == 0
     small = ops.linear_bf16(x[:n].contiguous(), w)
     ring = ops.linear_bf16(x[:256].contiguous(), w)
     big = ops.linear_bf16(x, w)

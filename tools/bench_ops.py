@@ -542,7 +542,7 @@ def bf16_ring_rows(C, dev, Ms=(32, 64, 128, 256)):
 
             res = {}
             for _ in range(2):
-                for cfg in (0, 1, 2):
+                for cfg in (0, 1, 2, 3):
                     C.tune("bf16_ring", cfg, 0)
                     res.setdefault(f"ring_c{cfg}", []).append(timeit(ring, iters=10, per_graph=ncopy))
                 C.tune("bf16_ring", 0, 0)
@@ -556,6 +556,104 @@ def bf16_ring_rows(C, dev, Ms=(32, 64, 128, 256)):
             out.append(row)
             print(row, flush=True)
         del ws, wps
+    return out
+
+
+def prio_rows(C, dev):
+    """Wave-priority A/B (cdna guide T5 / MI355X microarch item 4), interleaved in one process:
+    the 256-row decode GEMMs (ring2_256_diag scheduling bits: 256 compute waves prio 1, 512 loader
+    waves prio 1, 1024 prio 1 around each MFMA cluster; results exact) and the prefill GEMM
+    (prefill_prio: setprio around each k-tile's MFMA cluster)."""
+    out = []
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
+    bits = (0, 256, 512, 1024, 256 | 1024)
+    for name, (N, K) in shapes.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        ws = [ops.pack_int8_weight(torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)) for _ in range(ncopy)]
+        s2 = torch.rand(N, device=dev) * 0.01
+        M = 256
+        a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        s1 = torch.rand(M, device=dev) * 0.01
+        ctr = [0]
+        if name in ("o", "down"):
+            KT = K // 64
+            sg = torch.rand(KT, M, device=dev) * 0.01
+
+            def call():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.w8a8_gemm_splitk(a, sg, ws[ctr[0]], s2, None, N, K, 0)
+        elif name == "gate_up":
+            def call():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.w8a8_gemm_gluq(a, s1, ws[ctr[0]], s2, None, N, K)
+        else:
+            def call():
+                ctr[0] = (ctr[0] + 1) % ncopy
+                return C.w8a8_gemm(a, s1, ws[ctr[0]], s2, None, N, K)
+        res = {}
+        for _ in range(2):
+            for b in bits:
+                C.tune("ring2_256_diag", b, 0)
+                res.setdefault(b, []).append(timeit(call, iters=10, per_graph=ncopy))
+        C.tune("ring2_256_diag", 0, 0)
+        row = dict(op="rows256_prio", shape=name, M=M, N=N, K=K)
+        for b, ts in res.items():
+            row[f"bits{b}_us"] = round(min(ts), 2)
+        out.append(row)
+        print(row, flush=True)
+        del ws
+        for Mp in (2048, 16384):
+            w = ops.pack_int8_weight(torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev))
+            ap = torch.randint(-127, 128, (Mp, K), dtype=torch.int8, device=dev)
+            sp = torch.rand(Mp, device=dev) * 0.01
+            res = {}
+            per = max(2, min(20, int(4e11 // (Mp * N * K))))
+            for _ in range(2):
+                for pr in (0, 1):
+                    C.tune("prefill_prio", pr, 0)
+                    res.setdefault(pr, []).append(timeit(lambda: C.w8a8_gemm(ap, sp, w, s2, None, N, K), iters=5,
+                                                         per_graph=per))
+            C.tune("prefill_prio", 0, 0)
+            row = dict(op="prefill_prio", shape=name, M=Mp, N=N, K=K)
+            for pr, ts in res.items():
+                row[f"prio{pr}_TOPs"] = round(2 * Mp * N * K / min(ts) / 1e6, 1)
+            out.append(row)
+            print(row, flush=True)
+    return out
+
+
+def magic_rows(C, dev, M=256):
+    """Grouped-scale fold A/B at 256 rows (o / down split-K, interleaved): ring2_256_magic 1 (one
+    v_fmac per element on a magic-number-biased MFMA result) vs 0 (cvt + fma); plus the largest
+    difference between the two outputs relative to the output's scale."""
+    out = []
+    shapes = {"o": (4096, 4096), "down": (4096, 11008)}
+    for name, (N, K) in shapes.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        ws = [ops.pack_int8_weight(torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)) for _ in range(ncopy)]
+        s2 = torch.rand(N, device=dev) * 0.01
+        a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        sg = torch.rand(K // 64, M, device=dev) * 0.01
+        ctr = [0]
+
+        def call():
+            ctr[0] = (ctr[0] + 1) % ncopy
+            return C.w8a8_gemm_splitk(a, sg, ws[ctr[0]], s2, None, N, K, 0)
+        res = {}
+        for _ in range(3):
+            for mg in (1, 0):
+                C.tune("ring2_256_magic", mg, 0)
+                res.setdefault(mg, []).append(timeit(call, iters=10, per_graph=ncopy))
+        outs = {}
+        for mg in (1, 0):
+            C.tune("ring2_256_magic", mg, 0)
+            outs[mg] = C.w8a8_gemm_splitk(a, sg, ws[0], s2, None, N, K, 0).sum(0)
+        C.tune("ring2_256_magic", 1, 0)
+        err = ((outs[1] - outs[0]).abs().max() / outs[0].abs().max()).item()
+        row = dict(op="rows256_fold", shape=name, M=M, N=N, K=K, magic_us=round(min(res[1]), 2),
+                   exact_us=round(min(res[0]), 2), max_rel_diff=err)
+        out.append(row)
+        print(row, flush=True)
     return out
 
 
@@ -629,6 +727,10 @@ def main():
         rows += rows256_diag(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
+    if only is not None and "magic" in only:
+        rows += magic_rows(C, dev)
+    if only is not None and "prio" in only:
+        rows += prio_rows(C, dev)
     if only is not None and "bf16ring" in only:
         rows += bf16_ring_rows(C, dev)
     if a.out:
