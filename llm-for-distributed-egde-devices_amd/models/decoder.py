@@ -174,7 +174,7 @@ class MLP(nn.Module):
                 and ops.bf16_gemv_ok(x, self.up.weight, glu=True):
             # bf16 decode: gate_up GEMV with the SwiGLU epilogue (one launch, gemv_bf16.hip)
             return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, glu=True,
-                                             packed=self.up.decode_weight(x)))
+                                             packed=self.up.decode_weight(x, glu=True)))
         if self.act in ("gelu_tanh", "gelu") and type(self.up) is Linear and not down_q \
                 and not isinstance(x, QAct) and ops.bf16_gemv_ok(x, self.up.weight):
             # bf16 decode (Phi-2, Pythia): up-projection GEMV with the GELU epilogue

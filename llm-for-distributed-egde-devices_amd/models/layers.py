@@ -62,7 +62,7 @@ class Linear(nn.Module):
         wp = self.decode_weight(x)
         if self.split_k_out and wp is not None:
             K = x.shape[-1]
-            if ops.bf16_decode_mode(x, self.weight) == 2:
+            if ops.bf16_decode_mode(x, self.weight, split=True) == 2:
                 # 17-256 rows: the ring GEMM's split-K slices (the launcher picks S for the shape)
                 S = int(ops.ext().bf16_ring_splits(self.out_features, K))
                 if S > 1:
@@ -73,10 +73,10 @@ class Linear(nn.Module):
                                                              self.out_features, self.split_k_out))
         return ops.linear_bf16(x, self.weight, self.bias, packed=wp)
 
-    def decode_weight(self, x) -> "Optional[torch.Tensor]":
-        """Fragment-packed copy of the weight for the decode GEMV (``gemv_bf16.hip``), built on the
-        first decode-sized call (before any graph capture) and kept; None when not applicable."""
-        if not ops.bf16_gemv_ok(x, self.weight):
+    def decode_weight(self, x, glu: bool = False) -> "Optional[torch.Tensor]":
+        """Fragment-packed copy of the weight for the decode GEMV / ring GEMM, built on the first
+        decode-sized call (before any graph capture) and kept; None when not applicable."""
+        if not ops.bf16_decode_mode(x, self.weight, glu=glu, split=bool(self.split_k_out)):
             return None
         wp, ver = getattr(self, "_wp", None), self.weight._version   # in-place weight edits repack
         if wp is None or getattr(self, "_wp_ver", -1) != ver or wp.device != self.weight.device:

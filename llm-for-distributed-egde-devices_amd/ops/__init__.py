@@ -294,11 +294,12 @@ BF16_GEMV_MAX_ROWS = int(os.environ.get("EDGELLM_BF16_GEMV_ROWS", "16"))
 BF16_RING_MAX_ROWS = 256
 
 
-def bf16_decode_mode(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> int:
+def bf16_decode_mode(x: torch.Tensor, weight: torch.Tensor, glu: bool = False, split: bool = False) -> int:
     """Which HIP decode kernel ``linear_bf16`` runs for this call: 1 = ``gemv_bf16.hip`` (<=
     ``BF16_GEMV_MAX_ROWS`` rows), 2 = the bf16 ring GEMM (up to 256 rows, from the extension's
-    ``bf16_ring_min_rows`` (65), or from 17 rows for LM-head-wide N >= 16384), 0 = none
-    (hipBLASLt; measured ahead of the ring on qkv / gate_up at 17-64 rows).  GPU, bf16, K % 64 == 0, N % 16 == 0 (% 32 for
+    ``bf16_ring_min_rows`` (65), or from 17 rows for the fused SwiGLU, split-K outputs and
+    LM-head-wide N >= 16384), 0 = none (hipBLASLt; measured ahead of the ring on qkv at 17-64
+    rows).  GPU, bf16, K % 64 == 0, N % 16 == 0 (% 32 for
     the fused GLU)."""
     K = x.shape[-1]
     if not (_gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_contiguous()
@@ -308,8 +309,10 @@ def bf16_decode_mode(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -
     if 0 < M <= BF16_GEMV_MAX_ROWS:
         return 1
     lo = ext().bf16_ring_min_rows()
-    if not glu and weight.shape[0] >= 16384:
-        lo = min(lo, BF16_GEMV_MAX_ROWS + 1)          # LM-head-wide N: the ring wins from 17 rows
+    if glu or split or weight.shape[0] >= 16384:
+        # SwiGLU, split-K (o / down) and LM-head-wide N: the ring is ahead from 17 rows
+        # (profiles/bench_ops_r3_bf16ring_b.json); narrow plain outputs (qkv) from the default
+        lo = min(lo, BF16_GEMV_MAX_ROWS + 1)
     if lo <= M <= BF16_RING_MAX_ROWS:
         return 2
     return 0

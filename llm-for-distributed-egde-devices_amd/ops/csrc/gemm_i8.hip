@@ -1353,8 +1353,12 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   // element replaces cvt + fma.  The 12582912 * scale terms are taken out every 8 k-tiles from a
   // per-row running scale sum (ssum), which keeps the accumulator's magnitude, and so its
   // rounding, within 8 such terms.
+  // (hipcc, ROCm 7.2: with the MFMA's i32 result reinterpreted as float element by element and no
+  // pin on it, the generated code read only element 0 of the result for all four accumulator
+  // elements; the opaque C operand and the pinned result below give the correct per-element form)
   constexpr float MAGIC_F = 12582912.f;
-  const v4i MAGIC_I = v4i{0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
+  v4i MAGIC_I = v4i{0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
+  asm volatile("" : "+v"(MAGIC_I));
   float ssum[2] = {0.f, 0.f};
   auto unbias = [&]() {
     if constexpr (DT == 2) {
@@ -1379,9 +1383,11 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         const float sg = __builtin_bit_cast(float, f[2 + NTH + j][0]);
 #pragma unroll
         for (int t = 0; t < NTH; ++t) {
-          const v4i r = mfma_i8(f[2 + t], f[j], MAGIC_I);
+          v4i r = mfma_i8(f[2 + t], f[j], MAGIC_I);
+          asm volatile("" : "+v"(r));                 // (see MAGIC_F: keeps the four elements apart)
+          const v4f rf = __builtin_bit_cast(v4f, r);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) accf[j][t][q] = __builtin_fmaf(__builtin_bit_cast(float, r[q]), sg, accf[j][t][q]);
+          for (int q = 0; q < 4; ++q) accf[j][t][q] = __builtin_fmaf(rf[q], sg, accf[j][t][q]);
         }
         ssum[j] += sg;
       }

@@ -57,10 +57,15 @@ def test_rows256_out(cuda, cfg, nt, M, N, K):
 
 @pytest.mark.parametrize("cfg,nt", [(0, 0), (0, 1), (1, 1), (2, 1), (3, 1)])
 @pytest.mark.parametrize("M", [129, 200, 256])
-@pytest.mark.parametrize("grouped", [True, False])
+@pytest.mark.parametrize("grouped,magic", [(True, 1), (True, 0), (False, 1)])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008), (1024, 14336)])
-def test_rows256_splitk(cuda, cfg, nt, M, grouped, N, K):
+def test_rows256_splitk(cuda, cfg, nt, M, grouped, magic, N, K):
+    """Split-K slices vs the fp32 reference.  Grouped scales, default geometry: the one-VALU
+    magic-number fold (gemm_i8.hip DT = 2) rounds within 8 biased terms per accumulator, so it is
+    held to 1e-4 of the output's largest magnitude (measured 4.2-4.7e-5); the exact cvt + fma
+    fold (magic 0) and every other form to the exact-integer tolerance."""
     C = ops.ext()
+    C.tune("ring2_256_magic", magic, 0)
     torch.manual_seed(M * 7 + K)
     Mpad = (M + 15) // 16 * 16
     qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
@@ -69,14 +74,18 @@ def test_rows256_splitk(cuda, cfg, nt, M, grouped, N, K):
     sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
     bias = torch.randn(N, device=cuda).to(torch.bfloat16)
     wp = ops.pack_int8_weight(w)
-    with _tuned(C, cfg, nt):
-        parts = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, 0)
-        again = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, 0)
+    try:
+        with _tuned(C, cfg, nt):
+            parts = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, 0)
+            again = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, 0)
+    finally:
+        C.tune("ring2_256_magic", 1, 0)
     S = 4 if K // 128 >= 64 else 2
     assert parts.shape == (S, M, N)
     assert torch.equal(parts, again)
     ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
-    _close(parts.sum(0), ref, 1e-3, 1e-2)
+    atol = max(1e-3, 1e-4 * ref.abs().max().item()) if grouped and magic and cfg == 0 else 1e-3
+    _close(parts.sum(0), ref, atol, 1e-2)
 
 
 @pytest.mark.parametrize("cfg,nt", [(0, 0), (0, 1), (1, 1), (2, 1), (3, 1), (5, 1)])
