@@ -110,6 +110,34 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   const bf16_t* kb = kc + b * c_sb + kvh * c_sh + (size_t)start * D;
   const bf16_t* vb = vc + b * c_sb + kvh * c_sh + (size_t)start * D;
 
+  // K / V loads of UNROLL key groups from `base`: rows at or past `bound` load row 0 (unconditional
+  // 16-byte loads; consume() masks every key past nl)
+  constexpr int STEP = KPB * UNROLL;      // keys per workgroup per chunk
+  const int dc = dvalid ? d0 : 0;
+  auto load_b = [&](int base, int bound, uint4 (&kr)[UNROLL], uint4 (&vr)[UNROLL]) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = base + kl + u * KPB;
+      const size_t off = (size_t)(k < bound ? k : 0) * D + dc;
+      if constexpr (OCC > 0) {                   // read once per step: nontemporal
+        kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + off)));
+        vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + off)));
+      } else {
+        kr[u] = *reinterpret_cast<const uint4*>(kb + off);
+        vr[u] = *reinterpret_cast<const uint4*>(vb + off);
+      }
+    }
+  };
+  // OCC > 0: the wave's first chunk goes out now, before the q / RoPE / append work below (it
+  // needs only the split's start and length), so one memory round trip of each workgroup's
+  // critical path overlaps the q loads.  Bound n, not nl: in the split that owns the new position
+  // that row may load stale, and consume() masks it (key nl) like every key past nl.
+  const int base0 = wave * KPW;
+  uint4 ka[UNROLL], va[UNROLL];
+  if constexpr (OCC > 0) {
+    if (base0 < n) load_b(base0, n, ka, va);
+  }
+
   // q first: its loads (and the RoPE partner loads) overlap the KV append below
   float qf[G][8];
 #pragma unroll
@@ -186,8 +214,6 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   // (two register buffers, alternated by a 2x unrolled loop: copying a buffer that still has
   // loads outstanding would force a full wait).  Out-of-range keys load a clamped row and are
   // masked in the score (unconditional 16-byte loads; a conditional one compiles to branches).
-  constexpr int STEP = KPB * UNROLL;      // keys per workgroup per chunk
-  const int dc = dvalid ? d0 : 0;
   float m[G], l[G], acc[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
@@ -196,20 +222,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
   }
-  auto load = [&](int base, uint4 (&kr)[UNROLL], uint4 (&vr)[UNROLL]) {
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = base + kl + u * KPB;
-      const size_t off = (size_t)(k < nl ? k : 0) * D + dc;
-      if constexpr (OCC > 0) {                   // read once per step: nontemporal
-        kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + off)));
-        vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + off)));
-      } else {
-        kr[u] = *reinterpret_cast<const uint4*>(kb + off);
-        vr[u] = *reinterpret_cast<const uint4*>(vb + off);
-      }
-    }
-  };
+  auto load = [&](int base, uint4 (&kr)[UNROLL], uint4 (&vr)[UNROLL]) { load_b(base, nl, kr, vr); };
   auto consume = [&](int base, const uint4 (&kr)[UNROLL], const uint4 (&vr)[UNROLL]) {
     float s[UNROLL][G];
 #pragma unroll
@@ -285,13 +298,12 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     }
   }
   if constexpr (OCC > 0) {
-    uint4 ka[UNROLL], va[UNROLL];
-    for (int base = wave * KPW; base < nl; base += STEP) {  // wave-uniform trip count (shuffles inside)
-      load(base, ka, va);
+    for (int base = base0; base < nl; base += STEP) {  // wave-uniform trip count (shuffles inside)
+      if (base != base0) load(base, ka, va);           // the first chunk was issued at entry
       consume(base, ka, va);
     }
   } else {
-    uint4 ka[UNROLL], va[UNROLL], kb2[UNROLL], vb2[UNROLL];
+    uint4 kb2[UNROLL], vb2[UNROLL];
     int base = wave * KPW;                           // wave-uniform trip count (shuffles inside)
     if (base < nl) load(base, ka, va);
     while (base < nl) {

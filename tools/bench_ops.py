@@ -166,7 +166,7 @@ def other_rows(C, dev, only=None):
                             TBps=round(nbytes / t / 1e6, 2)))
             print(out[-1], flush=True)
         C.tune("decode_attn", 0, 0)
-    for Bf, L in (((64, 160), (128, 160), (128, 512)) if want("attn_fused") else ()):
+    for Bf, L in (((64, 160), (128, 160), (256, 150), (128, 512)) if want("attn_fused") else ()):
         # the model's decode attention: RoPE + KV append + attention + per-(token, 64) int8 output
         S = L + 8
         qkv = torch.randn(Bf, 3 * Hq * D, device=dev).bfloat16()
