@@ -35,6 +35,7 @@ struct Fuse {
   float* out_s;         // QOUT: [(Hq*D)/64][Mpad] scales
   int Mpad;
   int gs;               // query heads of one KV head split over gs workgroups (G = 1 in the kernel)
+  int early;            // OCC > 0: issue the first K/V chunk at kernel entry (A/B knob decode_attn_early)
 };
 
 // Rotate the 8 values at head offset e0 (HF rotate_half convention), x/partner read from `head`.
@@ -135,7 +136,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   const int base0 = wave * KPW;
   uint4 ka[UNROLL], va[UNROLL];
   if constexpr (OCC > 0) {
-    if (base0 < n) load_b(base0, n, ka, va);
+    if (fz.early && base0 < n) load_b(base0, n, ka, va);
   }
 
   // q first: its loads (and the RoPE partner loads) overlap the KV append below
@@ -299,7 +300,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   }
   if constexpr (OCC > 0) {
     for (int base = base0; base < nl; base += STEP) {  // wave-uniform trip count (shuffles inside)
-      if (base != base0) load(base, ka, va);           // the first chunk was issued at entry
+      if (base != base0 || !fz.early) load(base, ka, va);   // (early: the first chunk went out at entry)
       consume(base, ka, va);
     }
   } else {
@@ -414,8 +415,9 @@ static int g_target_wg = 512;   // >= 2 workgroups per CU before splitting K
 // sequences x 32 heads, context 160 (tools/bench_ops.py attn_fused): 57.7 / 60.4 / 66.6 us.
 static int g_attn_occ = 4;
 // query-head split for small grids (tune "decode_attn_gsplit"): 0 automatic, 1 off, 2 always (GQA)
-static int g_attn_gsplit = 0;
+static int g_attn_gsplit = 0, g_attn_early = 1;
 extern "C" void edge_decode_attn_gsplit(int v) { g_attn_gsplit = v; }
+extern "C" void edge_decode_attn_early(int v) { g_attn_early = v; }
 extern "C" void edge_decode_attn_config(int target_wg) { g_target_wg = target_wg > 0 ? target_wg : 512; }
 extern "C" void edge_decode_attn_occ(int occ) { g_attn_occ = occ == 0 || occ == 5 ? occ : 4; }
 
@@ -482,7 +484,7 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
   const bool gs_ok = G0 > 1 && (!fused || g_attn_occ != 0);
   const int gs = gs_ok && (g_attn_gsplit == 2 || (g_attn_gsplit == 0 && B * Hkv * nsplit < 128)) ? G0 : 1;
   const int G = G0 / gs;
-  const Fuse fz{pos, cs, fused ? rot : 0, q_sb, (int8_t*)out_q, out_s, Mpad, gs};
+  const Fuse fz{pos, cs, fused ? rot : 0, q_sb, (int8_t*)out_q, out_s, Mpad, gs, g_attn_early};
   const float sl2 = scale * 1.4426950408889634f;
   const size_t lds = (size_t)(NW * G * D + 2 * NW * G + 2 * G) * sizeof(float);
   const dim3 grid(nsplit, Hkv * gs, B);

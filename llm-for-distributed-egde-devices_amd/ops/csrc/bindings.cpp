@@ -89,6 +89,7 @@ int edge_bf16_ring_splits(int N, int K);
 void edge_bf16_ring_cfg(int cfg, int min_rows);
 int edge_bf16_ring_min_rows();
 void edge_decode_attn_gsplit(int v);
+void edge_decode_attn_early(int v);
 }
 
 namespace {
@@ -817,6 +818,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
     else if (what == "decode_attn_gsplit") edge_decode_attn_gsplit((int)a);
+    else if (what == "decode_attn_early") edge_decode_attn_early((int)a);
     else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);
     else if (what == "sample_rowwide") edge_sample_rowwide_min((int)a);
     else if (what == "prefill_fa") edge_prefill_fa((int)a);

@@ -174,14 +174,17 @@ def other_rows(C, dev, only=None):
         vc = torch.randn_like(kc)
         sl = torch.full((Bf,), L, dtype=torch.int32, device=dev)
         rope = ops.rope_tables(D, S, 10000.0, device=dev)
-        for occ in (0, 4, 5):
+        for occ, early in ((0, 1), (4, 0), (4, 1), (5, 0), (5, 1)):
             C.tune("decode_attn_occ", occ, 0)
-            t = timeit(lambda: C.decode_attn_fused(qkv, sl - 1, rope, kc, vc, sl, Hq, 1 / math.sqrt(D), L, D, True))
+            C.tune("decode_attn_early", early, 0)
+            t = min(timeit(lambda: C.decode_attn_fused(qkv, sl - 1, rope, kc, vc, sl, Hq, 1 / math.sqrt(D), L, D,
+                                                       True)) for _ in range(2))
             nbytes = 2 * Bf * Hq * L * D * 2
-            out.append(dict(op="decode_attn_fused_q", B=Bf, Hkv=Hq, ctx=L, occ=occ, us=round(t, 2),
+            out.append(dict(op="decode_attn_fused_q", B=Bf, Hkv=Hq, ctx=L, occ=occ, early=early, us=round(t, 2),
                             TBps=round(nbytes / t / 1e6, 2)))
             print(out[-1], flush=True)
         C.tune("decode_attn_occ", 4, 0)
+        C.tune("decode_attn_early", 1, 0)
     if want("small"):
         out += small_rows(C, dev, B, H, Hq, D)
     if want("sample"):
