@@ -170,6 +170,12 @@ class MLP(nn.Module):
                 return self.down(self.up.glu(x))
             return self.down(act_fn(self.up(x), "silu_glu_blocked", True))
         down_q = getattr(self.down, "takes_quantized_input", False)
+        if self.act in ("gelu_tanh", "gelu") and down_q and isinstance(x, QAct) and x.q.dim() == 2 \
+                and x.scale.dim() == 1 and getattr(self.up, "geluq_rows_ok", lambda m: False)(x.q.shape[0]) \
+                and getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0]):
+            # W8A8 GELU MLP (Phi-2, Pythia) at decode rows: up projection + GELU + per-(token, 64)
+            # int8 quantisation in one launch, consumed by the down projection's grouped-scale GEMV
+            return self.down(self.up.geluq(x, self.act))
         if self.act == "silu_glu" and type(self.up) is Linear and not down_q and not isinstance(x, QAct) \
                 and ops.bf16_gemv_ok(x, self.up.weight, glu=True):
             # bf16 decode: gate_up GEMV with the SwiGLU epilogue (one launch, gemv_bf16.hip)

@@ -389,6 +389,18 @@ def w8a8_glu(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Option
     return _ref.silu_mul(_ref.unblock_glu(y))
 
 
+def w8a8_geluq(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, act: str = "gelu_tanh",
+               w_ref: Optional[torch.Tensor] = None):
+    """Fused decode GELU MLP front half (M <= 64, N % 64 == 0): up projection -> gelu (tanh / erf)
+    of its bf16 output -> int8 per (token, 64 columns), one launch on GPU: (q [M, N], scales
+    [N/64, Mpad]) for the down projection's grouped-scale GEMV."""
+    if _gpu(qx):
+        return ext().w8a8_gemm_geluq(qx, x_scale, w_packed, w_scale, bias, N, K, act == "gelu_tanh")
+    w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
+    y = _ref.w8a8_linear(qx.reshape(-1, K), x_scale.reshape(-1), w, w_scale, bias, torch.bfloat16)
+    return _ref.quant_per_group(_ref.gelu(y, "tanh" if act == "gelu_tanh" else "none"))
+
+
 def quant_per_group(x):
     """Per-(token, 64 columns) int8: (q [M, K], scales [K/64, Mpad]) — the decode-GEMV input
     layout (ops/csrc/rowwise.hip::group_quant_kernel on GPU)."""

@@ -716,6 +716,28 @@ std::tuple<at::Tensor, at::Tensor> w8a8_gemm_gluq(const at::Tensor& a, const at:
   return {q, s};
 }
 
+// W8A8 up projection + GELU (tanh or erf) + per-(token, 64 columns) int8 quantisation in one launch
+// (M <= 64, N % 64 == 0): (q [M, N] int8, scales [N / 64, Mpad]) for the down projection's grouped-
+// scale GEMV — the GELU MLPs' (Phi-2, Pythia) replacement for GEMV -> act_kernel + quant.
+std::tuple<at::Tensor, at::Tensor> w8a8_gemm_geluq(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp,
+                                                   const at::Tensor& sw, const std::optional<at::Tensor>& bias,
+                                                   int64_t N, int64_t K, bool tanh_approx) {
+  DEVICE_GUARD(a);
+  need(a, at::kChar, "a");
+  TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
+  check_w8a8_operands(wp, sw, bias, N, K);
+  const int64_t M = rows_of(a), KT = (K + 63) / 64, Mpad = (M + 15) / 16 * 16;
+  TORCH_CHECK(M <= 64 && N % 64 == 0, "quantising GELU needs M <= 64 and N % 64 == 0");
+  TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GELU takes per-token activation scales");
+  auto q = at::empty({M, N}, a.options());
+  auto s = at::empty({N / 64, Mpad}, a.options().dtype(at::kFloat));
+  check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                       bias ? bias->data_ptr() : nullptr, q.data_ptr(), s.data_ptr<float>(), (int)M, (int)N, (int)K,
+                       (int)KT, 0, (int)Mpad, tanh_approx ? 4 : 5, stream()),
+        "w8a8_gemm_geluq");
+  return {q, s};
+}
+
 // ---------------------------------------------------------------------------------- sampler
 // Returns an empty tensor when the configuration needs the host fallback.
 at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& seen, double temperature,
@@ -796,6 +818,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm_splitk", &w8a8_gemm_splitk);
   m.def("rms_norm_parts", &rms_norm_parts);
   m.def("w8a8_gemm_gluq", &w8a8_gemm_gluq);
+  m.def("w8a8_gemm_geluq", &w8a8_gemm_geluq, "W8A8 GEMV + GELU + per-(token, 64) int8 quantisation (M <= 64)");
   m.def("group_quant", &group_quant);
   m.def("sample", &sample);
   m.def("sample_timestamps", &sample_timestamps);

@@ -39,7 +39,9 @@
 namespace {
 constexpr int NT = 256;
 constexpr int A_TOKEN = 0, A_GROUP = 1;
-constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GLUQ = 2, EPI_PART = 3;
+constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GLUQ = 2, EPI_PART = 3, EPI_GELUQT = 4, EPI_GELUQE = 5;
+// (EPI_GELUQT / EPI_GELUQE: gelu (tanh / erf) of the bf16 output, quantised per (token, 64 columns)
+// in the epilogue of a 4-tile workgroup — the GELU MLPs' (Phi-2, Pythia) up projection at <= 64 rows)
 
 __device__ __forceinline__ v4i mfma_i8(const v4i& a, const v4i& b, const v4i& c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
@@ -112,7 +114,9 @@ struct EpiPre {
 };
 
 template <int MB, int NTW, int NW, int EPI>
-constexpr int epi_units() { return (EPI == EPI_OUT || EPI == EPI_PART) ? NTW * MB : NTW / 2 * MB; }
+constexpr int epi_units() {
+  return (EPI == EPI_OUT || EPI == EPI_PART || EPI == EPI_GELUQT || EPI == EPI_GELUQE) ? NTW * MB : NTW / 2 * MB;
+}
 
 template <int MB, int NTW, int NW, int EPI>
 __device__ __forceinline__ EpiPre<(epi_units<MB, NTW, NW, EPI>() + NW - 1) / NW> epi_preload(
@@ -195,6 +199,57 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
         }
       }
     }
+  } else if constexpr (EPI == EPI_GELUQT || EPI == EPI_GELUQE) {
+    // unit (tile t, row block i): gelu of the bf16-rounded output (the unfused GEMM's), row maxima
+    // over the tile's 16 columns to LDS, one barrier, then each row's scale over the workgroup's
+    // 4 tiles (= one 64-column group; N % 64 == 0) and the int8 store
+    float h[OWN][4];
+    bool owner[OWN];
+    int tt[OWN], ii[OWN];
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      const int f = wave + o * NW;
+      const bool live = f < F;
+      const int t = live ? f / MB : 0, i = live ? f % MB : 0;
+      tt[o] = t;
+      ii[o] = i;
+      owner[o] = live && nt0 + t < NTt;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h[o][q] = 0.f;
+      if (owner[o]) {
+        const v4i tot = total(f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = i * 16 + 4 * (lane >> 4) + q;
+          const float v = (float)tot[q] * (row < M ? sa[row] : 0.f) * pre.s0[o] + pre.b0[o];
+          const float a = bf2f(f2bf(v));
+          float g;
+          if constexpr (EPI == EPI_GELUQT) g = 0.5f * a * (1.f + tanhf(0.7978845608028654f * (a + 0.044715f * a * a * a)));
+          else g = 0.5f * a * (1.f + erff(a * 0.7071067811865476f));
+          h[o][q] = bf2f(f2bf(g));            // the unfused activation output is bf16
+          float m = fabsf(h[o][q]);
+#pragma unroll
+          for (int d = 1; d < 16; d <<= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+          if ((lane & 15) == 0) gmax[i][t][4 * (lane >> 4) + q] = m;
+        }
+      }
+    }
+    __syncthreads();
+    int8_t* hq = reinterpret_cast<int8_t*>(outv);
+    const int grp = nt0 / 4;
+#pragma unroll
+    for (int o = 0; o < OWN; ++o) {
+      if (!owner[o]) continue;
+      const int t = tt[o], i = ii[o];
+      const int col = (nt0 + t) * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 4 * (lane >> 4) + q, row = i * 16 + rr;
+        const float amax = fmaxf(fmaxf(fmaxf(gmax[i][0][rr], gmax[i][1][rr]), fmaxf(gmax[i][2][rr], gmax[i][3][rr])), 1e-8f);
+        if (row < M) hq[(size_t)row * N + col] = quant_i8(h[o][q], 127.f / amax);
+        if (t == 0 && (lane & 15) == 0 && row < Mpad) os[(size_t)grp * Mpad + row] = row < M ? amax / 127.f : 0.f;
+      }
+    }
   } else {
     // pair p = (gate tile 2p, up tile 2p+1) -> feature (nt0/2 + p) * 16 + (lane & 15); a wave owns
     // pairs wave, wave + NW, ...  EPI_GLUQ: every owned pair's row maxima reach LDS before the
@@ -269,9 +324,11 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
                                                                  int NTt, int Mpad, int S) {
   constexpr int NW = TG * KW, TPW = NTW / TG;
   static_assert(NTW % TG == 0, "tiles split evenly over tile groups");
-  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && TPW % 2 == 0),
+  constexpr bool GELUQ = EPI == EPI_GELUQT || EPI == EPI_GELUQE;
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && (GELUQ || TPW % 2 == 0)),
                 "GLU: gate/up pairs per wave, per-token A");
   static_assert(EPI != EPI_GLUQ || NTW == 8, "quantising GLU: 64 features per workgroup");
+  static_assert(!GELUQ || NTW == 4, "quantising GELU: 64 columns per workgroup");
   // LDS reduction buffer: one partial set per k-wave, or per pair of k-waves when that would
   // exceed 128 KiB (the upper half adds into the lower half first)
   constexpr int KR = KW * NTW * MB * 1024 <= 131072 ? KW : KW / 2;
@@ -1929,6 +1986,18 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     if (r != -1) return r;
   }
   if (a_mode != A_TOKEN && M > 64) return -2;
+  if (epi == EPI_GELUQT || epi == EPI_GELUQE) {
+    // 4 tiles = one 64-column quant group per workgroup, 16 waves splitting K
+    if (a_mode != A_TOKEN || M > 64 || N % 64 != 0 || os == nullptr || Mpad < mblocks * 16) return -2;
+#define GQ(MBV, KWV)                                                                                              \
+  return epi == EPI_GELUQT                                                                                        \
+             ? launch_one<MBV, 4, 1, KWV, 2, A_TOKEN, EPI_GELUQT>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st) \
+             : launch_one<MBV, 4, 1, KWV, 2, A_TOKEN, EPI_GELUQE>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st)
+    if (mblocks <= 1) GQ(1, 16);
+    if (mblocks <= 2) GQ(2, 16);
+    GQ(4, 8);
+#undef GQ
+  }
   if (epi == EPI_GLU || epi == EPI_GLUQ) {
     const bool ldsa = KT == 64 && K == 4096 && N % 128 == 0 && g_gemv_unroll != 1;
     if (a_mode != A_TOKEN || M > (epi == EPI_GLUQ && ldsa ? 128 : 64) || N % (epi == EPI_GLUQ ? 128 : 32) != 0)

@@ -153,6 +153,17 @@ class W8A8Linear(nn.Module):
                            w_ref=self._wref(x.q), quant=quant)
         return QAct(*out) if quant else GroupQuantBF16(out)
 
+    def geluq_rows_ok(self, M: int) -> bool:
+        """Whether the fused up projection + GELU + grouped int8 quant takes M rows (GPU <= 64)."""
+        return M <= 64 and self.out_features % 64 == 0 and not self.glu_blocked
+
+    def geluq(self, x: QAct, act: str) -> QAct:
+        """GELU MLP front half in one launch (ops.w8a8_geluq): int8 h per (token, 64 columns)."""
+        K, N = self.in_features, self.out_features
+        q, s = ops.w8a8_geluq(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,
+                              act, w_ref=self._wref(x.q))
+        return QAct(q, s)
+
     def extra_repr(self):
         return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, W8A8 int8"
 

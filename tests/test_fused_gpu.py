@@ -584,3 +584,55 @@ def test_ring2_grouped_splitk(cuda, cfg, M, N, K, S):
     assert (s2 - s0).abs().max().item() <= 1e-4 * s0.abs().max().item() + 1e-5
     ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
     _close(s2, ref, 1e-3, 1e-2)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "gelu"])
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(10240, 2560), (8192, 2048), (128, 192)])
+def test_w8a8_geluq_matches_reference(cuda, act, M, N, K):
+    """Fused up projection + GELU + per-(token, 64) int8 (the GELU MLPs' decode path) == the
+    reference composition w8a8_linear -> bf16 -> gelu -> quant_per_group (dequantised values within
+    one int8 step of the group scale; scales to 1e-3 relative)."""
+    torch.manual_seed(M + N + (act == "gelu"))
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.004 + 1e-4
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    q, s = ops.w8a8_geluq(qx, sx, wp, sw, bias, N, K, act)
+    Mpad = (M + 15) // 16 * 16
+    assert q.shape == (M, N) and s.shape == (N // 64, Mpad)
+    assert (s[:, M:] == 0).all()
+    y = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.bfloat16)
+    rq, rs = _ref.quant_per_group(_ref.gelu(y, "tanh" if act == "gelu_tanh" else "none"))
+    _close(s[:, :M], rs[:, :M], 0.0, 1e-3)
+    step = s[:, :M].t().repeat_interleave(64, dim=1)
+    deq, rdeq = q.float() * step, rq.float() * rs[:, :M].t().repeat_interleave(64, dim=1)
+    assert ((deq - rdeq).abs() <= step * 1.01 + 1e-6).all()
+
+
+def test_w8a8_gelu_mlp_takes_fused_path(cuda):
+    """A W8A8 Phi-style (GELU, parallel residual) decoder at decode rows routes its MLP through the
+    fused GELU-quant kernel and stays close to the bf16 model at the logits."""
+    from edgellm.engine import KVCache
+    from edgellm.models import AttnCtx, build_model, tiny
+    from edgellm.quant import quantize_model
+    cfg = tiny("phi", hidden_size=256, num_heads=4, num_kv_heads=4, intermediate_size=1024, num_layers=2)
+    base = build_model(cfg, device=cuda, seed=3)
+    qm = quantize_model(build_model(cfg, device=cuda, seed=3), "w8a8")
+    B, T = 4, 12
+    ids = torch.randint(0, cfg.vocab_size, (B, T), generator=torch.Generator().manual_seed(0)).to(cuda)
+    outs = []
+    for m in (base, qm):
+        kv = KVCache(cfg, B, T + 4, dtype=m.dtype, device=cuda)
+        sp = torch.zeros(B, dtype=torch.int32, device=cuda)
+        with torch.no_grad():
+            m(ids, AttnCtx("prefill", B, T, sp, sp + T, T, kv.rows(0, B), m.rope_table(cuda)), logits="last")
+            pos = torch.full((B,), T, dtype=torch.int32, device=cuda)
+            outs.append(m(ids[:, -1:], AttnCtx("decode", B, 1, pos, pos + 1, T + 1, kv.rows(0, B),
+                                               m.rope_table(cuda))).float())
+    mlp = qm.layers[0].mlp
+    assert getattr(mlp.up, "geluq_rows_ok", lambda m: False)(B)
+    rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
+    assert rel < 0.1, rel
