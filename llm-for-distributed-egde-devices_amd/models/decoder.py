@@ -159,7 +159,9 @@ class MLP(nn.Module):
         self.up = Linear(cfg.hidden_size, up_out, cfg.mlp_bias, dtype, device)
         self.down = Linear(cfg.intermediate_size, cfg.hidden_size, cfg.mlp_bias, dtype, device)
 
-    def forward(self, x):
+    def forward(self, x, add=None):
+        """``add``: the attention branch of a parallel-residual block, added to the down
+        projection's output (in its decode GEMV's epilogue)."""
         if getattr(self.up, "glu_blocked", False):
             # W8A8 SwiGLU with 16-blocked gate_up rows: decode-sized batches take the fused
             # GEMV + SwiGLU epilogue (int8 h with per-group scales, or bf16 h that the down
@@ -167,28 +169,28 @@ class MLP(nn.Module):
             # activation kernel
             if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and self.up.glu_rows_ok(x.q.shape[0]) \
                     and (x.q.shape[0] <= 64 or getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0])):
-                return self.down(self.up.glu(x))
-            return self.down(act_fn(self.up(x), "silu_glu_blocked", True))
+                return self.down(self.up.glu(x), add=add)
+            return self.down(act_fn(self.up(x), "silu_glu_blocked", True), add=add)
         down_q = getattr(self.down, "takes_quantized_input", False)
         if self.act in ("gelu_tanh", "gelu") and down_q and isinstance(x, QAct) and x.q.dim() == 2 \
                 and x.scale.dim() == 1 and getattr(self.up, "geluq_rows_ok", lambda m: False)(x.q.shape[0]) \
                 and getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0]):
             # W8A8 GELU MLP (Phi-2, Pythia) at decode rows: up projection + GELU + per-(token, 64)
             # int8 quantisation in one launch, consumed by the down projection's grouped-scale GEMV
-            return self.down(self.up.geluq(x, self.act))
+            return self.down(self.up.geluq(x, self.act), add=add)
         if self.act == "silu_glu" and type(self.up) is Linear and not down_q and not isinstance(x, QAct) \
                 and ops.bf16_gemv_ok(x, self.up.weight, glu=True):
             # bf16 decode: gate_up GEMV with the SwiGLU epilogue (one launch, gemv_bf16.hip)
             return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, glu=True,
-                                             packed=self.up.decode_weight(x, glu=True)))
+                                             packed=self.up.decode_weight(x, glu=True)), add=add)
         if self.act in ("gelu_tanh", "gelu") and type(self.up) is Linear and not down_q \
                 and not isinstance(x, QAct) and ops.bf16_gemv_ok(x, self.up.weight):
             # bf16 decode (Phi-2, Pythia): up-projection GEMV with the GELU epilogue
             return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, act=self.act,
-                                             packed=self.up.decode_weight(x)))
+                                             packed=self.up.decode_weight(x)), add=add)
         h = self.up(x)
         h = act_fn(h, self.act, down_q)
-        return self.down(h)
+        return self.down(h, add=add)
 
 
 class DecoderLayer(nn.Module):
@@ -220,10 +222,11 @@ class DecoderLayer(nn.Module):
                 na, nm = quant_if(n, self.attn.qkv), quant_if(n, self.mlp.up)
             else:
                 na = nm = n
-            return self.attn(na, ctx) + self.mlp(nm), h
+            # attn + mlp: the sum is taken in the down projection's epilogue (one launch fewer)
+            return self.mlp(nm, add=self.attn(na, ctx)), h
         n1, h = self.norm1(x, residual, quant=qa)      # gpt_neox
         n2, _ = self.norm2(h, None, quant=qm)
-        return self.attn(n1, ctx) + self.mlp(n2), h
+        return self.mlp(n2, add=self.attn(n1, ctx)), h
 
 
 class DecoderLM(nn.Module):

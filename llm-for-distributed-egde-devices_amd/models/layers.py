@@ -56,11 +56,13 @@ class Linear(nn.Module):
         self.bias = (nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device), requires_grad=False)
                      if bias else None)
 
-    def forward(self, x):
+    def forward(self, x, add=None):
+        """``add``: the other branch of a parallel-residual block, added to the output (in the
+        decode GEMV's epilogue where that kernel runs)."""
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
         wp = self.decode_weight(x)
-        if self.split_k_out and wp is not None:
+        if self.split_k_out and wp is not None and add is None:
             K = x.shape[-1]
             if ops.bf16_decode_mode(x, self.weight, split=True) == 2:
                 # 17-256 rows: the ring GEMM's split-K slices (the launcher picks S for the shape)
@@ -71,7 +73,8 @@ class Linear(nn.Module):
             elif K // 64 >= self.split_k_out:
                 return PartialSum(ops.ext().gemv_bf16_splitk(x.reshape(-1, K), wp, self.bias,
                                                              self.out_features, self.split_k_out))
-        return ops.linear_bf16(x, self.weight, self.bias, packed=wp)
+        return ops.linear_bf16(x, self.weight, self.bias, packed=wp,
+                               add=None if add is None else add.reshape(*x.shape[:-1], self.out_features))
 
     def decode_weight(self, x, glu: bool = False) -> "Optional[torch.Tensor]":
         """Fragment-packed copy of the weight for the decode GEMV / ring GEMM, built on the first

@@ -334,40 +334,46 @@ _GEMV_EPI = {None: 0, "silu_glu": 1, "gelu_tanh": 2, "gelu": 3}
 
 
 def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = None,
-                packed: Optional[torch.Tensor] = None):
+                packed: Optional[torch.Tensor] = None, add: Optional[torch.Tensor] = None):
     """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` on the fragment-packed
     weight (``packed``: the layer's cached ``pack_bf16_weight(weight)``; packed per call when
     absent); ``glu``: weight = [gate | up] and the result is silu(gate) * up; ``act``
     "gelu_tanh" / "gelu": the activation of the bf16 output in the same kernel.  Everything else
-    is ``F.linear`` (hipBLASLt on GPU) followed by the activation op."""
+    is ``F.linear`` (hipBLASLt on GPU) followed by the activation op.  ``add`` (bf16, the output's
+    shape; plain outputs only): returns bf16(y + add), in the GEMV epilogue where it runs."""
     if glu:
         act = "silu_glu"
+    assert add is None or act is None, "addend: plain outputs only"
     mode = bf16_decode_mode(x, weight, glu)
     if mode == 1 or (mode == 2 and act in (None, "silu_glu")):
         wp = packed if packed is not None else pack_bf16_weight(weight)
         if mode == 1:
-            return ext().gemv_bf16(x, wp, bias, weight.shape[0], _GEMV_EPI[act])
-        return ext().gemm_bf16_ring(x, wp, bias, weight.shape[0], 1 if glu else 0, 0)
+            return ext().gemv_bf16(x, wp, bias, weight.shape[0], _GEMV_EPI[act], add)
+        y = ext().gemm_bf16_ring(x, wp, bias, weight.shape[0], 1 if glu else 0, 0)
+        return y if add is None else y + add
     if mode == 2:           # GELU MLPs: ring GEMM, then the activation kernel
         wp = packed if packed is not None else pack_bf16_weight(weight)
         return activation(ext().gemm_bf16_ring(x, wp, bias, weight.shape[0], 0, 0), act)
     y = torch.nn.functional.linear(x, weight, bias)
-    return y if act is None else activation(y, act)
+    y = y if act is None else activation(y, act)
+    return y if add is None else y + add
 
 
 def w8a8_linear(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,
-                out_dtype=torch.bfloat16):
+                out_dtype=torch.bfloat16, add: Optional[torch.Tensor] = None):
     """INT8 x INT8 -> int32 MFMA GEMM with per-channel weight dequant (+bias) -> bf16.
     ``x_scale`` is per token ([M]) or per (token, 64-column group) ([K/64, Mpad], M <= 64, from the
     fused producers).  ``out_dtype`` applies on CPU, where fp16/fp32 agents run; ``w_ref``
-    (canonical [N, K]) is only needed by the CPU path."""
+    (canonical [N, K]) is only needed by the CPU path.  ``add``: returns y + add (the other branch
+    of a parallel-residual block), in the GEMV epilogue at decode rows on GPU."""
     if _gpu(qx):
-        return ext().w8a8_gemm(qx, x_scale, w_packed, w_scale, bias, N, K)
+        return ext().w8a8_gemm(qx, x_scale, w_packed, w_scale, bias, N, K,
+                               None if add is None else add.contiguous())
     w = w_ref if w_ref is not None else unpack_int8_weight(w_packed, N, K)
     shp = qx.shape[:-1]
     xs = x_scale if x_scale.dim() == 2 else x_scale.reshape(-1)
-    out = _ref.w8a8_linear(qx.reshape(-1, K), xs, w, w_scale, bias, out_dtype)
-    return out.view(*shp, N)
+    out = _ref.w8a8_linear(qx.reshape(-1, K), xs, w, w_scale, bias, out_dtype).view(*shp, N)
+    return out if add is None else out + add.view(*shp, N).to(out.dtype)
 
 
 def w8a8_glu(qx, x_scale, w_packed, w_scale, bias, N: int, K: int, w_ref: Optional[torch.Tensor] = None,

@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
       for (int o = LPK; o < 64; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
       // cm is finite: key `base` (kl = 0, u = 0) is in range whenever a chunk is consumed
       const float mn = fmaxf(m[h], cm);
-      const float alpha = exp2f(m[h] - mn);        // 0 on the first chunk (m = -inf)
+      const float alpha = __builtin_amdgcn_exp2f(m[h] - mn);        // 0 on the first chunk (m = -inf)
       m[h] = mn;
       l[h] *= alpha;
 #pragma unroll
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
       unpack8(vr[u], vf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
-        const float p = exp2f(s[u][h] - m[h]);    // masked keys: exp2(-inf) = 0
+        const float p = __builtin_amdgcn_exp2f(s[u][h] - m[h]);    // masked keys: exp2(-inf) = 0
         l[h] += p;
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[h][j] += p * vf[j];

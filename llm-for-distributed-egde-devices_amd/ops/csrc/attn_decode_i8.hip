@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
 #pragma unroll
       for (int o = LPK; o < 64; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
       const float mn = fmaxf(m[h], cm);            // finite: key `base` is in range
-      const float alpha = exp2f(m[h] - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m[h] - mn);
       m[h] = mn;
       l[h] *= alpha;
       vbias[h] *= alpha;
@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(NT, OCC) decode_attn_i8_kernel(
       unpack16u(vr[u], vf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
-        const float p = exp2f(s[u][h] - m[h]);
+        const float p = __builtin_amdgcn_exp2f(s[u][h] - m[h]);
         l[h] += p;
         const float pv = p * vs[u];
         vbias[h] += pv;
@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(NT, 4) decode_attn_i8_wave_kernel(
 #pragma unroll
     for (int o = LPK; o < 64; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
     const float mn = fmaxf(m, cm);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
     m = mn;
     l *= alpha;
     vbias *= alpha;
@@ -508,7 +508,7 @@ __global__ void __launch_bounds__(NT, 4) decode_attn_i8_wave_kernel(
     for (int u = 0; u < U; ++u) {
       float vf[16];
       unpack16u(vr[buf][u], vf);
-      const float p = exp2f(s[u] - m);
+      const float p = __builtin_amdgcn_exp2f(s[u] - m);
       l += p;
       const float pv = p * vs[buf][u];
       vbias += pv;

@@ -170,11 +170,11 @@ __global__ void __launch_bounds__(NT) prefill_attn_kernel(
       for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
       const float mnew = fmaxf(m_i[i], mx);
       const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-      alpha[i] = exp2f(m_i[i] - msafe);
+      alpha[i] = __builtin_amdgcn_exp2f(m_i[i] - msafe);
       float rs = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const float p = exp2f(s[nt][i] - msafe);
+        const float p = __builtin_amdgcn_exp2f(s[nt][i] - msafe);
         s[nt][i] = p;
         rs += p;
       }
@@ -352,14 +352,15 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
       }
       asm volatile("" ::: "memory");                           // K fragments: one 32-key block in flight
     }
-    // ---- scale, mask, online softmax (one query per lane)
+    // ---- mask, online softmax (one query per lane).  The max runs over the raw scores (the scale
+    // is positive), and the scale folds into each exponent's fma: exp2(s * scale - m)
     const bool full = (k0 + FA_KT <= kend) && (!CAUSAL || k0 + FA_KT - 1 <= s0 + wq0);
     float mx = -INFINITY;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float v = sacc[kb][r] * scale_log2;
+        float v = sacc[kb][r];
         if (!full) {
           const int key = k0 + kb * 32 + 8 * (r >> 2) + 4 * hf + (r & 3);
           if (key >= kend || (CAUSAL && key > qpos)) v = -INFINITY;
@@ -368,9 +369,11 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
         mx = fmaxf(mx, v);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m_i, mx);
+    const float mnew = fmaxf(m_i, mx * scale_log2);
     const float msafe = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = exp2f(m_i - msafe);
+    // v_exp_f32 directly: exp2f adds a denormal-range fix-up (compare, select, add, multiply) to
+    // every exponential; arguments here are <= 0 and a probability below 2^-126 may flush to 0
+    const float alpha = __builtin_amdgcn_exp2f(m_i - msafe);
     float rs = 0.f;
     v8s pb[2][2];
 #pragma unroll
@@ -379,17 +382,21 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float pv = exp2f(sacc[kb][8 * ks + j] - msafe);
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][8 * ks + j], scale_log2, -msafe));
           rs += pv;
           pb[kb][ks][j] = (short)f2bf(pv);
         }
     rs += __shfl_xor(rs, 32, 64);
     l_i = l_i * alpha + rs;
     m_i = mnew;
+    // O rescale only when some query's running max moved (alpha != 1; multiplying by exactly 1 is
+    // the identity, so the skip is bit-exact): past the first tiles a new maximum is rare
+    if (__any(alpha != 1.f)) {
 #pragma unroll
-    for (int i = 0; i < G::DB; ++i)
+      for (int i = 0; i < G::DB; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    }
 
     // ---- O^T += V^T P^T: per 16-key step, lane group g reads keys {4 hf .. +3} and {8 + 4 hf .. +3}
     const int c16 = lane & 15, qq = c16 >> 2, pq = c16 & 3, g2 = (lane >> 4) & 1;

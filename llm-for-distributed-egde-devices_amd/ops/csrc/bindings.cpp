@@ -52,7 +52,7 @@ void edge_w8a8_rows256_cfg(int cfg, int nt);
 void edge_w8a8_rows256_diag(int v);
 void edge_w8a8_rows256_magic(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
-                   hipStream_t st);
+                   hipStream_t st, const void* add);
 int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
                           hipStream_t st);
 int edge_llmint8_prep(const void* x, int M, int K, float thr, int cmax, void* q, float* sa, int* cols, float* xo,
@@ -507,8 +507,11 @@ void check_w8a8_operands(const at::Tensor& wp, const at::Tensor& sw, const std::
   if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
 }
 
+// addend (optional, bf16 [.., N]): out = bf16(bf16(y) + addend) — the other branch of a parallel-
+// residual block, added in the GEMV epilogue at <= 64 rows (a separate add above)
 at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
-                     const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+                     const std::optional<at::Tensor>& bias, int64_t N, int64_t K,
+                     const std::optional<at::Tensor>& addend) {
   DEVICE_GUARD(a);
   need(a, at::kChar, "a");
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
@@ -518,6 +521,17 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
   auto os = a.sizes().vec();
   os.back() = N;
   auto out = at::empty(os, a.options().dtype(at::kBFloat16));
+  if (addend) {
+    need(*addend, at::kBFloat16, "addend");
+    TORCH_CHECK(addend->numel() == M * N, "addend must hold M * N elements");
+    if (M <= 64) {
+      check(edge_w8a8_gemm(a.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                           bias ? bias->data_ptr() : nullptr, out.data_ptr(), (float*)addend->data_ptr(), (int)M,
+                           (int)N, (int)K, (int)KT, mpad > 0 ? 1 : 0, (int)mpad, 0, stream()),
+            "w8a8_gemm");
+      return out;
+    }
+  }
   if (mpad == 0 && a.is_contiguous() && edge_w8a8_apack_ok((int)M, (int)N, (int)K, (int)KT)) {
     // prefill: A fragment-packed into a stream-ordered scratch, then the ring GEMM on contiguous pieces
     auto ap = at::empty({(M + 15) / 16 * 16 * K}, a.options());
@@ -531,6 +545,7 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
                        bias ? bias->data_ptr() : nullptr, out.data_ptr(), nullptr, (int)M, (int)N, (int)K, (int)KT,
                        mpad > 0 ? 1 : 0, (int)mpad, 0, stream()),
         "w8a8_gemm");
+  if (addend) out.add_(addend->view(out.sizes()));
   return out;
 }
 
@@ -566,7 +581,7 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
 // W fragment-packed (ops.pack_bf16_weight).  epi: 0 plain, 1 SwiGLU over [gate | up] (result
 // [.., N/2]), 2 gelu-tanh, 3 gelu (erf).
 at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
-                     int64_t epi) {
+                     int64_t epi, const std::optional<at::Tensor>& addend) {
   DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(wp, at::kBFloat16, "weight (packed)");
@@ -576,8 +591,12 @@ at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optio
   auto os = x.sizes().vec();
   os.back() = epi == 1 ? N / 2 : N;
   auto out = at::empty(os, x.options());
+  if (addend) {
+    need(*addend, at::kBFloat16, "addend");
+    TORCH_CHECK(epi == 0 && addend->numel() == M * N, "addend: plain output only, M * N elements");
+  }
   check(edge_gemv_bf16(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N,
-                       (int)K, (int)epi, stream()),
+                       (int)K, (int)epi, stream(), addend ? addend->data_ptr() : nullptr),
         "gemv_bf16");
   return out;
 }
@@ -802,14 +821,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("v2") = py::none(), py::arg("split") = -1, py::arg("cpos2") = py::none());
   m.def("decode_attn", &decode_attn);
   m.def("prefill_attn", &prefill_attn);
-  m.def("w8a8_gemm", &w8a8_gemm);
+  m.def("w8a8_gemm", &w8a8_gemm, py::arg("a"), py::arg("sa"), py::arg("wp"), py::arg("sw"), py::arg("bias"),
+        py::arg("N"), py::arg("K"), py::arg("addend") = py::none());
   m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");
   m.def("gemm_bf16_ring", &gemm_bf16_ring, "bf16 decode GEMM, 17-256 rows (ring2 kernel, bf16 MFMA)");
   m.def("bf16_ring_splits", [](int64_t N, int64_t K) { return (int64_t)edge_bf16_ring_splits((int)N, (int)K); });
   m.def("bf16_ring_min_rows", []() { return (int64_t)edge_bf16_ring_min_rows(); });
-  m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]");
+  m.def("gemv_bf16", &gemv_bf16, "bf16 decode GEMV (M <= 16), optional fused SwiGLU over [gate | up]", py::arg("x"),
+        py::arg("wp"), py::arg("bias"), py::arg("N"), py::arg("epi"), py::arg("addend") = py::none());
   m.def("decode_attn_fused", &decode_attn_fused);
   m.def("decode_attn_i8", &decode_attn_i8, "decode attention over an int8 KV cache, fused RoPE + quantising append");
   m.def("kv_dequant", &kv_dequant, "dequantise the first T rows of an int8 KV cache into a bf16 scratch");

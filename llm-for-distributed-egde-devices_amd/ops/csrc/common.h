@@ -74,6 +74,10 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return r;
 }
 
+// Softmax exponentials use __builtin_amdgcn_exp2f (a bare v_exp_f32): the libm exp2f wraps it in a
+// denormal-range fix-up (compare, select, add, multiply) per call, and softmax arguments are <= 0,
+// where a result below 2^-126 may flush to zero.
+
 __device__ __forceinline__ int8_t quant_i8(float v, float inv_scale) {
   float q = rintf(v * inv_scale);
   q = fminf(fmaxf(q, -127.f), 127.f);

@@ -182,6 +182,9 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
     }
   } else if constexpr (EPI == EPI_OUT) {
     bf16_t* out = reinterpret_cast<bf16_t*>(outv);
+    // os, unused by this epilogue, may carry a bf16 addend [M, N] (the other branch of a parallel-
+    // residual block): out = bf16(bf16(y) + addend), the unfused bf16 add's value
+    const bf16_t* add = reinterpret_cast<const bf16_t*>(os);
 #pragma unroll
     for (int o = 0; o < OWN; ++o) {
       const int f = wave + o * NW;
@@ -195,6 +198,7 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
         if (row < M && col < N) {
           float v = SCALED ? __builtin_bit_cast(v4f, tot)[q] : (float)tot[q] * sa[row];
           v = v * pre.s0[o] + pre.b0[o];
+          if (add != nullptr) v = bf2f(f2bf(v)) + bf2f(add[(size_t)row * N + col]);
           out[(size_t)row * N + col] = f2bf(v);
         }
       }
@@ -1900,8 +1904,8 @@ int launch_rows128(const void* A, const float* sa, const void* Wp, const float* 
 // EPI_OUT: 16 waves; KW = 16 while the LDS reduction fits (KW x NTW x MB KiB <= 128 KiB), else 8
 template <int MB, int AM>
 int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const void* Wp, const float* sw,
-               const void* bias, void* out, int M, int N, int K, int KT, int Mpad, hipStream_t st) {
-#define L(NTWV, KWV, UV) return launch_one<MB, NTWV, 1, KWV, UV, AM, EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, \
+               const void* bias, void* out, int M, int N, int K, int KT, int Mpad, hipStream_t st, float* add) {
+#define L(NTWV, KWV, UV) return launch_one<MB, NTWV, 1, KWV, UV, AM, EPI_OUT>(A, sa, Wp, sw, bias, out, add, M, N, K, \
                                                                           KT, Mpad, st)
 #define BY_KW(NTWV, UV)                                                   \
   do {                                                                    \
@@ -1963,6 +1967,8 @@ extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void*
 }
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).
+// epi 0: `os`, when not null, is a bf16 addend [M, N] added to the output (M <= 64 only; larger M
+//        must pass null).
 // epi 1: fused SwiGLU on 16-blocked gate/up rows, `out` is bf16 [M, N/2] (a_mode 0, M <= 64).
 // epi 2: as epi 1, then per-(token, 64 features) int8 quantisation: `out` int8 [M, N/2],
 //        `os` scales [N/128][Mpad] (N % 128 == 0).
@@ -2072,7 +2078,8 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : (NTt >= 512 ? min(4, (NTt + 128) / 256) : 1);
   const int un = g_gemv_unroll > 0 ? g_gemv_unroll : (ntw == 1 && KT >= 128 ? 4 : (mblocks > 2 ? 1 : 2));
   const int kw = g_gemv_kw > 0 ? g_gemv_kw : 16;
-#define OUT(MBV, AMV) return launch_out<MBV, AMV>(ntw, un, kw, A, sa, Wp, sw, bias, out, M, N, K, KT, Mpad, st)
+#define OUT(MBV, AMV) return launch_out<MBV, AMV>(ntw, un, kw, A, sa, Wp, sw, bias, out, M, N, K, KT, Mpad, st, \
+                                                  epi == EPI_OUT ? os : nullptr)
   if (a_mode == A_GROUP) {
     if (mblocks <= 1) OUT(1, A_GROUP);
     if (mblocks <= 2) OUT(2, A_GROUP);

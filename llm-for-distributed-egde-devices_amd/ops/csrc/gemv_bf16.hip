@@ -40,7 +40,8 @@ __device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
 template <int MB, int NTW, int U, int EPI>
 __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                            int M, int N, int K, int F, int S) {
+                                                            int M, int N, int K, int F, int S,
+                                                            const bf16_t* __restrict__ add) {
   static_assert(EPI != EPI_GLU || NTW % 2 == 0, "GLU: gate/up tile pairs");
   static_assert(MB * NTW <= 8 && MB * (EPI == EPI_GLU ? NTW / 2 : NTW) <= NW, "LDS reduction / output waves");
   __shared__ v4f red[NW][MB * NTW][64];
@@ -147,6 +148,9 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
         } else if constexpr (EPI == EPI_GELU) {
           const float a = bf2f(f2bf(v));
           v = 0.5f * a * (1.f + erff(a * 0.7071067811865476f));
+        } else {
+          // EPI_OUT with an addend (parallel-residual block): bf16(bf16(y) + add), the unfused add
+          if (add != nullptr && row < M && c0 < N) v = bf2f(f2bf(v)) + bf2f(add[(size_t)row * N + c0]);
         }
         if (row < M && c0 < N) out[(size_t)row * N + c0] = f2bf(v);
       }
@@ -156,10 +160,10 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
 
 template <int MB, int NTW, int U, int EPI>
 int launch_mb(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
-              hipStream_t st, int S) {
+              hipStream_t st, int S, const void* add = nullptr) {
   const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
   hipLaunchKernelGGL((gemv_bf16_kernel<MB, NTW, U, EPI>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
-                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S);
+                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S, (const bf16_t*)add);
   return (int)hipGetLastError();
 }
 
@@ -167,22 +171,23 @@ int launch_mb(const void* A, const void* W, const void* bias, void* out, int M, 
 // tiles (the LDS reduction holds MB x NTW tiles of 16 waves)
 template <int NTW, int U, int EPI>
 int launch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
-           hipStream_t st, int S = 1) {
+           hipStream_t st, int S = 1, const void* add = nullptr) {
   constexpr int G = EPI == EPI_GLU ? 2 : 1;                 // GLU keeps gate / up pairs
   constexpr int N2 = NTW > 4 ? 4 : (NTW < G ? G : NTW), N34 = NTW > 2 ? 2 : (NTW < G ? G : NTW);
   const int mb = (M + 15) / 16;
-  if (mb <= 1) return launch_mb<1, NTW, U, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
-  if (mb == 2) return launch_mb<2, N2, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
-  if (mb == 3) return launch_mb<3, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
-  return launch_mb<4, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S);
+  if (mb <= 1) return launch_mb<1, NTW, U, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  if (mb == 2) return launch_mb<2, N2, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  if (mb == 3) return launch_mb<3, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  return launch_mb<4, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
 }
 }  // namespace
 
-// W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N]; epi 1 (GLU):
+// W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N] (+ the bf16 addend `add`
+// [M, N] when not null: a parallel-residual block's other branch); epi 1 (GLU):
 // W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F] (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 64, K % 64 == 0,
 // N % 16 == 0.  Returns -2 for shapes it does not take.
 extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
-                              hipStream_t st) {
+                              hipStream_t st, const void* add) {
   if (M <= 0 || M > 64 || K % 64 != 0 || N % 16 != 0 || K <= 0) return -2;
   const int KP = K / 64;
   const int U = KP >= 64 ? 4 : 2;                            // k-pairs in flight per wave
@@ -204,7 +209,12 @@ extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, vo
                 : launch<1, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);
   if (epi == EPI_GELU_TANH) { PICK(EPI_GELU_TANH) }
   if (epi == EPI_GELU) { PICK(EPI_GELU) }
-  PICK(EPI_OUT)
+  // plain output, optionally + a bf16 addend [M, N]
+  if (nt >= 1024) return launch<4, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
+  if (nt >= 512) return U == 4 ? launch<2, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add)
+                               : launch<2, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
+  return U == 4 ? launch<1, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add)
+                : launch<1, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
 #undef PICK
 }
 

@@ -113,7 +113,9 @@ class W8A8Linear(nn.Module):
             self._w_cpu = self.int8_weight()
         return self._w_cpu
 
-    def forward(self, x):
+    def forward(self, x, add=None):
+        """``add``: the other branch of a parallel-residual block, added to the output (in the
+        decode GEMV's epilogue at <= 64 rows)."""
         if isinstance(x, GroupQuantBF16):             # decode: per-(token, 64) int8 input
             x = QAct(*ops.quant_per_group(x.x.reshape(-1, self.in_features)))
         if not isinstance(x, QAct):
@@ -122,6 +124,10 @@ class W8A8Linear(nn.Module):
         shp = x.q.shape[:-1]
         scale = x.scale if x.scale.dim() == 2 and x.q.dim() == 2 else x.scale.reshape(-1)
         M = x.q.numel() // K
+        if add is not None:
+            out = ops.w8a8_linear(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale, self.bias, N, K,
+                                  w_ref=self._wref(x.q), out_dtype=self.out_dtype, add=add.reshape(M, N))
+            return out.view(*shp, N)
         if self.split_k_out and x.q.is_cuda and ops.gpu_path(x.q) and K % 64 == 0 and 0 < M and \
                 ops.decode_rows_ok(M, K, 4 if M > 64 else 1):
             return PartialSum(ops.w8a8_linear_splitk(x.q.reshape(-1, K), scale, self.w_packed, self.w_scale,
@@ -214,7 +220,11 @@ class LLMInt8Linear(nn.Module):
         if bias is not None:
             self.bias.copy_(bias)
 
-    def forward(self, x):
+    def forward(self, x, add=None):
+        out = self._forward(x)
+        return out if add is None else out + add.view_as(out)
+
+    def _forward(self, x):
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(torch.bfloat16)
         K, N = self.in_features, self.out_features
@@ -269,10 +279,11 @@ class CPUDynamicLinear(nn.Module):
             self.q = torch.ao.quantization.quantize_dynamic(nn.Sequential(f), {nn.Linear}, dtype=torch.qint8)[0]
         self.out_dtype = lin.weight.dtype
 
-    def forward(self, x):
+    def forward(self, x, add=None):
         if isinstance(x, QAct):
             x = x.q.float() * x.scale[..., None]
-        return self.q(x.float()).to(self.out_dtype)
+        out = self.q(x.float()).to(self.out_dtype)
+        return out if add is None else out + add.view_as(out).to(out.dtype)
 
 
 def enable_fused_glu(model) -> int:

@@ -636,3 +636,28 @@ def test_w8a8_gelu_mlp_takes_fused_path(cuda):
     assert getattr(mlp.up, "geluq_rows_ok", lambda m: False)(B)
     rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
     assert rel < 0.1, rel
+
+
+@pytest.mark.parametrize("M", [1, 16, 40])
+def test_gemv_addend_matches_unfused_add(cuda, M):
+    """Parallel-residual fusion: the W8A8 (grouped and per-token scales) and bf16 decode GEMVs add a
+    bf16 addend in their epilogue == bf16(bf16(y) + addend), the unfused add, bit for bit."""
+    torch.manual_seed(M)
+    N, K = 2560, 10240
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.004 + 1e-4
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    add = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    C = ops.ext()
+    Mpad = (M + 15) // 16 * 16
+    for sx in (torch.rand(M, device=cuda) * 0.004 + 1e-4, torch.rand(K // 64, Mpad, device=cuda) * 0.004 + 1e-4):
+        y = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+        fused = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K, add)
+        assert torch.equal(fused, y + add)
+    xb = torch.randn(M, K, device=cuda).bfloat16()
+    wb = (torch.randn(N, K, device=cuda) * 0.02).bfloat16()
+    wpb = ops.pack_bf16_weight(wb)
+    yb = C.gemv_bf16(xb, wpb, bias, N, 0)
+    assert torch.equal(C.gemv_bf16(xb, wpb, bias, N, 0, add), yb + add)
