@@ -257,6 +257,7 @@ struct FaGeo {
   static constexpr int TILE = FA_KT * ROWB;              // one K (or V) tile
   static constexpr int SLOT = 2 * TILE;
   static constexpr int LDS = FA_RING * SLOT;             // 96 KiB (D 128) / 48 KiB (D 64)
+  static constexpr int LDS_STG = (FA_RING + 1) * SLOT;   // the staggered form's 4-slot ring
   static constexpr int RPP = 1024 / ROWB;                // key rows per 1 KiB DMA piece
   static constexpr int PIECES = TILE / 1024;             // per K (or V) tile
   static constexpr int PPW = 2 * PIECES / FA_W;          // pieces per wave per tile
@@ -272,7 +273,11 @@ __device__ __forceinline__ v16f mfma32_bf16(const v8s& a, const v8s& b, const v1
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int D, bool CAUSAL>
+// STG (stagger): waves 4-7 (the partners of waves 0-3 on the same SIMDs) defer each tile's O^T += V^T
+// P^T to the next tile's interval, so on every SIMD one wave's softmax VALU runs beside the other's
+// MFMAs instead of both waves hitting the same phase after each barrier (MI355X microarch item 9).
+// The deferred V tile stays readable one barrier longer, so the ring grows to 4 slots.
+template <int D, bool CAUSAL, bool STG = false>
 __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc, int64_t c_sb,
     int64_t c_sh, const int* __restrict__ start_pos, bf16_t* __restrict__ out, int T, int Hq, int Hkv,
@@ -303,9 +308,10 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     qf[kk] = tq < T ? *reinterpret_cast<const v8s*>(q + (((size_t)b * T + tq) * Hq + h) * D + kk * 16 + hf * 8)
                     : v8s{0, 0, 0, 0, 0, 0, 0, 0};
 
-  // ---- LDS-DMA of tile t into ring slot t % 3: 1 KiB pieces of RPP key rows, PPW per wave
+  // ---- LDS-DMA of tile t into ring slot t % RING: 1 KiB pieces of RPP key rows, PPW per wave
+  constexpr int RING = STG ? FA_RING + 1 : FA_RING;
   auto issue = [&](int t) {
-    char* slot = smem + (t % FA_RING) * G::SLOT;
+    char* slot = smem + (t % RING) * G::SLOT;
 #pragma unroll
     for (int j = 0; j < G::PPW; ++j) {
       const int p = wave * G::PPW + j;                         // [0, PIECES) K, then V
@@ -326,6 +332,43 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
   float m_i = -INFINITY, l_i = 0.f;
 
+  // O rescale (only when some query's running max moved: alpha != 1; multiplying by exactly 1 is the
+  // identity, so the skip is bit-exact and past the first tiles a new maximum is rare), then
+  // O^T += V^T P^T: per 16-key step, lane group g reads keys {4 hf .. +3} and {8 + 4 hf .. +3}
+  auto pv = [&](const char* vl, const v8s (&pb)[2][2], float alpha) {
+    if (__any(alpha != 1.f)) {
+#pragma unroll
+      for (int i = 0; i < G::DB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    }
+    const int c16 = lane & 15, qq = c16 >> 2, pq = c16 & 3, g2 = (lane >> 4) & 1;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kr1 = kb * 32 + ks * 16 + 4 * hf + qq, kr2 = kr1 + 8;
+#pragma unroll
+        for (int db = 0; db < G::DB; ++db) {
+          const int d0 = db * 32 + g2 * 16 + 4 * pq;
+          const char* a1 = vl + kr1 * G::ROWB + (((d0 >> 3) ^ G::swz(kr1)) << 4) + (d0 & 7) * 2;
+          const char* a2 = vl + kr2 * G::ROWB + (((d0 >> 3) ^ G::swz(kr2)) << 4) + (d0 & 7) * 2;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
+          const v8s vf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[db] = mfma32_bf16(vf, pb[kb][ks], o[db]);
+        }
+        // bound the V fragments the compiler keeps in flight to one 16-key step (register budget:
+        // 2 waves / SIMD = 256 VGPRs, and a spill would join this kernel's counted vmcnt)
+        asm volatile("" ::: "memory");
+      }
+  };
+  const bool late = STG && wave >= FA_W / 2;                   // wave-uniform
+  bool pend = false;
+  v8s pb_p[2][2];
+  float alpha_p = 1.f;
+  const char* vl_p = smem;
+
   if (ntiles > 0) issue(0);
   if (ntiles > 1) issue(1);
   for (int t = 0; t < ntiles; ++t) {
@@ -333,9 +376,15 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                              // tile t landed; slot of t - 1 free
     if (t + 2 < ntiles) issue(t + 2);
+    if constexpr (STG) {
+      if (late && pend) {                                      // the previous tile's O^T += V^T P^T
+        pv(vl_p, pb_p, alpha_p);
+        pend = false;
+      }
+    }
     const int k0 = t * FA_KT;
     if (wq0 >= T || (CAUSAL && k0 > s0 + wq0 + 31)) continue;  // nothing visible for this wave
-    const char* kl = smem + (t % FA_RING) * G::SLOT;
+    const char* kl = smem + (t % RING) * G::SLOT;
     const char* vl = kl + G::TILE;
 
     // ---- S^T = K Q^T for the two 32-key blocks
@@ -389,36 +438,22 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     rs += __shfl_xor(rs, 32, 64);
     l_i = l_i * alpha + rs;
     m_i = mnew;
-    // O rescale only when some query's running max moved (alpha != 1; multiplying by exactly 1 is
-    // the identity, so the skip is bit-exact): past the first tiles a new maximum is rare
-    if (__any(alpha != 1.f)) {
+    if constexpr (STG) {
+      if (late) {                                              // O^T update deferred one tile
 #pragma unroll
-      for (int i = 0; i < G::DB; ++i)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-    }
-
-    // ---- O^T += V^T P^T: per 16-key step, lane group g reads keys {4 hf .. +3} and {8 + 4 hf .. +3}
-    const int c16 = lane & 15, qq = c16 >> 2, pq = c16 & 3, g2 = (lane >> 4) & 1;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int kr1 = kb * 32 + ks * 16 + 4 * hf + qq, kr2 = kr1 + 8;
-#pragma unroll
-        for (int db = 0; db < G::DB; ++db) {
-          const int d0 = db * 32 + g2 * 16 + 4 * pq;
-          const char* a1 = vl + kr1 * G::ROWB + (((d0 >> 3) ^ G::swz(kr1)) << 4) + (d0 & 7) * 2;
-          const char* a2 = vl + kr2 * G::ROWB + (((d0 >> 3) ^ G::swz(kr2)) << 4) + (d0 & 7) * 2;
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
-          const v8s vf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[db] = mfma32_bf16(vf, pb[kb][ks], o[db]);
-        }
-        // bound the V fragments the compiler keeps in flight to one 16-key step (register budget:
-        // 2 waves / SIMD = 256 VGPRs, and a spill would join this kernel's counted vmcnt)
-        asm volatile("" ::: "memory");
+          for (int ks = 0; ks < 2; ++ks) pb_p[kb][ks] = pb[kb][ks];
+        alpha_p = alpha;
+        vl_p = vl;
+        pend = true;
+        continue;
       }
+    }
+    pv(vl, pb, alpha);
+  }
+  if constexpr (STG) {
+    if (late && pend) pv(vl_p, pb_p, alpha_p);                 // no DMA after the last tile: slot intact
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // no DMA outlives the workgroup
 
@@ -440,7 +475,8 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
 }  // namespace
 
 static int g_prefill_fa = 1;           // tune key "prefill_fa": 0 = the 16-row kernel only, 1 = auto, 2 = fa_kernel always
-extern "C" void edge_prefill_fa(int v) { g_prefill_fa = v; }
+static int g_prefill_fa_stag = 1;      // tune key "prefill_fa", second value: 1 = staggered wave halves, 0 = lockstep (A/B)
+extern "C" void edge_prefill_fa(int v, int stag) { g_prefill_fa = v; g_prefill_fa_stag = stag; }
 
 extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
                                  const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
@@ -462,9 +498,24 @@ extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void*
                                 FaGeo<DD>::LDS);                                                                   \
       (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
                                 FaGeo<DD>::LDS);                                                                   \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                FaGeo<DD>::LDS_STG);                                                               \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                FaGeo<DD>::LDS_STG);                                                               \
       fa_attr = true;                                                                                              \
     }                                                                                                              \
     const dim3 g((T + FA_QT - 1) / FA_QT, Hq, B);                                                                  \
+    if (g_prefill_fa_stag) {                                                                                       \
+      if (causal)                                                                                                  \
+        hipLaunchKernelGGL((fa_kernel<DD, true, true>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, (const bf16_t*)q,  \
+                           (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T,  \
+                           Hq, Hkv, sl2);                                                                          \
+      else                                                                                                         \
+        hipLaunchKernelGGL((fa_kernel<DD, false, true>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, (const bf16_t*)q, \
+                           (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T,  \
+                           Hq, Hkv, sl2);                                                                          \
+      break;                                                                                                       \
+    }                                                                                                              \
     if (causal)                                                                                                    \
       hipLaunchKernelGGL((fa_kernel<DD, true>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, (const bf16_t*)q,              \
                          (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \

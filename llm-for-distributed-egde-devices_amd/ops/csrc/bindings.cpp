@@ -40,7 +40,7 @@ int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, fl
                 int64_t* out_tok, void* workspace, hipStream_t st);
 size_t edge_sample_workspace(int B, int V);
 void edge_sample_rowwide_min(int v);
-void edge_prefill_fa(int v);
+void edge_prefill_fa(int v, int stag);
 int edge_sample_timestamps(int enable, unsigned long long* host_out16);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st, int mode, int* used);
@@ -865,7 +865,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "decode_attn_early") edge_decode_attn_early((int)a);
     else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);
     else if (what == "sample_rowwide") edge_sample_rowwide_min((int)a);
-    else if (what == "prefill_fa") edge_prefill_fa((int)a);
+    else if (what == "prefill_fa") edge_prefill_fa((int)a, b == 0 ? 1 : (int)b - 1);   // b: 0 default, 1 lockstep, 2 stagger
     else if (what == "bf16_ring") edge_bf16_ring_cfg((int)a, (int)b);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });

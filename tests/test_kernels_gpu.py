@@ -132,12 +132,14 @@ def test_prefill_attention(cuda, Hq, Hkv, D, T, starts):
     _close(out, ref, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("stag", [2, 1])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("Hq,Hkv,T,starts", [(8, 2, 600, (0, 300)), (4, 4, 1100, (0,)), (8, 8, 257, (0, 64)),
                                             (4, 1, 40, (1000, 3))])
-def test_prefill_attention_fa128(cuda, causal, Hq, Hkv, T, starts):
+def test_prefill_attention_fa128(cuda, stag, causal, Hq, Hkv, T, starts):
     """The D = 128 LDS-DMA ring kernel (fa_kernel) over many key tiles (ring wrap), partial query
-    tiles, chunked prefill offsets, GQA, against the fp32 reference and the 16-row kernel."""
+    tiles, chunked prefill offsets, GQA, against the fp32 reference and the 16-row kernel; both the
+    staggered (waves 4-7 defer each tile's P.V one tile, 4-slot ring) and the lockstep form."""
     C = ops.ext()
     D, B = 128, len(starts)
     S = max(starts) + T + 3
@@ -148,7 +150,7 @@ def test_prefill_attention_fa128(cuda, causal, Hq, Hkv, T, starts):
     scale = 1 / math.sqrt(D)
     ref = _ref.prefill_attention(q, kc, vc, sp, scale, causal)
     try:
-        C.tune("prefill_fa", 2, 0)                  # fa_kernel whatever the grid size
+        C.tune("prefill_fa", 2, stag)               # fa_kernel whatever the grid size
         out = C.prefill_attn(q, kc, vc, sp, scale, causal)
         C.tune("prefill_fa", 0, 0)
         old = C.prefill_attn(q, kc, vc, sp, scale, causal)

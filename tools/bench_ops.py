@@ -262,8 +262,8 @@ def prefill_rows(C, dev, Hq, D):
         sp0 = torch.full((1,), s0, dtype=torch.int32, device=dev)
         flops = 4 * T * (s0 + T / 2) * D * Hq
         row = dict(op="prefill_attn_causal", T=T, start=s0, H=Hq, Hkv=Hkv, D=D)
-        for name, v in (("fa", 2), ("old", 0)):
-            C.tune("prefill_fa", v, 0)
+        for name, v, stg in (("fa", 2, 2), ("fa_lockstep", 2, 1), ("old", 0, 0)):
+            C.tune("prefill_fa", v, stg)
             t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=10)
             row[f"{name}_us"], row[f"{name}_TFLOPs"] = round(t, 2), round(flops / t / 1e6, 1)
         C.tune("prefill_fa", 1, 0)
