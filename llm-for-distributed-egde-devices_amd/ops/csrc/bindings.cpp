@@ -88,6 +88,7 @@ int edge_gemm_bf16_ring(const void* A, const void* W, const void* bias, void* ou
 int edge_bf16_ring_splits(int N, int K);
 void edge_bf16_ring_cfg(int cfg, int min_rows);
 int edge_bf16_ring_min_rows();
+void edge_bf16_ring_splits_cfg(int s);
 void edge_decode_attn_gsplit(int v);
 void edge_decode_attn_early(int v);
 }
@@ -867,6 +868,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "sample_rowwide") edge_sample_rowwide_min((int)a);
     else if (what == "prefill_fa") edge_prefill_fa((int)a, b == 0 ? 1 : (int)b - 1);   // b: 0 default, 1 lockstep, 2 stagger
     else if (what == "bf16_ring") edge_bf16_ring_cfg((int)a, (int)b);
+    else if (what == "bf16_ring_splits") edge_bf16_ring_splits_cfg((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });
 }

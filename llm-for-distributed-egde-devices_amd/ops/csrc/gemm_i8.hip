@@ -2195,11 +2195,13 @@ int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int 
 }  // namespace
 
 // Split-K slices S for the bf16 ring path's EPI_PART at this (N, K): >= 4 stages of 64 k per slice
+static int g_bfr_splits = 0;                           // tune "bf16_ring_splits": forced S (0 = automatic)
+extern "C" void edge_bf16_ring_splits_cfg(int s) { g_bfr_splits = s; }
 extern "C" int edge_bf16_ring_splits(int N, int K) {
   const int stages = K / 64;                           // 128-B stages of bf16 k
   // two slices halve each workgroup's activation re-reads; narrow N takes more to fill the chip
   const int NTt = N / 16;
-  int S = NTt >= 192 ? 2 : (NTt >= 64 ? 4 : 8);
+  int S = g_bfr_splits > 0 ? g_bfr_splits : (NTt >= 192 ? 2 : (NTt >= 64 ? 4 : 8));
   while (S > 1 && stages < 4 * S) --S;
   return S;
 }

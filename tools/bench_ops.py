@@ -660,6 +660,34 @@ def magic_rows(C, dev, M=256):
     return out
 
 
+def bf16_splits_rows(C, dev, Ms=(128, 256)):
+    """bf16 ring split-K slice count for o / down (tune bf16_ring_splits), interleaved."""
+    out = []
+    for name, (N, K) in {"o": (4096, 4096), "down": (4096, 11008)}.items():
+        ncopy = max(2, (1 << 30) // (2 * N * K) + 1)
+        wps = [ops.pack_bf16_weight((torch.randn(N, K, device=dev) * 0.02).bfloat16()) for _ in range(ncopy)]
+        for M in Ms:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            ctr = [0]
+            res = {}
+            for _ in range(2):
+                for S in (2, 4, 8):
+                    if K // 64 < 4 * S:
+                        continue
+
+                    def call():
+                        ctr[0] = (ctr[0] + 1) % ncopy
+                        return C.gemm_bf16_ring(x, wps[ctr[0]], None, N, 3, S)
+                    res.setdefault(S, []).append(timeit(call, iters=10, per_graph=ncopy))
+            row = dict(op="bf16_ring_splits", shape=name, M=M, N=N, K=K)
+            for S, ts in res.items():
+                row[f"S{S}_us"] = round(min(ts), 2)
+            out.append(row)
+            print(row, flush=True)
+        del wps
+    return out
+
+
 def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
     """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
     interleaved in one process ((form, issue): form 0 automatic, 2 / 3 the LDS-DMA ring kernel at
@@ -730,6 +758,8 @@ def main():
         rows += rows256_diag(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
+    if only is not None and "bf16splits" in only:
+        rows += bf16_splits_rows(C, dev)
     if only is not None and "magic" in only:
         rows += magic_rows(C, dev)
     if only is not None and "prio" in only:
