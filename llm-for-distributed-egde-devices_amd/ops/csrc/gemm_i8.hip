@@ -2201,9 +2201,11 @@ static int g_bfr_splits = 0;                           // tune "bf16_ring_splits
 extern "C" void edge_bf16_ring_splits_cfg(int s) { g_bfr_splits = s; }
 extern "C" int edge_bf16_ring_splits(int N, int K) {
   const int stages = K / 64;                           // 128-B stages of bf16 k
-  // two slices halve each workgroup's activation re-reads; narrow N takes more to fill the chip
+  // fewer slices halve each workgroup's activation re-reads; narrow N takes more to fill the chip.
+  // N = 4096 measured S=4 over S=2 (o 14.4 vs 15.2 us at 128 rows, down 37.5 vs 42.8 us at 256 rows;
+  // +1.6 % / +3.1 % bench tok/s at 1x256 / 2x128, profiles/bench_ops_r3_bf16splits.json)
   const int NTt = N / 16;
-  int S = g_bfr_splits > 0 ? g_bfr_splits : (NTt >= 192 ? 2 : (NTt >= 64 ? 4 : 8));
+  int S = g_bfr_splits > 0 ? g_bfr_splits : (NTt >= 384 ? 2 : (NTt >= 64 ? 4 : 8));
   while (S > 1 && stages < 4 * S) --S;
   return S;
 }
