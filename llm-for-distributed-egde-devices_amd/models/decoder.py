@@ -30,7 +30,7 @@ import torch.nn as nn
 from .. import ops
 from ..utils import tracing
 from .configs import ModelConfig
-from .layers import Linear, Norm, PartialSum, QAct, act_fn, quant_if
+from .layers import Linear, Norm, PartialSum, PendingNorm, QAct, act_fn, quant_if
 
 # split-K slices of the bf16 o / down decode GEMVs (0 = off); N = 2048-4096 outputs have only
 # 128-256 tiles, so two slices put every CU to work
@@ -162,6 +162,10 @@ class MLP(nn.Module):
     def forward(self, x, add=None):
         """``add``: the attention branch of a parallel-residual block, added to the down
         projection's output (in its decode GEMV's epilogue)."""
+        if isinstance(x, PendingNorm):
+            if getattr(self.up, "glu_blocked", False):     # batch 1: norm in the gate_up prologue
+                return self.down(self.up.glu(x), add=add)
+            x = x.materialize()
         if getattr(self.up, "glu_blocked", False):
             # W8A8 SwiGLU with 16-blocked gate_up rows: decode-sized batches take the fused
             # GEMV + SwiGLU epilogue (int8 h with per-group scales, or bf16 h that the down
@@ -211,9 +215,12 @@ class DecoderLayer(nn.Module):
         qa = self.attn.qkv.takes_quantized_input
         qm = self.mlp.up.takes_quantized_input
         if not cfg.parallel_residual:
-            n1, h = self.norm1(x, residual, quant=qa)
+            # batch 1: each norm of a split-K sum runs in the prologue of the W8A8 GEMV after it
+            d1 = getattr(self.attn.qkv, "pending_norm_ok", lambda glu=False: False)()
+            d2 = getattr(self.mlp.up, "pending_norm_ok", lambda glu=False: False)(glu=True)
+            n1, h = self.norm1(x, residual, quant=qa, defer=d1)
             a = self.attn(n1, ctx)
-            n2, h2 = self.norm2(a, h, quant=qm)
+            n2, h2 = self.norm2(a, h, quant=qm, defer=d2)
             return self.mlp(n2), h2
         if cfg.shared_input_norm:                      # phi
             n, h = self.norm1(x, residual, quant=qa and qm)

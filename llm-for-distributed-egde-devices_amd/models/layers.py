@@ -38,6 +38,23 @@ class PartialSum(NamedTuple):
         return acc.to(torch.bfloat16)
 
 
+class PendingNorm(NamedTuple):
+    """RMSNorm + per-token int8 quant of a batch-1 split-K PartialSum (+ residual), deferred into
+    the prologue of the W8A8 GEMV that consumes it (ops.w8a8_gemv_norm): one launch fewer per
+    norm.  ``h`` is the residual-stream output [1, H], written by that GEMV.  ``materialize()``
+    runs the norm kernel instead (into ``h``) for a consumer that cannot take it."""
+    parts: torch.Tensor
+    residual: torch.Tensor
+    weight: torch.Tensor
+    eps: float
+    h: torch.Tensor
+
+    def materialize(self) -> "QAct":
+        y, s, r = ops.rms_norm_parts(self.parts, self.residual, self.weight, self.eps, True)
+        self.h.copy_(r.view_as(self.h))
+        return QAct(y, s)
+
+
 class GroupQuantBF16(NamedTuple):
     """bf16 activation that a W8A8 consumer quantises per (token, 64 columns) on the fly."""
     x: torch.Tensor
@@ -101,9 +118,15 @@ class Norm(nn.Module):
         self.bias = (nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device), requires_grad=False)
                      if kind == "layer" else None)
 
-    def forward(self, x, residual=None, quant: bool = False):
+    def forward(self, x, residual=None, quant: bool = False, defer: bool = False):
         """Returns (y, residual_out) where residual_out = x + residual; y is a QAct when quant.
-        ``x`` may be a PartialSum (split-K projection output), summed inside the norm kernel."""
+        ``x`` may be a PartialSum (split-K projection output), summed inside the norm kernel.
+        ``defer`` (the consumer is a W8A8 GEMV that takes it): at batch 1, y is a PendingNorm that
+        the consumer's kernel computes, and residual_out is the buffer it fills."""
+        if defer and quant and isinstance(x, PartialSum) and self.kind == "rms" and residual is not None \
+                and ops.gemv_norm_ok(x.parts):
+            h = torch.empty(1, x.parts.shape[2], dtype=residual.dtype, device=residual.device)
+            return PendingNorm(x.parts, residual, self.weight, self.eps, h), h
         if isinstance(x, PartialSum):
             if self.kind == "rms" and x.parts.is_cuda and ops.gpu_path(x.parts):
                 y, s, r = ops.rms_norm_parts(x.parts, residual, self.weight, self.eps, quant)

@@ -77,6 +77,26 @@ def rms_norm_parts(parts, residual, weight, eps, quant: bool):
     return ext().rms_norm_parts(parts, residual, weight, eps, quant)
 
 
+def gemv_norm_ok(parts) -> bool:
+    """Whether a batch-1 W8A8 GEMV can take the RMSNorm of these split-K slices [S, 1, K] in its
+    prologue (gemm_i8.hip NormIn: K 2048 / 4096, S <= 4; tune knob ``gemv_norm``)."""
+    return parts.is_cuda and parts.dim() == 3 and parts.shape[1] == 1 and 1 <= parts.shape[0] <= 4 \
+        and parts.shape[2] in (2048, 4096) and available() and bool(ext().gemv_norm_on())
+
+
+def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
+                   glu_quant: bool = False):
+    """Batch-1 W8A8 GEMV over RMSNorm(sum(parts) + residual), per-token int8, with the norm in the
+    GEMV's prologue; the new residual row goes to ``res_out``.  Returns bf16 y [1, N], or with
+    ``glu_quant`` (16-blocked gate_up) the quantising SwiGLU's (q [1, N/2], scales [N/128, 16]);
+    None when no kernel takes the shape (the caller runs the norm kernel instead)."""
+    r = ext().w8a8_gemv_norm(parts, residual.contiguous(), gamma, eps, res_out, w_packed, w_scale, bias, N, K,
+                             2 if glu_quant else 0)
+    if r is None:
+        return None
+    return r if glu_quant else r[0]
+
+
 def decode_rows_ok(M: int, K: int, splits: int = 1) -> bool:
     """Whether the decode GEMV family (grouped scales, split-K, quantising GLU) takes M rows at
     this K: every K up to 64 rows; 65-128 rows (two micro-batches in one) for the k-tile counts

@@ -320,14 +320,137 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
   }
 }
 
-template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI>
+// Batch-1 RMSNorm prologue (NRM > 0): the activation row is not an input but the RMSNorm of the
+// previous split-K projection's fp32 partial slices plus the residual row, quantised per token
+// (rowwise.hip norm_kernel<PART, HAS_RES, QUANT> moved into the consumer: one launch fewer per
+// norm, and the first weight step is in flight while the row is normalised).  Threads 0-255 run
+// the norm kernel's exact element layout and reduction order (NRM = its NCH chunks of 8 per
+// thread), so the int8 row and its scale are bit-identical; workgroup 0 writes the new residual.
+struct NormIn {
+  const float* part;      // [S][K] fp32 slices
+  const bf16_t* res;      // [K] residual in
+  const bf16_t* gamma;    // [K]
+  bf16_t* res_out;        // [K] residual out (must not alias res: other workgroups still read it)
+  float eps;
+  int S;
+};
+
+template <int NCH>
+__device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int8_t* aq, float* nsa, float* nred) {
+  const int t = threadIdx.x, w = t >> 6;
+  const bool act = t < 256;
+  float v[NCH][8];
+  float ss = 0.f, amax = 0.f;
+  if (act) {
+    uint4 rv[NCH];
+    float4 pv[NCH][4][2];                                   // S <= 4 slices (register budget)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = min((c * 256 + t) * 8, H - 8);
+      rv[c] = *reinterpret_cast<const uint4*>(na.res + e);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < na.S) {
+          const float4* p = reinterpret_cast<const float4*>(na.part + (size_t)k * H + e);
+          pv[c][k][0] = p[0];
+          pv[c][k][1] = p[1];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < na.S) {
+          const float4 p0 = pv[c][k][0], p1 = pv[c][k][1];
+          v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
+          v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
+        }
+      if (e < H) {
+        unpack8(pack8(v[c]), v[c]);                         // the projection's bf16 output
+        float r[8];
+        unpack8(rv[c], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+        const uint4 u = pack8(v[c]);                        // residual stream in bf16
+        if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + e) = u;
+        unpack8(u, v[c]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (e < H) ? v[c][j] - 0.f : 0.f;
+        ss += d * d;
+      }
+    }
+    ss = wave_sum(ss);
+    if ((t & 63) == 0) nred[w] = ss;
+  }
+  __syncthreads();
+  const float rstd = rsqrtf((((0.f + nred[0]) + nred[1]) + nred[2] + nred[3]) / (float)H + na.eps);
+  __syncthreads();
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        float wf[8];
+        unpack8(*reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - 0.f) * rstd * wf[j];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[c][j]));
+    amax = wave_max(amax);
+    if ((t & 63) == 0) nred[w] = amax;
+  }
+  __syncthreads();
+  float gm = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gm = fmaxf(gm, nred[i]);
+  gm = fmaxf(gm, 1e-8f);
+  const float inv = 127.f / gm;
+  if (t == 0) nsa[0] = gm / 127.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[c][j], inv)) << (8 * j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[c][4 + j], inv)) << (8 * j);
+        *reinterpret_cast<uint2*>(aq + e) = make_uint2(lo, hi);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI, int NRM = 0>
 __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                  const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                  const bf16_t* __restrict__ bias, void* __restrict__ outv,
                                                                  float* __restrict__ os, int M, int N, int K, int KT,
-                                                                 int NTt, int Mpad, int S) {
+                                                                 int NTt, int Mpad, int S, NormIn na) {
   constexpr int NW = TG * KW, TPW = NTW / TG;
   static_assert(NTW % TG == 0, "tiles split evenly over tile groups");
+  static_assert(NRM == 0 || (MB == 1 && AMODE == A_TOKEN && EPI != EPI_PART && NW == 16), "norm prologue: batch 1");
+  // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
+  __shared__ int8_t aq_l[NRM > 0 ? NRM * 2048 : 16];
+  __shared__ float nsa[16], nred[16];
   constexpr bool GELUQ = EPI == EPI_GELUQT || EPI == EPI_GELUQE;
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && (GELUQ || TPW % 2 == 0)),
                 "GLU: gate/up pairs per wave, per-token A");
@@ -361,8 +484,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   }
   const int8_t* ap[MB];
 #pragma unroll
-  for (int i = 0; i < MB; ++i) ap[i] = A + (size_t)min(i * 16 + (lane & 15), M - 1) * K;
-  const bool kfull = (K & 63) == 0;
+  for (int i = 0; i < MB; ++i) ap[i] = NRM > 0 ? aq_l : A + (size_t)min(i * 16 + (lane & 15), M - 1) * K;
+  const bool kfull = NRM > 0 || (K & 63) == 0;
   const auto pre = epi_preload<MB, NTW, NW, EPI>(sw, bias, nt0, NTt, wave, lane);
   v4i acc[TPW][MB];
   v4f accf[TPW][MB];
@@ -378,12 +501,14 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   };
   // one step = U k-tiles: weight fragments (nontemporal), activation fragments and (SCALED)
   // per-group scales; clamped addresses, no branches
-  auto issue = [&](Step& st, int kbase) {
+  auto issue_w = [&](Step& st, int kbase) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < TPW; ++j)
         st.b[u][j] = __builtin_nontemporal_load(wp[j] + (size_t)min(kbase + u * KW, kend - 1) * 64);
+  };
+  auto issue_a = [&](Step& st, int kbase) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = min(kbase + u * KW, kend - 1);
@@ -394,6 +519,20 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
         if constexpr (SCALED)
           st.sg[u][i] = *reinterpret_cast<const v4f*>(sa + (size_t)k * Mpad + min(i * 16, Mpad - 16) + 4 * (lane >> 4));
       }
+    }
+  };
+  auto issue = [&](Step& st, int kbase) {
+    issue_w(st, kbase);
+    issue_a(st, kbase);
+  };
+  // NRM: the first step's weight loads go out before the norm prologue; its activations after
+  auto first = [&](Step& st, int kbase) {
+    if constexpr (NRM > 0) {
+      issue_w(st, kbase);
+      norm_prologue<NRM>(na, K, aq_l, nsa, nred);
+      issue_a(st, kbase);
+    } else {
+      issue(st, kbase);
     }
   };
   auto compute = [&](const Step& st, int kbase) {
@@ -417,7 +556,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto fixed = [&](auto nk) {
     constexpr int NK = decltype(nk)::value, STEPS = (NK + KW * U - 1) / (KW * U);
     Step st[STEPS];
-    issue(st[0], kbeg + kw);
+    first(st[0], kbeg + kw);
 #pragma unroll
     for (int i = 0; i < STEPS; ++i) {                   // one step of lookahead, no register copies
       if (i + 1 < STEPS) issue(st[i + 1], kbeg + kw + (i + 1) * KW * U);
@@ -431,7 +570,21 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   if (FIXED_OK && nk == 64 && KW * U <= 64) fixed(std::integral_constant<int, 64>{});
   else if (FIXED_OK && nk == 32 && KW * U <= 32) fixed(std::integral_constant<int, 32>{});
   else if (FIXED_OK && nk == 16 && KW * U <= 16) fixed(std::integral_constant<int, 16>{});
-  else {
+  else if constexpr (NRM > 0) {
+    // next step's weights in flight during this step's MFMAs (the loop below leaves that to the
+    // scheduler; here the first step's weights are already loaded across the prologue)
+    Step st;
+    first(st, kbeg + kw);
+    for (int kt = kbeg + kw; kt < kend; kt += KW * U) {
+      Step nx;
+      if (kt + KW * U < kend) issue_w(nx, kt + KW * U);
+      compute(st, kt);
+      if (kt + KW * U < kend) {
+        issue_a(nx, kt + KW * U);
+        st = nx;
+      }
+    }
+  } else {
     for (int kt = kbeg + kw; kt < kend; kt += KW * U) {
       Step st;
       issue(st, kt);
@@ -459,8 +612,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     }
     __syncthreads();
   }
-  gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI>(&red[0][0][0], sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane,
-                                              ks);
+  gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI>(&red[0][0][0], NRM > 0 ? nsa : sa, pre, outv, os, gmax, M, N, NTt, Mpad,
+                                              nt0, wave, lane, ks);
 }
 
 // ------------------------------------------------------------------------ LDS-staged activations
@@ -1636,7 +1789,17 @@ int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, 
   const int NTt = (N + 15) / 16;
   hipLaunchKernelGGL((w8a8_gemv_kernel<MB, NTW, TG, KW, U, AM, EP>), dim3((NTt + NTW - 1) / NTW * S), dim3(TG * KW * 64),
                      0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, KT, NTt,
-                     Mpad, S);
+                     Mpad, S, NormIn{});
+  return (int)hipGetLastError();
+}
+
+template <int NTW, int TG, int KW, int EP, int NCH>
+int launch_norm(const NormIn& na, const void* Wp, const float* sw, const void* bias, void* out, float* os, int N,
+                int K, hipStream_t st) {
+  const int NTt = (N + 15) / 16;
+  hipLaunchKernelGGL((w8a8_gemv_kernel<1, NTW, TG, KW, 2, A_TOKEN, EP, NCH>), dim3((NTt + NTW - 1) / NTW),
+                     dim3(TG * KW * 64), 0, st, (const int8_t*)nullptr, (const float*)nullptr, (const int8_t*)Wp, sw,
+                     (const bf16_t*)bias, out, os, 1, N, K, K / 64, NTt, 16, 1, na);
   return (int)hipGetLastError();
 }
 
@@ -1966,6 +2129,33 @@ extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void*
   if (mblocks <= 2) SK(2, 16, A_TOKEN);
   SK(4, 8, A_TOKEN);
 #undef SK
+}
+
+// Batch-1 GEMV whose activation row is RMSNorm(sum of S fp32 partial slices + residual), int8
+// per token, computed in the kernel's prologue (NormIn above).  epi 0 (EPI_OUT: bf16 [1, N]) or
+// 2 (EPI_GLUQ: 16-blocked gate_up -> SwiGLU -> int8 per 64 features, `os` scales [N/128][16]).
+// K in {2048, 4096} (256 threads x NCH chunks of 8, NCH <= 2), 1 <= S <= 4; res_out written by
+// workgroup 0 and must not alias res.  -2: not taken.
+static int g_gemv_norm = 1;      // 0: the norm stays a kernel of its own (A/B knob "gemv_norm")
+extern "C" void edge_w8a8_gemv_norm_cfg(int on) { g_gemv_norm = on; }
+extern "C" int edge_w8a8_gemv_norm_on() { return g_gemv_norm; }
+extern "C" int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* gamma, float eps,
+                                   void* res_out, const void* Wp, const float* sw, const void* bias, void* out,
+                                   float* os, int N, int K, int epi, hipStream_t st) {
+  if (S < 1 || S > 4 || (K != 2048 && K != 4096) || N % 16 != 0 || res == nullptr || res_out == nullptr ||
+      res == res_out)
+    return -2;
+  const NormIn na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};
+  if (epi == EPI_OUT) {
+    return K == 4096 ? launch_norm<3, 1, 16, EPI_OUT, 2>(na, Wp, sw, bias, out, nullptr, N, K, st)
+                     : launch_norm<3, 1, 16, EPI_OUT, 1>(na, Wp, sw, bias, out, nullptr, N, K, st);
+  }
+  if (epi == EPI_GLUQ) {
+    if (N % 128 != 0 || os == nullptr) return -2;
+    return K == 4096 ? launch_norm<8, 2, 8, EPI_GLUQ, 2>(na, Wp, sw, bias, out, os, N, K, st)
+                     : launch_norm<8, 2, 8, EPI_GLUQ, 1>(na, Wp, sw, bias, out, os, N, K, st);
+  }
+  return -2;
 }
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).

@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops import _ref
-from ..models.layers import GroupQuantBF16, Linear, PartialSum, QAct
+from ..models.layers import GroupQuantBF16, Linear, PartialSum, PendingNorm, QAct
 
 # Decode MLP policy (A/B on MI355X, Llama-2-7B, profiles/bench_ops_r1_gemv16.json): the gate_up
 # GEMV quantises silu(g) * u in its own epilogue (8 tiles = 64 features per workgroup) for every
@@ -116,6 +116,14 @@ class W8A8Linear(nn.Module):
     def forward(self, x, add=None):
         """``add``: the other branch of a parallel-residual block, added to the output (in the
         decode GEMV's epilogue at <= 64 rows)."""
+        if isinstance(x, PendingNorm):                # batch 1: the norm runs in this GEMV's prologue
+            y = None
+            if add is None and not self.split_k_out:
+                y = ops.w8a8_gemv_norm(x.parts, x.residual, x.weight, x.eps, x.h, self.w_packed, self.w_scale,
+                                       self.bias, self.out_features, self.in_features)
+            if y is not None:
+                return y
+            x = x.materialize()
         if isinstance(x, GroupQuantBF16):             # decode: per-(token, 64) int8 input
             x = QAct(*ops.quant_per_group(x.x.reshape(-1, self.in_features)))
         if not isinstance(x, QAct):
@@ -148,11 +156,25 @@ class W8A8Linear(nn.Module):
         return M <= 64 or (self.out_features % 128 == 0 and ops.decode_rows_ok(M, self.in_features)
                            and ops.group_scale_rows_ok(M))
 
+    def pending_norm_ok(self, glu: bool = False) -> bool:
+        """Whether this projection takes a PendingNorm (batch-1 RMSNorm in its GEMV prologue)."""
+        if glu:
+            return self.glu_blocked and self.out_features % 128 == 0
+        return not self.split_k_out and not self.glu_blocked
+
     def glu(self, x: QAct):
         """Fused gate_up -> silu(g) * u (blocked layout, M <= 64) for the down projection: int8
         quantised per (token, 64 features) in the same kernel (``QAct`` with 2-D scales) when
-        ``glu_quant_rows(M)``, else bf16 h that the down projection quantises per group."""
+        ``glu_quant_rows(M)``, else bf16 h that the down projection quantises per group.  A
+        PendingNorm input (batch 1) is normalised in the same kernel's prologue."""
         K, N = self.in_features, self.out_features
+        if isinstance(x, PendingNorm):
+            if N % 128 == 0:
+                r = ops.w8a8_gemv_norm(x.parts, x.residual, x.weight, x.eps, x.h, self.w_packed, self.w_scale,
+                                       self.bias, N, K, glu_quant=True)
+                if r is not None:
+                    return QAct(*r)
+            x = x.materialize()
         M = x.q.numel() // K
         quant = N % 128 == 0 and (glu_quant_rows(M) or M > 64)
         out = ops.w8a8_glu(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,

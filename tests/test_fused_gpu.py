@@ -661,3 +661,80 @@ def test_gemv_addend_matches_unfused_add(cuda, M):
     wpb = ops.pack_bf16_weight(wb)
     yb = C.gemv_bf16(xb, wpb, bias, N, 0)
     assert torch.equal(C.gemv_bf16(xb, wpb, bias, N, 0, add), yb + add)
+
+
+@pytest.mark.parametrize("K,S", [(4096, 2), (4096, 1), (4096, 4), (2048, 4), (2048, 3)])
+def test_gemv_norm_prologue_bit_exact(cuda, K, S):
+    """Batch-1 RMSNorm in the consuming W8A8 GEMV's prologue (ops.w8a8_gemv_norm) == the norm kernel
+    over the split-K slices (ops.rms_norm_parts) followed by the plain GEMV / quantising SwiGLU
+    GEMV, bit for bit, and the new residual row it writes == the norm kernel's."""
+    torch.manual_seed(K + S)
+    parts = torch.randn(S, 1, K, device=cuda) * 0.5
+    res = torch.randn(1, K, device=cuda).bfloat16()
+    gamma = (torch.rand(K, device=cuda) + 0.5).bfloat16()
+    eps = 1e-5
+    q, s, r = ops.rms_norm_parts(parts, res, gamma, eps, True)
+    for N, glu in ((3 * K, False), (2 * 4 * K, True), (4 * K + 48, False)):
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+        wp = ops.pack_int8_weight(w)
+        sw = torch.rand(N, device=cuda) * 0.004 + 1e-4
+        bias = torch.randn(N, device=cuda).bfloat16()
+        h = torch.full((1, K), float("nan"), device=cuda).bfloat16()
+        fused = ops.w8a8_gemv_norm(parts, res, gamma, eps, h, wp, sw, bias, N, K, glu_quant=glu)
+        assert fused is not None
+        assert torch.equal(h, r)
+        if glu:
+            ref = ops.w8a8_glu(q, s, wp, sw, bias, N, K, quant=True)
+            assert torch.equal(fused[0], ref[0]) and torch.equal(fused[1], ref[1])
+        else:
+            assert torch.equal(fused, ops.w8a8_linear(q, s, wp, sw, bias, N, K))
+
+
+def test_gemv_norm_declines_unsupported(cuda):
+    """Shapes outside the prologue's layout return None (the caller runs the norm kernel)."""
+    K, N = 4096, 4096
+    wp = ops.pack_int8_weight(torch.zeros(N, K, dtype=torch.int8, device=cuda))
+    sw = torch.ones(N, device=cuda)
+    res = torch.zeros(1, K, device=cuda).bfloat16()
+    g = torch.ones(K, device=cuda).bfloat16()
+    h = torch.empty(1, K, device=cuda).bfloat16()
+    assert not ops.gemv_norm_ok(torch.zeros(5, 1, K, device=cuda))
+    assert ops.w8a8_gemv_norm(torch.zeros(5, 1, K, device=cuda), res, g, 1e-5, h, wp, sw, None, N, K) is None
+
+
+def test_llama_batch1_decode_defers_norms(cuda):
+    """A W8A8 Llama decoder (hidden 2048) at batch 1 runs its inner RMSNorms in the qkv / gate_up
+    GEMV prologues and produces the same logits as with the norm kernels (knob gemv_norm=0)."""
+    from edgellm.engine import KVCache
+    from edgellm.models import AttnCtx, build_model, tiny
+    from edgellm.models.layers import PendingNorm
+    from edgellm.quant import quantize_model
+    cfg = tiny("llama", hidden_size=2048, num_heads=16, num_kv_heads=4, intermediate_size=4096, num_layers=3)
+    qm = quantize_model(build_model(cfg, device=cuda, seed=5), "w8a8")
+    B, T = 1, 9
+    ids = torch.randint(0, cfg.vocab_size, (B, T), generator=torch.Generator().manual_seed(1)).to(cuda)
+    seen = []
+    orig = qm.layers[1].attn.qkv.forward
+
+    def spy(x, add=None):
+        seen.append(isinstance(x, PendingNorm))
+        return orig(x, add)
+
+    qm.layers[1].attn.qkv.forward = spy
+    C = ops.ext()
+    outs = []
+    try:
+        for on in (1, 0):
+            C.tune("gemv_norm", on, 0)
+            kv = KVCache(cfg, B, T + 4, dtype=qm.dtype, device=cuda)
+            sp = torch.zeros(B, dtype=torch.int32, device=cuda)
+            with torch.no_grad():
+                qm(ids, AttnCtx("prefill", B, T, sp, sp + T, T, kv.rows(0, B), qm.rope_table(cuda)), logits="last")
+                pos = torch.full((B,), T, dtype=torch.int32, device=cuda)
+                outs.append(qm(ids[:, -1:], AttnCtx("decode", B, 1, pos, pos + 1, T + 1, kv.rows(0, B),
+                                                    qm.rope_table(cuda))).float())
+    finally:
+        C.tune("gemv_norm", 1, 0)
+        del qm.layers[1].attn.qkv.forward
+    assert seen == [False, True, False, False], seen        # prefill, decode (knob on), prefill, decode
+    assert torch.equal(outs[0], outs[1])
