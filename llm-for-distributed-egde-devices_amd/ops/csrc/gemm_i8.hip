@@ -335,7 +335,7 @@ struct NormIn {
   int S;
 };
 
-template <int NCH>
+template <int NCH, int SMAX>
 __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int8_t* aq, float* nsa, float* nred) {
   const int t = threadIdx.x, w = t >> 6;
   const bool act = t < 256;
@@ -343,13 +343,13 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int8_t* a
   float ss = 0.f, amax = 0.f;
   if (act) {
     uint4 rv[NCH];
-    float4 pv[NCH][4][2];                                   // S <= 4 slices (register budget)
+    float4 pv[NCH][SMAX][2];                                // S <= SMAX slices (register budget)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int e = min((c * 256 + t) * 8, H - 8);
       rv[c] = *reinterpret_cast<const uint4*>(na.res + e);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
+      for (int k = 0; k < SMAX; ++k)
         if (k < na.S) {
           const float4* p = reinterpret_cast<const float4*>(na.part + (size_t)k * H + e);
           pv[c][k][0] = p[0];
@@ -362,7 +362,7 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int8_t* a
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
+      for (int k = 0; k < SMAX; ++k)
         if (k < na.S) {
           const float4 p0 = pv[c][k][0], p1 = pv[c][k][1];
           v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
@@ -449,7 +449,9 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   static_assert(NTW % TG == 0, "tiles split evenly over tile groups");
   static_assert(NRM == 0 || (MB == 1 && AMODE == A_TOKEN && EPI != EPI_PART && NW == 16), "norm prologue: batch 1");
   // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
-  __shared__ int8_t aq_l[NRM > 0 ? NRM * 2048 : 16];
+  // NRM = 8 * NCH + SMAX (norm_prologue<NCH, SMAX>)
+  constexpr int NCH_N = NRM / 8, SMAX_N = NRM % 8;
+  __shared__ int8_t aq_l[NRM > 0 ? NCH_N * 2048 : 16];
   __shared__ float nsa[16], nred[16];
   constexpr bool GELUQ = EPI == EPI_GELUQT || EPI == EPI_GELUQE;
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && (GELUQ || TPW % 2 == 0)),
@@ -529,7 +531,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto first = [&](Step& st, int kbase) {
     if constexpr (NRM > 0) {
       issue_w(st, kbase);
-      norm_prologue<NRM>(na, K, aq_l, nsa, nred);
+      norm_prologue<NCH_N, SMAX_N>(na, K, aq_l, nsa, nred);
       issue_a(st, kbase);
     } else {
       issue(st, kbase);
@@ -556,6 +558,19 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto fixed = [&](auto nk) {
     constexpr int NK = decltype(nk)::value, STEPS = (NK + KW * U - 1) / (KW * U);
     Step st[STEPS];
+    if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4) {
+      // batch-1 norm prologue: every step's weights (at most 2) in flight across it (K = 4096 with
+      // 4 slices keeps one step: its prologue registers would spill)
+#pragma unroll
+      for (int i = 0; i < STEPS; ++i) issue_w(st[i], kbeg + kw + i * KW * U);
+      norm_prologue<NCH_N, SMAX_N>(na, K, aq_l, nsa, nred);
+#pragma unroll
+      for (int i = 0; i < STEPS; ++i) {
+        issue_a(st[i], kbeg + kw + i * KW * U);
+        compute(st[i], kbeg + kw + i * KW * U);
+      }
+      return;
+    }
     first(st[0], kbeg + kw);
 #pragma unroll
     for (int i = 0; i < STEPS; ++i) {                   // one step of lookahead, no register copies
@@ -1793,11 +1808,11 @@ int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, 
   return (int)hipGetLastError();
 }
 
-template <int NTW, int TG, int KW, int EP, int NCH>
+template <int NTW, int TG, int KW, int EP, int NRM>
 int launch_norm(const NormIn& na, const void* Wp, const float* sw, const void* bias, void* out, float* os, int N,
                 int K, hipStream_t st) {
   const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_kernel<1, NTW, TG, KW, 2, A_TOKEN, EP, NCH>), dim3((NTt + NTW - 1) / NTW),
+  hipLaunchKernelGGL((w8a8_gemv_kernel<1, NTW, TG, KW, 2, A_TOKEN, EP, NRM>), dim3((NTt + NTW - 1) / NTW),
                      dim3(TG * KW * 64), 0, st, (const int8_t*)nullptr, (const float*)nullptr, (const int8_t*)Wp, sw,
                      (const bf16_t*)bias, out, os, 1, N, K, K / 64, NTt, 16, 1, na);
   return (int)hipGetLastError();
@@ -2146,15 +2161,19 @@ extern "C" int edge_w8a8_gemv_norm(const float* part, int S, const void* res, co
       res == res_out)
     return -2;
   const NormIn na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};
-  if (epi == EPI_OUT) {
-    return K == 4096 ? launch_norm<3, 1, 16, EPI_OUT, 2>(na, Wp, sw, bias, out, nullptr, N, K, st)
-                     : launch_norm<3, 1, 16, EPI_OUT, 1>(na, Wp, sw, bias, out, nullptr, N, K, st);
-  }
+  // template NRM = 8 * (K / 2048) + (S <= 2 ? 2 : 4): two-slice sums keep 32 VGPRs free, which
+  // lets the qkv form hold both of its weight steps across the prologue without spilling
+#define NRM_L(NTW, TG, KW, EP, OS)                                                                       \
+  return K == 4096 ? (S <= 2 ? launch_norm<NTW, TG, KW, EP, 18>(na, Wp, sw, bias, out, OS, N, K, st)     \
+                             : launch_norm<NTW, TG, KW, EP, 20>(na, Wp, sw, bias, out, OS, N, K, st))    \
+                   : (S <= 2 ? launch_norm<NTW, TG, KW, EP, 10>(na, Wp, sw, bias, out, OS, N, K, st)     \
+                             : launch_norm<NTW, TG, KW, EP, 12>(na, Wp, sw, bias, out, OS, N, K, st))
+  if (epi == EPI_OUT) NRM_L(3, 1, 16, EPI_OUT, nullptr);
   if (epi == EPI_GLUQ) {
     if (N % 128 != 0 || os == nullptr) return -2;
-    return K == 4096 ? launch_norm<8, 2, 8, EPI_GLUQ, 2>(na, Wp, sw, bias, out, os, N, K, st)
-                     : launch_norm<8, 2, 8, EPI_GLUQ, 1>(na, Wp, sw, bias, out, os, N, K, st);
+    NRM_L(8, 2, 8, EPI_GLUQ, os);
   }
+#undef NRM_L
   return -2;
 }
 
