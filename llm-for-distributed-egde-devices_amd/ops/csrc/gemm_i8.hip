@@ -2045,9 +2045,16 @@ extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
 // grouped-scale fold of the 256-row split-K kernels: 1 = one-VALU magic-number form, 0 = cvt + fma
 extern "C" void edge_w8a8_rows256_magic(int v) { g_r256_magic = v; }
 // split-K slices the 129-256-row kernels use for a K (0: none)
-static int g_r256_split_short = 2;      // tune "ring2_256_splits": slices for K < 8192 (o-like), A/B
-extern "C" void edge_w8a8_rows256_splits_cfg(int s) { g_r256_split_short = s == 4 ? 4 : 2; }
-extern "C" int edge_w8a8_rows256_splits(int K) { return K % 128 != 0 ? 0 : (K / 128 >= 64 ? 4 : g_r256_split_short); }
+// tune "ring2_256_splits=short[,long]": slices for K < 8192 (o-like) and K >= 8192 (down-like), A/B;
+// fewer slices also cut the fp32 partial bytes the next RMSNorm reads
+static int g_r256_split_short = 2, g_r256_split_long = 4;
+extern "C" void edge_w8a8_rows256_splits_cfg(int s, int l) {
+  g_r256_split_short = s == 4 ? 4 : 2;
+  g_r256_split_long = l == 2 || l == 8 ? l : 4;
+}
+extern "C" int edge_w8a8_rows256_splits(int K) {
+  return K % 128 != 0 ? 0 : (K / 128 >= 64 ? g_r256_split_long : g_r256_split_short);
+}
 // whether the 129-256-row decode kernels take this K (whole K; split-K at rows256_splits(K))
 extern "C" int edge_w8a8_rows256_ok(int K) { return K % 128 == 0 && K / 128 >= 8; }
 

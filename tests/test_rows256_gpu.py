@@ -118,3 +118,27 @@ def test_rows256_model_routes(cuda):
     output, split-K o / down partials, quantising GLU (decode_rows_ok routes 129-256 rows)."""
     assert ops.decode_rows_ok(256, 4096) and ops.decode_rows_ok(256, 11008, 4)
     assert not ops.decode_rows_ok(257, 4096)
+
+
+@pytest.mark.parametrize("short,long", [(2, 2), (4, 8), (2, 8)])
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 11008)])
+def test_rows256_splitk_slice_counts(cuda, short, long, M, N, K):
+    """Every slice count the ``ring2_256_splits=short,long`` knob selects (uneven stage splits
+    included: 86 stages in 8 slices) sums to the fp32 reference."""
+    C = ops.ext()
+    torch.manual_seed(M + K + long)
+    Mpad = (M + 15) // 16 * 16
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(K // 64, Mpad, device=cuda) * 0.01
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("ring2_256_splits", short, long)
+        parts = C.w8a8_gemm_splitk(qx, sx, wp, sw, None, N, K, 0)
+    finally:
+        C.tune("ring2_256_splits", 2, 0)
+    assert parts.shape == (long if K // 128 >= 64 else short, M, N)
+    ref = _ref.w8a8_linear(qx, sx, w, sw, None, torch.float32)
+    _close(parts.sum(0), ref, max(1e-3, 1e-4 * ref.abs().max().item()), 1e-2)
