@@ -215,7 +215,7 @@ class DecoderLayer(nn.Module):
         qa = self.attn.qkv.takes_quantized_input
         qm = self.mlp.up.takes_quantized_input
         if not cfg.parallel_residual:
-            # batch 1: each norm of a split-K sum runs in the prologue of the W8A8 GEMV after it
+            # <= 4 rows: each norm of a split-K sum runs in the prologue of the W8A8 GEMV after it
             d1 = getattr(self.attn.qkv, "pending_norm_ok", lambda glu=False: False)()
             d2 = getattr(self.mlp.up, "pending_norm_ok", lambda glu=False: False)(glu=True)
             n1, h = self.norm1(x, residual, quant=qa, defer=d1)

@@ -39,9 +39,9 @@ class PartialSum(NamedTuple):
 
 
 class PendingNorm(NamedTuple):
-    """RMSNorm + per-token int8 quant of a batch-1 split-K PartialSum (+ residual), deferred into
-    the prologue of the W8A8 GEMV that consumes it (ops.w8a8_gemv_norm): one launch fewer per
-    norm.  ``h`` is the residual-stream output [1, H], written by that GEMV.  ``materialize()``
+    """RMSNorm + per-token int8 quant of a decode split-K PartialSum (+ residual, M <= 4 rows),
+    deferred into the prologue of the W8A8 GEMV that consumes it (ops.w8a8_gemv_norm): one launch
+    fewer per norm.  ``h`` is the residual-stream output [M, H], written by that GEMV.  ``materialize()``
     runs the norm kernel instead (into ``h``) for a consumer that cannot take it."""
     parts: torch.Tensor
     residual: torch.Tensor
@@ -121,11 +121,11 @@ class Norm(nn.Module):
     def forward(self, x, residual=None, quant: bool = False, defer: bool = False):
         """Returns (y, residual_out) where residual_out = x + residual; y is a QAct when quant.
         ``x`` may be a PartialSum (split-K projection output), summed inside the norm kernel.
-        ``defer`` (the consumer is a W8A8 GEMV that takes it): at batch 1, y is a PendingNorm that
+        ``defer`` (the consumer is a W8A8 GEMV that takes it): at <= 4 rows, y is a PendingNorm that
         the consumer's kernel computes, and residual_out is the buffer it fills."""
         if defer and quant and isinstance(x, PartialSum) and self.kind == "rms" and residual is not None \
                 and ops.gemv_norm_ok(x.parts):
-            h = torch.empty(1, x.parts.shape[2], dtype=residual.dtype, device=residual.device)
+            h = torch.empty(x.parts.shape[1], x.parts.shape[2], dtype=residual.dtype, device=residual.device)
             return PendingNorm(x.parts, residual, self.weight, self.eps, h), h
         if isinstance(x, PartialSum):
             if self.kind == "rms" and x.parts.is_cuda and ops.gpu_path(x.parts):

@@ -78,17 +78,18 @@ def rms_norm_parts(parts, residual, weight, eps, quant: bool):
 
 
 def gemv_norm_ok(parts) -> bool:
-    """Whether a batch-1 W8A8 GEMV can take the RMSNorm of these split-K slices [S, 1, K] in its
-    prologue (gemm_i8.hip NormIn: K 2048 / 4096, S <= 4; tune knob ``gemv_norm``)."""
-    return parts.is_cuda and parts.dim() == 3 and parts.shape[1] == 1 and 1 <= parts.shape[0] <= 4 \
+    """Whether a decode W8A8 GEMV can take the RMSNorm of these split-K slices [S, M, K] in its
+    prologue (gemm_i8.hip NormIn: M <= 4, K 2048 / 4096, S <= 4; tune knob ``gemv_norm``)."""
+    return parts.is_cuda and parts.dim() == 3 and 1 <= parts.shape[1] <= 4 and 1 <= parts.shape[0] <= 4 \
         and parts.shape[2] in (2048, 4096) and available() and bool(ext().gemv_norm_on())
 
 
 def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
                    glu_quant: bool = False):
-    """Batch-1 W8A8 GEMV over RMSNorm(sum(parts) + residual), per-token int8, with the norm in the
-    GEMV's prologue; the new residual row goes to ``res_out``.  Returns bf16 y [1, N], or with
-    ``glu_quant`` (16-blocked gate_up) the quantising SwiGLU's (q [1, N/2], scales [N/128, 16]);
+    """Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual), per-token int8, with
+    the norm in the GEMV's prologue; the new residual rows go to ``res_out``.  Returns bf16 y [M, N],
+    or with ``glu_quant`` (16-blocked gate_up) the quantising SwiGLU's (q [M, N/2], scales
+    [N/128, 16]);
     None when no kernel takes the shape (the caller runs the norm kernel instead)."""
     r = ext().w8a8_gemv_norm(parts, residual.contiguous(), gamma, eps, res_out, w_packed, w_scale, bias, N, K,
                              2 if glu_quant else 0)

@@ -15,8 +15,8 @@ int edge_norm(const void* x, const void* res, const void* w, const void* b, void
               void* res_out, int rows, int H, float eps, int rms, int quant, const float* xpart, int S,
               hipStream_t st);
 int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* gamma, float eps, void* res_out,
-                        const void* Wp, const float* sw, const void* bias, void* out, float* os, int N, int K, int epi,
-                        hipStream_t st);
+                        const void* Wp, const float* sw, const void* bias, void* out, float* os, int M, int N, int K,
+                        int epi, hipStream_t st);
 void edge_w8a8_gemv_norm_cfg(int on);
 int edge_w8a8_gemv_norm_on();
 int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
@@ -702,11 +702,11 @@ std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
   return {q, s};
 }
 
-// Batch-1 W8A8 GEMV over RMSNorm(sum of split-K slices parts [S, 1, K] + residual), the norm and
-// its per-token int8 quantisation computed in the GEMV's prologue (gemm_i8.hip NormIn).
-// epi 0: (bf16 y [1, N], None, residual_out); epi 2 (16-blocked gate_up, quantising SwiGLU):
-// (int8 h [1, N/2], scales [N/128, 16]); the new residual row (sum + residual, bf16) is written
-// to res_out (K elements, not aliasing residual).  Returns None when no kernel takes it.
+// Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum of split-K slices parts [S, M, K] + residual),
+// the norm and its per-token int8 quantisation computed in the GEMV's prologue (gemm_i8.hip
+// NormIn).  epi 0: (bf16 y [M, N], None); epi 2 (16-blocked gate_up, quantising SwiGLU): (int8 h
+// [M, N/2], scales [N/128, 16]); the new residual rows (sum + residual, bf16) are written to
+// res_out ([M, K], not aliasing residual).  Returns None when no kernel takes it.
 std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_norm(
     const at::Tensor& parts, const at::Tensor& residual, const at::Tensor& gamma, double eps, const at::Tensor& res_out,
     const at::Tensor& wp, const at::Tensor& sw, const std::optional<at::Tensor>& bias, int64_t N, int64_t K,
@@ -716,25 +716,27 @@ std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_norm(
   need(residual, at::kBFloat16, "residual");
   need(gamma, at::kBFloat16, "gamma");
   check_w8a8_operands(wp, sw, bias, N, K);
-  TORCH_CHECK(parts.dim() == 3 && parts.size(1) == 1 && parts.size(2) == K, "parts must be [S, 1, K]");
-  TORCH_CHECK(residual.numel() == K && gamma.numel() == K, "residual / gamma must hold K elements");
+  TORCH_CHECK(parts.dim() == 3 && parts.size(2) == K, "parts must be [S, M, K]");
+  const int64_t M = parts.size(1);
+  TORCH_CHECK(residual.numel() == M * K && gamma.numel() == K, "residual [M, K] / gamma [K]");
   need(res_out, at::kBFloat16, "res_out");
-  TORCH_CHECK(res_out.numel() == K && res_out.data_ptr() != residual.data_ptr(), "res_out: K elements, not residual");
+  TORCH_CHECK(res_out.numel() == M * K && res_out.data_ptr() != residual.data_ptr(), "res_out: [M, K], not residual");
   TORCH_CHECK(epi == 0 || epi == 2, "epi 0 (out) or 2 (quantising GLU)");
   const int64_t S = parts.size(0);
-  if (!edge_w8a8_gemv_norm_on() || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % (epi == 2 ? 128 : 16) != 0)
+  if (!edge_w8a8_gemv_norm_on() || M < 1 || M > 4 || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % (epi == 2 ? 128 : 16) != 0)
     return std::nullopt;
   at::Tensor y;
   std::optional<at::Tensor> s;
   if (epi == 0) {
-    y = at::empty({1, N}, residual.options());
+    y = at::empty({M, N}, residual.options());
   } else {
-    y = at::empty({1, N / 2}, residual.options().dtype(at::kChar));
+    y = at::empty({M, N / 2}, residual.options().dtype(at::kChar));
     s = at::empty({N / 128, 16}, residual.options().dtype(at::kFloat));
   }
   check(edge_w8a8_gemv_norm(parts.data_ptr<float>(), (int)S, residual.data_ptr(), gamma.data_ptr(), (float)eps,
                             res_out.data_ptr(), wp.data_ptr(), sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr,
-                            y.data_ptr(), s ? s->data_ptr<float>() : nullptr, (int)N, (int)K, (int)epi, stream()),
+                            y.data_ptr(), s ? s->data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, (int)epi,
+                            stream()),
         "w8a8_gemv_norm");
   return std::make_tuple(y, s);
 }

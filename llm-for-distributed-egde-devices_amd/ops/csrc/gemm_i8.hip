@@ -320,123 +320,129 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
   }
 }
 
-// Batch-1 RMSNorm prologue (NRM > 0): the activation row is not an input but the RMSNorm of the
-// previous split-K projection's fp32 partial slices plus the residual row, quantised per token
-// (rowwise.hip norm_kernel<PART, HAS_RES, QUANT> moved into the consumer: one launch fewer per
-// norm, and the first weight step is in flight while the row is normalised).  Threads 0-255 run
-// the norm kernel's exact element layout and reduction order (NRM = its NCH chunks of 8 per
-// thread), so the int8 row and its scale are bit-identical; workgroup 0 writes the new residual.
+// Decode RMSNorm prologue (NRM > 0, M <= 4 rows): the activation rows are not an input but the
+// RMSNorm of the previous split-K projection's fp32 partial slices plus the residual, quantised
+// per token (rowwise.hip norm_kernel<PART, HAS_RES, QUANT> moved into the consumer: one launch
+// fewer per norm, and the first weight steps are in flight while the rows are normalised).  The
+// 1024 threads form four 256-thread groups, one row each; a group runs the norm kernel's
+// exact element layout and reduction order (NCH chunks of 8 per thread), so the int8 rows and
+// their scales are bit-identical.  Workgroup 0 writes the new residual rows.
 struct NormIn {
-  const float* part;      // [S][K] fp32 slices
-  const bf16_t* res;      // [K] residual in
+  const float* part;      // [S][M][K] fp32 slices
+  const bf16_t* res;      // [M][K] residual in
   const bf16_t* gamma;    // [K]
-  bf16_t* res_out;        // [K] residual out (must not alias res: other workgroups still read it)
+  bf16_t* res_out;        // [M][K] residual out (must not alias res: other workgroups still read it)
   float eps;
   int S;
 };
+constexpr int NRM_ROWS = 4;
 
 template <int NCH, int SMAX>
-__device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int8_t* aq, float* nsa, float* nred) {
-  const int t = threadIdx.x, w = t >> 6;
-  const bool act = t < 256;
-  float v[NCH][8];
-  float ss = 0.f, amax = 0.f;
-  if (act) {
-    uint4 rv[NCH];
-    float4 pv[NCH][SMAX][2];                                // S <= SMAX slices (register budget)
+__device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, int8_t* aq, float* nsa, float* nred) {
+  const int t = threadIdx.x & 255, g = threadIdx.x >> 8, w = t >> 6;
+  {                                                       // one pass: M <= NRM_ROWS = 4
+    const int row = g;
+    const bool act = row < M;
+    float v[NCH][8];
+    float ss = 0.f, amax = 0.f;
+    if (act) {
+      uint4 rv[NCH];
+      float4 pv[NCH][SMAX][2];                            // S <= SMAX slices (register budget)
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int e = min((c * 256 + t) * 8, H - 8);
-      rv[c] = *reinterpret_cast<const uint4*>(na.res + e);
+      for (int c = 0; c < NCH; ++c) {
+        const int e = min((c * 256 + t) * 8, H - 8);
+        rv[c] = *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e);
 #pragma unroll
-      for (int k = 0; k < SMAX; ++k)
-        if (k < na.S) {
-          const float4* p = reinterpret_cast<const float4*>(na.part + (size_t)k * H + e);
-          pv[c][k][0] = p[0];
-          pv[c][k][1] = p[1];
-        }
-    }
+        for (int k = 0; k < SMAX; ++k)
+          if (k < na.S) {
+            const float4* p = reinterpret_cast<const float4*>(na.part + ((size_t)k * M + row) * H + e);
+            pv[c][k][0] = p[0];
+            pv[c][k][1] = p[1];
+          }
+      }
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int e = (c * 256 + t) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
-#pragma unroll
-      for (int k = 0; k < SMAX; ++k)
-        if (k < na.S) {
-          const float4 p0 = pv[c][k][0], p1 = pv[c][k][1];
-          v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
-          v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
-        }
-      if (e < H) {
-        unpack8(pack8(v[c]), v[c]);                         // the projection's bf16 output
-        float r[8];
-        unpack8(rv[c], r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] += r[j];
-        const uint4 u = pack8(v[c]);                        // residual stream in bf16
-        if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + e) = u;
-        unpack8(u, v[c]);
-      } else {
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k)
+          if (k < na.S) {
+            const float4 p0 = pv[c][k][0], p1 = pv[c][k][1];
+            v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
+            v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
+          }
+        if (e < H) {
+          unpack8(pack8(v[c]), v[c]);                       // the projection's bf16 output
+          float r[8];
+          unpack8(rv[c], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+          const uint4 u = pack8(v[c]);                      // residual stream in bf16
+          if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + (size_t)row * H + e) = u;
+          unpack8(u, v[c]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (e < H) ? v[c][j] - 0.f : 0.f;
+          ss += d * d;
+        }
+      }
+      ss = wave_sum(ss);
+      if ((t & 63) == 0) nred[4 * g + w] = ss;
+    }
+    __syncthreads();
+    const float* gr = nred + 4 * g;
+    const float rstd = rsqrtf((((0.f + gr[0]) + gr[1]) + gr[2] + gr[3]) / (float)H + na.eps);
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
+        if (e < H) {
+          float wf[8];
+          unpack8(*reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - 0.f) * rstd * wf[j];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[c][j]));
+      amax = wave_max(amax);
+      if ((t & 63) == 0) nred[4 * g + w] = amax;
+    }
+    __syncthreads();
+    float gm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gm = fmaxf(gm, gr[i]);
+    gm = fmaxf(gm, 1e-8f);
+    const float inv = 127.f / gm;
+    if (act && t == 0) nsa[row] = gm / 127.f;
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
+        if (e < H) {
+          uint32_t lo = 0, hi = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[c][j], inv)) << (8 * j);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[c][4 + j], inv)) << (8 * j);
+          *reinterpret_cast<uint2*>(aq + (size_t)row * H + e) = make_uint2(lo, hi);
+        }
       }
     }
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int e = (c * 256 + t) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = (e < H) ? v[c][j] - 0.f : 0.f;
-        ss += d * d;
-      }
-    }
-    ss = wave_sum(ss);
-    if ((t & 63) == 0) nred[w] = ss;
+    __syncthreads();                                      // aq complete
   }
-  __syncthreads();
-  const float rstd = rsqrtf((((0.f + nred[0]) + nred[1]) + nred[2] + nred[3]) / (float)H + na.eps);
-  __syncthreads();
-  if (act) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int e = (c * 256 + t) * 8;
-      if (e < H) {
-        float wf[8];
-        unpack8(*reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - 0.f) * rstd * wf[j];
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[c][j]));
-    amax = wave_max(amax);
-    if ((t & 63) == 0) nred[w] = amax;
-  }
-  __syncthreads();
-  float gm = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) gm = fmaxf(gm, nred[i]);
-  gm = fmaxf(gm, 1e-8f);
-  const float inv = 127.f / gm;
-  if (t == 0) nsa[0] = gm / 127.f;
-  if (act) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int e = (c * 256 + t) * 8;
-      if (e < H) {
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[c][j], inv)) << (8 * j);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[c][4 + j], inv)) << (8 * j);
-        *reinterpret_cast<uint2*>(aq + e) = make_uint2(lo, hi);
-      }
-    }
-  }
-  __syncthreads();
 }
 
 template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI, int NRM = 0>
@@ -451,7 +457,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
   // NRM = 8 * NCH + SMAX (norm_prologue<NCH, SMAX>)
   constexpr int NCH_N = NRM / 8, SMAX_N = NRM % 8;
-  __shared__ int8_t aq_l[NRM > 0 ? NCH_N * 2048 : 16];
+  __shared__ int8_t aq_l[NRM > 0 ? NRM_ROWS * NCH_N * 2048 : 16];
   __shared__ float nsa[16], nred[16];
   constexpr bool GELUQ = EPI == EPI_GELUQT || EPI == EPI_GELUQE;
   static_assert(EPI == EPI_OUT || EPI == EPI_PART || (AMODE == A_TOKEN && (GELUQ || TPW % 2 == 0)),
@@ -486,7 +492,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   }
   const int8_t* ap[MB];
 #pragma unroll
-  for (int i = 0; i < MB; ++i) ap[i] = NRM > 0 ? aq_l : A + (size_t)min(i * 16 + (lane & 15), M - 1) * K;
+  for (int i = 0; i < MB; ++i)
+    ap[i] = (NRM > 0 ? aq_l : A) + (size_t)min(i * 16 + (lane & 15), M - 1) * K;
   const bool kfull = NRM > 0 || (K & 63) == 0;
   const auto pre = epi_preload<MB, NTW, NW, EPI>(sw, bias, nt0, NTt, wave, lane);
   v4i acc[TPW][MB];
@@ -531,7 +538,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto first = [&](Step& st, int kbase) {
     if constexpr (NRM > 0) {
       issue_w(st, kbase);
-      norm_prologue<NCH_N, SMAX_N>(na, K, aq_l, nsa, nred);
+      norm_prologue<NCH_N, SMAX_N>(na, K, M, aq_l, nsa, nred);
       issue_a(st, kbase);
     } else {
       issue(st, kbase);
@@ -563,7 +570,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
       // 4 slices keeps one step: its prologue registers would spill)
 #pragma unroll
       for (int i = 0; i < STEPS; ++i) issue_w(st[i], kbeg + kw + i * KW * U);
-      norm_prologue<NCH_N, SMAX_N>(na, K, aq_l, nsa, nred);
+      norm_prologue<NCH_N, SMAX_N>(na, K, M, aq_l, nsa, nred);
 #pragma unroll
       for (int i = 0; i < STEPS; ++i) {
         issue_a(st[i], kbeg + kw + i * KW * U);
@@ -1809,12 +1816,12 @@ int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, 
 }
 
 template <int NTW, int TG, int KW, int EP, int NRM>
-int launch_norm(const NormIn& na, const void* Wp, const float* sw, const void* bias, void* out, float* os, int N,
-                int K, hipStream_t st) {
+int launch_norm(const NormIn& na, const void* Wp, const float* sw, const void* bias, void* out, float* os, int M,
+                int N, int K, hipStream_t st) {
   const int NTt = (N + 15) / 16;
   hipLaunchKernelGGL((w8a8_gemv_kernel<1, NTW, TG, KW, 2, A_TOKEN, EP, NRM>), dim3((NTt + NTW - 1) / NTW),
                      dim3(TG * KW * 64), 0, st, (const int8_t*)nullptr, (const float*)nullptr, (const int8_t*)Wp, sw,
-                     (const bf16_t*)bias, out, os, 1, N, K, K / 64, NTt, 16, 1, na);
+                     (const bf16_t*)bias, out, os, M, N, K, K / 64, NTt, 16, 1, na);   // Mpad 16: scales [N/128][16]
   return (int)hipGetLastError();
 }
 
@@ -2153,9 +2160,10 @@ extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void*
 #undef SK
 }
 
-// Batch-1 GEMV whose activation row is RMSNorm(sum of S fp32 partial slices + residual), int8
-// per token, computed in the kernel's prologue (NormIn above).  epi 0 (EPI_OUT: bf16 [1, N]) or
-// 2 (EPI_GLUQ: 16-blocked gate_up -> SwiGLU -> int8 per 64 features, `os` scales [N/128][16]).
+// Decode GEMV (M <= 4 rows) whose activation rows are RMSNorm(sum of S fp32 partial slices +
+// residual), int8 per token, computed in the kernel's prologue (NormIn above).  epi 0 (EPI_OUT:
+// bf16 [M, N]) or 2 (EPI_GLUQ: 16-blocked gate_up -> SwiGLU -> int8 per 64 features, `os` scales
+// [N/128][16]).
 // K in {2048, 4096} (256 threads x NCH chunks of 8, NCH <= 2), 1 <= S <= 4; res_out written by
 // workgroup 0 and must not alias res.  -2: not taken.
 static int g_gemv_norm = 1;      // 0: the norm stays a kernel of its own (A/B knob "gemv_norm")
@@ -2163,18 +2171,18 @@ extern "C" void edge_w8a8_gemv_norm_cfg(int on) { g_gemv_norm = on; }
 extern "C" int edge_w8a8_gemv_norm_on() { return g_gemv_norm; }
 extern "C" int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* gamma, float eps,
                                    void* res_out, const void* Wp, const float* sw, const void* bias, void* out,
-                                   float* os, int N, int K, int epi, hipStream_t st) {
-  if (S < 1 || S > 4 || (K != 2048 && K != 4096) || N % 16 != 0 || res == nullptr || res_out == nullptr ||
+                                   float* os, int M, int N, int K, int epi, hipStream_t st) {
+  if (M < 1 || M > NRM_ROWS || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % 16 != 0 || res == nullptr || res_out == nullptr ||
       res == res_out)
     return -2;
   const NormIn na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};
   // template NRM = 8 * (K / 2048) + (S <= 2 ? 2 : 4): two-slice sums keep 32 VGPRs free, which
   // lets the qkv form hold both of its weight steps across the prologue without spilling
 #define NRM_L(NTW, TG, KW, EP, OS)                                                                       \
-  return K == 4096 ? (S <= 2 ? launch_norm<NTW, TG, KW, EP, 18>(na, Wp, sw, bias, out, OS, N, K, st)     \
-                             : launch_norm<NTW, TG, KW, EP, 20>(na, Wp, sw, bias, out, OS, N, K, st))    \
-                   : (S <= 2 ? launch_norm<NTW, TG, KW, EP, 10>(na, Wp, sw, bias, out, OS, N, K, st)     \
-                             : launch_norm<NTW, TG, KW, EP, 12>(na, Wp, sw, bias, out, OS, N, K, st))
+  return K == 4096 ? (S <= 2 ? launch_norm<NTW, TG, KW, EP, 18>(na, Wp, sw, bias, out, OS, M, N, K, st)     \
+                             : launch_norm<NTW, TG, KW, EP, 20>(na, Wp, sw, bias, out, OS, M, N, K, st))    \
+                   : (S <= 2 ? launch_norm<NTW, TG, KW, EP, 10>(na, Wp, sw, bias, out, OS, M, N, K, st)     \
+                             : launch_norm<NTW, TG, KW, EP, 12>(na, Wp, sw, bias, out, OS, M, N, K, st))
   if (epi == EPI_OUT) NRM_L(3, 1, 16, EPI_OUT, nullptr);
   if (epi == EPI_GLUQ) {
     if (N % 128 != 0 || os == nullptr) return -2;

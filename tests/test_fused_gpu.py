@@ -663,14 +663,15 @@ def test_gemv_addend_matches_unfused_add(cuda, M):
     assert torch.equal(C.gemv_bf16(xb, wpb, bias, N, 0, add), yb + add)
 
 
+@pytest.mark.parametrize("M", [1, 3, 4])
 @pytest.mark.parametrize("K,S", [(4096, 2), (4096, 1), (4096, 4), (2048, 4), (2048, 3)])
-def test_gemv_norm_prologue_bit_exact(cuda, K, S):
-    """Batch-1 RMSNorm in the consuming W8A8 GEMV's prologue (ops.w8a8_gemv_norm) == the norm kernel
-    over the split-K slices (ops.rms_norm_parts) followed by the plain GEMV / quantising SwiGLU
-    GEMV, bit for bit, and the new residual row it writes == the norm kernel's."""
-    torch.manual_seed(K + S)
-    parts = torch.randn(S, 1, K, device=cuda) * 0.5
-    res = torch.randn(1, K, device=cuda).bfloat16()
+def test_gemv_norm_prologue_bit_exact(cuda, K, S, M):
+    """Decode RMSNorm (1-4 rows) in the consuming W8A8 GEMV's prologue (ops.w8a8_gemv_norm) == the
+    norm kernel over the split-K slices (ops.rms_norm_parts) followed by the plain GEMV / quantising
+    SwiGLU GEMV, bit for bit, and the new residual rows it writes == the norm kernel's."""
+    torch.manual_seed(K + S + M)
+    parts = torch.randn(S, M, K, device=cuda) * 0.5
+    res = torch.randn(M, K, device=cuda).bfloat16()
     gamma = (torch.rand(K, device=cuda) + 0.5).bfloat16()
     eps = 1e-5
     q, s, r = ops.rms_norm_parts(parts, res, gamma, eps, True)
@@ -679,7 +680,7 @@ def test_gemv_norm_prologue_bit_exact(cuda, K, S):
         wp = ops.pack_int8_weight(w)
         sw = torch.rand(N, device=cuda) * 0.004 + 1e-4
         bias = torch.randn(N, device=cuda).bfloat16()
-        h = torch.full((1, K), float("nan"), device=cuda).bfloat16()
+        h = torch.full((M, K), float("nan"), device=cuda).bfloat16()
         fused = ops.w8a8_gemv_norm(parts, res, gamma, eps, h, wp, sw, bias, N, K, glu_quant=glu)
         assert fused is not None
         assert torch.equal(h, r)
@@ -699,11 +700,13 @@ def test_gemv_norm_declines_unsupported(cuda):
     g = torch.ones(K, device=cuda).bfloat16()
     h = torch.empty(1, K, device=cuda).bfloat16()
     assert not ops.gemv_norm_ok(torch.zeros(5, 1, K, device=cuda))
+    assert not ops.gemv_norm_ok(torch.zeros(2, 5, K, device=cuda))
     assert ops.w8a8_gemv_norm(torch.zeros(5, 1, K, device=cuda), res, g, 1e-5, h, wp, sw, None, N, K) is None
 
 
-def test_llama_batch1_decode_defers_norms(cuda):
-    """A W8A8 Llama decoder (hidden 2048) at batch 1 runs its inner RMSNorms in the qkv / gate_up
+@pytest.mark.parametrize("B", [1, 4])
+def test_llama_batch1_decode_defers_norms(cuda, B):
+    """A W8A8 Llama decoder (hidden 2048) at 1-4 rows runs its inner RMSNorms in the qkv / gate_up
     GEMV prologues and produces the same logits as with the norm kernels (knob gemv_norm=0)."""
     from edgellm.engine import KVCache
     from edgellm.models import AttnCtx, build_model, tiny
@@ -711,7 +714,7 @@ def test_llama_batch1_decode_defers_norms(cuda):
     from edgellm.quant import quantize_model
     cfg = tiny("llama", hidden_size=2048, num_heads=16, num_kv_heads=4, intermediate_size=4096, num_layers=3)
     qm = quantize_model(build_model(cfg, device=cuda, seed=5), "w8a8")
-    B, T = 1, 9
+    T = 9
     ids = torch.randint(0, cfg.vocab_size, (B, T), generator=torch.Generator().manual_seed(1)).to(cuda)
     seen = []
     orig = qm.layers[1].attn.qkv.forward
