@@ -77,10 +77,16 @@ def rms_norm_parts(parts, residual, weight, eps, quant: bool):
     return ext().rms_norm_parts(parts, residual, weight, eps, quant)
 
 
+# rows up to which decode norms move into the next GEMV's prologue (kernel: <= 4).  Measured on
+# Llama-2-7B W8A8: batch 1 p50 2.10 -> 1.96 ms; 4 rows 2.167 -> 2.179 ms (slower), so 1 by default
+NORM_FUSE_MAX_ROWS = int(os.environ.get("EDGELLM_NORM_FUSE_ROWS", "1"))
+
+
 def gemv_norm_ok(parts) -> bool:
     """Whether a decode W8A8 GEMV can take the RMSNorm of these split-K slices [S, M, K] in its
     prologue (gemm_i8.hip NormIn: M <= 4, K 2048 / 4096, S <= 4; tune knob ``gemv_norm``)."""
-    return parts.is_cuda and parts.dim() == 3 and 1 <= parts.shape[1] <= 4 and 1 <= parts.shape[0] <= 4 \
+    return parts.is_cuda and parts.dim() == 3 and 1 <= parts.shape[1] <= min(4, NORM_FUSE_MAX_ROWS) \
+        and 1 <= parts.shape[0] <= 4 \
         and parts.shape[2] in (2048, 4096) and available() and bool(ext().gemv_norm_on())
 
 

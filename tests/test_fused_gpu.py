@@ -701,11 +701,13 @@ def test_gemv_norm_declines_unsupported(cuda):
     h = torch.empty(1, K, device=cuda).bfloat16()
     assert not ops.gemv_norm_ok(torch.zeros(5, 1, K, device=cuda))
     assert not ops.gemv_norm_ok(torch.zeros(2, 5, K, device=cuda))
+    assert ops.gemv_norm_ok(torch.zeros(2, 1, K, device=cuda))
+    assert ops.gemv_norm_ok(torch.zeros(2, 4, K, device=cuda)) == (ops.NORM_FUSE_MAX_ROWS >= 4)
     assert ops.w8a8_gemv_norm(torch.zeros(5, 1, K, device=cuda), res, g, 1e-5, h, wp, sw, None, N, K) is None
 
 
 @pytest.mark.parametrize("B", [1, 4])
-def test_llama_batch1_decode_defers_norms(cuda, B):
+def test_llama_batch1_decode_defers_norms(cuda, B, monkeypatch):
     """A W8A8 Llama decoder (hidden 2048) at 1-4 rows runs its inner RMSNorms in the qkv / gate_up
     GEMV prologues and produces the same logits as with the norm kernels (knob gemv_norm=0)."""
     from edgellm.engine import KVCache
@@ -724,6 +726,7 @@ def test_llama_batch1_decode_defers_norms(cuda, B):
         return orig(x, add)
 
     qm.layers[1].attn.qkv.forward = spy
+    monkeypatch.setattr(ops, "NORM_FUSE_MAX_ROWS", 4)      # the default fuses at batch 1 only
     C = ops.ext()
     outs = []
     try:
