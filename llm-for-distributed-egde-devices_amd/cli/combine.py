@@ -58,8 +58,10 @@ def make_agent(name: str, model_id: str, precision: str, quant: str, device, sam
     (``launch``) this rank's pipeline stage behind a PipelineGenerator (parallel/pp_engine.py)."""
     if launch is not None:
         eng, tok, source, bounds = build_pp_engine(model_id, precision, quant, rt, launch, tag,
-                                                   max_batch=int(rt.get("batch_size") or 1))
-        logger.info(f"{name}: {source} pipelined over {launch[1]} ranks at layers {bounds} ({quant})")
+                                                   max_batch=int(rt.get("batch_size") or 1), gpus=gpus)
+        if eng.member:
+            logger.info(f"{name}: {source} pipelined over {len(eng.ranks)} ranks {eng.ranks} at layers {bounds} "
+                        f"({quant})")
         return Agent(name, eng, tok, sampling, cpu_prompt)
     devs = agent_devices(gpus, torch.device(device), int(rt.get("pp_size") or 1))
     model, tok, source = load_model(model_id, precision, quant, devs[0], rt.get("base_model_path"))
@@ -92,7 +94,7 @@ def run_ensemble(cfg: RunConfig, rt: dict, qa_specs, refiner_spec, cpu_variant: 
                                  launch=launch, tag=i))
     merge_kind = rt.get("merge") or cfg.merge
     refiner = None
-    if merge_kind == "refine" or refiner_spec is not None:
+    if merge_kind == "refine" and refiner_spec is not None:      # (vote: no refiner model is loaded)
         rn, rid, rprec = refiner_spec
         refiner = make_agent(rn, rid, rprec, quant, devices[len(agents) % len(devices)], sampling, rt,
                              launch=launch, tag=len(agents))

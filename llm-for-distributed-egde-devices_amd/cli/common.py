@@ -113,15 +113,37 @@ def pp_launch(rt: dict):
     return rank, world, dev
 
 
-def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch, tag: int, max_batch: int = 1):
+def agent_group(ranks, world: int):
+    """Process group of an agent's ranks: the default group when it spans the world, else a new
+    group.  Every rank must call this for every agent in the same order (dist.new_group)."""
+    import torch.distributed as dist
+    if list(ranks) == list(range(world)):
+        return None
+    return dist.new_group(list(ranks))
+
+
+def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch, tag: int, max_batch: int = 1,
+                    gpus=None):
     """This rank's stage of ``model_id`` behind a ``PipelineGenerator`` (the Generator interface
-    on the driver, rank 0).  Returns (engine, tokenizer, source, bounds)."""
-    from ..parallel.pp_engine import PipelineGenerator, load_stage
+    on the driver, rank 0).  ``gpus`` (YAML ``agents[].gpus``): the agent's rank group — one
+    process per GPU, so GPU index = rank; default all ranks.  A rank outside the group holds a
+    stub engine.  Returns (engine, tokenizer, source, bounds)."""
+    from ..parallel.pp_engine import PipelineGenerator, _cfg_of, load_stage
     rank, world, dev = launch
-    stage, tok, source, bounds = load_stage(model_id, precision, quant, dev, rt.get("base_model_path"), rank, world)
+    ranks = sorted(int(g) for g in gpus) if gpus else list(range(world))
+    assert ranks and all(0 <= r < world for r in ranks) and len(set(ranks)) == len(ranks), \
+        f"agent gpus {gpus} must be distinct ranks of the {world}-rank launch"
+    group = agent_group(ranks, world)
     kvd = rt.get("kv_dtype") or "bf16"
+    common = dict(max_batch=max_batch, max_seq=rt.get("max_seq", 2048), tag=tag, group=group, ranks=ranks)
+    if rank not in ranks:
+        cfg, tok, source = _cfg_of(model_id, precision, torch.device("cpu"), rt.get("base_model_path"))
+        eng = PipelineGenerator(None, -1, len(ranks), cfg=cfg, device=dev, **common)
+        return eng, tok, source, None
+    s_idx = ranks.index(rank)
+    stage, tok, source, bounds = load_stage(model_id, precision, quant, dev, rt.get("base_model_path"), s_idx,
+                                            len(ranks))
     if kvd == "int8" and stage.cfg.head_dim not in (64, 128, 256):
         kvd = "bf16"
-    eng = PipelineGenerator(stage, rank, world, max_batch=max_batch, max_seq=rt.get("max_seq", 2048), tag=tag,
-                            kv_dtype=kvd)
+    eng = PipelineGenerator(stage, s_idx, len(ranks), kv_dtype=kvd, **common)
     return eng, tok, source, bounds

@@ -45,11 +45,13 @@ class _Slot:
 
 
 class SlotDecoder:
-    def __init__(self, gen: Generator, sampling: SamplingParams, seed: int = 0, width: int = 2048):
+    def __init__(self, gen: Generator, sampling: SamplingParams, seed: int = 0, width: int = 2048,
+                 max_batch: Optional[int] = None):
         assert gen.attn_hook is None, "continuous batching needs per-row cache lengths (no HeadInfer offload)"
         self.gen, self.sp = gen, sampling
         self.model, self.cfg, self.device = gen.model, gen.cfg, gen.device
-        self.B = gen.kv.max_batch
+        # slots = the operator's batch cap (ServingEngine max_batch), at most the cache rows
+        self.B = min(int(max_batch), gen.kv.max_batch) if max_batch else gen.kv.max_batch
         self.V = self.cfg.vocab_size
         self.width = width
         self.st = _DecodeState(self.B, self.V, width, self.device)
@@ -152,8 +154,11 @@ class SlotDecoder:
             self.steps += 1
             done += 1
             for r, s in enumerate(self.slots):
-                if s is not None:
+                # a slot already at its budget rode along in the batched step (its row advanced on
+                # device) but produced no token of its request: it is released by the next poll
+                if s is not None and s.produced < s.max_new:
                     s.produced += 1
+                if s is not None:
                     self.host_len[r] += 1
             if any(s is not None and s.produced >= s.max_new for s in self.slots):
                 break
@@ -172,7 +177,7 @@ class SlotDecoder:
         out = []
         for r, row in zip(occ, rows):
             s = self.slots[r]
-            toks = row[s.col0 - c0:s.col0 - c0 + s.produced]
+            toks = row[s.col0 - c0:s.col0 - c0 + min(s.produced, s.max_new)]
             hit = s.eos is not None and s.eos in toks
             if hit:
                 toks = toks[:toks.index(s.eos) + 1]

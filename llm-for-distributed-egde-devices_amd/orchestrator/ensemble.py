@@ -96,9 +96,18 @@ def run_agents(agents: Sequence[Agent], prompts: Sequence[Sequence[str]], seeds:
     errors: List[BaseException] = []
     units: List[List[int]] = []
     shared: Dict[object, List[int]] = {}
+    # pipeline agents (one process per GPU under torchrun, parallel/pp_engine.py): one concurrent
+    # command for all of them — agents on disjoint rank groups decode at the same time, the rest in
+    # order.  Dispatch is on the engine's capability, never on its device type: co_generate drives
+    # a plain Generator's internals (start / step / precapture), which a pipeline engine lacks.
+    pipe = [i for i, a in enumerate(agents) if _is_pipeline(a.generator)]
+    if pipe:
+        _run_pipeline_agents(agents, pipe, prompts, seeds, legacy_decode, concurrent, out)
     for i, a in enumerate(agents):
+        if i in pipe:
+            continue
         dev = getattr(a, "device", None)
-        if concurrent and isinstance(dev, torch.device) and dev.type == "cuda":
+        if concurrent and _is_local_generator(a.generator) and isinstance(dev, torch.device) and dev.type == "cuda":
             if dev not in shared:
                 shared[dev] = []
                 units.append(shared[dev])
@@ -130,7 +139,7 @@ def run_agents(agents: Sequence[Agent], prompts: Sequence[Sequence[str]], seeds:
         except BaseException as e:  # surfaced after join
             errors.append(e)
 
-    devices = {getattr(a, "device", None) for a in agents}
+    devices = {getattr(agents[u[0]], "device", None) for u in units}
     if concurrent and len(units) > 1 and len(devices) > 1:
         threads = [threading.Thread(target=work, args=(idx,)) for idx in units]
         for t in threads:
@@ -143,6 +152,27 @@ def run_agents(agents: Sequence[Agent], prompts: Sequence[Sequence[str]], seeds:
     if errors:
         raise errors[0]
     return out
+
+
+def _is_pipeline(gen) -> bool:
+    """A multi-process pipeline engine (parallel.pp_engine.PipelineGenerator)."""
+    from ..parallel.pp_engine import PipelineGenerator
+    return isinstance(gen, PipelineGenerator)
+
+
+def _is_local_generator(gen) -> bool:
+    """An in-process engine that co_generate can drive side by side with others on one GPU."""
+    return isinstance(gen, Generator) and all(hasattr(gen, a) for a in ("start", "step", "precapture", "collect"))
+
+
+def _run_pipeline_agents(agents, idx, prompts, seeds, legacy_decode, concurrent, out):
+    from ..parallel.pp_engine import generate_concurrent
+    encs = [agents[i].encode_batch(prompts[i]) for i in idx]
+    jobs = [(agents[i].generator, ids, agents[i].sampling, seeds[i], getattr(agents[i].tokenizer, "eos_token_id", None))
+            for i, ids in zip(idx, encs)]
+    results = generate_concurrent(jobs) if concurrent else [r for j in jobs for r in generate_concurrent([j])]
+    for i, ids, res in zip(idx, encs, results):
+        out[i] = (agents[i].decode_batch(ids, res, legacy_decode), res)
 
 
 @dataclass

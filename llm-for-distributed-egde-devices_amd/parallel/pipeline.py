@@ -55,12 +55,17 @@ class PipelineResult:
 class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
                  group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None,
-                 lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True, kv_dtype: str = "bf16"):
+                 lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True, kv_dtype: str = "bf16",
+                 ranks: Optional[Sequence[int]] = None):
         """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
         to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
         HeadInfer").  The offloaded path is host-orchestrated on one compute stream, so it runs one
         lane and its decode steps run eagerly; its cache is built at ``run`` with prefill chunks
-        of min(prompt_len, ``prefill_chunk``) tokens and staging buffers of one micro-batch."""
+        of min(prompt_len, ``prefill_chunk``) tokens and staging buffers of one micro-batch.
+
+        ``rank`` / ``world`` are the stage index and stage count within ``group``; ``ranks`` maps
+        stage index -> global rank (default identity: the stages are ranks 0..world-1), so a model
+        can be pipelined over any rank subset (one ``dist.new_group`` per ensemble agent)."""
         assert lanes >= 1 and n_micro % lanes == 0, "micro-batches must split evenly over lanes"
         assert n_micro >= world * lanes, "need lanes x stages micro-batches to keep the ring full"
         offload = headinfer_heads is not None and headinfer_heads < model.cfg.num_kv_heads
@@ -76,6 +81,8 @@ class PipelineStage:
         assert self.is_first == (rank == 0) and self.is_last == (rank == world - 1)
         self.prev = (rank - 1) % world
         self.next = (rank + 1) % world
+        self.granks = list(ranks) if ranks is not None else list(range(world))
+        assert len(self.granks) == world, "one global rank per stage"
         self.h_on = headinfer_heads if offload else None
         self.prefill_chunk = max(1, prefill_chunk)
         self.kv_dtype = kv_dtype
@@ -122,14 +129,15 @@ class PipelineStage:
         if not sends and not recvs:
             return
         self.p2p_bytes += sum(t.numel() * t.element_size() for t, _ in sends)
+        g = self.granks
         if self.host_staged:
             bufs = [torch.empty(t.shape, dtype=t.dtype) for t, _ in recvs]
-            p2p = [dist.P2POp(dist.isend, t.cpu(), p, self.group) for t, p in sends]
-            p2p += [dist.P2POp(dist.irecv, h, p, self.group) for h, (_, p) in zip(bufs, recvs)]
+            p2p = [dist.P2POp(dist.isend, t.cpu(), g[p], self.group) for t, p in sends]
+            p2p += [dist.P2POp(dist.irecv, h, g[p], self.group) for h, (_, p) in zip(bufs, recvs)]
         else:
             bufs = None
-            p2p = [dist.P2POp(dist.isend, t, p, self.group) for t, p in sends]
-            p2p += [dist.P2POp(dist.irecv, t, p, self.group) for t, p in recvs]
+            p2p = [dist.P2POp(dist.isend, t, g[p], self.group) for t, p in sends]
+            p2p += [dist.P2POp(dist.irecv, t, g[p], self.group) for t, p in recvs]
         with trace_range("pp.exchange"):
             # RCCL: wait() makes the current stream wait on the communication (no host block)
             for w in dist.batch_isend_irecv(p2p):
@@ -140,11 +148,11 @@ class PipelineStage:
         debug_sync("pp.exchange")
 
     def _send_one(self, t: torch.Tensor, peer: int):
-        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, peer, self.group)]):
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, self.granks[peer], self.group)]):
             w.wait()
 
     def _recv_one(self, t: torch.Tensor, peer: int):
-        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, peer, self.group)]):
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, self.granks[peer], self.group)]):
             w.wait()
 
     # ------------------------------------------------------------------ compute

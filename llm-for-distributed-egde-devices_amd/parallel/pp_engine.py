@@ -98,79 +98,75 @@ class _Scorer:
 
 
 class PipelineGenerator:
-    """Generator-compatible front end of one model's pipeline stage on this rank."""
+    """Generator-compatible front end of one model's pipeline stage on this rank.
 
-    def __init__(self, stage_model: DecoderLM, rank: int, world: int, max_batch: int = 1, max_seq: int = 2048,
-                 tag: int = 0, lanes: int = 1, n_micro: Optional[int] = None, kv_dtype: str = "bf16",
-                 eos_every: int = 8, group=None, use_graphs: Optional[bool] = None):
+    ``rank`` / ``world``: this rank's stage index and the stage count of the model's rank group;
+    ``ranks``: the group's global ranks (default 0..world-1) and ``group`` its process group.  A
+    rank outside the group holds a STUB (``stage_model=None``, ``cfg`` and ``device`` given): it
+    joins the command broadcasts and skips the work, so every rank can hold one engine per agent
+    and agents on disjoint rank groups decode at the same time (``generate_concurrent``).
+    Commands always travel over the WORLD group from global rank 0 (the driver); results come back
+    from the group's last stage to rank 0."""
+
+    def __init__(self, stage_model: Optional[DecoderLM], rank: int, world: int, max_batch: int = 1,
+                 max_seq: int = 2048, tag: int = 0, lanes: int = 1, n_micro: Optional[int] = None,
+                 kv_dtype: str = "bf16", eos_every: int = 8, group=None, use_graphs: Optional[bool] = None,
+                 ranks: Optional[Sequence[int]] = None, cfg=None, device=None):
         self.rank, self.world, self.tag, self.group = rank, world, tag, group
+        self.ranks = list(ranks) if ranks is not None else list(range(world))
+        assert len(self.ranks) == world
+        self.grank = dist.get_rank() if dist.is_initialized() else 0
+        self.member = stage_model is not None
         M = max(n_micro or 0, world * lanes)
         b = max(1, math.ceil(max_batch / M))
-        self.stage = PipelineStage(stage_model, rank, world, b, M, min(max_seq, stage_model.cfg.max_position_embeddings),
-                                   group=group, lanes=lanes, kv_dtype=kv_dtype, use_graphs=use_graphs)
-        self.cfg, self.eos_every = stage_model.cfg, eos_every
-        self.max_seq = min(max_seq, stage_model.cfg.max_position_embeddings)   # as Generator
-        self.device = stage_model.device
-        self.nccl = self.stage.nccl
+        self.M, self.b = M, b
+        self.cfg = stage_model.cfg if self.member else cfg
+        assert self.cfg is not None, "a stub engine needs the model config"
+        self.max_seq = min(max_seq, self.cfg.max_position_embeddings)   # as Generator
+        if self.member:
+            self.stage = PipelineStage(stage_model, rank, world, b, M, self.max_seq, group=group, lanes=lanes,
+                                       kv_dtype=kv_dtype, use_graphs=use_graphs, ranks=self.ranks)
+            self.device = stage_model.device
+            self.nccl = self.stage.nccl
+        else:
+            self.stage = None
+            self.device = torch.device(device) if device is not None else torch.device("cpu")
+            self.nccl = dist.is_initialized() and dist.get_backend() == "nccl"
+        self.eos_every = eos_every
         self.cdev = self.device if self.nccl else torch.device("cpu")
         self.model = _Scorer(self)          # Agent / MetricSuite read generator.model
         self.last_rank = world - 1
+        self.last_ticks = 0
 
     # ------------------------------------------------------------------ comm helpers
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
-            dist.broadcast(t, 0, group=self.group)
+        """Driver -> every rank of the WORLD (command traffic)."""
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.broadcast(t, 0)
         return t
 
-    def _to_driver(self, t: torch.Tensor) -> torch.Tensor:
-        """Last rank -> rank 0 (in place on rank 0's buffer)."""
-        if self.world == 1:
-            return t
-        if self.rank == self.last_rank:
-            dist.send(t, 0, group=self.group)
-        elif self.rank == 0:
-            dist.recv(t, self.last_rank, group=self.group)
-        return t
+    def _deliver(self, ts: Sequence[torch.Tensor]) -> None:
+        """The group's last stage -> global rank 0 (world P2P), in place on rank 0's buffers."""
+        src = self.ranks[-1]
+        if src == 0:
+            return
+        for t in ts:
+            if self.grank == src:
+                dist.send(t, 0)
+            elif self.grank == 0:
+                dist.recv(t, src)
 
     # ------------------------------------------------------------------ driver API
     @torch.no_grad()
     def generate(self, prompts: Sequence[Sequence[int]], sampling: SamplingParams, seed: int = 0,
                  eos_token_id: Optional[int] = None, stop_at_eos: bool = True,
                  record_step_latency: bool = False) -> GenerationResult:
-        assert self.rank == 0, "the driver (rank 0) issues commands; workers run serve_workers()"
-        st = self.stage
-        n = len(prompts)
-        assert 0 < n <= st.M * st.b, f"{n} prompts > {st.M} micro-batches x {st.b} rows"
-        plens = [len(p) for p in prompts]
-        T = max(plens)
-        assert T + sampling.max_new_tokens <= self.max_seq, "prompt + max_new_tokens exceeds max_seq"
-        rows = list(prompts) + [prompts[0]] * (st.M * st.b - n)
-        ids = torch.zeros(len(rows), T, dtype=torch.long, device=self.cdev)
-        for i, p in enumerate(rows):
-            ids[i, :len(p)] = torch.tensor(p, dtype=torch.long)
-        lens = torch.tensor([len(p) for p in rows], dtype=torch.long, device=self.cdev)
-        hdr = torch.tensor([CMD_GENERATE, self.tag, n, T, sampling.max_new_tokens, seed,
-                            -1 if eos_token_id is None or not stop_at_eos else int(eos_token_id),
-                            int(sampling.do_sample), int(sampling.top_k or 0), 0, 0, 0],
-                           dtype=torch.long, device=self.cdev)
-        fl = torch.tensor([sampling.temperature, sampling.top_p if sampling.top_p is not None else 1.0,
-                           sampling.repetition_penalty, 0.0], dtype=torch.float64, device=self.cdev)
-        self._bcast(hdr)
-        self._bcast(fl)
-        self._bcast(ids)
-        self._bcast(lens)
-        toks, elapsed, ttft = self._run_generate(hdr, fl, ids, lens)
-        out = []
-        for r in toks[:n]:
-            if eos_token_id is not None and stop_at_eos and eos_token_id in r:
-                r = r[:r.index(eos_token_id) + 1]
-            out.append(r)
-        return GenerationResult(out, plens, elapsed, ttft, max(0.0, elapsed - ttft))
+        return generate_concurrent([(self, prompts, sampling, seed, eos_token_id)], stop_at_eos)[0]
 
     @torch.no_grad()
     def confidence(self, ids: List[int]) -> float:
         """mean over positions of max softmax(logits): one pipelined prefill of ``ids`` (K13)."""
-        assert self.rank == 0
+        assert self.grank == 0, "the driver (rank 0) issues commands"
         if not ids:
             return 0.0
         hdr = torch.zeros(_HDR, dtype=torch.long, device=self.cdev)
@@ -180,71 +176,140 @@ class PipelineGenerator:
         return self._run_score(t)
 
     # ------------------------------------------------------------------ every rank
-    def _run_generate(self, hdr, fl, ids, lens):
+    def _job_tensors(self, prompts, sampling: SamplingParams, seed: int, eos_token_id, stop_at_eos: bool):
+        """Driver: the broadcast form of one generate job (header, floats, padded ids, lengths)."""
+        n = len(prompts)
+        assert 0 < n <= self.M * self.b, f"{n} prompts > {self.M} micro-batches x {self.b} rows"
+        T = max(len(p) for p in prompts)
+        assert min(len(p) for p in prompts) >= 1, "empty prompt"
+        assert T + sampling.max_new_tokens <= self.max_seq, "prompt + max_new_tokens exceeds max_seq"
+        rows = list(prompts) + [prompts[0]] * (self.M * self.b - n)
+        ids = torch.zeros(len(rows), T, dtype=torch.long, device=self.cdev)
+        for i, p in enumerate(rows):
+            ids[i, :len(p)] = torch.tensor(p, dtype=torch.long)
+        lens = torch.tensor([len(p) for p in rows], dtype=torch.long, device=self.cdev)
+        hdr = torch.tensor([self.tag, n, T, sampling.max_new_tokens, seed,
+                            -1 if eos_token_id is None or not stop_at_eos else int(eos_token_id),
+                            int(sampling.do_sample), int(sampling.top_k or 0), 0, 0, 0, 0],
+                           dtype=torch.long, device=self.cdev)
+        fl = torch.tensor([sampling.temperature, sampling.top_p if sampling.top_p is not None else 1.0,
+                           sampling.repetition_penalty, 0.0], dtype=torch.float64, device=self.cdev)
+        return hdr, fl, ids, lens
+
+    def _run_local(self, hdr, fl, ids, lens):
+        """Member ranks: run the pipeline for one job; the last stage returns (tokens, timing)
+        buffers, the other ranks zeros of the same shape (filled on rank 0 by ``_deliver``)."""
+        n, T, max_new, seed, eos = (int(hdr[i]) for i in (1, 2, 3, 4, 5))
+        out = torch.zeros(self.M * self.b, max_new, dtype=torch.long, device=self.cdev)
+        timing = torch.zeros(3, dtype=torch.float64, device=self.cdev)
+        if not self.member:
+            return out, timing
         st = self.stage
-        n, T, max_new, seed, eos = (int(hdr[i]) for i in (2, 3, 4, 5, 6))
-        sp = SamplingParams(max_new_tokens=max_new, temperature=float(fl[0]), top_k=int(hdr[8]),
-                            top_p=float(fl[1]), repetition_penalty=float(fl[2]), do_sample=bool(int(hdr[7])))
+        sp = SamplingParams(max_new_tokens=max_new, temperature=float(fl[0]), top_k=int(hdr[7]),
+                            top_p=float(fl[1]), repetition_penalty=float(fl[2]), do_sample=bool(int(hdr[6])))
         M, b = st.M, st.b
-        dev = self.device
-        ids_d = ids.to(dev)
+        ids_d = ids.to(self.device)
         prompts = [ids_d[m * b:(m + 1) * b] for m in range(M)]
         res = st.run(prompts, T, sp, max_new - 1, seed=seed, prompt_lens=lens.view(M, b),
                      eos_token_id=None if eos < 0 else eos, eos_every=self.eos_every)
-        out = torch.zeros(M * b, max_new, dtype=torch.long, device=self.cdev)
-        timing = torch.zeros(3, dtype=torch.float64, device=self.cdev)
-        if self.rank == self.last_rank:
+        if st.is_last:
             out.copy_(torch.tensor(res.tokens, dtype=torch.long))
             timing[0] = res.elapsed_s
             timing[1] = res.stats.get("ttft_ms", 0.0) / 1e3
             timing[2] = res.ticks
-        self._to_driver(out)
-        self._to_driver(timing)
-        self.last_ticks = int(timing[2])                # ticks run (fewer when EOS ended the run)
-        return out.tolist(), float(timing[0]), float(timing[1])
+        return out, timing
 
     def _run_score(self, ids: torch.Tensor) -> float:
-        """One prefill of [1, T] through the stages (micro-batch 0's cache row 0)."""
-        st, dev = self.stage, self.device
-        T = ids.numel()
-        assert T <= self.max_seq
-        H = self.cfg.hidden_size
-        sp = torch.zeros(1, dtype=torch.int32, device=dev)
-        ctx = AttnCtx("prefill", 1, T, sp, sp + T, T, st.kv.rows(0, 1), st.rope)
-        hidden = None
-        if not st.is_first:
-            hidden = torch.empty(T, H, dtype=st.model.dtype, device=dev if self.nccl else "cpu")
-            dist.recv(hidden, st.prev, group=self.group)
-            hidden = hidden.to(dev)
-        out = st.model(ids.to(dev).view(1, T) if st.is_first else None, ctx, hidden=hidden, logits="all")
+        """One prefill of [1, T] through the stages (micro-batch 0's cache row 0); the value
+        reaches rank 0 from the last stage."""
         val = torch.zeros(1, dtype=torch.float64, device=self.cdev)
-        if st.is_last:
-            val[0] = float(ops.max_softmax_prob(out).mean())
-        else:
-            dist.send(out.contiguous() if self.nccl else out.contiguous().cpu(), st.next, group=self.group)
-        self._to_driver(val)
+        if self.member:
+            st, dev = self.stage, self.device
+            T = ids.numel()
+            assert T <= self.max_seq
+            H = self.cfg.hidden_size
+            sp = torch.zeros(1, dtype=torch.int32, device=dev)
+            ctx = AttnCtx("prefill", 1, T, sp, sp + T, T, st.kv.rows(0, 1), st.rope)
+            hidden = None
+            if not st.is_first:
+                hidden = torch.empty(T, H, dtype=st.model.dtype, device=dev if self.nccl else "cpu")
+                dist.recv(hidden, st.granks[st.prev], group=self.group)
+                hidden = hidden.to(dev)
+            out = st.model(ids.to(dev).view(1, T) if st.is_first else None, ctx, hidden=hidden, logits="all")
+            if st.is_last:
+                val[0] = float(ops.max_softmax_prob(out).mean())
+            else:
+                dist.send(out.contiguous() if self.nccl else out.contiguous().cpu(), st.granks[st.next],
+                          group=self.group)
+        self._deliver([val])
         return float(val[0])
 
 
+def generate_concurrent(jobs: Sequence[tuple], stop_at_eos: bool = True) -> List[GenerationResult]:
+    """Driver (rank 0): run several pipeline engines' generate jobs with ONE command —
+    ``jobs`` = [(engine, prompts, sampling, seed, eos_token_id)].  Every rank runs the jobs of
+    the groups it belongs to in job order, so engines on DISJOINT rank groups decode at the same
+    time (the reference runs its agents one after another: combine_model_fp_updated.py:194-200);
+    overlapping groups run one after another in that order.  Results then travel last stage ->
+    rank 0 in job order (after all compute, so no send waits on a rank still computing)."""
+    eng0 = jobs[0][0]
+    assert eng0.grank == 0, "the driver (rank 0) issues commands; workers run serve_workers()"
+    cmd = torch.zeros(_HDR, dtype=torch.long, device=eng0.cdev)
+    cmd[0], cmd[1] = CMD_GENERATE, len(jobs)
+    eng0._bcast(cmd)
+    payload = []
+    for eng, prompts, sp, seed, eos in jobs:
+        hdr, fl, ids, lens = eng._job_tensors(prompts, sp, seed, eos, stop_at_eos)
+        for t in (hdr, fl, ids, lens):
+            eng._bcast(t)
+        payload.append((eng, hdr, fl, ids, lens))
+    outs = _run_jobs(payload)
+    results = []
+    for (eng, prompts, sp, _, eos), (out, timing) in zip(jobs, outs):
+        toks = out.tolist()[:len(prompts)]
+        eng.last_ticks = int(timing[2])              # ticks run (fewer when EOS ended the run)
+        done = []
+        for r in toks:
+            if eos is not None and stop_at_eos and eos in r:
+                r = r[:r.index(eos) + 1]
+            done.append(r)
+        elapsed, ttft = float(timing[0]), float(timing[1])
+        results.append(GenerationResult(done, [len(p) for p in prompts], elapsed, ttft, max(0.0, elapsed - ttft)))
+    return results
+
+
+def _run_jobs(payload):
+    """Every rank: compute its member jobs in order, then deliver each job's result to rank 0."""
+    outs = [eng._run_local(hdr, fl, ids, lens) for eng, hdr, fl, ids, lens in payload]
+    for (eng, *_), o in zip(payload, outs):
+        eng._deliver(list(o))
+    return outs
+
+
 def serve_workers(engines: Dict[int, PipelineGenerator]) -> int:
-    """Worker loop of ranks > 0: execute the driver's commands on the stage of the addressed model
-    (``tag``) until STOP.  Returns the number of commands served."""
+    """Worker loop of ranks > 0: execute the driver's commands on the stages this rank holds
+    (every agent has an engine here, a stub where the rank is outside the agent's group) until
+    STOP.  Returns the number of commands served."""
     any_eng = next(iter(engines.values()))
     served = 0
     while True:
-        hdr = any_eng._bcast(torch.zeros(_HDR, dtype=torch.long, device=any_eng.cdev))
-        cmd, tag = int(hdr[0]), int(hdr[1])
+        hdr0 = any_eng._bcast(torch.zeros(_HDR, dtype=torch.long, device=any_eng.cdev))
+        cmd = int(hdr0[0])
         if cmd == CMD_STOP:
             return served
-        eng = engines[tag]
         if cmd == CMD_GENERATE:
-            fl = eng._bcast(torch.zeros(4, dtype=torch.float64, device=eng.cdev))
-            n_rows, T = eng.stage.M * eng.stage.b, int(hdr[3])
-            ids = eng._bcast(torch.zeros(n_rows, T, dtype=torch.long, device=eng.cdev))
-            lens = eng._bcast(torch.zeros(n_rows, dtype=torch.long, device=eng.cdev))
-            eng._run_generate(hdr, fl, ids, lens)
+            payload = []
+            for _ in range(int(hdr0[1])):
+                hdr = any_eng._bcast(torch.zeros(_HDR, dtype=torch.long, device=any_eng.cdev))
+                eng = engines[int(hdr[0])]
+                fl = eng._bcast(torch.zeros(4, dtype=torch.float64, device=eng.cdev))
+                ids = eng._bcast(torch.zeros(eng.M * eng.b, int(hdr[2]), dtype=torch.long, device=eng.cdev))
+                lens = eng._bcast(torch.zeros(eng.M * eng.b, dtype=torch.long, device=eng.cdev))
+                payload.append((eng, hdr, fl, ids, lens))
+            _run_jobs(payload)
         elif cmd == CMD_SCORE:
-            ids = eng._bcast(torch.zeros(int(hdr[2]), dtype=torch.long, device=eng.cdev))
+            eng = engines[int(hdr0[1])]
+            ids = eng._bcast(torch.zeros(int(hdr0[2]), dtype=torch.long, device=eng.cdev))
             eng._run_score(ids)
         else:
             raise RuntimeError(f"unknown pipeline command {cmd}")
@@ -253,7 +318,7 @@ def serve_workers(engines: Dict[int, PipelineGenerator]) -> int:
 
 def stop_workers(engine: PipelineGenerator) -> None:
     """Driver: release the workers' serve loop."""
-    if engine.world > 1 and engine.rank == 0:
+    if dist.is_initialized() and dist.get_world_size() > 1 and engine.grank == 0:
         hdr = torch.zeros(_HDR, dtype=torch.long, device=engine.cdev)
         hdr[0] = CMD_STOP
         engine._bcast(hdr)

@@ -40,6 +40,7 @@ class ServingEngine:
                       "decode_steps": 0, "max_concurrent": 0}
         # continuous batching needs per-row cache lengths: not with a HeadInfer-offloaded cache
         self.continuous = (generator.attn_hook is None) if continuous is None else continuous
+        self.width = 2048                          # SlotDecoder output columns per session
         self.steps_per_poll = max(1, steps_per_poll)
         self._stop = threading.Event()
         self._worker = threading.Thread(target=self._loop_continuous if self.continuous else self._loop, daemon=True)
@@ -48,8 +49,28 @@ class ServingEngine:
     # ------------------------------------------------------------------ API
     def submit(self, prompt_ids: List[int], sampling: SamplingParams, seed: int = 0) -> Future:
         fut: Future = Future()
+        err = self.reject_reason(prompt_ids, sampling)
+        if err is not None:                        # can never be served: fail now, never queue it
+            self.stats["errors"] += 1
+            fut.set_exception(ValueError(err))
+            return fut
         self.q.put((list(prompt_ids), sampling, seed, fut, time.perf_counter()))
         return fut
+
+    def reject_reason(self, prompt_ids: List[int], sampling: SamplingParams) -> Optional[str]:
+        """Why a request can never be admitted (None when it can): an empty prompt, prompt +
+        max_new_tokens beyond the cache, or (continuous mode) more new tokens than a session's
+        output width."""
+        n, new = len(prompt_ids), int(sampling.max_new_tokens)
+        if n == 0:
+            return "empty prompt"
+        if new < 1:
+            return "max_new_tokens must be >= 1"
+        if n + new > self.gen.max_seq:
+            return f"prompt ({n}) + max_new_tokens ({new}) exceeds the cache length {self.gen.max_seq}"
+        if self.continuous and new >= self.width:
+            return f"max_new_tokens ({new}) must be below the session width {self.width}"
+        return None
 
     def generate_request(self, req: Dict) -> Dict:
         ids = req.get("prompt_ids") or self.tok.encode(req.get("prompt") or "")
@@ -92,23 +113,33 @@ class ServingEngine:
             if self._stop.is_set() and not pending and (dec is None or not dec.busy()):
                 break
             try:
-                if dec is not None and not dec.busy() and (not pending or pending[0][1].key() != dec.sp.key()
-                                                           or dec.col * 2 > dec.width):
+                if dec is not None and not dec.busy() and (
+                        not pending or pending[0][1].key() != dec.sp.key() or dec.col * 2 > dec.width
+                        or not dec.can_admit(len(pending[0][0]), pending[0][1].max_new_tokens)):
                     dec = None                     # session drained: the queue head picks the next one
                 if dec is None and pending:
-                    dec = SlotDecoder(self.gen, pending[0][1], seed=pending[0][2])
+                    dec = SlotDecoder(self.gen, pending[0][1], seed=pending[0][2], width=self.width,
+                                      max_batch=self.max_batch)
                     self.stats["sessions"] += 1
                 if dec is None:
                     continue
-                # admit every waiting request of this session's sampling configuration that fits
+                # admit every waiting request of this session's sampling configuration that fits;
+                # a request whose admission fails is failed alone and dropped
                 keep = []
                 for it in pending:
                     ids, sp, _, fut, t_sub = it
                     if sp.key() == dec.sp.key() and dec.can_admit(len(ids), sp.max_new_tokens):
-                        dec.admit(ids, sp.max_new_tokens, eos, tag=it)
+                        try:
+                            dec.admit(ids, sp.max_new_tokens, eos, tag=it)
+                        except Exception as e:     # noqa: BLE001 - reported to that caller
+                            self.stats["errors"] += 1
+                            if not fut.done():
+                                fut.set_exception(e)
                     else:
                         keep.append(it)
                 pending = keep
+                if not dec.busy():
+                    continue                       # nothing admitted: the head opens a new session
                 occ = sum(s is not None for s in dec.slots)
                 self.stats["max_concurrent"] = max(self.stats["max_concurrent"], occ)
                 n = dec.step(self.steps_per_poll)

@@ -152,6 +152,37 @@ def test_serving_engine_continuous_batching(tmp_path):
         eng.close()
 
 
+def test_serving_engine_continuous_rejects_and_budgets():
+    """Continuous mode fails requests it can never admit (empty prompt, prompt + budget beyond the
+    cache, a budget wider than the session) at once and keeps serving the rest; a max_new_tokens=1
+    request admitted beside live slots returns exactly one token; ``max_batch`` caps the slots."""
+    from edgellm.serve.server import ServingEngine
+    from edgellm.utils.tokenizer import ByteTokenizer
+    cfg = tiny("llama")
+    m = build_model(cfg, dtype=torch.float32, seed=2)
+    eng = ServingEngine(Generator(m, max_batch=4, max_seq=64), ByteTokenizer(cfg.vocab_size), max_batch=2,
+                        steps_per_poll=1)
+    try:
+        sp = SamplingParams(max_new_tokens=6, do_sample=False)
+        bad = [eng.submit([], sp), eng.submit([1] * 60, sp),
+               eng.submit([1, 2], SamplingParams(max_new_tokens=4096, do_sample=False))]
+        for f in bad:
+            with pytest.raises(ValueError):
+                f.result(timeout=10)
+        long = eng.submit([1, 2, 3], SamplingParams(max_new_tokens=12, do_sample=False))
+        one = eng.submit([4, 5], SamplingParams(max_new_tokens=1, do_sample=False))
+        ok = eng.submit([7, 8, 9], sp)
+        assert len(one.result(timeout=60)["tokens"]) == 1
+        assert len(long.result(timeout=60)["tokens"]) == 12 and len(ok.result(timeout=60)["tokens"]) == 6
+        alone = Generator(m, max_batch=1, max_seq=64).generate([[4, 5]], SamplingParams(max_new_tokens=1,
+                                                                                        do_sample=False))
+        assert one.result()["tokens"] == alone.tokens[0]
+        st = eng.metrics()
+        assert st["errors"] == 3 and st["requests"] == 3 and st["max_concurrent"] <= 2
+    finally:
+        eng.close()
+
+
 def test_stage_server_replays_retried_step():
     cfg = tiny("gpt2", num_layers=2)
     s1 = build_model(cfg, dtype=torch.float32, first=1, last=2, seed=1)
