@@ -70,7 +70,12 @@ def parse(argv=None):
                     help="N = 1: time the RCCL PipelineStage engine (world-1 process group, device bound) "
                          "instead of the Generator, same config")
     ap.add_argument("--device", default=None, help="cuda (default when available) | cpu (gloo, tests)")
-    ap.add_argument("--partition", default="balanced", help="balanced | uniform | explicit '9,8,8,7'")
+    ap.add_argument("--partition", default="units",
+                    help="units (balanced over half-layer units: a stage boundary may fall between a layer's "
+                         "attention and MLP halves) | balanced (whole layers) | uniform | explicit '9,8,8,7'")
+    ap.add_argument("--pp-slack", type=int, default=0,
+                    help="N > 1: extra ticks per stage hop (1 = 2N micro-batches in flight, every RCCL hop "
+                         "overlapped with a tick of compute; doubles the per-token latency)")
     ap.add_argument("--latency-point", default="auto", choices=["auto", "off", "int8", "both"],
                     help="also report batch-1 p50 per-token latency (single GPU): int8 = the benchmark model at "
                          "micro-batch 1, both = plus a bf16 copy of the model (13.5 GB more, built for this only); "
@@ -95,17 +100,19 @@ def model_config(args):
     return cfg
 
 
-def build(args, device, first=0, last=None):
-    """Stage [first, last) of the benchmark model, quantised exactly as the unsplit model."""
+def build(args, device, first=0, last=None, units=None):
+    """Stage [first, last) of the benchmark model (or the half-layer units ``units=(ua, ub)`` of a
+    sub-layer split), quantised exactly as the unsplit model."""
     cfg = model_config(args)
     dtype = torch.bfloat16
     if args.quant == "w8a8_smoothquant":
         full = build_model(cfg, dtype=dtype, device=device, seed=args.seed)
         calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed)
-        model = smoothquant_stage(full, first, cfg.num_layers if last is None else last, calib, device=device)
+        model = smoothquant_stage(full, first, cfg.num_layers if last is None else last, calib, device=device,
+                                  units=units)
         del full
     else:
-        model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=args.seed)
+        model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=args.seed, units=units)
         if args.quant != "none":
             model = quantize_model(model, args.quant)
     if getattr(args, "lm_head", "bf16") == "int8" and model.has_head:
@@ -304,7 +311,7 @@ def main(argv=None):
                 + "; random prompts)",
         "config": {"model": args.model, "global_batch": res["global_batch"], "seq_len": args.prompt_len,
                    "parallelism": f"pp{args.gpus}", "quant": args.quant, "micro_batch": args.micro_batch,
-                   "micro_batches_in_flight": max(1, args.gpus) * max(1, args.lanes),
+                   "micro_batches_in_flight": res.get("micro_batches_in_flight", max(1, args.gpus) * max(1, args.lanes)),
                    "lanes": max(1, args.lanes), "partition": res.get("partition"),
                    "sampling": "T=0.7 top_k=50 top_p=0.9 rep=1.1",
                    "headinfer_heads": args.headinfer_heads,
@@ -333,6 +340,9 @@ def main(argv=None):
     if "per_rank" in res:
         out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
         out["per_rank"] = res["per_rank"]
+        for k in ("stage_cost_model_us", "stage_cost_spread", "slack"):
+            if k in res:
+                out[k] = res[k]
     print(json.dumps(out), flush=True)
     MetricsWriter(args.metrics_out).write(event="bench", **out)
     return out

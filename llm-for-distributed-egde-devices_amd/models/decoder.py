@@ -198,30 +198,49 @@ class MLP(nn.Module):
 
 
 class DecoderLayer(nn.Module):
-    def __init__(self, cfg: ModelConfig, idx: int, dtype, device):
+    """One decoder block.  ``has_attn`` / ``has_mlp`` False builds half a block (sequential-residual
+    architectures only): a pipeline stage boundary may then fall between the attention half
+    (norm1 + attention + o) and the MLP half (norm2 + MLP) of a layer.  The hand-off there is the
+    residual stream h2 = a + h, exactly the tensor a whole-layer boundary hands over."""
+
+    def __init__(self, cfg: ModelConfig, idx: int, dtype, device, has_attn: bool = True, has_mlp: bool = True):
         super().__init__()
+        assert has_attn or has_mlp
+        assert (has_attn and has_mlp) or not cfg.parallel_residual, "half layers need a sequential residual"
         self.cfg, self.idx = cfg, idx
-        self.norm1 = Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device)
-        self.norm2 = (None if cfg.shared_input_norm else Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device))
-        self.attn = Attention(cfg, idx, dtype, device)
-        self.mlp = MLP(cfg, dtype, device)
+        self.has_attn, self.has_mlp = has_attn, has_mlp
+        self.norm1 = Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device) if has_attn else None
+        self.norm2 = (None if cfg.shared_input_norm or not has_mlp
+                      else Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device))
+        self.attn = Attention(cfg, idx, dtype, device) if has_attn else None
+        self.mlp = MLP(cfg, dtype, device) if has_mlp else None
         if cfg.norm == "rms" and not cfg.parallel_residual:
             # o and down feed an RMSNorm (or the stage exit): bf16 decode GEMVs split K and the norm
             # kernel sums the fp32 slices (quantised replacements set their own split)
-            self.attn.o.split_k_out = self.mlp.down.split_k_out = BF16_SPLIT_K
+            if has_attn:
+                self.attn.o.split_k_out = BF16_SPLIT_K
+            if has_mlp:
+                self.mlp.down.split_k_out = BF16_SPLIT_K
 
     def forward(self, x, residual, ctx: AttnCtx):
         cfg = self.cfg
-        qa = self.attn.qkv.takes_quantized_input
-        qm = self.mlp.up.takes_quantized_input
         if not cfg.parallel_residual:
             # <= 4 rows: each norm of a split-K sum runs in the prologue of the W8A8 GEMV after it
-            d1 = getattr(self.attn.qkv, "pending_norm_ok", lambda glu=False: False)()
-            d2 = getattr(self.mlp.up, "pending_norm_ok", lambda glu=False: False)(glu=True)
-            n1, h = self.norm1(x, residual, quant=qa, defer=d1)
-            a = self.attn(n1, ctx)
-            n2, h2 = self.norm2(a, h, quant=qm, defer=d2)
+            qm = self.mlp.up.takes_quantized_input if self.has_mlp else False
+            d2 = getattr(self.mlp.up, "pending_norm_ok", lambda glu=False: False)(glu=True) if self.has_mlp else False
+            if self.has_attn:
+                qa = self.attn.qkv.takes_quantized_input
+                d1 = getattr(self.attn.qkv, "pending_norm_ok", lambda glu=False: False)()
+                n1, h = self.norm1(x, residual, quant=qa, defer=d1)
+                a = self.attn(n1, ctx)
+                if not self.has_mlp:
+                    return a, h                        # stage exit after the attention half
+                n2, h2 = self.norm2(a, h, quant=qm, defer=d2)
+            else:
+                n2, h2 = self.norm2(x, residual, quant=qm, defer=d2)   # MLP half: x = h2 from the stage before
             return self.mlp(n2), h2
+        qa = self.attn.qkv.takes_quantized_input
+        qm = self.mlp.up.takes_quantized_input
         if cfg.shared_input_norm:                      # phi
             n, h = self.norm1(x, residual, quant=qa and qm)
             if qa != qm:                               # mixed modes: feed each consumer its form
@@ -241,21 +260,31 @@ class DecoderLM(nn.Module):
     owns; embedding and head are present only on the first / last stage."""
 
     def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None, first: int = 0,
-                 last: Optional[int] = None):
+                 last: Optional[int] = None, split_first: bool = False, split_last: bool = False):
+        """``split_first``: layer ``first`` holds only its MLP half; ``split_last``: layer
+        ``last - 1`` only its attention half (sub-layer pipeline boundaries, see ``from_units``)."""
         super().__init__()
         self.cfg = cfg
         self.dtype = dtype
         self.first = first
         self.last = cfg.num_layers if last is None else last
-        self.has_embed = first == 0
-        self.has_head = self.last == cfg.num_layers
+        assert self.last > first or not (split_first or split_last)
+        assert not (split_first and split_last and self.last - first == 1), "an empty half-layer stage"
+        self.split_first, self.split_last = bool(split_first), bool(split_last)
+        self.units = (2 * first + self.split_first, 2 * self.last - self.split_last)
+        self.kv_first = first + self.split_first           # first layer with attention (KV cache)
+        self.has_embed = first == 0 and not self.split_first
+        self.has_head = self.last == cfg.num_layers and not self.split_last
         if self.has_embed:
             self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size, dtype=dtype, device=device),
                                       requires_grad=False)
             self.pos_embed = (nn.Parameter(torch.empty(cfg.max_position_embeddings, cfg.hidden_size, dtype=dtype,
                                                        device=device), requires_grad=False)
                               if cfg.pos_emb == "learned" else None)
-        self.layers = nn.ModuleList([DecoderLayer(cfg, i, dtype, device) for i in range(self.first, self.last)])
+        self.layers = nn.ModuleList([
+            DecoderLayer(cfg, i, dtype, device, has_attn=not (self.split_first and i == first),
+                         has_mlp=not (self.split_last and i == self.last - 1))
+            for i in range(self.first, self.last)])
         if self.has_head:
             self.final_norm = Norm(cfg.hidden_size, cfg.norm, cfg.norm_eps, dtype, device)
             if cfg.tie_word_embeddings and self.has_embed:
@@ -263,6 +292,13 @@ class DecoderLM(nn.Module):
             else:
                 self.lm_head = Linear(cfg.hidden_size, cfg.vocab_size, cfg.lm_head_bias, dtype, device)
         self._rope = None
+
+    @classmethod
+    def from_units(cls, cfg: ModelConfig, ua: int, ub: int, **kw) -> "DecoderLM":
+        """Stage of half-layer units [ua, ub): unit 2 i is layer i's attention half, 2 i + 1 its
+        MLP half (ub == 2 * num_layers: through the head)."""
+        assert 0 <= ua < ub <= 2 * cfg.num_layers or ua == ub == 2 * cfg.num_layers
+        return cls(cfg, first=ua // 2, last=(ub + 1) // 2, split_first=ua % 2 == 1, split_last=ub % 2 == 1, **kw)
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -372,8 +408,12 @@ def global_named_parameters(model: DecoderLM):
 
 
 def build_model(cfg: ModelConfig, dtype=torch.bfloat16, device=None, first: int = 0, last: Optional[int] = None,
-                seed: Optional[int] = 0) -> DecoderLM:
-    m = DecoderLM(cfg, dtype=dtype, device=device, first=first, last=last).eval()
+                seed: Optional[int] = 0, units: Optional[tuple] = None) -> DecoderLM:
+    """``units=(ua, ub)``: a sub-layer stage (``DecoderLM.from_units``) instead of layers [first, last)."""
+    if units is not None:
+        m = DecoderLM.from_units(cfg, units[0], units[1], dtype=dtype, device=device).eval()
+    else:
+        m = DecoderLM(cfg, dtype=dtype, device=device, first=first, last=last).eval()
     if seed is not None:
         init_random_(m, seed)
     return m

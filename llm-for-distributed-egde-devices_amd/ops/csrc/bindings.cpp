@@ -56,6 +56,7 @@ int edge_w8a8_rows256_splits(int K);
 void edge_w8a8_rows256_cfg(int cfg, int nt);
 void edge_w8a8_rows256_diag(int v);
 void edge_w8a8_rows256_magic(int v);
+void edge_w8a8_rows256_rst(int v);
 void edge_w8a8_rows256_splits_cfg(int s, int l);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st, const void* add);
@@ -903,6 +904,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "ring2_256") edge_w8a8_rows256_cfg((int)a, (int)b);
     else if (what == "ring2_256_diag") edge_w8a8_rows256_diag((int)a);
     else if (what == "ring2_256_magic") edge_w8a8_rows256_magic((int)a);
+    else if (what == "ring2_256_rst") edge_w8a8_rows256_rst((int)a);
     else if (what == "ring2_256_splits") edge_w8a8_rows256_splits_cfg((int)a, (int)b);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);

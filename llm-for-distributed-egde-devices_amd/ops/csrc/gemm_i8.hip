@@ -1385,8 +1385,13 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // NCW == 8: eight compute waves (two per SIMD) as 4 (rows) x 2 (tiles), each with 2 row blocks x
 // NTW / 2 tiles: the per-k-tile fold of the grouped scales (8 VALU per MFMA) then issues from two
 // waves per SIMD beside the other wave's MFMAs instead of serialising behind one wave's own.
+// RST (EPI_OUT / EPI_GLUQ, int8 operands): restaged epilogue.  After one more barrier (every DMA
+// into the ring has landed and no wave reads it) each compute wave writes its finished values into
+// its own LDS block and stores them back as 16-B row chunks: qkv's 12 x 8-B stores per lane become
+// 6 x 16-B, the quantising gate_up's 8 x 4-B become 2 x 16-B (a store tail is issue-bound:
+// MI355X_MICROARCH.md, attention epilogue store tail).
 template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true, int MS = 1,
-          int NAL = 0, int NCW = 4, int DT = 0>
+          int NAL = 0, int NCW = 4, int DT = 0, bool RST = false>
 __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
@@ -1414,6 +1419,10 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0) + EPK;
   static_assert(LDS_KB * 1024 <= 160 * 1024, "LDS budget");
   static_assert(NTW * 16 <= 256, "epilogue operand area");
+  static_assert(!RST || (DT == 0 && !SC && (EPI == EPI_OUT || EPI == EPI_GLUQ)), "restaged epilogues");
+  // restage blocks: per compute wave 32 rows, fp32 (EPI_OUT) or int8 (EPI_GLUQ), rows padded by 16 B
+  constexpr int RSB = EPI == EPI_OUT ? NTH * 16 * 4 + 16 : 80;
+  static_assert(!RST || NCW * 32 * RSB <= (LDS_KB - EPK) * 1024, "restage blocks fit below the epilogue area");
   __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_KB * 1024];
   int8_t* const wring = lds;
   int8_t* const aring = lds + RW * WST * 1024;
@@ -1483,6 +1492,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         issue(s + DA);                                  // into the slot of stage s - 1
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (RST) __builtin_amdgcn_s_barrier(); // the ring is free for the restaged epilogue
       return;
     }
   }
@@ -1518,6 +1528,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       issue(s + DW);                                  // into the slot of stage s - 1
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the workgroup
+    if constexpr (RST) __builtin_amdgcn_s_barrier();
     return;
   }
 
@@ -1694,11 +1705,41 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (RST) __builtin_amdgcn_s_barrier();    // every wave past the ring (loaders' DMA drained)
 
   if (diag & 16) return;                            // (diagnostic: no epilogue)
   // epilogue: lane holds row (2 wave + j) * 16 + (lane & 15), columns 4 (lane >> 4) .. + 3 of tile t
   const int g4 = 4 * (lane >> 4);
-  if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
+  if constexpr (RST && EPI == EPI_OUT) {
+    // fp32 values into the wave's block [32 rows][NTH * 16 columns], then 16-B bf16 row chunks out
+    constexpr int WC = NTH * 16, CPR = WC / 8;
+    static_assert((32 * CPR) % 64 == 0, "whole store rounds");
+    int8_t* const rs = lds + (size_t)wave * 32 * RSB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = j * 16 + (lane & 15);
+#pragma unroll
+      for (int t = 0; t < NTH; ++t) {
+        const int cl = (tb + t) * 16 + g4;
+        v4f v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (float)acc[j][t][q] * sa_r[j] * epi_sw[cl + q] + epi_b[cl + q];
+        *reinterpret_cast<v4f*>(rs + r * RSB + (t * 16 + g4) * 4) = v;
+      }
+    }
+    bf16_t* const o = reinterpret_cast<bf16_t*>(outv);
+#pragma unroll
+    for (int i = 0; i < 32 * CPR / 64; ++i) {
+      const int id = i * 64 + lane, r = id / CPR, cc = id % CPR;
+      const int lrow = 32 * mw + r, tile = nt0 + tb + cc / 2;
+      if (lrow < Ml && tile < NTt && (diag & 128) == 0) {
+        const v4f a = *reinterpret_cast<const v4f*>(rs + r * RSB + cc * 32);
+        const v4f b = *reinterpret_cast<const v4f*>(rs + r * RSB + cc * 32 + 16);
+        *reinterpret_cast<uint4*>(o + (size_t)(row0 + lrow) * N + (nt0 + tb) * 16 + cc * 8) =
+            uint4{pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]), pack_bf2(b[0], b[1]), pack_bf2(b[2], b[3])};
+      }
+    }
+  } else if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int lrow = (2 * mw + j) * 16 + (lane & 15);
@@ -1773,16 +1814,28 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
       amax = fmaxf(amax, 1e-8f);
       const float inv = 127.f / amax;
-      if (live && lrow < Ml) {
+      if (RST || (live && lrow < Ml)) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           uint32_t w = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) w |= (uint32_t)(uint8_t)quant_i8(h[p][q], inv) << (8 * q);
-          *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + ((nt0 + tb) / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
+          if constexpr (RST)                            // the wave's int8 block [32 rows][64 features]
+            *reinterpret_cast<uint32_t*>(lds + (size_t)wave * 32 * RSB + (j * 16 + (lane & 15)) * RSB + p * 16 + g4) = w;
+          else
+            *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + ((nt0 + tb) / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
         }
       }
       if (live && lane < 16 && row < Mpad) os[(size_t)grp64 * Mpad + row] = lrow < Ml ? amax / 127.f : 0.f;
+    }
+    if constexpr (RST) {                              // 32 rows x 64 B = two 16-B chunks per lane
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int id = i * 64 + lane, r = id >> 2, c16 = id & 3, lrow = 32 * mw + r;
+        if (live && lrow < Ml)
+          *reinterpret_cast<uint4*>(hq + (size_t)(row0 + lrow) * Fo + ((nt0 + tb) / 2) * 16 + c16 * 16) =
+              *reinterpret_cast<const uint4*>(lds + (size_t)wave * 32 * RSB + r * RSB + c16 * 16);
+      }
     }
   }
 }
@@ -1960,11 +2013,20 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
 // Tiles per workgroup are chosen for ~256 launched workgroups (the logical grid doubles).
 // cfg (EDGELLM_TUNE=ring2_256=c[,nt]): A/B geometries; nt = 0 (cfg 0 only) selects normal weight
 // allocation instead of nontemporal (1-4 % slower at M = 256).  -1: no kernel for this call.
-static int g_r256_cfg = 0, g_r256_nt = 1, g_r256_diag = 0, g_r256_magic = 1;
+static int g_r256_cfg = 0, g_r256_nt = 1, g_r256_diag = 0, g_r256_magic = 1, g_r256_rst = 1;
 template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV, int NCWV = 4, int DTV = 0>
 int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
                 int M, int N, int K, int Mpad, hipStream_t st, int S) {
   const int NTt = (N + 15) / 16, G = (NTt + NTWV - 1) / NTWV * S;
+  // restaged 16-B store epilogue (int8 operands, bf16 or quantised-GLU outputs, N % 16 == 0)
+  if constexpr (DTV == 0 && !SCV && (EPV == EPI_OUT || EPV == EPI_GLUQ)) {
+    if (g_r256_rst && N % 16 == 0) {
+      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV, DTV, true>),
+                         dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV, DTV>),
                      dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
@@ -2049,6 +2111,7 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
 
 extern "C" void edge_w8a8_rows256_cfg(int cfg, int nt) { g_r256_cfg = cfg; g_r256_nt = nt; }
 extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
+extern "C" void edge_w8a8_rows256_rst(int v) { g_r256_rst = v; }
 // grouped-scale fold of the 256-row split-K kernels: 1 = one-VALU magic-number form, 0 = cvt + fma
 extern "C" void edge_w8a8_rows256_magic(int v) { g_r256_magic = v; }
 // split-K slices the 129-256-row kernels use for a K (0: none)

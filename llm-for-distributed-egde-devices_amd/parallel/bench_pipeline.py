@@ -24,7 +24,7 @@ import torch
 import torch.distributed as dist
 
 from ..engine.generate import SamplingParams
-from .partition import partition_model, stage_costs
+from .partition import partition_model, partition_units, stage_costs, unit_stage_costs
 from .pipeline import PipelineStage, init_distributed
 from .watchdog import Watchdog
 
@@ -61,12 +61,23 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     # head GEMM 82 us + sampler 25 us + norm/embed ~10 us) -> 0.52; int8 head ~0.35 (estimate,
     # parallel/partition.py::layer_costs); bf16 models 0.4
     hcl = (0.35 if getattr(args, "lm_head", "bf16") == "int8" else 0.52) if args.quant != "none" else 0.4
-    bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
-                             weight_bytes=wbytes, explicit=explicit, head_cost_layers=hcl)
-    wd.beat("build")
-    _, model = build(args, device, first=bounds[rank], last=bounds[rank + 1])
     L = max(1, getattr(args, "lanes", 1))
-    M, P, b, T = world * L, world, args.micro_batch, args.prompt_len
+    slack = max(0, int(getattr(args, "pp_slack", 0)))
+    # micro-batch groups in flight: P (one per stage), or D (P - 1) + 2 with D = 1 + slack ticks per hop
+    n_groups = world if slack == 0 or world == 1 else (1 + slack) * (world - 1) + 2
+    M, P, b, T = n_groups * L, world, args.micro_batch, args.prompt_len
+    kvb = 1.0 if kv_dtype is not None and kv_dtype(args, cfg) == "int8" else 2.0
+    unit_kw = dict(rows=b, ctx=T + args.warmup + (args.steps + 1) // 2, weight_bytes=wbytes, kv_bytes=kvb,
+                   head_bytes=1.0 if getattr(args, "lm_head", "bf16") == "int8" else 2.0)
+    if args.partition == "units" and not explicit:
+        ubounds = partition_units(cfg, world, **unit_kw)
+    else:
+        bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
+                                 weight_bytes=wbytes, explicit=explicit, head_cost_layers=hcl)
+        ubounds = [2 * x for x in bounds]
+    ucost = unit_stage_costs(cfg, ubounds, **unit_kw)
+    wd.beat("build")
+    _, model = build(args, device, units=(ubounds[rank], ubounds[rank + 1]))
     W, K = args.warmup, args.steps
     S = W + K + 1
     g = torch.Generator().manual_seed(args.seed)
@@ -75,16 +86,17 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     # the stage's constructor joins every rank in one collective (eager RCCL communicator)
     stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs,
                           headinfer_heads=getattr(args, "headinfer_heads", None), lanes=L,
-                          kv_dtype=kv_dtype(args, cfg) if kv_dtype is not None else "bf16")
+                          kv_dtype=kv_dtype(args, cfg) if kv_dtype is not None else "bf16", slack=slack)
     if use_cuda:
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats(device)
-    # ticks count item groups of L micro-batches (one per lane)
-    t_a = (M + W * M) // L + (P - 1)
+    # ticks count item groups of L micro-batches (one per lane); the last stage lags D (P - 1)
+    D = 1 + slack
+    t_a = (M + W * M) // L + D * (P - 1)
     t_b = t_a + K * M // L
     # prefill window: tick 0 to the first tick after every prefill group left the last stage
     # (synchronised like the timed window; it ends before the warm-up decodes are timed)
-    t_p = M // L + (P - 1)
+    t_p = M // L + D * (P - 1)
     marks = {}
     stamps = []
 
@@ -132,15 +144,17 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
         per_rank = []
         for r, row in enumerate(allst):
             d = {k: round(float(v), 4) for k, v in zip(_STAT_KEYS, row[0].tolist()) if v == v}
-            d.update(rank=r, layers=[bounds[r], bounds[r + 1]])
+            d.update(rank=r, units=[ubounds[r], ubounds[r + 1]], layers=[ubounds[r] / 2, ubounds[r + 1] / 2])
             per_rank.append(d)
         ttft = [d["ttft_ms"] for d in per_rank if "ttft_ms" in d]
         res = dict(value=tokens / elapsed, ms_per_step=elapsed / K * 1e3, p50=float(lat.item()), global_batch=M * b,
                    prefill_tps=M * b * T / prefill_s if prefill_s > 0 else 0.0,
-                   mem_gb=float(mem.item()), partition=bounds, world_size=world, per_rank=per_rank,
+                   mem_gb=float(mem.item()), partition=[u / 2 for u in ubounds], world_size=world, per_rank=per_rank,
+                   stage_cost_model_us=[round(c, 1) for c in ucost],
+                   stage_cost_spread=round(max(ucost) / (sum(ucost) / len(ucost)), 4), slack=slack,
+                   micro_batches_in_flight=M,
                    bubble_frac_max=max(d.get("bubble_frac", 0.0) for d in per_rank),
-                   ttft_ms=ttft[0] if ttft else None,
-                   stage_cost_mb=[round(c / 1e6, 1) for c in stage_costs(cfg, bounds, wbytes, head_cost_layers=hcl)])
+                   ttft_ms=ttft[0] if ttft else None)
     dist.barrier()
     wd.stop()
     dist.destroy_process_group()

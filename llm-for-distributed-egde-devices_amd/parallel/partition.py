@@ -63,6 +63,54 @@ def balanced_partition(costs: Sequence[float], stages: int, head_cost: float = 0
     return bounds[::-1]
 
 
+# decode-time model of one half-layer unit on MI355X (us), calibrated on the 256-row W8A8 Llama-2-7B
+# bench step (profiles/rocprof_bench_default_r3_final.md): projections stream their weights at the
+# measured 256-row decode GEMM rate, attention its KV bytes at the measured attention rate, plus a
+# fixed per-half cost (RMSNorm launch + kernel boundaries); the head is its GEMM + sampler + norm.
+GEMM_BYTES_PER_US = 2.15e6
+ATTN_BYTES_PER_US = 5.9e6
+HALF_FIXED_US = 8.0
+HEAD_BYTES_PER_US = 3.2e6
+HEAD_FIXED_US = 35.0
+
+
+def decode_unit_costs(cfg: ModelConfig, rows: int = 256, ctx: int = 160, weight_bytes: float = 1.0,
+                      kv_bytes: float = 2.0, head_bytes: float = 2.0) -> Tuple[List[float], float]:
+    """Per half-layer unit costs (unit 2 i = layer i's norm1 + attention + o, 2 i + 1 = norm2 +
+    MLP) and the head's, in us per decode step of ``rows`` sequences at ``ctx`` cached tokens.
+    The attention half carries the KV stream, so at the bench's 256 x ~160 tokens it is about twice
+    the MLP half: whole layers (0.5 layer of head on the last stage) cannot balance 8 stages better
+    than max / mean 1.11, half layers can."""
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    w_attn = (cfg.qkv_size * H + H * cfg.q_size) * weight_bytes
+    w_mlp = ((2 if cfg.is_glu else 1) * I * H + I * H) * weight_bytes
+    kv = 2.0 * rows * ctx * cfg.num_kv_heads * cfg.head_dim * kv_bytes
+    attn = w_attn / GEMM_BYTES_PER_US + kv / ATTN_BYTES_PER_US + HALF_FIXED_US
+    mlp = w_mlp / GEMM_BYTES_PER_US + HALF_FIXED_US
+    head = H * cfg.vocab_size * head_bytes / HEAD_BYTES_PER_US + HEAD_FIXED_US
+    return [attn, mlp] * cfg.num_layers, head
+
+
+def partition_units(cfg: ModelConfig, stages: int, rows: int = 256, ctx: int = 160, weight_bytes: float = 1.0,
+                    kv_bytes: float = 2.0, head_bytes: float = 2.0) -> List[int]:
+    """Balanced stage boundaries in half-layer units (``DecoderLM.from_units``): a boundary may fall
+    between a layer's attention and MLP halves.  Sequential-residual models only; parallel-residual
+    ones (Phi-2, Pythia) get whole-layer boundaries (their units in pairs)."""
+    costs, head = decode_unit_costs(cfg, rows, ctx, weight_bytes, kv_bytes, head_bytes)
+    if cfg.parallel_residual:
+        layer = [costs[2 * i] + costs[2 * i + 1] for i in range(cfg.num_layers)]
+        return [2 * b for b in balanced_partition(layer, stages, head)]
+    return balanced_partition(costs, stages, head)
+
+
+def unit_stage_costs(cfg: ModelConfig, bounds: Sequence[int], **kw) -> List[float]:
+    """Modelled per-stage cost (us) of unit bounds (``partition_units``)."""
+    costs, head = decode_unit_costs(cfg, **kw)
+    out = [sum(costs[bounds[s]:bounds[s + 1]]) for s in range(len(bounds) - 1)]
+    out[-1] += head
+    return out
+
+
 def uniform_partition(L: int, stages: int) -> List[int]:
     return [round(i * L / stages) for i in range(stages + 1)]
 

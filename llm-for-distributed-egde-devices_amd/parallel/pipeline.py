@@ -56,7 +56,7 @@ class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
                  group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None,
                  lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True, kv_dtype: str = "bf16",
-                 ranks: Optional[Sequence[int]] = None):
+                 ranks: Optional[Sequence[int]] = None, slack: int = 0):
         """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
         to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
         HeadInfer").  The offloaded path is host-orchestrated on one compute stream, so it runs one
@@ -76,11 +76,13 @@ class PipelineStage:
         self.max_seq = max_seq
         self.group = group
         self.device = model.device
-        self.first, self.last = model.first, model.last
+        # KV layers: the stage's layers with an attention half (a stage opening on an MLP half has none for it)
+        self.first, self.last = getattr(model, "kv_first", model.first), model.last
         self.is_first, self.is_last = model.has_embed, model.has_head
         assert self.is_first == (rank == 0) and self.is_last == (rank == world - 1)
         self.prev = (rank - 1) % world
         self.next = (rank + 1) % world
+        self.slack = int(slack)                       # extra ticks per hop (P2P overlapped with compute)
         self.granks = list(ranks) if ranks is not None else list(range(world))
         assert len(self.granks) == world, "one global rank per stage"
         self.h_on = headinfer_heads if offload else None
@@ -111,6 +113,7 @@ class PipelineStage:
         self.streams = ([torch.cuda.Stream(self.device) for _ in range(lanes)]
                         if cuda and lanes > 1 else None)
         self.p2p_bytes = 0
+        self._copy_stream = None                      # host-staged sends (gloo with device tensors)
         self._plen, self._eos = None, None            # per-run: ragged prompt lengths, EOS id (last rank)
         if warm_comm and dist.is_initialized() and world > 1:
             self.warm_communicator()
@@ -125,26 +128,59 @@ class PipelineStage:
 
     # ------------------------------------------------------------------ p2p
     def _exchange(self, sends, recvs):
-        """sends/recvs: lists of (tensor, peer).  One grouped exchange (dist.P2POp batch)."""
+        """sends/recvs: lists of (tensor, peer stage).  One grouped exchange (dist.P2POp batch),
+        completed before returning (the current stream waits on it; host-staged: the host)."""
+        self._finish(self._post(sends, recvs))
+
+    def _post(self, sends, recvs, send_ready=None):
+        """Issue one grouped exchange without waiting for it; ``_finish`` completes it.  RCCL: the
+        communication stream first waits on everything already queued on the current stream (the
+        sends' producers), so posting BEFORE the next compute lets the transfer run beside it.
+        Host-staged (gloo with device tensors): the sends are copied to pinned host memory on a side
+        stream behind ``send_ready`` (an event after their producer), so the host never waits for
+        compute queued after it; received bytes land in pinned buffers until ``_finish``."""
         if not sends and not recvs:
-            return
+            return None
         self.p2p_bytes += sum(t.numel() * t.element_size() for t, _ in sends)
         g = self.granks
         if self.host_staged:
-            bufs = [torch.empty(t.shape, dtype=t.dtype) for t, _ in recvs]
-            p2p = [dist.P2POp(dist.isend, t.cpu(), g[p], self.group) for t, p in sends]
+            if self._copy_stream is None:
+                self._copy_stream = torch.cuda.Stream(self.device)
+            cs = self._copy_stream
+            host_sends = []
+            with torch.cuda.stream(cs):
+                if send_ready is not None:
+                    cs.wait_event(send_ready)
+                else:
+                    cs.wait_stream(torch.cuda.current_stream(self.device))
+                for t, _ in sends:
+                    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                    h.copy_(t, non_blocking=True)
+                    host_sends.append(h)
+            cs.synchronize()
+            bufs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t, _ in recvs]
+            p2p = [dist.P2POp(dist.isend, h, g[p], self.group) for h, (_, p) in zip(host_sends, sends)]
             p2p += [dist.P2POp(dist.irecv, h, g[p], self.group) for h, (_, p) in zip(bufs, recvs)]
         else:
             bufs = None
             p2p = [dist.P2POp(dist.isend, t, g[p], self.group) for t, p in sends]
             p2p += [dist.P2POp(dist.irecv, t, g[p], self.group) for t, p in recvs]
         with trace_range("pp.exchange"):
-            # RCCL: wait() makes the current stream wait on the communication (no host block)
-            for w in dist.batch_isend_irecv(p2p):
-                w.wait()
+            works = dist.batch_isend_irecv(p2p)
+        return works, bufs, [t for t, _ in recvs], p2p
+
+    def _finish(self, handle):
+        """Complete a posted exchange: RCCL — the current stream waits on it (no host block);
+        host-staged — the host waits, then the received bytes go to the device on the current
+        stream (ordered before the compute that reads them)."""
+        if handle is None:
+            return
+        works, bufs, dsts, _ = handle
+        for w in works:
+            w.wait()
         if bufs is not None:
-            for h, (t, _) in zip(bufs, recvs):
-                t.copy_(h)
+            for h, t in zip(bufs, dsts):
+                t.copy_(h, non_blocking=True)
         debug_sync("pp.exchange")
 
     def _send_one(self, t: torch.Tensor, peer: int):
@@ -340,12 +376,20 @@ class PipelineStage:
         def feeds_back(i):  # does item i's sampled token feed a later decode item?
             return (i < M and S >= 1) or (i >= M and (i - M) // M + 1 < S)
 
-        # tick t: rank r processes item group t - r (items [g L, (g + 1) L), one per lane, on the
-        # lanes' streams); every tick starts with ONE grouped exchange (the previous group's outputs
-        # out, this group's inputs in) ordered after all lanes' work and before any of the next
+        # tick t: rank r processes item group t - D r (items [g L, (g + 1) L), one per lane, on the
+        # lanes' streams).  D = 1 + slack ticks separate a group's visits of adjacent stages.  Every
+        # tick posts ONE grouped exchange: the outputs of this rank's previous tick out, the inputs
+        # of the group it computes at tick t + D - 1 in (and on stage 0 the tokens the last stage
+        # sampled at tick t - 1).  D = 1: the exchange completes before this tick's compute, which
+        # needs it.  D = 2: it completes one tick later, so the hop runs beside a whole tick of
+        # compute — at the price of 2P micro-batches in flight (the token ring then has 2P ticks).
         L = self.L
+        D = 1 + self.slack
+        assert D == 1 or M // L >= D * (P - 1) + 2 or P == 1, \
+            f"slack {self.slack} needs >= {D * (P - 1) + 2} micro-batch groups in flight, have {M // L}"
         n_groups = n_items // L
         cur_stream = torch.cuda.current_stream(dev) if self.cuda else None
+        R = D * self.rank                               # this rank's tick offset
 
         def group_valid(g):
             return 0 <= g < n_groups
@@ -367,15 +411,57 @@ class PipelineStage:
                 store[t] = time.perf_counter()
 
         t_start = time.perf_counter()
-        n_ticks = n_groups + P - 1
+        n_ticks = n_groups + D * (P - 1)
         # EOS agreement: from the tick after which the last stage has sampled every micro-batch's
         # first token, once per eos_every decode rounds (M / L ticks per round)
         eos_on = eos_token_id is not None and (P == 1 or dist.is_initialized())
-        eos_from, eos_period = (M // L) + P - 1, max(1, eos_every) * max(1, M // L)
+        eos_from, eos_period = (M // L) + D * (P - 1), max(1, eos_every) * max(1, M // L)
         stopped_at = None
-        t_first = P - 1 if self.is_last else -1     # tick whose prefill samples the first token
+        t_first = D * (P - 1) if self.is_last else -1   # tick whose prefill samples the first token
         ev_first: Dict[int, object] = {}
         mark(ev_first, -1)
+        due: Dict[int, object] = {}         # tick -> posted exchange whose receives it computes on
+        done_ev: Dict[int, object] = {}     # tick -> event after its compute (host-staged sends)
+        host_late = self.host_staged and D > 1
+
+        def exchange_for(t):
+            """(sends, recvs) of the exchange posted at tick t."""
+            prv_g, rcv_g = t - 1 - R, t + D - 1 - R
+            sends, recvs = [], []
+            if P == 1:
+                return sends, recvs
+            if group_valid(prv_g):
+                for prv in range(prv_g * L, prv_g * L + L):
+                    if not self.is_last:
+                        sends.append((pre_out[prv] if prv < M else self.hout[(prv - M) % M], self.next))
+                    elif feeds_back(prv):
+                        sends.append((self.tok[prv % M], 0))
+            if not self.is_first and group_valid(rcv_g):
+                for cur in range(rcv_g * L, rcv_g * L + L):
+                    if cur < M:
+                        pre_in[cur] = torch.empty(b * T, H, dtype=self.model.dtype, device=dev)
+                        recvs.append((pre_in[cur], self.prev))
+                    else:
+                        recvs.append((self.hin[(cur - M) % M], self.prev))
+            if self.is_first:
+                prod_g = t - 1 - D * (P - 1)    # group the last stage finished at tick t - 1
+                if group_valid(prod_g):
+                    for prod in range(prod_g * L, prod_g * L + L):
+                        if feeds_back(prod):
+                            recvs.append((self.tok[prod % M], P - 1))
+            return sends, recvs
+
+        def post(t):
+            sends, recvs = exchange_for(t)
+            nonlocal win_bytes
+            if w_a <= t < w_b:
+                win_bytes += sum(x.numel() * x.element_size() for x, _ in sends)
+            due[t + D - 1] = self._post(sends, recvs, send_ready=done_ev.pop(t - 1, None) if host_late else None)
+            if not self.is_last:
+                for prv in range((t - 1 - R) * L, (t - R) * L):
+                    if 0 <= prv < M:
+                        pre_out[prv] = None             # handed to the exchange (it holds the tensor)
+
         for t in range(n_ticks):
             if hook is not None:
                 hook(t)
@@ -383,74 +469,60 @@ class PipelineStage:
                 watchdog.beat(f"rank {self.rank} tick {t}/{n_ticks}")
             if fault is not None:
                 fault(t)
-            cur_g, prv_g = t - self.rank, t - 1 - self.rank
-            sends, recvs = [], []
-            if P > 1:
-                if group_valid(prv_g):
-                    for prv in range(prv_g * L, prv_g * L + L):
-                        if not self.is_last:
-                            sends.append((pre_out[prv] if prv < M else self.hout[(prv - M) % M], self.next))
-                        elif feeds_back(prv):
-                            sends.append((self.tok[prv % M], 0))
-                if not self.is_first and group_valid(cur_g):
-                    for cur in range(cur_g * L, cur_g * L + L):
-                        if cur < M:
-                            pre_in[cur] = torch.empty(b * T, H, dtype=self.model.dtype, device=dev)
-                            recvs.append((pre_in[cur], self.prev))
-                        else:
-                            recvs.append((self.hin[(cur - M) % M], self.prev))
-                if self.is_first:
-                    prod_g = t - P        # group the last stage finished at tick t-1
-                    if group_valid(prod_g):
-                        for prod in range(prod_g * L, prod_g * L + L):
-                            if feeds_back(prod):
-                                recvs.append((self.tok[prod % M], P - 1))
+            cur_g = t - R
             if self.streams:
                 for st in self.streams:
                     cur_stream.wait_stream(st)
             if w_a <= t - 1 < w_b:
                 mark(ev_done, t - 1)
-            if w_a <= t < w_b:
-                win_bytes += sum(x.numel() * x.element_size() for x, _ in sends)
-            self._exchange(sends, recvs)
+            if not host_late:
+                post(t)                                  # before this tick's compute: the hop overlaps it
+            self._finish(due.pop(t, None))
             if w_a <= t < w_b:
                 mark(ev_in, t)
             if self.streams:
                 for st in self.streams:
                     st.wait_stream(cur_stream)
-            if not group_valid(cur_g):
-                continue
-            with trace_range(f"pp.tick{t}"):
-                for cur in range(cur_g * L, cur_g * L + L):
-                    with lane_ctx(cur):
-                        if cur < M:                           # prefill item
-                            m = cur
-                            if self.streams and pre_in[m] is not None:
-                                pre_in[m].record_stream(self.streams[m % L])   # received on the exchange stream
-                            ids = prompts[m].to(dev) if self.is_first else None
-                            out = self._prefill(m, ids, T, pre_in[m])
-                            pre_in[m] = None
-                            if self.is_last:
-                                self._sample(m, out)
+            if group_valid(cur_g):
+                with trace_range(f"pp.tick{t}"):
+                    for cur in range(cur_g * L, cur_g * L + L):
+                        with lane_ctx(cur):
+                            if cur < M:                           # prefill item
+                                m = cur
+                                if self.streams and pre_in[m] is not None:
+                                    pre_in[m].record_stream(self.streams[m % L])   # received on the exchange stream
+                                ids = prompts[m].to(dev) if self.is_first else None
+                                out = self._prefill(m, ids, T, pre_in[m])
+                                pre_in[m] = None
+                                if self.is_last:
+                                    self._sample(m, out)
+                                else:
+                                    pre_out[m] = out
                             else:
-                                pre_out[m] = out
-                        else:
-                            k, m = divmod(cur - M, M)
-                            self._decode(m, T + k + 1)
+                                k, m = divmod(cur - M, M)
+                                self._decode(m, T + k + 1)
+            if host_late:
+                # host-staged slack: this tick's compute is queued first, then the exchange whose
+                # sends are the previous tick's outputs (the host waits only for that tick)
+                if self.streams:
+                    for st in self.streams:
+                        cur_stream.wait_stream(st)
+                e = torch.cuda.Event()
+                e.record(cur_stream)
+                done_ev[t] = e
+                post(t)
             debug_sync(f"pp.tick{t}")
             if t == t_first:
                 if self.streams:
                     for st in self.streams:
                         cur_stream.wait_stream(st)
                 mark(ev_first, t)
-            if not self.is_last and group_valid(prv_g):
-                for prv in range(prv_g * L, prv_g * L + L):
-                    if prv < M:
-                        pre_out[prv] = None                # sent this tick
             if eos_on and t >= eos_from and (t - eos_from) % eos_period == 0 and t < n_ticks - 1:
                 if self._all_hit():
                     stopped_at = t
                     break
+        for k in sorted(due):                            # (after an EOS stop: drain posted exchanges)
+            self._finish(due.pop(k))
         if self.streams:
             for st in self.streams:
                 cur_stream.wait_stream(st)

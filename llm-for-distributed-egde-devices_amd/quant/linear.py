@@ -316,6 +316,8 @@ def enable_fused_glu(model) -> int:
     n = 0
     if cfg.is_glu and cfg.act == "silu_glu" and cfg.intermediate_size % 64 == 0:
         for layer in model.layers:
+            if layer.mlp is None:
+                continue
             up = layer.mlp.up
             if isinstance(up, W8A8Linear) and isinstance(layer.mlp.down, W8A8Linear) and not up.glu_blocked:
                 up.block_glu_()
@@ -337,7 +339,7 @@ def enable_split_k_outputs(model) -> int:
         return 0
     n = 0
     for layer in model.layers:
-        for lin in (layer.attn.o, layer.mlp.down):
+        for lin in [m for m in (layer.attn and layer.attn.o, layer.mlp and layer.mlp.down) if m is not None]:
             if isinstance(lin, W8A8Linear) and lin.in_features % 64 == 0:
                 lin.split_k_out = SPLIT_K
                 n += 1

@@ -147,6 +147,8 @@ def quantize_model(model: DecoderLM, mode: str, calib_ids: Optional[torch.Tensor
         gpre = f"layers.{layer.idx}."
         for parent, attr, key in ((layer.attn, "qkv", "attn.qkv"), (layer.attn, "o", "attn.o"),
                                   (layer.mlp, "up", "mlp.up"), (layer.mlp, "down", "mlp.down")):
+            if parent is None:                 # half layer of a sub-layer pipeline stage
+                continue
             lin = getattr(parent, attr)
             if mode in ("w8a8_smoothquant", "w8a8"):
                 s = factors.get(gpre + key)
@@ -180,13 +182,18 @@ def quantize_head(model: DecoderLM) -> DecoderLM:
 
 @torch.no_grad()
 def smoothquant_stage(full: DecoderLM, first: int, last: int, calib_ids: torch.Tensor, alpha: float = 0.5,
-                      device=None) -> DecoderLM:
-    """Calibrate + smooth the FULL model once, then cut layers [first, last) into a W8A8 stage.
-    Every pipeline split (1/2/4/8) therefore gets bit-identical quantised weights for a layer."""
+                      device=None, units=None) -> DecoderLM:
+    """Calibrate + smooth the FULL model once, then cut layers [first, last) (or the half-layer
+    units ``units=(ua, ub)``) into a W8A8 stage.  Every pipeline split (1/2/4/8, whole or
+    sub-layer boundaries) therefore gets bit-identical quantised weights for a layer."""
     from ..models.decoder import global_named_parameters
     stats = collect_act_absmax(full, calib_ids.to(full.device))
     factors = smooth_model_(full, stats, alpha)
-    stage = DecoderLM(full.cfg, dtype=full.dtype, device=device or full.device, first=first, last=last).eval()
+    if units is not None:
+        stage = DecoderLM.from_units(full.cfg, units[0], units[1], dtype=full.dtype,
+                                     device=device or full.device).eval()
+    else:
+        stage = DecoderLM(full.cfg, dtype=full.dtype, device=device or full.device, first=first, last=last).eval()
     src = dict(global_named_parameters(full))
     for name, p in global_named_parameters(stage):
         if name == "lm_head.weight" and name not in src:

@@ -179,7 +179,7 @@ class StageServer:
         if s is None or s["kv"].max_batch != batch:
             if len(self.slots) >= self.max_requests:
                 self.slots.pop(next(iter(self.slots)))
-            s = {"kv": KVCache(self.model.cfg, batch, self.max_seq, self.model.first, self.model.last,
+            s = {"kv": KVCache(self.model.cfg, batch, self.max_seq, getattr(self.model, "kv_first", self.model.first), self.model.last,
                                self.model.dtype, self.model.device), "last": None}
             self.slots[seq_id] = s
         return s
@@ -297,7 +297,7 @@ class EdgePipeline:
         B, T = len(prompts), plens.pop()
         self._seq += 1
         seq_id = self._seq
-        kv = KVCache(self.first.cfg, B, self.max_seq, self.first.first, self.first.last, self.first.dtype,
+        kv = KVCache(self.first.cfg, B, self.max_seq, getattr(self.first, "kv_first", self.first.first), self.first.last, self.first.dtype,
                      self.first.device)
         ids = torch.tensor(prompts, dtype=torch.long, device=self.first.device)
         t0 = time.perf_counter()

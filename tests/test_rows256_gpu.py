@@ -113,6 +113,32 @@ def test_rows256_gluq(cuda, cfg, nt, M, F, K):
     assert (err <= 0.51 * step + 1e-2 * ref.float().view(M, F // 64, 64).abs() + 1e-3).all(), err.max().item()
 
 
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("kind,N,K", [("out", 12288, 4096), ("out", 2560, 2560), ("gluq", 22016, 4096),
+                                      ("gluq", 2048, 2048)])
+def test_rows256_restaged_epilogue_bitexact(cuda, M, kind, N, K):
+    """The restaged 16-B store epilogue (tune ring2_256_rst 1, default) writes the same bits as the
+    direct per-fragment stores (rst 0), including the ragged last rows of the upper half."""
+    C = ops.ext()
+    torch.manual_seed(M + N)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.004 + 1e-4
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    outs = []
+    try:
+        for rst in (0, 1):
+            C.tune("ring2_256_rst", rst, 0)
+            r = C.w8a8_gemm_gluq(qx, sx, wp, sw, bias, N, K) if kind == "gluq" else C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+            outs.append([t.clone() for t in r] if isinstance(r, (tuple, list)) else [r.clone()])
+    finally:
+        C.tune("ring2_256_rst", 1, 0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_rows256_model_routes(cuda):
     """A W8A8 Llama layer stack at 256 decode rows takes the fused path: grouped-scale attention
     output, split-K o / down partials, quantising GLU (decode_rows_ok routes 129-256 rows)."""

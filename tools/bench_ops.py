@@ -660,6 +660,54 @@ def magic_rows(C, dev, M=256):
     return out
 
 
+def knob_ab_rows(C, dev, knob, values=(1, 0), M=256, shapes=None):
+    """A/B of one tuning knob (``tune knob=v``) on the 256-row decode GEMMs, interleaved rounds,
+    cache-cold weights; also checks that every setting gives the same output bits as the first."""
+    out = []
+    shapes = shapes or {"qkv": (12288, 4096, "out"), "gate_up": (22016, 4096, "gluq"), "o": (4096, 4096, "part"),
+                        "down": (4096, 11008, "part")}
+    for name, (N, K, kind) in shapes.items():
+        ncopy = max(2, (1 << 30) // (N * K) + 1)
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
+        sw = torch.rand(N, device=dev) * 0.01
+        qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+        sx = (torch.rand(K // 64, (M + 15) // 16 * 16, device=dev) if kind == "part" else torch.rand(M, device=dev)) * 0.01
+        ctr = [0]
+
+        def call(wp=None):
+            if wp is None:
+                ctr[0] = (ctr[0] + 1) % ncopy
+                wp = wps[ctr[0]]
+            if kind == "gluq":
+                return C.w8a8_gemm_gluq(qx, sx, wp, sw, None, N, K)
+            if kind == "part":
+                return C.w8a8_gemm_splitk(qx, sx, wp, sw, None, N, K, 0)
+            return C.w8a8_gemm(qx, sx, wp, sw, None, N, K)
+        res, same = {}, True
+        ref = None
+        for v in values:
+            C.tune(knob, v, 0)
+            o = call(wps[0])
+            o = [x.clone() for x in o] if isinstance(o, (tuple, list)) else [o.clone()]
+            if ref is None:
+                ref = o
+            else:
+                same = same and all(torch.equal(a, b) for a, b in zip(ref, o))
+        for _ in range(3):
+            for v in values:
+                C.tune(knob, v, 0)
+                res.setdefault(v, []).append(timeit(call, iters=10, per_graph=ncopy))
+        C.tune(knob, values[0], 0)
+        row = dict(op=f"ab_{knob}", shape=name, M=M, N=N, K=K, identical=bool(same))
+        for v, ts in res.items():
+            row[f"{knob}{v}_us"] = round(min(ts), 2)
+        out.append(row)
+        print(row, flush=True)
+        del wps
+    return out
+
+
 def bf16_splits_rows(C, dev, Ms=(128, 256)):
     """bf16 ring split-K slice count for o / down (tune bf16_ring_splits), interleaved."""
     out = []
@@ -760,6 +808,9 @@ def main():
         rows += bf16_rows(C, dev)
     if only is not None and "bf16splits" in only:
         rows += bf16_splits_rows(C, dev)
+    if only is not None and "rst" in only:
+        rows += knob_ab_rows(C, dev, "ring2_256_rst", shapes={"qkv": (12288, 4096, "out"),
+                                                              "gate_up": (22016, 4096, "gluq")})
     if only is not None and "magic" in only:
         rows += magic_rows(C, dev)
     if only is not None and "prio" in only:
