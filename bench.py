@@ -52,6 +52,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama-2-7b")
     ap.add_argument("--quant", default="w8a8_smoothquant", choices=["none", "w8a8_smoothquant", "w8a8"])
+    ap.add_argument("--checkpoint", default=None,
+                    help="an edgellm INT8 checkpoint directory (python -m edgellm.cli.quantize): every rank reads "
+                         "only its stage instead of building + calibrating the full bf16 model")
     ap.add_argument("--micro-batch", type=int, default=256,
                     help="sequences per micro-batch (256: the largest the fused decode GEMMs take — the 129-256-row "
                          "kernels stream every weight once for all 256 sequences; 16-128 trade tok/s for latency)")
@@ -90,7 +93,10 @@ def parse(argv=None):
 
 
 def model_config(args):
-    if args.model.startswith("tiny:"):
+    if getattr(args, "checkpoint", None):
+        from edgellm.quant.checkpoint import checkpoint_config
+        cfg = checkpoint_config(args.checkpoint)
+    elif args.model.startswith("tiny:"):
         cfg = tiny(args.model.split(":", 1)[1], num_layers=8)   # 8 layers: splits up to 8 stages
     else:
         cfg = get_config(args.model)
@@ -105,6 +111,16 @@ def build(args, device, first=0, last=None, units=None):
     sub-layer split), quantised exactly as the unsplit model."""
     cfg = model_config(args)
     dtype = torch.bfloat16
+    if getattr(args, "checkpoint", None):
+        # an edgellm INT8 checkpoint (python -m edgellm.cli.quantize): this stage's tensors only
+        from edgellm.quant.checkpoint import load_quantized
+        model = load_quantized(args.checkpoint, device=device, first=first, last=last, dtype=dtype, units=units)
+        if getattr(args, "lm_head", "bf16") == "int8" and model.has_head:
+            model = quantize_head(model)
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+            torch.cuda.synchronize()
+        return cfg, model
     if args.quant == "w8a8_smoothquant":
         full = build_model(cfg, dtype=dtype, device=device, seed=args.seed)
         calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed)

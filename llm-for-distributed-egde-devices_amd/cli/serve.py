@@ -3,6 +3,8 @@
     python -m edgellm.cli.serve                                   # TimeService :50051 + REST :8000
     python -m edgellm.cli.serve --model tiny:llama --rest-port 8000     # + POST /generate engine
     python -m edgellm.cli.serve --model gpt2 --stage 6:12 --grpc-port 50052  # a gRPC pipeline stage
+    torchrun --nproc-per-node 4 -m edgellm.cli.serve --model llama-2-7b --quant w8a8_smoothquant
+                                                                  # engine pipelined over 4 GPUs (RCCL)
 
 TimeService and ``GET /`` are wire-compatible with the reference demo (Code/gRPC/server.py,
 rest_api.py); the stage service speaks edgellm.Stage (serve/proto/edgellm_stage.proto).
@@ -56,6 +58,8 @@ def build(args: argparse.Namespace):
                                    first=a, last=b)
         extra.append(StageServer(model, max_seq=args.max_seq).handler())
         log.info(f"stage layers [{a}, {b}) of {src}")
+    elif args.model and _launch(args) is not None:
+        engine = build_pipeline_engine(args, _launch(args))
     elif args.model:
         from ..models.registry import load_model
         from ..parallel.split import agent_devices, split_model
@@ -81,6 +85,37 @@ def build(args: argparse.Namespace):
         from ..serve.rest import make_app
         app = make_app(engine)
     return server, port, app, engine
+
+
+_LAUNCH = {}
+
+
+def _launch(args):
+    """torchrun (WORLD_SIZE > 1): (rank, world, device) with the process group up, else None."""
+    if "v" not in _LAUNCH:
+        from .common import pp_launch
+        _LAUNCH["v"] = pp_launch({"pp_size": None, "devices": args.device or ""})
+    return _LAUNCH["v"]
+
+
+def build_pipeline_engine(args, launch):
+    """Serving over the RCCL pipeline (one process per GPU under torchrun): every rank builds its
+    stage (``build_pp_engine``; an INT8 checkpoint directory as ``--model`` is read per stage), rank
+    0 wraps its ``PipelineGenerator`` in the ServingEngine; every other rank serves the driver's
+    pipeline commands (``serve_workers``) and never returns.  Requests are batched per sampling
+    configuration into the pipeline's M micro-batches of b rows (static batches: a batch runs to
+    completion across all stages; M >= P keeps every stage busy)."""
+    from ..parallel.pp_engine import serve_workers
+    from ..serve.server import ServingEngine
+    from .common import build_pp_engine
+    rt = dict(max_seq=args.max_seq, kv_dtype=args.kv_dtype, base_model_path=args.base_model_path)
+    eng, tok, src, bounds = build_pp_engine(args.model, args.precision, args.quant, rt, launch, tag=0,
+                                            max_batch=args.max_batch)
+    if launch[0] != 0:
+        serve_workers({0: eng})
+        raise SystemExit(0)
+    log.info(f"generation engine: {src} pipelined over {launch[1]} ranks at layers {bounds}")
+    return ServingEngine(eng, tok, args.max_batch, continuous=False)
 
 
 def main(argv: Optional[List[str]] = None):

@@ -49,13 +49,36 @@ def precision_dtype(precision: str, device) -> torch.dtype:
     return {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}.get(p, torch.bfloat16)
 
 
+def quantized_checkpoint_dir(name_or_path: str, base_dir: Optional[str] = None) -> Optional[str]:
+    """The directory of an edgellm int8 checkpoint (``edgellm.cli.quantize``) named by the model
+    id, directly or under ``base_dir``; None otherwise."""
+    import os
+    from ..quant.checkpoint import is_quantized_checkpoint
+    for c in (name_or_path, os.path.join(base_dir, name_or_path) if base_dir else None,
+              os.path.join(base_dir, name_or_path.replace("/", "_")) if base_dir else None):
+        if c and is_quantized_checkpoint(c):
+            return c
+    return None
+
+
 def load_model(name_or_path: str, precision: str = "bf16", quant: str = "none", device=None,
                base_dir: Optional[str] = None, first: int = 0, last: Optional[int] = None,
-               config_override: Optional[ModelConfig] = None) -> Tuple[DecoderLM, object, str]:
-    """Returns (model, tokenizer, source) with source "checkpoint:<dir>" or "random-init:<preset>"."""
+               config_override: Optional[ModelConfig] = None, units: Optional[tuple] = None
+               ) -> Tuple[DecoderLM, object, str]:
+    """Returns (model, tokenizer, source) with source "checkpoint:<dir>", "int8-checkpoint:<dir>"
+    (an edgellm quantised checkpoint: its stage is read directly, already quantised — ``quant``
+    is then the checkpoint's own mode) or "random-init:<preset>".  ``units``: a half-layer stage."""
     dtype = precision_dtype(precision, device)
+    qdir = quantized_checkpoint_dir(name_or_path, base_dir)
+    if qdir is not None:
+        from ..quant.checkpoint import load_quantized
+        model = load_quantized(qdir, device=device, first=first, last=last, dtype=dtype, units=units)
+        if quant not in (None, "none", model.quant_mode):
+            log.warning(f"{qdir} holds {model.quant_mode} weights: --quant {quant} ignored")
+        return model, load_tokenizer(qdir, model.cfg.vocab_size), f"int8-checkpoint:{qdir}"
     path = resolve_model_dir(name_or_path, base_dir)
     if path is not None:
+        assert units is None, "half-layer stages of HF checkpoints: load the whole layers"
         model = load_hf_model(path, dtype=dtype, device=device, first=first, last=last)
         tok = load_tokenizer(path, model.cfg.vocab_size)
         source = f"checkpoint:{path}"
@@ -71,7 +94,7 @@ def load_model(name_or_path: str, precision: str = "bf16", quant: str = "none", 
         else:
             cfg = get_config(preset)
         seed = zlib.crc32(name_or_path.encode()) & 0xFFFF
-        model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=seed)
+        model = build_model(cfg, dtype=dtype, device=device, first=first, last=last, seed=seed, units=units)
         tok = ByteTokenizer(max(259, cfg.vocab_size))
         source = f"random-init:{cfg.name or preset}"
         log.warning(f"No checkpoint for '{name_or_path}': using random-init {cfg.name or preset} weights "

@@ -50,8 +50,18 @@ def load_stage(model_id: str, precision: str, quant: str, device, base_dir: Opti
     partition by default), the embedding on rank 0, the head on the last rank.  Weights equal the
     unsplit model's (random-init weights are seeded by global parameter name; SmoothQuant calibrates
     and smooths the FULL model, then cuts the stage).  Returns (stage, tokenizer, source, bounds)."""
-    from ..models.registry import load_model
+    from ..models.registry import load_model, quantized_checkpoint_dir
     from .partition import partition_model
+    qdir = quantized_checkpoint_dir(model_id, base_dir)
+    if qdir is not None:
+        # an int8 checkpoint: this rank reads only its stage (no full bf16 model, no calibration)
+        from ..quant.checkpoint import checkpoint_config
+        cfg = checkpoint_config(qdir)
+        if bounds is None:
+            bounds = partition_model(cfg, world, "balanced", weight_bytes=1.0)
+        first, last = int(bounds[rank]), int(bounds[rank + 1])
+        stage, tok, source = load_model(qdir, precision, "none", device, None, first=first, last=last)
+        return stage, tok, source, list(bounds)
     full_needed = quant == "w8a8_smoothquant"
     if full_needed:
         full, tok, source = load_model(model_id, precision, "none", device, base_dir)
@@ -78,7 +88,13 @@ def load_stage(model_id: str, precision: str, quant: str, device, base_dir: Opti
 
 def _cfg_of(model_id, precision, device, base_dir):
     """Config + tokenizer of a model without materialising its layers (an embedding-only stage)."""
-    from ..models.registry import load_model
+    from ..models.registry import load_model, quantized_checkpoint_dir
+    qdir = quantized_checkpoint_dir(model_id, base_dir)
+    if qdir is not None:
+        from ..quant.checkpoint import checkpoint_config
+        from ..utils.tokenizer import load_tokenizer
+        cfg = checkpoint_config(qdir)
+        return cfg, load_tokenizer(qdir, cfg.vocab_size), f"int8-checkpoint:{qdir}"
     m, tok, source = load_model(model_id, precision, "none", device, base_dir, first=0, last=0)
     return m.cfg, tok, source
 

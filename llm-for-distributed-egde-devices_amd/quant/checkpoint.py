@@ -32,6 +32,22 @@ VERSION = 1
 _PROJ = (("attn", "qkv"), ("attn", "o"), ("mlp", "up"), ("mlp", "down"))
 
 
+def is_quantized_checkpoint(path: Optional[str]) -> bool:
+    """A directory written by ``save_quantized`` (``quant_config.json`` of this format)."""
+    if not path or not os.path.isdir(path):
+        return False
+    f = os.path.join(path, "quant_config.json")
+    if not os.path.exists(f):
+        return False
+    with open(f) as fh:
+        return json.load(fh).get("format") == FORMAT
+
+
+def checkpoint_config(path: str) -> ModelConfig:
+    with open(os.path.join(path, "quant_config.json")) as f:
+        return ModelConfig(**json.load(f)["model_config"])
+
+
 @torch.no_grad()
 def save_quantized(model: DecoderLM, path: str, extra: Optional[dict] = None) -> None:
     from safetensors.torch import save_file
@@ -41,7 +57,10 @@ def save_quantized(model: DecoderLM, path: str, extra: Optional[dict] = None) ->
     quant_names = set()
     for layer in model.layers:
         for a, b in _PROJ:
-            mod = getattr(getattr(layer, a), b)
+            parent = getattr(layer, a)
+            if parent is None:                   # half layer of a sub-layer stage
+                continue
+            mod = getattr(parent, b)
             p = f"layers.{layer.idx}.{a}.{b}"
             bias = mod.bias
             if isinstance(mod, W8A8Linear):          # canonical [gate | up] row order on disk
@@ -65,7 +84,7 @@ def save_quantized(model: DecoderLM, path: str, extra: Optional[dict] = None) ->
     save_file(tensors, os.path.join(path, "model.safetensors"))
     meta = {"format": FORMAT, "version": VERSION, "mode": mode, "model_config": model.cfg.to_dict(),
             "smoothing": "folded" if mode == "w8a8_smoothquant" else "none", "first": model.first,
-            "last": model.last}
+            "last": model.last, "units": list(getattr(model, "units", (2 * model.first, 2 * model.last)))}
     meta.update(extra or {})
     with open(os.path.join(path, "quant_config.json"), "w") as f:
         json.dump(meta, f, indent=2)
@@ -73,7 +92,11 @@ def save_quantized(model: DecoderLM, path: str, extra: Optional[dict] = None) ->
 
 @torch.no_grad()
 def load_quantized(path: str, device=None, first: int = 0, last: Optional[int] = None,
-                   dtype=torch.bfloat16) -> DecoderLM:
+                   dtype=torch.bfloat16, units: Optional[tuple] = None) -> DecoderLM:
+    """The stage [first, last) (or half-layer ``units``) of a quantised checkpoint.  Only that
+    stage's tensors are read, and no bf16 copy of a projection is ever materialised: the model is
+    built on the meta device and every tensor is created from the file on ``device`` (a pipeline
+    rank of a 7B model reads its ~1/P of 7 GB int8 instead of building and calibrating 13.5 GB)."""
     from safetensors import safe_open
     with open(os.path.join(path, "quant_config.json")) as f:
         meta = json.load(f)
@@ -81,15 +104,25 @@ def load_quantized(path: str, device=None, first: int = 0, last: Optional[int] =
         raise ValueError(f"{path} is not an {FORMAT} checkpoint")
     cfg = ModelConfig(**meta["model_config"])
     mode = meta["mode"]
-    model = DecoderLM(cfg, dtype=dtype, device=device, first=first, last=last).eval()
+    saved = tuple(meta.get("units") or (2 * meta.get("first", 0), 2 * meta.get("last", cfg.num_layers)))
+    if units is not None:
+        model = DecoderLM.from_units(cfg, units[0], units[1], dtype=dtype, device="meta").eval()
+    else:
+        model = DecoderLM(cfg, dtype=dtype, device="meta", first=first, last=last).eval()
+    ua, ub = model.units
+    assert saved[0] <= ua and ub <= saved[1], f"checkpoint holds units {saved}, stage needs {model.units}"
+    device = torch.device(device) if device is not None else torch.device("cpu")
     with safe_open(os.path.join(path, "model.safetensors"), framework="pt") as sf:
         keys = set(sf.keys())
         for layer in model.layers:
             for a, b in _PROJ:
+                parent = getattr(layer, a)
+                if parent is None:
+                    continue
                 p = f"layers.{layer.idx}.{a}.{b}"
                 if p + ".qweight" not in keys:
                     continue
-                lin = getattr(getattr(layer, a), b)
+                lin = getattr(parent, b)
                 bias = sf.get_tensor(p + ".bias").to(device) if p + ".bias" in keys else None
                 q = sf.get_tensor(p + ".qweight").to(device)
                 if p + ".SCB" in keys:
@@ -99,13 +132,32 @@ def load_quantized(path: str, device=None, first: int = 0, last: Optional[int] =
                 else:
                     new = W8A8Linear(lin.in_features, lin.out_features, bias is not None, device=device, dtype=dtype)
                     new.load_int8(q, sf.get_tensor(p + ".w_scale").to(device), bias)
-                setattr(getattr(layer, a), b, new)
-        for name, prm in global_named_parameters(model):
+                setattr(parent, b, new)
+        # every remaining (meta) parameter straight from the file onto the device
+        for name, prm in list(global_named_parameters(model)):
             src = name
             if src not in keys and name == "lm_head.weight" and cfg.tie_word_embeddings:
                 src = "embed"
-            prm.copy_(sf.get_tensor(src).to(device=prm.device, dtype=prm.dtype))
+            t = sf.get_tensor(src).to(device=device, dtype=prm.dtype)
+            _set_param(model, _local_name(model, name), t)
+    left = [n for n, t in list(model.named_parameters()) + list(model.named_buffers()) if t.is_meta]
+    assert not left, f"checkpoint left {left[:4]} unloaded"
     model.quant_mode = mode
     if mode in ("w8a8_smoothquant", "w8a8"):
         enable_fused_glu(model)
     return model
+
+
+def _local_name(model: DecoderLM, global_name: str) -> str:
+    if global_name.startswith("layers."):
+        _, idx, rest = global_name.split(".", 2)
+        return f"layers.{int(idx) - model.first}.{rest}"
+    return global_name
+
+
+def _set_param(model: torch.nn.Module, name: str, t: torch.Tensor) -> None:
+    mod = model
+    parts = name.split(".")
+    for p in parts[:-1]:
+        mod = getattr(mod, p)
+    mod._parameters[parts[-1]] = torch.nn.Parameter(t, requires_grad=False)

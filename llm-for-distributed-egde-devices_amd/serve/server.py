@@ -32,14 +32,18 @@ class ServingEngine:
         self.gen, self.tok = generator, tokenizer
         # one JSONL record per served batch (EDGELLM_METRICS=<path> or metrics_path)
         self.writer = MetricsWriter(metrics_path or os.environ.get("EDGELLM_METRICS"))
-        self.max_batch = min(max_batch, generator.kv.max_batch)
+        # rows one batch can hold: the cache rows (Generator) or the pipeline's micro-batches x rows
+        cap = generator.kv.max_batch if hasattr(generator, "kv") else generator.M * generator.b
+        self.max_batch = min(max_batch, cap)
         self.batch_wait_s = batch_wait_s
         self.q: "queue.Queue[tuple]" = queue.Queue()
         self.lat = LatencyHistogram()
         self.stats = {"requests": 0, "batches": 0, "generated_tokens": 0, "errors": 0, "sessions": 0,
                       "decode_steps": 0, "max_concurrent": 0}
         # continuous batching needs per-row cache lengths: not with a HeadInfer-offloaded cache
-        self.continuous = (generator.attn_hook is None) if continuous is None else continuous
+        # continuous batching drives a Generator's cache rows (not a HeadInfer cache, not a pipeline)
+        slots_ok = getattr(generator, "attn_hook", 1) is None
+        self.continuous = slots_ok if continuous is None else (continuous and slots_ok)
         self.width = 2048                          # SlotDecoder output columns per session
         self.steps_per_poll = max(1, steps_per_poll)
         self._stop = threading.Event()

@@ -1,0 +1,41 @@
+"""torchrun target of tests/test_serve_pipeline_cpu.py: the REST engine over a CPU gloo pipeline.
+Rank 0 posts concurrent POST /generate requests through a FastAPI TestClient and writes the tokens
+to argv[1]; the other ranks serve the pipeline commands until the driver stops them."""
+import argparse
+import json
+import sys
+import threading
+
+from edgellm.cli.serve import _launch, build_pipeline_engine
+from edgellm.parallel.pp_engine import stop_workers
+
+
+def main():
+    out_path, model = sys.argv[1], sys.argv[2]
+    args = argparse.Namespace(model=model, precision="fp32", quant="none", device="cpu", base_model_path=None,
+                              max_batch=4, max_seq=128, kv_dtype="bf16")
+    launch = _launch(args)
+    engine = build_pipeline_engine(args, launch)          # ranks > 0 never return
+    from fastapi.testclient import TestClient
+    from edgellm.serve.rest import make_app
+    client = TestClient(make_app(engine))
+    reqs = [{"prompt_ids": [1, 2, 3 + i], "max_new_tokens": 5 + (i % 3), "do_sample": False} for i in range(6)]
+    res = [None] * len(reqs)
+
+    def post(i):
+        r = client.post("/generate", json=reqs[i])
+        res[i] = r.json()["tokens"] if r.status_code == 200 else r.text
+
+    th = [threading.Thread(target=post, args=(i,)) for i in range(len(reqs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    metrics = client.get("/metrics").json()
+    engine.close()
+    stop_workers(engine.gen)
+    json.dump({"requests": reqs, "tokens": res, "metrics": metrics}, open(out_path, "w"))
+
+
+if __name__ == "__main__":
+    main()
