@@ -83,10 +83,12 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
                     print(out)
     target = target_path()
     if _stale(target, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", target,
+        tmp = target + ".tmp"
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
                f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
                "-lamdhip64", f"-Wl,-rpath,{lib}"]
         _run(cmd)
+        os.replace(tmp, target)          # atomic: a concurrent reader never sees a half-written library
     if verbose:
         print("built", target)
     return target

@@ -1123,6 +1123,194 @@ __global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ 
       *reinterpret_cast<const uint4*>(A + (size_t)row * K + (size_t)kt * 64 + 16 * (lane >> 4));
 }
 
+// ------------------------------------------------------------------------------------ x32
+// Prefill GEMM on v_mfma_i32_32x32x32_i8 with 256 x 256 block tiles (M >= 256, K % 64 == 0,
+// N % 8 == 0).  The LDS image is the big kernel's (1 KiB pieces of 16 rows x 64 k, activations
+// row-major or fragment-packed, weights packed), 4 stages of 32 KiB; what changes is the MFMA:
+//  * 8 waves as 2 (tokens) x 4 (columns), each 128 tokens x 64 columns = 4 x 2 blocks of 32 x 32.
+//    Per 32-k step a wave reads 6 fragments (4 activation + 2 weight blocks) for 8 MFMAs, so the
+//    LDS reads per MFMA-cycle are those of a 128 x 64 wave tile: the big kernel's 16x16x64 form
+//    holds its 64 x 64 tile's k-tile fragments (32 VGPRs) x 2 buffers + 64 accumulators, and at
+//    128 x 64 it spilled; a 32-k step's fragments are 24 VGPRs, so 128 accumulators + two steps of
+//    fragments fit, and a k-tile costs 1024 MFMA cycles per CU against 32 KiB of DMA (31 B/clk)
+//    and ~125 B/clk of LDS traffic.
+//  * A 32 x 32 x 32 operand of 32 rows = two stacked 16-row pieces: lane l reads piece 2 b +
+//    ((l >> 4) & 1), 16 B of lane slot (l & 15) + 16 (2 s + (l >> 5)) — row l & 31, k 32 s + 16 (l >> 5)
+//    of the 64-k tile (conflict-free: each 16-lane group covers the 64 banks once).
+//  * Operands swapped as in the big kernel (weights = A operand): a lane's accumulator holds one
+//    token (l & 31) and 4 runs of 4 consecutive columns 8 q + 4 (l >> 5).  The epilogue restages
+//    32 tokens x 64 columns per wave at a time (int32, XOR-swizzled 16-B chunks) and writes 16-B
+//    bf16 row chunks.
+//  * DT == 1: bf16 operands (the bf16 prefill GEMM): a fragment-packed bf16 weight (16 rows x 32 k
+//    per KiB) and a row-major bf16 activation have byte for byte the int8 layouts, with K counted
+//    in bytes, and v_mfma_f32_32x32x16_bf16 takes the same 16 B per lane (k 8 (l >> 5) .. + 8 of a
+//    16-k step) as the i8 form — so only the MFMA and the epilogue (fp32 sums + bias, no scales)
+//    change.  sa / sw are unused.
+template <bool APK, int DT = 0>
+__global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
+                                                              const int8_t* __restrict__ Wp, const float* __restrict__ sw,
+                                                              const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
+                                                              int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
+  constexpr int R = 4, BMV = 256, BNV = 256, NWV = 8;
+  constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
+  static_assert(R * STAGE <= 160 * 1024 && NWV * 32 * 256 <= R * STAGE, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  constexpr int GM = 4;
+  const int per_group = GM * grid_n;
+  const int grp = wgid / per_group, gm0 = grp * GM, gsz = min(GM, grid_m - gm0);
+  const int inr = wgid - grp * per_group;
+  const int bm = gm0 + inr % gsz, bn = inr / gsz;
+
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  uint32_t off[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int p = wave + NWV * i;
+    if (p < AP && APK) {
+      const int rb = min(bm * (BMV / 16) + p, (M + 15) / 16 - 1);
+      off[i] = (uint32_t)rb * (uint32_t)KT * 1024u + lane * 16;
+    } else if (p < AP) {
+      const int row = min(bm * BMV + p * 16 + (lane & 15), M - 1);
+      off[i] = (uint32_t)row * (uint32_t)K + 16 * (lane >> 4);
+    } else {
+      const int t = min(bn * BP + (p - AP), NTt - 1);
+      off[i] = (uint32_t)t * (uint32_t)KT * 1024u + lane * 16;
+    }
+  }
+  auto issue = [&](int st) {
+    const int kt = min(st, KT - 1);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const bool isa = wave + NWV * i < AP;
+      glds16((isa ? A + (size_t)kt * (APK ? 1024 : 64) : Wp + (size_t)kt * 1024) + off[i],
+             ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
+    }
+  };
+  // lane's byte in a 32-row operand block: piece offset ((l >> 4) & 1) KiB, lane slot
+  // (l & 15) + 32 (l >> 5) (k-step 0; k-step 1 adds 16 slots = 512 B)
+  const uint32_t lo = (((lane >> 4) & 1) << 10) + (((lane & 15) + 32 * (lane >> 5)) << 4);
+  const uint32_t ring0 = lds_off(ring) + lo;
+  const uint32_t abase = ring0 + (wm * 8) * 1024, wbase = ring0 + (AP + wn * 4) * 1024;
+  // fragments of stage st, k-step ks: fa[c] = activation block c (tokens 32 c..), fw[b] = weight block b
+  auto read_frags = [&](int st, int ks, v4i (&fa)[4], v4i (&fw)[2]) {
+    const uint32_t so = (st % R) * STAGE + ks * 512;
+    const uint32_t ab = abase + so, wb = wbase + so;
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fa[0]) : "v"(ab));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fa[1]) : "v"(ab));
+    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(fa[2]) : "v"(ab));
+    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(fa[3]) : "v"(ab));
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fw[0]) : "v"(wb));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fw[1]) : "v"(wb));
+  };
+  using AccT = std::conditional_t<DT == 1, v16f, v16i>;
+  AccT acc[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[c][b][r] = 0;
+  auto mma = [&](v4i (&fa)[4], v4i (&fw)[2]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(fa[c]));
+#pragma unroll
+    for (int b = 0; b < 2; ++b) asm volatile("" : "+v"(fw[b]));
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if constexpr (DT == 1)
+          acc[c][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8s, fw[b]), __builtin_bit_cast(v8s, fa[c]),
+                                                              acc[c][b], 0, 0, 0);
+        else
+          acc[c][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[b], fa[c], acc[c][b], 0, 0, 0);
+      }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) asm volatile("" : "+v"(acc[c][b]));
+  };
+
+#pragma unroll
+  for (int st = 0; st < R; ++st) issue(st);
+  v4i xa[4], xw[2], ya[4], yw[2];
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 1) * PPW) : "memory");
+  __builtin_amdgcn_s_barrier();
+  read_frags(0, 0, xa, xw);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int kt = 0; kt < KT; ++kt) {                   // x: (kt, step 0) in registers
+    read_frags(kt, 1, ya, yw);
+    mma(xa, xw);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < KT) {                                // wave-uniform
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 2) * PPW) : "memory");   // own DMA of kt + 1
+      __builtin_amdgcn_s_barrier();                   // kt + 1 landed everywhere; slot of kt free
+      issue(kt + R);
+      read_frags(kt + 1, 0, xa, xw);
+    }
+    mma(ya, yw);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-load stages past the end
+
+  // epilogue: acc[c][b] register r -> token wm*128 + 32 c + (l & 31), column
+  // wn*64 + 32 b + 8 (r >> 2) + 4 (l >> 5) + (r & 3).  Per c: the wave's 32 tokens x 64 columns of
+  // int32 go to its LDS block (256-B rows, 16-B chunk k of token t at k ^ (t & 15)), then each lane
+  // takes 8 consecutive columns (chunk pair lane & 7) of tokens it * 8 + (lane >> 3).
+  const int c8 = lane & 7, tl = lane & 31, hi = lane >> 5;
+  const int col0 = bn * BNV + wn * 64 + c8 * 8;
+  const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
+  float swv[8], bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = min(col0 + e, N - 1);
+    swv[e] = DT == 1 ? 1.f : sw[col];
+    bv[e] = bf2f(bp[bias != nullptr ? col : 0]);
+  }
+  __syncthreads();                                    // every wave is done with the ring
+  int8_t* wt = ring + wave * (32 * 256);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k16 = 8 * b + 2 * q + hi;           // 16-B chunk (4 int32 columns) of the 64
+        v4i v4;
+        if constexpr (DT == 1)
+          v4 = __builtin_bit_cast(v4i, v4f{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]});
+        else
+          v4 = v4i{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]};
+        *reinterpret_cast<v4i*>(wt + tl * 256 + ((k16 ^ (tl & 15)) << 4)) = v4;
+      }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int t = it * 8 + (lane >> 3);
+      const int row = bm * BMV + wm * 128 + c * 32 + t;
+      const float sr = DT == 1 ? 1.f : sa[min(row, M - 1)];
+      const v4i lo4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8) ^ (t & 15)) << 4));
+      const v4i hi4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8 + 1) ^ (t & 15)) << 4));
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (DT == 1) {
+          v[e] = __builtin_bit_cast(float, lo4[e]) + bv[e];
+          v[e + 4] = __builtin_bit_cast(float, hi4[e]) + bv[e + 4];
+        } else {
+          v[e] = (float)lo4[e] * sr * swv[e] + bv[e];
+          v[e + 4] = (float)hi4[e] * sr * swv[e + 4] + bv[e + 4];
+        }
+      }
+      if (row < M && col0 < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col0) = pack8(v);   // N % 8 == 0
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------- ring
 // 65-128 decode rows (two micro-batches or one 128-row micro-batch) on an LDS-DMA ring.
 // The ldsa kernel above stages activations through VGPRs (global load -> ds_write -> barrier) with
@@ -1144,14 +1332,10 @@ __global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ 
 // LDS-DMA (vmcnt(0)), draining the ring each stage.  Ordering is explicit instead: counted vmcnt
 // for this wave's own DMA, a bare s_barrier for the other waves', lgkmcnt(0) before the MFMAs.
 
-// LN (whole lines, C == 2): an activation piece is 8 rows x 128 B (two k-tiles) instead of one
-// fragment's 16 rows x 64 B.  Measured (tools/ingest_bw.hip), L2 -> LDS by LDS-DMA moves 1 KiB
-// pieces of whole 128-B lines at ~60 B/clk/CU but the 16-row x 64-B fragment pattern at ~18: at 128
-// rows the activation re-reads are 2.7x the weight bytes, so their access pattern, not HBM, set
-// the GEMV's rate.  Within a piece, lane l loads row l >> 3, 16-B chunk (l & 7) ^ (l >> 3) to LDS
-// position l: logical chunk c of row r sits at c ^ (r & 7), and the fragment reads (16 rows x
-// one chunk) hit 8 distinct 16-B bank groups per 8 rows.
-template <int NTW, int C, int R, bool SCALED, int EPI, bool LN = false>
+// (Activation pieces here are 16 rows x 64 B fragments; tools/ingest_bw.hip measured that pattern
+// at ~18 B/clk/CU L2 -> LDS against ~60 for whole 128-B lines, which is why the ring2 kernel below
+// DMAs whole-line pieces.)  This kernel remains the 65-128-row form for per-token-scaled split-K.
+template <int NTW, int C, int R, bool SCALED, int EPI>
 __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
@@ -1162,7 +1346,6 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
   constexpr int PPW = PIECES / NWV, PEXTRA = PIECES % NWV;   // waves < PEXTRA issue PPW + 1 pieces
   static_assert(R * STAGE <= 150 * 1024, "LDS ring budget");
   static_assert(EPI != EPI_GLUQ || NTW == 8, "GLUQ: 8 tiles = 64 features per workgroup");
-  static_assert(!LN || C == 2, "whole-line activation pieces cover two k-tiles");
   __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
   const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
   const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
@@ -1178,12 +1361,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 #pragma unroll
   for (int i = 0; i < PMAX; ++i) {
     const int p = min(wave + i * NWV, PIECES - 1);
-    if (p < APC && LN) {                             // activation lines: rows 8p .. 8p + 7, two k-tiles
-      const int row = min(p * 8 + (lane >> 3), M - 1);
-      src[i] = A + (size_t)row * K + (size_t)kbeg * 64 + 16 * ((lane & 7) ^ (lane >> 3));
-      stride[i] = 64;
-      klocal[i] = 0;
-    } else if (p < APC) {                            // activation fragment: row block p % MB
+    if (p < APC) {                            // activation fragment: row block p % MB
       const int row = min((p % MB) * 16 + (lane & 15), M - 1);
       src[i] = A + (size_t)row * K + (size_t)kbeg * 64 + 16 * (lane >> 4);
       stride[i] = 64;
@@ -1205,8 +1383,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
     for (int i = 0; i < PMAX; ++i) {
       if (i < PPW || wave < PEXTRA) {
         const int p = wave + i * NWV;
-        // past the slice: a valid, unused tile (line pieces: a valid pair, KTC % 2 == 0)
-        const int kt = LN && p < APC ? min(st * C, KTC - C) : min(st * C + klocal[i], KTC - 1);
+        const int kt = min(st * C + klocal[i], KTC - 1);   // past the slice: a valid, unused tile
         glds16(src[i] + (size_t)kt * stride[i], ring + (st % R) * STAGE + p * 1024);
       }
     }
@@ -1256,13 +1433,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
       if (s * C + c < KTC) {                          // wave-uniform
         v4i a[2], b[NTW];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if constexpr (LN)   // row block rb = 2 wave + j: pieces 2 rb, 2 rb + 1; chunk 4 c + (lane >> 4)
-            a[j] = lds_read16(base + (2 * (2 * wave + j) + ((lane & 15) >> 3)) * 1024 + (lane & 7) * 128 +
-                              (((4 * c + (lane >> 4)) ^ (lane & 7)) << 4));
-          else
-            a[j] = lds_read16(base + (c * MB + 2 * wave + j) * 1024 + lane * 16);
-        }
+        for (int j = 0; j < 2; ++j) a[j] = lds_read16(base + (c * MB + 2 * wave + j) * 1024 + lane * 16);
 #pragma unroll
         for (int t = 0; t < NTW; ++t) b[t] = lds_read16(base + (APC + c * NTW + t) * 1024 + lane * 16);
         v4f sgv[2];
@@ -1359,7 +1530,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // so one wave cannot keep a deep weight queue behind a shallow activation queue — separate waves
 // can:
 //   * NWL loader waves issue only weight tiles, DW = RW - 1 stages ahead (RW slots);
-//   * 4 compute waves issue only activation pieces (whole lines, as the ring kernel's LN form),
+//   * 4 compute waves issue only activation pieces (whole 128-B lines: 8 rows x 128 B per piece),
 //     DA = RA - 1 stages ahead, and own 2 row blocks x NTW tiles of accumulators each.
 // A stage is two k-tiles.  One bare barrier per stage: every wave first waits (counted vmcnt) for
 // its own DMA of stage s, then the barrier makes slot s visible to all and frees slot s - 1,
@@ -1370,7 +1541,7 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // loader waves) into a third ring, and every k-tile's int32 MFMA result is folded in fp32.
 // EPI_PART: blockIdx = group * S + slice; slice ks reduces stages [NS ks / S, NS (ks + 1) / S).
 // WNT: weight DMA with the nontemporal cache policy (default); false = normal allocation, so the
-// other lane's read of the same layer can hit the memory-side cache (A/B knob "weight_nt")
+// other lane's read of the same layer can hit the memory-side cache (no default uses it)
 // MS == 2 (129-256 rows, one 256-row decode micro-batch): the rows are cut into two halves of at
 // most 128 and each logical workgroup runs once per half.  The two halves of one weight panel are
 // blocks b and b + 8: under the observed round-robin dispatch they share an XCD, and the second
@@ -1385,13 +1556,11 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // NCW == 8: eight compute waves (two per SIMD) as 4 (rows) x 2 (tiles), each with 2 row blocks x
 // NTW / 2 tiles: the per-k-tile fold of the grouped scales (8 VALU per MFMA) then issues from two
 // waves per SIMD beside the other wave's MFMAs instead of serialising behind one wave's own.
-// RST (EPI_OUT / EPI_GLUQ, int8 operands): restaged epilogue.  After one more barrier (every DMA
-// into the ring has landed and no wave reads it) each compute wave writes its finished values into
-// its own LDS block and stores them back as 16-B row chunks: qkv's 12 x 8-B stores per lane become
-// 6 x 16-B, the quantising gate_up's 8 x 4-B become 2 x 16-B (a store tail is issue-bound:
-// MI355X_MICROARCH.md, attention epilogue store tail).
+// (A restaged 16-B store epilogue — qkv's 12 x 8-B stores per lane as 6 x 16-B, gate_up's 8 x 4-B as
+// 2 x 16-B — measured neutral at 256 rows, 22.74 vs 22.77 us / 34.65 vs 34.69: the tail is not
+// store-issue bound here, so the direct per-fragment stores stay.)
 template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true, int MS = 1,
-          int NAL = 0, int NCW = 4, int DT = 0, bool RST = false>
+          int NAL = 0, int NCW = 4, int DT = 0>
 __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
@@ -1419,10 +1588,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   constexpr int LDS_KB = RW * WST + RA * 16 + (SC ? RW : 0) + EPK;
   static_assert(LDS_KB * 1024 <= 160 * 1024, "LDS budget");
   static_assert(NTW * 16 <= 256, "epilogue operand area");
-  static_assert(!RST || (DT == 0 && !SC && (EPI == EPI_OUT || EPI == EPI_GLUQ)), "restaged epilogues");
-  // restage blocks: per compute wave 32 rows, fp32 (EPI_OUT) or int8 (EPI_GLUQ), rows padded by 16 B
-  constexpr int RSB = EPI == EPI_OUT ? NTH * 16 * 4 + 16 : 80;
-  static_assert(!RST || NCW * 32 * RSB <= (LDS_KB - EPK) * 1024, "restage blocks fit below the epilogue area");
   __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_KB * 1024];
   int8_t* const wring = lds;
   int8_t* const aring = lds + RW * WST * 1024;
@@ -1492,7 +1657,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         issue(s + DA);                                  // into the slot of stage s - 1
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (RST) __builtin_amdgcn_s_barrier(); // the ring is free for the restaged epilogue
       return;
     }
   }
@@ -1528,7 +1692,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       issue(s + DW);                                  // into the slot of stage s - 1
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the workgroup
-    if constexpr (RST) __builtin_amdgcn_s_barrier();
     return;
   }
 
@@ -1705,41 +1868,11 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (RST) __builtin_amdgcn_s_barrier();    // every wave past the ring (loaders' DMA drained)
 
   if (diag & 16) return;                            // (diagnostic: no epilogue)
   // epilogue: lane holds row (2 wave + j) * 16 + (lane & 15), columns 4 (lane >> 4) .. + 3 of tile t
   const int g4 = 4 * (lane >> 4);
-  if constexpr (RST && EPI == EPI_OUT) {
-    // fp32 values into the wave's block [32 rows][NTH * 16 columns], then 16-B bf16 row chunks out
-    constexpr int WC = NTH * 16, CPR = WC / 8;
-    static_assert((32 * CPR) % 64 == 0, "whole store rounds");
-    int8_t* const rs = lds + (size_t)wave * 32 * RSB;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = j * 16 + (lane & 15);
-#pragma unroll
-      for (int t = 0; t < NTH; ++t) {
-        const int cl = (tb + t) * 16 + g4;
-        v4f v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = (float)acc[j][t][q] * sa_r[j] * epi_sw[cl + q] + epi_b[cl + q];
-        *reinterpret_cast<v4f*>(rs + r * RSB + (t * 16 + g4) * 4) = v;
-      }
-    }
-    bf16_t* const o = reinterpret_cast<bf16_t*>(outv);
-#pragma unroll
-    for (int i = 0; i < 32 * CPR / 64; ++i) {
-      const int id = i * 64 + lane, r = id / CPR, cc = id % CPR;
-      const int lrow = 32 * mw + r, tile = nt0 + tb + cc / 2;
-      if (lrow < Ml && tile < NTt && (diag & 128) == 0) {
-        const v4f a = *reinterpret_cast<const v4f*>(rs + r * RSB + cc * 32);
-        const v4f b = *reinterpret_cast<const v4f*>(rs + r * RSB + cc * 32 + 16);
-        *reinterpret_cast<uint4*>(o + (size_t)(row0 + lrow) * N + (nt0 + tb) * 16 + cc * 8) =
-            uint4{pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]), pack_bf2(b[0], b[1]), pack_bf2(b[2], b[3])};
-      }
-    }
-  } else if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
+  if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int lrow = (2 * mw + j) * 16 + (lane & 15);
@@ -1814,39 +1947,26 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
       amax = fmaxf(amax, 1e-8f);
       const float inv = 127.f / amax;
-      if (RST || (live && lrow < Ml)) {
+      if (live && lrow < Ml) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           uint32_t w = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) w |= (uint32_t)(uint8_t)quant_i8(h[p][q], inv) << (8 * q);
-          if constexpr (RST)                            // the wave's int8 block [32 rows][64 features]
-            *reinterpret_cast<uint32_t*>(lds + (size_t)wave * 32 * RSB + (j * 16 + (lane & 15)) * RSB + p * 16 + g4) = w;
-          else
-            *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + ((nt0 + tb) / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
+          *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + ((nt0 + tb) / 2 + p) * 16 + g4) = w;   // Fo % 64 == 0
         }
       }
       if (live && lane < 16 && row < Mpad) os[(size_t)grp64 * Mpad + row] = lrow < Ml ? amax / 127.f : 0.f;
-    }
-    if constexpr (RST) {                              // 32 rows x 64 B = two 16-B chunks per lane
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int id = i * 64 + lane, r = id >> 2, c16 = id & 3, lrow = 32 * mw + r;
-        if (live && lrow < Ml)
-          *reinterpret_cast<uint4*>(hq + (size_t)(row0 + lrow) * Fo + ((nt0 + tb) / 2) * 16 + c16 * 16) =
-              *reinterpret_cast<const uint4*>(lds + (size_t)wave * 32 * RSB + r * RSB + c16 * 16);
-      }
     }
   }
 }
 }  // namespace
 
-static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2, g_ring2_cfg = 0, g_ring2_rot = 0;
-extern "C" void edge_w8a8_ring2_cfg(int v, int rot) { g_ring2_cfg = v; g_ring2_rot = rot; }
-static int g_w_nt = 1;
-extern "C" void edge_w8a8_weight_nt(int v) { g_w_nt = v; }
+static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2;
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel (BM = 128)
-static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0;
+static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0, g_prefill_x32 = 0;
+// prefill_x32: 0 off, 1 the 256 x 256 32x32x32 kernel when the grid fills >= 1 round of CUs (M >= 256)
+extern "C" void edge_w8a8_prefill_x32(int v) { g_prefill_x32 = v; }
 extern "C" void edge_w8a8_prefill_prio(int v) { g_prefill_prio = v; }
 extern "C" void edge_w8a8_prefill_apack(int v) { g_prefill_apack = v; }
 // b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
@@ -1888,146 +2008,95 @@ int launch_ldsa(const void* A, const float* sa, const void* Wp, const float* sw,
   return (int)hipGetLastError();
 }
 
-template <int NTW, int C, int R, bool SC, int EP, bool LN = false>
+template <int NTW, int C, int R, bool SC, int EP>
 int launch_ring(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                 float* os, int M, int N, int K, int Mpad, hipStream_t st, int S, int KTC) {
   const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_ring_kernel<NTW, C, R, SC, EP, LN>), dim3((NTt + NTW - 1) / NTW * S), dim3(256), 0, st,
+  hipLaunchKernelGGL((w8a8_gemv_ring_kernel<NTW, C, R, SC, EP>), dim3((NTt + NTW - 1) / NTW * S), dim3(256), 0, st,
                      (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S,
                      KTC);
   return (int)hipGetLastError();
 }
 
-// Ring kernel for 65-128 rows: NTW sized for ~256 workgroups (one per CU), k-tiles per stage and
-// ring depth for ~110-130 KiB of LDS-DMA in flight.  -1: no ring kernel for this call.
+// Ring kernels for 65-128 rows (geometries measured with tools/bench_ops.py --only ring):
+//  * grouped-scale split-K (o / down): ring2 with 8 compute waves (two per SIMD: the per-k-tile
+//    fold issues beside the partner's MFMAs), 2 weight + 2 activation loader waves, >= 4 stages
+//    per slice (down, K = 11008: 22.4 -> 20.1 us against the one-ring kernel);
+//  * qkv-like EPI_OUT (3 tiles) and the quantising GLU (8 tiles = one 64-feature group): ring2
+//    with dedicated weight loaders (the 2-lane bench 32.0k against 28.3k tok/s in round 2);
+//  * per-token-scaled split-K and the remaining shapes: the one-ring kernel (NTW for ~256 WGs).
+// -1: no ring kernel for this call.
 template <int EP>
 int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                         float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
   if (!g_gemv_ring || M <= 64 || M > 128 || K % 64 != 0 || (K / 64) % S != 0 || (EP == EPI_PART) != (S > 1)) return -1;
-  // decoupled-depth form, grouped-scale split-K (o / down): >= 4 stages per slice
+  const int NTt = (N + 15) / 16;
   if constexpr (EP == EPI_PART) {
-    if (g_gemv_ring == 2 && scaled && K % 128 == 0 && K / 128 >= 4 * S && Mpad >= 4 && Mpad % 4 == 0) {
-      const int NTt = (N + 15) / 16;
-#define R2S(NTWV, NWLV, RWV, RAV)                                                                                    \
-  do {                                                                                                           \
-    if (!g_w_nt) {                                                                                             \
-      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPI_PART, true, true, false>),          \
-                         dim3((NTt + NTWV - 1) / NTWV * S), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, \
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);          \
-      return (int)hipGetLastError();                                                                           \
-    }                                                                                                          \
-    hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPI_PART, true, true>),                     \
-                       dim3((NTt + NTWV - 1) / NTWV * S), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa,   \
-                       (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);            \
-    return (int)hipGetLastError();                                                                             \
-  } while (0)
-      // measured at M = 128 (tools/bench_ops.py --only ring): down (K = 11008) 22.4 -> 20.1 us with
-      // (4, 4, 8, 4).  o (K = 4096, 8 stages per slice) is 11.6 us LDS-staged and 12.0 here alone,
-      // but the 2-lane bench with o / down / qkv / gate_up all on ring2 (this geometry, no k
-      // rotation for qkv / gate_up) measured 32.9-33.4k against 32.2-32.4k tok/s (interleaved
-      // A/B, profiles/bench_ring2_cfg_ab_r2.jsonl).  cfg 7: o back on the LDS-staged kernel.
-      // cfg 0: 8 compute waves (two per SIMD) with 2 weight + 2 activation loader waves, the form
-      // that measured fastest at 256 rows (the fold issues beside the partner wave's MFMAs)
-      if (g_ring2_cfg == 0 && g_w_nt) {
-        hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<4, 2, 8, 4, EPI_PART, true, true, true, 1, 2, 8>),
-                           dim3((NTt + 3) / 4 * S), dim3(12 * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,
-                           (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);
-        return (int)hipGetLastError();
-      }
-      if (g_ring2_cfg == 0 || g_ring2_cfg == 1 || (g_ring2_cfg == 7 && K >= 8192)) R2S(4, 4, 8, 4);
-      if (g_ring2_cfg == 2) R2S(4, 2, 12, 3);
-      if (g_ring2_cfg == 3) R2S(2, 2, 16, 4);
-      if (g_ring2_cfg == 4) R2S(4, 4, 12, 3);
-      if (g_ring2_cfg == 5) R2S(4, 4, 6, 6);            // deeper activation ring (short o slices)
-      if (g_ring2_cfg == 6) R2S(4, 4, 5, 7);
-#undef R2S
+    if (scaled && K % 128 == 0 && K / 128 >= 4 * S && Mpad >= 4 && Mpad % 4 == 0) {
+      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<4, 2, 8, 4, EPI_PART, true, true, true, 1, 2, 8>),
+                         dim3((NTt + 3) / 4 * S), dim3(12 * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,
+                         (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);
+      return (int)hipGetLastError();
     }
   }
-  // decoupled-depth form (ring2): qkv-like EPI_OUT with 3 tiles per workgroup, quantising GLU
-  if (g_gemv_ring == 2 && !scaled && S == 1 && K % 128 == 0) {
-    const int NTt = (N + 15) / 16;
-#define R2(NTWV, NWLV, RWV, RAV, EPV)                                                                            \
-  do {                                                                                                           \
-    if (!g_w_nt) {                                                                                             \
-      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, true, false, false>),              \
-                         dim3((NTt + NTWV - 1) / NTWV), dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa,    \
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, 1);          \
-      return (int)hipGetLastError();                                                                           \
-    }                                                                                                          \
-    if (g_ring2_rot == 0) {                                                                                    \
-      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false>), dim3((NTt + NTWV - 1) / NTWV), \
-                         dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,            \
-                         (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, 1);                                 \
-      return (int)hipGetLastError();                                                                           \
-    }                                                                                                          \
-    hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV>), dim3((NTt + NTWV - 1) / NTWV),     \
-                       dim3((4 + NWLV) * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,              \
-                       (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, 1);                                   \
-    return (int)hipGetLastError();                                                                             \
-  } while (0)
+  if (!scaled && S == 1 && K % 128 == 0) {
     if constexpr (EP == EPI_GLUQ) {
       if (N % 128 == 0) {
-        if (g_ring2_cfg == 3) R2(8, 4, 6, 3, EPI_GLUQ);       // the first default (27.6 us)
-        if (g_ring2_cfg == 2) R2(8, 4, 4, 5, EPI_GLUQ);
-        R2(8, 4, 5, 4, EPI_GLUQ);
+        hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<8, 4, 5, 4, EPI_GLUQ, false>), dim3((NTt + 7) / 8), dim3(8 * 64), 0,
+                           st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt,
+                           Mpad, 1);
+        return (int)hipGetLastError();
       }
     } else if constexpr (EP == EPI_OUT) {
-      if (g_ring2_cfg == 4) R2(3, 3, 16, 3, EPI_OUT);      // the first default (18.3-19.0 us)
-      if (g_ring2_cfg == 2) R2(3, 6, 16, 3, EPI_OUT);
-      if (g_ring2_cfg == 3) R2(4, 4, 11, 4, EPI_OUT);
-      R2(3, 3, 14, 4, EPI_OUT);
+      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<3, 3, 14, 4, EPI_OUT, false>), dim3((NTt + 2) / 3), dim3(7 * 64), 0,
+                         st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt,
+                         Mpad, 1);
+      return (int)hipGetLastError();
     }
-#undef R2
   }
-  // per-(token, 64) scales (o / down): the per-k-tile fold serialises the MFMAs and the ring form
-  // measured slower than the LDS-staged kernel (o + down 24.8 us avg vs 12.1 / 22.3): off
+  // per-(token, 64) scales with a short K: the per-k-tile fold serialises the MFMAs and the ring
+  // form measured slower than the LDS-staged kernel (o + down 24.8 us avg vs 12.1 / 22.3): off
   if (scaled) return -1;
-  const int KTC = K / 64 / S, NTt = (N + 15) / 16;
-  if (g_gemv_ring == 3 && KTC % 2 == 0) {            // whole-line activation pieces
-    if constexpr (EP == EPI_GLUQ) {
-      if (N % 128 != 0) return -1;
-      return launch_ring<8, 2, 4, false, EPI_GLUQ, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-    } else {
-      const int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : max(1, min(4, (NTt * S + 128) / 256));
-      if (ntw == 1) return launch_ring<1, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-      if (ntw == 2) return launch_ring<2, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-      if (ntw == 3) return launch_ring<3, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-      return launch_ring<4, 2, 6, false, EP, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-    }
-  }
+  const int KTC = K / 64 / S;
   if constexpr (EP == EPI_GLUQ) {
-    if (scaled || N % 128 != 0) return -1;
+    if (N % 128 != 0) return -1;
     return launch_ring<8, 1, 8, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
   } else {
     const int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : max(1, min(4, (NTt * S + 128) / 256));
-#define RG(NTWV)                                                                                                      if (ntw == NTWV)                                                                                                      return scaled ? launch_ring<NTWV, 2, 5, true, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC)                        : launch_ring<NTWV, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-    RG(1) RG(2) RG(3) RG(4)
-#undef RG
+    if (ntw == 1) return launch_ring<1, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+    if (ntw == 2) return launch_ring<2, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+    if (ntw == 3) return launch_ring<3, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
+    return launch_ring<4, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
   }
-  return -1;
 }
 
 // 129-256 rows (one 256-row decode micro-batch): ring2 with the rows cut in two halves that stream
 // the same weight panel on one XCD (MS = 2), so a decode step reads every weight from HBM once for
 // all 256 sequences instead of once per 128-row lane, and with dedicated activation-loader waves.
-// Tiles per workgroup are chosen for ~256 launched workgroups (the logical grid doubles).
-// cfg (EDGELLM_TUNE=ring2_256=c[,nt]): A/B geometries; nt = 0 (cfg 0 only) selects normal weight
-// allocation instead of nontemporal (1-4 % slower at M = 256).  -1: no kernel for this call.
-static int g_r256_cfg = 0, g_r256_nt = 1, g_r256_diag = 0, g_r256_magic = 1, g_r256_rst = 1;
-template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, bool NTV, int NCWV = 4, int DTV = 0>
+// Tiles per workgroup are chosen for ~256 launched workgroups (the logical grid doubles); weights
+// stream nontemporal (1-4 % ahead of normal allocation at M = 256).  -1: no kernel for this call.
+// Geometries measured with tools/bench_ops.py --only rows256 (profiles/bench_ops_r3_rows256*.json):
+//  * split-K (o / down, >= 4 stages per slice): 8 compute waves (two per SIMD: the grouped-scale
+//    fold issues beside the partner's MFMAs: o 17.4 -> 14.9 us, down 34.8 -> 28.9), 2 + 2 loaders,
+//    4 tiles for o-like N (128 logical at 2 slices), 8 for down (N 4096, 4 slices); grouped scales
+//    fold with one VALU per element (DT = 2, magic-number bias);
+//  * quantising gate_up: one round of 16-tile workgroups, 8 compute waves each owning one
+//    64-feature group (43.7 -> 34.7 us against two rounds of 8-tile ones);
+//  * qkv-like EPI_OUT: 3 tiles for N <= 8192, 6 for qkv-sized N, 8 beyond.
+static int g_r256_diag = 0, g_r256_rot = 0;
+template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, int NCWV = 4, int DTV = 0>
 int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
                 int M, int N, int K, int Mpad, hipStream_t st, int S) {
   const int NTt = (N + 15) / 16, G = (NTt + NTWV - 1) / NTWV * S;
-  // restaged 16-B store epilogue (int8 operands, bf16 or quantised-GLU outputs, N % 16 == 0)
-  if constexpr (DTV == 0 && !SCV && (EPV == EPI_OUT || EPV == EPI_GLUQ)) {
-    if (g_r256_rst && N % 16 == 0) {
-      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV, DTV, true>),
-                         dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
-      return (int)hipGetLastError();
-    }
+  // A/B: k order rotated per workgroup (the 32 CUs of an XCD then do not request the same
+  // activation lines at the same moment)
+  if (g_r256_rot) {
+    hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, true, SCV, true, 2, NALV, NCWV, DTV>),
+                       dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
+                       (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
+    return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, NTV, 2, NALV, NCWV, DTV>),
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, true, 2, NALV, NCWV, DTV>),
                      dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
   return (int)hipGetLastError();
@@ -2038,69 +2107,24 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
                    float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
   if (M <= 128 || M > 256 || K % 128 != 0 || (EP == EPI_PART) != (S > 1) || (scaled && EP != EPI_PART)) return -1;
   const int NTt = (N + 15) / 16;
-  // (tiles, weight loaders, weight slots, activation slots, activation loaders); cfg 0 may flip the
-  // weight cache policy (nt knob), the A/B configs run nontemporal
-#define R256(NTWV, NWLV, RWV, RAV, NALV, SCV)                                                                    \
-  return g_r256_nt || g_r256_cfg ? launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, SCV, true>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S) \
-                                 : launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, SCV, false>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S)
-  // 8 waves (4 compute, 2 weight loaders, 2 activation loaders) keep 256 VGPRs per wave: the
-  // 10-wave form (4 weight loaders) spilled 236 B/lane at 8 tiles with grouped scales, and the
-  // spill traffic broke the loader waves' counted vmcnt (non-deterministic slices)
-  const int c = g_r256_cfg;
   if constexpr (EP == EPI_PART) {
-    // split-K (o / down; grouped scales from the fused producers, or per token): >= 4 stages per slice
     if (K / 128 < 4 * S || (scaled && (Mpad < M || Mpad % 16 != 0))) return -1;
     const bool narrow = (NTt + 3) / 4 * S <= 160;     // o (N 4096, 2 slices): 128 logical at 4 tiles
-#define R256S(NTWV, NWLV, RWV, RAV, NALV) \
-  do { if (scaled) R256(NTWV, NWLV, RWV, RAV, NALV, true); R256(NTWV, NWLV, RWV, RAV, NALV, false); } while (0)
-#define R256S8(NTWV, NWLV, RWV, RAV, NALV)                                                                       \
-  do {                                                                                                        \
-    if (scaled && g_r256_magic) return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, true, true, 8, 2>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
-    if (scaled) return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, true, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
-    return launch_r256<NTWV, NWLV, RWV, RAV, NALV, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S); \
-  } while (0)
-    // 8 compute waves (two per SIMD): the grouped-scale fold issues beside the partner's MFMAs
-    // (tools/bench_ops.py --only rows256, M = 256: o 17.4 -> 14.9 us, down 34.8 -> 28.9 us)
-    if (narrow) {
-      if (c == 1) R256S(4, 2, 8, 4, 2);              // 4 compute waves
-      if (c == 2) R256S(4, 4, 8, 4, 0);
-      if (c == 3) R256S(4, 2, 6, 6, 2);
-      R256S8(4, 2, 8, 4, 2);
-    }
-    if (c == 1) R256S(8, 2, 5, 4, 2);                 // down (N 4096, 4 slices): 128 logical at 8 tiles
-    if (c == 2) R256S(8, 4, 5, 4, 0);
-    if (c == 3) R256S(8, 2, 4, 5, 2);
-    R256S8(8, 2, 5, 4, 2);
-#undef R256S8
-#undef R256S
+    if (narrow)
+      return scaled ? launch_r256<4, 2, 8, 4, 2, EP, true, 8, 2>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S)
+                    : launch_r256<4, 2, 8, 4, 2, EP, false, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
+    return scaled ? launch_r256<8, 2, 5, 4, 2, EP, true, 8, 2>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S)
+                  : launch_r256<8, 2, 5, 4, 2, EP, false, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
   } else if constexpr (EP == EPI_GLUQ) {
     if (N % 128 != 0 || scaled) return -1;
-    if (c == 1) R256(8, 2, 5, 4, 1, false);
-    if (c == 2) R256(8, 4, 5, 4, 0, false);
-    if (c == 3) R256(8, 2, 4, 5, 2, false);
-    if (c == 5) R256(8, 2, 5, 4, 2, false);           // the two-round form below
-    // one round: 16 tiles per workgroup (gate_up N 22016 at 8 tiles = 344 launched workgroups = 2
-    // rounds; a quant group is 8 tiles) = 172 workgroups, 8 compute waves each owning one group
-    // (tools/bench_ops.py --only rows256, M = 256: gate_up 43.7 -> 34.7 us)
-    if (NTt % 16 == 0) return launch_r256<16, 2, 3, 3, 2, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
-    R256(8, 2, 5, 4, 2, false);
+    if (NTt % 16 == 0) return launch_r256<16, 2, 3, 3, 2, EP, false, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
+    return launch_r256<8, 2, 5, 4, 2, EP, false>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
   } else {
     if (scaled || S != 1) return -1;
-    // ~128 logical workgroups (256 launched): 3 tiles for N <= 6144, 6 for qkv-sized N
-    if (NTt <= 512) {
-      if (c == 2) R256(3, 3, 14, 4, 0, false);
-      R256(3, 2, 14, 4, 2, false);
-    }
-    if (c == 4) R256(8, 2, 5, 4, 2, false);
-    if (NTt <= 1024) {
-      if (c == 1) return launch_r256<6, 2, 7, 4, 2, EP, false, true, 8>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
-      if (c == 2) R256(6, 4, 7, 4, 0, false);
-      if (c == 3) R256(6, 2, 6, 5, 2, false);
-      R256(6, 2, 7, 4, 2, false);
-    }
-    R256(8, 2, 5, 4, 2, false);
+    if (NTt <= 512) return launch_r256<3, 2, 14, 4, 2, EP, false>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
+    if (NTt <= 1024) return launch_r256<6, 2, 7, 4, 2, EP, false>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
+    return launch_r256<8, 2, 5, 4, 2, EP, false>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
   }
-#undef R256
   return -1;
 }
 
@@ -2109,22 +2133,12 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
 // whole, and K = 4096 / 11008 / 14336 in 4 split-K slices); -1 = no kernel for this shape.
 }  // namespace
 
-extern "C" void edge_w8a8_rows256_cfg(int cfg, int nt) { g_r256_cfg = cfg; g_r256_nt = nt; }
 extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
-extern "C" void edge_w8a8_rows256_rst(int v) { g_r256_rst = v; }
-// grouped-scale fold of the 256-row split-K kernels: 1 = one-VALU magic-number form, 0 = cvt + fma
-extern "C" void edge_w8a8_rows256_magic(int v) { g_r256_magic = v; }
-// split-K slices the 129-256-row kernels use for a K (0: none)
-// tune "ring2_256_splits=short[,long]": slices for K < 8192 (o-like) and K >= 8192 (down-like), A/B;
-// fewer slices also cut the fp32 partial bytes the next RMSNorm reads
-static int g_r256_split_short = 2, g_r256_split_long = 4;
-extern "C" void edge_w8a8_rows256_splits_cfg(int s, int l) {
-  g_r256_split_short = s == 4 ? 4 : 2;
-  g_r256_split_long = l == 2 || l == 8 ? l : 4;
-}
-extern "C" int edge_w8a8_rows256_splits(int K) {
-  return K % 128 != 0 ? 0 : (K / 128 >= 64 ? g_r256_split_long : g_r256_split_short);
-}
+extern "C" void edge_w8a8_rows256_rot(int v) { g_r256_rot = v; }
+// split-K slices the 129-256-row kernels use for a K (0: none): 2 for o-like K, 4 for down-like K
+// (fewer slices also cut the fp32 partial bytes the next RMSNorm reads;
+// profiles/bench_r3_down_splits_ab.jsonl, bench_r3_i8_o_splits_ab.jsonl)
+extern "C" int edge_w8a8_rows256_splits(int K) { return K % 128 != 0 ? 0 : (K / 128 >= 64 ? 4 : 2); }
 // whether the 129-256-row decode kernels take this K (whole K; split-K at rows256_splits(K))
 extern "C" int edge_w8a8_rows256_ok(int K) { return K % 128 == 0 && K / 128 >= 8; }
 
@@ -2333,6 +2347,12 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     // the ring's counted vmcnt — the same hazard that broke a decode kernel — so it is gone.)
     const int grid_n = (NTt * 16 + 255) / 256;
     const int grid_m = (M + 127) / 128;
+    if (g_prefill_x32 && M >= 256 && ((M + 255) / 256) * grid_n >= 192) {
+      const int gm2 = (M + 255) / 256;
+      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+      return (int)hipGetLastError();
+    }
 #define BIGK(BMV, ISS)                                                                                           \
   hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
@@ -2402,6 +2422,12 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
   const int NTt = (N + 15) / 16;
   const int grid_n = (NTt * 16 + 255) / 256;
   const int grid_m = (M + 127) / 128;
+  if (g_prefill_x32 && M >= 256 && ((M + 255) / 256) * grid_n >= 192) {
+    const int gm2 = (M + 255) / 256;
+    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
+                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+    return (int)hipGetLastError();
+  }
   if (g_prefill_prio)
     hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
                        (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
@@ -2413,6 +2439,23 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
   return (int)hipGetLastError();
 }
 
+// bf16 prefill GEMM y = x . W^T (+ bias) on the x32 kernel: x bf16 [M, K] row-major, W fragment-packed
+// bf16 (ops.pack_bf16_weight), M >= 256, K % 64 == 0, N % 16 == 0.  -2: not taken (the caller runs
+// hipBLASLt); g_bf16_x32 0 turns it off (A/B knob "bf16_x32").
+static int g_bf16_x32 = 1;
+extern "C" void edge_bf16_x32_cfg(int v) { g_bf16_x32 = v; }
+extern "C" int edge_gemm_bf16_x32(const void* A, const void* W, const void* bias, void* out, int M, int N, int K,
+                                  hipStream_t st) {
+  if (!g_bf16_x32 || M < 256 || K % 64 != 0 || K <= 0 || N % 16 != 0) return -2;
+  const int Kb = 2 * K, KT = Kb / 64, NTt = N / 16;
+  const int grid_n = (N + 255) / 256, grid_m = (M + 255) / 256;
+  if ((int64_t)grid_m * grid_n < 192 || (int64_t)M * Kb >= ((int64_t)1 << 32)) return -2;
+  hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 1>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A,
+                     nullptr, (const int8_t*)W, nullptr, (const bf16_t*)bias, (bf16_t*)out, M, N, Kb, KT, NTt, grid_m,
+                     grid_n);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------ bf16 ring2
 // bf16 decode projections at 17-256 rows on the ring2 kernel (DT = 1).  The bf16 fragment-packed
 // weight (ops.pack_bf16_weight: 1 KiB tiles of 16 rows x 32 k) and a row-major bf16 activation
@@ -2421,14 +2464,9 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
 // and swaps the MFMA for v_mfma_f32_16x16x32_bf16 (same 16 cycles per 64 B of k as the i8 form).
 // Rows 129-256 run as two 128-row halves that share each weight panel through one XCD's L2
 // (MS = 2), so a 256-row decode step reads the bf16 weights from HBM once.
-// cfg (EDGELLM_TUNE=bf16_ring=c[,max_rows]): 0 automatic, 1-3 alternative geometries (A/B);
-// max_rows: the bf16 ring path takes 17..max_rows rows (0 -> 256).
-// Default row floor 65: at 17-64 rows the ring kernel still computes 128-row tiles and re-reads
-// the (clamped) activation lines, and hipBLASLt is ahead on qkv / gate_up (LM-head-wide N excepted:
-// edge_bf16_ring_min_rows_for)
-static int g_bfr_cfg = 0, g_bfr_min = 65;
-extern "C" void edge_bf16_ring_cfg(int cfg, int min_rows) { g_bfr_cfg = cfg; g_bfr_min = min_rows > 0 ? min_rows : 65; }
-extern "C" int edge_bf16_ring_min_rows() { return g_bfr_min; }
+// Row floor 65: at 17-64 rows the ring kernel still computes 128-row tiles and re-reads the
+// (clamped) activation lines, and hipBLASLt is ahead on qkv / gate_up.
+extern "C" int edge_bf16_ring_min_rows() { return 65; }
 
 namespace {
 template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int NCWV, int EPV, int MSV>
@@ -2437,14 +2475,14 @@ int launch_bfr(const void* A, const void* W, const void* bias, void* out, int M,
   const dim3 grid(MSV == 2 ? (G + 7) / 8 * 16 : G);
   hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, false, true, MSV, NALV, NCWV, 1>), grid,
                      dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, nullptr, (const int8_t*)W, nullptr,
-                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G, g_r256_diag & ~255);
+                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G, 0);
   return (int)hipGetLastError();
 }
 
 template <int MSV>
 int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi, int S,
                  hipStream_t st) {
-  const int NTt = N / 16, c = g_bfr_cfg;
+  const int NTt = N / 16;
   // logical workgroups wanted: ~256 launched blocks (MS = 2 launches each logical workgroup twice)
   const int want = MSV == 2 ? 128 : 256;
 #define BFR(NTWV, NWLV, RWV, RAV, NALV, NCWV, EPV) \
@@ -2454,24 +2492,18 @@ int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int 
     // bf16ring, Llama-2-7B gate_up at 256 rows: 16 tiles / 172 blocks 64.4 us, 8 tiles / 344
     // blocks 80.6 us)
     const int ft = NTt / 2;
-    if (c == 1) BFR(4, 2, 10, 4, 2, 4, EPI_GLU);
-    if (c == 2) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
-    if (c == 3) BFR(8, 2, 5, 4, 2, 4, EPI_GLU);
     if (MSV == 2 && ft >= 8 * 64) BFR(16, 2, 3, 3, 2, 8, EPI_GLU);
     if (ft >= 4 * 128) BFR(8, 2, 5, 4, 2, 4, EPI_GLU);
     BFR(4, 2, 10, 4, 2, 4, EPI_GLU);
   }
   if (epi == EPI_PART) {                              // split-K slices (o / down before the norm)
     const int per = NTt * S / want;
-    if (c == 1) BFR(2, 2, 14, 4, 2, 4, EPI_PART);
     if (per >= 6) BFR(8, 2, 5, 4, 2, 4, EPI_PART);
     if (per >= 3) BFR(4, 2, 10, 4, 2, 4, EPI_PART);
     if (per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_PART);
     BFR(1, 2, 16, 4, 2, 4, EPI_PART);
   }
   const int per = (NTt + want / 2) / want;            // EPI_OUT
-  if (c == 1 && per >= 2) BFR(2, 2, 14, 4, 2, 4, EPI_OUT);
-  if (c == 3 && per >= 7) BFR(8, 2, 5, 4, 2, 4, EPI_OUT);
   if (per >= 12) BFR(16, 2, 3, 3, 2, 8, EPI_OUT);     // LM heads: one round (32000 x 4096 at 256 rows)
   if (per >= 7) BFR(8, 2, 5, 4, 2, 4, EPI_OUT);
   if (per >= 5) BFR(6, 2, 7, 4, 2, 4, EPI_OUT);
@@ -2484,15 +2516,13 @@ int bfr_dispatch(const void* A, const void* W, const void* bias, void* out, int 
 }  // namespace
 
 // Split-K slices S for the bf16 ring path's EPI_PART at this (N, K): >= 4 stages of 64 k per slice
-static int g_bfr_splits = 0;                           // tune "bf16_ring_splits": forced S (0 = automatic)
-extern "C" void edge_bf16_ring_splits_cfg(int s) { g_bfr_splits = s; }
 extern "C" int edge_bf16_ring_splits(int N, int K) {
   const int stages = K / 64;                           // 128-B stages of bf16 k
   // fewer slices halve each workgroup's activation re-reads; narrow N takes more to fill the chip.
   // N = 4096 measured S=4 over S=2 (o 14.4 vs 15.2 us at 128 rows, down 37.5 vs 42.8 us at 256 rows;
   // +1.6 % / +3.1 % bench tok/s at 1x256 / 2x128, profiles/bench_ops_r3_bf16splits.json)
   const int NTt = N / 16;
-  int S = g_bfr_splits > 0 ? g_bfr_splits : (NTt >= 384 ? 2 : (NTt >= 64 ? 4 : 8));
+  int S = NTt >= 384 ? 2 : (NTt >= 64 ? 4 : 8);
   while (S > 1 && stages < 4 * S) --S;
   return S;
 }

@@ -100,14 +100,15 @@ def run_agents(agents: Sequence[Agent], prompts: Sequence[Sequence[str]], seeds:
     # command for all of them — agents on disjoint rank groups decode at the same time, the rest in
     # order.  Dispatch is on the engine's capability, never on its device type: co_generate drives
     # a plain Generator's internals (start / step / precapture), which a pipeline engine lacks.
-    pipe = [i for i, a in enumerate(agents) if _is_pipeline(a.generator)]
+    pipe = [i for i, a in enumerate(agents) if _is_pipeline(getattr(a, "generator", None))]
     if pipe:
         _run_pipeline_agents(agents, pipe, prompts, seeds, legacy_decode, concurrent, out)
     for i, a in enumerate(agents):
         if i in pipe:
             continue
         dev = getattr(a, "device", None)
-        if concurrent and _is_local_generator(a.generator) and isinstance(dev, torch.device) and dev.type == "cuda":
+        if concurrent and _is_local_generator(getattr(a, "generator", None)) and isinstance(dev, torch.device) \
+                and dev.type == "cuda":
             if dev not in shared:
                 shared[dev] = []
                 units.append(shared[dev])

@@ -498,7 +498,7 @@ def test_bf16_model_split_k_decode_matches_unsplit(cuda):
 RING_DEFAULT = 2     # gemm_i8.hip g_gemv_ring
 
 
-@pytest.mark.parametrize("ring", [1, 2, 3])
+@pytest.mark.parametrize("ring", [2])
 @pytest.mark.parametrize("M", [65, 100, 128])
 @pytest.mark.parametrize("N,K,S", [(12288, 4096, 1), (6144, 4096, 1), (4096, 4096, 4), (4096, 11008, 4),
                                    (12304, 4096, 1)])
@@ -528,7 +528,7 @@ def test_gemv_ring_matches_ldsa(cuda, ring, M, N, K, S):
     assert torch.equal(ring_out, old)
 
 
-@pytest.mark.parametrize("ring", [1, 2, 3])
+@pytest.mark.parametrize("ring", [2])
 @pytest.mark.parametrize("M", [65, 128])
 def test_gluq_ring_matches_ldsa(cuda, ring, M):
     """gate_up + SwiGLU + int8 quantisation on the ring kernel vs the LDS-staged kernel: the
@@ -553,10 +553,9 @@ def test_gluq_ring_matches_ldsa(cuda, ring, M):
     assert (q1.int() - q0.int()).abs().max() <= 1      # __expf in both; identical but for fma contraction
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M", [65, 100, 128])
 @pytest.mark.parametrize("N,K,S", [(4096, 4096, 4), (4096, 11008, 4), (1024, 14336, 4)])
-def test_ring2_grouped_splitk(cuda, cfg, M, N, K, S):
+def test_ring2_grouped_splitk(cuda, M, N, K, S):
     """o / down at 65-128 rows: the decoupled-depth ring kernel with per-(token, 64) scales folded
     per k-tile and split-K slices on stage boundaries, vs the LDS-staged kernel (slices on k-tile
     boundaries: the slice sums agree to fp32 rounding) and the fp32 reference."""
@@ -571,14 +570,12 @@ def test_ring2_grouped_splitk(cuda, cfg, M, N, K, S):
     wp = ops.pack_int8_weight(w)
     try:
         C.tune("gemv_ring", 2, 0)
-        C.tune("ring2_cfg", cfg, 1)
         p2 = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
         again = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
         C.tune("gemv_ring", 0, 0)
         p0 = C.w8a8_gemm_splitk(qx, sx, wp, sw, bias, N, K, S)
     finally:
         C.tune("gemv_ring", RING_DEFAULT, 0)
-        C.tune("ring2_cfg", 0, 0)
     assert torch.equal(p2, again)                      # deterministic
     s2, s0 = p2.sum(0), p0.sum(0)
     assert (s2 - s0).abs().max().item() <= 1e-4 * s0.abs().max().item() + 1e-5

@@ -1,0 +1,35 @@
+"""Prefill INT8 GEMM on v_mfma_i32_32x32x32_i8 (gemm_i8.hip ``w8a8_gemm_x32_kernel``, 256 x 256
+block tiles, tune "prefill_x32") against the fp32 reference op, row-major and fragment-packed A
+(the APK path at >= 2048 rows x N >= 8192), ragged M."""
+import pytest
+import torch
+
+from edgellm import ops
+from edgellm.ops import _ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M", [256, 777, 2048])
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (22016, 4096)])
+def test_prefill_x32_matches_reference(cuda, M, N, K):
+    C = ops.ext()
+    torch.manual_seed(M + N)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.01
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    try:
+        C.tune("prefill_x32", 0, 0)
+        base = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+        C.tune("prefill_x32", 1, 0)
+        out = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+    finally:
+        C.tune("prefill_x32", 0, 0)
+    # int32 sums are exact in any order: the same bits as the 16x16x64 kernel
+    assert torch.equal(out, base)
+    ref = _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32)
+    err = (out.float() - ref).abs()
+    assert (err <= 1e-2 + 1e-2 * ref.abs()).all(), err.max().item()

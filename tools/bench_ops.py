@@ -323,87 +323,14 @@ def batch1_rows(C, dev, M=1):
     return out
 
 
-def ring_rows(C, dev, Ms=(128, 96)):
-    """65-128-row decode GEMVs, cache-cold, per kernel form (tune gemv_ring: 0 LDS-staged,
-    1 one-ring LDS-DMA, 2 decoupled weight / activation depths): qkv and the quantising gate_up."""
-    out = []
-    for name, (N, K) in {"qkv": (12288, 4096), "gate_up": (22016, 4096)}.items():
-        ncopy = max(2, (1 << 30) // (N * K) + 1)
-        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
-        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
-        sw = torch.rand(N, device=dev) * 0.01
-        for M in Ms:
-            qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-            sx = torch.rand(M, device=dev) * 0.01
-            ctr = [0]
-
-            def call():
-                ctr[0] = (ctr[0] + 1) % ncopy
-                if name == "gate_up":
-                    return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
-                return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
-
-            res = {}
-            # (form, ring2 config, k rotation): form 0 LDS-staged, 1 one-ring, 3 one-ring + whole
-            # activation lines, 2 decoupled depths + whole lines (ring2)
-            forms = [(0, 0, 1), (1, 0, 1), (3, 0, 1), (2, 0, 0), (2, 0, 1), (2, 1, 0), (2, 1, 1), (2, 2, 1)]
-            for rnd in range(3):
-                for form, cfg, rot in forms:
-                    C.tune("gemv_ring", form, 0)
-                    C.tune("ring2_cfg", cfg, rot)
-                    res.setdefault(form * 100 + cfg * 10 + rot, []).append(timeit(call, iters=10, per_graph=ncopy))
-            C.tune("gemv_ring", 2, 0)
-            C.tune("ring2_cfg", 0, 0)
-            row = dict(op="w8a8_rows128", shape=name, M=M, N=N, K=K)
-            for form, ts in res.items():
-                row[f"ring{form}_us"] = round(min(ts), 2)
-                row[f"ring{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
-            out.append(row)
-            print(row, flush=True)
-        del wps
-    # o / down: per-(token, 64) activation scales, split-K S = 4 fp32 slices (form 0 LDS-staged,
-    # form 2 ring2 with the scale ring, configs 0-3)
-    for name, (N, K) in {"o": (4096, 4096), "down": (4096, 11008)}.items():
-        ncopy = max(2, (1 << 30) // (N * K) + 1)
-        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
-        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
-        sw = torch.rand(N, device=dev) * 0.01
-        for M in Ms:
-            qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-            sx = torch.rand(K // 64, (M + 15) // 16 * 16, device=dev) * 0.01
-            ctr = [0]
-
-            def call():
-                ctr[0] = (ctr[0] + 1) % ncopy
-                return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, 4)
-
-            res = {}
-            for rnd in range(3):
-                for form, cfg in [(0, 0), (2, 0), (2, 1), (2, 2), (2, 3), (2, 4)]:
-                    C.tune("gemv_ring", form, 0)
-                    C.tune("ring2_cfg", cfg, 1)
-                    res.setdefault(form * 100 + cfg * 10 + 1, []).append(timeit(call, iters=10, per_graph=ncopy))
-            C.tune("gemv_ring", 2, 0)
-            C.tune("ring2_cfg", 0, 0)
-            row = dict(op="w8a8_rows128_grouped_splitk4", shape=name, M=M, N=N, K=K)
-            for form, ts in res.items():
-                row[f"ring{form}_us"] = round(min(ts), 2)
-                row[f"ring{form}_TBps"] = round(N * K / min(ts) / 1e6, 2)
-            out.append(row)
-            print(row, flush=True)
-        del wps
-    return out
-
-
 def rows256_rows(C, dev, M=256):
     """One 256-row decode micro-batch (row-split ring2, weights read once) against two 128-row
-    launches (the 2-lane form, weights read twice), cache-cold, every launcher geometry
-    (tune ring2_256 = cfg, nt) timed interleaved: qkv, o / down (grouped scales, split-K) and the
-    quantising gate_up."""
+    launches (the 2-lane form, weights read twice), cache-cold: qkv, o / down (grouped scales,
+    split-K) and the quantising gate_up."""
     out = []
     shapes = {"qkv": (12288, 4096, "out"), "o": (4096, 4096, "part"), "gate_up": (22016, 4096, "gluq"),
               "down": (4096, 11008, "part"), "o_token": (4096, 4096, "part_tok"),
-              "down_token": (4096, 11008, "part_tok"), "gate_up_bf16out": (22016, 4096, "out")}
+              "down_token": (4096, 11008, "part_tok")}
     for name, (N, K, kind) in shapes.items():
         ncopy = max(2, (1 << 30) // (N * K) + 1)
         w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
@@ -426,13 +353,9 @@ def rows256_rows(C, dev, M=256):
             return call
 
         c256, c128 = make(M), make(M // 2)
-        forms = [(0, 1), (0, 0), (1, 1), (2, 1), (3, 1), (4, 1), (5, 1)]
         res = {}
         for rnd in range(3):
-            for cfg, nt in forms:
-                C.tune("ring2_256", cfg, nt)
-                res.setdefault(f"r256_c{cfg}_nt{nt}", []).append(timeit(c256, iters=10, per_graph=ncopy))
-            C.tune("ring2_256", 0, 1)
+            res.setdefault("r256", []).append(timeit(c256, iters=10, per_graph=ncopy))
             res.setdefault("two_x128", []).append(2 * timeit(c128, iters=10, per_graph=ncopy))
         row = dict(op="w8a8_rows256", shape=name, M=M, N=N, K=K, weight_MB=round(N * K / 1e6, 1))
         for form, ts in res.items():
@@ -442,7 +365,6 @@ def rows256_rows(C, dev, M=256):
         print(row, flush=True)
         del wps
     return out
-
 
 def rows256_diag(C, dev, M=256):
     """Where a 256-row decode GEMM's time goes: the same launch with parts of the ring switched off
@@ -515,7 +437,7 @@ def bf16_rows(C, dev, Ms=(8, 16, 32, 48, 64)):
 
 def bf16_ring_rows(C, dev, Ms=(32, 64, 128, 256)):
     """bf16 decode projections at 17-256 rows (Llama-2-7B shapes), cache-cold: the bf16 ring GEMM
-    (gemm_i8.hip ring2 kernel in bf16 operand mode; geometry cfg 0 / 1 / 2 interleaved) against
+    (gemm_i8.hip ring2 kernel in bf16 operand mode) interleaved with
     hipBLASLt (torch.nn.functional.linear; gate_up + the SwiGLU kernel) and, up to 64 rows, the
     gemv_bf16.hip GEMV.  o / down are timed in their split-K form (fp32 slices for the norm)."""
     out = []
@@ -545,10 +467,7 @@ def bf16_ring_rows(C, dev, Ms=(32, 64, 128, 256)):
 
             res = {}
             for _ in range(2):
-                for cfg in (0, 1, 2, 3):
-                    C.tune("bf16_ring", cfg, 0)
-                    res.setdefault(f"ring_c{cfg}", []).append(timeit(ring, iters=10, per_graph=ncopy))
-                C.tune("bf16_ring", 0, 0)
+                res.setdefault("ring", []).append(timeit(ring, iters=10, per_graph=ncopy))
                 res.setdefault("hipblaslt", []).append(timeit(blas, iters=10, per_graph=ncopy))
                 if M <= 64:
                     res.setdefault("gemv", []).append(timeit(gemv, iters=10, per_graph=ncopy))
@@ -625,41 +544,6 @@ def prio_rows(C, dev):
     return out
 
 
-def magic_rows(C, dev, M=256):
-    """Grouped-scale fold A/B at 256 rows (o / down split-K, interleaved): ring2_256_magic 1 (one
-    v_fmac per element on a magic-number-biased MFMA result) vs 0 (cvt + fma); plus the largest
-    difference between the two outputs relative to the output's scale."""
-    out = []
-    shapes = {"o": (4096, 4096), "down": (4096, 11008)}
-    for name, (N, K) in shapes.items():
-        ncopy = max(2, (1 << 30) // (N * K) + 1)
-        ws = [ops.pack_int8_weight(torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)) for _ in range(ncopy)]
-        s2 = torch.rand(N, device=dev) * 0.01
-        a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-        sg = torch.rand(K // 64, M, device=dev) * 0.01
-        ctr = [0]
-
-        def call():
-            ctr[0] = (ctr[0] + 1) % ncopy
-            return C.w8a8_gemm_splitk(a, sg, ws[ctr[0]], s2, None, N, K, 0)
-        res = {}
-        for _ in range(3):
-            for mg in (1, 0):
-                C.tune("ring2_256_magic", mg, 0)
-                res.setdefault(mg, []).append(timeit(call, iters=10, per_graph=ncopy))
-        outs = {}
-        for mg in (1, 0):
-            C.tune("ring2_256_magic", mg, 0)
-            outs[mg] = C.w8a8_gemm_splitk(a, sg, ws[0], s2, None, N, K, 0).sum(0)
-        C.tune("ring2_256_magic", 1, 0)
-        err = ((outs[1] - outs[0]).abs().max() / outs[0].abs().max()).item()
-        row = dict(op="rows256_fold", shape=name, M=M, N=N, K=K, magic_us=round(min(res[1]), 2),
-                   exact_us=round(min(res[0]), 2), max_rel_diff=err)
-        out.append(row)
-        print(row, flush=True)
-    return out
-
-
 def knob_ab_rows(C, dev, knob, values=(1, 0), M=256, shapes=None):
     """A/B of one tuning knob (``tune knob=v``) on the 256-row decode GEMMs, interleaved rounds,
     cache-cold weights; also checks that every setting gives the same output bits as the first."""
@@ -708,31 +592,32 @@ def knob_ab_rows(C, dev, knob, values=(1, 0), M=256, shapes=None):
     return out
 
 
-def bf16_splits_rows(C, dev, Ms=(128, 256)):
-    """bf16 ring split-K slice count for o / down (tune bf16_ring_splits), interleaved."""
+def x32_rows(C, dev, Ms=(2048, 16384)):
+    """Prefill INT8 GEMM: the 256 x 256 v_mfma_i32_32x32x32_i8 kernel (tune prefill_x32 1) against
+    the default 128 x 256 16x16x64 kernel, interleaved, Llama-2-7B shapes."""
     out = []
-    for name, (N, K) in {"o": (4096, 4096), "down": (4096, 11008)}.items():
-        ncopy = max(2, (1 << 30) // (2 * N * K) + 1)
-        wps = [ops.pack_bf16_weight((torch.randn(N, K, device=dev) * 0.02).bfloat16()) for _ in range(ncopy)]
+    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
+    for name, (N, K) in shapes.items():
+        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
+        wp = ops.pack_int8_weight(w)
+        s2 = torch.rand(N, device=dev) * 0.01
         for M in Ms:
-            x = torch.randn(M, K, device=dev).bfloat16()
-            ctr = [0]
+            a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            s1 = torch.rand(M, device=dev) * 0.01
             res = {}
-            for _ in range(2):
-                for S in (2, 4, 8):
-                    if K // 64 < 4 * S:
-                        continue
-
-                    def call():
-                        ctr[0] = (ctr[0] + 1) % ncopy
-                        return C.gemm_bf16_ring(x, wps[ctr[0]], None, N, 3, S)
-                    res.setdefault(S, []).append(timeit(call, iters=10, per_graph=ncopy))
-            row = dict(op="bf16_ring_splits", shape=name, M=M, N=N, K=K)
-            for S, ts in res.items():
-                row[f"S{S}_us"] = round(min(ts), 2)
+            per = max(2, min(20, int(4e11 // (M * N * K))))
+            for _ in range(3):
+                for v in (0, 1):
+                    C.tune("prefill_x32", v, 0)
+                    res.setdefault(v, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K), iters=5,
+                                                        per_graph=per))
+            C.tune("prefill_x32", 0, 0)
+            row = dict(op="w8a8_gemm_prefill_x32", shape=name, M=M, N=N, K=K)
+            for v, ts in res.items():
+                row[f"x32_{v}_us"] = round(min(ts), 1)
+                row[f"x32_{v}_TOPs"] = round(2 * M * N * K / min(ts) / 1e6, 1)
             out.append(row)
             print(row, flush=True)
-        del wps
     return out
 
 
@@ -798,21 +683,16 @@ def main():
         rows += prefill_gemm_rows(C, dev)
     if only is not None and "m1" in only:
         rows += batch1_rows(C, dev)
-    if only is not None and "ring" in only:
-        rows += ring_rows(C, dev)
     if only is not None and "rows256" in only:
         rows += rows256_rows(C, dev)
     if only is not None and "r256diag" in only:
         rows += rows256_diag(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
-    if only is not None and "bf16splits" in only:
-        rows += bf16_splits_rows(C, dev)
-    if only is not None and "rst" in only:
-        rows += knob_ab_rows(C, dev, "ring2_256_rst", shapes={"qkv": (12288, 4096, "out"),
-                                                              "gate_up": (22016, 4096, "gluq")})
-    if only is not None and "magic" in only:
-        rows += magic_rows(C, dev)
+    if only is not None and "x32" in only:
+        rows += x32_rows(C, dev)
+    if only is not None and "rot" in only:
+        rows += knob_ab_rows(C, dev, "ring2_256_rot", values=(0, 1))
     if only is not None and "prio" in only:
         rows += prio_rows(C, dev)
     if only is not None and "bf16ring" in only:
