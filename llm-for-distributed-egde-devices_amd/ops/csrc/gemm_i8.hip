@@ -1192,8 +1192,9 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
     }
   };
   // lane's byte in a 32-row operand block: piece offset ((l >> 4) & 1) KiB, lane slot
-  // (l & 15) + 32 (l >> 5) (k-step 0; k-step 1 adds 16 slots = 512 B)
-  const uint32_t lo = (((lane >> 4) & 1) << 10) + (((lane & 15) + 32 * (lane >> 5)) << 4);
+  // (l & 15) + 16 (l >> 5) = row l & 15 of the piece, 16-B k chunk l >> 5 (k-step 0; k-step 1 is
+  // chunks 2, 3: 32 slots = 512 B further)
+  const uint32_t lo = (((lane >> 4) & 1) << 10) + (((lane & 15) + 16 * (lane >> 5)) << 4);
   const uint32_t ring0 = lds_off(ring) + lo;
   const uint32_t abase = ring0 + (wm * 8) * 1024, wbase = ring0 + (AP + wn * 4) * 1024;
   // fragments of stage st, k-step ks: fa[c] = activation block c (tokens 32 c..), fw[b] = weight block b
@@ -1295,12 +1296,13 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
       const float sr = DT == 1 ? 1.f : sa[min(row, M - 1)];
       const v4i lo4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8) ^ (t & 15)) << 4));
       const v4i hi4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8 + 1) ^ (t & 15)) << 4));
+      const v4f lof = __builtin_bit_cast(v4f, lo4), hif = __builtin_bit_cast(v4f, hi4);
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if constexpr (DT == 1) {
-          v[e] = __builtin_bit_cast(float, lo4[e]) + bv[e];
-          v[e + 4] = __builtin_bit_cast(float, hi4[e]) + bv[e + 4];
+          v[e] = lof[e] + bv[e];
+          v[e + 4] = hif[e] + bv[e + 4];
         } else {
           v[e] = (float)lo4[e] * sr * swv[e] + bv[e];
           v[e + 4] = (float)hi4[e] * sr * swv[e + 4] + bv[e + 4];
