@@ -56,6 +56,7 @@ int edge_w8a8_rows256_ok(int K);
 int edge_w8a8_rows256_splits(int K);
 void edge_w8a8_rows256_diag(int v);
 void edge_w8a8_prefill_x32(int v);
+void edge_w8a8_prefill_stages(int v);
 void edge_w8a8_rows256_rot(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st, const void* add);
@@ -929,6 +930,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
     else if (what == "ring2_256_diag") edge_w8a8_rows256_diag((int)a);
     else if (what == "prefill_x32") edge_w8a8_prefill_x32((int)a);
+    else if (what == "prefill_stages") edge_w8a8_prefill_stages((int)a);
     else if (what == "bf16_x32") edge_bf16_x32_cfg((int)a);
     else if (what == "ring2_256_rot") edge_w8a8_rows256_rot((int)a);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);

@@ -913,12 +913,12 @@ __device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_r
 //    ~60 for contiguous pieces.  The LDS image is identical, only the DMA source offsets change.
 // PRIO: s_setprio(1) around each k-tile's MFMA cluster (cdna guide T5: keeps hipcc from moving the
 // MFMAs across the barriers into the fragment reads / DMA issue; A/B knob prefill_prio)
-template <int BMV, int ISS, bool APK = false, bool PRIO = false>
+template <int BMV, int ISS, bool APK = false, bool PRIO = false, int RV = 4>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                               int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
-  constexpr int R = 4, BNV = 256, NWV = 8;
+  constexpr int R = RV, BNV = 256, NWV = 8;
   constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
   constexpr int MI = BMV / 32, NJ = 4;                        // row blocks / column tiles per wave
   static_assert(PIECES % NWV == 0, "pieces per wave");
@@ -1146,12 +1146,12 @@ __global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ 
 //    in bytes, and v_mfma_f32_32x32x16_bf16 takes the same 16 B per lane (k 8 (l >> 5) .. + 8 of a
 //    16-k step) as the i8 form — so only the MFMA and the epilogue (fp32 sums + bias, no scales)
 //    change.  sa / sw are unused.
-template <bool APK, int DT = 0>
+template <bool APK, int DT = 0, int RV = 4>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                               int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
-  constexpr int R = 4, BMV = 256, BNV = 256, NWV = 8;
+  constexpr int R = RV, BMV = 256, BNV = 256, NWV = 8;
   constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
   static_assert(R * STAGE <= 160 * 1024 && NWV * 32 * 256 <= R * STAGE, "LDS budget");
   __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
@@ -1967,6 +1967,10 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2;
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel (BM = 128)
 static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0, g_prefill_x32 = 0;
+// ring depth of the prefill GEMMs (A/B): 0 = 4 stages; 6 = the 128 x 256 kernel with 6 (144 KiB),
+// 5 = the 256 x 256 x32 kernel with 5 (160 KiB)
+static int g_prefill_stages = 0;
+extern "C" void edge_w8a8_prefill_stages(int v) { g_prefill_stages = v; }
 // prefill_x32: 0 off, 1 the 256 x 256 32x32x32 kernel when the grid fills >= 1 round of CUs (M >= 256)
 extern "C" void edge_w8a8_prefill_x32(int v) { g_prefill_x32 = v; }
 extern "C" void edge_w8a8_prefill_prio(int v) { g_prefill_prio = v; }
@@ -2351,14 +2355,24 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     const int grid_m = (M + 127) / 128;
     if (g_prefill_x32 && M >= 256 && ((M + 255) / 256) * grid_n >= 192) {
       const int gm2 = (M + 255) / 256;
-      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+      if (g_prefill_stages == 5)
+        hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 0, 5>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A,
+                           sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+      else
+        hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
+                           (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
       return (int)hipGetLastError();
     }
 #define BIGK(BMV, ISS)                                                                                           \
   hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
     const int iss = g_prefill_iss;
+    if (g_prefill_stages == 6 && iss == 2 && !g_prefill_prio) {
+      hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, false, false, 6>), dim3(grid_m * grid_n), dim3(512), 0, st,
+                         (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
+                         grid_m, grid_n);
+      return (int)hipGetLastError();
+    }
     if (g_prefill_prio && iss == 2) {
       hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, false, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
                          (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
@@ -2426,11 +2440,19 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
   const int grid_m = (M + 127) / 128;
   if (g_prefill_x32 && M >= 256 && ((M + 255) / 256) * grid_n >= 192) {
     const int gm2 = (M + 255) / 256;
-    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
-                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+    if (g_prefill_stages == 5)
+      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true, 0, 5>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+    else
+      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
     return (int)hipGetLastError();
   }
-  if (g_prefill_prio)
+  if (g_prefill_stages == 6 && !g_prefill_prio)
+    hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, false, 6>), dim3(grid_m * grid_n), dim3(512), 0, st,
+                       (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
+                       grid_m, grid_n);
+  else if (g_prefill_prio)
     hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
                        (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
                        grid_m, grid_n);
@@ -2452,9 +2474,14 @@ extern "C" int edge_gemm_bf16_x32(const void* A, const void* W, const void* bias
   const int Kb = 2 * K, KT = Kb / 64, NTt = N / 16;
   const int grid_n = (N + 255) / 256, grid_m = (M + 255) / 256;
   if ((int64_t)grid_m * grid_n < 192 || (int64_t)M * Kb >= ((int64_t)1 << 32)) return -2;
-  hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 1>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A,
-                     nullptr, (const int8_t*)W, nullptr, (const bf16_t*)bias, (bf16_t*)out, M, N, Kb, KT, NTt, grid_m,
-                     grid_n);
+  if (g_prefill_stages == 5)
+    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 1, 5>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A,
+                       nullptr, (const int8_t*)W, nullptr, (const bf16_t*)bias, (bf16_t*)out, M, N, Kb, KT, NTt, grid_m,
+                       grid_n);
+  else
+    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 1>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A,
+                       nullptr, (const int8_t*)W, nullptr, (const bf16_t*)bias, (bf16_t*)out, M, N, Kb, KT, NTt, grid_m,
+                       grid_n);
   return (int)hipGetLastError();
 }
 
