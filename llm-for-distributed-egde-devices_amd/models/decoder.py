@@ -61,7 +61,6 @@ class AttnCtx:
     # are right-padded to T, so a real token never attends to a pad (causal) and the pads' cache
     # entries lie past the row's length, where decode overwrites them before any read
     last_pos: Optional[torch.Tensor] = None
-    prefetch: Optional[object] = None    # WeightPrefetcher of small-batch decode (after each qkv)
 
     def last_rows(self, device) -> torch.Tensor:
         """Flat row indices [B] of each sequence's last real token in a [B*T, H] activation."""
@@ -80,8 +79,6 @@ class Attention(nn.Module):
     def forward(self, x, ctx: AttnCtx):
         cfg = self.cfg
         qkv = self.qkv(x)                                   # [B*T, qkv]
-        if ctx.prefetch is not None:
-            ctx.prefetch.after_qkv(self.layer_idx)
         k_cache, v_cache = ctx.kv.layer(self.layer_idx)
         rot = cfg.rotary_dim if cfg.pos_emb == "rope" else 0
         if ctx.attn_hook is not None:
@@ -332,17 +329,6 @@ class DecoderLM(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward_layers(self, x: torch.Tensor, ctx: AttnCtx, residual: Optional[torch.Tensor] = None):
-        pf = WeightPrefetcher.for_step(self, ctx)
-        if pf is not None:
-            ctx.prefetch = pf
-            try:
-                return self._forward_layers(x, ctx, residual)
-            finally:
-                ctx.prefetch = None
-                pf.join()
-        return self._forward_layers(x, ctx, residual)
-
-    def _forward_layers(self, x: torch.Tensor, ctx: AttnCtx, residual: Optional[torch.Tensor] = None):
         if tracing.TRACE:                      # roctx range per layer (rocprofv3 --marker-trace)
             for layer in self.layers:
                 with tracing.trace_range(f"{ctx.mode}.layer{layer.idx}"):
@@ -388,71 +374,6 @@ class DecoderLM(nn.Module):
         if isinstance(x, PartialSum):
             x = x.materialize()
         return x + residual if residual is not None else x
-
-
-# --------------------------------------------------------------------------- weight prefetch
-# EDGELLM_PREFETCH: bit mask of the projections whose weights a small-batch decode step streams
-# into the Infinity Cache on a side stream right after each layer's qkv GEMV (1 o, 2 gate_up,
-# 4 down, 8 the next layer's qkv), so the GEMVs that follow the latency-bound attention read them
-# from the memory-side cache; 0 (default) off.  EDGELLM_PREFETCH_ROWS: the largest decode batch
-# that takes it; EDGELLM_PREFETCH_BLOCKS: workgroups of the prefetch kernel.
-PREFETCH_MASK = int(os.environ.get("EDGELLM_PREFETCH", "0"))
-PREFETCH_ROWS = int(os.environ.get("EDGELLM_PREFETCH_ROWS", "4"))
-PREFETCH_BLOCKS = int(os.environ.get("EDGELLM_PREFETCH_BLOCKS", "128"))
-
-
-class WeightPrefetcher:
-    """Fork / join of one decode step's weight prefetches (graph-capturable: the side stream waits
-    on an event of the capturing stream and the capturing stream joins it before the head)."""
-    _streams = {}
-
-    def __init__(self, model: "DecoderLM", mask: int):
-        self.model, self.mask = model, mask
-        dev = model.device
-        if dev not in WeightPrefetcher._streams:
-            WeightPrefetcher._streams[dev] = torch.cuda.Stream(dev)
-        self.side = WeightPrefetcher._streams[dev]
-        self.main = torch.cuda.current_stream(dev)
-        self.by_idx = {layer.idx: k for k, layer in enumerate(model.layers)}
-        self.forked = False
-
-    @classmethod
-    def for_step(cls, model: "DecoderLM", ctx: AttnCtx) -> Optional["WeightPrefetcher"]:
-        if not PREFETCH_MASK or ctx.mode != "decode" or ctx.B > PREFETCH_ROWS or ctx.attn_hook is not None:
-            return None
-        if not torch.cuda.is_available() or model.device.type != "cuda":
-            return None
-        return cls(model, PREFETCH_MASK)
-
-    def _weights(self, layer):
-        out = []
-        if layer.attn is not None and self.mask & 1:
-            out.append(getattr(layer.attn.o, "w_packed", None))
-        if layer.mlp is not None and self.mask & 2:
-            out.append(getattr(layer.mlp.up, "w_packed", None))
-        if layer.mlp is not None and self.mask & 4:
-            out.append(getattr(layer.mlp.down, "w_packed", None))
-        k = self.by_idx[layer.idx]
-        if self.mask & 8 and k + 1 < len(self.model.layers) and self.model.layers[k + 1].attn is not None:
-            out.append(getattr(self.model.layers[k + 1].attn.qkv, "w_packed", None))
-        return [w for w in out if w is not None]
-
-    def after_qkv(self, layer_idx: int):
-        layer = self.model.layers[self.by_idx[layer_idx]]
-        ws = self._weights(layer)
-        if not ws:
-            return
-        ev = torch.cuda.Event()
-        ev.record(self.main)
-        self.side.wait_event(ev)
-        with torch.cuda.stream(self.side):
-            for w in ws:
-                ops.prefetch(w, PREFETCH_BLOCKS)
-        self.forked = True
-
-    def join(self):
-        if self.forked:
-            self.main.wait_stream(self.side)
 
 
 # --------------------------------------------------------------------------- initialisation

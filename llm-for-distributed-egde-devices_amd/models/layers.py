@@ -96,8 +96,7 @@ class Linear(nn.Module):
     def decode_weight(self, x, glu: bool = False) -> "Optional[torch.Tensor]":
         """Fragment-packed copy of the weight for the decode GEMV / ring GEMM, built on the first
         decode-sized call (before any graph capture) and kept; None when not applicable."""
-        if not (ops.bf16_decode_mode(x, self.weight, glu=glu, split=bool(self.split_k_out))
-                or ops.bf16_prefill_x32_ok(x, self.weight)):
+        if not ops.bf16_decode_mode(x, self.weight, glu=glu, split=bool(self.split_k_out)):
             return None
         wp, ver = getattr(self, "_wp", None), self.weight._version   # in-place weight edits repack
         if wp is None or getattr(self, "_wp_ver", -1) != ver or wp.device != self.weight.device:

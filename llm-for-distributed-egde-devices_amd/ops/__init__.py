@@ -296,13 +296,6 @@ def prefill_attention(q, k_cache, v_cache, start_pos, scale, causal=True):
 # --------------------------------------------------------------------------- INT8 GEMM
 
 
-def prefetch(t: torch.Tensor, blocks: int = 0) -> None:
-    """Stream ``t``'s bytes through the cache hierarchy on the current stream (Infinity Cache
-    warm-up for a kernel that reads them next; a no-op off the GPU path)."""
-    if _gpu(t):
-        ext().prefetch(t, blocks)
-
-
 def pack_int8_weight(w: torch.Tensor) -> torch.Tensor:
     """[N, K] int8 -> MFMA-fragment-packed 1 KiB tiles (see csrc/gemm_i8.hip header).
     N is padded to 16 and K to 64 with zeros."""
@@ -367,17 +360,6 @@ def pack_bf16_weight(w: torch.Tensor) -> torch.Tensor:
 _GEMV_EPI = {None: 0, "silu_glu": 1, "gelu_tanh": 2, "gelu": 3}
 
 
-# bf16 prefill projections (>= 256 rows) on the 32x32x16 MFMA GEMM (gemm_i8.hip x32 kernel, DT = 1)
-# over the layer's fragment-packed weight copy instead of hipBLASLt: EDGELLM_BF16_X32=1 (A/B)
-BF16_PREFILL_X32 = os.environ.get("EDGELLM_BF16_X32", "0") == "1"
-
-
-def bf16_prefill_x32_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    K = x.shape[-1]
-    return (BF16_PREFILL_X32 and _gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
-            and x.is_contiguous() and K % 64 == 0 and weight.shape[0] % 16 == 0 and x.numel() // max(K, 1) >= 256)
-
-
 def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = None,
                 packed: Optional[torch.Tensor] = None, add: Optional[torch.Tensor] = None):
     """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` on the fragment-packed
@@ -399,12 +381,7 @@ def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = No
     if mode == 2:           # GELU MLPs: ring GEMM, then the activation kernel
         wp = packed if packed is not None else pack_bf16_weight(weight)
         return activation(ext().gemm_bf16_ring(x, wp, bias, weight.shape[0], 0, 0), act)
-    y = None
-    if bf16_prefill_x32_ok(x, weight):
-        wp = packed if packed is not None else pack_bf16_weight(weight)
-        y = ext().gemm_bf16_x32(x, wp, bias, weight.shape[0])     # None: the shape is not taken
-    if y is None:
-        y = torch.nn.functional.linear(x, weight, bias)
+    y = torch.nn.functional.linear(x, weight, bias)
     y = y if act is None else activation(y, act)
     return y if add is None else y + add
 

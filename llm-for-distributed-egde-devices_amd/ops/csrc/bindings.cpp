@@ -47,7 +47,6 @@ size_t edge_sample_workspace(int B, int V);
 void edge_sample_rowwide_min(int v);
 void edge_prefill_fa(int v, int stag);
 int edge_sample_timestamps(int enable, unsigned long long* host_out16);
-int edge_prefetch(const void* p, int64_t bytes, int* sink, int blocks, hipStream_t st);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st, int mode, int* used);
 void edge_w8a8_gemv_config(int nw, int unroll);
@@ -56,7 +55,6 @@ int edge_w8a8_rows256_ok(int K);
 int edge_w8a8_rows256_splits(int K);
 void edge_w8a8_rows256_diag(int v);
 void edge_w8a8_prefill_x32(int v);
-void edge_w8a8_prefill_stages(int v);
 void edge_w8a8_rows256_rot(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st, const void* add);
@@ -88,8 +86,6 @@ int edge_kv_quant_append(const void* src, int64_t x_sb, int64_t x_sh, const int*
 void edge_decode_attn_occ(int occ);
 int edge_kv_dequant(const void* src, int64_t c_sb, int64_t c_sh, const float* sc, int64_t s_sb, int64_t s_sh, void* dst,
                     int64_t d_sb, int64_t d_sh, int B, int Hkv, int T, int D, hipStream_t st);
-int edge_gemm_bf16_x32(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, hipStream_t st);
-void edge_bf16_x32_cfg(int v);
 int edge_gemm_bf16_ring(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi, int S,
                         hipStream_t st);
 int edge_bf16_ring_splits(int N, int K);
@@ -626,25 +622,6 @@ at::Tensor gemv_bf16_splitk(const at::Tensor& x, const at::Tensor& wp, const std
 // bf16 decode projection at 17-256 rows on the ring2 kernel (gemm_i8.hip, bf16 operand mode) over
 // the same fragment-packed weight as gemv_bf16.  epi 0: bf16 [.., N]; 1: SwiGLU over [gate | up]
 // -> bf16 [.., N / 2]; 3: split-K fp32 partial slices [S, M, N] (S = 0: the launcher's choice).
-// bf16 prefill GEMM on the 256 x 256 32x32x16 MFMA kernel; an undefined tensor when the shape is not
-// taken (the caller then runs hipBLASLt)
-at::Tensor gemm_bf16_x32(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N) {
-  DEVICE_GUARD(x);
-  need(x, at::kBFloat16, "x");
-  need(wp, at::kBFloat16, "weight (packed)");
-  const int64_t K = x.size(-1), M = rows_of(x);
-  TORCH_CHECK(wp.numel() == N * K, "packed weight must hold N * K elements");
-  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
-  auto os = x.sizes().vec();
-  os.back() = N;
-  at::Tensor out = at::empty(os, x.options());
-  const int rc = edge_gemm_bf16_x32(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(),
-                                    (int)M, (int)N, (int)K, stream());
-  if (rc == -2) return at::Tensor();
-  check(rc, "gemm_bf16_x32");
-  return out;
-}
-
 at::Tensor gemm_bf16_ring(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
                           int64_t epi, int64_t S) {
   DEVICE_GUARD(x);
@@ -871,12 +848,6 @@ int64_t copy_head_block(at::Tensor& dst, const at::Tensor& src, int64_t mode) {
 }
 
 // stream a device tensor's bytes through the cache hierarchy (MALL warm-up ahead of a reader)
-void prefetch(const at::Tensor& t, int64_t blocks) {
-  DEVICE_GUARD(t);
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "prefetch: contiguous device tensor");
-  check(edge_prefetch(t.data_ptr(), (int64_t)(t.numel() * t.element_size()) & ~(int64_t)15, nullptr, (int)blocks,
-                      stream()), "prefetch");
-}
 
 }  // namespace
 
@@ -921,17 +892,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "whether the 65-128 row decode GEMV has a kernel for K (in S split-K slices)");
   m.def("rows256_ok", [](int64_t K) { return edge_w8a8_rows256_ok((int)K) != 0; },
         "whether the 129-256 row decode GEMMs (row-split ring2) take this K");
-  m.def("gemm_bf16_x32", &gemm_bf16_x32, "bf16 prefill GEMM (M >= 256) on the 32x32x16 MFMA kernel; undefined if not taken");
-  m.def("prefetch", &prefetch, "stream a tensor through the cache hierarchy (Infinity Cache warm-up)",
-        py::arg("t"), py::arg("blocks") = 0);
   m.def("tune", [](const std::string& what, int64_t a, int64_t b) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
     else if (what == "ring2_256_diag") edge_w8a8_rows256_diag((int)a);
     else if (what == "prefill_x32") edge_w8a8_prefill_x32((int)a);
-    else if (what == "prefill_stages") edge_w8a8_prefill_stages((int)a);
-    else if (what == "bf16_x32") edge_bf16_x32_cfg((int)a);
     else if (what == "ring2_256_rot") edge_w8a8_rows256_rot((int)a);
     else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);

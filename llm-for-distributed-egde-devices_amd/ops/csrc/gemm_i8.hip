@@ -913,12 +913,12 @@ __device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_r
 //    ~60 for contiguous pieces.  The LDS image is identical, only the DMA source offsets change.
 // PRIO: s_setprio(1) around each k-tile's MFMA cluster (cdna guide T5: keeps hipcc from moving the
 // MFMAs across the barriers into the fragment reads / DMA issue; A/B knob prefill_prio)
-template <int BMV, int ISS, bool APK = false, bool PRIO = false, int RV = 4>
+template <int BMV, int ISS, bool APK = false, bool PRIO = false>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                               int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
-  constexpr int R = RV, BNV = 256, NWV = 8;
+  constexpr int R = 4, BNV = 256, NWV = 8;
   constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
   constexpr int MI = BMV / 32, NJ = 4;                        // row blocks / column tiles per wave
   static_assert(PIECES % NWV == 0, "pieces per wave");
@@ -1141,17 +1141,20 @@ __global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ 
 //    token (l & 31) and 4 runs of 4 consecutive columns 8 q + 4 (l >> 5).  The epilogue restages
 //    32 tokens x 64 columns per wave at a time (int32, XOR-swizzled 16-B chunks) and writes 16-B
 //    bf16 row chunks.
-//  * DT == 1: bf16 operands (the bf16 prefill GEMM): a fragment-packed bf16 weight (16 rows x 32 k
-//    per KiB) and a row-major bf16 activation have byte for byte the int8 layouts, with K counted
-//    in bytes, and v_mfma_f32_32x32x16_bf16 takes the same 16 B per lane (k 8 (l >> 5) .. + 8 of a
-//    16-k step) as the i8 form — so only the MFMA and the epilogue (fp32 sums + bias, no scales)
-//    change.  sa / sw are unused.
-template <bool APK, int DT = 0, int RV = 4>
+//  * The two waves of each SIMD are de-phased: waves 0-3 issue a stage's LDS-DMA pieces right after
+//    the barrier, waves 4-7 after their second MFMA step, so after every barrier one wave per SIMD
+//    runs MFMAs while the other issues DMA (+4-10 % over issuing together).
+//  * Measured against the 128 x 256 16x16x64 kernel (tools/bench_ops.py --only x32, Llama-2-7B shapes):
+//    2.17-2.30 vs 2.10-2.15 POPS at M = 16384, behind it at <= 384 tiles (qkv at M = 2048: 1.77 vs
+//    2.05), so the launcher takes it from 512 tiles (two full rounds of the 256 CUs).  The same
+//    kernel on bf16 operands (v_mfma_f32_32x32x16_bf16) ran 1.19-1.24 PF against hipBLASLt's
+//    1.46-1.61 PF and was dropped.
+template <bool APK>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                               int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
-  constexpr int R = RV, BMV = 256, BNV = 256, NWV = 8;
+  constexpr int R = 4, BMV = 256, BNV = 256, NWV = 8;
   constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
   static_assert(R * STAGE <= 160 * 1024 && NWV * 32 * 256 <= R * STAGE, "LDS budget");
   __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
@@ -1167,6 +1170,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
+  const bool late = wave >= 4;                        // DMA after the second MFMA step (see above)
   uint32_t off[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
@@ -1208,8 +1212,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
     asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fw[0]) : "v"(wb));
     asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fw[1]) : "v"(wb));
   };
-  using AccT = std::conditional_t<DT == 1, v16f, v16i>;
-  AccT acc[4][2];
+  v16i acc[4][2];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -1225,11 +1228,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        if constexpr (DT == 1)
-          acc[c][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8s, fw[b]), __builtin_bit_cast(v8s, fa[c]),
-                                                              acc[c][b], 0, 0, 0);
-        else
-          acc[c][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[b], fa[c], acc[c][b], 0, 0, 0);
+        acc[c][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[b], fa[c], acc[c][b], 0, 0, 0);
       }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -1251,10 +1250,11 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
     if (kt + 1 < KT) {                                // wave-uniform
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 2) * PPW) : "memory");   // own DMA of kt + 1
       __builtin_amdgcn_s_barrier();                   // kt + 1 landed everywhere; slot of kt free
-      issue(kt + R);
+      if (!late) issue(kt + R);
       read_frags(kt + 1, 0, xa, xw);
     }
     mma(ya, yw);
+    if (late && kt + 1 < KT) issue(kt + R);           // waves 4-7: behind this k-tile's second MFMA step
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-load stages past the end
@@ -1270,7 +1270,7 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int col = min(col0 + e, N - 1);
-    swv[e] = DT == 1 ? 1.f : sw[col];
+    swv[e] = sw[col];
     bv[e] = bf2f(bp[bias != nullptr ? col : 0]);
   }
   __syncthreads();                                    // every wave is done with the ring
@@ -1282,31 +1282,21 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int k16 = 8 * b + 2 * q + hi;           // 16-B chunk (4 int32 columns) of the 64
-        v4i v4;
-        if constexpr (DT == 1)
-          v4 = __builtin_bit_cast(v4i, v4f{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]});
-        else
-          v4 = v4i{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]};
+        const v4i v4 = v4i{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]};
         *reinterpret_cast<v4i*>(wt + tl * 256 + ((k16 ^ (tl & 15)) << 4)) = v4;
       }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int t = it * 8 + (lane >> 3);
       const int row = bm * BMV + wm * 128 + c * 32 + t;
-      const float sr = DT == 1 ? 1.f : sa[min(row, M - 1)];
+      const float sr = sa[min(row, M - 1)];
       const v4i lo4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8) ^ (t & 15)) << 4));
       const v4i hi4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8 + 1) ^ (t & 15)) << 4));
-      const v4f lof = __builtin_bit_cast(v4f, lo4), hif = __builtin_bit_cast(v4f, hi4);
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if constexpr (DT == 1) {
-          v[e] = lof[e] + bv[e];
-          v[e + 4] = hif[e] + bv[e + 4];
-        } else {
-          v[e] = (float)lo4[e] * sr * swv[e] + bv[e];
-          v[e + 4] = (float)hi4[e] * sr * swv[e + 4] + bv[e + 4];
-        }
+        v[e] = (float)lo4[e] * sr * swv[e] + bv[e];
+        v[e + 4] = (float)hi4[e] * sr * swv[e + 4] + bv[e + 4];
       }
       if (row < M && col0 < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col0) = pack8(v);   // N % 8 == 0
     }
@@ -1966,11 +1956,12 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
 
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2;
 // prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel (BM = 128)
-static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0, g_prefill_x32 = 0;
-// ring depth of the prefill GEMMs (A/B): 0 = 4 stages; 6 = the 128 x 256 kernel with 6 (144 KiB),
-// 5 = the 256 x 256 x32 kernel with 5 (160 KiB)
-static int g_prefill_stages = 0;
-extern "C" void edge_w8a8_prefill_stages(int v) { g_prefill_stages = v; }
+static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0, g_prefill_x32 = 1;
+// the 256 x 256 x32 kernel: g_prefill_x32 0 never, 1 from 512 tiles (default), 2 from 192 tiles (tests)
+static bool x32_takes(int M, int grid_n) {
+  const int64_t tiles = (int64_t)((M + 255) / 256) * grid_n;
+  return g_prefill_x32 && M >= 256 && tiles >= (g_prefill_x32 == 2 ? 192 : 512);
+}
 // prefill_x32: 0 off, 1 the 256 x 256 32x32x32 kernel when the grid fills >= 1 round of CUs (M >= 256)
 extern "C" void edge_w8a8_prefill_x32(int v) { g_prefill_x32 = v; }
 extern "C" void edge_w8a8_prefill_prio(int v) { g_prefill_prio = v; }
@@ -2353,26 +2344,16 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     // the ring's counted vmcnt — the same hazard that broke a decode kernel — so it is gone.)
     const int grid_n = (NTt * 16 + 255) / 256;
     const int grid_m = (M + 127) / 128;
-    if (g_prefill_x32 && M >= 256 && ((M + 255) / 256) * grid_n >= 192) {
+    if (x32_takes(M, grid_n)) {
       const int gm2 = (M + 255) / 256;
-      if (g_prefill_stages == 5)
-        hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 0, 5>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A,
-                           sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
-      else
-        hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
-                           (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
+                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
       return (int)hipGetLastError();
     }
 #define BIGK(BMV, ISS)                                                                                           \
   hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
                      (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
     const int iss = g_prefill_iss;
-    if (g_prefill_stages == 6 && iss == 2 && !g_prefill_prio) {
-      hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, false, false, 6>), dim3(grid_m * grid_n), dim3(512), 0, st,
-                         (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
-                         grid_m, grid_n);
-      return (int)hipGetLastError();
-    }
     if (g_prefill_prio && iss == 2) {
       hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, false, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
                          (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
@@ -2438,21 +2419,13 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
   const int NTt = (N + 15) / 16;
   const int grid_n = (NTt * 16 + 255) / 256;
   const int grid_m = (M + 127) / 128;
-  if (g_prefill_x32 && M >= 256 && ((M + 255) / 256) * grid_n >= 192) {
+  if (x32_takes(M, grid_n)) {
     const int gm2 = (M + 255) / 256;
-    if (g_prefill_stages == 5)
-      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true, 0, 5>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
-    else
-      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
+                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
     return (int)hipGetLastError();
   }
-  if (g_prefill_stages == 6 && !g_prefill_prio)
-    hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, false, 6>), dim3(grid_m * grid_n), dim3(512), 0, st,
-                       (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
-                       grid_m, grid_n);
-  else if (g_prefill_prio)
+  if (g_prefill_prio)
     hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
                        (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
                        grid_m, grid_n);
@@ -2460,28 +2433,6 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
     hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
                        (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
                        grid_m, grid_n);
-  return (int)hipGetLastError();
-}
-
-// bf16 prefill GEMM y = x . W^T (+ bias) on the x32 kernel: x bf16 [M, K] row-major, W fragment-packed
-// bf16 (ops.pack_bf16_weight), M >= 256, K % 64 == 0, N % 16 == 0.  -2: not taken (the caller runs
-// hipBLASLt); g_bf16_x32 0 turns it off (A/B knob "bf16_x32").
-static int g_bf16_x32 = 1;
-extern "C" void edge_bf16_x32_cfg(int v) { g_bf16_x32 = v; }
-extern "C" int edge_gemm_bf16_x32(const void* A, const void* W, const void* bias, void* out, int M, int N, int K,
-                                  hipStream_t st) {
-  if (!g_bf16_x32 || M < 256 || K % 64 != 0 || K <= 0 || N % 16 != 0) return -2;
-  const int Kb = 2 * K, KT = Kb / 64, NTt = N / 16;
-  const int grid_n = (N + 255) / 256, grid_m = (M + 255) / 256;
-  if ((int64_t)grid_m * grid_n < 192 || (int64_t)M * Kb >= ((int64_t)1 << 32)) return -2;
-  if (g_prefill_stages == 5)
-    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 1, 5>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A,
-                       nullptr, (const int8_t*)W, nullptr, (const bf16_t*)bias, (bf16_t*)out, M, N, Kb, KT, NTt, grid_m,
-                       grid_n);
-  else
-    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, 1>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A,
-                       nullptr, (const int8_t*)W, nullptr, (const bf16_t*)bias, (bf16_t*)out, M, N, Kb, KT, NTt, grid_m,
-                       grid_n);
   return (int)hipGetLastError();
 }
 

@@ -87,32 +87,3 @@ extern "C" int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, c
   return 0;
 }
 
-// ------------------------------------------------------------------ memory-side cache prefetch
-// Streams [p, p + bytes) through the default cache policy so the lines land in the 256 MB
-// Infinity Cache (MALL) ahead of a kernel that will read them (batch-1 decode: the next
-// projections' weights while the latency-bound attention leaves HBM idle).  Loads only; the XOR
-// of the data is stored to `sink` under a condition that practically never holds, which keeps the
-// loads alive.  16-B loads, UNROLL in flight per thread, grid-stride.
-namespace {
-constexpr int PF_UNROLL = 4;
-__global__ void __launch_bounds__(256) prefetch_kernel(const uint4* __restrict__ p, int64_t n16, int* __restrict__ sink) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  uint32_t acc = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride * PF_UNROLL) {
-    uint4 v[PF_UNROLL];
-#pragma unroll
-    for (int u = 0; u < PF_UNROLL; ++u) v[u] = i + u * stride < n16 ? p[i + u * stride] : uint4{0, 0, 0, 0};
-#pragma unroll
-    for (int u = 0; u < PF_UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-  }
-  if (acc == 0x9E3779B9u && sink != nullptr) sink[0] = (int)acc;
-}
-}  // namespace
-
-extern "C" int edge_prefetch(const void* p, int64_t bytes, int* sink, int blocks, hipStream_t st) {
-  const int64_t n16 = bytes / 16;
-  if (n16 <= 0) return 0;
-  blocks = blocks > 0 ? blocks : 256;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)p, n16, sink);
-  return (int)hipGetLastError();
-}

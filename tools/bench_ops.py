@@ -593,8 +593,8 @@ def knob_ab_rows(C, dev, knob, values=(1, 0), M=256, shapes=None):
 
 
 def x32_rows(C, dev, Ms=(2048, 16384)):
-    """Prefill INT8 GEMM: the 256 x 256 v_mfma_i32_32x32x32_i8 kernel (tune prefill_x32 1) against
-    the default 128 x 256 16x16x64 kernel, interleaved, Llama-2-7B shapes."""
+    """Prefill INT8 GEMM: the 256 x 256 v_mfma_i32_32x32x32_i8 kernel (tune prefill_x32 2: from 192
+    tiles) against the 128 x 256 16x16x64 kernel (prefill_x32 0), interleaved, Llama-2-7B shapes."""
     out = []
     shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
     for name, (N, K) in shapes.items():
@@ -607,121 +607,15 @@ def x32_rows(C, dev, Ms=(2048, 16384)):
             res = {}
             per = max(2, min(20, int(4e11 // (M * N * K))))
             for _ in range(3):
-                for v in (0, 1):
+                for v in (0, 2):
                     C.tune("prefill_x32", v, 0)
                     res.setdefault(v, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K), iters=5,
                                                         per_graph=per))
-            C.tune("prefill_x32", 0, 0)
+            C.tune("prefill_x32", 1, 0)
             row = dict(op="w8a8_gemm_prefill_x32", shape=name, M=M, N=N, K=K)
             for v, ts in res.items():
                 row[f"x32_{v}_us"] = round(min(ts), 1)
                 row[f"x32_{v}_TOPs"] = round(2 * M * N * K / min(ts) / 1e6, 1)
-            out.append(row)
-            print(row, flush=True)
-    return out
-
-
-def bf16x32_rows(C, dev, Ms=(512, 2048, 16384)):
-    """bf16 prefill GEMM: the 256 x 256 v_mfma_f32_32x32x16_bf16 kernel (gemm_bf16_x32) against
-    F.linear (hipBLASLt), interleaved, Llama-2-7B shapes."""
-    out = []
-    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
-    for name, (N, K) in shapes.items():
-        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
-        wp = ops.pack_bf16_weight(w)
-        for M in Ms:
-            x = torch.randn(M, K, device=dev).bfloat16()
-            if C.gemm_bf16_x32(x, wp, None, N) is None:
-                continue
-            per = max(2, min(20, int(2e11 // (M * N * K))))
-            res = {}
-            for _ in range(3):
-                res.setdefault("x32", []).append(timeit(lambda: C.gemm_bf16_x32(x, wp, None, N), iters=5, per_graph=per))
-                res.setdefault("hipblaslt", []).append(timeit(lambda: torch.nn.functional.linear(x, w), iters=5,
-                                                              per_graph=per))
-            row = dict(op="gemm_bf16_prefill", shape=name, M=M, N=N, K=K)
-            for k, ts in res.items():
-                row[k + "_us"] = round(min(ts), 1)
-                row[k + "_TFs"] = round(2 * M * N * K / min(ts) / 1e6, 1)
-            out.append(row)
-            print(row, flush=True)
-    return out
-
-
-def stages_rows(C, dev, Ms=(2048, 16384)):
-    """Prefill GEMM ring depth (tune prefill_stages): the 128 x 256 16x16x64 kernel at 4 / 6 stages and
-    the 256 x 256 32x32x32 kernel at 4 / 5 stages (INT8), the bf16 x32 kernel at 4 / 5 stages against
-    hipBLASLt; interleaved, Llama-2-7B shapes."""
-    out = []
-    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
-    forms = {"big4": (0, 0), "big6": (0, 6), "x32_4": (1, 0), "x32_5": (1, 5)}
-    for name, (N, K) in shapes.items():
-        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
-        wp = ops.pack_int8_weight(w)
-        s2 = torch.rand(N, device=dev) * 0.01
-        wb = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
-        wbp = ops.pack_bf16_weight(wb)
-        for M in Ms:
-            a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-            s1 = torch.rand(M, device=dev) * 0.01
-            xb = torch.randn(M, K, device=dev).bfloat16()
-            per = max(2, min(20, int(4e11 // (M * N * K))))
-            res = {}
-            for _ in range(3):
-                for form, (x32, stg) in forms.items():
-                    C.tune("prefill_x32", x32, 0)
-                    C.tune("prefill_stages", stg, 0)
-                    res.setdefault(form, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K), iters=5,
-                                                           per_graph=per))
-                for form, stg in (("bf16_x32_4", 0), ("bf16_x32_5", 5)):
-                    C.tune("prefill_stages", stg, 0)
-                    if C.gemm_bf16_x32(xb, wbp, None, N) is not None:
-                        res.setdefault(form, []).append(timeit(lambda: C.gemm_bf16_x32(xb, wbp, None, N), iters=5,
-                                                               per_graph=per))
-                res.setdefault("bf16_hipblaslt", []).append(timeit(lambda: torch.nn.functional.linear(xb, wb),
-                                                                   iters=5, per_graph=per))
-            C.tune("prefill_x32", 0, 0)
-            C.tune("prefill_stages", 0, 0)
-            row = dict(op="prefill_gemm_stages", shape=name, M=M, N=N, K=K)
-            for form, ts in res.items():
-                row[form + "_us"] = round(min(ts), 1)
-                row[form + "_T"] = round(2 * M * N * K / min(ts) / 1e6, 1)
-            out.append(row)
-            print(row, flush=True)
-    return out
-
-
-def prefill_gemm_rows(C, dev, Ms=(512, 2048, 16384)):
-    """Prefill INT8 GEMM at Llama-2-7B projection shapes, random operands, every kernel form timed
-    interleaved in one process ((form, issue): form 0 automatic, 2 / 3 the LDS-DMA ring kernel at
-    256 / 128 rows per block; issue 0 / 1 / 2 = DMA pieces before the fragment reads / after the
-    MFMAs / interleaved into them)."""
-    out = []
-    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
-    # (prefill_gemm form, DMA issue point, A fragment-packed first)
-    forms = {"auto": (0, 2, 1), "auto_rowmajorA": (0, 2, 0), "ring256_apack": (2, 2, 2), "ring128_apack": (3, 2, 2),
-             "ring256_ilv": (2, 2, 0), "ring128_ilv": (3, 2, 0)}
-    for name, (N, K) in shapes.items():
-        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
-        wp = ops.pack_int8_weight(w)
-        s2 = torch.rand(N, device=dev) * 0.01
-        for M in Ms:
-            a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-            s1 = torch.rand(M, device=dev) * 0.01
-            res = {}
-            for rnd in range(2):
-                for form, v in forms.items():
-                    C.tune("prefill_gemm", v[0], v[1])
-                    C.tune("prefill_apack", v[2], 0)
-                    per = max(2, min(20, int(4e11 // (M * N * K))))
-                    res.setdefault(form, []).append(timeit(lambda: C.w8a8_gemm(a, s1, wp, s2, None, N, K),
-                                                           iters=5, per_graph=per))
-            C.tune("prefill_gemm", 0, 2)
-            C.tune("prefill_apack", 1, 0)
-            row = dict(op="w8a8_gemm_prefill", shape=name, M=M, N=N, K=K)
-            for form, ts in res.items():
-                row[form + "_us"] = round(min(ts), 1)
-                row[form + "_TOPs"] = round(2 * M * N * K / min(ts) / 1e6, 1)
             out.append(row)
             print(row, flush=True)
     return out
@@ -749,8 +643,6 @@ def main():
     if only is None or "glu" in only:
         rows += glu_rows(C, dev)
     rows += other_rows(C, dev, only)
-    if only is not None and "pgemm" in only:
-        rows += prefill_gemm_rows(C, dev)
     if only is not None and "m1" in only:
         rows += batch1_rows(C, dev)
     if only is not None and "rows256" in only:
@@ -761,10 +653,6 @@ def main():
         rows += bf16_rows(C, dev)
     if only is not None and "x32" in only:
         rows += x32_rows(C, dev)
-    if only is not None and "stages" in only:
-        rows += stages_rows(C, dev)
-    if only is not None and "bf16x32" in only:
-        rows += bf16x32_rows(C, dev)
     if only is not None and "rot" in only:
         rows += knob_ab_rows(C, dev, "ring2_256_rot", values=(0, 1))
     if only is not None and "prio" in only:

@@ -1,4 +1,5 @@
 # Round-4: 2 lanes x 256 rows, batch-1 weight-prefetch A/B, 1-GPU 2-rank gloo pipeline rehearsal
+# (EDGELLM_PREFETCH, the batch-1 weight prefetch, measured slower here and was removed afterwards)
 set -o pipefail
 export PYTHONUNBUFFERED=1
 D=gpurun_out/r4h; mkdir -p $D
