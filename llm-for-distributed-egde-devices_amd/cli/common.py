@@ -109,7 +109,13 @@ def pp_launch(rt: dict):
     # tear the process group down before interpreter exit (a live group's threads abort the
     # process at exit, which torchrun reports as a failed rank)
     atexit.register(lambda: dist.is_initialized() and dist.destroy_process_group())
-    dev = torch.device("cpu") if want_cpu else torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not want_cpu and dist.get_backend() != "nccl":
+        # rehearsal (EDGELLM_DIST_BACKEND=gloo): more ranks than GPUs share them, P2P host-staged
+        local %= max(1, torch.cuda.device_count())
+    dev = torch.device("cpu") if want_cpu else torch.device("cuda", local)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
     return rank, world, dev
 
 
