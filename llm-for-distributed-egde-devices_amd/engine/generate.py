@@ -11,7 +11,6 @@ Timing follows both reference TPS definitions (``GenerationResult``).
 """
 from __future__ import annotations
 
-import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
