@@ -204,11 +204,17 @@ def run_single(args):
     if device.type == "cuda":
         torch.cuda.empty_cache()
     lat_pts = latency_points(args, device, model, cfg) if args.headinfer_heads is None else {}
+    one_lane = {}
+    if L > 1 and device.type == "cuda" and args.latency_point != "off":
+        # the same micro-batch in ONE lane: the latency side of the lanes trade-off
+        one_lane = dict(micro_batch=B, lanes=1, steps=min(args.steps, 20),
+                        **batch1_p50(model, cfg, args, device, min(args.steps, 20), rows=B))
+        torch.cuda.empty_cache()
     offload = {}
     if kv is not None:
         offload = dict(h_on=kv.h_on, h_off=kv.h_off, chunk_size=kv.chunk_size, h2d_gb=round(kv.bytes_h2d / 1e9, 3),
                        d2h_gb=round(kv.bytes_d2h / 1e9, 3), transports=dict(kv.transports))
-    return dict(latency_point=lat_pts, offload=offload,value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
+    return dict(latency_point=lat_pts, one_lane_point=one_lane, offload=offload, value=tokens / dt, ms_per_step=dt / args.steps * 1e3, p50=p50, p90=p90, lat_max=lmax, global_batch=B * L,
                 prefill_tps=B * L * args.prompt_len / prefill_s, build_s=t_build, graphs=graphs,
                 mem_gb=mem, partition=[0, cfg.num_layers], ttft_ms=ttft_ms, world_size=1, kv_gpu_gb=kv_gpu,
                 kv_host_gb=(kv.host_bytes() / 1e9 if kv is not None else 0.0))
@@ -223,14 +229,15 @@ def kv_dtype(args, cfg) -> str:
 
 
 @torch.no_grad()
-def batch1_p50(model, cfg, args, device, steps: int) -> dict:
-    """Batch-1 decode latency of ``model`` (graph-captured, same sampling config): p50 / p90 of
-    per-token device-event intervals over ``steps`` tokens after a warm-up."""
+def batch1_p50(model, cfg, args, device, steps: int, rows: int = 1) -> dict:
+    """Decode latency of ``model`` at ``rows`` sequences in one lane (graph-captured, same sampling
+    config): p50 / p90 of per-token device-event intervals over ``steps`` tokens after a warm-up."""
     W = max(4, args.warmup)
     max_seq = args.prompt_len + W + steps + 16
-    gen = Generator(model, max_batch=1, max_seq=max_seq, use_graphs=not args.no_graphs, kv_dtype=kv_dtype(args, cfg))
+    gen = Generator(model, max_batch=rows, max_seq=max_seq, use_graphs=not args.no_graphs,
+                    kv_dtype=kv_dtype(args, cfg))
     g = torch.Generator().manual_seed(args.seed + 1)
-    prompt = torch.randint(0, cfg.vocab_size, (1, args.prompt_len), generator=g).tolist()
+    prompt = torch.randint(0, cfg.vocab_size, (rows, args.prompt_len), generator=g).tolist()
     sp = SamplingParams(max_new_tokens=W + steps + 2, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
     gen.start(prompt, sp, seed=args.seed)
     gen.step(W, record_latency=False)
@@ -244,7 +251,7 @@ def batch1_p50(model, cfg, args, device, steps: int) -> dict:
     ev = gen._run["events"][n0:]
     lat = sorted(ev[i - 1].elapsed_time(ev[i]) for i in range(1, len(ev))) or [dt / steps * 1e3]
     out = dict(p50_ms=round(lat[len(lat) // 2], 4), p90_ms=round(lat[int(len(lat) * 0.9)], 4),
-               tokens_per_s=round(steps / dt, 1), ttft_ms=round(gen._run["t_prefill"] * 1e3, 3))
+               tokens_per_s=round(rows * steps / dt, 1), ttft_ms=round(gen._run["t_prefill"] * 1e3, 3))
     del gen
     return out
 
@@ -355,6 +362,8 @@ def main(argv=None):
         out["offload"] = res["offload"]
     if res.get("latency_point"):
         out["latency_point"] = res["latency_point"]
+    if res.get("one_lane_point"):
+        out["one_lane_point"] = res["one_lane_point"]
     if "per_rank" in res:
         out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
         out["per_rank"] = res["per_rank"]
