@@ -255,7 +255,7 @@ def prefill_rows(C, dev, Hq, D):
     # prefill attention (MFMA)
     D0 = D
     for T, Hkv, s0, D in ((512, Hq, 0, D0), (1024, Hq, 0, D0), (2048, Hq, 0, D0), (8192, Hq // 4, 0, D0),
-                          (4096, Hq // 4, 28672, D0), (1024, 8, 0, 64)):
+                          (4096, Hq // 4, 28672, D0), (32768, Hq // 4, 0, D0), (1024, 8, 0, 64)):
         q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
         kc = torch.randn(1, Hkv, s0 + T, D, device=dev).bfloat16()
         vc = torch.randn_like(kc)
@@ -264,12 +264,12 @@ def prefill_rows(C, dev, Hq, D):
         row = dict(op="prefill_attn_causal", T=T, start=s0, H=Hq, Hkv=Hkv, D=D)
         for name, v, stg in (("fa", 2, 2), ("fa_lockstep", 2, 1), ("old", 0, 0)):
             C.tune("prefill_fa", v, stg)
-            t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=10)
+            t = timeit(lambda: C.prefill_attn(q, kc, vc, sp0, 1 / math.sqrt(D), True), iters=10,
+                       per_graph=2 if T >= 16384 else 20)
             row[f"{name}_us"], row[f"{name}_TFLOPs"] = round(t, 2), round(flops / t / 1e6, 1)
         C.tune("prefill_fa", 1, 0)
         out.append(row)
         print(row, flush=True)
-    out += prefill_gemm_rows(C, dev)
     return out
 
 
