@@ -29,7 +29,6 @@ bubble fraction over a window of ticks (``run(stats_window=...)`` -> ``PipelineR
 """
 from __future__ import annotations
 
-import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -42,10 +41,6 @@ from ..engine.generate import GRAPH_BUCKET, SamplingParams, needs_host_sampler
 from ..engine.kv_cache import KVCache
 from ..models.decoder import AttnCtx, DecoderLM
 from ..utils.tracing import debug_sync, trace_range
-
-# host-staged exchanges (gloo with device tensors): 1 = synchronous copies on the current stream
-# (A/B against the side-stream pinned staging)
-_STAGE_SYNC = os.environ.get("EDGELLM_PP_STAGE_SYNC", "0") == "1"
 
 
 @dataclass
@@ -148,15 +143,12 @@ class PipelineStage:
             return None
         self.p2p_bytes += sum(t.numel() * t.element_size() for t, _ in sends)
         g = self.granks
-        if self.host_staged and _STAGE_SYNC and send_ready is None:
-            bufs = [torch.empty(t.shape, dtype=t.dtype) for t, _ in recvs]
-            p2p = [dist.P2POp(dist.isend, t.cpu(), g[p], self.group) for t, p in sends]
-            p2p += [dist.P2POp(dist.irecv, h, g[p], self.group) for h, (_, p) in zip(bufs, recvs)]
-        elif self.host_staged:
+        if self.host_staged:
             if self._copy_stream is None:
                 self._copy_stream = torch.cuda.Stream(self.device)
             cs = self._copy_stream
             producer = torch.cuda.current_stream(self.device)   # (taken before cs becomes current)
+            assert producer != cs, "the copy stream must wait on the sends' producer, not on itself"
             host_sends = []
             with torch.cuda.stream(cs):
                 if send_ready is not None:
@@ -190,7 +182,7 @@ class PipelineStage:
             w.wait()
         if bufs is not None:
             for h, t in zip(bufs, dsts):
-                t.copy_(h, non_blocking=not _STAGE_SYNC)
+                t.copy_(h, non_blocking=True)
         debug_sync("pp.exchange")
 
     def _send_one(self, t: torch.Tensor, peer: int):
