@@ -11,10 +11,12 @@ stage busy:
   rank s processes item i at tick i + s (lockstep); with M >= P micro-batches the token of
   decode(k, m) reaches stage 0 exactly when decode(k+1, m) starts (M - P ticks of slack).
 
-Per tick each rank issues ONE grouped P2P exchange through ``dist.batch_isend_irecv`` (send the
-previous tick's outputs, receive this tick's inputs — grouped, so no send/recv ordering deadlock;
-on RCCL one ncclGroupStart/End over the process group's communicator), then runs its layers for
-the micro-batches of the tick.  The same P2POp path runs under gloo on the CPU, which is how the
+Per tick each rank issues one grouped P2P exchange per lane through ``dist.batch_isend_irecv``
+(send the lane's previous outputs, receive its next inputs — grouped, so no send/recv ordering
+deadlock; on RCCL one ncclGroupStart/End over the process group's communicator), issued and
+completed on that lane's HIP stream, then runs its layers for the micro-batches of the tick.  A
+lane's hop therefore waits only for that lane's compute and runs beside the other lanes' compute,
+and no lane waits for the others at a tick boundary.  The same P2POp path runs under gloo on the CPU, which is how the
 multi-rank schedule is tested without GPUs.  The decode compute of each micro-batch is captured in
 a HIP graph per KV-length bucket (all buckets of a run are captured at the first capture, before
 any timed region); the P2P ops stay outside the graphs on RCCL's stream, ordered by stream waits,
@@ -426,20 +428,25 @@ class PipelineStage:
         done_ev: Dict[int, object] = {}     # tick -> event after its compute (host-staged sends)
         host_late = self.host_staged and D > 1
 
-        def exchange_for(t):
-            """(sends, recvs) of the exchange posted at tick t."""
+        # lanes on GPU streams: every lane posts and completes its OWN exchange on its stream, so a
+        # lane's hop waits only for that lane's compute and overlaps the other lanes' compute, and no
+        # lane waits at a tick boundary for the others (items of different lanes never share data)
+        per_lane = self.streams is not None
+
+        def exchange_for(t, lanes):
+            """(sends, recvs) of the exchange posted at tick t for the given lanes of the group."""
             prv_g, rcv_g = t - 1 - R, t + D - 1 - R
             sends, recvs = [], []
             if P == 1:
                 return sends, recvs
             if group_valid(prv_g):
-                for prv in range(prv_g * L, prv_g * L + L):
+                for prv in (prv_g * L + l for l in lanes):
                     if not self.is_last:
                         sends.append((pre_out[prv] if prv < M else self.hout[(prv - M) % M], self.next))
                     elif feeds_back(prv):
                         sends.append((self.tok[prv % M], 0))
             if not self.is_first and group_valid(rcv_g):
-                for cur in range(rcv_g * L, rcv_g * L + L):
+                for cur in (rcv_g * L + l for l in lanes):
                     if cur < M:
                         pre_in[cur] = torch.empty(b * T, H, dtype=self.model.dtype, device=dev)
                         recvs.append((pre_in[cur], self.prev))
@@ -448,22 +455,47 @@ class PipelineStage:
             if self.is_first:
                 prod_g = t - 1 - D * (P - 1)    # group the last stage finished at tick t - 1
                 if group_valid(prod_g):
-                    for prod in range(prod_g * L, prod_g * L + L):
+                    for prod in (prod_g * L + l for l in lanes):
                         if feeds_back(prod):
                             recvs.append((self.tok[prod % M], P - 1))
             return sends, recvs
 
         def post(t):
-            sends, recvs = exchange_for(t)
             nonlocal win_bytes
-            if w_a <= t < w_b:
-                win_bytes += sum(x.numel() * x.element_size() for x, _ in sends)
-            due[t + D - 1] = self._post(sends, recvs, send_ready=done_ev.pop(t - 1, None) if host_late else None)
+            parts = [(l,) for l in range(L)] if per_lane else [tuple(range(L))]
+            handles = []
+            for lanes in parts:
+                # under the lane's stream: receive buffers are allocated on it, the sends wait on it
+                with (lane_ctx(lanes[0]) if per_lane else _nullctx()):
+                    sends, recvs = exchange_for(t, lanes)
+                    if w_a <= t < w_b:
+                        win_bytes += sum(x.numel() * x.element_size() for x, _ in sends)
+                    ready = done_ev.pop((t - 1, lanes[0]), None) if host_late else None
+                    handles.append(self._post(sends, recvs, send_ready=ready))
+            due[t + D - 1] = handles
             if not self.is_last:
                 for prv in range((t - 1 - R) * L, (t - R) * L):
                     if 0 <= prv < M:
                         pre_out[prv] = None             # handed to the exchange (it holds the tensor)
 
+        def finish(t):
+            for i, h in enumerate(due.pop(t, None) or []):
+                with (lane_ctx(i) if per_lane else _nullctx()):
+                    self._finish(h)
+
+        def mark_on(store, t):                   # per-lane mode: one event per lane stream
+            if per_lane:
+                store[t] = []
+                for st in self.streams:
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record(st)
+                    store[t].append(e)
+            else:
+                mark(store, t)
+
+        if per_lane:
+            for st in self.streams:
+                st.wait_stream(cur_stream)
         for t in range(n_ticks):
             if hook is not None:
                 hook(t)
@@ -472,27 +504,19 @@ class PipelineStage:
             if fault is not None:
                 fault(t)
             cur_g = t - R
-            if self.streams:
-                for st in self.streams:
-                    cur_stream.wait_stream(st)
             if w_a <= t - 1 < w_b:
-                mark(ev_done, t - 1)
+                mark_on(ev_done, t - 1)
             if not host_late:
                 post(t)                                  # before this tick's compute: the hop overlaps it
-            self._finish(due.pop(t, None))
+            finish(t)
             if w_a <= t < w_b:
-                mark(ev_in, t)
-            if self.streams:
-                for st in self.streams:
-                    st.wait_stream(cur_stream)
+                mark_on(ev_in, t)
             if group_valid(cur_g):
                 with trace_range(f"pp.tick{t}"):
                     for cur in range(cur_g * L, cur_g * L + L):
                         with lane_ctx(cur):
                             if cur < M:                           # prefill item
                                 m = cur
-                                if self.streams and pre_in[m] is not None:
-                                    pre_in[m].record_stream(self.streams[m % L])   # received on the exchange stream
                                 ids = prompts[m].to(dev) if self.is_first else None
                                 out = self._prefill(m, ids, T, pre_in[m])
                                 pre_in[m] = None
@@ -506,12 +530,10 @@ class PipelineStage:
             if host_late:
                 # host-staged slack: this tick's compute is queued first, then the exchange whose
                 # sends are the previous tick's outputs (the host waits only for that tick)
-                if self.streams:
-                    for st in self.streams:
-                        cur_stream.wait_stream(st)
-                e = torch.cuda.Event()
-                e.record(cur_stream)
-                done_ev[t] = e
+                for lanes in ([(l,) for l in range(L)] if per_lane else [tuple(range(L))]):
+                    e = torch.cuda.Event()
+                    e.record(self.streams[lanes[0]] if per_lane else cur_stream)
+                    done_ev[(t, lanes[0])] = e
                 post(t)
             debug_sync(f"pp.tick{t}")
             if t == t_first:
@@ -520,11 +542,14 @@ class PipelineStage:
                         cur_stream.wait_stream(st)
                 mark(ev_first, t)
             if eos_on and t >= eos_from and (t - eos_from) % eos_period == 0 and t < n_ticks - 1:
+                if per_lane:
+                    for st in self.streams:
+                        cur_stream.wait_stream(st)
                 if self._all_hit():
                     stopped_at = t
                     break
         for k in sorted(due):                            # (after an EOS stop: drain posted exchanges)
-            self._finish(due.pop(k))
+            finish(k)
         if self.streams:
             for st in self.streams:
                 cur_stream.wait_stream(st)
@@ -571,6 +596,8 @@ class PipelineStage:
         ticks = [t for t in range(t_a, t_b) if t in ev_in and t in ev_done]
         if not ticks:
             return {}
+        if isinstance(ev_in[ticks[0]], list):
+            return self._window_stats_lanes(ev_in, ev_done, ticks, t_b - t_a, nbytes)
         if self.cuda:
             dt = lambda a, b: a.elapsed_time(b)             # noqa: E731
         else:
@@ -584,6 +611,33 @@ class PipelineStage:
                     p2p_wait_ms_per_tick=(sum(waits) / len(waits)) if waits else 0.0,
                     span_ms=span, bubble_frac=max(0.0, 1.0 - sum(busy) / span) if span > 0 else 0.0,
                     p2p_bytes_per_tick=nbytes / max(1, t_b - t_a))
+
+
+    @staticmethod
+    def _window_stats_lanes(ev_in, ev_done, ticks, n_ticks, nbytes) -> Dict[str, float]:
+        """Per-lane exchanges: a lane computes from its inputs' arrival to its own done event, and
+        the lanes overlap, so the busy time is the UNION of every lane's compute intervals; the P2P
+        wait is each lane's done(t - 1) -> inputs(t), averaged over lanes."""
+        ref = ev_in[ticks[0]][0]
+        at = lambda e: ref.elapsed_time(e)                  # noqa: E731
+        iv = sorted((at(ev_in[t][l]), at(ev_done[t][l])) for t in ticks for l in range(len(ev_in[t])))
+        busy, (cs, ce) = 0.0, iv[0]
+        for a, z in iv[1:]:
+            if a > ce:
+                busy, cs, ce = busy + (ce - cs), a, z
+            else:
+                ce = max(ce, z)
+        busy += ce - cs
+        waits = [at(ev_in[t][l]) - at(ev_done[t - 1][l]) for t in ticks if t - 1 in ev_done
+                 for l in range(len(ev_in[t]))]
+        span = max(z for _, z in iv) - min(a for a, _ in iv)
+        busy_t = [max(at(ev_done[t][l]) for l in range(len(ev_in[t]))) - min(at(ev_in[t][l]) for l in range(len(ev_in[t])))
+                  for t in ticks]
+        busy_s = sorted(busy_t)
+        return dict(ticks=len(ticks), compute_ms_per_tick=busy / len(ticks), compute_ms_p50=busy_s[len(busy_s) // 2],
+                    p2p_wait_ms_per_tick=(sum(waits) / len(waits)) if waits else 0.0, span_ms=span,
+                    bubble_frac=max(0.0, 1.0 - busy / span) if span > 0 else 0.0,
+                    p2p_bytes_per_tick=nbytes / max(1, n_ticks))
 
 
 class _nullctx:
