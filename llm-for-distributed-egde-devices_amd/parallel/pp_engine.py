@@ -270,12 +270,14 @@ def generate_concurrent(jobs: Sequence[tuple], stop_at_eos: bool = True) -> List
     rank 0 in job order (after all compute, so no send waits on a rank still computing)."""
     eng0 = jobs[0][0]
     assert eng0.grank == 0, "the driver (rank 0) issues commands; workers run serve_workers()"
+    # every job is validated and packed BEFORE the command goes out: a job rejected after the
+    # header was broadcast would leave the workers blocked in the next broadcast
+    packed = [(eng, *eng._job_tensors(prompts, sp, seed, eos, stop_at_eos)) for eng, prompts, sp, seed, eos in jobs]
     cmd = torch.zeros(_HDR, dtype=torch.long, device=eng0.cdev)
     cmd[0], cmd[1] = CMD_GENERATE, len(jobs)
     eng0._bcast(cmd)
     payload = []
-    for eng, prompts, sp, seed, eos in jobs:
-        hdr, fl, ids, lens = eng._job_tensors(prompts, sp, seed, eos, stop_at_eos)
+    for eng, hdr, fl, ids, lens in packed:
         for t in (hdr, fl, ids, lens):
             eng._bcast(t)
         payload.append((eng, hdr, fl, ids, lens))

@@ -49,6 +49,11 @@ def _worker(rank, world, port, arch, sp_kw, eos, q, prompts=PROMPTS):
         res = eng.generate(prompts, sp, seed=11, eos_token_id=eos)
         ticks = eng.last_ticks
         conf = eng.confidence([5, 9, 2, 7, 7, 1])
+        try:                                     # rejected on the driver before any command goes out
+            eng.generate([[1] * 39], sp, seed=11)
+            raise RuntimeError("an oversized job must be rejected")
+        except AssertionError:
+            pass
         again = eng.generate(prompts[:2], sp, seed=11, eos_token_id=eos)     # engine reuse, fewer rows
         stop_workers(eng)
         q.put((res.tokens, conf, again.tokens, eng.stage.M, eng.stage.b, ticks))
