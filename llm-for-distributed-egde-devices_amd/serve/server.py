@@ -172,19 +172,23 @@ class ServingEngine:
 
     # ------------------------------------------------------------------ static-batch worker
     def _loop(self):
+        """Static batches: the queue head's sampling configuration and every waiting request with the
+        same one (up to max_batch) run as one generate call.  After close() the requests already
+        queued are still served, then the loop exits."""
         pending: List[tuple] = []
-        while not self._stop.is_set():
-            try:
-                item = self.q.get(timeout=0.1) if not pending else self.q.get_nowait()
-                if item is None:
-                    break
-                pending.append(item)
-                continue
-            except queue.Empty:
-                pass
+        while True:
             if not pending:
-                continue
-            time.sleep(self.batch_wait_s)          # let concurrent submitters join the batch
+                if self._stop.is_set():
+                    break
+                try:
+                    item = self.q.get(timeout=0.1)
+                except queue.Empty:
+                    continue
+                if item is None:
+                    self._stop.set()
+                    continue
+                pending.append(item)
+                time.sleep(self.batch_wait_s)      # let concurrent submitters join the batch
             while True:
                 try:
                     item = self.q.get_nowait()
@@ -192,11 +196,12 @@ class ServingEngine:
                     break
                 if item is None:
                     self._stop.set()
-                    break
-                pending.append(item)
+                else:
+                    pending.append(item)
             key = pending[0][1]
             batch = [p for p in pending if p[1] == key][: self.max_batch]
-            pending = [p for p in pending if p not in batch]
+            taken = {id(p) for p in batch}
+            pending = [p for p in pending if id(p) not in taken]
             self._run(batch)
 
     def _run(self, batch: List[tuple]):

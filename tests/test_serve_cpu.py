@@ -118,6 +118,22 @@ def test_serving_engine_batches_concurrent_requests(tmp_path):
         eng.close()
 
 
+def test_serving_engine_static_close_serves_queued():
+    """close() right after submits: the static loop still answers every queued request."""
+    from edgellm.serve.server import ServingEngine
+    from edgellm.utils.tokenizer import ByteTokenizer
+    cfg = tiny("llama")
+    m = build_model(cfg, dtype=torch.float32, seed=2)
+    eng = ServingEngine(Generator(m, max_batch=2, max_seq=64), ByteTokenizer(cfg.vocab_size), max_batch=2,
+                        batch_wait_s=0.0, continuous=False)
+    sp = SamplingParams(max_new_tokens=3, do_sample=False)
+    futs = [eng.submit([1, 2, 3 + i], sp) for i in range(5)]
+    eng.q.put(None)                              # the close() sentinel behind the requests
+    outs = [f.result(timeout=60) for f in futs]
+    eng.close()
+    assert all(len(o["tokens"]) == 3 for o in outs) and eng.metrics()["requests"] == 5
+
+
 def test_serving_engine_continuous_batching(tmp_path):
     """Iteration-level batching: requests of different lengths / budgets arriving while others
     decode are admitted into free slots between steps, finished slots are reused at once, and every
