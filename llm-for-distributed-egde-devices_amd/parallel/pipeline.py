@@ -554,7 +554,7 @@ class PipelineStage:
             for st in self.streams:
                 cur_stream.wait_stream(st)
         if w_a <= n_ticks - 1 < w_b:
-            mark(ev_done, n_ticks - 1)
+            mark_on(ev_done, n_ticks - 1)
         if self.cuda:
             torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t_start
