@@ -78,18 +78,9 @@ class Attention(nn.Module):
 
     def forward(self, x, ctx: AttnCtx):
         cfg = self.cfg
+        qkv = self.qkv(x)                                   # [B*T, qkv]
         k_cache, v_cache = ctx.kv.layer(self.layer_idx)
         rot = cfg.rotary_dim if cfg.pos_emb == "rope" else 0
-        if isinstance(x, PendingNorm) and ctx.mode == "decode" and ctx.B == 1 and ctx.attn_hook is None \
-                and not getattr(ctx.kv, "quantized", False) and self.o.takes_quantized_input \
-                and getattr(self.o, "group_scales_ok", lambda m: False)(1):
-            # batch 1: norm -> qkv GEMV -> RoPE + KV append + attention -> int8 for o, one launch
-            r = ops.w8a8_gemv_norm_att(x, self.qkv.w_packed, self.qkv.w_scale, self.qkv.bias, cfg.hidden_size,
-                                       k_cache, v_cache, ctx.start_pos, ctx.seq_lens, ctx.rope, rot, cfg.num_heads,
-                                       self.scale, ctx.max_len)
-            if r is not None:
-                return self.o(QAct(*r))
-        qkv = self.qkv(x)                                   # [B*T, qkv]
         if ctx.attn_hook is not None:
             # int8 offload (HeadInferKV kv_dtype="int8") hands decode output to a W8A8 o-proj as
             # per-(token, 64) int8, like the resident int8 path

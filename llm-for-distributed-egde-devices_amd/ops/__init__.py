@@ -104,38 +104,6 @@ def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scal
     return r if glu_quant else r[0]
 
 
-# Batch-1 decode: the qkv GEMV runs the attention in its tail (gemm_i8.hip att_tail) while the
-# cache holds at most this many keys; one workgroup walks a KV-head group's whole cache, so long
-# contexts go back to the split-K attention launch.  0 disables (A/B).
-ATT_TAIL_MAX_LEN = int(os.environ.get("EDGELLM_ATT_TAIL_MAX", "1024"))
-_ATT_CNT = {}
-
-
-def _att_counters(k_cache, Hkv: int) -> torch.Tensor:
-    """The arrival counters of one layer cache (int32 [Hkv], zero between launches; the kernel's
-    last arriver resets its entry).  One set per cache, so concurrent sequences never share one."""
-    key = (k_cache.device.index, k_cache.data_ptr())
-    c = _ATT_CNT.get(key)
-    if c is None or c.numel() < Hkv:
-        c = _ATT_CNT[key] = torch.zeros(Hkv, dtype=torch.int32, device=k_cache.device)
-    return c
-
-
-def w8a8_gemv_norm_att(pn, w_packed, w_scale, bias, K: int, k_cache, v_cache, start_pos, seq_lens, rope,
-                       rotary_dim: int, num_heads: int, scale: float, max_len_hint: int):
-    """Batch-1 decode step of one attention block from its PendingNorm input ``pn``: the qkv W8A8
-    GEMV with the norm in its prologue and RoPE + KV append + attention in its tail, one launch.
-    Returns (int8 [1, Hq*D], scales [Hq*D/64, 16]) for the o projection, or None when the kernel does
-    not take the geometry (the caller runs the unfused path)."""
-    if not (0 < max_len_hint <= ATT_TAIL_MAX_LEN) or not gemv_norm_ok(pn.parts) or pn.parts.shape[1] != 1:
-        return None
-    kc, vc = k_cache[:1], v_cache[:1]
-    r = ext().w8a8_gemv_norm_att(pn.parts, pn.residual.contiguous(), pn.weight, pn.eps, pn.h, w_packed, w_scale,
-                                 bias, K, kc, vc, start_pos, seq_lens, rope if rotary_dim else None, rotary_dim,
-                                 num_heads, scale, _att_counters(kc, kc.shape[1]))
-    return None if r is None else (r[1], r[2])
-
-
 def decode_rows_ok(M: int, K: int, splits: int = 1) -> bool:
     """Whether the decode GEMV family (grouped scales, split-K, quantising GLU) takes M rows at
     this K: every K up to 64 rows; 65-128 rows (two micro-batches in one) for the k-tile counts

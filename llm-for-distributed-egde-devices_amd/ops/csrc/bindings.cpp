@@ -18,10 +18,6 @@ int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* g
                         const void* Wp, const float* sw, const void* bias, void* out, float* os, int M, int N, int K,
                         int epi, hipStream_t st);
 void edge_w8a8_gemv_norm_cfg(int on);
-int edge_w8a8_gemv_norm_att(const float* part, int S, const void* res, const void* gamma, float eps, void* res_out,
-                            const void* Wp, const float* sw, const void* bias, void* out, int K, int Hq, int Hkv, int D,
-                            void* kc, void* vc, int64_t c_sh, const int* pos, const int* lens, const float* cs, int rot,
-                            float scale, void* q8, float* s8, int Mpad, int* cnt, hipStream_t st);
 int edge_w8a8_gemv_norm_on();
 int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                           float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S, hipStream_t st);
@@ -740,54 +736,6 @@ std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_norm(
   return std::make_tuple(y, s);
 }
 
-// Batch-1 decode: qkv GEMV over the norm prologue (as w8a8_gemv_norm, M = 1) with the attention tail
-// (gemm_i8.hip att_tail): RoPE, the KV append at pos and the attention of every KV-head group run
-// in the same launch.  Returns (qkv bf16 [1, N], attention int8 [1, Hq * D], scales [Hq * D / 64, 16])
-// or None when no instantiation takes the geometry.  cnt: int32 [Hkv] zeros owned by the caller
-// (one per concurrently running decode), left zero by the kernel.
-std::optional<std::tuple<at::Tensor, at::Tensor, at::Tensor>> w8a8_gemv_norm_att(
-    const at::Tensor& parts, const at::Tensor& residual, const at::Tensor& gamma, double eps, const at::Tensor& res_out,
-    const at::Tensor& wp, const at::Tensor& sw, const std::optional<at::Tensor>& bias, int64_t K, at::Tensor& k_cache,
-    at::Tensor& v_cache, const at::Tensor& pos, const at::Tensor& lens, const std::optional<at::Tensor>& rope, int64_t rot,
-    int64_t Hq, double scale, at::Tensor& cnt) {
-  DEVICE_GUARD(parts);
-  need(parts, at::kFloat, "parts");
-  need(residual, at::kBFloat16, "residual");
-  need(gamma, at::kBFloat16, "gamma");
-  TORCH_CHECK(parts.dim() == 3 && parts.size(1) == 1 && parts.size(2) == K, "parts must be [S, 1, K]");
-  TORCH_CHECK(residual.numel() == K && gamma.numel() == K, "residual [1, K] / gamma [K]");
-  need(res_out, at::kBFloat16, "res_out");
-  TORCH_CHECK(res_out.numel() == K && res_out.data_ptr() != residual.data_ptr(), "res_out: [1, K], not residual");
-  check_cache(k_cache, "k_cache", k_cache.size(3));
-  check_cache(v_cache, "v_cache", k_cache.size(3));
-  TORCH_CHECK(k_cache.size(0) == 1 && k_cache.strides() == v_cache.strides(), "one sequence's caches [1, Hkv, S, D]");
-  const int64_t Hkv = k_cache.size(1), D = k_cache.size(3), N = (Hq + 2 * Hkv) * D;
-  check_w8a8_operands(wp, sw, bias, N, K);
-  need(pos, at::kInt, "pos");
-  need(lens, at::kInt, "lens");
-  TORCH_CHECK(pos.numel() == 1 && lens.numel() == 1, "one sequence");
-  need(cnt, at::kInt, "cnt");
-  TORCH_CHECK(cnt.numel() >= Hkv, "cnt: [Hkv] counters");
-  const float* cs = nullptr;
-  if (rot > 0) {
-    TORCH_CHECK(rope.has_value(), "rope table required for rot > 0");
-    need(*rope, at::kFloat, "rope");
-    TORCH_CHECK(rope->size(-2) * 2 == rot, "rope table width must be rot/2");
-    cs = rope->data_ptr<float>();
-  }
-  auto y = at::empty({1, N}, residual.options());
-  auto q8 = at::empty({1, Hq * D}, residual.options().dtype(at::kChar));
-  auto s8 = at::empty({Hq * D / 64, 16}, residual.options().dtype(at::kFloat));
-  const int rc = edge_w8a8_gemv_norm_att(
-      parts.data_ptr<float>(), (int)parts.size(0), residual.data_ptr(), gamma.data_ptr(), (float)eps, res_out.data_ptr(),
-      wp.data_ptr(), sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr, y.data_ptr(), (int)K, (int)Hq, (int)Hkv,
-      (int)D, k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(1), pos.data_ptr<int>(), lens.data_ptr<int>(), cs,
-      (int)rot, (float)scale, q8.data_ptr(), s8.data_ptr<float>(), 16, cnt.data_ptr<int>(), stream());
-  if (rc == -2) return std::nullopt;
-  check(rc, "w8a8_gemv_norm_att");
-  return std::make_tuple(y, q8, s8);
-}
-
 // gate_up projection (16-blocked rows) fused with silu(g) * u: returns bf16 h [M, N/2].
 at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                          const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
@@ -935,7 +883,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rms_norm_parts", &rms_norm_parts);
   m.def("w8a8_gemm_gluq", &w8a8_gemm_gluq);
   m.def("w8a8_gemv_norm", &w8a8_gemv_norm, "batch-1 W8A8 GEMV with the RMSNorm of split-K slices in its prologue");
-  m.def("w8a8_gemv_norm_att", &w8a8_gemv_norm_att, "batch-1 qkv GEMV (norm prologue) with the decode attention tail");
   m.def("gemv_norm_on", []() { return edge_w8a8_gemv_norm_on() != 0; });
   m.def("w8a8_gemm_geluq", &w8a8_gemm_geluq, "W8A8 GEMV + GELU + per-(token, 64) int8 quantisation (M <= 64)");
   m.def("group_quant", &group_quant);

@@ -141,14 +141,10 @@ __device__ __forceinline__ EpiPre<(epi_units<MB, NTW, NW, EPI>() + NW - 1) / NW>
   return p;
 }
 
-typedef __attribute__((address_space(1))) uint32_t gu32;   // global-segment words for agent-scope atomics
-typedef __attribute__((address_space(1))) int gi32;
-
 // Reduce the KW partial fragments in `red` ([KW][NTW*MB][64] v4i) and write the outputs.
 // sa: per-token scales (A_TOKEN; may point to LDS), unused when SCALED.  EPI_GLUQ needs every
-// wave to arrive (it holds a workgroup barrier).  WT (EPI_OUT, M = 1): the row is stored write-
-// through (sc1 dword stores of bf16 pairs) for a consumer workgroup of the same launch (att_tail).
-template <int MB, int NTW, int NW, int KW, bool SCALED, int EPI, bool WT = false, int OWN>
+// wave to arrive (it holds a workgroup barrier).
+template <int MB, int NTW, int NW, int KW, bool SCALED, int EPI, int OWN>
 __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const float* sa, const EpiPre<OWN>& pre,
                                               void* __restrict__ outv, float* __restrict__ os, float (*gmax)[4][16],
                                               int M, int N, int NTt, int Mpad, int nt0, int wave, int lane, int ks = 0) {
@@ -196,15 +192,6 @@ __device__ __forceinline__ void gemv_epilogue(const v4i* __restrict__ red, const
       if (f >= F || nt0 + t >= NTt) continue;
       const v4i tot = total(f);
       const int col = (nt0 + t) * 16 + (lane & 15);
-      if constexpr (WT) {                       // row 0 sits in lanes 0-15, element 0
-        static_assert(MB == 1, "write-through rows: M = 1");
-        const float v = (SCALED ? __builtin_bit_cast(v4f, tot)[0] : (float)tot[0] * sa[0]) * pre.s0[o] + pre.b0[o];
-        const uint32_t b = f2bf(v);
-        const uint32_t hi = __shfl_down(b, 1, 64);
-        if (lane < 16 && (lane & 1) == 0 && col < N)
-          __hip_atomic_store((gu32*)(out + col), b | (hi << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        continue;
-      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = i * 16 + 4 * (lane >> 4) + q;
@@ -347,275 +334,8 @@ struct NormIn {
   bf16_t* res_out;        // [M][K] residual out (must not alias res: other workgroups still read it)
   float eps;
   int S;
-  // ATT (batch-1 qkv GEMV with the attention tail, see att_tail): the layer's caches of the one
-  // sequence, its positions, the rope table, the int8 attention output and the arrival counters
-  int* att_cnt;           // [Hkv] zero between launches (the last arriver resets its entry)
-  bf16_t* kc;             // [Hkv][S_max][D] head-major K cache of this sequence
-  bf16_t* vc;
-  int64_t c_sh;           // head stride (elements)
-  const int* pos;         // [1] cache position of the new token
-  const int* lens;        // [1] keys after the append (pos + 1)
-  const float* cs;        // rope table [max_pos][rot/2] float2 (cos, sin), or null
-  int rot;
-  int8_t* out_q;          // [Hq * D] int8 attention output
-  float* out_s;           // [(Hq * D) / 64][Mpad] per-64-column scales
-  int Mpad, Hq, Hkv;
-  float scale_log2;       // softmax scale * log2(e)
 };
 constexpr int NRM_ROWS = 4;
-
-// ------------------------------------------------------------------------------ attention tail
-// Batch-1 decode: the qkv GEMV's workgroups own 16-column tiles of the [q | k | v] row; the tiles of
-// one KV-head group (its G query heads, its key, its value: (G + 2) D / 16 tiles) are spread over
-// several workgroups.  After writing its tiles, a workgroup adds its tile count for each group to
-// that group's arrival counter (release fence, device-scope atomic); the workgroup that completes a
-// group (acquire fence) runs that group's decode attention — RoPE, the KV append, an online
-// softmax over the keys split across its 16 waves, the merge in LDS and the per-(token, 64) int8
-// output for the W8A8 o-projection — and resets the counter.  Nothing ever waits on another
-// workgroup, and the separate attention launch (and its ramp) disappears.
-
-// 16 B of the handed-off row at element e: an sc1 buffer load (bypasses this CU's L1, which may hold
-// stale lines of it; aux 16 = sc1)
-__device__ __forceinline__ uint4 row_ld(__amdgpu_buffer_rsrc_t rs, int e) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, e * 2, 0, 16));
-}
-
-// Rotate the 8 values at row element h0 + e0 (HF rotate_half over the head at h0), the partner half
-// read from the row.
-__device__ __forceinline__ void att_rope8(__amdgpu_buffer_rsrc_t rs, int h0, int e0, int rot, const float2* csp,
-                                          float (&v)[8]) {
-  const int half = rot / 2;
-  const bool lo = e0 < half;
-  const int pe = lo ? e0 + half : e0 - half;
-  const int fi = lo ? e0 : e0 - half;
-  float p[8];
-  unpack8(row_ld(rs, h0 + pe), p);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float2 r = csp[fi + j];
-    v[j] = lo ? (v[j] * r.x - p[j] * r.y) : (v[j] * r.x + p[j] * r.y);
-  }
-}
-
-// One KV-head group's attention over the workgroup's NWV waves.  lds: >= NWV * (G * D + 2 G) + 2 G floats.
-template <int D, int G, int NWV>
-__device__ __forceinline__ void att_group(const NormIn& at, const bf16_t* __restrict__ row, int g, float* lds,
-                                          int wave, int lane) {
-  constexpr int LPK = D / 8, KPW = 64 / LPK, KPB = KPW * NWV, UN = G * D >= 512 ? 1 : G >= 4 ? 2 : 4, STEP = KPB * UN;
-  const int dl = lane % LPK, kl = lane / LPK, d0 = dl * 8;
-  const int pos = at.pos[0], nl = at.lens[0] - 1;             // cache keys [0, nl); key nl = the new one
-  const bf16_t* kb = at.kc + (size_t)g * at.c_sh;
-  const bf16_t* vb = at.vc + (size_t)g * at.c_sh;
-  uint4 kr[UN], vr[UN];
-  auto load = [&](int base) {
-#pragma unroll
-    for (int u = 0; u < UN; ++u) {
-      const int k = base + kl + u * KPB;
-      const size_t off = (size_t)(k < nl ? k : 0) * D + d0;
-      kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + off)));
-      vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + off)));
-    }
-  };
-  const int base0 = wave * KPW;
-  if (base0 < nl) load(base0);                                // first chunk in flight across the q work
-  const float2* csp = at.rot > 0 ? reinterpret_cast<const float2*>(at.cs) + (size_t)pos * (at.rot / 2) : nullptr;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(row), 0, (at.Hq + 2 * at.Hkv) * D * 2, 0x00020000);
-  float qf[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const int qh = (g * G + h) * D;
-    unpack8(row_ld(rs, qh + d0), qf[h]);
-    if (d0 < at.rot) {
-      att_rope8(rs, qh, d0, at.rot, csp, qf[h]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[h][j] = bf2f(f2bf(qf[h][j]));   // q is bf16 in the unfused path
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[h][j] *= at.scale_log2;
-  }
-  // the new key / value: every lane rebuilds its 8 dims; wave 0's first key group appends them
-  float kn[8], vn[8];
-  {
-    const int kh = (at.Hq + g) * D, vh = (at.Hq + at.Hkv + g) * D;
-    unpack8(row_ld(rs, kh + d0), kn);
-    if (d0 < at.rot) att_rope8(rs, kh, d0, at.rot, csp, kn);
-    unpack8(row_ld(rs, vh + d0), vn);
-    if (wave == 0 && kl == 0) {
-      *reinterpret_cast<uint4*>(at.kc + (size_t)g * at.c_sh + (size_t)pos * D + d0) = pack8(kn);
-      *reinterpret_cast<uint4*>(at.vc + (size_t)g * at.c_sh + (size_t)pos * D + d0) = pack8(vn);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { kn[j] = bf2f(f2bf(kn[j])); vn[j] = bf2f(f2bf(vn[j])); }   // the cached values
-  }
-  float m[G], l[G], acc[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    m[h] = -INFINITY;
-    l[h] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
-  }
-  if (wave == 0) {                                            // the new key seeds wave 0's softmax
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      float sp = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sp += qf[h][j] * kn[j];
-#pragma unroll
-      for (int o = LPK / 2; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 64);
-      m[h] = sp;
-      if (kl == 0) {
-        l[h] = 1.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[h][j] = vn[j];
-      }
-    }
-  }
-  for (int base = base0; base < nl; base += STEP) {          // wave-uniform trip count (shuffles inside)
-    if (base != base0) load(base);
-    float sc[UN][G];
-#pragma unroll
-    for (int u = 0; u < UN; ++u) {
-      float kf[8];
-      unpack8(kr[u], kf);
-#pragma unroll
-      for (int h = 0; h < G; ++h) {
-        float a = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a += qf[h][j] * kf[j];
-        sc[u][h] = a;
-      }
-    }
-#pragma unroll
-    for (int o = LPK / 2; o > 0; o >>= 1)
-#pragma unroll
-      for (int u = 0; u < UN; ++u)
-#pragma unroll
-        for (int h = 0; h < G; ++h) sc[u][h] += __shfl_xor(sc[u][h], o, 64);
-#pragma unroll
-    for (int u = 0; u < UN; ++u)
-      if (base + kl + u * KPB >= nl) {
-#pragma unroll
-        for (int h = 0; h < G; ++h) sc[u][h] = -INFINITY;
-      }
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      float cm = sc[0][h];
-#pragma unroll
-      for (int u = 1; u < UN; ++u) cm = fmaxf(cm, sc[u][h]);
-#pragma unroll
-      for (int o = LPK; o < 64; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
-      const float mn = fmaxf(m[h], cm);                       // finite: key `base` is in range
-      const float alpha = __builtin_amdgcn_exp2f(m[h] - mn);
-      m[h] = mn;
-      l[h] *= alpha;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[h][j] *= alpha;
-    }
-#pragma unroll
-    for (int u = 0; u < UN; ++u) {
-      float vf[8];
-      unpack8(vr[u], vf);
-#pragma unroll
-      for (int h = 0; h < G; ++h) {
-        const float p = __builtin_amdgcn_exp2f(sc[u][h] - m[h]);
-        l[h] += p;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[h][j] += p * vf[j];
-      }
-    }
-  }
-#pragma unroll
-  for (int o = LPK; o < 64; o <<= 1)
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      l[h] += __shfl_xor(l[h], o, 64);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[h][j] += __shfl_xor(acc[h][j], o, 64);
-    }
-  float* red = lds;                                           // [NWV][G][D]
-  float* wm = red + NWV * G * D;                              // [NWV][G]
-  float* wl = wm + NWV * G;                                   // [NWV][G]
-  float* lstat = wl + NWV * G;                                // [G]
-  if (lane == 0) {
-#pragma unroll
-    for (int h = 0; h < G; ++h) wm[wave * G + h] = m[h];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    float M = wm[h];
-#pragma unroll
-    for (int w = 1; w < NWV; ++w) M = fmaxf(M, wm[w * G + h]);
-    const float sc_w = m[h] == -INFINITY ? 0.f : exp2f(m[h] - M);   // a wave without keys: 0
-    if (kl == 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[(wave * G + h) * D + d0 + j] = acc[h][j] * sc_w;
-    }
-    if (lane == 0) wl[wave * G + h] = l[h] * sc_w;
-  }
-  __syncthreads();
-  if (threadIdx.x < G) {
-    float L = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) L += wl[w * G + threadIdx.x];
-    lstat[threadIdx.x] = L;
-  }
-  __syncthreads();
-  // G * D is a multiple of 64: each 64-column quant group is one wave of this loop
-  for (int i = threadIdx.x; i < G * D; i += NWV * 64) {
-    const int h = i / D, d = i - h * D;
-    float a = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) a += red[(w * G + h) * D + d];
-    const float v = bf2f(f2bf(a / lstat[h]));
-    const int col = (g * G + h) * D + d;
-    const float amax = fmaxf(wave_max(fabsf(v)), 1e-8f);
-    at.out_q[col] = quant_i8(v, 127.f / amax);
-    if (lane == 0) at.out_s[(size_t)(col >> 6) * at.Mpad] = amax / 127.f;
-  }
-  __syncthreads();                                            // LDS free for the next group
-}
-
-// The tail itself: count this workgroup's tiles per KV-head group, publish, run the completed groups.
-template <int D, int G, int NWV>
-__device__ __forceinline__ void att_tail(const NormIn& at, const bf16_t* __restrict__ row, int nt0, int ntw, int NTt,
-                                         float* lds, int wave, int lane) {
-  int* own = reinterpret_cast<int*>(lds);                     // [2] completed groups of this workgroup
-  // hand-off (counter form, write-through payload): every wave drains its sc1 row stores, the
-  // barrier, then one lane's relaxed agent-scope add per group; the workgroup whose add completes a
-  // group reads the row with sc1 loads only (no fence on either side)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    own[0] = own[1] = -1;
-    const int qcols = at.Hq * D, kcols = at.Hkv * D, total = (G + 2) * D / 16;
-    int grp[2] = {-1, -1}, cnt[2] = {0, 0};
-    for (int t = nt0; t < min(nt0 + ntw, NTt); ++t) {
-      const int c = t * 16;
-      const int gr = c < qcols ? c / D / G : (c < qcols + kcols ? (c - qcols) / D : (c - qcols - kcols) / D);
-      const int k = grp[0] == gr || grp[0] < 0 ? 0 : 1;
-      grp[k] = gr;
-      cnt[k] += 1;
-    }
-    int n = 0;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (grp[k] < 0) continue;
-      gi32* c = (gi32*)(at.att_cnt + grp[k]);
-      if (__hip_atomic_fetch_add(c, cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cnt[k] == total) {
-        __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // reset for the next launch
-        own[n++] = grp[k];
-      }
-    }
-  }
-  __syncthreads();
-  const int o0 = own[0], o1 = own[1];
-  __syncthreads();                                            // own[] read before the LDS is reused
-  if (o0 >= 0) att_group<D, G, NWV>(at, row, o0, lds, wave, lane);
-  if (o1 >= 0) att_group<D, G, NWV>(at, row, o1, lds, wave, lane);
-}
 
 template <int NCH, int SMAX>
 __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, int8_t* aq, float* nsa, float* nred) {
@@ -725,7 +445,7 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
   }
 }
 
-template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI, int NRM = 0, int ATT = 0>
+template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI, int NRM = 0>
 __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                  const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                                  const bf16_t* __restrict__ bias, void* __restrict__ outv,
@@ -914,16 +634,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     }
     __syncthreads();
   }
-  gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI, (ATT > 0)>(&red[0][0][0], NRM > 0 ? nsa : sa, pre, outv, os, gmax, M, N,
-                                                         NTt, Mpad, nt0, wave, lane, ks);
-  if constexpr (ATT > 0) {
-    // ATT 1: D 128, G 1 (Llama-2-7B); 2: D 128, G 4 (Llama-3-8B); 3: D 64, G 4 (Llama-3.2-1B)
-    constexpr int AD = ATT == 3 ? 64 : 128, AG = ATT == 1 ? 1 : 4;
-    static_assert(MB == 1 && NW == 16 && EPI == EPI_OUT, "attention tail: batch-1 qkv GEMV, 16 waves");
-    static_assert(sizeof(red) >= sizeof(float) * (NW * (AG * AD + 2 * AG) + 2 * AG) + 16, "attention tail LDS");
-    att_tail<AD, AG, NW>(na, reinterpret_cast<const bf16_t*>(outv), nt0, NTW, NTt, reinterpret_cast<float*>(&red[0][0][0]),
-                         wave, lane);
-  }
+  gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI>(&red[0][0][0], NRM > 0 ? nsa : sa, pre, outv, os, gmax, M, N, NTt, Mpad,
+                                              nt0, wave, lane, ks);
 }
 
 // ------------------------------------------------------------------------ LDS-staged activations
@@ -2273,11 +1985,11 @@ int launch_one(const void* A, const float* sa, const void* Wp, const float* sw, 
   return (int)hipGetLastError();
 }
 
-template <int NTW, int TG, int KW, int EP, int NRM, int ATT = 0>
+template <int NTW, int TG, int KW, int EP, int NRM>
 int launch_norm(const NormIn& na, const void* Wp, const float* sw, const void* bias, void* out, float* os, int M,
                 int N, int K, hipStream_t st) {
   const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_kernel<1, NTW, TG, KW, 2, A_TOKEN, EP, NRM, ATT>), dim3((NTt + NTW - 1) / NTW),
+  hipLaunchKernelGGL((w8a8_gemv_kernel<1, NTW, TG, KW, 2, A_TOKEN, EP, NRM>), dim3((NTt + NTW - 1) / NTW),
                      dim3(TG * KW * 64), 0, st, (const int8_t*)nullptr, (const float*)nullptr, (const int8_t*)Wp, sw,
                      (const bf16_t*)bias, out, os, M, N, K, K / 64, NTt, 16, 1, na);   // Mpad 16: scales [N/128][16]
   return (int)hipGetLastError();
@@ -2552,46 +2264,6 @@ extern "C" int edge_w8a8_gemv_norm(const float* part, int S, const void* res, co
   }
 #undef NRM_L
   return -2;
-}
-
-// Batch-1 qkv GEMV (norm prologue as above) with the attention tail (att_tail): `out` gets the bf16
-// [q | k | v] row, q8 / s8 the int8 attention output and its per-64-column scales ([Hq D / 64][Mpad]),
-// and the new key / value are appended at pos.  cnt: [Hkv] zeros (restored by the kernel).
-// -2: no instantiation for this geometry (D 128 with G 1 or 4, D 64 with G 4; K 2048 / 4096).
-extern "C" int edge_w8a8_gemv_norm_att(const float* part, int S, const void* res, const void* gamma, float eps,
-                                       void* res_out, const void* Wp, const float* sw, const void* bias, void* out,
-                                       int K, int Hq, int Hkv, int D, void* kc, void* vc, int64_t c_sh, const int* pos,
-                                       const int* lens, const float* cs, int rot, float scale, void* q8, float* s8,
-                                       int Mpad, int* cnt, hipStream_t st) {
-  const int G = Hkv > 0 ? Hq / Hkv : 0, N = (Hq + 2 * Hkv) * D;
-  const int att = (D == 128 && G == 1) ? 1 : (D == 128 && G == 4) ? 2 : (D == 64 && G == 4) ? 3 : 0;
-  if (!g_gemv_norm || att == 0 || G * Hkv != Hq || S < 1 || S > 4 || (K != 2048 && K != 4096) || res == nullptr ||
-      res_out == nullptr || res == res_out || cnt == nullptr || (rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)))
-    return -2;
-  NormIn na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};
-  na.att_cnt = cnt;
-  na.kc = (bf16_t*)kc;
-  na.vc = (bf16_t*)vc;
-  na.c_sh = c_sh;
-  na.pos = pos;
-  na.lens = lens;
-  na.cs = cs;
-  na.rot = rot;
-  na.out_q = (int8_t*)q8;
-  na.out_s = s8;
-  na.Mpad = Mpad;
-  na.Hq = Hq;
-  na.Hkv = Hkv;
-  na.scale_log2 = scale * 1.4426950408889634f;
-#define NRM_A(ATTV)                                                                                                 \
-  return K == 4096 ? (S <= 2 ? launch_norm<3, 1, 16, EPI_OUT, 18, ATTV>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)  \
-                             : launch_norm<3, 1, 16, EPI_OUT, 20, ATTV>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)) \
-                   : (S <= 2 ? launch_norm<3, 1, 16, EPI_OUT, 10, ATTV>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)  \
-                             : launch_norm<3, 1, 16, EPI_OUT, 12, ATTV>(na, Wp, sw, bias, out, nullptr, 1, N, K, st))
-  if (att == 1) NRM_A(1);
-  if (att == 2) NRM_A(2);
-  NRM_A(3);
-#undef NRM_A
 }
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).

@@ -724,7 +724,6 @@ def test_llama_batch1_decode_defers_norms(cuda, B, monkeypatch):
 
     qm.layers[1].attn.qkv.forward = spy
     monkeypatch.setattr(ops, "NORM_FUSE_MAX_ROWS", 4)      # the default fuses at batch 1 only
-    monkeypatch.setattr(ops, "ATT_TAIL_MAX_LEN", 0)        # qkv GEMV without the attention tail
     C = ops.ext()
     outs = []
     try:
