@@ -3,7 +3,7 @@
 set -o pipefail
 export PYTHONUNBUFFERED=1
 D=gpurun_out/r4v; mkdir -p $D
-for L in; do
+for L in 1 2; do
   timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 --lanes $L --kv-dtype int8 --latency-point off > $D/kv8_lanes$L.log 2>&1 || exit $?
 done
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
