@@ -112,12 +112,8 @@ class SlotDecoder:
         logits = self.model(st.tok.view(B, 1), ctx)
         nxt = ops.sample(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
                          sp.do_sample)
-        st.tok.copy_(nxt)
-        st.out.scatter_(1, st.step.view(1, 1).expand(B, 1), nxt.view(B, 1))
-        st.pos.add_(self.active)                        # free slots stay at position 0
-        st.seq_lens.add_(self.active)
-        st.rng[1:].add_(1)
-        st.step.add_(1)
+        # free slots stay at position 0 (increments = the active flags)
+        ops.decode_advance(nxt, st.tok, st.out, st.step, st.pos, st.seq_lens, st.rng, self.active)
 
     def _bucket(self, n: int) -> int:
         return min(self.gen.max_seq, ((n + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)

@@ -156,12 +156,7 @@ class Generator:
         logits = self.model(st.tok.view(B, 1), ctx)
         nxt = ops.sample(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
                          sp.do_sample)
-        st.tok.copy_(nxt)
-        st.out.scatter_(1, st.step.view(1, 1).expand(B, 1), nxt.view(B, 1))
-        st.pos.add_(1)
-        st.seq_lens.add_(1)
-        st.rng[1:].add_(1)
-        st.step.add_(1)
+        ops.decode_advance(nxt, st.tok, st.out, st.step, st.pos, st.seq_lens, st.rng)
 
     def _graph_for(self, st: _DecodeState, B: int, bucket: int, sp: SamplingParams):
         key = (B, bucket, sp.key(), id(st))

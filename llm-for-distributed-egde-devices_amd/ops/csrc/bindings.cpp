@@ -44,6 +44,8 @@ int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, fl
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, void* workspace, hipStream_t st);
 size_t edge_sample_workspace(int B, int V);
+int edge_decode_advance(const int64_t* nxt, int64_t* tok, int64_t* out, int64_t out_sb, int ncols, int64_t* step,
+                        int* pos, int* lens, int* rng, const int* inc, int B, hipStream_t st);
 void edge_sample_rowwide_min(int v);
 void edge_prefill_fa(int v, int stag);
 int edge_sample_timestamps(int enable, unsigned long long* host_out16);
@@ -820,6 +822,34 @@ at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& see
   return out;
 }
 
+// After the sampler: tok = nxt, out[:, step] = nxt, pos += inc, seq_lens += inc (inc: int32 [B] or
+// None = 1), rng[1] += 1, step += 1 (one launch; the decode state's buffers, all on the sampler's device).
+void decode_advance(const at::Tensor& nxt, at::Tensor& tok, at::Tensor& out, at::Tensor& step, at::Tensor& pos,
+                    at::Tensor& seq_lens, at::Tensor& rng, const std::optional<at::Tensor>& inc) {
+  DEVICE_GUARD(nxt);
+  need(nxt, at::kLong, "nxt");
+  need(tok, at::kLong, "tok");
+  need(out, at::kLong, "out");
+  need(step, at::kLong, "step");
+  need(pos, at::kInt, "pos");
+  need(seq_lens, at::kInt, "seq_lens");
+  need(rng, at::kInt, "rng");
+  const int64_t B = nxt.numel();
+  TORCH_CHECK(tok.numel() == B && pos.numel() == B && seq_lens.numel() == B && step.numel() == 1 && rng.numel() == 2,
+              "decode_advance: B-row state, one step counter, [seed, step] rng");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == B && out.stride(1) == 1, "out: [B, max_new] with contiguous rows");
+  TORCH_CHECK(nxt.is_contiguous() && tok.is_contiguous() && pos.is_contiguous() && seq_lens.is_contiguous() &&
+              rng.is_contiguous(), "decode_advance: contiguous state");
+  if (inc) {
+    need(*inc, at::kInt, "inc");
+    TORCH_CHECK(inc->numel() == B && inc->is_contiguous(), "inc: int32 [B]");
+  }
+  check(edge_decode_advance(nxt.data_ptr<int64_t>(), tok.data_ptr<int64_t>(), out.data_ptr<int64_t>(), out.stride(0),
+                            (int)out.size(1), step.data_ptr<int64_t>(), pos.data_ptr<int>(), seq_lens.data_ptr<int>(),
+                            rng.data_ptr<int>(), inc ? inc->data_ptr<int>() : nullptr, (int)B, stream()),
+        "decode_advance");
+}
+
 std::vector<int64_t> sample_timestamps(bool enable) {
   std::vector<unsigned long long> ts(16, 0);
   check(edge_sample_timestamps(enable ? 1 : 0, ts.data()), "sample_timestamps");
@@ -887,6 +917,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm_geluq", &w8a8_gemm_geluq, "W8A8 GEMV + GELU + per-(token, 64) int8 quantisation (M <= 64)");
   m.def("group_quant", &group_quant);
   m.def("sample", &sample);
+  m.def("decode_advance", &decode_advance, "decode-step bookkeeping after the sampler (one launch)");
   m.def("sample_timestamps", &sample_timestamps);
   m.def("rows128_ok", [](int64_t K, int64_t S) { return edge_w8a8_rows128_ok((int)K, (int)S) != 0; },
         "whether the 65-128 row decode GEMV has a kernel for K (in S split-K slices)");

@@ -655,7 +655,41 @@ __global__ void __launch_bounds__(NTR) topk_rowwide_kernel(const void* __restric
     if (seen != nullptr) seen[base + bi] = 1;
   }
 }
+
+// Decode-step bookkeeping after the sampler, one launch for what were five element-wise ops (each
+// a kernel boundary in the captured step: ~4.5 us apiece at batch 1): tok = nxt, out[:, step] =
+// nxt, pos += inc, seq_lens += inc (inc = 1, or the per-row active flags of a slot decoder), rng[1] += 1,
+// step += 1.  One workgroup: every thread reads step before the barrier, thread 0 advances it after.
+__global__ void __launch_bounds__(256) decode_advance_kernel(const int64_t* __restrict__ nxt, int64_t* __restrict__ tok,
+                                                             int64_t* __restrict__ out, int64_t out_sb, int ncols,
+                                                             int64_t* __restrict__ step, int* __restrict__ pos,
+                                                             int* __restrict__ lens, int* __restrict__ rng,
+                                                             const int* __restrict__ inc, int B) {
+  const int64_t s = step[0];
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int64_t t = nxt[b];
+    tok[b] = t;
+    if (s >= 0 && s < ncols) out[b * out_sb + s] = t;
+    const int d = inc != nullptr ? inc[b] : 1;
+    pos[b] += d;
+    lens[b] += d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    step[0] = s + 1;
+    rng[1] += 1;
+  }
+}
 }  // namespace
+
+extern "C" int edge_decode_advance(const int64_t* nxt, int64_t* tok, int64_t* out, int64_t out_sb, int ncols,
+                                   int64_t* step, int* pos, int* lens, int* rng, const int* inc, int B,
+                                   hipStream_t st) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(256), 0, st, nxt, tok, out, out_sb, ncols, step, pos, lens,
+                     rng, inc, B);
+  return (int)hipGetLastError();
+}
 
 // Rows at or above which the whole-row sampler form runs (V % 8 == 0, V <= 32K: 32 keys per
 // thread stay in registers, 64 spill; top_k <= 128);

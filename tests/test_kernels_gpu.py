@@ -346,3 +346,26 @@ def test_sampler_greedy_and_topk_support(cuda):
     p = torch.softmax(torch.tensor([2.0, 1.0, 0.5]), 0)
     assert counts[3:].sum() == 0
     assert torch.allclose(counts[:3] / 3000, p, atol=0.03)
+
+
+@pytest.mark.parametrize("B", [1, 3, 300])
+@pytest.mark.parametrize("with_inc", [False, True])
+def test_decode_advance_matches_torch_ops(cuda, B, with_inc):
+    """The one-launch decode bookkeeping (ops.decode_advance) == the element-wise torch ops it
+    replaces: tok, out column, pos / seq_lens increments (per-row flags for the slot decoder),
+    rng step and column counter; two steps in a row."""
+    g = torch.Generator().manual_seed(B)
+    state = dict(tok=torch.zeros(B, dtype=torch.long), out=torch.zeros(B, 7, dtype=torch.long),
+                 step=torch.tensor([2], dtype=torch.long), pos=torch.randint(0, 50, (B,), generator=g).int(),
+                 seq_lens=None, rng=torch.tensor([123, 4], dtype=torch.int32))
+    state["seq_lens"] = state["pos"] + 1
+    inc = torch.randint(0, 2, (B,), generator=g).int() if with_inc else None
+    ref = {k: v.clone() for k, v in state.items()}
+    gpu = {k: v.to(cuda) for k, v in state.items()}
+    for _ in range(2):
+        nxt = torch.randint(0, 32000, (B,), generator=g)
+        ops.decode_advance(nxt, ref["tok"], ref["out"], ref["step"], ref["pos"], ref["seq_lens"], ref["rng"], inc)
+        ops.decode_advance(nxt.to(cuda), gpu["tok"], gpu["out"], gpu["step"], gpu["pos"], gpu["seq_lens"], gpu["rng"],
+                           inc.to(cuda) if inc is not None else None)
+    for k in state:
+        assert torch.equal(gpu[k].cpu(), ref[k]), k
