@@ -173,9 +173,16 @@ def quantize_head(model: DecoderLM) -> DecoderLM:
     into the final norm): halves the head's 2 V H bytes, the largest single GEMM of a decode step
     (262 MB bf16 at Llama-2-7B), which is what the pipeline's last stage carries on top of its
     layers.  Off by default — the reference, like bitsandbytes and SmoothQuant, keeps the head in
-    16 bits.  Untied heads only (a tied head shares the embedding matrix)."""
+    16 bits.  A tied head (Llama-3.2-1B: the 525 MB embedding doubles as the head) gets an int8 copy
+    of the embedding matrix as its head; the embedding lookup keeps the bf16 table."""
     if model.lm_head is not None and not isinstance(model.lm_head, W8A8Linear):
         model.lm_head = W8A8Linear.from_float(model.lm_head, None)
+        model.head_quant = "w8a8"
+    elif model.lm_head is None and model.has_head and model.has_embed:
+        from types import SimpleNamespace
+        tied = SimpleNamespace(weight=model.embed, bias=None, in_features=model.cfg.hidden_size,
+                               out_features=model.cfg.vocab_size)
+        model.lm_head = W8A8Linear.from_float(tied, None)
         model.head_quant = "w8a8"
     return model
 

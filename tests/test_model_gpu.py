@@ -131,16 +131,20 @@ def test_w8a8_decode_beyond_gemv_rows(cuda, B):
     _rows_match_small_batch(model, prompts, B, cuda)
 
 
-@pytest.mark.parametrize("B", [4, 256])
-def test_int8_lm_head_close_to_bf16(cuda, B):
+@pytest.mark.parametrize("B", [1, 4, 256])
+@pytest.mark.parametrize("arch", ["llama2", "llama"])
+def test_int8_lm_head_close_to_bf16(cuda, B, arch):
     """quantize_head: W8A8 LM head (final norm emits int8 + scales, 16-blocked int8 GEMM) against
-    the bf16 head of the same W8A8 model: decode logits within 3 % relative, top-1 mostly equal."""
+    the bf16 head of the same W8A8 model: decode logits within 3 % relative, top-1 mostly equal.
+    "llama" ties the head to the embedding: the int8 head is a copy, the lookup stays bf16."""
     from edgellm.quant import quantize_head
-    cfg = tiny("llama2", hidden_size=512, num_heads=4, num_kv_heads=4, intermediate_size=1024, num_layers=2,
+    cfg = tiny(arch, hidden_size=512, num_heads=4, num_kv_heads=4, intermediate_size=1024, num_layers=2,
                vocab_size=4096)
+    assert cfg.tie_word_embeddings == (arch == "llama")
     base = quantize_model(build_model(cfg, device=cuda, seed=4), "w8a8")
     q8 = quantize_head(copy.deepcopy(base))
     assert q8.lm_head.takes_quantized_input
+    assert q8.embed.dtype == base.embed.dtype and torch.equal(q8.embed, base.embed)
     ids = torch.randint(0, cfg.vocab_size, (B, 9), generator=torch.Generator().manual_seed(2)).to(cuda)
     outs = []
     for m in (base, q8):

@@ -31,7 +31,7 @@ import torch  # noqa: E402
 import edgellm  # noqa: E402,F401
 from edgellm.engine import Generator, SamplingParams  # noqa: E402
 from edgellm.models import build_model, get_config  # noqa: E402
-from edgellm.quant import quantize_model, synthetic_calibration  # noqa: E402
+from edgellm.quant import quantize_head, quantize_model, synthetic_calibration  # noqa: E402
 
 # BASELINE.md (ACL.pdf p.7 Table 3): tokens/sec on an A100 40GB, batch 1
 PUBLISHED = {("phi-2", "fp"): 42.0725, ("pythia-1b", "fp"): 104.1318, ("llama-3.2-1b", "fp"): 51.8408,
@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=64)
     ap.add_argument("--new-tokens", type=int, default=200)
     ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--lm-head", default="bf16", choices=["bf16", "int8"],
+                    help="int8: W8A8 LM head for the quantised modes (quant.quantize_head; the reference keeps "
+                         "its head in 16 bits, so such rows are labelled '+int8_head')")
     a = ap.parse_args()
     dev = torch.device("cuda")
     for name in a.models.split(","):
@@ -57,6 +60,8 @@ def main():
             if mode != "none":
                 calib = synthetic_calibration(cfg, n=4, T=64, device=dev) if mode == "w8a8_smoothquant" else None
                 model = quantize_model(model, mode, calib_ids=calib)
+                if a.lm_head == "int8" and mode == "w8a8_smoothquant":
+                    model = quantize_head(model)
             gen = Generator(model, max_batch=1, max_seq=a.prompt_len + a.new_tokens + 8)
             gen.generate(prompt, sp, seed=1)               # warm-up (graph capture, allocator)
             best = None
@@ -68,7 +73,8 @@ def main():
                 wall = time.perf_counter() - t0
                 steps = sorted(res.step_ms) if res.step_ms else [float("nan")]
                 pub = PUBLISHED.get((name, "fp" if mode == "none" else "int8"))
-                row = dict(model=name, mode=mode, batch=1, prompt_len=a.prompt_len, new_tokens=res.num_generated,
+                label = mode + ("+int8_head" if a.lm_head == "int8" and mode == "w8a8_smoothquant" else "")
+                row = dict(model=name, mode=label, batch=1, prompt_len=a.prompt_len, new_tokens=res.num_generated,
                            tps_incl_prompt=round(res.tps_incl_prompt(), 1), tps_generated=round(res.tps_generated(), 1),
                            wall_s=round(wall, 4), p50_step_ms=round(steps[len(steps) // 2], 3),
                            published_tps=pub, vs_published=round(res.tps_incl_prompt() / pub, 1) if pub else None)
