@@ -416,6 +416,12 @@ static int g_target_wg = 512;   // >= 2 workgroups per CU before splitting K
 static int g_attn_occ = 4;
 // query-head split for small grids (tune "decode_attn_gsplit"): 0 automatic, 1 off, 2 always (GQA)
 static int g_attn_gsplit = 0, g_attn_early = 1;
+// MHA grids below this many workgroups (batch 1: 32 on Llama-2-7B) take the double-buffered form:
+// each workgroup walks its keys in several chunks, and there the next chunk in flight beats the
+// single-buffered form's extra occupancy (tools/recipes/r4occ_b1.sh: 1 x 200 keys 8.71 -> 7.95 us,
+// batch-1 Llama-2-7B 1.960 -> 1.919 ms; 16 x 200 is slower, 16.6 vs 14.6 us).  Tune "decode_attn_small".
+static int g_attn_small_wg = 64;
+extern "C" void edge_decode_attn_small(int v) { g_attn_small_wg = v; }
 extern "C" void edge_decode_attn_gsplit(int v) { g_attn_gsplit = v; }
 extern "C" void edge_decode_attn_early(int v) { g_attn_early = v; }
 extern "C" void edge_decode_attn_config(int target_wg) { g_target_wg = target_wg > 0 ? target_wg : 512; }
@@ -425,7 +431,7 @@ namespace {
 template <int D, int G, bool DI, bool FU, bool QO>
 void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q_sb, void* k_cache, void* v_cache,
                  int64_t c_sb, int64_t c_sh, const int* seq_lens, float sl2, int ch, int nsplit, void* out,
-                 int64_t o_sb, float* part_acc, float* part_ml, const Fuse& fz) {
+                 int64_t o_sb, float* part_acc, float* part_ml, const Fuse& fz, bool small_grid) {
 #define ATTN_ARGS grid, dim3(NT), lds, st, (const bf16_t*)q, q_sb, (bf16_t*)k_cache, (bf16_t*)v_cache, c_sb, c_sh, \
                   seq_lens, sl2, ch, nsplit, (bf16_t*)out, o_sb, part_acc, part_ml, fz
   if constexpr (FU) {                           // the model's decode step: barrier-free form selectable
@@ -434,7 +440,7 @@ void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q
     constexpr int OCC4 = G <= 2 ? 4 : (G == 4 ? 2 : 1), OCC5 = G <= 2 ? 5 : OCC4;
     // (8- and 16-wave workgroups for batch-1 grids measured slower: Llama-3.2-1B decode step
     // 1.08 -> 1.19 ms with 8 waves)
-    if (g_attn_occ == 4) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4>), ATTN_ARGS); return; }
+    if (g_attn_occ == 4 && !small_grid) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4>), ATTN_ARGS); return; }
     if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC5>), ATTN_ARGS); return; }
   }
   hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 0>), ATTN_ARGS);
@@ -489,9 +495,10 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
   const size_t lds = (size_t)(NW * G * D + 2 * NW * G + 2 * G) * sizeof(float);
   const dim3 grid(nsplit, Hkv * gs, B);
   const bool direct = nsplit == 1;
+  const bool small_grid = G0 == 1 && direct && fused && B * Hkv < g_attn_small_wg;
 #define DK(DD, GG, DI, FU, QO)                                                                                     \
   launch_attn<DD, GG, DI, FU, QO>(grid, lds, st, q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, out, \
-                                  o_sb, part_acc, part_ml, fz)
+                                  o_sb, part_acc, part_ml, fz, small_grid)
 #define DLAUNCH(DD, GG)                                                     \
   do {                                                                      \
     if (direct) {                                                           \

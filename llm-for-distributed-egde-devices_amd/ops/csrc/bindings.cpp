@@ -93,6 +93,7 @@ int edge_gemm_bf16_ring(const void* A, const void* W, const void* bias, void* ou
 int edge_bf16_ring_splits(int N, int K);
 int edge_bf16_ring_min_rows();
 void edge_decode_attn_gsplit(int v);
+void edge_decode_attn_small(int v);
 void edge_decode_attn_early(int v);
 }
 
@@ -935,6 +936,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "prefill_prio") edge_w8a8_prefill_prio((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
+    else if (what == "decode_attn_small") edge_decode_attn_small((int)a);
     else if (what == "decode_attn_gsplit") edge_decode_attn_gsplit((int)a);
     else if (what == "decode_attn_early") edge_decode_attn_early((int)a);
     else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);

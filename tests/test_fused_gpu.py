@@ -27,10 +27,12 @@ def _close(a, b, atol, rtol=0.0):
 
 @pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 32, 128, 128), (32, 8, 128, 128), (32, 8, 64, 64), (32, 32, 80, 32),
                                           (8, 8, 256, 64), (12, 12, 64, 0)])
-@pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333)])
+@pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333), (200,), (513,)])
 @pytest.mark.parametrize("quant", [False, True])
 @pytest.mark.parametrize("occ", [0, 4, 5])
 def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant, occ):
+    """(one sequence: MHA grids below decode_attn_small workgroups take the double-buffered form
+    under the default occ 4)"""
     if quant and D % 64:
         pytest.skip("per-group output needs D % 64 == 0")
     C = ops.ext()

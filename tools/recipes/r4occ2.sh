@@ -1,0 +1,9 @@
+# Round-4: small MHA decode grids on the double-buffered attention form by default — tests and
+# the batch-1 points (Llama-2-7B bench latency point, the reference's 1B configs)
+set -o pipefail
+export PYTHONUNBUFFERED=1
+D=gpurun_out/r4occ2; mkdir -p $D
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fused_gpu.py tests/test_model_gpu.py tests/test_cogen_gpu.py > $D/tests.log 2>&1 || exit $?
+timeout -k 10 400 python3 bench.py --micro-batch 1 --lanes 1 --steps 64 --warmup 8 --latency-point off > $D/b1.log 2>&1 || exit $?
+EDGELLM_TUNE="decode_attn_small=0" timeout -k 10 400 python3 bench.py --micro-batch 1 --lanes 1 --steps 64 --warmup 8 --latency-point off > $D/b1_off.log 2>&1 || exit $?
+timeout -k 10 900 python3 tools/bench_reference_config.py --modes none,w8a8_smoothquant --repeats 3 > $D/refcfg.log 2>&1 || exit $?
