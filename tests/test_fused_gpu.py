@@ -43,6 +43,27 @@ def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant, occ):
         C.tune("decode_attn_occ", 4, 0)
 
 
+@pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 32, 128, 128), (32, 32, 80, 32), (8, 8, 256, 64), (12, 12, 64, 0),
+                                          (32, 8, 64, 64), (32, 8, 128, 128)])
+@pytest.mark.parametrize("lens", [(1,), (200,), (255, 3), (300,), (700,)])
+@pytest.mark.parametrize("small", [64, 0])
+@pytest.mark.parametrize("quant", [False, True])
+def test_decode_attention_small_grid_forms(cuda, Hq, Hkv, D, rot, lens, small, quant):
+    """Small grids: the double-buffered form MHA grids below 64 workgroups take by default
+    (decode_attn_small 64) and the single-buffered form (0 = routing off) against the reference;
+    GQA grids keep the query-head split either way."""
+    if quant and D % 64:
+        pytest.skip("per-group output needs D % 64 == 0")
+    C = ops.ext()
+    C.tune("decode_attn_small", small, 0)
+    try:
+        # (255,): one rotated key element lands within 1e-8 of zero, where the kernel's and torch's
+        # fp32 contractions round to different bf16 values: the cache is checked to 1 bf16 ulp there
+        _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant, exact_cache=False)
+    finally:
+        C.tune("decode_attn_small", 64, 0)
+
+
 @pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 8, 64, 64), (32, 8, 128, 128), (16, 2, 128, 64), (8, 4, 256, 64)])
 @pytest.mark.parametrize("lens", [(1, 17, 200), (4096, 1000, 3333), (300,)])
 @pytest.mark.parametrize("gsplit", [1, 2])
@@ -67,7 +88,7 @@ def test_decode_attention_gsplit(cuda, Hq, Hkv, D, rot, lens, gsplit, quant):
         C.tune("decode_attn_gsplit", 0, 0)
 
 
-def _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant):
+def _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant, exact_cache=True):
     cuda = torch.device("cuda")
     torch.manual_seed(3)
     B = len(lens)
@@ -84,7 +105,11 @@ def _check_decode_attention_fused(C, Hq, Hkv, D, rot, lens, quant):
     out, s = C.decode_attn_fused(qkv, pos, rope, kc, vc, sl, Hq, scale, max(lens), rot, quant)
     q = _ref.rope_kv_write(qkv, pos, rope, kr, vr, Hq, Hkv, D, rot)
     ref = _ref.decode_attention(q.view(B, Hq, D), kr, vr, sl, scale)
-    assert torch.equal(kc, kr) and torch.equal(vc, vr), "KV append differs from rope_kv_write"
+    if exact_cache:
+        assert torch.equal(kc, kr) and torch.equal(vc, vr), "KV append differs from rope_kv_write"
+    else:
+        assert torch.equal(vc, vr), "V append differs"
+        _close(kc, kr, 1e-6, 1 / 128)
     if quant:
         qr, sr = _ref.quant_per_group(ref.reshape(B, Hq * D))
         deq = out.float() * s[:, :B].t().repeat_interleave(64, 1)
