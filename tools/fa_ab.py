@@ -1,0 +1,65 @@
+#!/usr/bin/env python
+"""Interleaved A/B of the flash-prefill wave schedules (tune ``prefill_fa`` second value as the binding
+reads it: 2 staggered (the default), 1 lockstep) at the TTFT-relevant causal shapes: several rounds in
+one process, variants rotated each round, median TF/s per variant.  Round 4
+(profiles/fa_schedule_ab_r4.json): staggered 3.5-5.5 % over lockstep at D = 128, lockstep +1 % at
+D = 64; a staggered form without the one-step V-fragment window was 1-3 % slower and was not kept.
+
+    python tools/fa_ab.py [--rounds 5] [--out file.json]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import edgellm  # noqa: E402,F401
+from edgellm import ops  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from bench_ops import timeit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    C = ops.ext()
+    rows = []
+    for T, Hq, Hkv, s0, D in ((32768, 32, 8, 0, 128), (4096, 32, 8, 28672, 128), (8192, 32, 8, 0, 128),
+                              (2048, 32, 32, 0, 128), (1024, 32, 8, 0, 64)):
+        q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
+        kc = torch.randn(1, Hkv, s0 + T, D, device=dev).bfloat16()
+        vc = torch.randn_like(kc)
+        sp = torch.full((1,), s0, dtype=torch.int32, device=dev)
+        flops = 4 * T * (s0 + T / 2) * D * Hq
+        res = {2: [], 1: []}
+        order = [2, 1]
+        for r in range(a.rounds):
+            for stg in order[r % 2:] + order[:r % 2]:
+                C.tune("prefill_fa", 2, stg)
+                t = timeit(lambda: C.prefill_attn(q, kc, vc, sp, 1 / math.sqrt(D), True), iters=5,
+                           per_graph=2 if T >= 16384 else 10)
+                res[stg].append(flops / t / 1e6)
+        C.tune("prefill_fa", 1, 0)
+        row = dict(T=T, start=s0, Hq=Hq, Hkv=Hkv, D=D)
+        for stg, name in ((2, "staggered"), (1, "lockstep")):
+            v = sorted(res[stg])
+            row[name + "_TFLOPs_median"] = round(v[len(v) // 2], 1)
+            row[name + "_TFLOPs_all"] = [round(x, 1) for x in res[stg]]
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        del q, kc, vc
+        torch.cuda.empty_cache()
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
