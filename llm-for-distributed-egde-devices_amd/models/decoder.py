@@ -318,9 +318,27 @@ class DecoderLM(nn.Module):
     def head_weight(self) -> torch.Tensor:
         return self.embed if self.lm_head is None else self.lm_head.weight
 
-    def embed_tokens(self, ids: torch.Tensor, start_pos: torch.Tensor) -> torch.Tensor:
-        """ids [B, T] -> hidden [B*T, H]"""
+    def _first_norm_deferred(self, rows: int) -> bool:
+        """Whether the first layer's RMSNorm can run in its qkv GEMV's prologue at ``rows`` decode
+        rows: the embedding is then handed over as one fp32 split-K slice (no residual), which
+        saves the norm launch (batch 1)."""
+        if rows > ops.NORM_FUSE_MAX_ROWS or self.pos_embed is not None or self.cfg.parallel_residual:
+            return False
+        first = self.layers[0] if len(self.layers) else None
+        if first is None or not first.has_attn or first.norm1 is None or first.norm1.kind != "rms":
+            return False
+        qkv = first.attn.qkv
+        return bool(getattr(qkv, "takes_quantized_input", False) and
+                    getattr(qkv, "pending_norm_ok", lambda glu=False: False)())
+
+    def embed_tokens(self, ids: torch.Tensor, start_pos: torch.Tensor, decode: bool = False):
+        """ids [B, T] -> hidden [B*T, H] (``decode`` at batch 1 with a deferrable first norm: a
+        PartialSum [1, B*T, H] of fp32 rows, which the first norm sums like a split-K slice)."""
         B, T = ids.shape
+        if decode and ops.gpu_path(self.embed) and self._first_norm_deferred(B * T):
+            xf = ops.embedding(ids.reshape(-1), self.embed, out_f32=True)
+            if ops.gemv_norm_ok(xf.view(1, B * T, -1)):
+                return PartialSum(xf.view(1, B * T, -1))
         x = ops.embedding(ids.reshape(-1), self.embed)
         if self.pos_embed is not None:
             pos = (start_pos.long()[:, None] + torch.arange(T, device=ids.device)[None]).reshape(-1)
@@ -367,7 +385,7 @@ class DecoderLM(nn.Module):
                 logits: str = "last"):
         """First stage: ids [B, T]; later stages: hidden [B*T, H] from the previous stage.
         Returns logits on the last stage, otherwise the hidden handed to the next stage."""
-        x = self.embed_tokens(ids, ctx.start_pos) if self.has_embed else hidden
+        x = self.embed_tokens(ids, ctx.start_pos, decode=ctx.mode == "decode") if self.has_embed else hidden
         x, residual = self.forward_layers(x, ctx, None)
         if self.has_head:
             return self.head(x, residual, ctx, logits)

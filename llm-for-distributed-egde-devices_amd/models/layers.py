@@ -123,9 +123,9 @@ class Norm(nn.Module):
         ``x`` may be a PartialSum (split-K projection output), summed inside the norm kernel.
         ``defer`` (the consumer is a W8A8 GEMV that takes it): at <= 4 rows, y is a PendingNorm that
         the consumer's kernel computes, and residual_out is the buffer it fills."""
-        if defer and quant and isinstance(x, PartialSum) and self.kind == "rms" and residual is not None \
-                and ops.gemv_norm_ok(x.parts):
-            h = torch.empty(x.parts.shape[1], x.parts.shape[2], dtype=residual.dtype, device=residual.device)
+        if defer and quant and isinstance(x, PartialSum) and self.kind == "rms" and ops.gemv_norm_ok(x.parts):
+            # residual None: a stage's first norm, over the embedding as one fp32 slice
+            h = torch.empty(x.parts.shape[1], x.parts.shape[2], dtype=self.weight.dtype, device=x.parts.device)
             return PendingNorm(x.parts, residual, self.weight, self.eps, h), h
         if isinstance(x, PartialSum):
             if self.kind == "rms" and x.parts.is_cuda and ops.gpu_path(x.parts):

@@ -92,13 +92,13 @@ def gemv_norm_ok(parts) -> bool:
 
 def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
                    glu_quant: bool = False):
-    """Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual), per-token int8, with
+    """Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual (None: no residual)), per-token int8, with
     the norm in the GEMV's prologue; the new residual rows go to ``res_out``.  Returns bf16 y [M, N],
     or with ``glu_quant`` (16-blocked gate_up) the quantising SwiGLU's (q [M, N/2], scales
     [N/128, 16]);
     None when no kernel takes the shape (the caller runs the norm kernel instead)."""
-    r = ext().w8a8_gemv_norm(parts, residual.contiguous(), gamma, eps, res_out, w_packed, w_scale, bias, N, K,
-                             2 if glu_quant else 0)
+    r = ext().w8a8_gemv_norm(parts, residual.contiguous() if residual is not None else None, gamma, eps, res_out,
+                             w_packed, w_scale, bias, N, K, 2 if glu_quant else 0)
     if r is None:
         return None
     return r if glu_quant else r[0]
@@ -488,10 +488,13 @@ def max_softmax_prob(logits):
     return _ref.max_softmax_prob(logits)
 
 
-def embedding(ids, table):
+def embedding(ids, table, out_f32: bool = False):
+    """Rows of ``table`` (bf16) for ``ids``; ``out_f32``: as fp32 (exact), e.g. the one split-K slice
+    of a first norm deferred into the next GEMV (models.decoder.DecoderLM.embed_tokens)."""
     if _gpu(table):
-        return ext().embedding(ids.long().contiguous(), table)
-    return _ref.embedding(ids, table)
+        return ext().embedding(ids.long().contiguous(), table, out_f32)
+    out = _ref.embedding(ids, table)
+    return out.float() if out_f32 else out
 
 
 rope_tables = _ref.rope_tables

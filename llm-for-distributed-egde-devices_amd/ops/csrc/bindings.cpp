@@ -24,7 +24,8 @@ int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const 
 int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant, hipStream_t st);
 int edge_quant(const void* x, void* q, float* s, int rows, int H, hipStream_t st);
 int edge_group_quant(const void* x, void* q, float* s, int M, int K, int Mpad, hipStream_t st);
-int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, hipStream_t st);
+int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, int out_f32,
+                   hipStream_t st);
 int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st);
 int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, void* q_out, void* k_cache,
                        void* v_cache, int B, int T, int Hq, int Hkv, int D, int rot, int64_t c_sb, int64_t c_sh,
@@ -221,15 +222,16 @@ std::tuple<at::Tensor, at::Tensor> quant(const at::Tensor& x) {
   return {q, s};
 }
 
-at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table) {
+// out_f32: fp32 rows (the bf16 values, exact) — the one split-K "slice" a deferred first norm sums
+at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table, bool out_f32) {
   DEVICE_GUARD(ids);
   need(ids, at::kLong, "ids");
   need(table, at::kBFloat16, "table");
   auto os = ids.sizes().vec();
   os.push_back(table.size(1));
-  auto out = at::empty(os, table.options());
+  auto out = at::empty(os, out_f32 ? table.options().dtype(at::kFloat) : table.options());
   check(edge_embedding(ids.data_ptr<int64_t>(), table.data_ptr(), out.data_ptr(), (int)ids.numel(),
-                       (int)table.size(1), (int)table.size(0), stream()),
+                       (int)table.size(1), (int)table.size(0), out_f32 ? 1 : 0, stream()),
         "embedding");
   return out;
 }
@@ -706,19 +708,24 @@ std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
 // [M, N/2], scales [N/128, 16]); the new residual rows (sum + residual, bf16) are written to
 // res_out ([M, K], not aliasing residual).  Returns None when no kernel takes it.
 std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_norm(
-    const at::Tensor& parts, const at::Tensor& residual, const at::Tensor& gamma, double eps, const at::Tensor& res_out,
+    const at::Tensor& parts, const std::optional<at::Tensor>& residual, const at::Tensor& gamma, double eps,
+    const at::Tensor& res_out,
     const at::Tensor& wp, const at::Tensor& sw, const std::optional<at::Tensor>& bias, int64_t N, int64_t K,
     int64_t epi) {
   DEVICE_GUARD(parts);
   need(parts, at::kFloat, "parts");
-  need(residual, at::kBFloat16, "residual");
   need(gamma, at::kBFloat16, "gamma");
   check_w8a8_operands(wp, sw, bias, N, K);
   TORCH_CHECK(parts.dim() == 3 && parts.size(2) == K, "parts must be [S, M, K]");
   const int64_t M = parts.size(1);
-  TORCH_CHECK(residual.numel() == M * K && gamma.numel() == K, "residual [M, K] / gamma [K]");
+  TORCH_CHECK(gamma.numel() == K, "gamma [K]");
   need(res_out, at::kBFloat16, "res_out");
-  TORCH_CHECK(res_out.numel() == M * K && res_out.data_ptr() != residual.data_ptr(), "res_out: [M, K], not residual");
+  TORCH_CHECK(res_out.numel() == M * K, "res_out: [M, K]");
+  if (residual) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == M * K && res_out.data_ptr() != residual->data_ptr(),
+                "residual [M, K], not aliasing res_out");
+  }
   TORCH_CHECK(epi == 0 || epi == 2, "epi 0 (out) or 2 (quantising GLU)");
   const int64_t S = parts.size(0);
   if (!edge_w8a8_gemv_norm_on() || M < 1 || M > 4 || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % (epi == 2 ? 128 : 16) != 0)
@@ -726,12 +733,13 @@ std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_norm(
   at::Tensor y;
   std::optional<at::Tensor> s;
   if (epi == 0) {
-    y = at::empty({M, N}, residual.options());
+    y = at::empty({M, N}, res_out.options());
   } else {
-    y = at::empty({M, N / 2}, residual.options().dtype(at::kChar));
-    s = at::empty({N / 128, 16}, residual.options().dtype(at::kFloat));
+    y = at::empty({M, N / 2}, res_out.options().dtype(at::kChar));
+    s = at::empty({N / 128, 16}, res_out.options().dtype(at::kFloat));
   }
-  check(edge_w8a8_gemv_norm(parts.data_ptr<float>(), (int)S, residual.data_ptr(), gamma.data_ptr(), (float)eps,
+  check(edge_w8a8_gemv_norm(parts.data_ptr<float>(), (int)S, residual ? residual->data_ptr() : nullptr,
+                            gamma.data_ptr(), (float)eps,
                             res_out.data_ptr(), wp.data_ptr(), sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr,
                             y.data_ptr(), s ? s->data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, (int)epi,
                             stream()),
@@ -888,7 +896,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm", &norm);
   m.def("act", &act);
   m.def("quant", &quant);
-  m.def("embedding", &embedding);
+  m.def("embedding", &embedding, py::arg("ids"), py::arg("table"), py::arg("out_f32") = false);
   m.def("max_prob", &max_prob);
   m.def("rope_kv_write", &rope_kv_write, py::arg("qkv"), py::arg("start_pos"), py::arg("rope"), py::arg("k_cache"),
         py::arg("v_cache"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("rot"), py::arg("k2") = py::none(),

@@ -351,7 +351,8 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int e = min((c * 256 + t) * 8, H - 8);
-        rv[c] = *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e);
+        rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e)
+                                  : uint4{0u, 0u, 0u, 0u};                 // no residual (a stage's first norm)
 #pragma unroll
         for (int k = 0; k < SMAX; ++k)
           if (k < na.S) {
@@ -2238,15 +2239,16 @@ extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void*
 // residual), int8 per token, computed in the kernel's prologue (NormIn above).  epi 0 (EPI_OUT:
 // bf16 [M, N]) or 2 (EPI_GLUQ: 16-blocked gate_up -> SwiGLU -> int8 per 64 features, `os` scales
 // [N/128][16]).
-// K in {2048, 4096} (256 threads x NCH chunks of 8, NCH <= 2), 1 <= S <= 4; res_out written by
-// workgroup 0 and must not alias res.  -2: not taken.
+// K in {2048, 4096} (256 threads x NCH chunks of 8, NCH <= 2), 1 <= S <= 4; res may be null (no
+// residual: a stage's first norm over the embedding); res_out written by workgroup 0 and must not
+// alias res.  -2: not taken.
 static int g_gemv_norm = 1;      // 0: the norm stays a kernel of its own (A/B knob "gemv_norm")
 extern "C" void edge_w8a8_gemv_norm_cfg(int on) { g_gemv_norm = on; }
 extern "C" int edge_w8a8_gemv_norm_on() { return g_gemv_norm; }
 extern "C" int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* gamma, float eps,
                                    void* res_out, const void* Wp, const float* sw, const void* bias, void* out,
                                    float* os, int M, int N, int K, int epi, hipStream_t st) {
-  if (M < 1 || M > NRM_ROWS || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % 16 != 0 || res == nullptr || res_out == nullptr ||
+  if (M < 1 || M > NRM_ROWS || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % 16 != 0 || res_out == nullptr ||
       res == res_out)
     return -2;
   const NormIn na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};

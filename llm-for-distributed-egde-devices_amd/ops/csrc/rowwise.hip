@@ -270,14 +270,25 @@ __global__ void __launch_bounds__(NT) quant_kernel(const bf16_t* __restrict__ x,
 }
 
 // ----------------------------------------------------------------------------- embedding
+template <bool F32>
 __global__ void __launch_bounds__(NT) embed_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
-                                                   bf16_t* __restrict__ out, int H, int V) {
+                                                   void* __restrict__ out, int H, int V) {
   const size_t row = blockIdx.x;
   int64_t id = ids[row];
   id = id < 0 ? 0 : (id >= V ? V - 1 : id);
   const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)id * H);
-  uint4* dst = reinterpret_cast<uint4*>(out + row * H);
-  for (int e = threadIdx.x; e < H / 8; e += NT) dst[e] = src[e];
+  if constexpr (F32) {                                  // fp32 rows: the bf16 values widened (exact)
+    float4* dst = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + row * H);
+    for (int e = threadIdx.x; e < H / 8; e += NT) {
+      float v[8];
+      unpack8(src[e], v);
+      dst[2 * e] = make_float4(v[0], v[1], v[2], v[3]);
+      dst[2 * e + 1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  } else {
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(out) + row * H);
+    for (int e = threadIdx.x; e < H / 8; e += NT) dst[e] = src[e];
+  }
 }
 
 // ----------------------------------------------------------------------------- confidence
@@ -417,11 +428,12 @@ extern "C" int edge_quant(const void* x, void* q, float* s, int rows, int H, hip
   return (int)hipGetLastError();
 }
 
-extern "C" int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V,
+extern "C" int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, int out_f32,
                               hipStream_t st) {
   if (H % 8) return -2;
   if (rows == 0) return 0;
-  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, (bf16_t*)out, H, V);
+  if (out_f32) hipLaunchKernelGGL(embed_kernel<true>, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, out, H, V);
+  else hipLaunchKernelGGL(embed_kernel<false>, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, out, H, V);
   return (int)hipGetLastError();
 }
 

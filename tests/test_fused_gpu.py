@@ -768,3 +768,33 @@ def test_llama_batch1_decode_defers_norms(cuda, B, monkeypatch):
         del qm.layers[1].attn.qkv.forward
     assert seen == [False, True, False, False], seen        # prefill, decode (knob on), prefill, decode
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_first_norm_deferred_over_fp32_embedding(cuda, B, monkeypatch):
+    """At batch 1 (<= NORM_FUSE_MAX_ROWS rows) the first layer's RMSNorm runs in its qkv GEMV's
+    prologue over the embedding handed over as one fp32 slice with no residual
+    (DecoderLM.embed_tokens -> PartialSum): decode logits and the residual stream equal the
+    bf16-embedding path's bit for bit."""
+    from edgellm.engine import KVCache
+    from edgellm.models import AttnCtx, build_model, tiny
+    from edgellm.models.decoder import DecoderLM
+    from edgellm.quant import quantize_model
+    cfg = tiny("llama", hidden_size=2048, num_heads=16, num_kv_heads=4, intermediate_size=4096, num_layers=2)
+    qm = quantize_model(build_model(cfg, device=cuda, seed=6), "w8a8")
+    monkeypatch.setattr(ops, "NORM_FUSE_MAX_ROWS", 4)
+    T = 7
+    ids = torch.randint(0, cfg.vocab_size, (B, T), generator=torch.Generator().manual_seed(3)).to(cuda)
+    assert qm._first_norm_deferred(B)
+    outs = []
+    for on in (True, False):
+        if not on:
+            monkeypatch.setattr(DecoderLM, "_first_norm_deferred", lambda self, rows: False)
+        kv = KVCache(cfg, B, T + 4, dtype=qm.dtype, device=cuda)
+        sp = torch.zeros(B, dtype=torch.int32, device=cuda)
+        with torch.no_grad():
+            qm(ids, AttnCtx("prefill", B, T, sp, sp + T, T, kv.rows(0, B), qm.rope_table(cuda)), logits="last")
+            pos = torch.full((B,), T, dtype=torch.int32, device=cuda)
+            outs.append(qm(ids[:, -1:], AttnCtx("decode", B, 1, pos, pos + 1, T + 1, kv.rows(0, B),
+                                                qm.rope_table(cuda))).float())
+    assert torch.equal(outs[0], outs[1])
