@@ -94,6 +94,7 @@ class _DecodeState:
         self.step = torch.zeros(1, dtype=torch.long, device=device)       # column in out
         self.out = torch.zeros(B, max_new, dtype=torch.long, device=device)
         self.seen = torch.zeros(B, V, dtype=torch.uint8, device=device)
+        self.ctr = torch.zeros(1, dtype=torch.int32, device=device)       # sampler arrival counter
 
 
 class Generator:
@@ -154,9 +155,8 @@ class Generator:
         ctx = AttnCtx("decode", B, 1, st.pos, st.seq_lens, max_len, self.kv.rows(0, B), self.rope,
                       attn_hook=self.attn_hook)
         logits = self.model(st.tok.view(B, 1), ctx)
-        nxt = ops.sample(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
-                         sp.do_sample)
-        ops.decode_advance(nxt, st.tok, st.out, st.step, st.pos, st.seq_lens, st.rng)
+        ops.sample_advance(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
+                           st.tok, st.out, st.step, st.pos, st.seq_lens, st.ctr, sp.do_sample)
 
     def _graph_for(self, st: _DecodeState, B: int, bucket: int, sp: SamplingParams):
         key = (B, bucket, sp.key(), id(st))

@@ -482,6 +482,25 @@ def decode_advance(nxt, tok, out, step, pos, seq_lens, rng, inc=None) -> None:
     step.add_(1)
 
 
+FUSE_ADVANCE = os.environ.get("EDGELLM_FUSE_ADVANCE", "1") != "0"
+
+
+def sample_advance(logits, seen, temperature, top_k, top_p, repetition_penalty, rng, tok, out, step, pos, seq_lens,
+                   ctr, do_sample: bool = True):
+    """``sample`` then ``decode_advance`` (inc = 1); on the GPU the bookkeeping runs in the
+    sampler's last launch (one kernel boundary fewer per decode step).  ``ctr``: int32 [1] zero
+    buffer the kernel uses as an arrival counter (it stays zero between calls).  Returns nxt."""
+    if _gpu(logits) and FUSE_ADVANCE:
+        nxt = ext().sample_advance(logits, seen, float(temperature), int(top_k or 0),
+                                   float(top_p if top_p is not None else 1.0), float(repetition_penalty),
+                                   bool(do_sample), rng, tok, out, step, pos, seq_lens, ctr)
+        if nxt.numel() > 0 or logits.shape[0] == 0:
+            return nxt
+    nxt = sample(logits, seen, temperature, top_k, top_p, repetition_penalty, rng, do_sample)
+    decode_advance(nxt, tok, out, step, pos, seq_lens, rng)
+    return nxt
+
+
 def max_softmax_prob(logits):
     if _gpu(logits):
         return ext().max_prob(logits.contiguous())

@@ -45,6 +45,10 @@ int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, fl
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, void* workspace, hipStream_t st);
 size_t edge_sample_workspace(int B, int V);
+int edge_sample_advance(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
+                        float inv_temperature, float penalty, int top_k, float top_p, int do_sample, int* rng,
+                        int64_t* out_tok, void* workspace, int64_t* tok, int64_t* out, int64_t out_sb, int ncols,
+                        int64_t* step, int* pos, int* lens, int* ctr, hipStream_t st);
 int edge_decode_advance(const int64_t* nxt, int64_t* tok, int64_t* out, int64_t out_sb, int ncols, int64_t* step,
                         int* pos, int* lens, int* rng, const int* inc, int B, hipStream_t st);
 void edge_sample_rowwide_min(int v);
@@ -859,6 +863,44 @@ void decode_advance(const at::Tensor& nxt, at::Tensor& tok, at::Tensor& out, at:
         "decode_advance");
 }
 
+// sample + decode_advance (inc = 1) with the bookkeeping in the sampler's last launch.  ctr: int32 [1],
+// zero before the first call (each call leaves it zero).  Returns an empty tensor when the
+// configuration needs the host fallback (nothing was launched then).
+at::Tensor sample_advance(const at::Tensor& logits, const std::optional<at::Tensor>& seen, double temperature,
+                          int64_t top_k, double top_p, double penalty, bool do_sample, at::Tensor& rng, at::Tensor& tok,
+                          at::Tensor& out, at::Tensor& step, at::Tensor& pos, at::Tensor& seq_lens, at::Tensor& ctr) {
+  DEVICE_GUARD(logits);
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat);
+  need(rng, at::kInt, "rng");
+  need(tok, at::kLong, "tok");
+  need(out, at::kLong, "out");
+  need(step, at::kLong, "step");
+  need(pos, at::kInt, "pos");
+  need(seq_lens, at::kInt, "seq_lens");
+  need(ctr, at::kInt, "ctr");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  if (seen) { need(*seen, at::kByte, "seen"); TORCH_CHECK(seen->sizes() == logits.sizes()); }
+  TORCH_CHECK(tok.numel() == B && pos.numel() == B && seq_lens.numel() == B && step.numel() == 1 && rng.numel() == 2 &&
+              ctr.numel() >= 1, "sample_advance: B-row state, one step counter, [seed, step] rng, a counter");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == B && out.stride(1) == 1, "out: [B, max_new] with contiguous rows");
+  TORCH_CHECK(tok.is_contiguous() && pos.is_contiguous() && seq_lens.is_contiguous() && rng.is_contiguous(),
+              "sample_advance: contiguous state");
+  auto nxt = at::empty({B}, logits.options().dtype(at::kLong));
+  auto ws = at::empty({(int64_t)edge_sample_workspace((int)B, (int)V)}, logits.options().dtype(at::kByte));
+  const double inv_t = temperature > 0 ? 1.0 / temperature : 1.0;
+  const int rc = edge_sample_advance(logits.data_ptr(), bf, seen ? seen->data_ptr<uint8_t>() : nullptr, (int)B, (int)V,
+                                     (float)temperature, (float)inv_t, (float)penalty, (int)top_k, (float)top_p,
+                                     do_sample, rng.data_ptr<int>(), nxt.data_ptr<int64_t>(), ws.data_ptr(),
+                                     tok.data_ptr<int64_t>(), out.data_ptr<int64_t>(), out.stride(0), (int)out.size(1),
+                                     step.data_ptr<int64_t>(), pos.data_ptr<int>(), seq_lens.data_ptr<int>(),
+                                     ctr.data_ptr<int>(), stream());
+  if (rc == -5) return at::Tensor();
+  check(rc, "sample_advance");
+  return nxt;
+}
+
 std::vector<int64_t> sample_timestamps(bool enable) {
   std::vector<unsigned long long> ts(16, 0);
   check(edge_sample_timestamps(enable ? 1 : 0, ts.data()), "sample_timestamps");
@@ -926,6 +968,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm_geluq", &w8a8_gemm_geluq, "W8A8 GEMV + GELU + per-(token, 64) int8 quantisation (M <= 64)");
   m.def("group_quant", &group_quant);
   m.def("sample", &sample);
+  m.def("sample_advance", &sample_advance, "sampler + decode-step bookkeeping in the sampler's last launch");
   m.def("decode_advance", &decode_advance, "decode-step bookkeeping after the sampler (one launch)");
   m.def("sample_timestamps", &sample_timestamps);
   m.def("rows128_ok", [](int64_t K, int64_t S) { return edge_w8a8_rows128_ok((int)K, (int)S) != 0; },

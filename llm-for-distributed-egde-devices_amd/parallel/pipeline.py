@@ -250,10 +250,15 @@ class PipelineStage:
                       attn_hook=self.attn_hook)
         out = self.model(self.tok[m].view(b, 1) if self.is_first else None, ctx,
                          hidden=None if self.is_first else self.hin[m])
-        if self.is_last:
-            self._sample(m, out)
-        else:
-            self.hout[m].copy_(out)
+        if self.is_last:                              # sampler + bookkeeping (pos / lens += 1 included)
+            sp = self.sampling
+            nxt = ops.sample_advance(out, self.seen[m], sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty,
+                                     self.rng[m], self.tok[m], self.out[m], self.step[m], self.pos[m], self.lens[m],
+                                     self.ctr[m], sp.do_sample)
+            if self._eos is not None:
+                self.hit[m].logical_or_(nxt.eq(self._eos))
+            return
+        self.hout[m].copy_(out)
         self.pos[m].add_(1)
         self.lens[m].add_(1)
 
@@ -352,6 +357,7 @@ class PipelineStage:
             self.rng = [torch.tensor([(seed + 7919 * m) & 0x7FFFFFFF, 0], dtype=torch.int32, device=dev)
                         for m in range(M)]
             self.step = [torch.zeros(1, dtype=torch.long, device=dev) for _ in range(M)]
+            self.ctr = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(M)]   # sampler counters
             self.out = [torch.zeros(b, S + 1, dtype=torch.long, device=dev) for _ in range(M)]
         # repetition-penalty history needs the prompt ids on the last stage
         pdev = "cpu" if self.host_staged else dev

@@ -84,3 +84,27 @@ def test_ragged_batched_prefill_matches_one_at_a_time():
         for p, toks in zip(prompts, res.tokens):
             alone = Generator(m, max_batch=1, max_seq=64).generate([p], sp)
             assert toks == alone.tokens[0], arch
+
+
+def test_sample_advance_is_sample_then_decode_advance():
+    """ops.sample_advance (the decode step's sampler + bookkeeping) == ops.sample followed by
+    ops.decode_advance on the CPU path; the GPU fused launch is pinned against the same pair in
+    tests/test_kernels_gpu.py::test_sample_advance_matches_sample_then_advance."""
+    from edgellm import ops
+    g = torch.Generator().manual_seed(0)
+    B, V = 3, 97
+    mk = lambda: dict(tok=torch.zeros(B, dtype=torch.long), out=torch.zeros(B, 4, dtype=torch.long),  # noqa: E731
+                      step=torch.tensor([0]), pos=torch.tensor([5, 6, 7], dtype=torch.int32),
+                      lens=torch.tensor([6, 7, 8], dtype=torch.int32), rng=torch.tensor([11, 0], dtype=torch.int32),
+                      seen=torch.zeros(B, V, dtype=torch.uint8))
+    a, b = mk(), mk()
+    ctr = torch.zeros(1, dtype=torch.int32)
+    for _ in range(3):
+        logits = torch.randn(B, V, generator=g)
+        nxt = ops.sample(logits, a["seen"], 0.8, 10, 0.9, 1.1, a["rng"], True)
+        ops.decode_advance(nxt, a["tok"], a["out"], a["step"], a["pos"], a["lens"], a["rng"])
+        nb = ops.sample_advance(logits, b["seen"], 0.8, 10, 0.9, 1.1, b["rng"], b["tok"], b["out"], b["step"],
+                                b["pos"], b["lens"], ctr, True)
+        assert torch.equal(nb, nxt)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k

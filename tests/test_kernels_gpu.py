@@ -369,3 +369,40 @@ def test_decode_advance_matches_torch_ops(cuda, B, with_inc):
                            inc.to(cuda) if inc is not None else None)
     for k in state:
         assert torch.equal(gpu[k].cpu(), ref[k]), k
+
+
+@pytest.mark.parametrize("B", [1, 3, 130])
+@pytest.mark.parametrize("cfg", ["greedy", "full", "topk50_topp0.9", "topk300", "topk50_rowwide"])
+def test_sample_advance_matches_sample_then_advance(cuda, B, cfg):
+    """The sampler with the decode bookkeeping in its last launch (ops.sample_advance: every
+    final-kernel form — argmax merge, top-k merge, whole-row, single-workgroup) == ops.sample then
+    ops.decode_advance: same tokens, same state, three steps in a row (the arrival counter is
+    left at zero after each launch, so a captured step can replay)."""
+    C = ops.ext()
+    V = 32000
+    args = dict(greedy=(0.0, 0, 1.0, 1.1, False), full=(1.0, 0, 1.0, 1.0, True),
+                **{"topk50_topp0.9": (0.7, 50, 0.9, 1.1, True), "topk300": (0.8, 300, 0.95, 1.0, True),
+                   "topk50_rowwide": (0.7, 50, 0.9, 1.1, True)})[cfg]
+    g = torch.Generator().manual_seed(B + len(cfg))
+    pos = torch.randint(0, 50, (B,), generator=g).int()
+    state = dict(tok=torch.zeros(B, dtype=torch.long), out=torch.zeros(B, 5, dtype=torch.long),
+                 step=torch.tensor([1], dtype=torch.long), pos=pos, seq_lens=pos + 1,
+                 rng=torch.tensor([321, 9], dtype=torch.int32),
+                 seen=(torch.rand(B, V, generator=g) < 0.005).to(torch.uint8))
+    ref = {k: v.to(cuda) for k, v in state.items()}
+    fused = {k: v.to(cuda) for k, v in state.items()}
+    ctr = torch.zeros(1, dtype=torch.int32, device=cuda)
+    try:
+        C.tune("sample_rowwide", 1 if cfg.endswith("rowwide") else 0, 0)
+        for _ in range(3):
+            logits = (torch.randn(B, V, generator=g) * 3).bfloat16().to(cuda)
+            nxt = ops.sample(logits, ref["seen"], *args[:4], ref["rng"], args[4])
+            ops.decode_advance(nxt, ref["tok"], ref["out"], ref["step"], ref["pos"], ref["seq_lens"], ref["rng"])
+            nf = C.sample_advance(logits, fused["seen"], args[0], args[1], args[2], args[3], args[4], fused["rng"],
+                                  fused["tok"], fused["out"], fused["step"], fused["pos"], fused["seq_lens"], ctr)
+            assert torch.equal(nf, nxt)
+            assert int(ctr.item()) == 0
+    finally:
+        C.tune("sample_rowwide", 128, 0)
+    for k in state:
+        assert torch.equal(fused[k], ref[k]), k
