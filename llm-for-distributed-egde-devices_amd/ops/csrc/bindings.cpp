@@ -52,6 +52,7 @@ int edge_sample_advance(const void* logits, int is_bf16, uint8_t* seen, int B, i
 int edge_decode_advance(const int64_t* nxt, int64_t* tok, int64_t* out, int64_t out_sb, int ncols, int64_t* step,
                         int* pos, int* lens, int* rng, const int* inc, int B, hipStream_t st);
 void edge_sample_rowwide_min(int v);
+void edge_sample_vec(int v);
 void edge_prefill_fa(int v, int stag);
 int edge_sample_timestamps(int enable, unsigned long long* host_out16);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
@@ -992,6 +993,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "decode_attn_early") edge_decode_attn_early((int)a);
     else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);
     else if (what == "sample_rowwide") edge_sample_rowwide_min((int)a);
+    else if (what == "sample_vec") edge_sample_vec((int)a);
     else if (what == "prefill_fa") edge_prefill_fa((int)a, b == 0 ? 1 : (int)b - 1);   // b: 0 default, 1 lockstep, 2 stagger
     else if (what == "gemv_norm") edge_w8a8_gemv_norm_cfg((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);

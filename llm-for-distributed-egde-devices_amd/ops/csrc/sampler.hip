@@ -315,13 +315,47 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
   if (threadIdx.x == 0) pc[(size_t)row * C + c] = ckey(bv, bi);
 }
 
+// Thread `o0 / EPT`'s run of EPT consecutive processed scores of a chunk (element o = o0 + j):
+// 16-byte logits loads and 8-byte `seen` loads when the run is whole and `vec` (V % 8 == 0, aligned
+// rows), else one element at a time.  Invalid elements are -inf.
+template <bool BF16, int EPT>
+__device__ __forceinline__ void load_run(const void* lg, const uint8_t* seen, size_t base, int c0, int o0, int nvalid,
+                                         bool vec, float inv_t, float pen, float (&sv)[EPT]) {
+  static_assert(EPT % 8 == 0, "runs of whole 8-element groups");
+  if (vec && o0 + EPT <= nvalid) {
+    const size_t e0 = base + c0 + o0;
+#pragma unroll
+    for (int q = 0; q < EPT / 8; ++q) {
+      float v[8];
+      if constexpr (BF16) {
+        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(lg) + e0 + 8 * q), v);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lg) + e0 + 8 * q);
+        const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lg) + e0 + 8 * q + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      const uint64_t sn = seen != nullptr ? *reinterpret_cast<const uint64_t*>(seen + e0 + 8 * q) : 0ull;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float x = v[u];
+        if ((sn >> (8 * u)) & 0xffu) x = x < 0.f ? x * pen : x / pen;
+        sv[8 * q + u] = x * inv_t;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j)
+      sv[j] = o0 + j < nvalid ? proc<BF16>(lg, seen, base, c0 + o0 + j, inv_t, pen) : -INFINITY;
+  }
+}
+
 // Per-chunk candidate superset -> pc[(row*C + c)*CCAP + s] as composite keys (unused slots 0),
-// pthr[row*C + c] = threshold key.
+// pthr[row*C + c] = threshold key.  Thread t holds the chunk's elements [t * EPT, (t + 1) * EPT).
 template <bool BF16, int EPT>
 __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__ logits,
                                                         const uint8_t* __restrict__ seen, int V, int C, float inv_t,
                                                         float pen, int top_k, uint64_t* __restrict__ pc,
-                                                        uint32_t* __restrict__ pthr) {
+                                                        uint32_t* __restrict__ pthr, int vec) {
   __shared__ uint32_t red[2 * NW];
   __shared__ int scr[2 * NW];
   __shared__ int cnt;
@@ -333,10 +367,10 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
   float sv[EPT];
   uint32_t kr[EPT];
   uint32_t kmin = 0xffffffffu, kmax = 0u;
+  load_run<BF16, EPT>(logits, seen, base, c0, tid * EPT, nvalid, vec != 0, inv_t, pen, sv);
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int o = j * NT + tid;
-    sv[j] = o < nvalid ? proc<BF16>(logits, seen, base, c0 + o, inv_t, pen) : -INFINITY;
+    const int o = tid * EPT + j;
     kr[j] = o < nvalid ? f2key(sv[j]) : 0u;
     if (o < nvalid) { kmin = min(kmin, kr[j]); kmax = max(kmax, kr[j]); }
   }
@@ -369,7 +403,7 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
   const size_t slot0 = ((size_t)row * C + c) * CCAP;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int o = j * NT + tid;
+    const int o = tid * EPT + j;
     const bool ok = o < nvalid && kr[j] >= thr;
     const int s = wave_alloc(ok, &cnt);
     if (ok && s < CCAP) pc[slot0 + s] = ckey(sv[j], c0 + o);
@@ -739,6 +773,9 @@ extern "C" int edge_decode_advance(const int64_t* nxt, int64_t* tok, int64_t* ou
 // tune key "sample_rowwide" (0 = never).
 static int g_sample_rowwide_min = 128;
 extern "C" void edge_sample_rowwide_min(int v) { g_sample_rowwide_min = v; }
+// Split top-k form: 16-byte score loads in the chunk kernel (tune key "sample_vec"; 0 = per element).
+static int g_sample_vec = 1;
+extern "C" void edge_sample_vec(int v) { g_sample_vec = v; }
 
 // Debug: enable/read the merge-phase timestamps (ticks of the 100 MHz wall clock).
 extern "C" int edge_sample_timestamps(int enable, unsigned long long* host_out16) {
@@ -785,8 +822,10 @@ static int sample_launch(const void* logits, int is_bf16, uint8_t* seen, int B, 
     else { if (ns <= 2) RW(false, 2); else RW(false, 4); }
 #undef RW
   } else if (mode == 2) {
+    const int vec = g_sample_vec && V % 8 == 0 && reinterpret_cast<uintptr_t>(logits) % 16 == 0 &&
+                    (seen == nullptr || reinterpret_cast<uintptr_t>(seen) % 8 == 0);
 #define TC(BF, E) hipLaunchKernelGGL((topk_chunk_kernel<BF, E>), g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, \
-                                     penalty, top_k, pc, pthr)
+                                     penalty, top_k, pc, pthr, vec)
     if (is_bf16) { if (ept == 8) TC(true, 8); else TC(true, 16); }
     else { if (ept == 8) TC(false, 8); else TC(false, 16); }
 #undef TC

@@ -292,7 +292,7 @@ def test_w8a8_gemv_variants(cuda, ntw, nw, u, M, N, K):
     _close(out, _ref.w8a8_linear(qx, sx, w, sw, None, torch.float32), 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("V", [512, 32000, 50304, 128256])
+@pytest.mark.parametrize("V", [512, 1001, 32000, 50304, 100008, 128256])   # 1001 / 100008: per-element loads, partial runs
 @pytest.mark.parametrize("cfg", [(0.7, 50, 0.9, 1.1), (0.5, 30, 0.85, 1.2), (1.0, 0, 1.0, 1.0), (0.8, 20, 1.0, 1.3),
                                  (0.9, 200, 0.95, 1.0), (0.0, 0, 1.0, 1.3)])
 @pytest.mark.parametrize("form", ["split", "rowwide"])
