@@ -287,34 +287,6 @@ __device__ __forceinline__ void pad8(uint64_t* fc, int n) {
   if (t < ((n + 7) & ~7)) fc[t] = 0ull;
 }
 
-// ---------------------------------------------------------------- phase 1
-// Per-chunk best composite (value, then lower id) of the processed (MODE 1: + Gumbel noise)
-// scores -> pc[row*C + c].
-template <bool BF16, int MODE, int EPT>
-__global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict__ logits,
-                                                          const uint8_t* __restrict__ seen, int V, int C, float inv_t,
-                                                          float pen, const int* __restrict__ rng,
-                                                          uint64_t* __restrict__ pc) {
-  __shared__ float rv[NW];
-  __shared__ int ri[NW];
-  const int c = blockIdx.x, row = blockIdx.y;
-  const size_t base = (size_t)row * V;
-  const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
-  float bv = -INFINITY;
-  int bi = 0x7fffffff;
-#pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int i = c * (NT * EPT) + j * NT + threadIdx.x;
-    if (i < V) {
-      float s = proc<BF16>(logits, seen, base, i, inv_t, pen);
-      if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
-      if (better(s, i, bv, bi)) { bv = s; bi = i; }
-    }
-  }
-  block_argmax(bv, bi, rv, ri);
-  if (threadIdx.x == 0) pc[(size_t)row * C + c] = ckey(bv, bi);
-}
-
 // Thread `o0 / EPT`'s run of EPT consecutive processed scores of a chunk (element o = o0 + j):
 // 16-byte logits loads and 8-byte `seen` loads when the run is whole and `vec` (V % 8 == 0, aligned
 // rows), else one element at a time.  Invalid elements are -inf.
@@ -347,6 +319,37 @@ __device__ __forceinline__ void load_run(const void* lg, const uint8_t* seen, si
     for (int j = 0; j < EPT; ++j)
       sv[j] = o0 + j < nvalid ? proc<BF16>(lg, seen, base, c0 + o0 + j, inv_t, pen) : -INFINITY;
   }
+}
+
+// ---------------------------------------------------------------- phase 1
+// Per-chunk best composite (value, then lower id) of the processed (MODE 1: + Gumbel noise)
+// scores -> pc[row*C + c].
+template <bool BF16, int MODE, int EPT>
+__global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict__ logits,
+                                                          const uint8_t* __restrict__ seen, int V, int C, float inv_t,
+                                                          float pen, const int* __restrict__ rng,
+                                                          uint64_t* __restrict__ pc, int vec) {
+  __shared__ float rv[NW];
+  __shared__ int ri[NW];
+  const int c = blockIdx.x, row = blockIdx.y;
+  const size_t base = (size_t)row * V;
+  const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
+  const int c0 = c * (NT * EPT), o0 = threadIdx.x * EPT, nvalid = min(NT * EPT, V - c0);
+  float sv[EPT];
+  load_run<BF16, EPT>(logits, seen, base, c0, o0, nvalid, vec != 0, inv_t, pen, sv);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int i = c0 + o0 + j;
+    if (o0 + j < nvalid) {
+      float s = sv[j];
+      if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
+      if (better(s, i, bv, bi)) { bv = s; bi = i; }
+    }
+  }
+  block_argmax(bv, bi, rv, ri);
+  if (threadIdx.x == 0) pc[(size_t)row * C + c] = ckey(bv, bi);
 }
 
 // Per-chunk candidate superset -> pc[(row*C + c)*CCAP + s] as composite keys (unused slots 0),
@@ -773,7 +776,7 @@ extern "C" int edge_decode_advance(const int64_t* nxt, int64_t* tok, int64_t* ou
 // tune key "sample_rowwide" (0 = never).
 static int g_sample_rowwide_min = 128;
 extern "C" void edge_sample_rowwide_min(int v) { g_sample_rowwide_min = v; }
-// Split top-k form: 16-byte score loads in the chunk kernel (tune key "sample_vec"; 0 = per element).
+// Split forms: 16-byte score loads in the chunk kernels (tune key "sample_vec"; 0 = per element).
 static int g_sample_vec = 1;
 extern "C" void edge_sample_vec(int v) { g_sample_vec = v; }
 
@@ -809,6 +812,9 @@ static int sample_launch(const void* logits, int is_bf16, uint8_t* seen, int B, 
   uint64_t* pc = reinterpret_cast<uint64_t*>(workspace);
   uint32_t* pthr = reinterpret_cast<uint32_t*>(pc + (size_t)B * C * CCAP);
   const dim3 g1(C, B);
+  // phase-1 chunk kernels: 16-byte score loads (whole aligned runs)
+  const int vec = g_sample_vec && V % 8 == 0 && reinterpret_cast<uintptr_t>(logits) % 16 == 0 &&
+                  (seen == nullptr || reinterpret_cast<uintptr_t>(seen) % 8 == 0);
   if (mode == 2 && top_k > CCAP) {
     if (is_bf16) hipLaunchKernelGGL(topk_row_kernel<true>, dim3(B), dim3(NT), 0, st, logits, seen, V, inv_t, penalty,
                                     top_k, top_p, rng, out_tok, adv);
@@ -822,8 +828,6 @@ static int sample_launch(const void* logits, int is_bf16, uint8_t* seen, int B, 
     else { if (ns <= 2) RW(false, 2); else RW(false, 4); }
 #undef RW
   } else if (mode == 2) {
-    const int vec = g_sample_vec && V % 8 == 0 && reinterpret_cast<uintptr_t>(logits) % 16 == 0 &&
-                    (seen == nullptr || reinterpret_cast<uintptr_t>(seen) % 8 == 0);
 #define TC(BF, E) hipLaunchKernelGGL((topk_chunk_kernel<BF, E>), g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, \
                                      penalty, top_k, pc, pthr, vec)
     if (is_bf16) { if (ept == 8) TC(true, 8); else TC(true, 16); }
@@ -833,9 +837,9 @@ static int sample_launch(const void* logits, int is_bf16, uint8_t* seen, int B, 
                        out_tok, adv);
   } else {
 #define AC(BF, MD) do { if (ept == 8) hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 8>), g1, dim3(NT), 0, st, logits, \
-                                                        seen, V, C, inv_t, penalty, rng, pc); \
+                                                        seen, V, C, inv_t, penalty, rng, pc, vec); \
                            else hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 16>), g1, dim3(NT), 0, st, logits, seen, \
-                                                   V, C, inv_t, penalty, rng, pc); } while (0)
+                                                   V, C, inv_t, penalty, rng, pc, vec); } while (0)
     if (is_bf16) { if (mode == 0) AC(true, 0); else AC(true, 1); }
     else { if (mode == 0) AC(false, 0); else AC(false, 1); }
 #undef AC
