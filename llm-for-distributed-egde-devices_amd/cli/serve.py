@@ -39,6 +39,8 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--headinfer-heads", type=int, default=None, help="HeadInfer: KV heads per layer kept on the GPU")
     ap.add_argument("--prefill-chunk", type=int, default=4096, help="chunked prefill size (HeadInfer)")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"])
+    ap.add_argument("--static-batches", action="store_true",
+                    help="pipeline engine: run each batch to completion (default: continuous batching)")
     return ap.parse_args(argv)
 
 
@@ -103,8 +105,9 @@ def build_pipeline_engine(args, launch):
     stage (``build_pp_engine``; an INT8 checkpoint directory as ``--model`` is read per stage), rank
     0 wraps its ``PipelineGenerator`` in the ServingEngine; every other rank serves the driver's
     pipeline commands (``serve_workers``) and never returns.  Requests are batched per sampling
-    configuration into the pipeline's M micro-batches of b rows (static batches: a batch runs to
-    completion across all stages; M >= P keeps every stage busy)."""
+    configuration into the pipeline's M micro-batches of b rows.  Default: continuous batching
+    (parallel.pp_slots: the M x b rows are slots; a request joins between decode rounds and
+    leaves when done); ``--static-batches``: each batch runs to completion across all stages."""
     from ..parallel.pp_engine import serve_workers
     from ..serve.server import ServingEngine
     from .common import build_pp_engine
@@ -115,7 +118,12 @@ def build_pipeline_engine(args, launch):
         serve_workers({0: eng})
         raise SystemExit(0)
     log.info(f"generation engine: {src} pipelined over {launch[1]} ranks at layers {bounds}")
-    return ServingEngine(eng, tok, args.max_batch, continuous=False)
+    # continuous batching over the pipeline rows (parallel.pp_slots); --static-batches: run each
+    # batch of equal-sampling requests to completion instead
+    srv = ServingEngine(eng, tok, args.max_batch, continuous=not getattr(args, "static_batches", False))
+    import atexit
+    atexit.register(srv.close)             # release the worker ranks however rank 0 exits
+    return srv
 
 
 def main(argv: Optional[List[str]] = None):

@@ -34,6 +34,7 @@ from .. import ops
 from ..engine.generate import GenerationResult, SamplingParams
 from ..models.decoder import AttnCtx, DecoderLM
 from .pipeline import PipelineStage
+from .pp_slots import CMD_SLOT_ADMIT, CMD_SLOT_OPEN, CMD_SLOT_STEP, handle_slot_command
 
 CMD_GENERATE, CMD_SCORE, CMD_STOP = 1, 2, 3
 _HDR = 12
@@ -153,6 +154,23 @@ class PipelineGenerator:
         self.model = _Scorer(self)          # Agent / MetricSuite read generator.model
         self.last_rank = world - 1
         self.last_ticks = 0
+        self.attn_hook = None               # resident KV rows: continuous batching applies (pp_slots)
+        self._slot_sess = None
+        self._stopped = False
+
+    # a failure after a command went out leaves the other ranks part-way through its P2P: the
+    # serving front end must not go on to the next command (serve.server.ServingEngine exits)
+    fatal_on_error = True
+
+    def slot_decoder(self, sampling: SamplingParams, seed: int = 0, width: int = 2048,
+                     max_batch: Optional[int] = None):
+        """Continuous-batching session over the pipeline's rows (parallel.pp_slots)."""
+        from .pp_slots import PipelineSlotDecoder
+        return PipelineSlotDecoder(self, sampling, seed=seed, width=width, max_batch=max_batch)
+
+    def shutdown(self) -> None:
+        """Driver: release the workers' command loop (once; ``stop_workers`` is idempotent)."""
+        stop_workers(self)
 
     # ------------------------------------------------------------------ comm helpers
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
@@ -329,13 +347,18 @@ def serve_workers(engines: Dict[int, PipelineGenerator]) -> int:
             eng = engines[int(hdr0[1])]
             ids = eng._bcast(torch.zeros(int(hdr0[2]), dtype=torch.long, device=eng.cdev))
             eng._run_score(ids)
+        elif cmd in (CMD_SLOT_OPEN, CMD_SLOT_ADMIT, CMD_SLOT_STEP):
+            handle_slot_command(engines[int(hdr0[1])], hdr0)
         else:
             raise RuntimeError(f"unknown pipeline command {cmd}")
         served += 1
 
 
 def stop_workers(engine: PipelineGenerator) -> None:
-    """Driver: release the workers' serve loop."""
+    """Driver: release the workers' serve loop (a second call sends nothing: nobody listens)."""
+    if getattr(engine, "_stopped", False):
+        return
+    engine._stopped = True
     if dist.is_initialized() and dist.get_world_size() > 1 and engine.grank == 0:
         hdr = torch.zeros(_HDR, dtype=torch.long, device=engine.cdev)
         hdr[0] = CMD_STOP

@@ -14,7 +14,16 @@ def make_app(engine=None):
     from fastapi import FastAPI, HTTPException
     from pydantic import BaseModel
 
-    app = FastAPI(title="edgellm")
+    import contextlib
+
+    @contextlib.asynccontextmanager
+    async def lifespan(_app):
+        yield
+        # server shutdown (Ctrl-C on uvicorn): drain the engine and release a pipeline's worker ranks
+        if engine is not None and hasattr(engine, "close"):
+            engine.close()
+
+    app = FastAPI(title="edgellm", lifespan=lifespan)
 
     class GenerateRequest(BaseModel):
         prompt: Optional[str] = None

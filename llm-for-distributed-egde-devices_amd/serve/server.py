@@ -42,10 +42,12 @@ class ServingEngine:
                       "decode_steps": 0, "max_concurrent": 0}
         # continuous batching needs per-row cache lengths: not with a HeadInfer-offloaded cache
         # continuous batching drives a Generator's cache rows (not a HeadInfer cache, not a pipeline)
+        # (a PipelineGenerator opens its sessions through generator.slot_decoder: parallel.pp_slots)
         slots_ok = getattr(generator, "attn_hook", 1) is None
         self.continuous = slots_ok if continuous is None else (continuous and slots_ok)
         self.width = 2048                          # SlotDecoder output columns per session
         self.steps_per_poll = max(1, steps_per_poll)
+        self._closed = False
         self._stop = threading.Event()
         self._worker = threading.Thread(target=self._loop_continuous if self.continuous else self._loop, daemon=True)
         self._worker.start()
@@ -88,9 +90,29 @@ class ServingEngine:
         return {**self.stats, **lat}
 
     def close(self):
+        """Stop the worker (requests already queued are served first), then release a pipeline
+        engine's worker ranks (``shutdown``: their command loop returns and the job exits).
+        Idempotent; called from the REST app's shutdown event and at interpreter exit."""
+        if self._closed:
+            return
+        self._closed = True
         self._stop.set()
         self.q.put(None)
-        self._worker.join(timeout=10)
+        self._worker.join(timeout=600 if getattr(self.gen, "fatal_on_error", False) else 10)
+        shutdown = getattr(self.gen, "shutdown", None)
+        if shutdown is not None and not self._worker.is_alive():   # never beside a running command
+            shutdown()
+
+    def _fatal(self, e: BaseException):
+        """A pipeline engine failed after a command went out: the worker ranks are part-way through
+        its P2P, so the next command would not line up with them.  Fail the caller(s) and exit the
+        process non-zero (torchrun then tears the job down) instead of serving on."""
+        import sys
+        import traceback
+        sys.stderr.write(f"[edgellm serve] fatal pipeline error, exiting: {e!r}\n")
+        traceback.print_exc()
+        sys.stderr.flush()
+        os._exit(70)
 
     # ------------------------------------------------------------------ continuous worker
     def _loop_continuous(self):
@@ -122,8 +144,12 @@ class ServingEngine:
                         or not dec.can_admit(len(pending[0][0]), pending[0][1].max_new_tokens)):
                     dec = None                     # session drained: the queue head picks the next one
                 if dec is None and pending:
-                    dec = SlotDecoder(self.gen, pending[0][1], seed=pending[0][2], width=self.width,
-                                      max_batch=self.max_batch)
+                    factory = getattr(self.gen, "slot_decoder", None)
+                    if factory is not None:
+                        dec = factory(pending[0][1], seed=pending[0][2], width=self.width, max_batch=self.max_batch)
+                    else:
+                        dec = SlotDecoder(self.gen, pending[0][1], seed=pending[0][2], width=self.width,
+                                          max_batch=self.max_batch)
                     self.stats["sessions"] += 1
                 if dec is None:
                     continue
@@ -136,6 +162,8 @@ class ServingEngine:
                         try:
                             dec.admit(ids, sp.max_new_tokens, eos, tag=it)
                         except Exception as e:     # noqa: BLE001 - reported to that caller
+                            if getattr(self.gen, "fatal_on_error", False):
+                                raise
                             self.stats["errors"] += 1
                             if not fut.done():
                                 fut.set_exception(e)
@@ -156,6 +184,8 @@ class ServingEngine:
                     if s is not None and not s.tag[3].done():
                         s.tag[3].set_exception(e)
                 dec = None
+                if getattr(self.gen, "fatal_on_error", False):
+                    self._fatal(e)
 
     def _finish(self, it: tuple, res, occ: int):
         toks = res.tokens[0]
@@ -215,6 +245,8 @@ class ServingEngine:
             self.stats["errors"] += 1
             for b in batch:
                 b[3].set_exception(e)
+            if getattr(self.gen, "fatal_on_error", False):
+                self._fatal(e)
             return
         self.stats["batches"] += 1
         steps = max((len(t) for t in res.tokens), default=0)
