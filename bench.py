@@ -14,9 +14,12 @@ micro-batches concurrently on separate HIP streams (default 2 x 256 sequences: e
 decode GEMMs read a weight once for its 256 rows, and one lane's HBM-bound attention overlaps the
 other lane's GEMMs), so per-GPU work per step is constant (weak scaling: global batch =
 micro-batch x lanes x N).
-Weights: random-init Llama-2-7B architecture; the FULL model is SmoothQuant-calibrated on
-synthetic tokens and smoothed once, then each rank keeps its layers, so every split runs
-bit-identical INT8 weights.  Data: random prompt ids.  ``--device cpu --model tiny:llama``
+Weights: random-init Llama-2-7B architecture (seeded by global parameter name, so a stage's
+bf16 weights equal the unsplit model's), SmoothQuant-calibrated on synthetic tokens: at N = 1
+the full model; at N > 1 each rank builds only its stage and calibrates it on the activations
+the previous stage sends (``--calib stage``, default; ``--calib full`` builds + calibrates the
+full model on every rank and cuts the stage, bit-identical INT8 weights for every split).
+Data: random prompt ids.  ``--device cpu --model tiny:llama``
 exercises the same code paths on CPU (gloo) for tests.
 """
 from __future__ import annotations
@@ -78,6 +81,9 @@ def parse(argv=None):
     ap.add_argument("--partition", default="units",
                     help="units (balanced over half-layer units: a stage boundary may fall between a layer's "
                          "attention and MLP halves) | balanced (whole layers) | uniform | explicit '9,8,8,7'")
+    ap.add_argument("--calib", default="stage", choices=["stage", "full"],
+                    help="N > 1: SmoothQuant calibration per stage over P2P (each rank builds only its stage) "
+                         "or of the full model on every rank")
     ap.add_argument("--pp-slack", type=int, default=0,
                     help="N > 1: extra ticks per stage hop (1 = 2N micro-batches in flight, every RCCL hop "
                          "overlapped with a tick of compute; doubles the per-token latency)")
@@ -123,7 +129,24 @@ def build(args, device, first=0, last=None, units=None):
             torch.cuda.empty_cache()
             torch.cuda.synchronize()
         return cfg, model
-    if args.quant == "w8a8_smoothquant":
+    if args.quant == "w8a8_smoothquant" and getattr(args, "calib", "stage") == "stage" and _pipeline_rank() is not None:
+        # per-stage SmoothQuant: this rank builds only its stage and calibrates it on the bf16
+        # activations the previous stage sends over the pipeline's P2P path (no full model here)
+        import torch.distributed as dist
+        from edgellm.quant.smoothquant import smoothquant_stage_p2p
+        rank, world = _pipeline_rank()
+        calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed)
+        cdev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+        def recv_prev(shape, dt):
+            t = torch.empty(shape, dtype=dt, device=cdev)
+            dist.recv(t, rank - 1)
+            return t
+
+        model = smoothquant_stage_p2p(cfg, calib, recv_prev, lambda t: dist.send(t.to(cdev), rank + 1),
+                                      first=first, last=last, units=units, dtype=dtype, device=device,
+                                      seed=args.seed)
+    elif args.quant == "w8a8_smoothquant":
         full = build_model(cfg, dtype=dtype, device=device, seed=args.seed)
         calib = synthetic_calibration(cfg, n=2, T=64, device=device, seed=args.seed)
         model = smoothquant_stage(full, first, cfg.num_layers if last is None else last, calib, device=device,
@@ -139,6 +162,14 @@ def build(args, device, first=0, last=None, units=None):
         torch.cuda.empty_cache()
         torch.cuda.synchronize()
     return cfg, model
+
+
+def _pipeline_rank():
+    """(rank, world) inside a multi-rank pipeline launch with the process group up, else None."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_rank(), dist.get_world_size()
+    return None
 
 
 def _sync(device):

@@ -33,6 +33,16 @@ def add_runtime_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     g.add_argument("--batch_size", type=int, default=None,
                    help="questions decoded together per agent (YAML parallel.microbatches; 1 = the reference)")
     g.add_argument("--kv_dtype", default=None, choices=["bf16", "int8"], help="KV-cache dtype (default bf16)")
+    g.add_argument("--partition", default=None,
+                   help="torchrun pipelines: balanced | units (half-layer stage bounds from the decode cost model) | "
+                        "uniform | '8,8,8,8' (YAML parallel.partition)")
+    g.add_argument("--pp_lanes", type=int, default=None,
+                   help="torchrun pipelines: micro-batches each stage runs concurrently (YAML parallel.lanes)")
+    g.add_argument("--pp_slack", type=int, default=None,
+                   help="torchrun pipelines: extra ticks per hop, P2P overlapped with compute (YAML parallel.slack)")
+    g.add_argument("--calib", default=None, choices=["stage", "full"],
+                   help="torchrun + w8a8_smoothquant: calibrate each stage on the activations it receives "
+                        "(stage, default) or the full model on every rank (full) (YAML parallel.calib)")
     g.add_argument("--metrics_jsonl", default=None, help="append structured per-sample metrics here")
     return p
 
@@ -49,7 +59,7 @@ def pop_runtime(args: argparse.Namespace) -> dict:
     """Remove runtime-only keys so the remaining namespace is the reference's flag set."""
     keys = ["quant", "precision", "devices", "num_samples", "seed", "max_seq", "progress", "base_model_path",
             "no_legacy_decode", "no_reference_in_refiner", "merge", "serial", "headinfer_heads", "metrics_jsonl",
-            "prefill_chunk", "pp_size", "batch_size", "kv_dtype"]
+            "prefill_chunk", "pp_size", "batch_size", "kv_dtype", "partition", "pp_lanes", "pp_slack", "calib"]
     return {k: args.__dict__.pop(k) for k in keys if k in args.__dict__}
 
 
@@ -65,6 +75,11 @@ def resolve_runtime(cfg, rt: dict) -> dict:
         rt["headinfer_heads"] = cfg.offload.gpu_kv_budget_heads if cfg.offload.gpu_kv_budget_heads is not None else 0
     if rt.get("prefill_chunk") is None:
         rt["prefill_chunk"] = cfg.offload.chunk_size
+    par = cfg.parallel
+    rt["partition"] = rt.get("partition") or getattr(par, "partition", "balanced") or "balanced"
+    rt["pp_lanes"] = max(1, int(rt.get("pp_lanes") or getattr(par, "lanes", 1) or 1))
+    rt["pp_slack"] = max(0, int(rt.get("pp_slack") if rt.get("pp_slack") is not None else getattr(par, "slack", 0) or 0))
+    rt["calib"] = rt.get("calib") or getattr(par, "calib", "stage") or "stage"
     rt.setdefault("kv_dtype", None)
     rt["kv_dtype"] = rt["kv_dtype"] or "bf16"
     return rt
@@ -141,14 +156,19 @@ def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch,
         f"agent gpus {gpus} must be distinct ranks of the {world}-rank launch"
     group = agent_group(ranks, world)
     kvd = rt.get("kv_dtype") or "bf16"
-    common = dict(max_batch=max_batch, max_seq=rt.get("max_seq", 2048), tag=tag, group=group, ranks=ranks)
+    lanes, slack = int(rt.get("pp_lanes") or 1), int(rt.get("pp_slack") or 0)
+    common = dict(max_batch=max_batch, max_seq=rt.get("max_seq", 2048), tag=tag, group=group, ranks=ranks,
+                  lanes=lanes, slack=slack)
     if rank not in ranks:
         cfg, tok, source = _cfg_of(model_id, precision, torch.device("cpu"), rt.get("base_model_path"))
         eng = PipelineGenerator(None, -1, len(ranks), cfg=cfg, device=dev, **common)
         return eng, tok, source, None
     s_idx = ranks.index(rank)
+    M, b = PipelineGenerator.geometry(len(ranks), max_batch, lanes, slack)
     stage, tok, source, bounds = load_stage(model_id, precision, quant, dev, rt.get("base_model_path"), s_idx,
-                                            len(ranks))
+                                            len(ranks), partition=rt.get("partition") or "balanced", group=group,
+                                            ranks=ranks, calib=rt.get("calib") or "stage", rows=b,
+                                            ctx=min(int(rt.get("max_seq", 2048)), 256))
     if kvd == "int8" and stage.cfg.head_dim not in (64, 128, 256):
         kvd = "bf16"
     eng = PipelineGenerator(stage, s_idx, len(ranks), kv_dtype=kvd, **common)

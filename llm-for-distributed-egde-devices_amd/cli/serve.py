@@ -39,6 +39,12 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--headinfer-heads", type=int, default=None, help="HeadInfer: KV heads per layer kept on the GPU")
     ap.add_argument("--prefill-chunk", type=int, default=4096, help="chunked prefill size (HeadInfer)")
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "int8"])
+    ap.add_argument("--partition", default="balanced",
+                    help="torchrun pipeline: balanced | units (half-layer bounds) | uniform | '8,8,8,8'")
+    ap.add_argument("--pp-lanes", type=int, default=1, help="torchrun pipeline: concurrent micro-batches per stage")
+    ap.add_argument("--pp-slack", type=int, default=0, help="torchrun pipeline: extra ticks per stage hop")
+    ap.add_argument("--calib", default="stage", choices=["stage", "full"],
+                    help="torchrun + w8a8_smoothquant: per-stage calibration over P2P (stage) or full model")
     ap.add_argument("--static-batches", action="store_true",
                     help="pipeline engine: run each batch to completion (default: continuous batching)")
     return ap.parse_args(argv)
@@ -111,7 +117,9 @@ def build_pipeline_engine(args, launch):
     from ..parallel.pp_engine import serve_workers
     from ..serve.server import ServingEngine
     from .common import build_pp_engine
-    rt = dict(max_seq=args.max_seq, kv_dtype=args.kv_dtype, base_model_path=args.base_model_path)
+    rt = dict(max_seq=args.max_seq, kv_dtype=args.kv_dtype, base_model_path=args.base_model_path,
+              partition=getattr(args, "partition", "balanced"), pp_lanes=getattr(args, "pp_lanes", 1),
+              pp_slack=getattr(args, "pp_slack", 0), calib=getattr(args, "calib", "stage"))
     eng, tok, src, bounds = build_pp_engine(args.model, args.precision, args.quant, rt, launch, tag=0,
                                             max_batch=args.max_batch)
     if launch[0] != 0:

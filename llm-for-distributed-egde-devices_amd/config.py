@@ -50,7 +50,10 @@ REFINER_SAMPLING = dict(temperature=0.5, top_k=30, top_p=0.9, repetition_penalty
 class ParallelConfig:
     pp_size: int = 1            # pipeline stages (one process per GPU)
     microbatches: int = 1       # sequences groups in flight through the pipeline
-    partition: str = "balanced"  # balanced (by bytes) | uniform | explicit "8,8,8,8"
+    partition: str = "balanced"  # balanced (by bytes) | units (half-layer decode cost model) | uniform | "8,8,8,8"
+    lanes: int = 1              # micro-batches each stage decodes concurrently on HIP streams
+    slack: int = 0              # extra ticks per stage hop (1: every P2P hop overlapped with a tick)
+    calib: str = "stage"        # SmoothQuant under torchrun: per-stage over P2P | full (every rank)
 
 
 @dataclass

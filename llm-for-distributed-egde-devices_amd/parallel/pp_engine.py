@@ -32,11 +32,13 @@ import torch.distributed as dist
 
 from .. import ops
 from ..engine.generate import GenerationResult, SamplingParams
+from ..utils.log import get_logger
 from ..models.decoder import AttnCtx, DecoderLM
 from .pipeline import PipelineStage
 from .pp_slots import CMD_SLOT_ADMIT, CMD_SLOT_OPEN, CMD_SLOT_STEP, handle_slot_command
 
 CMD_GENERATE, CMD_SCORE, CMD_STOP = 1, 2, 3
+log = get_logger("pp_engine")
 _HDR = 12
 
 
@@ -45,46 +47,99 @@ def distributed_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+def stage_unit_bounds(cfg, world: int, partition: str = "balanced", quant: str = "none", rows: int = 1,
+                      ctx: int = 256, kv_bytes: float = 2.0) -> List[int]:
+    """Stage boundaries in half-layer units (unit 2 i = layer i's attention half, 2 i + 1 its MLP
+    half).  ``units``: the decode cost model (parallel.partition.partition_units) at ``rows`` rows
+    and ``ctx`` cached tokens — a boundary may fall inside a layer; ``balanced`` / ``uniform`` /
+    explicit "8,8,8,8": whole layers (bytes per decode step)."""
+    from .partition import partition_model, partition_units
+    wb = 1.0 if quant not in (None, "none") else 2.0
+    if partition == "units":
+        return list(partition_units(cfg, world, rows=max(1, rows), ctx=ctx, weight_bytes=wb, kv_bytes=kv_bytes))
+    explicit = partition if "," in partition else None
+    mode = "uniform" if partition == "uniform" else "balanced"
+    return [2 * x for x in partition_model(cfg, world, mode, weight_bytes=wb, explicit=explicit)]
+
+
+def _peak_build_mb(device) -> float:
+    """Peak memory of this rank so far: device allocator peak on a GPU, max RSS on the CPU."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        return torch.cuda.max_memory_allocated(dev) / 2 ** 20
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
+
+
 def load_stage(model_id: str, precision: str, quant: str, device, base_dir: Optional[str], rank: int, world: int,
-               bounds: Optional[Sequence[int]] = None):
-    """This rank's pipeline stage of ``model_id``: layers [bounds[rank], bounds[rank+1]) (balanced
-    partition by default), the embedding on rank 0, the head on the last rank.  Weights equal the
-    unsplit model's (random-init weights are seeded by global parameter name; SmoothQuant calibrates
-    and smooths the FULL model, then cuts the stage).  Returns (stage, tokenizer, source, bounds)."""
+               bounds: Optional[Sequence[int]] = None, partition: str = "balanced", group=None,
+               ranks: Optional[Sequence[int]] = None, calib: str = "stage", rows: int = 1, ctx: int = 256):
+    """This rank's pipeline stage of ``model_id``: half-layer units [ub[rank], ub[rank+1]) of
+    ``stage_unit_bounds`` (``partition``; ``bounds`` = explicit LAYER bounds), the embedding on
+    stage 0, the head on the last.  Random-init weights are seeded by global parameter name, so a
+    stage's weights equal the unsplit model's.
+
+    SmoothQuant (``quant="w8a8_smoothquant"``, no int8 checkpoint):
+      * ``calib="stage"`` (default under a multi-rank launch): the rank builds ONLY its stage and
+        calibrates it on the activations the previous stage sends it over the pipeline's P2P
+        path (``quant.smoothquant.smoothquant_stage_p2p``; every member of the group joins, in
+        stage order) — no rank materialises layers it does not own;
+      * ``calib="full"``: every rank builds + calibrates the full model and cuts its stage.
+    An int8 checkpoint directory is read stage-locally (no calibration).
+    ``group`` / ``ranks``: the model's process group and its global ranks (stage i = ranks[i]).
+    Returns (stage, tokenizer, source, layer bounds; halves as .5)."""
     from ..models.registry import load_model, quantized_checkpoint_dir
-    from .partition import partition_model
     qdir = quantized_checkpoint_dir(model_id, base_dir)
+    cfg, tok, source = _cfg_of(model_id, precision, torch.device("cpu"), base_dir)
+    if qdir is not None:
+        quant = "w8a8"          # (bytes per weight for the partition's cost model)
+    if bounds is not None:
+        ub = [int(round(2 * float(x))) for x in bounds]
+    else:
+        ub = stage_unit_bounds(cfg, world, partition, quant, rows, ctx)
+    ua, ubb = ub[rank], ub[rank + 1]
+    whole = ua % 2 == 0 and ubb % 2 == 0
+    loc = dict(first=ua // 2, last=ubb // 2) if whole else dict(units=(ua, ubb))
+    lb = [u / 2 if u % 2 else u // 2 for u in ub]
     if qdir is not None:
         # an int8 checkpoint: this rank reads only its stage (no full bf16 model, no calibration)
-        from ..quant.checkpoint import checkpoint_config
-        cfg = checkpoint_config(qdir)
-        if bounds is None:
-            bounds = partition_model(cfg, world, "balanced", weight_bytes=1.0)
-        first, last = int(bounds[rank]), int(bounds[rank + 1])
-        stage, tok, source = load_model(qdir, precision, "none", device, None, first=first, last=last)
-        return stage, tok, source, list(bounds)
-    full_needed = quant == "w8a8_smoothquant"
-    if full_needed:
-        full, tok, source = load_model(model_id, precision, "none", device, base_dir)
-        cfg = full.cfg
-    else:
-        full = None
-        cfg, tok, source = _cfg_of(model_id, precision, device, base_dir)
-    if bounds is None:
-        wb = 1.0 if quant not in (None, "none") else 2.0
-        bounds = partition_model(cfg, world, "balanced", weight_bytes=wb)
-    first, last = int(bounds[rank]), int(bounds[rank + 1])
-    if full_needed:
-        from ..quant.smoothquant import smoothquant_stage
+        stage, tok, source = load_model(qdir, precision, "none", device, None, **loc)
+    elif quant == "w8a8_smoothquant":
         text = ("Question: when did the first world war begin and which countries fought in it? Answer: "
                 "The First World War began in 1914 after the assassination of Archduke Franz Ferdinand.")
         ids = tok.encode(text)[:64]
-        calib = torch.tensor([[i % full.cfg.vocab_size for i in ids]], device=full.device)
-        stage = smoothquant_stage(full, first, last, calib, device=device)
-        del full
+        calib_ids = torch.tensor([[i % cfg.vocab_size for i in ids]], device=device)
+        if calib == "stage" and world > 1 and dist.is_initialized():
+            from ..quant.smoothquant import smoothquant_stage_p2p
+            granks = list(ranks) if ranks is not None else list(range(world))
+            nccl = dist.get_backend(group) == "nccl"
+            cdev = torch.device(device) if nccl else torch.device("cpu")
+
+            def recv_prev(shape, dtype):
+                t = torch.empty(shape, dtype=dtype, device=cdev)
+                dist.recv(t, granks[rank - 1], group=group)
+                return t
+
+            def send_next(t):
+                dist.send(t.to(cdev).contiguous(), granks[rank + 1], group=group)
+
+            stage = smoothquant_stage_p2p(
+                cfg, calib_ids, recv_prev, send_next,
+                build=lambda: load_model(model_id, precision, "none", device, base_dir, **loc)[0])
+        else:
+            from ..quant.smoothquant import smoothquant_stage
+            full, tok, source = load_model(model_id, precision, "none", device, base_dir)
+            stage = smoothquant_stage(full, loc.get("first", ua // 2), loc.get("last", ubb // 2), calib_ids,
+                                      device=device, units=loc.get("units"))
+            del full
     else:
-        stage, tok, source = load_model(model_id, precision, quant, device, base_dir, first=first, last=last)
-    return stage, tok, source, list(bounds)
+        stage, tok, source = load_model(model_id, precision, quant, device, base_dir, **loc)
+    nparam = sum(p.numel() * p.element_size() for p in stage.parameters()) + \
+        sum(b.numel() * b.element_size() for b in stage.buffers())
+    log.info(f"stage {rank}/{world} of {source}: units [{ua}, {ubb}) = layers [{lb[rank]}, {lb[rank + 1]}), "
+             f"weights {nparam / 2 ** 20:.1f} MiB, peak build memory {_peak_build_mb(device):.1f} MiB "
+             f"({'per-stage' if quant == 'w8a8_smoothquant' and calib == 'stage' and world > 1 else 'no'} calibration)")
+    return stage, tok, source, lb
 
 
 def _cfg_of(model_id, precision, device, base_dir):
@@ -128,21 +183,21 @@ class PipelineGenerator:
     def __init__(self, stage_model: Optional[DecoderLM], rank: int, world: int, max_batch: int = 1,
                  max_seq: int = 2048, tag: int = 0, lanes: int = 1, n_micro: Optional[int] = None,
                  kv_dtype: str = "bf16", eos_every: int = 8, group=None, use_graphs: Optional[bool] = None,
-                 ranks: Optional[Sequence[int]] = None, cfg=None, device=None):
+                 ranks: Optional[Sequence[int]] = None, cfg=None, device=None, slack: int = 0):
         self.rank, self.world, self.tag, self.group = rank, world, tag, group
         self.ranks = list(ranks) if ranks is not None else list(range(world))
         assert len(self.ranks) == world
         self.grank = dist.get_rank() if dist.is_initialized() else 0
         self.member = stage_model is not None
-        M = max(n_micro or 0, world * lanes)
-        b = max(1, math.ceil(max_batch / M))
+        M, b = self.geometry(world, max_batch, lanes, slack, n_micro)
         self.M, self.b = M, b
+        self.lanes, self.slack = lanes, slack
         self.cfg = stage_model.cfg if self.member else cfg
         assert self.cfg is not None, "a stub engine needs the model config"
         self.max_seq = min(max_seq, self.cfg.max_position_embeddings)   # as Generator
         if self.member:
             self.stage = PipelineStage(stage_model, rank, world, b, M, self.max_seq, group=group, lanes=lanes,
-                                       kv_dtype=kv_dtype, use_graphs=use_graphs, ranks=self.ranks)
+                                       kv_dtype=kv_dtype, use_graphs=use_graphs, ranks=self.ranks, slack=slack)
             self.device = stage_model.device
             self.nccl = self.stage.nccl
         else:
@@ -157,6 +212,15 @@ class PipelineGenerator:
         self.attn_hook = None               # resident KV rows: continuous batching applies (pp_slots)
         self._slot_sess = None
         self._stopped = False
+
+    @staticmethod
+    def geometry(world: int, max_batch: int, lanes: int = 1, slack: int = 0, n_micro: Optional[int] = None):
+        """(M micro-batches, b rows each) for ``max_batch`` sequences: M covers the micro-batch
+        groups a stage hop keeps in flight (P, or (1 + slack)(P - 1) + 2 with slack) times the lanes."""
+        groups = world if slack == 0 or world == 1 else (1 + slack) * (world - 1) + 2
+        M = max(n_micro or 0, groups * max(1, lanes))
+        M = -(-M // max(1, lanes)) * max(1, lanes)
+        return M, max(1, math.ceil(max_batch / M))
 
     # a failure after a command went out leaves the other ranks part-way through its P2P: the
     # serving front end must not go on to the next command (serve.server.ServingEngine exits)

@@ -72,11 +72,17 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
     for j, layer in enumerate(model.layers):
         pre = f"layers.{j}."                       # stats are keyed by local module names
         gpre = f"layers.{layer.idx}."               # factors by GLOBAL layer index
-        qkv, o, up, down = layer.attn.qkv, layer.attn.o, layer.mlp.up, layer.mlp.down
-        dev = qkv.weight.device
+        # half layers (a sub-layer stage): every fold below stays inside its own half
+        qkv, o = (layer.attn.qkv, layer.attn.o) if layer.attn is not None else (None, None)
+        up, down = (layer.mlp.up, layer.mlp.down) if layer.mlp is not None else (None, None)
+        if qkv is None:
+            stats = {k: v for k, v in stats.items() if not k.startswith(pre + "attn.")}
+        if up is None:
+            stats = {k: v for k, v in stats.items() if not k.startswith(pre + "mlp.")}
         # ---- qkv (+ up when phi shares the norm)
         xs = stats.get(pre + "attn.qkv")
         if xs is not None:
+            dev = qkv.weight.device
             wmax = qkv.weight.float().abs().amax(0)
             if cfg.shared_input_norm:
                 xs = torch.maximum(xs, stats.get(pre + "mlp.up", xs))
@@ -88,11 +94,13 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
                 factors[gpre + "mlp.up"] = s
         # ---- up (separate norm2)
         if not cfg.shared_input_norm and pre + "mlp.up" in stats:
+            dev = up.weight.device
             s = _smooth_factor(stats[pre + "mlp.up"].to(dev), up.weight.float().abs().amax(0), alpha)
             _fold_norm(layer.norm2, s)
             factors[gpre + "mlp.up"] = s
         # ---- o: fold into v rows (shared across the q heads of a kv group)
         if pre + "attn.o" in stats:
+            dev = qkv.weight.device
             xs = stats[pre + "attn.o"].to(dev).view(hk, g, d).amax(1)              # [hk, d]
             wm = o.weight.float().abs().amax(0).view(hk, g, d).amax(1)
             s_kv = _smooth_factor(xs, wm, alpha)                                    # [hk, d]
@@ -103,6 +111,7 @@ def smooth_model_(model: DecoderLM, stats: Dict[str, torch.Tensor], alpha: float
             factors[gpre + "attn.o"] = s_kv[:, None, :].expand(hk, g, d).reshape(-1)
         # ---- down: fold into the up half of the GLU weight
         if cfg.is_glu and pre + "mlp.down" in stats:
+            dev = up.weight.device
             f = cfg.intermediate_size
             s = _smooth_factor(stats[pre + "mlp.down"].to(dev), down.weight.float().abs().amax(0), alpha)
             up.weight[f:] = (up.weight[f:].float() / s[:, None]).to(up.weight.dtype)
@@ -206,6 +215,56 @@ def smoothquant_stage(full: DecoderLM, first: int, last: int, calib_ids: torch.T
         if name == "lm_head.weight" and name not in src:
             name = "embed"                     # tied head on a head-only stage
         p.copy_(src[name])
+    return quantize_model(stage, "w8a8_smoothquant", factors=factors)
+
+
+@torch.no_grad()
+def smoothquant_stage_p2p(cfg, calib_ids: torch.Tensor, recv_prev, send_next, first: int = 0,
+                          last: Optional[int] = None, units=None, dtype=torch.bfloat16, device=None,
+                          seed: Optional[int] = 0, alpha: float = 0.5, build=None) -> DecoderLM:
+    """SmoothQuant for ONE pipeline stage without the full model on this rank: the stage's bf16
+    layers are built (``build()``, default random-init ``build_model`` seeded by global parameter
+    name), the calibration activations come from the previous stage over the pipeline's P2P path
+    (``recv_prev(shape, dtype) -> tensor``; stage 0 embeds ``calib_ids`` [N, T]), this stage's
+    projection inputs are measured, its bf16 outputs go on to the next stage (``send_next``),
+    and then it is smoothed and quantised.  The stage sees exactly the activations it sees at
+    inference, so a rank never materialises layers it does not own (peak build memory ~ 1/P of
+    the full model's); with fp32 activations the factors equal ``smoothquant_stage``'s bit for bit."""
+    from ..engine.kv_cache import KVCache
+    from ..models.decoder import build_model
+    stage = build() if build is not None else build_model(cfg, dtype=dtype, device=device, first=first, last=last,
+                                                         seed=seed, units=units)
+    dev = stage.device
+    N, T = calib_ids.shape
+    H = cfg.hidden_size
+    hidden = None if stage.has_embed else recv_prev((N, T, H), stage.dtype)
+    stats: Dict[str, torch.Tensor] = {}
+    hooks = []
+    for name, mod in stage.named_modules():
+        if isinstance(mod, Linear) and (".attn." in f".{name}" or ".mlp." in f".{name}"):
+            def hook(m, inp, name=name):
+                x = inp[0]
+                a = x.detach().reshape(-1, x.shape[-1]).abs().amax(0).float()
+                stats[name] = torch.maximum(stats[name], a) if name in stats else a
+            hooks.append(mod.register_forward_pre_hook(hook))
+    outs = []
+    try:
+        kv = KVCache(cfg, 1, T, first_layer=getattr(stage, "kv_first", stage.first), last_layer=stage.last,
+                     dtype=stage.dtype, device=dev)
+        rope = stage.rope_table(dev)
+        for i in range(N):
+            sp = torch.zeros(1, dtype=torch.int32, device=dev)
+            ctx = AttnCtx("prefill", 1, T, sp, sp + T, T, kv, rope)
+            out = stage(calib_ids[i:i + 1].to(dev) if stage.has_embed else None, ctx,
+                        hidden=None if hidden is None else hidden[i].to(dev))
+            if not stage.has_head:
+                outs.append(out.view(T, H))
+    finally:
+        for h in hooks:
+            h.remove()
+    if not stage.has_head:
+        send_next(torch.stack(outs).contiguous())
+    factors = smooth_model_(stage, stats, alpha)
     return quantize_model(stage, "w8a8_smoothquant", factors=factors)
 
 

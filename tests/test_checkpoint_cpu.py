@@ -91,3 +91,56 @@ agents:
     assert len(a) == len(b) == 2
     for x, y in zip(a, b):
         assert x["answers"] == y["answers"] and x["final"] == y["final"]
+
+
+@pytest.mark.parametrize("source", ["per_stage_calibration", "checkpoint"])
+def test_combine_torchrun_4_ranks_half_layers_lanes(tmp_path, source):
+    """4 ranks, half-layer stage bounds (``--partition units``: every stage one attention or MLP
+    half of the 2-layer tiny Llamas), 2 lanes: the CLI pipeline engine runs the bench's schedule.
+    SmoothQuant W8A8 either calibrated PER STAGE over the P2P path (no rank builds the full model)
+    or read stage-locally from an int8 checkpoint — answers equal the single-process run."""
+    from edgellm.cli import combine, quantize
+    agents = """
+merge: vote
+agents:
+  - {name: qa1, model: "tiny:llama", precision: fp32, quant: w8a8_smoothquant}
+  - {name: qa2, model: "tiny:llama2", precision: fp32, quant: w8a8_smoothquant}
+"""
+    mem = _tiny_yaml(tmp_path, agents)
+    single = tmp_path / "single.jsonl"
+    combine.main(["--config", mem, "--devices", "cpu", "--num_samples", "2", "--max_seq", "512",
+                  "--metrics_jsonl", str(single)])
+    cfg_path = mem
+    if source == "checkpoint":
+        cks = [quantize.main(["--model", m, "--quant", "w8a8_smoothquant", "--out", str(tmp_path / f"ck{i}"),
+                              "--precision", "fp32", "--device", "cpu"]) for i, m in enumerate(["tiny:llama",
+                                                                                              "tiny:llama2"])]
+        (tmp_path / "ck_yaml").mkdir()
+        cfg_path = _tiny_yaml(tmp_path / "ck_yaml", f"""
+merge: vote
+agents:
+  - {{name: qa1, model: "{cks[0]}", precision: fp32}}
+  - {{name: qa2, model: "{cks[1]}", precision: fp32}}
+""")
+    piped = tmp_path / "piped.jsonl"
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "-m", "edgellm.cli.combine", "--config", cfg_path,
+           "--devices", "cpu", "--num_samples", "2", "--max_seq", "512", "--metrics_jsonl", str(piped),
+           "--partition", "units", "--pp_lanes", "2", "--calib", "stage"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert "pipelined over 4 ranks" in r.stdout
+    # every stage is one half layer: units [r, r + 1) on rank r
+    for rk in range(4):
+        assert f"stage {rk}/4 of " in r.stdout and f"units [{rk}, {rk + 1})" in r.stdout
+    if source == "checkpoint":
+        assert "int8-checkpoint:" in r.stdout
+    else:
+        assert "(per-stage calibration)" in r.stdout
+    a, b = _rows(single), _rows(piped)
+    assert len(a) == len(b) == 2
+    for x, y in zip(a, b):
+        assert x["answers"] == y["answers"] and x["final"] == y["final"]

@@ -115,3 +115,40 @@ def test_decode_rows_capability_table():
     assert lin.group_scales_ok(128) and lin.group_scales_ok(64)
     up = W8A8Linear(4096, 22016, bias=False)
     assert up.glu_rows_ok(128) and not W8A8Linear(2048, 11008, bias=False).glu_rows_ok(100)
+
+
+@pytest.mark.parametrize("bounds", [[0, 3, 8], [0, 5, 11, 16]])
+def test_smoothquant_stage_p2p_equals_full_model_calibration(bounds):
+    """Per-stage SmoothQuant (each stage calibrated on the activations the previous stage sends
+    it, no rank building the full model) gives the same int8 weights, scales and folded norms as
+    calibrating the full model and cutting the stage — fp32, whole-layer and half-layer bounds."""
+    from edgellm.models.decoder import global_named_parameters
+    from edgellm.quant.smoothquant import smoothquant_stage, smoothquant_stage_p2p, synthetic_calibration
+    cfg = tiny("llama", num_layers=8)
+    calib = synthetic_calibration(cfg, n=2, T=16, seed=3)
+    full = build_model(cfg, dtype=torch.float32, seed=7)
+    units = len(bounds) == 4 or bounds[-1] == 16
+    box = {}
+
+    def recv(shape, dtype):
+        t = box.pop("h")
+        assert tuple(t.shape) == tuple(shape) and t.dtype == dtype
+        return t
+
+    def send(t):
+        box["h"] = t
+
+    for s in range(len(bounds) - 1):
+        a, b = bounds[s], bounds[s + 1]
+        kw = dict(units=(a, b)) if units else dict(first=a, last=b)
+        ref = smoothquant_stage(copy.deepcopy(full), a, b, calib, units=(a, b) if units else None)
+        got = smoothquant_stage_p2p(cfg, calib, recv, send, dtype=torch.float32, seed=7, **kw)
+        rb = dict(global_named_parameters(ref))
+        gb = dict(global_named_parameters(got))
+        assert rb.keys() == gb.keys()
+        for k in rb:
+            assert torch.equal(rb[k], gb[k]), k
+        rbuf = dict(ref.named_buffers())
+        for k, v in got.named_buffers():
+            assert torch.equal(v, rbuf[k]), k
+    assert not box, "the last stage sends nothing"
