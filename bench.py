@@ -398,7 +398,7 @@ def main(argv=None):
     if "per_rank" in res:
         out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
         out["per_rank"] = res["per_rank"]
-        for k in ("stage_cost_model_us", "stage_cost_spread", "slack"):
+        for k in ("stage_cost_model_us", "stage_cost_spread", "slack", "host_issue_us_per_tick_max"):
             if k in res:
                 out[k] = res[k]
     print(json.dumps(out), flush=True)

@@ -7,7 +7,10 @@
 Same YAML keys / 13 CLI flags / log lines as Code/Base Models/combine_model_fp_updated.py:138-232
 (and Code/Quantised Models/combiner_quant_updated.py).  Agents run concurrently on separate
 GPUs; the refiner merges (or a majority vote).  Per-sample metrics: ROUGE-1/2/L, BERTScore,
-BLEU, cosine, confidence (scored with the refiner), combo TPS = mean of the QA agents' TPS.
+BLEU, cosine, confidence (scored with the refiner, as combine_model_fp_updated.py:208; a vote
+merge loads no refiner, so there the FIRST QA agent scores it — every metrics row names its scorer
+in ``confidence_scorer``: do not compare vote-mode confidence with refiner-scored runs), combo TPS =
+mean of the QA agents' TPS.
 """
 from __future__ import annotations
 
@@ -123,6 +126,10 @@ def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_vari
     logger.info("Loading embedder model...")
     suite = MetricSuite(build_embedder(cfg.embedder_model, rt.get("base_model_path"), devices[0]))
     scorer = refiner or agents[0]
+    scorer_name = "refiner" if refiner is not None else f"agent:{agents[0].name}"
+    if refiner is None:
+        logger.warning(f"merge=vote: confidence is scored with QA agent '{agents[0].name}' (no refiner is loaded); "
+                       "the reference scores it with the refiner")
     progress = ProgressLog(rt.get("progress"))
     done = progress.done()
     results = Results()
@@ -163,7 +170,8 @@ def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_vari
             if rt.get("metrics_jsonl"):
                 with open(rt["metrics_jsonl"], "a") as f:
                     f.write(json.dumps({"index": i, **m, "agent_tps": res.tps, "wall_s": res.wall_s,
-                                        "answers": res.answers, "final": res.final}) + "\n")
+                                        "confidence_scorer": scorer_name, "answers": res.answers,
+                                        "final": res.final}) + "\n")
             if cpu_variant:
                 logger.info(f"[Q{i + 1}] Total time: {res.wall_s:.2f} sec\n")
         # QA agents' generated tokens of this batch (each result holds every row of the batch)

@@ -60,6 +60,8 @@ __device__ __forceinline__ int cidx(uint64_t c) { return (int)(~(uint32_t)c); }
 // nxt, pos / seq_lens += 1), and the last row to finish (an agent-scope arrival counter; row 0 itself
 // at B = 1) advances step and rng[1].  Every workgroup has read step and rng[1] before it arrives,
 // so none sees the advanced values.  At batch 1 this removes a launch (~4 us of a 1.9 ms step).
+// The final kernels that take an Adv read rng through a plain (not __restrict__) pointer: adv.rng
+// writes the same words, so the compiler must not treat the rng load as invariant.
 struct Adv {
   int64_t* tok;
   int64_t* out;
@@ -287,12 +289,20 @@ __device__ __forceinline__ void pad8(uint64_t* fc, int n) {
   if (t < ((n + 7) & ~7)) fc[t] = 0ull;
 }
 
-// Thread `o0 / EPT`'s run of EPT consecutive processed scores of a chunk (element o = o0 + j):
-// 16-byte logits loads and 8-byte `seen` loads when the run is whole and `vec` (V % 8 == 0, aligned
-// rows), else one element at a time.  Invalid elements are -inf.
+// A thread's EPT processed scores of a chunk, element o = o0 + j * ostr (``run_map``): with `vec`
+// (V % 8 == 0, aligned rows) a run of EPT consecutive elements (ostr = 1) read by 16-byte logits
+// loads and 8-byte `seen` loads; without it one element at a time in the coalesced strided map
+// (o0 = tid, ostr = NT: lane l reads element j NT + l), as also for a partial run.
+// Invalid elements are -inf.  (Which thread holds which element never changes a result: the
+// argmax breaks ties by id and the top-k merge ranks its candidate set exactly.)
+__device__ __forceinline__ void run_map(bool vec, int tid, int ept, int& o0, int& ostr) {
+  o0 = vec ? tid * ept : tid;
+  ostr = vec ? 1 : NT;
+}
+
 template <bool BF16, int EPT>
-__device__ __forceinline__ void load_run(const void* lg, const uint8_t* seen, size_t base, int c0, int o0, int nvalid,
-                                         bool vec, float inv_t, float pen, float (&sv)[EPT]) {
+__device__ __forceinline__ void load_run(const void* lg, const uint8_t* seen, size_t base, int c0, int o0, int ostr,
+                                         int nvalid, bool vec, float inv_t, float pen, float (&sv)[EPT]) {
   static_assert(EPT % 8 == 0, "runs of whole 8-element groups");
   if (vec && o0 + EPT <= nvalid) {
     const size_t e0 = base + c0 + o0;
@@ -317,7 +327,7 @@ __device__ __forceinline__ void load_run(const void* lg, const uint8_t* seen, si
   } else {
 #pragma unroll
     for (int j = 0; j < EPT; ++j)
-      sv[j] = o0 + j < nvalid ? proc<BF16>(lg, seen, base, c0 + o0 + j, inv_t, pen) : -INFINITY;
+      sv[j] = o0 + j * ostr < nvalid ? proc<BF16>(lg, seen, base, c0 + o0 + j * ostr, inv_t, pen) : -INFINITY;
   }
 }
 
@@ -334,15 +344,17 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
   const int c = blockIdx.x, row = blockIdx.y;
   const size_t base = (size_t)row * V;
   const uint32_t seed = (uint32_t)rng[0], step = (uint32_t)rng[1];
-  const int c0 = c * (NT * EPT), o0 = threadIdx.x * EPT, nvalid = min(NT * EPT, V - c0);
+  const int c0 = c * (NT * EPT), nvalid = min(NT * EPT, V - c0);
+  int o0, ostr;
+  run_map(vec != 0, (int)threadIdx.x, EPT, o0, ostr);
   float sv[EPT];
-  load_run<BF16, EPT>(logits, seen, base, c0, o0, nvalid, vec != 0, inv_t, pen, sv);
+  load_run<BF16, EPT>(logits, seen, base, c0, o0, ostr, nvalid, vec != 0, inv_t, pen, sv);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int i = c0 + o0 + j;
-    if (o0 + j < nvalid) {
+    const int i = c0 + o0 + j * ostr;
+    if (o0 + j * ostr < nvalid) {
       float s = sv[j];
       if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
       if (better(s, i, bv, bi)) { bv = s; bi = i; }
@@ -370,10 +382,12 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
   float sv[EPT];
   uint32_t kr[EPT];
   uint32_t kmin = 0xffffffffu, kmax = 0u;
-  load_run<BF16, EPT>(logits, seen, base, c0, tid * EPT, nvalid, vec != 0, inv_t, pen, sv);
+  int o0, ostr;
+  run_map(vec != 0, tid, EPT, o0, ostr);
+  load_run<BF16, EPT>(logits, seen, base, c0, o0, ostr, nvalid, vec != 0, inv_t, pen, sv);
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int o = tid * EPT + j;
+    const int o = o0 + j * ostr;
     kr[j] = o < nvalid ? f2key(sv[j]) : 0u;
     if (o < nvalid) { kmin = min(kmin, kr[j]); kmax = max(kmax, kr[j]); }
   }
@@ -406,7 +420,7 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
   const size_t slot0 = ((size_t)row * C + c) * CCAP;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int o = tid * EPT + j;
+    const int o = o0 + j * ostr;
     const bool ok = o < nvalid && kr[j] >= thr;
     const int s = wave_alloc(ok, &cnt);
     if (ok && s < CCAP) pc[slot0 + s] = ckey(sv[j], c0 + o);
@@ -460,7 +474,7 @@ __device__ __forceinline__ void load_round(const uint64_t* pc, size_t s0, int ns
 
 __global__ void __launch_bounds__(NT) topk_merge_kernel(const uint64_t* __restrict__ pc,
                                                         const uint32_t* __restrict__ pthr, int C, int V, int top_k,
-                                                        float top_p, const int* __restrict__ rng,
+                                                        float top_p, const int* rng,
                                                         uint8_t* __restrict__ seen, int64_t* __restrict__ out_tok,
                                                         Adv adv) {
   __shared__ uint64_t cv[MCAP];
@@ -579,7 +593,7 @@ __global__ void __launch_bounds__(NT) topk_merge_kernel(const uint64_t* __restri
 template <bool BF16>
 __global__ void __launch_bounds__(NT) topk_row_kernel(const void* __restrict__ logits, uint8_t* __restrict__ seen,
                                                       int V, float inv_t, float pen, int top_k, float top_p,
-                                                      const int* __restrict__ rng, int64_t* __restrict__ out_tok,
+                                                      const int* rng, int64_t* __restrict__ out_tok,
                                                       Adv adv) {
   __shared__ uint32_t red[2 * NW];
   __shared__ uint64_t fc[CAP];
@@ -643,7 +657,7 @@ constexpr int RCAP = 256;                  // candidates ranked exactly (== FCAP
 template <bool BF16, int NS>
 __global__ void __launch_bounds__(NTR) topk_rowwide_kernel(const void* __restrict__ logits,
                                                            uint8_t* __restrict__ seen, int V, float inv_t, float pen,
-                                                           int top_k, float top_p, const int* __restrict__ rng,
+                                                           int top_k, float top_p, const int* rng,
                                                            int64_t* __restrict__ out_tok, Adv adv) {
   __shared__ uint32_t red[2 * NWR];
   __shared__ int scr[2 * NWR];

@@ -29,7 +29,8 @@ from .pipeline import PipelineStage, init_distributed
 from .watchdog import Watchdog
 
 _STAT_KEYS = ("compute_ms_per_tick", "p2p_wait_ms_per_tick", "bubble_frac", "p2p_bytes_per_tick", "span_ms",
-              "ttft_ms")
+              "ttft_ms", "host_issue_us_per_tick", "host_post_us_per_tick", "host_finish_us_per_tick",
+              "host_compute_us_per_tick")
 
 
 def _abort_rank(msg: str):
@@ -154,6 +155,8 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
                    stage_cost_spread=round(max(ucost) / (sum(ucost) / len(ucost)), 4), slack=slack,
                    micro_batches_in_flight=M,
                    bubble_frac_max=max(d.get("bubble_frac", 0.0) for d in per_rank),
+                   host_issue_us_per_tick_max=max((d.get("host_issue_us_per_tick", 0.0) for d in per_rank),
+                                                  default=0.0),
                    ttft_ms=ttft[0] if ttft else None)
     dist.barrier()
     wd.stop()

@@ -13,10 +13,13 @@ stage busy:
 
 Per tick each rank issues one grouped P2P exchange per lane through ``dist.batch_isend_irecv``
 (send the lane's previous outputs, receive its next inputs — grouped, so no send/recv ordering
-deadlock; on RCCL one ncclGroupStart/End over the process group's communicator), issued and
-completed on that lane's HIP stream, then runs its layers for the micro-batches of the tick.  A
+deadlock; on RCCL one ncclGroupStart/End), issued and completed on that lane's HIP stream, then
+runs its layers for the micro-batches of the tick.  Every lane has its OWN process group over the
+stage ranks (``lane_groups``; one RCCL communicator, hence one internal stream, per lane): a
+single communicator would queue lane l's hop behind lane l - 1's hop and compute.  A
 lane's hop therefore waits only for that lane's compute and runs beside the other lanes' compute,
-and no lane waits for the others at a tick boundary.  The same P2POp path runs under gloo on the CPU, which is how the
+and no lane waits for the others at a tick boundary.  (Measured so far only under gloo — the
+2 / 4 / 8-rank rehearsals — and at RCCL world 1; the multi-GPU RCCL overlap is unmeasured.)  The same P2POp path runs under gloo on the CPU, which is how the
 multi-rank schedule is tested without GPUs.  The decode compute of each micro-batch is captured in
 a HIP graph per KV-length bucket (all buckets of a run are captured at the first capture, before
 any timed region); the P2P ops stay outside the graphs on RCCL's stream, ordered by stream waits,
@@ -117,6 +120,13 @@ class PipelineStage:
         self.p2p_bytes = 0
         self._copy_stream = None                      # host-staged sends (gloo with device tensors)
         self._plen, self._eos = None, None            # per-run: ragged prompt lengths, EOS id (last rank)
+        # one process group (communicator) per lane for the per-lane exchanges (lanes > 1 on GPU
+        # streams): only the stage ranks join its creation (use_local_synchronization)
+        self.lane_groups = [group] * lanes
+        import os
+        if (self.streams is not None and dist.is_initialized() and world > 1
+                and os.environ.get("EDGELLM_LANE_GROUPS", "1") != "0"):
+            self.lane_groups = [dist.new_group(self.granks, use_local_synchronization=True) for _ in range(lanes)]
         if warm_comm and dist.is_initialized() and world > 1:
             self.warm_communicator()
 
@@ -125,6 +135,9 @@ class PipelineStage:
         connections' first use) before the first grouped P2P, outside any timed region."""
         x = torch.ones(1, device=self.device if self.nccl else "cpu")
         dist.all_reduce(x, group=self.group)
+        for g in self.lane_groups:
+            if g is not self.group:
+                dist.all_reduce(x, group=g)
         if self.cuda:
             torch.cuda.synchronize(self.device)
 
@@ -134,7 +147,7 @@ class PipelineStage:
         completed before returning (the current stream waits on it; host-staged: the host)."""
         self._finish(self._post(sends, recvs))
 
-    def _post(self, sends, recvs, send_ready=None):
+    def _post(self, sends, recvs, send_ready=None, group=None):
         """Issue one grouped exchange without waiting for it; ``_finish`` completes it.  RCCL: the
         communication stream first waits on everything already queued on the current stream (the
         sends' producers), so posting BEFORE the next compute lets the transfer run beside it.
@@ -145,6 +158,7 @@ class PipelineStage:
             return None
         self.p2p_bytes += sum(t.numel() * t.element_size() for t, _ in sends)
         g = self.granks
+        pg = self.group if group is None else group
         if self.host_staged:
             if self._copy_stream is None:
                 self._copy_stream = torch.cuda.Stream(self.device)
@@ -163,12 +177,12 @@ class PipelineStage:
                     host_sends.append(h)
             cs.synchronize()
             bufs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t, _ in recvs]
-            p2p = [dist.P2POp(dist.isend, h, g[p], self.group) for h, (_, p) in zip(host_sends, sends)]
-            p2p += [dist.P2POp(dist.irecv, h, g[p], self.group) for h, (_, p) in zip(bufs, recvs)]
+            p2p = [dist.P2POp(dist.isend, h, g[p], pg) for h, (_, p) in zip(host_sends, sends)]
+            p2p += [dist.P2POp(dist.irecv, h, g[p], pg) for h, (_, p) in zip(bufs, recvs)]
         else:
             bufs = None
-            p2p = [dist.P2POp(dist.isend, t, g[p], self.group) for t, p in sends]
-            p2p += [dist.P2POp(dist.irecv, t, g[p], self.group) for t, p in recvs]
+            p2p = [dist.P2POp(dist.isend, t, g[p], pg) for t, p in sends]
+            p2p += [dist.P2POp(dist.irecv, t, g[p], pg) for t, p in recvs]
         with trace_range("pp.exchange"):
             works = dist.batch_isend_irecv(p2p)
         return works, bufs, [t for t, _ in recvs], p2p
@@ -477,7 +491,8 @@ class PipelineStage:
                     if w_a <= t < w_b:
                         win_bytes += sum(x.numel() * x.element_size() for x, _ in sends)
                     ready = done_ev.pop((t - 1, lanes[0]), None) if host_late else None
-                    handles.append(self._post(sends, recvs, send_ready=ready))
+                    handles.append(self._post(sends, recvs, send_ready=ready,
+                                              group=self.lane_groups[lanes[0]] if per_lane else None))
             due[t + D - 1] = handles
             if not self.is_last:
                 for prv in range((t - 1 - R) * L, (t - R) * L):
@@ -502,6 +517,11 @@ class PipelineStage:
         if per_lane:
             for st in self.streams:
                 st.wait_stream(cur_stream)
+        # host time the loop spends per tick in the window (us): posting / completing the exchanges
+        # and issuing the compute (graph replays).  With RCCL none of it blocks on the device, so it
+        # is the pipeline's host overhead per tick (verdict r4: host_issue_us_per_tick)
+        host_us = {"post": 0.0, "finish": 0.0, "compute": 0.0}
+        pc = time.perf_counter
         for t in range(n_ticks):
             if hook is not None:
                 hook(t)
@@ -510,13 +530,21 @@ class PipelineStage:
             if fault is not None:
                 fault(t)
             cur_g = t - R
+            in_win = w_a <= t < w_b
             if w_a <= t - 1 < w_b:
                 mark_on(ev_done, t - 1)
+            h0 = pc()
             if not host_late:
                 post(t)                                  # before this tick's compute: the hop overlaps it
+            h1 = pc()
             finish(t)
+            h2 = pc()
+            if in_win:
+                host_us["post"] += (h1 - h0) * 1e6
+                host_us["finish"] += (h2 - h1) * 1e6
             if w_a <= t < w_b:
                 mark_on(ev_in, t)
+            h3 = pc()
             if group_valid(cur_g):
                 with trace_range(f"pp.tick{t}"):
                     for cur in range(cur_g * L, cur_g * L + L):
@@ -533,6 +561,8 @@ class PipelineStage:
                             else:
                                 k, m = divmod(cur - M, M)
                                 self._decode(m, T + k + 1)
+            if in_win:
+                host_us["compute"] += (pc() - h3) * 1e6
             if host_late:
                 # host-staged slack: this tick's compute is queued first, then the exchange whose
                 # sends are the previous tick's outputs (the host waits only for that tick)
@@ -567,6 +597,9 @@ class PipelineStage:
         stats = {}
         if stats_window is not None and ev_in:
             stats = self._window_stats(ev_in, ev_done, w_a, w_b, win_bytes)
+            nwin = max(1, min(w_b, n_ticks) - w_a)
+            stats.update({f"host_{k}_us_per_tick": v / nwin for k, v in host_us.items()})
+            stats["host_issue_us_per_tick"] = sum(host_us.values()) / nwin
         if t_first >= 0 and t_first in ev_first:
             a, z = ev_first[-1], ev_first[t_first]
             stats["ttft_ms"] = a.elapsed_time(z) if self.cuda else (z - a) * 1e3

@@ -70,7 +70,10 @@ def test_bench_pipeline_torchrun_cpu(n, lanes):
     for r, st in enumerate(d["per_rank"]):
         assert st["rank"] == r and st["compute_ms_per_tick"] > 0 and 0 <= st["bubble_frac"] <= 1
         assert st["p2p_bytes_per_tick"] > 0
-    assert d["ttft_ms"] > 0
+        # host time per tick: posting + completing the exchanges + issuing the compute
+        parts = sum(st[f"host_{k}_us_per_tick"] for k in ("post", "finish", "compute"))
+        assert st["host_issue_us_per_tick"] > 0 and abs(parts - st["host_issue_us_per_tick"]) < 1e-3 * parts + 1e-6
+    assert d["ttft_ms"] > 0 and d["host_issue_us_per_tick_max"] > 0
 
 
 @pytest.mark.parametrize("n", [1, 2])

@@ -108,6 +108,8 @@ def test_rccl_world1_pipeline(cuda, record_property):
     self_p2p = rec.get("self_p2p", "hung: no result within the child's time limit")
     record_property("rccl_self_p2p", self_p2p)
     print(f"[rccl world1] self-peer P2P via PipelineStage._exchange: {self_p2p}")
-    assert self_p2p == "ok" or self_p2p.startswith(("refused", "hung")), self_p2p
+    # RCCL (ROCm 7.2 / torch 2.10) accepts a self-peer grouped send/recv: the one P2P path a
+    # one-GPU box can exercise end to end (tools/recipes/r5b_rccl.sh records it in profiles/)
+    assert self_p2p == "ok", self_p2p
     if state == "done":
         assert p.exitcode == 0, p.exitcode
