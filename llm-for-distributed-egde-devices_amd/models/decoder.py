@@ -231,7 +231,8 @@ class DecoderLayer(nn.Module):
             if self.has_attn:
                 qa = self.attn.qkv.takes_quantized_input
                 d1 = getattr(self.attn.qkv, "pending_norm_ok", lambda glu=False: False)()
-                n1, h = self.norm1(x, residual, quant=qa, defer=d1)
+                # 129-256 rows: the qkv projection takes the int8 rows fragment-packed (w8a8_r256)
+                n1, h = self.norm1(x, residual, quant=qa, defer=d1, packed_for=self.attn.qkv if qa else None)
                 a = self.attn(n1, ctx)
                 if not self.has_mlp:
                     return a, h                        # stage exit after the attention half

@@ -20,9 +20,12 @@ from .. import ops
 
 
 class QAct(NamedTuple):
-    """Per-token symmetric INT8 activation: x ~= q * scale[:, None]."""
+    """Per-token symmetric INT8 activation: x ~= q * scale[:, None].  ``packed``: q is the [M, K]
+    view of a fragment-packed [256, K] buffer (the 256-row decode GEMM's operand layout, written by
+    the norm kernel: ops.rms_norm_quant(..., packed=True)); only ``W8A8Linear`` reads it."""
     q: torch.Tensor
     scale: torch.Tensor
+    packed: bool = False
 
 
 class PartialSum(NamedTuple):
@@ -118,11 +121,21 @@ class Norm(nn.Module):
         self.bias = (nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device), requires_grad=False)
                      if kind == "layer" else None)
 
-    def forward(self, x, residual=None, quant: bool = False, defer: bool = False):
+    def forward(self, x, residual=None, quant: bool = False, defer: bool = False, packed_for=None):
         """Returns (y, residual_out) where residual_out = x + residual; y is a QAct when quant.
         ``x`` may be a PartialSum (split-K projection output), summed inside the norm kernel.
         ``defer`` (the consumer is a W8A8 GEMV that takes it): at <= 4 rows, y is a PendingNorm that
-        the consumer's kernel computes, and residual_out is the buffer it fills."""
+        the consumer's kernel computes, and residual_out is the buffer it fills.
+        ``packed_for`` (the consumer projection): when it takes a fragment-packed activation at these
+        rows (``W8A8Linear.takes_packed``), the int8 rows are written packed (QAct.packed)."""
+        if quant and self.kind == "rms" and packed_for is not None:
+            M = (x.parts.shape[1] if isinstance(x, PartialSum) else x.numel() // x.shape[-1])
+            if getattr(packed_for, "takes_packed", lambda m: False)(M):
+                if isinstance(x, PartialSum):
+                    y, s, r = ops.rms_norm_parts(x.parts, residual, self.weight, self.eps, True, packed=True)
+                else:
+                    y, s, r = ops.rms_norm_quant(x, self.weight, self.eps, residual, packed=True)
+                return QAct(y, s, True), r
         if defer and quant and isinstance(x, PartialSum) and self.kind == "rms" and ops.gemv_norm_ok(x.parts):
             # residual None: a stage's first norm, over the embedding as one fp32 slice
             h = torch.empty(x.parts.shape[1], x.parts.shape[2], dtype=self.weight.dtype, device=x.parts.device)

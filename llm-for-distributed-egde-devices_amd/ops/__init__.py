@@ -71,10 +71,34 @@ def gpu_path(t: torch.Tensor) -> bool:
     return _gpu(t)
 
 
-def rms_norm_parts(parts, residual, weight, eps, quant: bool):
+def rms_norm_parts(parts, residual, weight, eps, quant: bool, packed: bool = False):
     """RMSNorm of the in-order sum of split-K partial slices parts [S, M, H] (fp32) rounded to bf16
-    (+ residual): returns (y bf16 | q int8, per-token scale | None, h = bf16 sum (+ residual))."""
-    return ext().rms_norm_parts(parts, residual, weight, eps, quant)
+    (+ residual): returns (y bf16 | q int8, per-token scale | None, h = bf16 sum (+ residual)).
+    ``packed`` (quant, 129-256 rows): q is the [M, H] view of a fragment-packed [256, H] buffer for
+    the 256-row decode GEMM (``w8a8_r256``)."""
+    return ext().rms_norm_parts(parts, residual, weight, eps, 2 if (quant and packed) else int(quant))
+
+
+def r256_ok(M: int, N: int, K: int) -> bool:
+    """Whether the packed-activation 256-row decode GEMM (gemm_i8.hip w8a8_r256_kernel) takes this
+    W8A8 shape on the GPU (129-256 rows; tune knob ``r256_packed``)."""
+    return 128 < M <= 256 and available() and bool(ext().r256_ok(M, N, K))
+
+
+def w8a8_r256(qx_packed, x_scale, w_packed, w_scale, bias, N: int, K: int):
+    """W8A8 GEMM of a fragment-packed activation (``rms_norm_quant(..., packed=True)``) at 129-256
+    rows -> bf16 [M, N]; None when the packed kernel does not take the shape."""
+    out = ext().w8a8_r256(qx_packed, x_scale.reshape(-1), w_packed, w_scale, bias, N, K)
+    return out if out.numel() else None
+
+
+def unpack_a(q_packed, M: int, K: int):
+    """Row-major int8 [M, K] of a fragment-packed activation (piece (rb, kt) = 16 rows x 64 k at
+    (rb * K/64 + kt) * 1024, lane l's 16 B = row 16 rb + (l & 15), k 64 kt + 16 (l >> 4) ..)."""
+    KT = K // 64
+    buf = torch.as_strided(q_packed, (256 * K,), (1,))
+    t = buf.view(16, KT, 4, 16, 16)                     # [rb, kt, k16 group, row in rb, byte]
+    return t.permute(0, 3, 1, 2, 4).reshape(256, K)[:M].contiguous()
 
 
 # rows up to which decode norms move into the next GEMV's prologue (kernel: <= 4).  Measured on
@@ -150,15 +174,16 @@ def layer_norm(x, weight, bias, eps, residual=None):
     return _ref.layer_norm(x, weight, bias, eps, residual)
 
 
-def rms_norm_quant(x, weight, eps, residual=None):
+def rms_norm_quant(x, weight, eps, residual=None, packed: bool = False):
+    """``packed`` (GPU, 129-256 rows): the int8 rows fragment-packed for ``w8a8_r256``."""
     if _gpu(x):
-        return ext().norm(x, residual, weight, None, eps, True, True)
+        return ext().norm(x, residual, weight, None, eps, True, 2 if packed else 1)
     return _ref.rms_norm_quant(x, weight, eps, residual)
 
 
 def layer_norm_quant(x, weight, bias, eps, residual=None):
     if _gpu(x):
-        return ext().norm(x, residual, weight, bias, eps, False, True)
+        return ext().norm(x, residual, weight, bias, eps, False, 1)
     return _ref.layer_norm_quant(x, weight, bias, eps, residual)
 
 

@@ -12,7 +12,7 @@
 
 extern "C" {
 int edge_norm(const void* x, const void* res, const void* w, const void* b, void* y, void* yq, float* ys,
-              void* res_out, int rows, int H, float eps, int rms, int quant, const float* xpart, int S,
+              void* res_out, int rows, int H, float eps, int rms, int quant, const float* xpart, int S, int h16,
               hipStream_t st);
 int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* gamma, float eps, void* res_out,
                         const void* Wp, const float* sw, const void* bias, void* out, float* os, int M, int N, int K,
@@ -21,12 +21,13 @@ void edge_w8a8_gemv_norm_cfg(int on);
 int edge_w8a8_gemv_norm_on();
 int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                           float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S, hipStream_t st);
-int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant, hipStream_t st);
+int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant, int h16,
+             hipStream_t st);
 int edge_quant(const void* x, void* q, float* s, int rows, int H, hipStream_t st);
 int edge_group_quant(const void* x, void* q, float* s, int M, int K, int Mpad, hipStream_t st);
-int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, int out_f32,
+int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, int out_f32, int h16,
                    hipStream_t st);
-int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st);
+int edge_max_prob(const void* logits, float* out, int rows, int V, int dt, hipStream_t st);
 int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, void* q_out, void* k_cache,
                        void* v_cache, int B, int T, int Hq, int Hkv, int D, int rot, int64_t c_sb, int64_t c_sh,
                        int S, void* k2, void* v2, int64_t c2_sb, int64_t c2_sh, int S2, int split_h,
@@ -101,6 +102,10 @@ int edge_bf16_ring_min_rows();
 void edge_decode_attn_gsplit(int v);
 void edge_decode_attn_small(int v);
 void edge_decode_attn_early(int v);
+int edge_w8a8_r256_ok(int M, int N, int K, int epi);
+int edge_w8a8_r256(const void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                   int M, int N, int K, int epi, hipStream_t st);
+void edge_w8a8_r256_cfg(int on);
 }
 
 namespace {
@@ -124,26 +129,48 @@ void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
 
 int64_t rows_of(const at::Tensor& x) { return x.numel() / x.size(-1); }
 
+// A 16-bit float activation / weight: bf16 (the default) or fp16 (the fp16 agents).  Returns 1 for
+// fp16, 0 for bf16.
+int need16(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, name, " has dtype ",
+              t.scalar_type(), ", expected bfloat16 or float16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  return t.scalar_type() == at::kHalf ? 1 : 0;
+}
+void need_same(const at::Tensor& t, const at::Tensor& like, const char* name) {
+  TORCH_CHECK(t.scalar_type() == like.scalar_type(), name, " has dtype ", t.scalar_type(), ", expected ",
+              like.scalar_type());
+}
+
 // ---------------------------------------------------------------------------------- norms
 std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Tensor& x,
                                                                     const std::optional<at::Tensor>& residual,
                                                                     const at::Tensor& w,
                                                                     const std::optional<at::Tensor>& b, double eps,
-                                                                    bool rms, bool quant) {
+                                                                    bool rms, int64_t quant) {
   DEVICE_GUARD(x);
-  need(x, at::kBFloat16, "x");
-  need(w, at::kBFloat16, "weight");
+  const int h16 = need16(x, "x");
+  TORCH_CHECK(!(h16 && quant), "int8 output from fp16 rows is not supported");
+  need16(w, "weight");
+  need_same(w, x, "weight");
   const int64_t H = x.size(-1), R = rows_of(x);
   TORCH_CHECK(w.numel() == H, "norm weight size mismatch");
-  if (b) { need(*b, at::kBFloat16, "bias"); TORCH_CHECK(b->numel() == H); }
+  if (b) { need16(*b, "bias"); need_same(*b, x, "bias"); TORCH_CHECK(b->numel() == H); }
   at::Tensor res_out = x;
   if (residual) {
-    need(*residual, at::kBFloat16, "residual");
+    need16(*residual, "residual");
+    need_same(*residual, x, "residual");
     TORCH_CHECK(residual->sizes() == x.sizes(), "residual shape mismatch");
     res_out = at::empty_like(x);
   }
   at::Tensor y, s;
-  if (quant) {
+  if (quant == 2) {
+    // fragment-packed for the 256-row decode GEMM: a [256, H] buffer, its first R "rows" returned
+    TORCH_CHECK(R <= 256 && H % 64 == 0 && x.dim() == 2, "packed int8 output: <= 256 rows, H % 64 == 0");
+    y = at::empty({256, H}, x.options().dtype(at::kChar)).narrow(0, 0, R);
+    s = at::empty({R}, x.options().dtype(at::kFloat));
+  } else if (quant) {
     y = at::empty(x.sizes(), x.options().dtype(at::kChar));
     auto ss = x.sizes().vec();
     ss.pop_back();
@@ -154,7 +181,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
   check(edge_norm(x.data_ptr(), residual ? residual->data_ptr() : nullptr, w.data_ptr(),
                   b ? b->data_ptr() : nullptr, quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr,
                   quant ? s.data_ptr<float>() : nullptr, residual ? res_out.data_ptr() : nullptr, (int)R, (int)H,
-                  (float)eps, rms, quant, nullptr, 0, stream()),
+                  (float)eps, rms, quant, nullptr, 0, h16, stream()),
         "norm");
   return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
 }
@@ -163,7 +190,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
 // slice order, rounded to bf16): returns (y or q, scale, h) with h = bf16(sum) (+ residual).
 std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(const at::Tensor& parts,
                                                                               const std::optional<at::Tensor>& residual,
-                                                                              const at::Tensor& w, double eps, bool quant) {
+                                                                              const at::Tensor& w, double eps, int64_t quant) {
   DEVICE_GUARD(parts);
   need(parts, at::kFloat, "parts");
   need(w, at::kBFloat16, "weight");
@@ -177,7 +204,11 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(con
     TORCH_CHECK(residual->numel() == R * H, "residual shape mismatch");
   }
   at::Tensor y, s;
-  if (quant) {
+  if (quant == 2) {                                   // fragment-packed (see norm)
+    TORCH_CHECK(R <= 256 && H % 64 == 0, "packed int8 output: <= 256 rows, H % 64 == 0");
+    y = at::empty({256, H}, opts.dtype(at::kChar)).narrow(0, 0, R);
+    s = at::empty({R}, opts.dtype(at::kFloat));
+  } else if (quant) {
     y = at::empty({R, H}, opts.dtype(at::kChar));
     s = at::empty({R}, opts.dtype(at::kFloat));
   } else {
@@ -185,7 +216,8 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(con
   }
   check(edge_norm(nullptr, residual ? residual->data_ptr() : nullptr, w.data_ptr(), nullptr,
                   quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr, quant ? s.data_ptr<float>() : nullptr,
-                  res_out.data_ptr(), (int)R, (int)H, (float)eps, 1, quant, parts.data_ptr<float>(), (int)S, stream()),
+                  res_out.data_ptr(), (int)R, (int)H, (float)eps, 1, quant, parts.data_ptr<float>(), (int)S, 0,
+                  stream()),
         "rms_norm_parts");
   return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
 }
@@ -194,7 +226,8 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(con
 // ---------------------------------------------------------------------------------- activations
 std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64_t mode, bool quant) {
   DEVICE_GUARD(x);
-  need(x, at::kBFloat16, "x");
+  const int h16 = need16(x, "x");
+  TORCH_CHECK(!(h16 && quant), "int8 output from fp16 rows is not supported");
   const int64_t W = x.size(-1), R = rows_of(x);
   const int64_t F = (mode == 0 || mode == 3) ? W / 2 : W;
   TORCH_CHECK(mode != 3 || F % 16 == 0, "blocked GLU needs F % 16 == 0");
@@ -210,7 +243,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> act(const at::Tensor& x, int64
     y = at::empty(os, x.options());
   }
   check(edge_act(x.data_ptr(), quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr,
-                 quant ? s.data_ptr<float>() : nullptr, (int)R, (int)F, (int)mode, quant, stream()),
+                 quant ? s.data_ptr<float>() : nullptr, (int)R, (int)F, (int)mode, quant, h16, stream()),
         "act");
   return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt};
 }
@@ -231,12 +264,12 @@ std::tuple<at::Tensor, at::Tensor> quant(const at::Tensor& x) {
 at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table, bool out_f32) {
   DEVICE_GUARD(ids);
   need(ids, at::kLong, "ids");
-  need(table, at::kBFloat16, "table");
+  const int h16 = need16(table, "table");
   auto os = ids.sizes().vec();
   os.push_back(table.size(1));
   auto out = at::empty(os, out_f32 ? table.options().dtype(at::kFloat) : table.options());
   check(edge_embedding(ids.data_ptr<int64_t>(), table.data_ptr(), out.data_ptr(), (int)ids.numel(),
-                       (int)table.size(1), (int)table.size(0), out_f32 ? 1 : 0, stream()),
+                       (int)table.size(1), (int)table.size(0), out_f32 ? 1 : 0, h16, stream()),
         "embedding");
   return out;
 }
@@ -244,8 +277,8 @@ at::Tensor embedding(const at::Tensor& ids, const at::Tensor& table, bool out_f3
 at::Tensor max_prob(const at::Tensor& logits) {
   DEVICE_GUARD(logits);
   TORCH_CHECK(logits.is_cuda() && logits.is_contiguous());
-  const bool bf = logits.scalar_type() == at::kBFloat16;
-  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
+  const int bf = logits.scalar_type() == at::kBFloat16 ? 1 : logits.scalar_type() == at::kHalf ? 2 : 0;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "logits must be bf16, fp16 or f32");
   const int64_t V = logits.size(-1), R = rows_of(logits);
   auto os = logits.sizes().vec();
   os.pop_back();
@@ -563,6 +596,25 @@ at::Tensor w8a8_gemm(const at::Tensor& a, const at::Tensor& sa, const at::Tensor
 
 // Split-K W8A8 GEMV (decode, M <= 64, <= 128 where rows128_ok(K, S), <= 256 where rows256_ok(K)): fp32 partial slices
 // [S, M, N] (w-scale and bias applied; bias in slice 0) for a consumer that sums them (rms_norm_parts).  S = 0 picks the split count.
+// 129-256 decode rows on a fragment-packed activation (norm(..., quant=2)): ap is the [M, K] view of
+// a [256, K] packed buffer; sa per-token [M].  Returns bf16 [M, N], or an empty tensor when the packed
+// kernel does not take the shape.
+at::Tensor w8a8_r256(const at::Tensor& ap, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
+                     const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
+  DEVICE_GUARD(ap);
+  need(ap, at::kChar, "a");
+  need(sa, at::kFloat, "a_scale");
+  const int64_t M = ap.size(0);
+  TORCH_CHECK(ap.dim() == 2 && ap.size(1) == K && ap.stride(0) == K, "a must be the [M, K] view of a packed buffer");
+  check_w8a8_operands(wp, sw, bias, N, K);
+  if (!edge_w8a8_r256_ok((int)M, (int)N, (int)K, 0)) return at::Tensor();
+  at::Tensor out = at::empty({M, N}, sw.options().dtype(at::kBFloat16));
+  check(edge_w8a8_r256(ap.data_ptr(), sa.data_ptr<float>(), wp.data_ptr(), sw.data_ptr<float>(),
+                       bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N, (int)K, 0, stream()),
+        "w8a8_r256");
+  return out;
+}
+
 at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                             const std::optional<at::Tensor>& bias, int64_t N, int64_t K, int64_t S) {
   DEVICE_GUARD(a);
@@ -962,6 +1014,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kv_quant_append", &kv_quant_append, "quantise bf16 K/V rows into an int8 KV cache (prefill append)");
   m.def("w8a8_gemm_glu", &w8a8_gemm_glu);
   m.def("w8a8_gemm_splitk", &w8a8_gemm_splitk);
+  m.def("w8a8_r256", &w8a8_r256, "129-256-row W8A8 GEMM on a fragment-packed activation (empty: shape not taken)");
+  m.def("r256_ok", [](int64_t M, int64_t N, int64_t K) { return edge_w8a8_r256_ok((int)M, (int)N, (int)K, 0) != 0; },
+        "whether the packed-activation 256-row kernel takes this shape");
   m.def("rms_norm_parts", &rms_norm_parts);
   m.def("w8a8_gemm_gluq", &w8a8_gemm_gluq);
   m.def("w8a8_gemv_norm", &w8a8_gemv_norm, "batch-1 W8A8 GEMV with the RMSNorm of split-K slices in its prologue");
@@ -996,6 +1051,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "sample_vec") edge_sample_vec((int)a);
     else if (what == "prefill_fa") edge_prefill_fa((int)a, b == 0 ? 1 : (int)b - 1);   // b: 0 default, 1 lockstep, 2 stagger
     else if (what == "gemv_norm") edge_w8a8_gemv_norm_cfg((int)a);
+    else if (what == "r256_packed") edge_w8a8_r256_cfg((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });
 }

@@ -1,6 +1,7 @@
 // Shared device helpers for the edgellm CDNA4 (gfx950) kernels.
 // Wave size is 64 everywhere (hard-coded: gfx950 has no wave32 mode for these kernels).
 #pragma once
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,6 +35,41 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   uint4 v;
   v.x = pack_bf2(f[0], f[1]); v.y = pack_bf2(f[2], f[3]);
   v.z = pack_bf2(f[4], f[5]); v.w = pack_bf2(f[6], f[7]);
+  return v;
+}
+
+// 16-bit float elements in memory as raw uint16 bits: bf16 (H = false, the default everywhere) or IEEE
+// fp16 (H = true: the reference's fp16 agents, Code/Base Models/phi2-pythia_fp_updated.py:32).
+// Kernels that move activations take a `bool H` template flag and convert through these.
+template <bool H>
+__device__ __forceinline__ float e2f(uint32_t u16) {
+  if constexpr (H) return __half2float(__ushort_as_half((unsigned short)u16));
+  else return bf2f(u16);
+}
+template <bool H>
+__device__ __forceinline__ uint16_t f2e(float f) {
+  if constexpr (H) return __half_as_ushort(__float2half(f));     // round to nearest even
+  else return f2bf(f);
+}
+template <bool H>
+__device__ __forceinline__ uint32_t pack_e2(float lo, float hi) {
+  return (uint32_t)f2e<H>(lo) | ((uint32_t)f2e<H>(hi) << 16);
+}
+template <bool H>
+__device__ __forceinline__ void unpack8e(const uint4& v, float* f) {
+  if constexpr (H) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = e2f<true>(w[i] & 0xffffu); f[2 * i + 1] = e2f<true>(w[i] >> 16); }
+  } else {
+    unpack8(v, f);
+  }
+}
+template <bool H>
+__device__ __forceinline__ uint4 pack8e(const float* f) {
+  uint4 v;
+  v.x = pack_e2<H>(f[0], f[1]); v.y = pack_e2<H>(f[2], f[3]);
+  v.z = pack_e2<H>(f[4], f[5]); v.w = pack_e2<H>(f[6], f[7]);
   return v;
 }
 

@@ -1953,6 +1953,297 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     }
   }
 }
+
+// ------------------------------------------------------------------------------------ r256
+// 129-256 decode rows (one 256-row decode micro-batch), activations FRAGMENT-PACKED: piece (rb, kt)
+// = 1 KiB at (rb * KT + kt) * 1024, lane l's 16 B = A[16 rb + (l & 15)][64 kt + 16 (l >> 4) ..]
+// (pack_a_kernel's layout; the decode producers — RMSNorm + quant, attention's int8 output, the
+// quantising SwiGLU epilogue — write it directly, `Mpad` rows).
+// Why: in ring2 above a compute wave's activation rows are private to it, so staging the activation
+// half through LDS buys nothing but a layout change and costs 16 KiB of LDS-DMA writes + 16 KiB of
+// LDS reads per 2-k-tile stage beside the weight ring's traffic.  Here every compute wave loads
+// its own A fragments global -> VGPR, DA stages ahead (one coalesced 1 KiB load per fragment, L2
+// hits), and only the weight panel — shared by all compute waves — goes through the LDS-DMA ring
+// (NWL loader waves, RW slots, one bare barrier per stage as in ring2).  Measured against ring2 with
+// tools/r256_lab.hip (Llama-2-7B shapes, 256 rows, HBM-cold weights): qkv 22.0-23.6 -> 20.6 us,
+// plain gate_up 45 -> 38.5, plain o 15.3 -> 11.3.
+// Geometry: RG x TG compute waves; wave (rg, tg) owns row blocks [rg RBW, (rg + 1) RBW) of the
+// workgroup's rows (RBW = rows / 16 / RG) and tiles [tg NTH, (tg + 1) NTH) (NTH = NTW / TG).
+// MS = 2: 128-row halves, blocks b and b + 8 share a weight panel (ring2's mapping); MS = 1: all 256
+// rows in one workgroup (every weight byte read by one CU).  NSL stages (2 k-tiles each) per
+// workgroup, fully unrolled so every activation register set has a name and the compiler waits on
+// them with counted vmcnt; EPI_PART: S split-K slices of NSL stages (K = 128 S NSL).
+// SC: per-(token, 64) activation scales [KT][Mpad] (the o / down inputs), loaded beside the
+// fragments, every k-tile's int32 MFMA sum folded into fp32 with ring2's one-VALU magic-number fold.
+// Epilogues: EPI_OUT bf16 (+ bias), EPI_PART fp32 slices, EPI_GLUQ SwiGLU + int8 per 64 features
+// (NTH == 8: a wave's tiles are one quant group), optionally written fragment-packed (PKO) for the
+// next 256-row GEMM.
+template <int NTW, int RG, int TG, int NWL, int RW, int DA, int MS, int NSL, int EPI, bool SC, bool PKO = false>
+__global__ void __launch_bounds__((RG * TG + NWL) * 64, 1) w8a8_r256_kernel(
+    const int8_t* __restrict__ Ap, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
+    const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
+    int M, int N, int NTt, int Mpad, int KT, int S, int G) {
+  constexpr int NCW = RG * TG, NTH = NTW / TG, ROWS = 256 / MS, RBW = ROWS / 16 / RG;
+  constexpr int WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, APS = RBW * 2;   // A loads per stage
+  static_assert(NTW % TG == 0 && (ROWS / 16) % RG == 0 && WST % NWL == 0, "geometry");
+  static_assert(DW * WPW <= 63 && DA * APS * (SC ? 2 : 1) <= 63 && DA >= 1, "vmcnt range");
+  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTH == 8 && !SC), "epilogues");
+  static_assert(!PKO || EPI == EPI_GLUQ, "packed output: the quantising SwiGLU epilogue");
+  constexpr int EPC = NTW * 16 <= 128 ? 128 : 256;
+  constexpr int LDS_B = RW * WST * 1024 + 2 * EPC * 4;
+  static_assert(LDS_B <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) int8_t lds[LDS_B];
+  int8_t* const wring = lds;
+  float* const epi_sw = reinterpret_cast<float*>(lds + RW * WST * 1024);
+  float* const epi_b = epi_sw + EPC;
+  int lbid = (int)blockIdx.x, row0 = 0;
+  if constexpr (MS == 2) {
+    // ring2's mapping: both halves of a panel (and neighbouring column groups) on one XCD under
+    // round-robin dispatch; EPI_PART keeps the round-robin order (an XCD holds a fixed subset of
+    // the K slices, whose activation bytes then stay in its L2).  Speed only.
+    const int x = (int)blockIdx.x & 7, j = (int)blockIdx.x >> 3, gx = (G + 7) >> 3;
+    row0 = (j & 1) * 128;
+    lbid = EPI == EPI_PART ? x | ((j >> 1) << 3) : x * gx + (j >> 1);
+    if ((j >> 1) >= gx || lbid >= G) return;        // whole workgroup: no barrier is left waiting
+  } else {
+    if (lbid >= G) return;
+  }
+  const int Ml = min(ROWS, M - row0);
+  const int grp = EPI == EPI_PART ? lbid / S : lbid;
+  const int ks = EPI == EPI_PART ? lbid % S : 0;
+  const int sbeg = ks * NSL;                          // first stage of this workgroup
+  // stages of this workgroup: NSL, fewer in the last split-K slice of a K that S does not divide
+  // (stages past nloc re-load its last stage and are skipped: the barrier count stays NSL)
+  const int nloc = min(NSL, KT / 2 - sbeg);
+  const int nt0 = grp * NTW;
+  auto phys_tile = [&](int t) -> int { return min(nt0 + t, NTt - 1); };
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  if (wave >= NCW) {                                  // ---- weight loaders: pieces (k-tile c, tile t)
+    const int lw = wave - NCW;
+    uint32_t woff[WPW];
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int q = lw * WPW + i, c = q / NTW, t = q % NTW;
+      woff[i] = ((uint32_t)phys_tile(t) * (uint32_t)KT + c) * 1024u + lane * 16;
+    }
+    auto issue = [&](int st) {                        // stages past the end re-load the last one
+      const int8_t* wb = Wp + (size_t)(sbeg + min(st, nloc - 1)) * 2048;
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
+    };
+    for (int st = 0; st < DW; ++st) issue(st);
+    for (int s = 0; s < NSL; ++s) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DW - 1) * WPW) : "memory");   // own pieces of stage s
+      __builtin_amdgcn_s_barrier();
+      issue(s + DW);                                  // into the slot of stage s - 1
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the workgroup
+    return;
+  }
+
+  // ---- compute wave (rg, tg)
+  const int rg = wave % RG, tg = wave / RG, tb = tg * NTH;
+  {
+    const int c = threadIdx.x;                        // >= 128 compute threads; EPC columns
+    for (int cc = c; cc < NTW * 16; cc += NCW * 64) {
+      const int col = min(phys_tile(cc >> 4) * 16 + (cc & 15), N - 1);
+      epi_sw[cc] = sw != nullptr ? sw[col] : 1.f;
+      epi_b[cc] = bias != nullptr ? bf2f(bias[col]) : 0.f;
+    }
+  }
+  float sa_r[RBW];
+#pragma unroll
+  for (int j = 0; j < RBW; ++j) sa_r[j] = SC ? 1.f : sa[row0 + min((rg * RBW + j) * 16 + (lane & 15), Ml - 1)];
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  const int8_t* ap = Ap + ((size_t)(row0 / 16 + rg * RBW) * KT + (size_t)sbeg * 2) * 1024 + lane * 16;
+  const float* sp = sa + (size_t)sbeg * 2 * Mpad + row0 + rg * RBW * 16 + (lane & 15);   // SC
+  v4i af[DA][RBW][2];
+  float sf[DA][RBW][2];
+  auto load_a = [&](int st, v4i (&f)[RBW][2], float (&g)[RBW][2]) {
+    const int p = min(st, nloc - 1);                  // past the end: re-load the last stage (unused)
+#pragma unroll
+    for (int j = 0; j < RBW; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        f[j][c] = *reinterpret_cast<const v4i*>(ap + ((size_t)j * KT + 2 * p + c) * 1024);
+        if constexpr (SC) g[j][c] = sp[(size_t)(2 * p + c) * Mpad + j * 16];
+      }
+  };
+  v4i acc[RBW][NTH];
+  v4f accf[RBW][NTH];
+#pragma unroll
+  for (int j = 0; j < RBW; ++j)
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) { acc[j][t] = v4i{0, 0, 0, 0}; accf[j][t] = v4f{0.f, 0.f, 0.f, 0.f}; }
+  // the one-VALU grouped-scale fold (ring2 DT = 2): each k-tile's MFMA starts from the bits of
+  // 1.5 * 2^23, so the int32 sum read as a float is 12582912 + sum; the offsets come out every 4
+  // stages from a per-row running scale sum
+  constexpr float MAGIC_F = 12582912.f;
+  v4i MAGIC_I = v4i{0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
+  asm volatile("" : "+v"(MAGIC_I));
+  float ssum[RBW];
+#pragma unroll
+  for (int j = 0; j < RBW; ++j) ssum[j] = 0.f;
+  auto unbias = [&]() {
+#pragma unroll
+    for (int j = 0; j < RBW; ++j) {
+      const float cb = -MAGIC_F * ssum[j];
+#pragma unroll
+      for (int t = 0; t < NTH; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) accf[j][t][q] += cb;
+      ssum[j] = 0.f;
+    }
+  };
+  const uint32_t w0 = lds_off(wring) + lane * 16 + tb * 1024;
+  auto read_w = [&](int st, int c, v4i (&f)[NTH]) { lds_read_row<NTH>(w0 + ((st % RW) * WST + c * NTW) * 1024, f); };
+  auto mma = [&](const v4i (&a)[RBW][2], const float (&g)[RBW][2], int c, v4i (&f)[NTH]) {
+#pragma unroll
+    for (int i = 0; i < NTH; ++i) asm volatile("" : "+v"(f[i]));
+    if constexpr (SC) {
+#pragma unroll
+      for (int j = 0; j < RBW; ++j) {
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) {
+          v4i r = mfma_i8(f[t], a[j][c], MAGIC_I);
+          asm volatile("" : "+v"(r));                 // (ring2: keeps the four elements apart)
+          const v4f rf = __builtin_bit_cast(v4f, r);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) accf[j][t][q] = __builtin_fmaf(rf[q], g[j][c], accf[j][t][q]);
+        }
+        ssum[j] += g[j][c];
+      }
+#pragma unroll
+      for (int j = 0; j < RBW; ++j)
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(accf[j][t]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < RBW; ++j)
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) acc[j][t] = mfma_i8(f[t], a[j][c], acc[j][t]);
+#pragma unroll
+      for (int j = 0; j < RBW; ++j)
+#pragma unroll
+        for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(acc[j][t]));
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < DA; ++u) load_a(u, af[u], sf[u]);
+  v4i xw[NTH], yw[NTH];
+  __builtin_amdgcn_s_barrier();                      // weight stage 0 visible
+  read_w(0, 0, xw);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) {
+    const bool live = s < nloc;                       // wave-uniform
+    read_w(s, 1, yw);
+    if (live) mma(af[s % DA], sf[s % DA], 0, xw);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (s + 1 < NSL) {
+      __builtin_amdgcn_s_barrier();                  // stage s + 1's weights; frees stage s - 1's slot
+      read_w(s + 1, 0, xw);
+    }
+    if (live) mma(af[s % DA], sf[s % DA], 1, yw);
+    if constexpr (SC) {
+      if ((s & 3) == 3 || s + 1 == NSL) unbias();
+    }
+    load_a(s + DA, af[s % DA], sf[s % DA]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue: lane holds row (rg RBW + j) * 16 + (lane & 15), columns 4 (lane >> 4) .. + 3 of tile t
+  const int g4 = 4 * (lane >> 4);
+  if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
+#pragma unroll
+    for (int j = 0; j < RBW; ++j) {
+      const int lrow = (rg * RBW + j) * 16 + (lane & 15);
+      if (lrow >= Ml) continue;
+      const int row = row0 + lrow;
+#pragma unroll
+      for (int t = 0; t < NTH; ++t) {
+        const int cl = (tb + t) * 16 + g4, col = nt0 * 16 + cl;
+        if (col >= N) continue;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float a = SC ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j];
+          v[q] = a * epi_sw[cl + q] + ((EPI == EPI_OUT || ks == 0) ? epi_b[cl + q] : 0.f);
+        }
+        if constexpr (EPI == EPI_PART) {
+          float* o = reinterpret_cast<float*>(outv) + ((size_t)ks * M + row) * N + col;
+          if (col + 3 < N && (N & 3) == 0) *reinterpret_cast<v4f*>(o) = v4f{v[0], v[1], v[2], v[3]};
+          else for (int q = 0; q < 4 && col + q < N; ++q) o[q] = v[q];
+        } else {
+          bf16_t* o = reinterpret_cast<bf16_t*>(outv) + (size_t)row * N + col;
+          if (col + 3 < N && (N & 3) == 0) *reinterpret_cast<uint2*>(o) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+          else for (int q = 0; q < 4 && col + q < N; ++q) o[q] = f2bf(v[q]);
+        }
+      }
+    }
+  } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
+    const int Fo = N / 2, grp64 = (nt0 + tb) / 8;
+    int8_t* hq = reinterpret_cast<int8_t*>(outv);
+    const bool live = nt0 + tb + 7 < NTt;
+    const int FT = Fo / 64;                           // k-tiles of the packed output (the down input)
+#pragma unroll
+    for (int j = 0; j < RBW; ++j) {
+      const int lrow = (rg * RBW + j) * 16 + (lane & 15);
+      const int row = row0 + lrow;
+      float h[4][4], amax = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cg = (tb + 2 * p) * 16 + g4 + q, cu = cg + 16;
+          const float g = bf2f(f2bf((float)acc[j][2 * p][q] * sa_r[j] * epi_sw[cg] + epi_b[cg]));   // the unfused GEMM output is bf16
+          const float u = bf2f(f2bf((float)acc[j][2 * p + 1][q] * sa_r[j] * epi_sw[cu] + epi_b[cu]));
+          h[p][q] = g / (1.f + __expf(-g)) * u;
+          amax = fmaxf(amax, fabsf(h[p][q]));
+        }
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));   // the row's 64 features sit in lanes l, l ^ 16, l ^ 32, l ^ 48
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      amax = fmaxf(amax, 1e-8f);
+      const float inv = 127.f / amax;
+      if (live && (PKO ? row < Mpad : lrow < Ml)) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          uint32_t w = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w |= (uint32_t)(uint8_t)quant_i8(h[p][q], inv) << (8 * q);
+          const int f = ((nt0 + tb) / 2 + p) * 16 + g4;          // output feature (4 consecutive)
+          if constexpr (PKO) {
+            // packed piece (row / 16, f / 64), lane slot (row & 15) + 16 ((f & 63) >> 4), byte f & 15
+            const size_t off = ((size_t)(row >> 4) * FT + (f >> 6)) * 1024 + ((row & 15) + 16 * ((f & 63) >> 4)) * 16 + (f & 15);
+            *reinterpret_cast<uint32_t*>(hq + off) = lrow < Ml ? w : 0u;
+          } else {
+            *reinterpret_cast<uint32_t*>(hq + (size_t)row * Fo + f) = w;   // Fo % 64 == 0
+          }
+        }
+      }
+      if (live && lane < 16 && row < Mpad) os[(size_t)grp64 * Mpad + row] = lrow < Ml ? amax / 127.f : 0.f;
+    }
+  }
+}
+
+// One r256 configuration: -1 when it does not take the shape (K % 128, or S slices of NSL stages
+// not covering K / 128 with every slice non-empty).
+template <int NTW, int RG, int TG, int NWL, int RW, int DA, int MS, int NSL, int EPI, bool SC, bool PKO = false>
+int launch_r256x(const void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
+                 float* os, int M, int N, int K, int Mpad, int S, hipStream_t st) {
+  const int NTt = (N + 15) / 16, KT = K / 64, NS = KT / 2;
+  if (K % 128 != 0 || M > 256 || Mpad < 256 || S < 1 || (EPI != EPI_PART && S != 1) || NSL * S < NS ||
+      NSL * (S - 1) >= NS)
+    return -1;
+  const int G = (NTt + NTW - 1) / NTW * S;
+  const int blocks = MS == 2 ? (G + 7) / 8 * 16 : G;
+  hipLaunchKernelGGL((w8a8_r256_kernel<NTW, RG, TG, NWL, RW, DA, MS, NSL, EPI, SC, PKO>), dim3(blocks),
+                     dim3((RG * TG + NWL) * 64), 0, st, (const int8_t*)Ap, sa, (const int8_t*)Wp, sw,
+                     (const bf16_t*)bias, out, os, M, N, NTt, Mpad, KT, S, G);
+  return (int)hipGetLastError();
+}
 }  // namespace
 
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2;
@@ -2130,6 +2421,30 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
 // blocks of accumulators.  Instantiated for the k-tile counts of the 4096-hidden models (K = 4096
 // whole, and K = 4096 / 11008 / 14336 in 4 split-K slices); -1 = no kernel for this shape.
 }  // namespace
+
+// 129-256 decode rows on FRAGMENT-PACKED activations (w8a8_r256_kernel; the producers write the
+// packed layout: rowwise.hip norm quant = 2).  Ap: a [256, K] packed buffer; sa: per-token scales
+// [>= M]; epi 0: bf16 out [M, N] (+ bias).  Geometries from tools/r256_lab.hip (Llama-2-7B, 256
+// rows, HBM-cold weights): 6 tiles (96 columns) per 128-row half for qkv-sized N, 2 tiles for
+// N <= 8192 (o-sized: 11.3 us against ring2's 15.3).  -2: no packed kernel for this shape (the
+// caller then feeds row-major activations to edge_w8a8_gemm).
+static int g_r256_packed = 1;
+extern "C" void edge_w8a8_r256_cfg(int on) { g_r256_packed = on; }
+extern "C" int edge_w8a8_r256_ok(int M, int N, int K, int epi) {
+  return g_r256_packed && M > 128 && M <= 256 && epi == EPI_OUT && (K == 2048 || K == 4096) && N % 4 == 0;
+}
+extern "C" int edge_w8a8_r256(const void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
+                              void* out, int M, int N, int K, int epi, hipStream_t st) {
+  if (!edge_w8a8_r256_ok(M, N, K, epi)) return -2;
+  const int NTt = (N + 15) / 16;
+  const bool wide = NTt > 512;
+#define R256(NTW, RW, NSL) return launch_r256x<NTW, 4, 1, 2, RW, 3, 2, NSL, EPI_OUT, false>(Ap, sa, Wp, sw, bias, out, \
+                                                                                    nullptr, M, N, K, 256, 1, st)
+  if (K == 4096) { if (wide) R256(6, 7, 32); R256(2, 14, 32); }
+  if (wide) R256(6, 7, 16);
+  R256(2, 14, 16);
+#undef R256
+}
 
 extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
 extern "C" void edge_w8a8_rows256_rot(int v) { g_r256_rot = v; }

@@ -18,14 +18,14 @@ struct Row {
 };
 
 // Load a bf16 row (optionally + residual) into registers. Elements >= H read as 0.
-template <int NCH>
+template <int NCH, bool HF = false>
 __device__ __forceinline__ void load_row(const bf16_t* __restrict__ x, int H, float (&v)[NCH][8]) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int e = (c * NT + threadIdx.x) * 8;
     if (e < H) {
       uint4 u = *reinterpret_cast<const uint4*>(x + e);
-      unpack8(u, v[c]);
+      unpack8e<HF>(u, v[c]);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
@@ -33,19 +33,24 @@ __device__ __forceinline__ void load_row(const bf16_t* __restrict__ x, int H, fl
   }
 }
 
-template <int NCH>
+template <int NCH, bool HF = false>
 __device__ __forceinline__ void store_row(bf16_t* __restrict__ y, int H, const float (&v)[NCH][8]) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int e = (c * NT + threadIdx.x) * 8;
-    if (e < H) *reinterpret_cast<uint4*>(y + e) = pack8(v[c]);
+    if (e < H) *reinterpret_cast<uint4*>(y + e) = pack8e<HF>(v[c]);
   }
 }
 
-// Quantise registers to int8 with a per-row scale (block-reduced absmax).
+// Quantise registers to int8 with a per-row scale (block-reduced absmax).  pkt > 0: row `row` goes
+// to the FRAGMENT-PACKED int8 layout of the 256-row decode GEMM (gemm_i8.hip w8a8_r256_kernel):
+// piece (row / 16, k / 64) = 1 KiB at (row / 16 * pkt + k / 64) * 1024, byte (row & 15 +
+// 16 ((k & 63) >> 4)) * 16 + (k & 15); pkt = H / 64 k-tiles.  A thread's 8 consecutive k stay 8
+// contiguous bytes.  Otherwise q is the row (row-major).
 template <int NCH>
 __device__ __forceinline__ void quant_store(float (&v)[NCH][8], int H, int8_t* __restrict__ q,
-                                            float* __restrict__ scale_out, float* red) {
+                                            float* __restrict__ scale_out, float* red, int pkt = 0,
+                                            size_t row = 0) {
   float amax = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -65,7 +70,10 @@ __device__ __forceinline__ void quant_store(float (&v)[NCH][8], int H, int8_t* _
       for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[c][j], inv)) << (8 * j);
 #pragma unroll
       for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[c][4 + j], inv)) << (8 * j);
-      *reinterpret_cast<uint2*>(q + e) = make_uint2(lo, hi);
+      int8_t* dst = pkt > 0 ? q + ((row >> 4) * (size_t)pkt + (e >> 6)) * 1024 +
+                                  ((row & 15) + 16 * ((e & 63) >> 4)) * 16 + (e & 15)
+                            : q + e;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
     }
   }
 }
@@ -74,12 +82,12 @@ __device__ __forceinline__ void quant_store(float (&v)[NCH][8], int H, int8_t* _
 // PART: x arrives as S fp32 split-K partial slices [S][rows][H] of a W8A8 projection
 // (gemm_i8.hip EPI_PART); they are summed in slice order and rounded to bf16 — the value the
 // unsplit GEMV would have written — and that bf16 row is always written to res_out.
-template <int NCH, bool RMS, bool HAS_RES, bool QUANT, bool PART>
+template <int NCH, bool RMS, bool HAS_RES, bool QUANT, bool PART, bool HF = false>
 __global__ void __launch_bounds__(NT) norm_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ b, bf16_t* __restrict__ y, int8_t* __restrict__ yq,
     float* __restrict__ ys, bf16_t* __restrict__ res_out, int H, float eps, const float* __restrict__ xpart,
-    int S) {
+    int S, int pkt) {
   __shared__ float red[NT / 64];
   const size_t row = blockIdx.x;
   // gamma (and beta) chunks are loaded up front with the row, so no global load sits between
@@ -128,22 +136,22 @@ __global__ void __launch_bounds__(NT) norm_kernel(
           v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
         }
       if (e < H) {
-        unpack8(pack8(v[c]), v[c]);                        // the GEMV output is bf16
-        if constexpr (!HAS_RES) *reinterpret_cast<uint4*>(res_out + row * H + e) = pack8(v[c]);
+        unpack8e<HF>(pack8e<HF>(v[c]), v[c]);                        // the GEMV output is bf16
+        if constexpr (!HAS_RES) *reinterpret_cast<uint4*>(res_out + row * H + e) = pack8e<HF>(v[c]);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
       }
     }
   } else {
-    load_row<NCH>(x + row * H, H, v);
+    load_row<NCH, HF>(x + row * H, H, v);
   }
   if constexpr (HAS_RES) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if ((c * NT + (int)threadIdx.x) * 8 >= H) continue;    // clamped load: not this row's data
       float r[8];
-      unpack8(rv[c], r);
+      unpack8e<HF>(rv[c], r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] += r[j];
     }
@@ -152,9 +160,9 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     for (int c = 0; c < NCH; ++c) {
       const int e = (c * NT + threadIdx.x) * 8;
       if (e < H) {
-        uint4 u = pack8(v[c]);
+        uint4 u = pack8e<HF>(v[c]);
         *reinterpret_cast<uint4*>(res_out + row * H + e) = u;
-        unpack8(u, v[c]);
+        unpack8e<HF>(u, v[c]);
       }
     }
   }
@@ -183,8 +191,8 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     const int e = (c * NT + threadIdx.x) * 8;
     if (e < H) {
       float wf[8], bfv[8];
-      unpack8(wv[c], wf);
-      if constexpr (!RMS) unpack8(bv[c], bfv);
+      unpack8e<HF>(wv[c], wf);
+      if constexpr (!RMS) unpack8e<HF>(bv[c], bfv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = (v[c][j] - mean) * rstd * wf[j];
@@ -194,16 +202,17 @@ __global__ void __launch_bounds__(NT) norm_kernel(
     }
   }
   if constexpr (QUANT) {
-    quant_store<NCH>(v, H, yq + row * H, ys + row, red);
+    if (pkt > 0) quant_store<NCH>(v, H, yq, ys + row, red, pkt, row);
+    else quant_store<NCH>(v, H, yq + row * H, ys + row, red);
   } else {
-    store_row<NCH>(y + row * H, H, v);
+    store_row<NCH, HF>(y + row * H, H, v);
   }
 }
 
 // ----------------------------------------------------------------------------- activations
 // MODE 0: silu(gate)*up with input [gate | up] of width 2F; 1: gelu tanh; 2: gelu erf;
 // 3: silu GLU over the 16-blocked [gate(16) | up(16)] layout (F % 16 == 0)
-template <int NCH, int MODE, bool QUANT>
+template <int NCH, int MODE, bool QUANT, bool HF = false>
 __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                  int8_t* __restrict__ yq, float* __restrict__ ys, int F) {
   __shared__ float red[NT / 64];
@@ -212,8 +221,8 @@ __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, b
   if constexpr (MODE == 0) {
     const bf16_t* xr = x + row * (size_t)(2 * F);
     float u[NCH][8];
-    load_row<NCH>(xr, F, v);
-    load_row<NCH>(xr + F, F, u);
+    load_row<NCH, HF>(xr, F, v);
+    load_row<NCH, HF>(xr + F, F, u);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -231,8 +240,8 @@ __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, b
       if (e < F) {
         const bf16_t* g = xr + (e >> 4) * 32 + (e & 15);
         float u[8];
-        unpack8(*reinterpret_cast<const uint4*>(g), v[c]);
-        unpack8(*reinterpret_cast<const uint4*>(g + 16), u);
+        unpack8e<HF>(*reinterpret_cast<const uint4*>(g), v[c]);
+        unpack8e<HF>(*reinterpret_cast<const uint4*>(g + 16), u);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = v[c][j] / (1.f + __expf(-v[c][j])) * u[j];
       } else {
@@ -241,7 +250,7 @@ __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, b
       }
     }
   } else {
-    load_row<NCH>(x + row * (size_t)F, F, v);
+    load_row<NCH, HF>(x + row * (size_t)F, F, v);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -256,21 +265,21 @@ __global__ void __launch_bounds__(NT) act_kernel(const bf16_t* __restrict__ x, b
       }
   }
   if constexpr (QUANT) quant_store<NCH>(v, F, yq + row * (size_t)F, ys + row, red);
-  else store_row<NCH>(y + row * (size_t)F, F, v);
+  else store_row<NCH, HF>(y + row * (size_t)F, F, v);
 }
 
-template <int NCH>
+template <int NCH, bool HF = false>
 __global__ void __launch_bounds__(NT) quant_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
                                                    float* __restrict__ s, int H) {
   __shared__ float red[NT / 64];
   const size_t row = blockIdx.x;
   float v[NCH][8];
-  load_row<NCH>(x + row * (size_t)H, H, v);
+  load_row<NCH, HF>(x + row * (size_t)H, H, v);
   quant_store<NCH>(v, H, q + row * (size_t)H, s + row, red);
 }
 
 // ----------------------------------------------------------------------------- embedding
-template <bool F32>
+template <bool F32, bool HF = false>
 __global__ void __launch_bounds__(NT) embed_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
                                                    void* __restrict__ out, int H, int V) {
   const size_t row = blockIdx.x;
@@ -281,7 +290,7 @@ __global__ void __launch_bounds__(NT) embed_kernel(const int64_t* __restrict__ i
     float4* dst = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + row * H);
     for (int e = threadIdx.x; e < H / 8; e += NT) {
       float v[8];
-      unpack8(src[e], v);
+      unpack8e<HF>(src[e], v);
       dst[2 * e] = make_float4(v[0], v[1], v[2], v[3]);
       dst[2 * e + 1] = make_float4(v[4], v[5], v[6], v[7]);
     }
@@ -293,14 +302,14 @@ __global__ void __launch_bounds__(NT) embed_kernel(const int64_t* __restrict__ i
 
 // ----------------------------------------------------------------------------- confidence
 // out[row] = max_v softmax(l)[v] = 1 / sum_v exp(l_v - max)   (online, one pass)
-template <bool BF16>
+template <bool BF16, bool HF = false>
 __global__ void __launch_bounds__(NT) max_prob_kernel(const void* __restrict__ logits, float* __restrict__ out, int V) {
   __shared__ float red[NT / 64];
   const size_t row = blockIdx.x;
   float m = -INFINITY, s = 0.f;
   for (int i = threadIdx.x; i < V; i += NT) {
     float l;
-    if constexpr (BF16) l = bf2f(reinterpret_cast<const bf16_t*>(logits)[row * V + i]);
+    if constexpr (BF16) l = e2f<HF>(reinterpret_cast<const bf16_t*>(logits)[row * V + i]);   // 16-bit logits
     else l = reinterpret_cast<const float*>(logits)[row * V + i];
     if (l > m) { s = s * __expf(m - l) + 1.f; m = l; }
     else s += __expf(l - m);
@@ -326,8 +335,12 @@ __global__ void __launch_bounds__(NT) max_prob_kernel(const void* __restrict__ l
 
 extern "C" int edge_norm(const void* x, const void* res, const void* w, const void* b, void* y, void* yq,
                          float* ys, void* res_out, int rows, int H, float eps, int rms, int quant,
-                         const float* xpart, int S, hipStream_t st) {
-  if (H % 8) return -2;
+                         const float* xpart, int S, int h16, hipStream_t st) {
+  // quant 2: int8 output fragment-packed for the 256-row decode GEMM (H % 64 == 0, <= 256 rows)
+  if (H % 8 || (quant == 2 && (H % 64 != 0 || rows > 256))) return -2;
+  // h16: fp16 rows (the fp16 agents' bf16-free path): plain norms only, no int8 output / partials
+  if (h16 && (quant || xpart != nullptr)) return -2;
+  const int pkt = quant == 2 ? H / 64 : 0;
   if (xpart != nullptr && (!rms || res_out == nullptr || S < 1)) return -2;
   if (rows == 0) return 0;
   const bf16_t *X = (const bf16_t*)x, *R = (const bf16_t*)res, *W = (const bf16_t*)w, *Bb = (const bf16_t*)b;
@@ -335,13 +348,19 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
   int8_t* Q = (int8_t*)yq;
 #define LAUNCH_NORM(RMS, HR, QU) \
   hipLaunchKernelGGL((norm_kernel<NCH, RMS, HR, QU, false>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, \
-                     eps, nullptr, 0)
+                     eps, nullptr, 0, pkt)
 #define LAUNCH_NORMP(HR, QU) \
   hipLaunchKernelGGL((norm_kernel<NCH, true, HR, QU, true>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, RO, H, \
-                     eps, xpart, S)
+                     eps, xpart, S, pkt)
   if (xpart != nullptr && (S < 1 || S > 8 || H % 8 != 0)) return -2;   // partial slices: 1..8
+#define LAUNCH_NORMH(RMS, HR) \
+  hipLaunchKernelGGL((norm_kernel<NCH, RMS, HR, false, false, true>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, \
+                     RO, H, eps, nullptr, 0, 0)
   NCH_DISPATCH(H, {
-    if (xpart != nullptr) {
+    if (h16) {
+      if (rms) { if (res) LAUNCH_NORMH(true, true); else LAUNCH_NORMH(true, false); }
+      else { if (res) LAUNCH_NORMH(false, true); else LAUNCH_NORMH(false, false); }
+    } else if (xpart != nullptr) {
       if (res) { if (quant) LAUNCH_NORMP(true, true); else LAUNCH_NORMP(true, false); }
       else { if (quant) LAUNCH_NORMP(false, true); else LAUNCH_NORMP(false, false); }
     } else if (rms) {
@@ -354,30 +373,37 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
   });
 #undef LAUNCH_NORM
 #undef LAUNCH_NORMP
+#undef LAUNCH_NORMH
   return (int)hipGetLastError();
 }
 
 extern "C" int edge_act(const void* x, void* y, void* yq, float* ys, int rows, int F, int mode, int quant,
-                        hipStream_t st) {
-  if (F % 8) return -2;
+                        int h16, hipStream_t st) {
+  if (F % 8 || (h16 && quant)) return -2;
   if (rows == 0) return 0;
   const bf16_t* X = (const bf16_t*)x;
   bf16_t* Y = (bf16_t*)y;
   int8_t* Q = (int8_t*)yq;
 #define LAUNCH_ACT(M, QU) hipLaunchKernelGGL((act_kernel<NCH, M, QU>), dim3(rows), dim3(NT), 0, st, X, Y, Q, ys, F)
+#define LAUNCH_ACTH(M) hipLaunchKernelGGL((act_kernel<NCH, M, false, true>), dim3(rows), dim3(NT), 0, st, X, Y, Q, ys, F)
   NCH_DISPATCH(F, {
-    if (mode == 0) { if (quant) LAUNCH_ACT(0, true); else LAUNCH_ACT(0, false); }
+    if (h16) {
+      if (mode == 0) LAUNCH_ACTH(0); else if (mode == 1) LAUNCH_ACTH(1); else if (mode == 3) LAUNCH_ACTH(3);
+      else LAUNCH_ACTH(2);
+    } else if (mode == 0) { if (quant) LAUNCH_ACT(0, true); else LAUNCH_ACT(0, false); }
     else if (mode == 1) { if (quant) LAUNCH_ACT(1, true); else LAUNCH_ACT(1, false); }
     else if (mode == 3) { if (quant) LAUNCH_ACT(3, true); else LAUNCH_ACT(3, false); }
     else { if (quant) LAUNCH_ACT(2, true); else LAUNCH_ACT(2, false); }
   });
 #undef LAUNCH_ACT
+#undef LAUNCH_ACTH
   return (int)hipGetLastError();
 }
 
 // Per-(row, 64-column) int8 quantisation (decode GEMV input layout: scales [K/64][Mpad]).  One
 // wave covers 512 columns of a row, 8 per lane; a group's 8 lanes reduce its absmax with three
 // xor-shuffles.  Used between the fused SwiGLU GEMV and the down projection.
+template <bool HF = false>
 __global__ void __launch_bounds__(NT) group_quant_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
                                                          float* __restrict__ s, int M, int K, int Mpad) {
   const int gw = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
@@ -388,7 +414,7 @@ __global__ void __launch_bounds__(NT) group_quant_kernel(const bf16_t* __restric
   const int e = wr * 512 + lane * 8;
   const bool ok = e < K;                       // K % 64 == 0: a group's 8 lanes agree
   float v[8];
-  if (ok) unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * K + e), v);
+  if (ok) unpack8e<HF>(*reinterpret_cast<const uint4*>(x + (size_t)row * K + e), v);
   else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = 0.f;
@@ -414,7 +440,7 @@ extern "C" int edge_group_quant(const void* x, void* q, float* s, int M, int K, 
   if (K % 64 || Mpad < M) return -2;
   if (M == 0) return 0;
   const int waves = M * ((K + 511) / 512);
-  hipLaunchKernelGGL(group_quant_kernel, dim3((waves + 3) / 4), dim3(NT), 0, st, (const bf16_t*)x, (int8_t*)q, s, M, K,
+  hipLaunchKernelGGL(group_quant_kernel<false>, dim3((waves + 3) / 4), dim3(NT), 0, st, (const bf16_t*)x, (int8_t*)q, s, M, K,
                      Mpad);
   return (int)hipGetLastError();
 }
@@ -429,17 +455,20 @@ extern "C" int edge_quant(const void* x, void* q, float* s, int rows, int H, hip
 }
 
 extern "C" int edge_embedding(const int64_t* ids, const void* table, void* out, int rows, int H, int V, int out_f32,
-                              hipStream_t st) {
+                              int h16, hipStream_t st) {
   if (H % 8) return -2;
   if (rows == 0) return 0;
-  if (out_f32) hipLaunchKernelGGL(embed_kernel<true>, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, out, H, V);
+  if (out_f32 && h16) hipLaunchKernelGGL((embed_kernel<true, true>), dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, out, H, V);
+  else if (out_f32) hipLaunchKernelGGL(embed_kernel<true>, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, out, H, V);
   else hipLaunchKernelGGL(embed_kernel<false>, dim3(rows), dim3(NT), 0, st, ids, (const bf16_t*)table, out, H, V);
   return (int)hipGetLastError();
 }
 
-extern "C" int edge_max_prob(const void* logits, float* out, int rows, int V, int is_bf16, hipStream_t st) {
+// dt: 0 fp32 logits, 1 bf16, 2 fp16
+extern "C" int edge_max_prob(const void* logits, float* out, int rows, int V, int dt, hipStream_t st) {
   if (rows == 0) return 0;
-  if (is_bf16) hipLaunchKernelGGL((max_prob_kernel<true>), dim3(rows), dim3(NT), 0, st, logits, out, V);
+  if (dt == 2) hipLaunchKernelGGL((max_prob_kernel<true, true>), dim3(rows), dim3(NT), 0, st, logits, out, V);
+  else if (dt == 1) hipLaunchKernelGGL((max_prob_kernel<true>), dim3(rows), dim3(NT), 0, st, logits, out, V);
   else hipLaunchKernelGGL((max_prob_kernel<false>), dim3(rows), dim3(NT), 0, st, logits, out, V);
   return (int)hipGetLastError();
 }

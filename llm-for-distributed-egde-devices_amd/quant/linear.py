@@ -113,9 +113,22 @@ class W8A8Linear(nn.Module):
             self._w_cpu = self.int8_weight()
         return self._w_cpu
 
+    def takes_packed(self, M: int) -> bool:
+        """Whether this projection takes a fragment-packed activation at M rows (the 256-row decode
+        GEMM on the GPU: ops.r256_ok; not split-K outputs, not the GLU projection)."""
+        return (self.w_packed.is_cuda and not self.split_k_out and not self.glu_blocked and
+                ops.r256_ok(M, self.out_features, self.in_features))
+
     def forward(self, x, add=None):
         """``add``: the other branch of a parallel-residual block, added to the output (in the
         decode GEMV's epilogue at <= 64 rows)."""
+        if isinstance(x, QAct) and x.packed:
+            K, N = self.in_features, self.out_features
+            M = x.q.shape[0]
+            y = ops.w8a8_r256(x.q, x.scale, self.w_packed, self.w_scale, self.bias, N, K) if add is None else None
+            if y is not None:
+                return y
+            x = QAct(ops.unpack_a(x.q, M, K), x.scale)      # (a consumer that cannot take it)
         if isinstance(x, PendingNorm):                # batch 1: the norm runs in this GEMV's prologue
             y = None
             if add is None and not self.split_k_out:

@@ -114,3 +114,80 @@ def test_rows256_model_routes(cuda):
     output, split-K o / down partials, quantising GLU (decode_rows_ok routes 129-256 rows)."""
     assert ops.decode_rows_ok(256, 4096) and ops.decode_rows_ok(256, 11008, 4)
     assert not ops.decode_rows_ok(257, 4096)
+
+
+def _r256(C, on):
+    class _Ctx:
+        def __enter__(self):
+            C.tune("r256_packed", on, 0)
+
+        def __exit__(self, *a):
+            C.tune("r256_packed", 1, 0)
+            return False
+    return _Ctx()
+
+
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("H", [4096, 2048])
+@pytest.mark.parametrize("parts", [0, 2])
+def test_norm_packed_output_is_pack_of_rows(cuda, M, H, parts):
+    """The norm kernel's fragment-packed int8 output (quant = 2) is exactly pack_a of its row-major
+    output (same values and scales), and ops.unpack_a inverts it."""
+    C = ops.ext()
+    torch.manual_seed(M + H + parts)
+    w = (torch.rand(H, device=cuda) + 0.5).to(torch.bfloat16)
+    res = torch.randn(M, H, device=cuda).to(torch.bfloat16)
+    if parts:
+        xp = torch.randn(parts, M, H, device=cuda)
+        q0, s0, r0 = C.rms_norm_parts(xp, res, w, 1e-5, 1)
+        q1, s1, r1 = C.rms_norm_parts(xp, res, w, 1e-5, 2)
+    else:
+        x = torch.randn(M, H, device=cuda).to(torch.bfloat16)
+        q0, s0, r0 = C.norm(x, res, w, None, 1e-5, True, 1)
+        q1, s1, r1 = C.norm(x, res, w, None, 1e-5, True, 2)
+    assert torch.equal(s0, s1) and torch.equal(r0, r1)
+    assert q1.shape == (M, H) and q1.stride(0) == H
+    assert torch.equal(ops.unpack_a(q1, M, H), q0)
+
+
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("N,K", [(12288, 4096), (6144, 4096), (4096, 4096), (6144, 2048), (2048, 2048)])
+def test_r256_packed_equals_ring2(cuda, M, N, K):
+    """The packed-activation 256-row kernel (w8a8_r256_kernel: activations global -> VGPR, only
+    the weight panel through LDS) is bit-identical to the row-major ring2 kernel, and within the
+    fp32 reference's tolerance."""
+    C = ops.ext()
+    assert ops.r256_ok(M, N, K)
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w_n = (torch.rand(K, device=cuda) + 0.5).to(torch.bfloat16)
+    qx, sx, _ = C.norm(x, None, w_n, None, 1e-5, True, 1)
+    qp, sp, _ = C.norm(x, None, w_n, None, 1e-5, True, 2)
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    ring = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+    out = ops.w8a8_r256(qp, sp, wp, sw, bias, N, K)
+    assert out is not None and torch.equal(out, ring)
+    _close(out, _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32), 1e-2, 1e-2)
+
+
+def test_r256_model_logits_unchanged(cuda):
+    """A W8A8 Llama decoder at 256 decode rows: the packed qkv path (norm1 writes packed rows, qkv
+    runs w8a8_r256) gives bit-identical logits to the row-major ring2 path."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.quant import quantize_model
+    C = ops.ext()
+    cfg = tiny("llama2", num_layers=2, hidden_size=2048, intermediate_size=5504, num_heads=16, num_kv_heads=16,
+               head_dim=128, vocab_size=1024)
+    model = quantize_model(build_model(cfg, device=cuda, seed=3), "w8a8_smoothquant")
+    prompts = torch.randint(0, cfg.vocab_size, (256, 9), generator=torch.Generator().manual_seed(1)).tolist()
+    sp = SamplingParams(max_new_tokens=6, do_sample=False, repetition_penalty=1.1)
+    outs = []
+    for on in (1, 0):
+        with _r256(C, on):
+            gen = Generator(model, max_batch=256, max_seq=32, use_graphs=False)
+            outs.append(gen.generate(prompts, sp).tokens)
+    assert outs[0] == outs[1]
