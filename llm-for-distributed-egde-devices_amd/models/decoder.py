@@ -339,7 +339,7 @@ class DecoderLM(nn.Module):
         if decode and ops.gpu_path(self.embed) and self._first_norm_deferred(B * T):
             xf = ops.embedding(ids.reshape(-1), self.embed, out_f32=True)
             if ops.gemv_norm_ok(xf.view(1, B * T, -1)):
-                return PartialSum(xf.view(1, B * T, -1))
+                return PartialSum(xf.view(1, B * T, -1), self.embed.dtype)
         x = ops.embedding(ids.reshape(-1), self.embed)
         if self.pos_embed is not None:
             pos = (start_pos.long()[:, None] + torch.arange(T, device=ids.device)[None]).reshape(-1)

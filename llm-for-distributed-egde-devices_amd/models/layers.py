@@ -29,16 +29,17 @@ class QAct(NamedTuple):
 
 
 class PartialSum(NamedTuple):
-    """Split-K output of a W8A8 decode projection: fp32 slices [S, M, N] whose in-order sum,
-    rounded to bf16, is the projection's output.  RMSNorm consumes it directly (one kernel
-    adds the slices); anything else calls ``materialize()``."""
+    """Split-K output of a decode projection: fp32 slices [S, M, N] whose in-order sum, rounded
+    to ``dtype`` (the model's 16-bit type), is the projection's output.  RMSNorm consumes it
+    directly (one kernel adds the slices); anything else calls ``materialize()``."""
     parts: torch.Tensor
+    dtype: torch.dtype = torch.bfloat16
 
     def materialize(self) -> torch.Tensor:
         acc = self.parts[0].clone()
         for s in range(1, self.parts.shape[0]):      # same order as the norm kernel
             acc += self.parts[s]
-        return acc.to(torch.bfloat16)
+        return acc.to(self.dtype)
 
 
 class PendingNorm(NamedTuple):
@@ -92,7 +93,7 @@ class Linear(nn.Module):
                                                                self.out_features, 3, S))
             elif K // 64 >= self.split_k_out:
                 return PartialSum(ops.ext().gemv_bf16_splitk(x.reshape(-1, K), wp, self.bias,
-                                                             self.out_features, self.split_k_out))
+                                                             self.out_features, self.split_k_out), x.dtype)
         return ops.linear_bf16(x, self.weight, self.bias, packed=wp,
                                add=None if add is None else add.reshape(*x.shape[:-1], self.out_features))
 
@@ -108,7 +109,7 @@ class Linear(nn.Module):
         return wp
 
     def extra_repr(self):
-        return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, bf16"
+        return f"{self.in_features}->{self.out_features}, bias={self.bias is not None}, {str(self.weight.dtype)[6:]}"
 
 
 class Norm(nn.Module):

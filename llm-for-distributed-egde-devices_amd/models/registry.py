@@ -39,14 +39,23 @@ def preset_for(name: str) -> Optional[str]:
     return None
 
 
-def precision_dtype(precision: str, device) -> torch.dtype:
-    """The HIP kernels run bf16; the reference's fp16 agents (combine_model_fp_updated.py:32-34)
-    therefore execute in bf16 on the GPU (same bytes, wider range).  CPU keeps the request."""
+def precision_dtype(precision: str, device, quant: str = "none") -> torch.dtype:
+    """torch dtype of a model's 16-bit tensors for the reference's ``precision`` flag
+    (combine_model_fp_updated.py:32-34: fp16 unless "bf16"; phi2-pythia_fp_updated.py:32).  The
+    GPU runs fp16 and bf16 models on their own kernel instantiations (fp16 MFMA GEMV / attention,
+    fp16 norms and RoPE).  Quantised models (``quant`` != none) keep bf16 activations on the GPU:
+    the INT8 GEMM epilogues write bf16."""
     p = (precision or "bf16").lower()
     dev = torch.device(device) if device is not None else torch.device("cpu")
+    want = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}.get(p, torch.bfloat16)
     if dev.type == "cuda":
-        return torch.bfloat16
-    return {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}.get(p, torch.bfloat16)
+        if quant not in (None, "none") and want != torch.bfloat16:
+            log.info(f"precision {p} with --quant {quant}: the INT8 kernels run bf16 activations")
+            return torch.bfloat16
+        if want == torch.float32:
+            log.info("precision fp32 on the GPU: the HIP kernels run 16-bit; using bf16")
+            return torch.bfloat16
+    return want
 
 
 def quantized_checkpoint_dir(name_or_path: str, base_dir: Optional[str] = None) -> Optional[str]:
@@ -68,7 +77,7 @@ def load_model(name_or_path: str, precision: str = "bf16", quant: str = "none", 
     """Returns (model, tokenizer, source) with source "checkpoint:<dir>", "int8-checkpoint:<dir>"
     (an edgellm quantised checkpoint: its stage is read directly, already quantised — ``quant``
     is then the checkpoint's own mode) or "random-init:<preset>".  ``units``: a half-layer stage."""
-    dtype = precision_dtype(precision, device)
+    dtype = precision_dtype(precision, device, quant)
     qdir = quantized_checkpoint_dir(name_or_path, base_dir)
     if qdir is not None:
         from ..quant.checkpoint import load_quantized

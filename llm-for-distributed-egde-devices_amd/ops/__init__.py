@@ -347,19 +347,21 @@ BF16_RING_MAX_ROWS = 256
 
 
 def bf16_decode_mode(x: torch.Tensor, weight: torch.Tensor, glu: bool = False, split: bool = False) -> int:
-    """Which HIP decode kernel ``linear_bf16`` runs for this call: 1 = ``gemv_bf16.hip`` (<=
+    """Which HIP decode kernel ``linear_bf16`` runs for this call (bf16, or fp16 for the GEMV): 1 = ``gemv_bf16.hip`` (<=
     ``BF16_GEMV_MAX_ROWS`` rows), 2 = the bf16 ring GEMM (up to 256 rows, from the extension's
     ``bf16_ring_min_rows`` (65), or from 17 rows for the fused SwiGLU, split-K outputs and
     LM-head-wide N >= 16384), 0 = none (hipBLASLt; measured ahead of the ring on qkv at 17-64
     rows).  GPU, bf16, K % 64 == 0, N % 16 == 0 (% 32 for
     the fused GLU)."""
     K = x.shape[-1]
-    if not (_gpu(x) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.is_contiguous()
-            and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0):
+    if not (_gpu(x) and x.dtype in (torch.bfloat16, torch.float16) and weight.dtype == x.dtype
+            and x.is_contiguous() and K % 64 == 0 and weight.shape[0] % (32 if glu else 16) == 0):
         return 0
     M = x.numel() // max(K, 1)
     if 0 < M <= BF16_GEMV_MAX_ROWS:
         return 1
+    if x.dtype != torch.bfloat16:          # fp16: the GEMV only (the ring GEMM is bf16)
+        return 0
     lo = ext().bf16_ring_min_rows()
     if glu or split or weight.shape[0] >= 16384:
         # SwiGLU, split-K (o / down) and LM-head-wide N: the ring is ahead from 17 rows
@@ -376,7 +378,7 @@ def bf16_gemv_ok(x: torch.Tensor, weight: torch.Tensor, glu: bool = False) -> bo
 
 
 def pack_bf16_weight(w: torch.Tensor) -> torch.Tensor:
-    """[N, K] bf16 -> MFMA-fragment order for ``gemv_bf16.hip``: 1 KiB tiles of 16 rows x 32 k,
+    """[N, K] bf16 (or fp16) -> MFMA-fragment order for ``gemv_bf16.hip``: 1 KiB tiles of 16 rows x 32 k,
     lane l holding W[16 nt + (l & 15)][32 kt + 8 (l >> 4) .. +8] (N % 16 == 0, K % 32 == 0)."""
     N, K = w.shape
     return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(-1)
@@ -387,7 +389,7 @@ _GEMV_EPI = {None: 0, "silu_glu": 1, "gelu_tanh": 2, "gelu": 3}
 
 def linear_bf16(x, weight, bias=None, glu: bool = False, act: Optional[str] = None,
                 packed: Optional[torch.Tensor] = None, add: Optional[torch.Tensor] = None):
-    """bf16 projection.  Decode-sized inputs on GPU take ``gemv_bf16.hip`` on the fragment-packed
+    """16-bit projection (bf16, or fp16 for the fp16 agents: the GEMV's fp16 MFMA instantiation).  Decode-sized inputs on GPU take ``gemv_bf16.hip`` on the fragment-packed
     weight (``packed``: the layer's cached ``pack_bf16_weight(weight)``; packed per call when
     absent); ``glu``: weight = [gate | up] and the result is silu(gate) * up; ``act``
     "gelu_tanh" / "gelu": the activation of the bf16 output in the same kernel.  Everything else
@@ -470,11 +472,18 @@ def quant_per_group(x):
 # --------------------------------------------------------------------------- sampling / misc
 
 
+def _logits32(logits):
+    """The sampler reads bf16 or fp32 logits; fp16 logits (fp16 agents) are widened to fp32 first,
+    as HF's generate does before its logits processors."""
+    return logits.float() if logits.dtype == torch.float16 else logits
+
+
 def sample(logits, seen, temperature, top_k, top_p, repetition_penalty, rng: torch.Tensor,
            do_sample: bool = True):
     """Fused sampler. ``rng`` = int32 tensor [seed, step] on the logits' device (the step is
     read on device so the launch is graph-capturable)."""
     if _gpu(logits):
+        logits = _logits32(logits)
         out = ext().sample(logits, seen, float(temperature), int(top_k or 0), float(top_p if top_p is not None else 1.0),
                            float(repetition_penalty), bool(do_sample), rng)
         if out.numel() > 0 or logits.shape[0] == 0:
@@ -516,6 +525,7 @@ def sample_advance(logits, seen, temperature, top_k, top_p, repetition_penalty, 
     sampler's last launch (one kernel boundary fewer per decode step).  ``ctr``: int32 [1] zero
     buffer the kernel uses as an arrival counter (it stays zero between calls).  Returns nxt."""
     if _gpu(logits) and FUSE_ADVANCE:
+        logits = _logits32(logits)
         nxt = ext().sample_advance(logits, seen, float(temperature), int(top_k or 0),
                                    float(top_p if top_p is not None else 1.0), float(repetition_penalty),
                                    bool(do_sample), rng, tok, out, step, pos, seq_lens, ctr)

@@ -39,6 +39,7 @@ struct Fuse {
 };
 
 // Rotate the 8 values at head offset e0 (HF rotate_half convention), x/partner read from `head`.
+template <bool HF>
 __device__ __forceinline__ void rope8(const bf16_t* __restrict__ head, int e0, int rot, const float2* csp,
                                       float (&v)[8]) {
   const int half = rot / 2;
@@ -46,7 +47,7 @@ __device__ __forceinline__ void rope8(const bf16_t* __restrict__ head, int e0, i
   const int pe = lo ? e0 + half : e0 - half;
   const int fi = lo ? e0 : e0 - half;
   float p[8];
-  unpack8(*reinterpret_cast<const uint4*>(head + pe), p);
+  unpack8e<HF>(*reinterpret_cast<const uint4*>(head + pe), p);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float2 r = csp[fi + j];
@@ -66,7 +67,8 @@ template <int D> struct Lanes { static constexpr int v = (D / 8 <= 8) ? 8 : ((D 
 // OCC > 0: single-buffered key loop, nontemporal K/V loads and at least OCC waves per SIMD
 // (occupancy instead of a second register buffer), and FUSED keeps the new key in registers (no
 // append barrier); OCC = 0: two register buffers, no occupancy target.  NWV: waves per workgroup.
-template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC, int NWV = NW>
+// HF: q / K / V / out are IEEE fp16 instead of bf16 (the reference's fp16 agents); fp32 softmax.
+template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC, bool HF, int NWV = NW>
 __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     int64_t c_sb, int64_t c_sh, const int* __restrict__ seq_lens, float scale_log2, int CH, int nsplit,
@@ -145,12 +147,12 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   for (int h = 0; h < G; ++h) {
     if (dvalid) {
       const bf16_t* qh = q + b * q_sb + (size_t)(qh0 + h) * D;
-      unpack8(*reinterpret_cast<const uint4*>(qh + d0), qf[h]);
+      unpack8e<HF>(*reinterpret_cast<const uint4*>(qh + d0), qf[h]);
       if constexpr (FUSED) {
         if (d0 < fz.rot) {
-          rope8(qh, d0, fz.rot, reinterpret_cast<const float2*>(fz.cs) + (size_t)fz.pos[b] * (fz.rot / 2), qf[h]);
+          rope8<HF>(qh, d0, fz.rot, reinterpret_cast<const float2*>(fz.cs) + (size_t)fz.pos[b] * (fz.rot / 2), qf[h]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qf[h][j] = bf2f(f2bf(qf[h][j]));   // q is bf16 in the unfused path
+          for (int j = 0; j < 8; ++j) qf[h][j] = e2f<HF>(f2e<HF>(qf[h][j]));   // q is 16-bit in the unfused path
         }
       }
 #pragma unroll
@@ -180,13 +182,13 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
         const bool is_v = kl == 1;
         const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + kvh) * D;
         float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(head + d0), v);
-        if (!is_v && d0 < fz.rot) rope8(head, d0, fz.rot, csp, v);
+        unpack8e<HF>(*reinterpret_cast<const uint4*>(head + d0), v);
+        if (!is_v && d0 < fz.rot) rope8<HF>(head, d0, fz.rot, csp, v);
         if (blockIdx.y % fz.gs == 0)
-          *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + d0) = pack8(v);
+          *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + d0) = pack8e<HF>(v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {                // the cached bf16 value
-          const float r = bf2f(f2bf(v[j]));
+        for (int j = 0; j < 8; ++j) {                // the cached 16-bit value
+          const float r = e2f<HF>(f2e<HF>(v[j]));
           knew[j] = is_v ? 0.f : r;
           vnew[j] = is_v ? r : 0.f;
         }
@@ -198,9 +200,9 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
           const int e0 = (is_v ? c - D / 8 : c) * 8;
           const bf16_t* head = row + (size_t)((is_v ? Hq + Hkv : Hq) + kvh) * D;
           float v[8];
-          unpack8(*reinterpret_cast<const uint4*>(head + e0), v);
-          if (!is_v && e0 < fz.rot) rope8(head, e0, fz.rot, csp, v);
-          *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + e0) = pack8(v);
+          unpack8e<HF>(*reinterpret_cast<const uint4*>(head + e0), v);
+          if (!is_v && e0 < fz.rot) rope8<HF>(head, e0, fz.rot, csp, v);
+          *reinterpret_cast<uint4*>((is_v ? vc : kc) + b * c_sb + kvh * c_sh + (size_t)pos * D + e0) = pack8e<HF>(v);
         }
       }
       // Only this workgroup reads the new row, so the barrier's workgroup-scope release/acquire is
@@ -229,7 +231,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       float kf[8];
-      unpack8(kr[u], kf);
+      unpack8e<HF>(kr[u], kf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         float a = 0.f;
@@ -268,7 +270,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       float vf[8];
-      unpack8(vr[u], vf);
+      unpack8e<HF>(vr[u], vf);
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         const float p = __builtin_amdgcn_exp2f(s[u][h] - m[h]);    // masked keys: exp2(-inf) = 0
@@ -362,12 +364,12 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     const int hq = qh0 + h;
     if (DIRECT) {
       if constexpr (QOUT) {     // D % 64 == 0: each 64-column group is one wave of this loop
-        const float vq = bf2f(f2bf(a / lstat[h]));
+        const float vq = e2f<HF>(f2e<HF>(a / lstat[h]));
         const int col = hq * D + d;
         quant_group_store(vq, fz.out_q + (size_t)b * Hq * D + col, fz.out_s + (size_t)(col >> 6) * fz.Mpad + b,
                           threadIdx.x & 63);
       } else {
-        out[b * o_sb + (size_t)hq * D + d] = f2bf(a / lstat[h]);
+        out[b * o_sb + (size_t)hq * D + d] = f2e<HF>(a / lstat[h]);
       }
     } else {
       part_acc[(((size_t)b * Hq + hq) * nsplit + split) * D + d] = a;
@@ -380,7 +382,7 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
   }
 }
 
-template <bool QOUT>
+template <bool QOUT, bool HF>
 __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __restrict__ part_acc,
                                                              const float* __restrict__ part_ml, int nsplit, int D,
                                                              bf16_t* __restrict__ out, int64_t o_sb, Fuse fz) {
@@ -399,10 +401,10 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(const float* __rest
       if (ml[2 * s] != -INFINITY) a += exp2f(ml[2 * s] - M) * pa[(size_t)s * D + d];
     if constexpr (QOUT) {
       const int col = hq * D + d;
-      quant_group_store(bf2f(f2bf(a * invL)), fz.out_q + (size_t)b * Hq * D + col,
+      quant_group_store(e2f<HF>(f2e<HF>(a * invL)), fz.out_q + (size_t)b * Hq * D + col,
                         fz.out_s + (size_t)(col >> 6) * fz.Mpad + b, threadIdx.x & 63);
     } else {
-      out[b * o_sb + (size_t)hq * D + d] = f2bf(a * invL);
+      out[b * o_sb + (size_t)hq * D + d] = f2e<HF>(a * invL);
     }
   }
 }
@@ -428,7 +430,7 @@ extern "C" void edge_decode_attn_config(int target_wg) { g_target_wg = target_wg
 extern "C" void edge_decode_attn_occ(int occ) { g_attn_occ = occ == 0 || occ == 5 ? occ : 4; }
 
 namespace {
-template <int D, int G, bool DI, bool FU, bool QO>
+template <int D, int G, bool DI, bool FU, bool QO, bool HF>
 void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q_sb, void* k_cache, void* v_cache,
                  int64_t c_sb, int64_t c_sh, const int* seq_lens, float sl2, int ch, int nsplit, void* out,
                  int64_t o_sb, float* part_acc, float* part_ml, const Fuse& fz, bool small_grid) {
@@ -440,10 +442,10 @@ void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q
     constexpr int OCC4 = G <= 2 ? 4 : (G == 4 ? 2 : 1), OCC5 = G <= 2 ? 5 : OCC4;
     // (8- and 16-wave workgroups for batch-1 grids measured slower: Llama-3.2-1B decode step
     // 1.08 -> 1.19 ms with 8 waves)
-    if (g_attn_occ == 4 && !small_grid) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4>), ATTN_ARGS); return; }
-    if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC5>), ATTN_ARGS); return; }
+    if (g_attn_occ == 4 && !small_grid) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4, HF>), ATTN_ARGS); return; }
+    if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC5, HF>), ATTN_ARGS); return; }
   }
-  hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 0>), ATTN_ARGS);
+  hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, 0, HF>), ATTN_ARGS);
 #undef ATTN_ARGS
 }
 }  // namespace
@@ -468,21 +470,14 @@ extern "C" int edge_decode_attn_plan(int B, int Hkv, int max_len, int D, int* ch
   return 0;
 }
 
-// q: [B, *] rows with the Hq query heads at offset 0 (q_sb elements apart).  FUSED (pos != null):
-// q points at the QKV projection output, rows hold [q heads | k heads | v heads], the new token's
-// k/v are appended to the caches at pos[b] and q is rotated in-kernel.  QOUT (out_q != null,
-// D % 64 == 0): int8 output + [Hq*D/64][Mpad] scales instead of bf16 `out`.
-extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb,
-                                int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale,
-                                int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
-                                const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
-                                hipStream_t st) {
-  if (B == 0) return 0;
+namespace {
+template <bool HF>
+int run_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb, int64_t c_sh,
+             const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch, int nsplit, void* out,
+             int64_t o_sb, float* part_acc, float* part_ml, const int* pos, const float* cs, int rot, void* out_q,
+             float* out_s, int Mpad, hipStream_t st) {
   const int G0 = Hq / Hkv;
-  if (G0 * Hkv != Hq) return -2;
   const bool fused = pos != nullptr, qout = out_q != nullptr;
-  if (qout && (D % 64 != 0 || Mpad < B)) return -2;
-  if (fused && rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
   // grids of a few dozen workgroups (batch 1-4 on a GQA model: 8 KV heads) are bound by each
   // workgroup's serial chain over its keys x G query heads: give every query head its own
   // workgroup instead (K/V rows re-read G times, from L2).  Needs the barrier-free fused form
@@ -496,14 +491,17 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
   const dim3 grid(nsplit, Hkv * gs, B);
   const bool direct = nsplit == 1;
   const bool small_grid = G0 == 1 && direct && fused && B * Hkv < g_attn_small_wg;
+  // fp16 rows (HF) have no int8-output form: the fp16 agents' o-projection is fp16
 #define DK(DD, GG, DI, FU, QO)                                                                                     \
-  launch_attn<DD, GG, DI, FU, QO>(grid, lds, st, q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, out, \
-                                  o_sb, part_acc, part_ml, fz, small_grid)
+  launch_attn<DD, GG, DI, FU, QO, HF>(grid, lds, st, q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, sl2, ch, nsplit, \
+                                      out, o_sb, part_acc, part_ml, fz, small_grid)
 #define DLAUNCH(DD, GG)                                                     \
   do {                                                                      \
     if (direct) {                                                           \
-      if (fused) { if (qout) DK(DD, GG, true, true, true); else DK(DD, GG, true, true, false); } \
-      else { if (qout) DK(DD, GG, true, false, true); else DK(DD, GG, true, false, false); }     \
+      if constexpr (!HF) {                                                  \
+        if (qout) { if (fused) DK(DD, GG, true, true, true); else DK(DD, GG, true, false, true); break; } \
+      }                                                                     \
+      if (fused) DK(DD, GG, true, true, false); else DK(DD, GG, true, false, false);             \
     } else {                                                                \
       if (fused) DK(DD, GG, false, true, false); else DK(DD, GG, false, false, false);           \
     }                                                                       \
@@ -528,10 +526,38 @@ extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void
 #undef DK
   if (!direct) {
     const dim3 cg(Hq, B), cb(D <= 128 ? 128 : 256);
-    if (qout) hipLaunchKernelGGL(decode_combine_kernel<true>, cg, cb, 0, st, part_acc, part_ml, nsplit, D, (bf16_t*)out,
-                                 o_sb, fz);
-    else hipLaunchKernelGGL(decode_combine_kernel<false>, cg, cb, 0, st, part_acc, part_ml, nsplit, D, (bf16_t*)out,
-                            o_sb, fz);
+    if constexpr (!HF) {
+      if (qout) {
+        hipLaunchKernelGGL((decode_combine_kernel<true, false>), cg, cb, 0, st, part_acc, part_ml, nsplit, D,
+                           (bf16_t*)out, o_sb, fz);
+        return (int)hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((decode_combine_kernel<false, HF>), cg, cb, 0, st, part_acc, part_ml, nsplit, D, (bf16_t*)out,
+                       o_sb, fz);
   }
   return (int)hipGetLastError();
+}
+}  // namespace
+
+// q: [B, *] rows with the Hq query heads at offset 0 (q_sb elements apart).  FUSED (pos != null):
+// q points at the QKV projection output, rows hold [q heads | k heads | v heads], the new token's
+// k/v are appended to the caches at pos[b] and q is rotated in-kernel.  QOUT (out_q != null,
+// D % 64 == 0, bf16 only): int8 output + [Hq*D/64][Mpad] scales instead of `out`.  h16: q, caches
+// and out are fp16.
+extern "C" int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb,
+                                int64_t c_sh, const int* seq_lens, int B, int Hq, int Hkv, int D, float scale,
+                                int ch, int nsplit, void* out, int64_t o_sb, float* part_acc, float* part_ml,
+                                const int* pos, const float* cs, int rot, void* out_q, float* out_s, int Mpad,
+                                int h16, hipStream_t st) {
+  if (B == 0) return 0;
+  const int G0 = Hq / Hkv;
+  if (G0 * Hkv != Hq) return -2;
+  const bool fused = pos != nullptr, qout = out_q != nullptr;
+  if (qout && (D % 64 != 0 || Mpad < B || h16)) return -2;
+  if (fused && rot > 0 && (cs == nullptr || rot % 16 != 0 || rot > D)) return -2;
+  return h16 ? run_attn<true>(q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, B, Hq, Hkv, D, scale, ch, nsplit, out,
+                              o_sb, part_acc, part_ml, pos, cs, rot, out_q, out_s, Mpad, st)
+             : run_attn<false>(q, q_sb, k_cache, v_cache, c_sb, c_sh, seq_lens, B, Hq, Hkv, D, scale, ch, nsplit, out,
+                               o_sb, part_acc, part_ml, pos, cs, rot, out_q, out_s, Mpad, st);
 }

@@ -1,4 +1,5 @@
-// Causal flash-attention forward for prefill / chunked prefill on bf16 MFMA.
+// Causal flash-attention forward for prefill / chunked prefill on bf16 MFMA (fp16
+// MFMA for the fp16 agents: template flag HF, same tiling — the f16 MFMAs run at the bf16 rate).
 //
 // q [B, T, Hq, D] for positions start_pos[b] + t; K/V from the head-major caches [B, Hkv, S, D]
 // (already written by rope_kv_write), keys [0, start_pos[b] + T).  GQA: kv head = h / (Hq/Hkv).
@@ -24,8 +25,13 @@ constexpr int KT = 64;   // keys per tile
 
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-__device__ __forceinline__ v4f mfma_bf16(const v8s& a, const v8s& b, const v4f& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+
+template <bool HF>
+__device__ __forceinline__ v4f mfma_16(const v8s& a, const v8s& b, const v4f& c) {
+  if constexpr (HF)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a), __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ void glds16_fa(const void* g, void* lds_base) {
@@ -50,7 +56,7 @@ struct Geo {
   static constexpr int NKK = DP / 32;                 // QK^T k-steps
 };
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool HF>
 __global__ void __launch_bounds__(NT) prefill_attn_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc, int64_t c_sb,
     int64_t c_sh, const int* __restrict__ start_pos, bf16_t* __restrict__ out, int T, int Hq, int Hkv,
@@ -148,7 +154,7 @@ __global__ void __launch_bounds__(NT) prefill_attn_kernel(
 #pragma unroll
       for (int kk = 0; kk < G::NKK; ++kk) {
         const v8s kf = *reinterpret_cast<const v8s*>(k_lds + (nt * 16 + c16) * G::KS + (kk * 32 + 8 * g4) * 2);
-        s[nt] = mfma_bf16(qf[kk], kf, s[nt]);
+        s[nt] = mfma_16<HF>(qf[kk], kf, s[nt]);
       }
     }
     // ---- online softmax; lane holds S[row = 4*g4 + i][key = nt*16 + c16]
@@ -188,12 +194,12 @@ __global__ void __launch_bounds__(NT) prefill_attn_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[dt][i] *= alpha[i];
 
-    // ---- P -> LDS (bf16), row-major [16][64] with padded rows
+    // ---- P -> LDS (16-bit), row-major [16][64] with padded rows
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<bf16_t*>(p_lds + (4 * g4 + i) * G::PS + (nt * 16 + c16) * 2) = f2bf(s[nt][i]);
+        *reinterpret_cast<bf16_t*>(p_lds + (4 * g4 + i) * G::PS + (nt * 16 + c16) * 2) = f2e<HF>(s[nt][i]);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's P writes landed
     __builtin_amdgcn_wave_barrier();
 
@@ -209,7 +215,7 @@ __global__ void __launch_bounds__(NT) prefill_attn_kernel(
         const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0));
         const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0 + 4 * G::VS));
         const v8s vf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dt] = mfma_bf16(pf, vf, o[dt]);
+        o[dt] = mfma_16<HF>(pf, vf, o[dt]);
       }
     }
   }
@@ -222,7 +228,7 @@ __global__ void __launch_bounds__(NT) prefill_attn_kernel(
       const float inv = l_i[i] > 0.f ? 1.f / l_i[i] : 0.f;
 #pragma unroll
       for (int dt = 0; dt < G::NDT; ++dt)
-        out[(((size_t)b * T + t) * Hq + h) * D + dt * 16 + c16] = f2bf(o[dt][i] * inv);
+        out[(((size_t)b * T + t) * Hq + h) * D + dt * 16 + c16] = f2e<HF>(o[dt][i] * inv);
     }
   }
 }
@@ -269,15 +275,18 @@ struct FaGeo {
   }
 };
 
-__device__ __forceinline__ v16f mfma32_bf16(const v8s& a, const v8s& b, const v16f& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+template <bool HF>
+__device__ __forceinline__ v16f mfma_32(const v8s& a, const v8s& b, const v16f& c) {
+  if constexpr (HF)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(v8h, a), __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 // STG (stagger): waves 4-7 (the partners of waves 0-3 on the same SIMDs) defer each tile's O^T += V^T
 // P^T to the next tile's interval, so on every SIMD one wave's softmax VALU runs beside the other's
 // MFMAs instead of both waves hitting the same phase after each barrier (MI355X microarch item 9).
 // The deferred V tile stays readable one barrier longer, so the ring grows to 4 slots.
-template <int D, bool CAUSAL, bool STG = false>
+template <int D, bool CAUSAL, bool STG, bool HF>
 __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc, int64_t c_sb,
     int64_t c_sh, const int* __restrict__ start_pos, bf16_t* __restrict__ out, int T, int Hq, int Hkv,
@@ -356,7 +365,7 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
           const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
           const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
           const v8s vf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[db] = mfma32_bf16(vf, pb[kb][ks], o[db]);
+          o[db] = mfma_32<HF>(vf, pb[kb][ks], o[db]);
         }
         // bound the V fragments the compiler keeps in flight to one 16-key step (register budget:
         // 2 waves / SIMD = 256 VGPRs, and a spill would join this kernel's counted vmcnt)
@@ -397,7 +406,7 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
 #pragma unroll
       for (int kk = 0; kk < G::KK; ++kk) {
         const v8s kf = *reinterpret_cast<const v8s*>(kl + kr * G::ROWB + (((2 * kk + hf) ^ G::swz(kr)) << 4));
-        sacc[kb] = mfma32_bf16(kf, qf[kk], sacc[kb]);
+        sacc[kb] = mfma_32<HF>(kf, qf[kk], sacc[kb]);
       }
       asm volatile("" ::: "memory");                           // K fragments: one 32-key block in flight
     }
@@ -433,7 +442,7 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
         for (int j = 0; j < 8; ++j) {
           const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][8 * ks + j], scale_log2, -msafe));
           rs += pv;
-          pb[kb][ks][j] = (short)f2bf(pv);
+          pb[kb][ks][j] = (short)f2e<HF>(pv);
         }
     rs += __shfl_xor(rs, 32, 64);
     l_i = l_i * alpha + rs;
@@ -466,8 +475,8 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         uint2 w;
-        w.x = pack_bf2(o[db][4 * j] * inv, o[db][4 * j + 1] * inv);
-        w.y = pack_bf2(o[db][4 * j + 2] * inv, o[db][4 * j + 3] * inv);
+        w.x = pack_e2<HF>(o[db][4 * j] * inv, o[db][4 * j + 1] * inv);
+        w.y = pack_e2<HF>(o[db][4 * j + 2] * inv, o[db][4 * j + 3] * inv);
         *reinterpret_cast<uint2*>(orow + db * 32 + 8 * j + 4 * hf) = w;
       }
   }
@@ -478,12 +487,13 @@ static int g_prefill_fa = 1;           // tune key "prefill_fa": 0 = the 16-row 
 static int g_prefill_fa_stag = 1;      // tune key "prefill_fa", second value: 1 = staggered wave halves, 0 = lockstep (A/B)
 extern "C" void edge_prefill_fa(int v, int stag) { g_prefill_fa = v; g_prefill_fa_stag = stag; }
 
-extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
-                                 const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
-                                 int causal, hipStream_t st) {
-  if (B * T == 0) return 0;
-  if (Hq % Hkv) return -2;
-  const float sl2 = scale * 1.4426950408889634f;
+namespace {
+template <bool HF>
+int run_prefill(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
+                const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float sl2, int causal,
+                hipStream_t st) {
+#define ARGS (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, \
+             Hq, Hkv, sl2
   // fa_kernel takes 256 queries per workgroup: below ~128 workgroups (short prompts, few heads) the
   // 64-row kernel keeps more CUs busy (tools/bench_ops.py --only prefill, D 128: T 512 x 32 heads
   // 23.4 vs 27.6 us, T 1024 54.8 vs 50.2, T 2048 198 vs 98, 4K chunk over 28K cached keys 6.09 vs
@@ -494,36 +504,24 @@ extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void*
   do {                                                                                                             \
     static bool fa_attr = false;                                                                                   \
     if (!fa_attr) {                                                                                                \
-      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, true>, hipFuncAttributeMaxDynamicSharedMemorySize,      \
-                                FaGeo<DD>::LDS);                                                                   \
-      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
-                                FaGeo<DD>::LDS);                                                                   \
-      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                FaGeo<DD>::LDS_STG);                                                               \
-      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                FaGeo<DD>::LDS_STG);                                                               \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, true, false, HF>,                                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FaGeo<DD>::LDS);                       \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false, false, HF>,                                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FaGeo<DD>::LDS);                       \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, true, true, HF>,                                        \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FaGeo<DD>::LDS_STG);                   \
+      (void)hipFuncSetAttribute((const void*)fa_kernel<DD, false, true, HF>,                                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FaGeo<DD>::LDS_STG);                   \
       fa_attr = true;                                                                                              \
     }                                                                                                              \
     const dim3 g((T + FA_QT - 1) / FA_QT, Hq, B);                                                                  \
     if (g_prefill_fa_stag) {                                                                                       \
-      if (causal)                                                                                                  \
-        hipLaunchKernelGGL((fa_kernel<DD, true, true>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, (const bf16_t*)q,  \
-                           (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T,  \
-                           Hq, Hkv, sl2);                                                                          \
-      else                                                                                                         \
-        hipLaunchKernelGGL((fa_kernel<DD, false, true>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, (const bf16_t*)q, \
-                           (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T,  \
-                           Hq, Hkv, sl2);                                                                          \
+      if (causal) hipLaunchKernelGGL((fa_kernel<DD, true, true, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, ARGS); \
+      else hipLaunchKernelGGL((fa_kernel<DD, false, true, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, ARGS);     \
       break;                                                                                                       \
     }                                                                                                              \
-    if (causal)                                                                                                    \
-      hipLaunchKernelGGL((fa_kernel<DD, true>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, (const bf16_t*)q,              \
-                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \
-                         Hkv, sl2);                                                                                \
-    else                                                                                                           \
-      hipLaunchKernelGGL((fa_kernel<DD, false>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, (const bf16_t*)q,             \
-                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \
-                         Hkv, sl2);                                                                                \
+    if (causal) hipLaunchKernelGGL((fa_kernel<DD, true, false, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, ARGS);    \
+    else hipLaunchKernelGGL((fa_kernel<DD, false, false, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, ARGS);          \
   } while (0)
     if (D == 128) FA(128);
     else FA(64);
@@ -535,20 +533,14 @@ extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void*
   do {                                                                                                            \
     static bool attr_set = false; /* >64 KiB dynamic LDS (D=256): raise the per-kernel cap once */                \
     if (!attr_set && Geo<DD>::LDS > 65536) {                                                                      \
-      (void)hipFuncSetAttribute((const void*)prefill_attn_kernel<DD, true>,                                        \
+      (void)hipFuncSetAttribute((const void*)prefill_attn_kernel<DD, true, HF>,                                    \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Geo<DD>::LDS);                         \
-      (void)hipFuncSetAttribute((const void*)prefill_attn_kernel<DD, false>,                                       \
+      (void)hipFuncSetAttribute((const void*)prefill_attn_kernel<DD, false, HF>,                                   \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Geo<DD>::LDS);                         \
     }                                                                                                             \
     attr_set = true;                                                                                              \
-    if (causal)                                                                                                   \
-      hipLaunchKernelGGL((prefill_attn_kernel<DD, true>), grid, dim3(NT), Geo<DD>::LDS, st, (const bf16_t*)q,       \
-                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \
-                         Hkv, sl2);                                                                               \
-    else                                                                                                          \
-      hipLaunchKernelGGL((prefill_attn_kernel<DD, false>), grid, dim3(NT), Geo<DD>::LDS, st, (const bf16_t*)q,      \
-                         (const bf16_t*)k_cache, (const bf16_t*)v_cache, c_sb, c_sh, start_pos, (bf16_t*)out, T, Hq, \
-                         Hkv, sl2);                                                                               \
+    if (causal) hipLaunchKernelGGL((prefill_attn_kernel<DD, true, HF>), grid, dim3(NT), Geo<DD>::LDS, st, ARGS);   \
+    else hipLaunchKernelGGL((prefill_attn_kernel<DD, false, HF>), grid, dim3(NT), Geo<DD>::LDS, st, ARGS);         \
   } while (0)
   switch (D) {
     case 64: PL(64); break;
@@ -558,5 +550,18 @@ extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void*
     default: return -4;
   }
 #undef PL
+#undef ARGS
   return (int)hipGetLastError();
+}
+}  // namespace
+
+// h16: q, caches and out are fp16 (fp16 MFMA), else bf16
+extern "C" int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
+                                 const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
+                                 int causal, int h16, hipStream_t st) {
+  if (B * T == 0) return 0;
+  if (Hq % Hkv) return -2;
+  const float sl2 = scale * 1.4426950408889634f;
+  return h16 ? run_prefill<true>(q, k_cache, v_cache, c_sb, c_sh, start_pos, out, B, T, Hq, Hkv, D, sl2, causal, st)
+             : run_prefill<false>(q, k_cache, v_cache, c_sb, c_sh, start_pos, out, B, T, Hq, Hkv, D, sl2, causal, st);
 }

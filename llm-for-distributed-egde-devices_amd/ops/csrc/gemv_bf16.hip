@@ -23,21 +23,28 @@
 //   EPI_PART: split-K, workgroup (group, ks) reduces k-pairs [KP ks / S, KP (ks + 1) / S) and
 //            writes fp32 partials part[ks][M][N] (bias in slice 0) for a norm kernel that sums
 //            them (the o / down projections of RMSNorm decoders; N = 2048 has only 128 tiles).
+// HF: fp16 activations / weights / outputs on v_mfma_f32_16x16x32_f16 (the reference's fp16 agents,
+// Phi-2 / Pythia); the same fragment layout and epilogues with fp16 roundings.
 #include "common.h"
 
 namespace {
 constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GELU_TANH = 2, EPI_GELU = 3, EPI_PART = 4;
 constexpr int NW = 16;
 
-__device__ __forceinline__ v4f mfma_bf16(const v8s& a, const v8s& b, const v4f& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+
+template <bool HF>
+__device__ __forceinline__ v4f mfma_16(const v8s& a, const v8s& b, const v4f& c) {
+  if constexpr (HF)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a), __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
   return __builtin_bit_cast(v8s, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p)));
 }
 
-template <int MB, int NTW, int U, int EPI>
+template <int MB, int NTW, int U, int EPI, bool HF>
 __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                             int M, int N, int K, int F, int S,
@@ -94,8 +101,8 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
         for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
           for (int j = 0; j < NTW; ++j) {
-            acc[mb][j] = mfma_bf16(a[u][mb][0], b[u][j][0], acc[mb][j]);
-            acc[mb][j] = mfma_bf16(a[u][mb][1], b[u][j][1], acc[mb][j]);
+            acc[mb][j] = mfma_16<HF>(a[u][mb][0], b[u][j][0], acc[mb][j]);
+            acc[mb][j] = mfma_16<HF>(a[u][mb][1], b[u][j][1], acc[mb][j]);
           }
       }
     }
@@ -119,16 +126,16 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
     if constexpr (EPI == EPI_GLU) {
       const int c1 = col_of(tw + NTW / 2);
       const v4f g4 = total(tw), u4 = total(tw + NTW / 2);
-      const float bg = bias != nullptr ? bf2f(bias[c0]) : 0.f, bu = bias != nullptr ? bf2f(bias[c1]) : 0.f;
+      const float bg = bias != nullptr ? e2f<HF>(bias[c0]) : 0.f, bu = bias != nullptr ? e2f<HF>(bias[c1]) : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * mb + 4 * (lane >> 4) + q;
-        const float g = bf2f(f2bf(g4[q] + bg)), u = bf2f(f2bf(u4[q] + bu));
-        if (row < M && c0 < F) out[(size_t)row * F + c0] = f2bf(g / (1.f + __expf(-g)) * u);
+        const float g = e2f<HF>(f2e<HF>(g4[q] + bg)), u = e2f<HF>(f2e<HF>(u4[q] + bu));
+        if (row < M && c0 < F) out[(size_t)row * F + c0] = f2e<HF>(g / (1.f + __expf(-g)) * u);
       }
     } else if constexpr (EPI == EPI_PART) {
       const v4f s4 = total(tw);
-      const float bv = bias != nullptr && c0 < N && ks == 0 ? bf2f(bias[c0]) : 0.f;
+      const float bv = bias != nullptr && c0 < N && ks == 0 ? e2f<HF>(bias[c0]) : 0.f;
       float* part = reinterpret_cast<float*>(out) + (size_t)ks * M * N;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -137,92 +144,107 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
       }
     } else {
       const v4f s4 = total(tw);
-      const float bv = bias != nullptr && c0 < N ? bf2f(bias[c0]) : 0.f;
+      const float bv = bias != nullptr && c0 < N ? e2f<HF>(bias[c0]) : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * mb + 4 * (lane >> 4) + q;
         float v = s4[q] + bv;
         if constexpr (EPI == EPI_GELU_TANH) {
-          const float a = bf2f(f2bf(v)), k0 = 0.7978845608028654f, k1 = 0.044715f;
+          const float a = e2f<HF>(f2e<HF>(v)), k0 = 0.7978845608028654f, k1 = 0.044715f;
           v = 0.5f * a * (1.f + tanhf(k0 * (a + k1 * a * a * a)));
         } else if constexpr (EPI == EPI_GELU) {
-          const float a = bf2f(f2bf(v));
+          const float a = e2f<HF>(f2e<HF>(v));
           v = 0.5f * a * (1.f + erff(a * 0.7071067811865476f));
         } else {
-          // EPI_OUT with an addend (parallel-residual block): bf16(bf16(y) + add), the unfused add
-          if (add != nullptr && row < M && c0 < N) v = bf2f(f2bf(v)) + bf2f(add[(size_t)row * N + c0]);
+          // EPI_OUT with an addend (parallel-residual block): rnd(rnd(y) + add), the unfused add
+          if (add != nullptr && row < M && c0 < N) v = e2f<HF>(f2e<HF>(v)) + e2f<HF>(add[(size_t)row * N + c0]);
         }
-        if (row < M && c0 < N) out[(size_t)row * N + c0] = f2bf(v);
+        if (row < M && c0 < N) out[(size_t)row * N + c0] = f2e<HF>(v);
       }
     }
   }
 }
 
-template <int MB, int NTW, int U, int EPI>
+template <int MB, int NTW, int U, int EPI, bool HF>
 int launch_mb(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
               hipStream_t st, int S, const void* add = nullptr) {
   const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
-  hipLaunchKernelGGL((gemv_bf16_kernel<MB, NTW, U, EPI>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
+  hipLaunchKernelGGL((gemv_bf16_kernel<MB, NTW, U, EPI, HF>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
                      (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S, (const bf16_t*)add);
   return (int)hipGetLastError();
 }
 
 // NTW / U chosen for one row block; more row blocks keep U = 2 (registers) and at most 8 / MB
 // tiles (the LDS reduction holds MB x NTW tiles of 16 waves)
-template <int NTW, int U, int EPI>
+template <int NTW, int U, int EPI, bool HF>
 int launch(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
            hipStream_t st, int S = 1, const void* add = nullptr) {
   constexpr int G = EPI == EPI_GLU ? 2 : 1;                 // GLU keeps gate / up pairs
   constexpr int N2 = NTW > 4 ? 4 : (NTW < G ? G : NTW), N34 = NTW > 2 ? 2 : (NTW < G ? G : NTW);
   const int mb = (M + 15) / 16;
-  if (mb <= 1) return launch_mb<1, NTW, U, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
-  if (mb == 2) return launch_mb<2, N2, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
-  if (mb == 3) return launch_mb<3, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
-  return launch_mb<4, N34, 2, EPI>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  if (mb <= 1) return launch_mb<1, NTW, U, EPI, HF>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  if (mb == 2) return launch_mb<2, N2, 2, EPI, HF>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  if (mb == 3) return launch_mb<3, N34, 2, EPI, HF>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
+  return launch_mb<4, N34, 2, EPI, HF>(A, W, bias, out, M, N, K, F, tiles, st, S, add);
 }
-}  // namespace
 
 // W: fragment-packed bf16 (ops.pack_bf16_weight).  epi 0: out bf16 [M, N] (+ the bf16 addend `add`
 // [M, N] when not null: a parallel-residual block's other branch); epi 1 (GLU):
 // W = [gate | up] with N = 2F, out = silu(gate) * up bf16 [M, F] (F % 16 == 0); epi 2 / 3: gelu (tanh / erf) of the bf16 output.  M <= 64, K % 64 == 0,
 // N % 16 == 0.  Returns -2 for shapes it does not take.
-extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
-                              hipStream_t st, const void* add) {
+template <bool HF>
+int gemv_run(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi, hipStream_t st,
+             const void* add) {
   if (M <= 0 || M > 64 || K % 64 != 0 || N % 16 != 0 || K <= 0) return -2;
   const int KP = K / 64;
   const int U = KP >= 64 ? 4 : 2;                            // k-pairs in flight per wave
   if (epi == EPI_GLU) {
     if (N % 32 != 0) return -2;
     const int F = N / 2, ft = F / 16;
-    if (ft >= 512) return launch<4, 2, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st);
-    return U == 4 ? launch<2, 4, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st)
-                  : launch<2, 2, EPI_GLU>(A, W, bias, out, M, N, K, F, ft, st);
+    if (ft >= 512) return launch<4, 2, EPI_GLU, HF>(A, W, bias, out, M, N, K, F, ft, st);
+    return U == 4 ? launch<2, 4, EPI_GLU, HF>(A, W, bias, out, M, N, K, F, ft, st)
+                  : launch<2, 2, EPI_GLU, HF>(A, W, bias, out, M, N, K, F, ft, st);
   }
   if (epi != EPI_OUT && epi != EPI_GELU_TANH && epi != EPI_GELU) return -2;
   const int nt = N / 16;
   // ~256 workgroups: one tile each below 512 tiles, then 2 or 4
 #define PICK(EP)                                                                               \
-  if (nt >= 1024) return launch<4, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);                \
-  if (nt >= 512) return U == 4 ? launch<2, 4, EP>(A, W, bias, out, M, N, K, 0, nt, st)         \
-                               : launch<2, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);        \
-  return U == 4 ? launch<1, 4, EP>(A, W, bias, out, M, N, K, 0, nt, st)                        \
-                : launch<1, 2, EP>(A, W, bias, out, M, N, K, 0, nt, st);
+  if (nt >= 1024) return launch<4, 2, EP, HF>(A, W, bias, out, M, N, K, 0, nt, st);                \
+  if (nt >= 512) return U == 4 ? launch<2, 4, EP, HF>(A, W, bias, out, M, N, K, 0, nt, st)         \
+                               : launch<2, 2, EP, HF>(A, W, bias, out, M, N, K, 0, nt, st);        \
+  return U == 4 ? launch<1, 4, EP, HF>(A, W, bias, out, M, N, K, 0, nt, st)                        \
+                : launch<1, 2, EP, HF>(A, W, bias, out, M, N, K, 0, nt, st);
   if (epi == EPI_GELU_TANH) { PICK(EPI_GELU_TANH) }
   if (epi == EPI_GELU) { PICK(EPI_GELU) }
   // plain output, optionally + a bf16 addend [M, N]
-  if (nt >= 1024) return launch<4, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
-  if (nt >= 512) return U == 4 ? launch<2, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add)
-                               : launch<2, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
-  return U == 4 ? launch<1, 4, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add)
-                : launch<1, 2, EPI_OUT>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
+  if (nt >= 1024) return launch<4, 2, EPI_OUT, HF>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
+  if (nt >= 512) return U == 4 ? launch<2, 4, EPI_OUT, HF>(A, W, bias, out, M, N, K, 0, nt, st, 1, add)
+                               : launch<2, 2, EPI_OUT, HF>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
+  return U == 4 ? launch<1, 4, EPI_OUT, HF>(A, W, bias, out, M, N, K, 0, nt, st, 1, add)
+                : launch<1, 2, EPI_OUT, HF>(A, W, bias, out, M, N, K, 0, nt, st, 1, add);
 #undef PICK
 }
 
 // Split-K form: fp32 partial slices part [S, M, N] (bias in slice 0), one 16-column tile per group.
-extern "C" int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K,
-                                     int S, hipStream_t st) {
+template <bool HF>
+int gemv_splitk_run(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
+                    hipStream_t st) {
   if (M <= 0 || M > 64 || K % 64 != 0 || N % 16 != 0 || S < 1 || S > K / 64) return -2;
   const int nt = N / 16, kps = K / 64 / S;
-  return kps >= 64 ? launch<1, 4, EPI_PART>(A, W, bias, part, M, N, K, 0, nt, st, S)
-                   : launch<1, 2, EPI_PART>(A, W, bias, part, M, N, K, 0, nt, st, S);
+  return kps >= 64 ? launch<1, 4, EPI_PART, HF>(A, W, bias, part, M, N, K, 0, nt, st, S)
+                   : launch<1, 2, EPI_PART, HF>(A, W, bias, part, M, N, K, 0, nt, st, S);
+}
+}  // namespace
+
+// h16: fp16 operands / outputs (fragment-packed fp16 weights), else bf16
+extern "C" int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
+                              hipStream_t st, const void* add, int h16) {
+  return h16 ? gemv_run<true>(A, W, bias, out, M, N, K, epi, st, add)
+             : gemv_run<false>(A, W, bias, out, M, N, K, epi, st, add);
+}
+
+extern "C" int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K,
+                                     int S, hipStream_t st, int h16) {
+  return h16 ? gemv_splitk_run<true>(A, W, bias, part, M, N, K, S, st)
+             : gemv_splitk_run<false>(A, W, bias, part, M, N, K, S, st);
 }

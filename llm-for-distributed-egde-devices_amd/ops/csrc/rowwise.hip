@@ -338,8 +338,8 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
                          const float* xpart, int S, int h16, hipStream_t st) {
   // quant 2: int8 output fragment-packed for the 256-row decode GEMM (H % 64 == 0, <= 256 rows)
   if (H % 8 || (quant == 2 && (H % 64 != 0 || rows > 256))) return -2;
-  // h16: fp16 rows (the fp16 agents' bf16-free path): plain norms only, no int8 output / partials
-  if (h16 && (quant || xpart != nullptr)) return -2;
+  // h16: fp16 rows (the fp16 agents' bf16-free path): no int8 output
+  if (h16 && quant) return -2;
   const int pkt = quant == 2 ? H / 64 : 0;
   if (xpart != nullptr && (!rms || res_out == nullptr || S < 1)) return -2;
   if (rows == 0) return 0;
@@ -356,8 +356,13 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
 #define LAUNCH_NORMH(RMS, HR) \
   hipLaunchKernelGGL((norm_kernel<NCH, RMS, HR, false, false, true>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, \
                      RO, H, eps, nullptr, 0, 0)
+#define LAUNCH_NORMPH(HR) \
+  hipLaunchKernelGGL((norm_kernel<NCH, true, HR, false, true, true>), dim3(rows), dim3(NT), 0, st, X, R, W, Bb, Y, Q, ys, \
+                     RO, H, eps, xpart, S, 0)
   NCH_DISPATCH(H, {
-    if (h16) {
+    if (h16 && xpart != nullptr) {
+      if (res) LAUNCH_NORMPH(true); else LAUNCH_NORMPH(false);
+    } else if (h16) {
       if (rms) { if (res) LAUNCH_NORMH(true, true); else LAUNCH_NORMH(true, false); }
       else { if (res) LAUNCH_NORMH(false, true); else LAUNCH_NORMH(false, false); }
     } else if (xpart != nullptr) {
@@ -374,6 +379,7 @@ extern "C" int edge_norm(const void* x, const void* res, const void* w, const vo
 #undef LAUNCH_NORM
 #undef LAUNCH_NORMP
 #undef LAUNCH_NORMH
+#undef LAUNCH_NORMPH
   return (int)hipGetLastError();
 }
 

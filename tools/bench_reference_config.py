@@ -9,6 +9,10 @@ combiners' definition), p50 per-token step latency, and the ratio to the publish
 for the same model and precision (fp16/bf16 -> mode ``none``; INT8 -> ``llm_int8``, the same
 bitsandbytes algorithm, and ``w8a8_smoothquant``, the MFMA INT8 path).
 
+The unquantised rows run each model in the reference's own precision: fp16 for Phi-2 and Pythia
+(``phi2-pythia_fp_updated.py:32``), bf16 for Llama-3.2-1B (``Llama_bf16_updated.py:32``);
+``--precision bf16|fp16`` overrides.  The INT8 modes keep bf16 activations (their GEMM epilogues).
+
 Random-init weights of each architecture (no checkpoints offline) and random prompt ids of a
 typical NQ prompt length; EOS is disabled, so every generation runs the full 200 tokens.
 
@@ -34,6 +38,7 @@ from edgellm.models import build_model, get_config  # noqa: E402
 from edgellm.quant import quantize_head, quantize_model, synthetic_calibration  # noqa: E402
 
 # BASELINE.md (ACL.pdf p.7 Table 3): tokens/sec on an A100 40GB, batch 1
+REF_PRECISION = {"phi-2": torch.float16, "pythia-1b": torch.float16, "llama-3.2-1b": torch.bfloat16}
 PUBLISHED = {("phi-2", "fp"): 42.0725, ("pythia-1b", "fp"): 104.1318, ("llama-3.2-1b", "fp"): 51.8408,
              ("phi-2", "int8"): 17.0744, ("pythia-1b", "int8"): 39.0937, ("llama-3.2-1b", "int8"): 25.8326}
 
@@ -45,6 +50,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=64)
     ap.add_argument("--new-tokens", type=int, default=200)
     ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--precision", default="ref", choices=["ref", "bf16", "fp16"],
+                    help="activation dtype of the unquantised rows (ref: the reference's per-model choice)")
     ap.add_argument("--lm-head", default="bf16", choices=["bf16", "int8"],
                     help="int8: W8A8 LM head for the quantised modes (quant.quantize_head; the reference keeps "
                          "its head in 16 bits, so such rows are labelled '+int8_head')")
@@ -56,7 +63,11 @@ def main():
         prompt = torch.randint(0, cfg.vocab_size, (1, a.prompt_len), generator=g).tolist()
         sp = SamplingParams(max_new_tokens=a.new_tokens)
         for mode in a.modes.split(","):
-            model = build_model(cfg, device=dev, seed=0)
+            dtype = torch.bfloat16
+            if mode == "none":
+                dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(a.precision,
+                                                                          REF_PRECISION.get(name, torch.bfloat16))
+            model = build_model(cfg, dtype=dtype, device=dev, seed=0)
             if mode != "none":
                 calib = synthetic_calibration(cfg, n=4, T=64, device=dev) if mode == "w8a8_smoothquant" else None
                 model = quantize_model(model, mode, calib_ids=calib)
@@ -74,7 +85,7 @@ def main():
                 steps = sorted(res.step_ms) if res.step_ms else [float("nan")]
                 pub = PUBLISHED.get((name, "fp" if mode == "none" else "int8"))
                 label = mode + ("+int8_head" if a.lm_head == "int8" and mode == "w8a8_smoothquant" else "")
-                row = dict(model=name, mode=label, batch=1, prompt_len=a.prompt_len, new_tokens=res.num_generated,
+                row = dict(model=name, mode=label, dtype=str(dtype)[6:], batch=1, prompt_len=a.prompt_len, new_tokens=res.num_generated,
                            tps_incl_prompt=round(res.tps_incl_prompt(), 1), tps_generated=round(res.tps_generated(), 1),
                            wall_s=round(wall, 4), p50_step_ms=round(steps[len(steps) // 2], 3),
                            published_tps=pub, vs_published=round(res.tps_incl_prompt() / pub, 1) if pub else None)
