@@ -31,21 +31,28 @@ int edge_max_prob(const void* logits, float* out, int rows, int V, int dt, hipSt
 int edge_rope_kv_write(const void* qkv, const int* start_pos, const float* cs, void* q_out, void* k_cache,
                        void* v_cache, int B, int T, int Hq, int Hkv, int D, int rot, int64_t c_sb, int64_t c_sh,
                        int S, void* k2, void* v2, int64_t c2_sb, int64_t c2_sh, int S2, int split_h,
-                       const int* cpos2, hipStream_t st);
+                       const int* cpos2, int h16, hipStream_t st);
 int edge_decode_attn_plan(int B, int Hkv, int max_len, int D, int* ch_out, int* nsplit_out);
 int edge_decode_attn(const void* q, int64_t q_sb, void* k_cache, void* v_cache, int64_t c_sb, int64_t c_sh,
                      const int* seq_lens, int B, int Hq, int Hkv, int D, float scale, int ch, int nsplit, void* out,
                      int64_t o_sb, float* part_acc, float* part_ml, const int* pos, const float* cs, int rot,
-                     void* out_q, float* out_s, int Mpad, hipStream_t st);
+                     void* out_q, float* out_s, int Mpad, int h16, hipStream_t st);
 int edge_prefill_attn(const void* q, const void* k_cache, const void* v_cache, int64_t c_sb, int64_t c_sh,
                       const int* start_pos, void* out, int B, int T, int Hq, int Hkv, int D, float scale,
-                      int causal, hipStream_t st);
+                      int causal, int h16, hipStream_t st);
 int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                    float* os, int M, int N, int K, int KT, int a_mode, int Mpad, int epi, hipStream_t st);
 int edge_sample(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                 float inv_temperature, float penalty, int top_k, float top_p, int do_sample, const int* rng,
                 int64_t* out_tok, void* workspace, hipStream_t st);
 size_t edge_sample_workspace(int B, int V);
+int edge_sample_shard_mode(int do_sample, float temperature, int top_k, float top_p, int V);
+int edge_sample_shard_chunks(int Vs, int V);
+int edge_sample_shard(const void* logits, int is_bf16, const uint8_t* seen, int B, int Vs, int v0, int V,
+                      float temperature, float inv_temperature, float penalty, int top_k, float top_p, int do_sample,
+                      const int* rng, uint64_t* pc, uint32_t* pthr, hipStream_t st);
+int edge_sample_merge(const uint64_t* pc, const uint32_t* pthr, int B, int C, int V, float temperature, int top_k,
+                      float top_p, int do_sample, const int* rng, int64_t* out_tok, hipStream_t st);
 int edge_sample_advance(const void* logits, int is_bf16, uint8_t* seen, int B, int V, float temperature,
                         float inv_temperature, float penalty, int top_k, float top_p, int do_sample, int* rng,
                         int64_t* out_tok, void* workspace, int64_t* tok, int64_t* out, int64_t out_sb, int ncols,
@@ -66,9 +73,9 @@ void edge_w8a8_rows256_diag(int v);
 void edge_w8a8_prefill_x32(int v);
 void edge_w8a8_rows256_rot(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
-                   hipStream_t st, const void* add);
+                   hipStream_t st, const void* add, int h16);
 int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
-                          hipStream_t st);
+                          hipStream_t st, int h16);
 int edge_llmint8_prep(const void* x, int M, int K, float thr, int cmax, void* q, float* sa, int* cols, float* xo,
                       int* count, hipStream_t st);
 int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int* count, const void* wt,
@@ -131,11 +138,11 @@ int64_t rows_of(const at::Tensor& x) { return x.numel() / x.size(-1); }
 
 // A 16-bit float activation / weight: bf16 (the default) or fp16 (the fp16 agents).  Returns 1 for
 // fp16, 0 for bf16.
-int need16(const at::Tensor& t, const char* name) {
+int need16(const at::Tensor& t, const char* name, bool contiguous = true) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, name, " has dtype ",
               t.scalar_type(), ", expected bfloat16 or float16");
-  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(!contiguous || t.is_contiguous(), name, " must be contiguous");
   return t.scalar_type() == at::kHalf ? 1 : 0;
 }
 void need_same(const at::Tensor& t, const at::Tensor& like, const char* name) {
@@ -186,21 +193,24 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> norm(const at::Ten
   return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
 }
 
-// RMSNorm whose input is S fp32 split-K partial slices [S, M, H] of a W8A8 projection (summed in
-// slice order, rounded to bf16): returns (y or q, scale, h) with h = bf16(sum) (+ residual).
+// RMSNorm whose input is S fp32 split-K partial slices [S, M, H] of a decode projection (summed in
+// slice order, rounded to the weight's 16-bit type): returns (y or q, scale, h) with h = rnd(sum)
+// (+ residual).  fp16 weights: no int8 output.
 std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(const at::Tensor& parts,
                                                                               const std::optional<at::Tensor>& residual,
                                                                               const at::Tensor& w, double eps, int64_t quant) {
   DEVICE_GUARD(parts);
   need(parts, at::kFloat, "parts");
-  need(w, at::kBFloat16, "weight");
+  const int h16 = need16(w, "weight");
+  TORCH_CHECK(!(h16 && quant), "int8 output from fp16 rows is not supported");
   TORCH_CHECK(parts.dim() == 3, "parts must be [S, M, H]");
   const int64_t S = parts.size(0), R = parts.size(1), H = parts.size(2);
   TORCH_CHECK(w.numel() == H, "norm weight size mismatch");
   auto opts = w.options();
   at::Tensor res_out = at::empty({R, H}, opts);
   if (residual) {
-    need(*residual, at::kBFloat16, "residual");
+    need16(*residual, "residual");
+    need_same(*residual, w, "residual");
     TORCH_CHECK(residual->numel() == R * H, "residual shape mismatch");
   }
   at::Tensor y, s;
@@ -216,7 +226,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>, at::Tensor> rms_norm_parts(con
   }
   check(edge_norm(nullptr, residual ? residual->data_ptr() : nullptr, w.data_ptr(), nullptr,
                   quant ? nullptr : y.data_ptr(), quant ? y.data_ptr() : nullptr, quant ? s.data_ptr<float>() : nullptr,
-                  res_out.data_ptr(), (int)R, (int)H, (float)eps, 1, quant, parts.data_ptr<float>(), (int)S, 0,
+                  res_out.data_ptr(), (int)R, (int)H, (float)eps, 1, quant, parts.data_ptr<float>(), (int)S, h16,
                   stream()),
         "rms_norm_parts");
   return {y, quant ? std::optional<at::Tensor>(s) : std::nullopt, res_out};
@@ -288,8 +298,10 @@ at::Tensor max_prob(const at::Tensor& logits) {
 }
 
 // ---------------------------------------------------------------------------------- rope + kv
-void check_cache(const at::Tensor& c, const char* name, int64_t D) {
-  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
+// 16-bit KV cache rows: bf16, or fp16 for fp16 activations (dt)
+void check_cache(const at::Tensor& c, const char* name, int64_t D, at::ScalarType dt = at::kBFloat16) {
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == dt, name, " must be a ", dt == at::kHalf ? "fp16" : "bf16",
+              " GPU tensor (the activations' dtype)");
   TORCH_CHECK(c.dim() == 4 && c.size(3) == D && c.stride(3) == 1 && c.stride(2) == D,
               name, " must be [B, Hkv, S, D] with contiguous rows");
 }
@@ -299,10 +311,11 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
                          const std::optional<at::Tensor>& k2, const std::optional<at::Tensor>& v2, int64_t split,
                          const std::optional<at::Tensor>& cpos2) {
   DEVICE_GUARD(qkv);
-  need(qkv, at::kBFloat16, "qkv");
+  const int h16 = need16(qkv, "qkv");
+  const auto dt = qkv.scalar_type();
   need(start_pos, at::kInt, "start_pos");
-  check_cache(k_cache, "k_cache", D);
-  check_cache(v_cache, "v_cache", D);
+  check_cache(k_cache, "k_cache", D, dt);
+  check_cache(v_cache, "v_cache", D, dt);
   TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.sizes() == v_cache.sizes());
   const int64_t B = k_cache.size(0);
   TORCH_CHECK(start_pos.numel() == B, "start_pos must have one entry per cache row");
@@ -310,8 +323,8 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
   TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D && k_cache.size(1) == split_h, "qkv / cache head mismatch");
   if (split_h < Hkv) {
     TORCH_CHECK(k2.has_value() && v2.has_value(), "split cache needs k2/v2");
-    check_cache(*k2, "k2", D);
-    check_cache(*v2, "v2", D);
+    check_cache(*k2, "k2", D, dt);
+    check_cache(*v2, "v2", D, dt);
     TORCH_CHECK(k2->strides() == v2->strides() && k2->size(0) == B && k2->size(1) == Hkv - split_h);
     if (cpos2) { need(*cpos2, at::kInt, "cpos2"); TORCH_CHECK(cpos2->numel() == B); }
   }
@@ -330,7 +343,7 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
                            (int)D, (int)rot, k_cache.stride(0), k_cache.stride(1), (int)k_cache.size(2),
                            sp2 ? k2->data_ptr() : nullptr, sp2 ? v2->data_ptr() : nullptr, sp2 ? k2->stride(0) : 0,
                            sp2 ? k2->stride(1) : 0, sp2 ? (int)k2->size(2) : 0, (int)split_h,
-                           (sp2 && cpos2) ? cpos2->data_ptr<int>() : nullptr, stream()),
+                           (sp2 && cpos2) ? cpos2->data_ptr<int>() : nullptr, h16, stream()),
         "rope_kv_write");
   return q;
 }
@@ -339,11 +352,12 @@ at::Tensor rope_kv_write(const at::Tensor& qkv, const at::Tensor& start_pos, con
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                        const at::Tensor& seq_lens, double scale, int64_t max_len_hint) {
   DEVICE_GUARD(q);
-  TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && q.dim() == 3, "q must be bf16 [B, Hq, D]");
+  const int h16 = need16(q, "q", false);
+  TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
   TORCH_CHECK(q.stride(2) == 1 && q.stride(1) == q.size(2), "q heads must be contiguous");
   const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
-  check_cache(k_cache, "k_cache", D);
-  check_cache(v_cache, "v_cache", D);
+  check_cache(k_cache, "k_cache", D, q.scalar_type());
+  check_cache(v_cache, "v_cache", D, q.scalar_type());
   TORCH_CHECK(k_cache.strides() == v_cache.strides());
   need(seq_lens, at::kInt, "seq_lens");
   TORCH_CHECK(seq_lens.numel() == B && k_cache.size(0) == B);
@@ -361,7 +375,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
                          k_cache.stride(1), seq_lens.data_ptr<int>(), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
                          ch, nsplit, out.data_ptr(), out.stride(0), nsplit > 1 ? pacc.data_ptr<float>() : nullptr,
                          nsplit > 1 ? pml.data_ptr<float>() : nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0,
-                         stream()),
+                         h16, stream()),
         "decode_attn");
   return out;
 }
@@ -374,12 +388,13 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_fused(
     at::Tensor& v_cache, const at::Tensor& seq_lens, int64_t Hq, double scale, int64_t max_len_hint, int64_t rot,
     bool quant_out) {
   DEVICE_GUARD(qkv);
-  need(qkv, at::kBFloat16, "qkv");
+  const int h16 = need16(qkv, "qkv");
+  TORCH_CHECK(!(h16 && quant_out), "int8 attention output from fp16 rows is not supported");
   TORCH_CHECK(qkv.dim() == 2, "qkv must be [B, (Hq + 2 Hkv) * D]");
   const int64_t B = qkv.size(0), D = k_cache.size(3), Hkv = k_cache.size(1);
   TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width does not match the cache geometry");
-  check_cache(k_cache, "k_cache", D);
-  check_cache(v_cache, "v_cache", D);
+  check_cache(k_cache, "k_cache", D, qkv.scalar_type());
+  check_cache(v_cache, "v_cache", D, qkv.scalar_type());
   TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.size(0) == B);
   need(start_pos, at::kInt, "start_pos");
   need(seq_lens, at::kInt, "seq_lens");
@@ -413,7 +428,7 @@ std::tuple<at::Tensor, std::optional<at::Tensor>> decode_attn_fused(
                          ch, nsplit, quant_out ? nullptr : out.data_ptr(), quant_out ? 0 : out.stride(0),
                          nsplit > 1 ? pacc.data_ptr<float>() : nullptr, nsplit > 1 ? pml.data_ptr<float>() : nullptr,
                          start_pos.data_ptr<int>(), cs, (int)rot, quant_out ? oq.data_ptr() : nullptr,
-                         quant_out ? os->data_ptr<float>() : nullptr, (int)Mpad, stream()),
+                         quant_out ? os->data_ptr<float>() : nullptr, (int)Mpad, h16, stream()),
         "decode_attn_fused");
   if (quant_out) return {oq, os};
   return {out, std::nullopt};
@@ -513,18 +528,18 @@ void kv_dequant(const at::Tensor& cache, const at::Tensor& scales, at::Tensor& d
 at::Tensor prefill_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                         const at::Tensor& start_pos, double scale, bool causal) {
   DEVICE_GUARD(q);
-  need(q, at::kBFloat16, "q");
+  const int h16 = need16(q, "q");
   TORCH_CHECK(q.dim() == 4, "q must be [B, T, Hq, D]");
   const int64_t B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3);
-  check_cache(k_cache, "k_cache", D);
-  check_cache(v_cache, "v_cache", D);
+  check_cache(k_cache, "k_cache", D, q.scalar_type());
+  check_cache(v_cache, "v_cache", D, q.scalar_type());
   TORCH_CHECK(k_cache.strides() == v_cache.strides() && k_cache.size(0) == B);
   need(start_pos, at::kInt, "start_pos");
   TORCH_CHECK(start_pos.numel() == B);
   auto out = at::empty_like(q);
   check(edge_prefill_attn(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1),
                           start_pos.data_ptr<int>(), out.data_ptr(), (int)B, (int)T, (int)Hq, (int)k_cache.size(1),
-                          (int)D, (float)scale, causal, stream()),
+                          (int)D, (float)scale, causal, h16, stream()),
         "prefill_attn");
   return out;
 }
@@ -647,20 +662,20 @@ at::Tensor w8a8_gemm_splitk(const at::Tensor& a, const at::Tensor& sa, const at:
 at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
                      int64_t epi, const std::optional<at::Tensor>& addend) {
   DEVICE_GUARD(x);
-  need(x, at::kBFloat16, "x");
-  need(wp, at::kBFloat16, "weight (packed)");
+  const int h16 = need16(x, "x");
+  need_same(wp, x, "weight (packed)");
   const int64_t K = x.size(-1), M = rows_of(x);
   TORCH_CHECK(wp.numel() == N * K, "packed weight must hold N * K elements");
-  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+  if (bias) { need_same(*bias, x, "bias"); TORCH_CHECK(bias->numel() == N); }
   auto os = x.sizes().vec();
   os.back() = epi == 1 ? N / 2 : N;
   auto out = at::empty(os, x.options());
   if (addend) {
-    need(*addend, at::kBFloat16, "addend");
+    need_same(*addend, x, "addend");
     TORCH_CHECK(epi == 0 && addend->numel() == M * N, "addend: plain output only, M * N elements");
   }
   check(edge_gemv_bf16(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M, (int)N,
-                       (int)K, (int)epi, stream(), addend ? addend->data_ptr() : nullptr),
+                       (int)K, (int)epi, stream(), addend ? addend->data_ptr() : nullptr, h16),
         "gemv_bf16");
   return out;
 }
@@ -669,14 +684,14 @@ at::Tensor gemv_bf16(const at::Tensor& x, const at::Tensor& wp, const std::optio
 at::Tensor gemv_bf16_splitk(const at::Tensor& x, const at::Tensor& wp, const std::optional<at::Tensor>& bias,
                             int64_t N, int64_t S) {
   DEVICE_GUARD(x);
-  need(x, at::kBFloat16, "x");
-  need(wp, at::kBFloat16, "weight (packed)");
+  const int h16 = need16(x, "x");
+  need_same(wp, x, "weight (packed)");
   const int64_t K = x.size(-1), M = rows_of(x);
   TORCH_CHECK(wp.numel() == N * K, "packed weight must hold N * K elements");
-  if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+  if (bias) { need_same(*bias, x, "bias"); TORCH_CHECK(bias->numel() == N); }
   auto part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
   check(edge_gemv_bf16_splitk(x.data_ptr(), wp.data_ptr(), bias ? bias->data_ptr() : nullptr, part.data_ptr<float>(),
-                              (int)M, (int)N, (int)K, (int)S, stream()),
+                              (int)M, (int)N, (int)K, (int)S, stream(), h16),
         "gemv_bf16_splitk");
   return part;
 }
@@ -888,6 +903,67 @@ at::Tensor sample(const at::Tensor& logits, const std::optional<at::Tensor>& see
   return out;
 }
 
+// Vocab-sharded sampler (parallel/vocab_head.py).  sample_shard: phase 1 over logits [B, Vs] =
+// columns [v0, v0 + Vs) of a V-wide row -> (pc int64 [B, C * 128] composites + pthr int32 [B, C])
+// for top-k, or (pc [B, C], empty) for greedy / full-vocab sampling; None when the configuration
+// does not shard (top-k > 128, top-p without top-k).
+std::optional<std::tuple<at::Tensor, at::Tensor>> sample_shard(const at::Tensor& logits,
+                                                               const std::optional<at::Tensor>& seen, double temperature,
+                                                               int64_t top_k, double top_p, double penalty,
+                                                               bool do_sample, const at::Tensor& rng, int64_t v0,
+                                                               int64_t V) {
+  DEVICE_GUARD(logits);
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == at::kFloat, "sample_shard: bf16 or fp32 logits");
+  need(rng, at::kInt, "rng");
+  const int64_t B = logits.size(0), Vs = logits.size(1);
+  TORCH_CHECK(v0 >= 0 && v0 + Vs <= V, "shard outside the vocabulary");
+  if (seen) { need(*seen, at::kByte, "seen"); TORCH_CHECK(seen->sizes() == logits.sizes()); }
+  const int mode = edge_sample_shard_mode(do_sample, (float)temperature, (int)top_k, (float)top_p, (int)V);
+  if (mode < 0) return std::nullopt;
+  const int64_t C = edge_sample_shard_chunks((int)Vs, (int)V);
+  auto pc = at::empty({B, mode == 2 ? C * 128 : C}, logits.options().dtype(at::kLong));
+  auto pthr = at::empty({B, mode == 2 ? C : 0}, logits.options().dtype(at::kInt));
+  const double inv_t = temperature > 0 ? 1.0 / temperature : 1.0;
+  check(edge_sample_shard(logits.data_ptr(), bf, seen ? seen->data_ptr<uint8_t>() : nullptr, (int)B, (int)Vs, (int)v0,
+                          (int)V, (float)temperature, (float)inv_t, (float)penalty, (int)top_k, (float)top_p, do_sample,
+                          rng.data_ptr<int>(), reinterpret_cast<uint64_t*>(pc.data_ptr<int64_t>()),
+                          mode == 2 ? reinterpret_cast<uint32_t*>(pthr.data_ptr<int>()) : nullptr, stream()),
+        "sample_shard");
+  return std::make_tuple(pc, pthr);
+}
+
+// Phase 2 over the shards' lists concatenated per row (pc [B, C_total * 128] + pthr [B, C_total],
+// or pc [B, C_total]) -> tokens int64 [B].
+at::Tensor sample_merge(const at::Tensor& pc, const at::Tensor& pthr, int64_t V, double temperature, int64_t top_k,
+                        double top_p, bool do_sample, const at::Tensor& rng) {
+  DEVICE_GUARD(pc);
+  need(pc, at::kLong, "pc");
+  need(rng, at::kInt, "rng");
+  const int mode = edge_sample_shard_mode(do_sample, (float)temperature, (int)top_k, (float)top_p, (int)V);
+  TORCH_CHECK(mode >= 0, "sample_merge: configuration is not shardable");
+  const int64_t B = pc.size(0);
+  int64_t C = pc.size(1);
+  if (mode == 2) {
+    need(pthr, at::kInt, "pthr");
+    TORCH_CHECK(pthr.size(0) == B && pc.size(1) == pthr.size(1) * 128, "pc / pthr shapes");
+    C = pthr.size(1);
+  }
+  auto out = at::empty({B}, pc.options());
+  check(edge_sample_merge(reinterpret_cast<const uint64_t*>(pc.data_ptr<int64_t>()),
+                          mode == 2 ? reinterpret_cast<const uint32_t*>(pthr.data_ptr<int>()) : nullptr, (int)B, (int)C,
+                          (int)V, (float)temperature, (int)top_k, (float)top_p, do_sample, rng.data_ptr<int>(),
+                          out.data_ptr<int64_t>(), stream()),
+        "sample_merge");
+  return out;
+}
+
+int64_t sample_shard_chunks(int64_t Vs, int64_t V) { return edge_sample_shard_chunks((int)Vs, (int)V); }
+int64_t sample_shard_mode(bool do_sample, double temperature, int64_t top_k, double top_p, int64_t V) {
+  return edge_sample_shard_mode(do_sample, (float)temperature, (int)top_k, (float)top_p, (int)V);
+}
+
 // After the sampler: tok = nxt, out[:, step] = nxt, pos += inc, seq_lens += inc (inc: int32 [B] or
 // None = 1), rng[1] += 1, step += 1 (one launch; the decode state's buffers, all on the sampler's device).
 void decode_advance(const at::Tensor& nxt, at::Tensor& tok, at::Tensor& out, at::Tensor& step, at::Tensor& pos,
@@ -1024,6 +1100,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w8a8_gemm_geluq", &w8a8_gemm_geluq, "W8A8 GEMV + GELU + per-(token, 64) int8 quantisation (M <= 64)");
   m.def("group_quant", &group_quant);
   m.def("sample", &sample);
+  m.def("sample_shard", &sample_shard, "sampler phase 1 over a vocab shard (global ids)");
+  m.def("sample_merge", &sample_merge, "sampler phase 2 over the shards' concatenated candidate lists");
+  m.def("sample_shard_chunks", &sample_shard_chunks);
+  m.def("sample_shard_mode", &sample_shard_mode);
   m.def("sample_advance", &sample_advance, "sampler + decode-step bookkeeping in the sampler's last launch");
   m.def("decode_advance", &decode_advance, "decode-step bookkeeping after the sampler (one launch)");
   m.def("sample_timestamps", &sample_timestamps);

@@ -333,12 +333,13 @@ __device__ __forceinline__ void load_run(const void* lg, const uint8_t* seen, si
 
 // ---------------------------------------------------------------- phase 1
 // Per-chunk best composite (value, then lower id) of the processed (MODE 1: + Gumbel noise)
-// scores -> pc[row*C + c].
+// scores -> pc[row*C + c].  v0: global token id of column 0 (a vocab shard of the LM head: the
+// noise and the composite carry global ids, so shard results merge exactly).
 template <bool BF16, int MODE, int EPT>
 __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict__ logits,
                                                           const uint8_t* __restrict__ seen, int V, int C, float inv_t,
                                                           float pen, const int* __restrict__ rng,
-                                                          uint64_t* __restrict__ pc, int vec) {
+                                                          uint64_t* __restrict__ pc, int vec, int v0) {
   __shared__ float rv[NW];
   __shared__ int ri[NW];
   const int c = blockIdx.x, row = blockIdx.y;
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
   int bi = 0x7fffffff;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    const int i = c0 + o0 + j * ostr;
+    const int i = v0 + c0 + o0 + j * ostr;
     if (o0 + j * ostr < nvalid) {
       float s = sv[j];
       if constexpr (MODE == 1) s += gumbel(seed, row, step, i);
@@ -366,11 +367,12 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
 
 // Per-chunk candidate superset -> pc[(row*C + c)*CCAP + s] as composite keys (unused slots 0),
 // pthr[row*C + c] = threshold key.  Thread t holds the chunk's elements [t * EPT, (t + 1) * EPT).
+// v0: global id of column 0 (vocab shard).
 template <bool BF16, int EPT>
 __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__ logits,
                                                         const uint8_t* __restrict__ seen, int V, int C, float inv_t,
                                                         float pen, int top_k, uint64_t* __restrict__ pc,
-                                                        uint32_t* __restrict__ pthr, int vec) {
+                                                        uint32_t* __restrict__ pthr, int vec, int v0) {
   __shared__ uint32_t red[2 * NW];
   __shared__ int scr[2 * NW];
   __shared__ int cnt;
@@ -423,7 +425,7 @@ __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__
     const int o = o0 + j * ostr;
     const bool ok = o < nvalid && kr[j] >= thr;
     const int s = wave_alloc(ok, &cnt);
-    if (ok && s < CCAP) pc[slot0 + s] = ckey(sv[j], c0 + o);
+    if (ok && s < CCAP) pc[slot0 + s] = ckey(sv[j], v0 + c0 + o);
   }
   __syncthreads();
   for (int s = min(cnt, CCAP) + tid; s < CCAP; s += NT) pc[slot0 + s] = 0ull;
@@ -843,7 +845,7 @@ static int sample_launch(const void* logits, int is_bf16, uint8_t* seen, int B, 
 #undef RW
   } else if (mode == 2) {
 #define TC(BF, E) hipLaunchKernelGGL((topk_chunk_kernel<BF, E>), g1, dim3(NT), 0, st, logits, seen, V, C, inv_t, \
-                                     penalty, top_k, pc, pthr, vec)
+                                     penalty, top_k, pc, pthr, vec, 0)
     if (is_bf16) { if (ept == 8) TC(true, 8); else TC(true, 16); }
     else { if (ept == 8) TC(false, 8); else TC(false, 16); }
 #undef TC
@@ -851,9 +853,9 @@ static int sample_launch(const void* logits, int is_bf16, uint8_t* seen, int B, 
                        out_tok, adv);
   } else {
 #define AC(BF, MD) do { if (ept == 8) hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 8>), g1, dim3(NT), 0, st, logits, \
-                                                        seen, V, C, inv_t, penalty, rng, pc, vec); \
+                                                        seen, V, C, inv_t, penalty, rng, pc, vec, 0); \
                            else hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 16>), g1, dim3(NT), 0, st, logits, seen, \
-                                                   V, C, inv_t, penalty, rng, pc, vec); } while (0)
+                                                   V, C, inv_t, penalty, rng, pc, vec, 0); } while (0)
     if (is_bf16) { if (mode == 0) AC(true, 0); else AC(true, 1); }
     else { if (mode == 0) AC(false, 0); else AC(false, 1); }
 #undef AC
@@ -884,4 +886,75 @@ extern "C" int edge_sample_advance(const void* logits, int is_bf16, uint8_t* see
   const Adv adv{tok, out, out_sb, ncols, step, pos, lens, ctr, rng};
   return sample_launch(logits, is_bf16, seen, B, V, temperature, inv_temperature, penalty, top_k, top_p, do_sample,
                        rng, out_tok, workspace, adv, st);
+}
+
+// ---------------------------------------------------------------- vocab-sharded LM head
+// A pipeline whose LM head is split by vocabulary over its ranks (parallel/vocab_head.py): every
+// rank runs phase 1 on its shard [v0, v0 + Vs) (global ids in the composites and the noise), the
+// candidate lists travel to one rank, and phase 2 merges the concatenated lists [B][C_total] —
+// the same two kernels as one unsplit row, so the token is the one the unsplit sampler draws.
+// mode: 0 greedy, 1 full-vocab sampling, 2 top-k (<= CCAP) (+ top-p); -5: not shardable.
+static int shard_mode(int do_sample, float temperature, int top_k, float top_p, int V) {
+  if (!do_sample || temperature <= 0.f) return 0;
+  if ((top_k <= 0 || top_k >= V) && top_p >= 1.f) return 1;
+  if (top_k > 0 && top_k <= CCAP && top_k < V) return 2;
+  return -5;
+}
+
+extern "C" int edge_sample_shard_mode(int do_sample, float temperature, int top_k, float top_p, int V) {
+  return shard_mode(do_sample, temperature, top_k, top_p, V);
+}
+
+// Chunks of a shard of Vs scores (phase-1 chunk width for a V-wide row).
+extern "C" int edge_sample_shard_chunks(int Vs, int V) {
+  const int ch = NT * chunk_ept(V);
+  return (Vs + ch - 1) / ch;
+}
+
+// Phase 1 over one shard: pc [B][C][CCAP] + pthr [B][C] (mode 2) or pc [B][C] (modes 0 / 1).
+extern "C" int edge_sample_shard(const void* logits, int is_bf16, const uint8_t* seen, int B, int Vs, int v0, int V,
+                                 float temperature, float inv_temperature, float penalty, int top_k, float top_p,
+                                 int do_sample, const int* rng, uint64_t* pc, uint32_t* pthr, hipStream_t st) {
+  const int mode = shard_mode(do_sample, temperature, top_k, top_p, V);
+  if (mode < 0) return mode;
+  if (B == 0) return 0;
+  const float inv_t = mode == 0 ? 1.f : inv_temperature;
+  const int ept = chunk_ept(V);
+  const int C = (Vs + NT * ept - 1) / (NT * ept);
+  const dim3 g1(C, B);
+  const int vec = g_sample_vec && Vs % 8 == 0 && reinterpret_cast<uintptr_t>(logits) % 16 == 0 &&
+                  (seen == nullptr || reinterpret_cast<uintptr_t>(seen) % 8 == 0);
+  if (mode == 2) {
+#define TC(BF, E) hipLaunchKernelGGL((topk_chunk_kernel<BF, E>), g1, dim3(NT), 0, st, logits, seen, Vs, C, inv_t, \
+                                     penalty, top_k, pc, pthr, vec, v0)
+    if (is_bf16) { if (ept == 8) TC(true, 8); else TC(true, 16); }
+    else { if (ept == 8) TC(false, 8); else TC(false, 16); }
+#undef TC
+  } else {
+#define AC(BF, MD) do { if (ept == 8) hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 8>), g1, dim3(NT), 0, st, logits, \
+                                                        seen, Vs, C, inv_t, penalty, rng, pc, vec, v0); \
+                           else hipLaunchKernelGGL((argmax_chunk_kernel<BF, MD, 16>), g1, dim3(NT), 0, st, logits, seen, \
+                                                   Vs, C, inv_t, penalty, rng, pc, vec, v0); } while (0)
+    if (is_bf16) { if (mode == 0) AC(true, 0); else AC(true, 1); }
+    else { if (mode == 0) AC(false, 0); else AC(false, 1); }
+#undef AC
+  }
+  return (int)hipGetLastError();
+}
+
+// Phase 2 over the concatenated shard lists (C chunks per row in total) -> out_tok [B].  No `seen`
+// update here: each rank marks the sampled ids of its own shard.
+extern "C" int edge_sample_merge(const uint64_t* pc, const uint32_t* pthr, int B, int C, int V, float temperature,
+                                 int top_k, float top_p, int do_sample, const int* rng, int64_t* out_tok,
+                                 hipStream_t st) {
+  const int mode = shard_mode(do_sample, temperature, top_k, top_p, V);
+  if (mode < 0) return mode;
+  if (B == 0) return 0;
+  const Adv none{};
+  if (mode == 2)
+    hipLaunchKernelGGL(topk_merge_kernel, dim3(B), dim3(NT), 0, st, pc, pthr, C, V, top_k, top_p, rng, nullptr,
+                       out_tok, none);
+  else
+    hipLaunchKernelGGL(argmax_merge_kernel, dim3(B), dim3(64), 0, st, pc, C, V, nullptr, out_tok, none);
+  return (int)hipGetLastError();
 }
