@@ -87,6 +87,10 @@ def parse(argv=None):
     ap.add_argument("--pp-slack", type=int, default=0,
                     help="N > 1: extra ticks per stage hop (1 = 2N micro-batches in flight, every RCCL hop "
                          "overlapped with a tick of compute; doubles the per-token latency)")
+    ap.add_argument("--pp-vocab-split", default="on", choices=["on", "off"],
+                    help="N > 1: split the LM head by vocabulary over every rank (each rank its logits slice + "
+                         "sampler phase 1, rank 0 the merge) instead of the whole head on the last stage; one "
+                         "more micro-batch group in flight (parallel/vocab_head.py)")
     ap.add_argument("--latency-point", default="auto", choices=["auto", "off", "int8", "both"],
                     help="also report batch-1 p50 per-token latency (single GPU): int8 = the benchmark model at "
                          "micro-batch 1, both = plus a bf16 copy of the model (13.5 GB more, built for this only); "
@@ -375,6 +379,7 @@ def main(argv=None):
                                 else "bf16"),
                    "compute": ("W8A8 INT8 MFMA GEMMs, bf16 norms / softmax, "
                                + ("W8A8 int8 LM head" if args.lm_head == "int8" else "bf16 LM head")
+                               + (f" split by vocabulary over {args.gpus} ranks" if res.get("vocab_split") else "")
                                if args.quant != "none" else "bf16 GEMMs / attention / norms")},
         "p50_token_latency_ms": round(res["p50"], 4),
         "p90_token_latency_ms": round(res.get("p90", res["p50"]), 4),
@@ -398,7 +403,7 @@ def main(argv=None):
     if "per_rank" in res:
         out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
         out["per_rank"] = res["per_rank"]
-        for k in ("stage_cost_model_us", "stage_cost_spread", "slack", "host_issue_us_per_tick_max"):
+        for k in ("stage_cost_model_us", "stage_cost_spread", "slack", "host_issue_us_per_tick_max", "vocab_split"):
             if k in res:
                 out[k] = res[k]
     print(json.dumps(out), flush=True)

@@ -359,15 +359,20 @@ class DecoderLM(nn.Module):
 
     def head(self, x: torch.Tensor, residual: Optional[torch.Tensor], ctx: AttnCtx,
              logits: str = "last") -> torch.Tensor:
-        """Final norm + LM head. logits: "last" (one row per sequence) or "all"."""
-        if isinstance(x, PartialSum) and logits == "last" and ctx.T > 1:
+        """Final norm + LM head. logits: "last" (one row per sequence) or "all"; "hidden": the
+        final-normed last rows only, for an LM head split by vocabulary over pipeline ranks
+        (parallel/vocab_head.py)."""
+        last = logits in ("last", "hidden")
+        if isinstance(x, PartialSum) and last and ctx.T > 1:
             x = x.materialize()
-        if logits == "last" and ctx.T > 1:
+        if last and ctx.T > 1:
             idx = ctx.last_rows(x.device)
             x = x.index_select(0, idx)
             residual = residual.index_select(0, idx) if residual is not None else None
-        qh = getattr(self.lm_head, "takes_quantized_input", False)     # int8 LM head (quant.quantize_head)
+        qh = getattr(self.lm_head, "takes_quantized_input", False) and logits != "hidden"   # int8 LM head
         h, _ = self.final_norm(x, residual, quant=qh)
+        if logits == "hidden":
+            return h
         return self.lm_head(h) if self.lm_head is not None else self._tied_head(h)
 
     def _tied_head(self, h: torch.Tensor) -> torch.Tensor:
@@ -415,6 +420,16 @@ def init_random_(model: DecoderLM, seed: int = 0, std: float = 0.02) -> DecoderL
             g = torch.Generator(device=p.device).manual_seed((seed * 1000003 + zlib.crc32(name.encode())) % (2 ** 63))
             p.copy_(torch.randn(p.shape, generator=g, device=p.device, dtype=torch.float32).mul_(std).to(p.dtype))
     return model
+
+
+def random_head_weight(cfg: ModelConfig, seed: int = 0, dtype=torch.bfloat16, device=None,
+                       std: float = 0.02) -> torch.Tensor:
+    """The LM-head weight [V, H] ``init_random_`` gives a model holding the head (the embedding of a
+    tied model), built on a rank that holds no head (a vocab shard of it, parallel/vocab_head.py)."""
+    name = "embed" if cfg.tie_word_embeddings else "lm_head.weight"
+    g = torch.Generator(device=device).manual_seed((seed * 1000003 + zlib.crc32(name.encode())) % (2 ** 63))
+    return torch.randn((cfg.vocab_size, cfg.hidden_size), generator=g, device=device,
+                       dtype=torch.float32).mul_(std).to(dtype)
 
 
 def global_named_parameters(model: DecoderLM):

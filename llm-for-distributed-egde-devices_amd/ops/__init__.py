@@ -501,6 +501,105 @@ def sample(logits, seen, temperature, top_k, top_p, repetition_penalty, rng: tor
     return tok
 
 
+# --------------------------------------------------------------------------- vocab-sharded sampling
+SHARD_CCAP = 128          # candidates per chunk list (sampler.hip CCAP): top-k shards up to this k
+
+
+def shard_mode(temperature, top_k, top_p, V: int, do_sample: bool = True) -> int:
+    """Sampler mode of a vocab-sharded head: 0 greedy, 1 full-vocab sampling, 2 top-k (<= 128)
+    (+ top-p); -1 when the configuration does not shard (top-p without top-k, top-k > 128)."""
+    tk = int(top_k or 0)
+    tp = float(top_p if top_p is not None else 1.0)
+    if not do_sample or temperature <= 0:
+        return 0
+    if (tk <= 0 or tk >= V) and tp >= 1.0:
+        return 1
+    if 0 < tk <= SHARD_CCAP and tk < V:
+        return 2
+    return -1
+
+
+def shard_candidate_shapes(B: int, Vs: int, V: int, mode: int, device) -> list:
+    """(shape, dtype) of the tensors ``sample_shard`` returns for a shard of Vs columns — the
+    receive buffers of the rank that merges."""
+    if torch.device(device).type == "cuda" and not _REF_ON_GPU:
+        C = int(ext().sample_shard_chunks(Vs, V))
+        if mode == 2:
+            return [((B, C * SHARD_CCAP), torch.long), ((B, C), torch.int32)]
+        return [((B, C), torch.long)]
+    k = min(SHARD_CCAP, Vs) if mode == 2 else 1
+    return [((B, k), torch.float32), ((B, k), torch.long)]
+
+
+def sample_shard(logits, seen, temperature, top_k, top_p, repetition_penalty, rng, v0: int, V: int,
+                 do_sample: bool = True):
+    """Sampler phase 1 over a vocab shard: ``logits`` [B, Vs] are columns [v0, v0 + Vs) of the
+    V-wide rows, ``seen`` the shard's repetition-penalty flags.  Returns the shard's candidate
+    tensors (``shard_candidate_shapes``) for ``sample_merge``; the ids in them are global, so the
+    merged token is exactly the unsplit sampler's (same processing, same counter-based noise)."""
+    mode = shard_mode(temperature, top_k, top_p, V, do_sample)
+    assert mode >= 0, "sampling configuration does not shard over the vocabulary"
+    if _gpu(logits):
+        r = ext().sample_shard(_logits32(logits), seen, float(temperature), int(top_k or 0),
+                               float(top_p if top_p is not None else 1.0), float(repetition_penalty),
+                               bool(do_sample), rng, int(v0), int(V))
+        return tuple(r) if mode == 2 else (r[0],)
+    s = logits.float()
+    if seen is not None and repetition_penalty != 1.0:     # the processor order of _ref.process_logits
+        m = seen.bool()
+        s = torch.where(m, torch.where(s < 0, s * repetition_penalty, s / repetition_penalty), s)
+    B, Vs = s.shape
+    ids = torch.arange(v0, v0 + Vs, device=s.device).expand(B, Vs)
+    if mode >= 1 and temperature != 1.0:
+        s = s * (1.0 / temperature)
+    if mode == 1:
+        import numpy as np
+        seed, step = (int(v) for v in rng.tolist())
+        rows = np.arange(B, dtype=np.uint32)[:, None]
+        u = _ref.uniform_hash(seed, rows, step, np.arange(v0, v0 + Vs, dtype=np.uint32)[None, :]).astype(np.float32)
+        s = s + torch.from_numpy(-np.log(-np.log(u))).to(s.device)
+    if mode <= 1:                                          # best (value, then lower id): argmax = first max
+        i = s.argmax(-1, keepdim=True)
+        return s.gather(1, i), ids.gather(1, i)
+    vals, idx = torch.topk(s, min(SHARD_CCAP, Vs), dim=-1)
+    kth = vals[:, min(int(top_k), Vs) - 1:min(int(top_k), Vs)]
+    return vals.masked_fill(vals < kth, float("-inf")), ids.gather(1, idx)
+
+
+def sample_merge(shards, V: int, temperature, top_k, top_p, rng, do_sample: bool = True):
+    """Sampler phase 2 over every shard's candidates (``sample_shard`` outputs, in shard order)
+    -> tokens [B] (int64): the token the unsplit sampler draws from the whole row."""
+    mode = shard_mode(temperature, top_k, top_p, V, do_sample)
+    first = shards[0][0]
+    if _gpu(first):
+        pc = torch.cat([s[0] for s in shards], 1)
+        pthr = torch.cat([s[1] for s in shards], 1) if mode == 2 else torch.empty(0, dtype=torch.int32,
+                                                                                   device=first.device)
+        return ext().sample_merge(pc, pthr, int(V), float(temperature), int(top_k or 0),
+                                  float(top_p if top_p is not None else 1.0), bool(do_sample), rng)
+    vals = torch.cat([s[0] for s in shards], 1)
+    ids = torch.cat([s[1] for s in shards], 1)
+    if mode <= 1:
+        best = vals.amax(1, keepdim=True)
+        big = torch.full_like(ids, torch.iinfo(torch.long).max)
+        return torch.where(vals == best, ids, big).amin(1)
+    full = torch.full((vals.shape[0], V), float("-inf"), device=vals.device)
+    full.scatter_(1, ids, vals)
+    seed, step = (int(v) for v in rng.tolist())
+    # the shards applied penalty and temperature: the remaining processors are top-k / top-p
+    return _ref.sample(full, None, 1.0, top_k, top_p, 1.0, seed, step, True)
+
+
+def seen_mark(seen, tok, v0: int) -> None:
+    """Set the repetition-penalty flag of each row's token in a vocab shard's ``seen`` [B, Vs]
+    (tokens outside [v0, v0 + Vs) leave the row unchanged; graph-capturable)."""
+    Vs = seen.shape[1]
+    j = tok.view(-1, 1) - v0
+    inr = (j >= 0) & (j < Vs)
+    jc = j.clamp(0, Vs - 1)
+    seen.scatter_(1, jc, seen.gather(1, jc) | inr.to(seen.dtype))
+
+
 def decode_advance(nxt, tok, out, step, pos, seq_lens, rng, inc=None) -> None:
     """Decode-step bookkeeping after sampling: tok = nxt, out[:, step] = nxt, pos += inc,
     seq_lens += inc (``inc``: int32 [B] per-row increments, default 1), rng[1] += 1, step += 1 —

@@ -64,21 +64,32 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     hcl = (0.35 if getattr(args, "lm_head", "bf16") == "int8" else 0.52) if args.quant != "none" else 0.4
     L = max(1, getattr(args, "lanes", 1))
     slack = max(0, int(getattr(args, "pp_slack", 0)))
-    # micro-batch groups in flight: P (one per stage), or D (P - 1) + 2 with D = 1 + slack ticks per hop
-    n_groups = world if slack == 0 or world == 1 else (1 + slack) * (world - 1) + 2
+    # LM head split by vocabulary over the ranks (bf16 head; the bench's sampling shards)
+    vs = (world > 1 and getattr(args, "pp_vocab_split", "off") == "on" and getattr(args, "lm_head", "bf16") != "int8")
+    # micro-batch groups in flight: P (one per stage), or D (P - 1) + 2 with D = 1 + slack ticks per hop;
+    # the vocab split D (P + 1) (the token reaches rank 0 two hops later)
+    if vs:
+        n_groups = (1 + slack) * (world + 1)
+    else:
+        n_groups = world if slack == 0 or world == 1 else (1 + slack) * (world - 1) + 2
     M, P, b, T = n_groups * L, world, args.micro_batch, args.prompt_len
     kvb = 1.0 if kv_dtype is not None and kv_dtype(args, cfg) == "int8" else 2.0
     unit_kw = dict(rows=b, ctx=T + args.warmup + (args.steps + 1) // 2, weight_bytes=wbytes, kv_bytes=kvb,
                    head_bytes=1.0 if getattr(args, "lm_head", "bf16") == "int8" else 2.0)
     if args.partition == "units" and not explicit:
-        ubounds = partition_units(cfg, world, **unit_kw)
+        ubounds = partition_units(cfg, world, head_split=vs, **unit_kw)
     else:
         bounds = partition_model(cfg, world, "uniform" if args.partition == "uniform" else "balanced",
                                  weight_bytes=wbytes, explicit=explicit, head_cost_layers=hcl)
         ubounds = [2 * x for x in bounds]
-    ucost = unit_stage_costs(cfg, ubounds, **unit_kw)
+    ucost = unit_stage_costs(cfg, ubounds, head_split=vs, **unit_kw)
     wd.beat("build")
     _, model = build(args, device, units=(ubounds[rank], ubounds[rank + 1]))
+    shard = None
+    if vs:
+        from .vocab_head import build_head_shard
+        shard = build_head_shard(cfg, rank, world, model=model, seed=args.seed, dtype=torch.bfloat16, device=device,
+                                 checkpoint=getattr(args, "checkpoint", None))
     W, K = args.warmup, args.steps
     S = W + K + 1
     g = torch.Generator().manual_seed(args.seed)
@@ -87,7 +98,8 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     # the stage's constructor joins every rank in one collective (eager RCCL communicator)
     stage = PipelineStage(model, rank, world, b, M, max_seq=T + S + 8, use_graphs=not args.no_graphs,
                           headinfer_heads=getattr(args, "headinfer_heads", None), lanes=L,
-                          kv_dtype=kv_dtype(args, cfg) if kv_dtype is not None else "bf16", slack=slack)
+                          kv_dtype=kv_dtype(args, cfg) if kv_dtype is not None else "bf16", slack=slack,
+                          vocab_split=vs, head_shard=shard)
     if use_cuda:
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats(device)
@@ -97,7 +109,7 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
     t_b = t_a + K * M // L
     # prefill window: tick 0 to the first tick after every prefill group left the last stage
     # (synchronised like the timed window; it ends before the warm-up decodes are timed)
-    t_p = M // L + D * (P - 1)
+    t_p = M // L + D * (P + 1 if vs else P - 1)
     marks = {}
     stamps = []
 
@@ -153,7 +165,7 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
                    mem_gb=float(mem.item()), partition=[u / 2 for u in ubounds], world_size=world, per_rank=per_rank,
                    stage_cost_model_us=[round(c, 1) for c in ucost],
                    stage_cost_spread=round(max(ucost) / (sum(ucost) / len(ucost)), 4), slack=slack,
-                   micro_batches_in_flight=M,
+                   micro_batches_in_flight=M, vocab_split=vs,
                    bubble_frac_max=max(d.get("bubble_frac", 0.0) for d in per_rank),
                    host_issue_us_per_tick_max=max((d.get("host_issue_us_per_tick", 0.0) for d in per_rank),
                                                   default=0.0),

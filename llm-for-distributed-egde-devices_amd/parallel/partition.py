@@ -27,8 +27,9 @@ def layer_costs(cfg: ModelConfig, weight_bytes: float = 1.0, head_bytes: float =
 
 
 def balanced_partition(costs: Sequence[float], stages: int, head_cost: float = 0.0,
-                       embed_cost: float = 0.0) -> List[int]:
-    """Boundaries b[0]=0 < b[1] < ... < b[P]=L minimising max stage cost."""
+                       embed_cost: float = 0.0, stage_extra: Optional[Sequence[float]] = None) -> List[int]:
+    """Boundaries b[0]=0 < b[1] < ... < b[P]=L minimising max stage cost (``stage_extra[s]``: a
+    fixed cost of stage s on top of its layers, e.g. its share of a vocab-split LM head)."""
     L = len(costs)
     assert 1 <= stages <= L, "need at least one layer per stage"
     pre = [0.0]
@@ -41,6 +42,8 @@ def balanced_partition(costs: Sequence[float], stages: int, head_cost: float = 0
             c += embed_cost
         if s == stages - 1:
             c += head_cost
+        if stage_extra is not None:
+            c += stage_extra[s]
         return c
 
     INF = float("inf")
@@ -72,6 +75,12 @@ ATTN_BYTES_PER_US = 5.9e6
 HALF_FIXED_US = 8.0
 HEAD_BYTES_PER_US = 3.2e6
 HEAD_FIXED_US = 35.0
+# vocab-split head (parallel/vocab_head.py): per stage its rows of the head GEMM + the sampler's
+# phase 1 over them + the penalty-flag update; rank 0 the merge (phase 2 + bookkeeping); the last
+# stage the final norm
+SHARD_FIXED_US = 12.0
+MERGE_US = 10.0
+FINAL_NORM_US = 4.0
 
 
 def decode_unit_costs(cfg: ModelConfig, rows: int = 256, ctx: int = 160, weight_bytes: float = 1.0,
@@ -91,23 +100,40 @@ def decode_unit_costs(cfg: ModelConfig, rows: int = 256, ctx: int = 160, weight_
     return [attn, mlp] * cfg.num_layers, head
 
 
+def head_split_extra(cfg: ModelConfig, stages: int, head_bytes: float = 2.0) -> List[float]:
+    """Per-stage cost (us) of an LM head split by vocabulary over ``stages`` ranks."""
+    shard = cfg.hidden_size * cfg.vocab_size * head_bytes / stages / HEAD_BYTES_PER_US + SHARD_FIXED_US
+    extra = [shard] * stages
+    extra[0] += MERGE_US
+    extra[-1] += FINAL_NORM_US
+    return extra
+
+
 def partition_units(cfg: ModelConfig, stages: int, rows: int = 256, ctx: int = 160, weight_bytes: float = 1.0,
-                    kv_bytes: float = 2.0, head_bytes: float = 2.0) -> List[int]:
+                    kv_bytes: float = 2.0, head_bytes: float = 2.0, head_split: bool = False) -> List[int]:
     """Balanced stage boundaries in half-layer units (``DecoderLM.from_units``): a boundary may fall
     between a layer's attention and MLP halves.  Sequential-residual models only; parallel-residual
-    ones (Phi-2, Pythia) get whole-layer boundaries (their units in pairs)."""
+    ones (Phi-2, Pythia) get whole-layer boundaries (their units in pairs).  ``head_split``: the LM
+    head is split by vocabulary over every stage (``head_split_extra``) instead of sitting on the last."""
     costs, head = decode_unit_costs(cfg, rows, ctx, weight_bytes, kv_bytes, head_bytes)
+    extra = head_split_extra(cfg, stages, head_bytes) if head_split and stages > 1 else None
+    head = 0.0 if extra is not None else head
     if cfg.parallel_residual:
         layer = [costs[2 * i] + costs[2 * i + 1] for i in range(cfg.num_layers)]
-        return [2 * b for b in balanced_partition(layer, stages, head)]
-    return balanced_partition(costs, stages, head)
+        return [2 * b for b in balanced_partition(layer, stages, head, stage_extra=extra)]
+    return balanced_partition(costs, stages, head, stage_extra=extra)
 
 
-def unit_stage_costs(cfg: ModelConfig, bounds: Sequence[int], **kw) -> List[float]:
+def unit_stage_costs(cfg: ModelConfig, bounds: Sequence[int], head_split: bool = False, **kw) -> List[float]:
     """Modelled per-stage cost (us) of unit bounds (``partition_units``)."""
     costs, head = decode_unit_costs(cfg, **kw)
-    out = [sum(costs[bounds[s]:bounds[s + 1]]) for s in range(len(bounds) - 1)]
-    out[-1] += head
+    P = len(bounds) - 1
+    out = [sum(costs[bounds[s]:bounds[s + 1]]) for s in range(P)]
+    if head_split and P > 1:
+        for s, e in enumerate(head_split_extra(cfg, P, kw.get("head_bytes", 2.0))):
+            out[s] += e
+    else:
+        out[-1] += head
     return out
 
 

@@ -61,7 +61,8 @@ class PipelineStage:
     def __init__(self, model: DecoderLM, rank: int, world: int, micro_batch: int, n_micro: int, max_seq: int,
                  group=None, use_graphs: Optional[bool] = None, headinfer_heads: Optional[int] = None,
                  lanes: int = 1, prefill_chunk: int = 4096, warm_comm: bool = True, kv_dtype: str = "bf16",
-                 ranks: Optional[Sequence[int]] = None, slack: int = 0):
+                 ranks: Optional[Sequence[int]] = None, slack: int = 0, vocab_split: bool = False,
+                 head_shard=None):
         """``headinfer_heads``: keep only this many KV heads per layer on the GPU and offload the rest
         to pinned host memory (edgellm.offload.HeadInferKV; BASELINE config "8-way pipeline +
         HeadInfer").  The offloaded path is host-orchestrated on one compute stream, so it runs one
@@ -70,7 +71,14 @@ class PipelineStage:
 
         ``rank`` / ``world`` are the stage index and stage count within ``group``; ``ranks`` maps
         stage index -> global rank (default identity: the stages are ranks 0..world-1), so a model
-        can be pipelined over any rank subset (one ``dist.new_group`` per ensemble agent)."""
+        can be pipelined over any rank subset (one ``dist.new_group`` per ensemble agent).
+
+        ``vocab_split`` (world > 1): the LM head is split by vocabulary over every rank
+        (parallel/vocab_head.py; ``head_shard`` = this rank's rows): the last stage hands its
+        final-normed hidden rows to every rank, each rank runs its logits slice + sampler phase 1,
+        rank 0 merges (phase 2), owns the sampled tokens and sends them to the other ranks for their
+        repetition-penalty flags.  Needs D (P + 1) micro-batch groups in flight (D = 1 + slack); runs
+        whenever the sampling configuration shards (ops.shard_mode), else the last stage samples."""
         assert lanes >= 1 and n_micro % lanes == 0, "micro-batches must split evenly over lanes"
         assert n_micro >= world * lanes, "need lanes x stages micro-batches to keep the ring full"
         offload = headinfer_heads is not None and headinfer_heads < model.cfg.num_kv_heads
@@ -127,6 +135,15 @@ class PipelineStage:
         if (self.streams is not None and dist.is_initialized() and world > 1
                 and os.environ.get("EDGELLM_LANE_GROUPS", "1") != "0"):
             self.lane_groups = [dist.new_group(self.granks, use_local_synchronization=True) for _ in range(lanes)]
+        self.vs_req = bool(vocab_split) and world > 1
+        self.shard = head_shard
+        self.vs = False                               # per run: vocab split active
+        if self.vs_req:
+            from .vocab_head import shard_bounds
+            assert head_shard is not None, "vocab_split needs this rank's head shard"
+            self.vs_bounds = shard_bounds(self.cfg.vocab_size, world)
+            assert (head_shard.v0, head_shard.v1) == (self.vs_bounds[rank], self.vs_bounds[rank + 1]), \
+                "head shard rows do not match vocab_head.shard_bounds"
         if warm_comm and dist.is_initialized() and world > 1:
             self.warm_communicator()
 
@@ -245,7 +262,7 @@ class PipelineStage:
             x_h = None
             if hidden is not None:
                 x_h = hidden.view(b, T, H)[:, c0:c1].contiguous().view(b * (c1 - c0), H) if C < T else hidden
-            out = self.model(x_ids, ctx, hidden=x_h, logits="last")
+            out = self.model(x_ids, ctx, hidden=x_h, logits="hidden" if self.vs else "last")
             if not self.is_last and C < T:
                 outs.append(out.view(b, c1 - c0, H))
         if outs:
@@ -263,7 +280,13 @@ class PipelineStage:
         ctx = AttnCtx("decode", b, 1, self.pos[m], self.lens[m], max_len, self._rows(m), self.rope,
                       attn_hook=self.attn_hook)
         out = self.model(self.tok[m].view(b, 1) if self.is_first else None, ctx,
-                         hidden=None if self.is_first else self.hin[m])
+                         hidden=None if self.is_first else self.hin[m],
+                         logits="hidden" if self.vs else "last")
+        if self.is_last and self.vs:                  # vocab split: the final-normed rows go to every rank
+            self.hfin[m].copy_(out)
+            self.pos[m].add_(1)
+            self.lens[m].add_(1)
+            return
         if self.is_last:                              # sampler + bookkeeping (pos / lens += 1 included)
             sp = self.sampling
             nxt = ops.sample_advance(out, self.seen[m], sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty,
@@ -286,6 +309,35 @@ class PipelineStage:
         self.step[m].add_(1)
         if self._eos is not None:                     # device-side EOS flags (graph-capturable)
             self.hit[m].logical_or_(nxt.eq(self._eos))
+
+    # ------------------------------------------------------------------ vocab-split head
+    def _vs_shard(self, m: int):
+        """This rank's logits slice + sampler phase 1 for micro-batch m (rows in hfin[m])."""
+        self.cand[m] = self.shard.candidates(self.hfin[m], self.seen[m], self.sampling, self.rng[m])
+        if not self.is_first:
+            self.rng[m][1:].add_(1)                   # rank 0 advances after its merge (same step)
+
+    def _vs_merge(self, m: int):
+        """Rank 0: phase 2 over every shard's candidates -> the token of each row of m."""
+        sp = self.sampling
+        nxt = ops.sample_merge([self.cand.pop(m)] + self.cand_in[m], self.cfg.vocab_size, sp.temperature, sp.top_k,
+                               sp.top_p, self.rng[m], sp.do_sample)
+        self.tok[m].copy_(nxt)
+        self.out[m].scatter_(1, self.step[m].view(1, 1).expand(self.b, 1), nxt.view(self.b, 1))
+        self.rng[m][1:].add_(1)
+        self.step[m].add_(1)
+        ops.seen_mark(self.seen[m], nxt, self.shard.v0)
+        if self._eos is not None:
+            self.hit[m].logical_or_(nxt.eq(self._eos))
+
+    def _vs_seen_init(self, ids: torch.Tensor, m: int):
+        """Mark prompt ids [b, T] that fall in this rank's vocab shard (pads already replaced)."""
+        Vs, v0 = self.shard.Vs, self.shard.v0
+        j = ids.to(self.device) - v0
+        j = torch.where((j >= 0) & (j < Vs), j, torch.full_like(j, Vs))
+        tmp = torch.zeros(self.b, Vs + 1, dtype=torch.uint8, device=self.device)
+        tmp.scatter_(1, j, 1)
+        self.seen[m].bitwise_or_(tmp[:, :Vs])
 
     def _bucket(self, max_len: int) -> int:
         return min(self.max_seq, ((max_len + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
@@ -353,9 +405,15 @@ class PipelineStage:
             assert int(pl.max()) <= T and int(pl.min()) >= 1
             if int(pl.min()) < T:
                 self._plen = [pl[m].clone() for m in range(M)]
+        # vocab-split head for this run (when the sampling configuration shards); the sampling rank
+        # owns the tokens: rank 0 under the split (it merges), else the last stage
+        self.vs = self.vs_req and ops.shard_mode(sampling.temperature, sampling.top_k, sampling.top_p, V,
+                                                 sampling.do_sample) >= 0
+        samp = self.is_first if self.vs else self.is_last
+        self._samp = samp
         self._eos = (torch.tensor(int(eos_token_id), dtype=torch.long, device=dev)
-                     if eos_token_id is not None and self.is_last else None)
-        if self.is_last:
+                     if eos_token_id is not None and samp else None)
+        if samp:
             self.hit = [torch.zeros(b, dtype=torch.bool, device=dev) for _ in range(M)]
         if self.h_on is not None:
             self._build_offload_kv(T)
@@ -366,16 +424,45 @@ class PipelineStage:
         self._graphs.clear()
         self._pools.clear()
         self._final_bucket = self._bucket(T + S + 1)
-        if self.is_last:
-            self.seen = [torch.zeros(b, V, dtype=torch.uint8, device=dev) for _ in range(M)]
+        if self.vs or self.is_last:
+            Vs = self.shard.Vs if self.vs else V
+            self.seen = [torch.zeros(b, Vs, dtype=torch.uint8, device=dev) for _ in range(M)]
             self.rng = [torch.tensor([(seed + 7919 * m) & 0x7FFFFFFF, 0], dtype=torch.int32, device=dev)
                         for m in range(M)]
+        if samp:
             self.step = [torch.zeros(1, dtype=torch.long, device=dev) for _ in range(M)]
-            self.ctr = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(M)]   # sampler counters
             self.out = [torch.zeros(b, S + 1, dtype=torch.long, device=dev) for _ in range(M)]
-        # repetition-penalty history needs the prompt ids on the last stage
+        if self.is_last and not self.vs:
+            self.ctr = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(M)]   # sampler counters
+        if self.vs:
+            H = self.cfg.hidden_size
+            mode = ops.shard_mode(sampling.temperature, sampling.top_k, sampling.top_p, V, sampling.do_sample)
+            self.hfin = [torch.zeros(b, H, dtype=self.model.dtype, device=dev) for _ in range(M)]
+            self.cand: Dict[int, tuple] = {}
+            if self.is_first:                        # receive buffers for the other ranks' candidates
+                vb = self.vs_bounds
+                self.cand_in = [[tuple(torch.empty(shp, dtype=dt, device=dev) for shp, dt in
+                                       ops.shard_candidate_shapes(b, vb[r + 1] - vb[r], V, mode, dev))
+                                 for r in range(1, P)] for _ in range(M)]
+            else:
+                self.tokin = [torch.zeros(b, dtype=torch.long, device=dev) for _ in range(M)]
+        # repetition-penalty history needs the prompt ids on the sampling rank(s)
         pdev = "cpu" if self.host_staged else dev
-        if self.is_last:
+        if self.vs:
+            if self.is_first:
+                stacked = torch.stack([p.to(pdev) for p in prompts])
+                for r in range(1, P):
+                    self._send_one(stacked, r)
+            else:
+                stacked = torch.zeros(M, b, T, dtype=torch.long, device=pdev)
+                self._recv_one(stacked, 0)
+            for m in range(M):
+                ids = stacked[m].to(dev)
+                if self._plen is not None:              # pads repeat the row's first token
+                    pos = torch.arange(T, device=dev)[None, :]
+                    ids = torch.where(pos < self._plen[m][:, None], ids, ids[:, :1])
+                self._vs_seen_init(ids, m)
+        elif self.is_last:
             if self.is_first or (prompts is not None and prompt_lens is not None):
                 for m in range(M):
                     ids = prompts[m].to(dev)
@@ -411,6 +498,11 @@ class PipelineStage:
         D = 1 + self.slack
         assert D == 1 or M // L >= D * (P - 1) + 2 or P == 1, \
             f"slack {self.slack} needs >= {D * (P - 1) + 2} micro-batch groups in flight, have {M // L}"
+        # vocab split: group g's hidden leaves the last stage at tick g + D(P-1), every rank runs its
+        # head shard at g + DP, rank 0 merges at g + D(P+1) and feeds the token to the group's next
+        # step, which starts there at g + M/L
+        assert not self.vs or M // L >= D * (P + 1), \
+            f"vocab split needs >= {D * (P + 1)} micro-batch groups in flight, have {M // L}"
         n_groups = n_items // L
         cur_stream = torch.cuda.current_stream(dev) if self.cuda else None
         R = D * self.rank                               # this rank's tick offset
@@ -435,13 +527,14 @@ class PipelineStage:
                 store[t] = time.perf_counter()
 
         t_start = time.perf_counter()
-        n_ticks = n_groups + D * (P - 1)
+        n_ticks = n_groups + D * (P + 1 if self.vs else P - 1)
         # EOS agreement: from the tick after which the last stage has sampled every micro-batch's
         # first token, once per eos_every decode rounds (M / L ticks per round)
         eos_on = eos_token_id is not None and (P == 1 or dist.is_initialized())
-        eos_from, eos_period = (M // L) + D * (P - 1), max(1, eos_every) * max(1, M // L)
+        eos_from, eos_period = (M // L) + D * (P + 1 if self.vs else P - 1), max(1, eos_every) * max(1, M // L)
         stopped_at = None
-        t_first = D * (P - 1) if self.is_last else -1   # tick whose prefill samples the first token
+        # tick whose prefill samples the first token (vocab split: rank 0's first merge)
+        t_first = (D * (P + 1) if self.is_first else -1) if self.vs else (D * (P - 1) if self.is_last else -1)
         ev_first: Dict[int, object] = {}
         mark(ev_first, -1)
         due: Dict[int, object] = {}         # tick -> posted exchange whose receives it computes on
@@ -463,6 +556,8 @@ class PipelineStage:
                 for prv in (prv_g * L + l for l in lanes):
                     if not self.is_last:
                         sends.append((pre_out[prv] if prv < M else self.hout[(prv - M) % M], self.next))
+                    elif self.vs:                       # final-normed rows to every other rank's head shard
+                        sends.extend((self.hfin[prv % M], r) for r in range(P - 1))
                     elif feeds_back(prv):
                         sends.append((self.tok[prv % M], 0))
             if not self.is_first and group_valid(rcv_g):
@@ -472,12 +567,29 @@ class PipelineStage:
                         recvs.append((pre_in[cur], self.prev))
                     else:
                         recvs.append((self.hin[(cur - M) % M], self.prev))
-            if self.is_first:
+            if self.is_first and not self.vs:
                 prod_g = t - 1 - D * (P - 1)    # group the last stage finished at tick t - 1
                 if group_valid(prod_g):
                     for prod in (prod_g * L + l for l in lanes):
                         if feeds_back(prod):
                             recvs.append((self.tok[prod % M], P - 1))
+            if self.vs:                # (after the hand-offs: P2P ops of a rank pair match in posting order)
+                hg, cg, mg = t - 1 - D * (P - 1), t - 1 - D * P, t - 1 - D * (P + 1)
+                if not self.is_last and group_valid(hg):
+                    recvs.extend((self.hfin[i % M], P - 1) for i in (hg * L + l for l in lanes))
+                if group_valid(cg):
+                    for i in (cg * L + l for l in lanes):
+                        if self.is_first:
+                            recvs.extend((x, r + 1) for r, c in enumerate(self.cand_in[i % M]) for x in c)
+                        else:
+                            sends.extend((x, 0) for x in self.cand.pop(i % M))
+                if group_valid(mg):
+                    for i in (mg * L + l for l in lanes):
+                        if feeds_back(i):
+                            if self.is_first:
+                                sends.extend((self.tok[i % M], r) for r in range(1, P))
+                            else:
+                                recvs.append((self.tokin[i % M], 0))
             return sends, recvs
 
         def post(t):
@@ -545,6 +657,21 @@ class PipelineStage:
             if w_a <= t < w_b:
                 mark_on(ev_in, t)
             h3 = pc()
+            if self.vs:                                  # head shards, rank 0's merges, penalty flags
+                with trace_range(f"pp.vocab{t}"):
+                    if not self.is_first and group_valid(t - D * (P + 2)):
+                        for cur in range((t - D * (P + 2)) * L, (t - D * (P + 2)) * L + L):
+                            if feeds_back(cur):
+                                with lane_ctx(cur):
+                                    ops.seen_mark(self.seen[cur % M], self.tokin[cur % M], self.shard.v0)
+                    if self.is_first and group_valid(t - D * (P + 1)):
+                        for cur in range((t - D * (P + 1)) * L, (t - D * (P + 1)) * L + L):
+                            with lane_ctx(cur):
+                                self._vs_merge(cur % M)
+                    if group_valid(t - D * P):
+                        for cur in range((t - D * P) * L, (t - D * P) * L + L):
+                            with lane_ctx(cur):
+                                self._vs_shard(cur % M)
             if group_valid(cur_g):
                 with trace_range(f"pp.tick{t}"):
                     for cur in range(cur_g * L, cur_g * L + L):
@@ -554,7 +681,9 @@ class PipelineStage:
                                 ids = prompts[m].to(dev) if self.is_first else None
                                 out = self._prefill(m, ids, T, pre_in[m])
                                 pre_in[m] = None
-                                if self.is_last:
+                                if self.is_last and self.vs:
+                                    self.hfin[m].copy_(out)
+                                elif self.is_last:
                                     self._sample(m, out)
                                 else:
                                     pre_out[m] = out
@@ -604,7 +733,7 @@ class PipelineStage:
             a, z = ev_first[-1], ev_first[t_first]
             stats["ttft_ms"] = a.elapsed_time(z) if self.cuda else (z - a) * 1e3
         toks = None
-        if self.is_last:
+        if samp:
             toks = []
             for m in range(M):
                 toks.extend(self.out[m].tolist())
@@ -613,9 +742,10 @@ class PipelineStage:
         return PipelineResult(toks, n_ticks if stopped_at is None else stopped_at + 1, elapsed, stats=stats)
 
     def _all_hit(self) -> bool:
-        """Every rank joins: True when the last stage has seen EOS in every row (one all-reduce
-        of a device flag; the host waits for it, once per check period)."""
-        if self.is_last:
+        """Every rank joins: True when the sampling rank (the last stage; rank 0 under the vocab
+        split) has seen EOS in every row (one all-reduce of a device flag; the host waits for it, once
+        per check period)."""
+        if self._samp:
             if self.streams:
                 cur = torch.cuda.current_stream(self.device)
                 for st in self.streams:

@@ -148,6 +148,20 @@ def load_quantized(path: str, device=None, first: int = 0, last: Optional[int] =
     return model
 
 
+def load_head_rows(path: str, v0: int, v1: int, device=None, dtype=torch.bfloat16):
+    """Rows [v0, v1) of a quantised checkpoint's (16-bit) LM head and its bias, read as a slice
+    (a vocab shard of the head, parallel/vocab_head.py: no rank reads the whole matrix)."""
+    from safetensors import safe_open
+    cfg = checkpoint_config(path)
+    with safe_open(os.path.join(path, "model.safetensors"), framework="pt") as sf:
+        keys = set(sf.keys())
+        assert "lm_head.qweight" not in keys, "vocab split: 16-bit LM head only"
+        name = "lm_head.weight" if "lm_head.weight" in keys or not cfg.tie_word_embeddings else "embed"
+        w = sf.get_slice(name)[v0:v1].to(device=device, dtype=dtype)
+        b = sf.get_slice("lm_head.bias")[v0:v1].to(device=device, dtype=dtype) if "lm_head.bias" in keys else None
+    return w, b
+
+
 def _local_name(model: DecoderLM, global_name: str) -> str:
     if global_name.startswith("layers."):
         _, idx, rest = global_name.split(".", 2)

@@ -54,16 +54,21 @@ def test_bench_metrics_out_and_tracing_cpu(tmp_path):
     assert rec["event"] == "bench" and rec["value"] == d["value"] and rec["metric"] == d["metric"]
 
 
-@pytest.mark.parametrize("n,lanes", [(2, 1), (2, 2), (3, 2), (4, 2), (8, 1), (8, 2)])
-def test_bench_pipeline_torchrun_cpu(n, lanes):
+@pytest.mark.parametrize("n,lanes,vs", [(2, 1, "on"), (2, 2, "on"), (2, 2, "off"), (3, 2, "on"), (4, 2, "on"),
+                                         (8, 1, "on"), (8, 2, "on"), (8, 1, "off")])
+def test_bench_pipeline_torchrun_cpu(n, lanes, vs):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *COMMON,
-           "--lanes", str(lanes)]
+           "--lanes", str(lanes), "--pp-vocab-split", vs]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
-    assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * n * lanes and d["value"] > 0
+    # vocab split (default): the head over every rank, one more micro-batch group in flight
+    groups = n + 1 if vs == "on" else n
+    assert d["vocab_split"] == (vs == "on")
+    assert d["n_gpus"] == n and d["config"]["global_batch"] == 2 * groups * lanes and d["value"] > 0
+    assert len(d["stage_cost_model_us"]) == n and d["stage_cost_spread"] >= 1.0
     assert d["config"]["parallelism"] == f"pp{n}" and len(d["config"]["partition"]) == n + 1
     # per-rank window statistics from every stage (compute / P2P wait / bubble / bytes per tick)
     assert d["world_size"] == n and len(d["per_rank"]) == n

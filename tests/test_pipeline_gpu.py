@@ -43,7 +43,7 @@ def _sampling(S, do_sample):
 
 
 def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q, lanes=1, headinfer_heads=None,
-            prefill_chunk=4096):
+            prefill_chunk=4096, vocab_split=False):
     import edgellm  # noqa: F401
     from edgellm.parallel.pipeline import PipelineStage
     from datetime import timedelta
@@ -56,12 +56,18 @@ def _worker(rank, world, port, arch, quant, M, b, T, S, do_sample, q, lanes=1, h
     _, model = _model(arch, quant, bounds[rank], bounds[rank + 1])
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, cfg.vocab_size, (b, T), generator=g) for _ in range(M)]
+    shard = None
+    if vocab_split:
+        from edgellm.parallel.vocab_head import build_head_shard
+        shard = build_head_shard(cfg, rank, world, model=model, seed=7, dtype=torch.bfloat16, device="cuda:0")
     st = PipelineStage(model, rank, world, b, M, max_seq=T + S + 4, lanes=lanes, headinfer_heads=headinfer_heads,
-                       prefill_chunk=prefill_chunk)
+                       prefill_chunk=prefill_chunk, vocab_split=vocab_split, head_shard=shard)
     assert st.host_staged and st.use_graphs
-    n_ticks = (M + S * M) // lanes + world - 1
+    lag = world + 1 if vocab_split else world - 1
+    n_ticks = (M + S * M) // lanes + lag
     res = st.run(prompts if rank == 0 else None, T, _sampling(S, do_sample), S, seed=5,
-                 stats_window=(M // lanes + world - 1, n_ticks))
+                 stats_window=(M // lanes + lag, n_ticks))
+    assert st.vs == vocab_split
     assert res.stats["compute_ms_per_tick"] > 0 and 0 <= res.stats["bubble_frac"] <= 1
     if res.tokens is not None:
         q.put(res.tokens)
@@ -105,14 +111,22 @@ def test_pipeline_gpu_headinfer_chunked(cuda, world):
     _run("w8a8", 1, world, True, headinfer_heads=1, prefill_chunk=4)
 
 
-def _run(quant, lanes, world, do_sample, headinfer_heads=None, prefill_chunk=4096):
+@pytest.mark.parametrize("quant,lanes,world", [("none", 1, 2), ("w8a8", 2, 2), ("w8a8", 1, 4)])
+@pytest.mark.parametrize("do_sample", [False, True])
+def test_pipeline_gpu_vocab_split_matches_unsplit(cuda, quant, lanes, world, do_sample):
+    """LM head split by vocabulary over the ranks (every rank its logits slice + the sampler's
+    phase 1 on the GPU, rank 0 the merge kernel): tokens equal the unsplit model's."""
+    _run(quant, lanes, world, do_sample, vocab_split=True)
+
+
+def _run(quant, lanes, world, do_sample, headinfer_heads=None, prefill_chunk=4096, vocab_split=False):
     arch, b, T, S = "llama", 4, 9, 12
-    M = world * lanes
+    M = (world + 1 if vocab_split else world) * lanes
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, arch, quant, M, b, T, S, do_sample, q, lanes,
-                                               headinfer_heads, prefill_chunk))
+                                               headinfer_heads, prefill_chunk, vocab_split))
              for r in range(world)]
     for p in procs:
         p.start()
