@@ -311,16 +311,50 @@ class PipelineStage:
             self.hit[m].logical_or_(nxt.eq(self._eos))
 
     # ------------------------------------------------------------------ vocab-split head
+    def _vs_graphed(self, kind: str, m: int, fn):
+        """Run a vocab-split step of micro-batch m (``fn(m)`` -> its output tensors or None) eagerly
+        the first time, then from a HIP graph captured on the second call (a pool per lane, apart
+        from the decode graphs' pools), replayed afterwards; the captured outputs are static,
+        returned on every call."""
+        if not self.graphs_ok:
+            return fn(m)
+        key = (kind, m)
+        g = self._vs_graphs.get(key)
+        if g is None:
+            if key not in self._vs_warm:
+                self._vs_warm.add(key)
+                return fn(m)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            lane = m % self.L                     # one pool per lane: lanes replay concurrently
+            with torch.cuda.graph(g, pool=self._vs_pools.get(lane), capture_error_mode="thread_local"):
+                self._vs_outs[key] = fn(m)
+            if lane not in self._vs_pools:
+                self._vs_pools[lane] = g.pool()
+            self._vs_graphs[key] = g
+        g.replay()
+        return self._vs_outs[key]
+
     def _vs_shard(self, m: int):
         """This rank's logits slice + sampler phase 1 for micro-batch m (rows in hfin[m])."""
-        self.cand[m] = self.shard.candidates(self.hfin[m], self.seen[m], self.sampling, self.rng[m])
-        if not self.is_first:
-            self.rng[m][1:].add_(1)                   # rank 0 advances after its merge (same step)
+        def body(m):
+            c = self.shard.candidates(self.hfin[m], self.seen[m], self.sampling, self.rng[m])
+            if not self.is_first:
+                self.rng[m][1:].add_(1)               # rank 0 advances after its merge (same step)
+            return c
+        self.cand[m] = self._vs_graphed("shard", m, body)
+
+    def _vs_seen(self, m: int):
+        """Ranks >= 1: mark the token rank 0 sent for micro-batch m in this shard's penalty flags."""
+        self._vs_graphed("seen", m, lambda m: ops.seen_mark(self.seen[m], self.tokin[m], self.shard.v0))
 
     def _vs_merge(self, m: int):
         """Rank 0: phase 2 over every shard's candidates -> the token of each row of m."""
+        self._vs_graphed("merge", m, self._vs_merge_body)
+
+    def _vs_merge_body(self, m: int):
         sp = self.sampling
-        nxt = ops.sample_merge([self.cand.pop(m)] + self.cand_in[m], self.cfg.vocab_size, sp.temperature, sp.top_k,
+        nxt = ops.sample_merge([self.cand[m]] + self.cand_in[m], self.cfg.vocab_size, sp.temperature, sp.top_k,
                                sp.top_p, self.rng[m], sp.do_sample)
         self.tok[m].copy_(nxt)
         self.out[m].scatter_(1, self.step[m].view(1, 1).expand(self.b, 1), nxt.view(self.b, 1))
@@ -423,6 +457,10 @@ class PipelineStage:
         self._warm: Dict[int, bool] = {}
         self._graphs.clear()
         self._pools.clear()
+        self._vs_graphs: Dict[tuple, object] = {}
+        self._vs_outs: Dict[tuple, object] = {}
+        self._vs_warm = set()
+        self._vs_pools: Dict[int, object] = {}
         self._final_bucket = self._bucket(T + S + 1)
         if self.vs or self.is_last:
             Vs = self.shard.Vs if self.vs else V
@@ -582,7 +620,7 @@ class PipelineStage:
                         if self.is_first:
                             recvs.extend((x, r + 1) for r, c in enumerate(self.cand_in[i % M]) for x in c)
                         else:
-                            sends.extend((x, 0) for x in self.cand.pop(i % M))
+                            sends.extend((x, 0) for x in self.cand[i % M])
                 if group_valid(mg):
                     for i in (mg * L + l for l in lanes):
                         if feeds_back(i):
@@ -663,7 +701,7 @@ class PipelineStage:
                         for cur in range((t - D * (P + 2)) * L, (t - D * (P + 2)) * L + L):
                             if feeds_back(cur):
                                 with lane_ctx(cur):
-                                    ops.seen_mark(self.seen[cur % M], self.tokin[cur % M], self.shard.v0)
+                                    self._vs_seen(cur % M)
                     if self.is_first and group_valid(t - D * (P + 1)):
                         for cur in range((t - D * (P + 1)) * L, (t - D * (P + 1)) * L + L):
                             with lane_ctx(cur):
