@@ -130,10 +130,9 @@ def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scal
 
 def decode_rows_ok(M: int, K: int, splits: int = 1) -> bool:
     """Whether the decode GEMV family (grouped scales, split-K, quantising GLU) takes M rows at
-    this K: every K up to 64 rows; 65-128 rows (two micro-batches in one) for the k-tile counts
-    gemm_i8.hip instantiates (K = 4096 whole; 4096 / 11008 / 14336 in 4 slices); 129-256 rows
-    (one 256-row micro-batch: the row-split ring2 kernels, split-K count fixed per K) for
-    K % 128 == 0."""
+    this K: every K up to 64 rows; 65-128 rows (two micro-batches in one: the ring2 kernel) for
+    K % 128 == 0 (split-K: >= 4 stages of 128 k per slice); 129-256 rows (one 256-row
+    micro-batch: the row-split ring2 kernels, split-K count fixed per K) for K % 128 == 0."""
     if M <= 64:
         return True
     if M > 256 or not available():

@@ -69,9 +69,7 @@ void edge_w8a8_gemv_config(int nw, int unroll);
 int edge_w8a8_rows128_ok(int K, int S);
 int edge_w8a8_rows256_ok(int K);
 int edge_w8a8_rows256_splits(int K);
-void edge_w8a8_rows256_diag(int v);
 void edge_w8a8_prefill_x32(int v);
-void edge_w8a8_rows256_rot(int v);
 int edge_gemv_bf16(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
                    hipStream_t st, const void* add, int h16);
 int edge_gemv_bf16_splitk(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
@@ -82,9 +80,7 @@ int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int*
                          const float* scb, int M, int N, int cmax, hipStream_t st);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_gemv_ring(int on);
-void edge_w8a8_prefill_gemm(int v, int b);
 void edge_w8a8_prefill_apack(int v);
-void edge_w8a8_prefill_prio(int v);
 int edge_w8a8_apack_ok(int M, int N, int K, int KT);
 int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
                        void* out, int M, int N, int K, int KT, hipStream_t st);
@@ -847,8 +843,9 @@ std::tuple<at::Tensor, at::Tensor> w8a8_gemm_gluq(const at::Tensor& a, const at:
   TORCH_CHECK(a.size(-1) == K, "activation K mismatch");
   check_w8a8_operands(wp, sw, bias, N, K);
   const int64_t M = rows_of(a), KT = (K + 63) / 64, Mpad = (M + 15) / 16 * 16;
-  TORCH_CHECK((M <= (K == 4096 ? 128 : 64) || (M <= 256 && edge_w8a8_rows256_ok((int)K))) && N % 128 == 0,
-              "quantising GLU needs M <= 64 (128 at K = 4096, 256 where rows256_ok(K)) and N % 128 == 0");
+  TORCH_CHECK((M <= 64 || (M <= 128 && edge_w8a8_rows128_ok((int)K, 1)) || (M <= 256 && edge_w8a8_rows256_ok((int)K)))
+                  && N % 128 == 0,
+              "quantising GLU needs M <= 64 (128 where rows128_ok(K), 256 where rows256_ok(K)) and N % 128 == 0");
   TORCH_CHECK(a_scale_mpad(sa, M, KT) == 0, "fused GLU takes per-token activation scales");
   auto q = at::empty({M, N / 2}, a.options());
   auto s = at::empty({N / 128, Mpad}, a.options().dtype(at::kFloat));
@@ -1115,12 +1112,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (what == "gemv") edge_w8a8_gemv_config((int)a, (int)b);
     else if (what == "gemv_ntw") edge_w8a8_gemv_ntw((int)a);
     else if (what == "gemv_ring") edge_w8a8_gemv_ring((int)a);
-    else if (what == "ring2_256_diag") edge_w8a8_rows256_diag((int)a);
     else if (what == "prefill_x32") edge_w8a8_prefill_x32((int)a);
-    else if (what == "ring2_256_rot") edge_w8a8_rows256_rot((int)a);
-    else if (what == "prefill_gemm") edge_w8a8_prefill_gemm((int)a, (int)b);
     else if (what == "prefill_apack") edge_w8a8_prefill_apack((int)a);
-    else if (what == "prefill_prio") edge_w8a8_prefill_prio((int)a);
     else if (what == "decode_attn") edge_decode_attn_config((int)a);
     else if (what == "decode_attn_occ") edge_decode_attn_occ((int)a);
     else if (what == "decode_attn_small") edge_decode_attn_small((int)a);

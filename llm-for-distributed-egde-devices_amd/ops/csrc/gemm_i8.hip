@@ -10,11 +10,12 @@
 // row-major [M, K]; its fragment is lane l <- A[m0 + (l & 15)][k0 + 16*(l >> 4) .. +16].
 // Both operands use the same (lane, byte) -> k map, so the MFMA sums the right products.
 //
-// Kernels:
-//   gemv:  M <= 64 (decode).  HBM-bound on W: a workgroup owns NTW 16-column tiles of one
-//          16-row block, its NW waves split K (k-tile kt -> wave kt % NW) and keep UNROLL
-//          fragments per tile in flight (no LDS staging: the weights are read exactly once,
-//          nontemporal), partial sums reduced through LDS.  Activation modes:
+// Decode kernels (the prefill GEMMs are in gemm_i8_prefill.hip, the shared layout and helpers in
+// gemm_i8.h):
+//   gemv:  M <= 64.  HBM-bound on W: a workgroup owns NTW 16-column tiles of one 16-row block,
+//          its NW waves split K (k-tile kt -> wave kt % NW) and keep UNROLL fragments per tile in
+//          flight (no LDS staging: the weights are read exactly once, nontemporal), partial sums
+//          reduced through LDS.  Activation modes:
 //            A_TOKEN  int8 A, one scale per token (from the fused norm+quant kernel)
 //            A_GROUP  int8 A, one scale per (token, 64 columns) [KT][Mpad] (fused attention)
 //          With per-group scales each k-tile's MFMA starts from zero and is folded into a float
@@ -25,56 +26,13 @@
 //          (2 or 4 tiles per workgroup; rowwise.hip::group_quant_kernel quantises it for the down
 //          projection); EPI_GLUQ (8 tiles = 64 features) also quantises h per (token, 64 features)
 //          in the epilogue and writes int8 h + scales [N/128][Mpad] directly.
-//   ldsa:  gemv with the activations staged through LDS once per workgroup and one tile per
-//          wave: the 33-128 row GLUQ at K = 4096, and every projection at 65-128 rows (two
-//          decode micro-batches in one) for the k-tile counts of 4096-hidden models.
-//   big:   M > 128 (prefill). 128x256 / 256x256 block tile, 8 waves, BK=64, a 4-stage
-//          global_load_lds ring (counted vmcnt, bare barriers), register-double-buffered
-//          fragments, LDS-restaged 16-B store epilogue (see the kernel).
-//   tiled: 65-128 rows without a decode kernel, ragged shapes. 128x128 block tile, 4 waves in
-//          2x2, both operands staged with global_load_lds, LDS double buffer.
-#include "common.h"
+//   ring2: 65-256 rows (and the bf16 decode projections at 17-256 rows): both operands by
+//          LDS-DMA into rings of decoupled depth, dedicated weight / activation loader waves.
+//   r256:  129-256 rows on fragment-packed activations (qkv).
+#include "gemm_i8.h"
 #include <type_traits>
 
 namespace {
-constexpr int NT = 256;
-constexpr int A_TOKEN = 0, A_GROUP = 1;
-constexpr int EPI_OUT = 0, EPI_GLU = 1, EPI_GLUQ = 2, EPI_PART = 3, EPI_GELUQT = 4, EPI_GELUQE = 5;
-// (EPI_GELUQT / EPI_GELUQE: gelu (tanh / erf) of the bf16 output, quantised per (token, 64 columns)
-// in the epilogue of a 4-tile workgroup — the GELU MLPs' (Phi-2, Pythia) up projection at <= 64 rows)
-
-__device__ __forceinline__ v4i mfma_i8(const v4i& a, const v4i& b, const v4i& c) {
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void store_out(bf16_t* __restrict__ out, int M, int N, int row, int col, int acc,
-                                          const float* __restrict__ sa, const float* __restrict__ sw,
-                                          const bf16_t* __restrict__ bias) {
-  if (row < M && col < N) {
-    float v = (float)acc * sa[row] * sw[col];
-    if (bias) v += bf2f(bias[col]);
-    out[(size_t)row * N + col] = f2bf(v);
-  }
-}
-
-__device__ __forceinline__ void store_out_f(bf16_t* __restrict__ out, int M, int N, int row, int col, float v,
-                                            const float* __restrict__ sw, const bf16_t* __restrict__ bias) {
-  if (row < M && col < N) {
-    v *= sw[col];
-    if (bias) v += bf2f(bias[col]);
-    out[(size_t)row * N + col] = f2bf(v);
-  }
-}
-
-__device__ __forceinline__ void fold(v4f& accf, const v4i& t, const v4f& s) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) accf[q] += (float)t[q] * s[q];
-}
-__device__ __forceinline__ void fold1(v4f& accf, const v4i& t, float s) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) accf[q] += (float)t[q] * s;
-}
-
 // int8 A fragment of k-tile k for this lane's row (ragged K: byte-wise, zero padded)
 __device__ __forceinline__ v4i load_a_i8(const int8_t* __restrict__ arow_p, bool aval, int k, int kend, int akc,
                                          int K, bool k16) {
@@ -101,7 +59,6 @@ __device__ __forceinline__ v4i load_a_i8(const int8_t* __restrict__ arow_p, bool
 // the epilogue reads from global memory (weight scales, bias, per-token scales) is loaded at
 // kernel start, so the tail of the kernel never waits on an HBM round trip.
 
-__device__ const bf16_t g_zero_bf16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifndef GEMV_UNROLL_FIXED
 #define GEMV_UNROLL_FIXED 1
 #endif
@@ -639,882 +596,6 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
                                               nt0, wave, lane, ks);
 }
 
-// ------------------------------------------------------------------------ LDS-staged activations
-// At 64 decode rows the weight-stationary GEMV above holds 8 tiles x 4 row blocks of accumulators
-// per wave (128 VGPRs), so only 8 waves fit and each waits one memory latency per step.  Here the
-// workgroup stages each step's activation fragments (C k-tiles x MB row blocks) in LDS once
-// (register-staged: global load, ds_write, one barrier per step; two LDS buffers) and every wave
-// reads them from there.  Wave w owns TPW tiles for all MB row blocks and one k-slice of every
-// step (NTW / TPW tile groups x KH k-slices), so its accumulators are TPW x MB fragments and its
-// registers go to prefetch: D steps of weight and activation loads are in flight per wave.  K is
-// a compile-time 64 * KTC and the step loop unrolls fully, so every register set has a name and
-// the compiler waits with counted vmcnt.  Loads are issued per step as [weights, activations],
-// so the wait that retires a step's activations (before their LDS write) retires only loads the
-// next step needs anyway.  The reduction over the KH k-slices reuses the activation buffers.
-// Measured on gate_up at 64 rows (22016 x 4096, SwiGLU + int8 epilogue): 26.3 us against 33.9 us
-// for the weight-stationary kernel; TPW 1 / 2, D 1..6 and 8- or 16-wave register staging (tile
-// groups sharing one LDS image) all land at 26-29 us, the per-CU load rate of 172 busy CUs.
-// KTC (k-tiles per workgroup) need not be a multiple of the step: the last step's missing k-tiles
-// are skipped by wave-uniform branches.  EPI_PART: workgroup (group, ks) reduces k-tiles
-// [ks * KTC, (ks + 1) * KTC) and writes fp32 partials (KT == S * KTC).  SCALED (A_GROUP): each
-// step's per-(token, 64) scales are staged beside the activations and every k-tile's exact int32
-// MFMA sum is folded into a float accumulator with its scale.
-template <int MB, int NTW, int TPW, int KH, int KPW, int D, int KTC, bool SCALED, int EPI>
-__global__ void __launch_bounds__(NTW / TPW * KH * 64) w8a8_gemv_ldsa_kernel(
-    const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
-    const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
-    int M, int N, int K, int NTt, int Mpad, int S) {
-  constexpr int TG = NTW / TPW, NW = TG * KH, C = KH * KPW, STEPS = (KTC + C - 1) / C;
-  constexpr int DD = D < STEPS ? D : STEPS - 1;          // steps in flight ahead
-  constexpr int F = NTW * MB, NFRAG = C * MB, FPW = NFRAG / NW;
-  constexpr int ROWS = MB * 16, SCH = SCALED ? C * ROWS / 256 : 0;   // waves staging 64 x v4f scales
-  constexpr int ABYTES = 2 * NFRAG * 1024 + 2 * C * ROWS * 4 * (SCALED ? 1 : 0), RBYTES = KH * F * 1024;
-  static_assert(NTW % TPW == 0 && NFRAG % NW == 0 && DD >= 1 && SCH <= NW && (!SCALED || C * ROWS % 256 == 0), "shape");
-  static_assert(RBYTES <= 131072 && ABYTES <= 131072, "LDS budget");
-  static_assert(EPI == EPI_OUT || EPI == EPI_PART || (EPI == EPI_GLUQ && NTW == 8 && !SCALED), "epilogues");
-  __shared__ __attribute__((aligned(16))) v4i lds[(ABYTES > RBYTES ? ABYTES : RBYTES) / 16];
-  __shared__ float gmax[MB][4][16];
-  float* lsc = reinterpret_cast<float*>(lds + 2 * NFRAG * 64);   // [2][C][ROWS] staged scales
-  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
-  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
-  const int kbeg = ks * KTC, KT = K / 64;
-  const int nt0 = grp * NTW;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int t0 = (wave % TG) * TPW, h = wave / TG;
-  const int akc = 16 * (lane >> 4);
-  const v4i* wp[TPW];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j)
-    wp[j] = reinterpret_cast<const v4i*>(Wp + ((size_t)min(nt0 + t0 + j, NTt - 1) * KT + kbeg) * 1024);
-  const int8_t* asrc[FPW];
-  int fid[FPW], fk[FPW];
-#pragma unroll
-  for (int i = 0; i < FPW; ++i) {
-    const int f = wave + i * NW;                           // fragment (k-tile f / MB, rows f % MB)
-    fid[i] = f;
-    fk[i] = f / MB;
-    asrc[i] = A + (size_t)min((f % MB) * 16 + (lane & 15), M - 1) * K + (size_t)kbeg * 64 + akc;
-  }
-  // scale staging: wave w < SCH loads v4f e = w * 64 + lane of the step's [C][ROWS] block
-  const int se = (wave * 64 + lane) * 4, skk = se / ROWS, srow = min(se % ROWS, Mpad - 4);
-  const auto pre = epi_preload<MB, NTW, NW, EPI>(sw, bias, nt0, NTt, wave, lane);
-  v4i acc[TPW][MB];
-  v4f accf[TPW][MB];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j)
-#pragma unroll
-    for (int i = 0; i < MB; ++i) { acc[j][i] = v4i{0, 0, 0, 0}; accf[j][i] = v4f{0.f, 0.f, 0.f, 0.f}; }
-  v4i w[DD + 1][TPW][KPW], ast[DD][FPW];
-  v4f sst[DD];
-  // s is a compile-time value after unrolling; k-tiles past KTC are clamped (loads) or skipped
-  auto issue = [&](int s) {
-#pragma unroll
-    for (int j = 0; j < TPW; ++j)
-#pragma unroll
-      for (int u = 0; u < KPW; ++u)
-        w[s % (DD + 1)][j][u] = __builtin_nontemporal_load(wp[j] + min(s * C + h * KPW + u, KTC - 1) * 64 + lane);
-#pragma unroll
-    for (int i = 0; i < FPW; ++i)
-      ast[s % DD][i] = *reinterpret_cast<const v4i*>(asrc[i] + min(s * C + fk[i], KTC - 1) * 64);
-    if constexpr (SCALED)
-      if (wave < SCH)
-        sst[s % DD] = *reinterpret_cast<const v4f*>(sa + (size_t)(kbeg + min(s * C + skk, KTC - 1)) * Mpad + srow);
-  };
-  auto stage = [&](int s) {
-#pragma unroll
-    for (int i = 0; i < FPW; ++i)
-      if ((s + 1) * C <= KTC || s * C + fk[i] < KTC) lds[((size_t)(s & 1) * NFRAG + fid[i]) * 64 + lane] = ast[s % DD][i];
-    if constexpr (SCALED)
-      if (wave < SCH) *reinterpret_cast<v4f*>(lsc + (s & 1) * C * ROWS + se) = sst[s % DD];
-  };
-#pragma unroll
-  for (int s = 0; s < DD; ++s) issue(s);
-  stage(0);
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < STEPS; ++s) {
-    if (s + DD < STEPS) issue(s + DD);
-#pragma unroll
-    for (int u = 0; u < KPW; ++u) {
-      if ((s + 1) * C <= KTC || s * C + h * KPW + u < KTC) {   // wave-uniform: ragged last step
-#pragma unroll
-        for (int i = 0; i < MB; ++i) {
-          const v4i a = lds[((size_t)(s & 1) * NFRAG + (h * KPW + u) * MB + i) * 64 + lane];
-          if constexpr (SCALED) {
-            const v4f sg = *reinterpret_cast<const v4f*>(lsc + (s & 1) * C * ROWS + (h * KPW + u) * ROWS + i * 16 +
-                                                         4 * (lane >> 4));
-#pragma unroll
-            for (int j = 0; j < TPW; ++j) fold(accf[j][i], mfma_i8(a, w[s % (DD + 1)][j][u], v4i{0, 0, 0, 0}), sg);
-            // pin the folds every 4 row blocks: unpinned, the compiler sinks every step's cvt/fma
-            // chain to the epilogue and keeps all MFMA results alive (100+ spilled VGPRs)
-            if (i % 4 == 3)
-#pragma unroll
-              for (int ii = i - 3; ii <= i; ++ii)
-#pragma unroll
-                for (int j = 0; j < TPW; ++j) asm volatile("" : "+v"(accf[j][ii]));
-          } else {
-#pragma unroll
-            for (int j = 0; j < TPW; ++j) acc[j][i] = mfma_i8(a, w[s % (DD + 1)][j][u], acc[j][i]);
-          }
-        }
-      }
-    }
-    if (s + 1 < STEPS) {
-      stage(s + 1);
-      __syncthreads();
-    }
-  }
-  __syncthreads();                                         // activation buffers become the reduction buffer
-#pragma unroll
-  for (int j = 0; j < TPW; ++j)
-#pragma unroll
-    for (int i = 0; i < MB; ++i)
-      lds[((size_t)h * F + (t0 + j) * MB + i) * 64 + lane] = SCALED ? __builtin_bit_cast(v4i, accf[j][i]) : acc[j][i];
-  __syncthreads();
-  gemv_epilogue<MB, NTW, NW, KH, SCALED, EPI>(lds, sa, pre, outv, os, gmax, M, N, NTt, Mpad, nt0, wave, lane, ks);
-}
-
-// ------------------------------------------------------------------------------------ tiled
-// Block tile 128 x 128, BK = 64. LDS image per buffer: A 8 x 1 KiB fragments, B 8 x 1 KiB.
-constexpr int BM = 128, BN = 128;
-
-__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
-// streaming form (cache policy nt): weight bytes read once per step, kept out of the way of the
-// L2-resident activation panel every workgroup re-reads
-__device__ __forceinline__ void glds16_nt(const void* g, void* lds_base) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2);
-}
-
-__global__ void __launch_bounds__(NT) w8a8_gemm_tiled_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
-                                                             const int8_t* __restrict__ Wp, const float* __restrict__ sw,
-                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                             int M, int N, int K, int KT, int NTt, int grid_n) {
-  extern __shared__ __attribute__((aligned(16))) int8_t smem[];  // 2 x (8 KiB A + 8 KiB B)
-  // XCD-aware remap: consecutive dispatch ids round-robin over 8 XCDs; give each XCD a
-  // contiguous run of tiles along N so blocks sharing an A panel share an L2.
-  const int nwg = gridDim.x;
-  const int orig = blockIdx.x;
-  int wgid = orig;
-  if (nwg % 8 == 0) wgid = (orig % 8) * (nwg / 8) + orig / 8;
-  const int bn = wgid % grid_n, bm = wgid / grid_n;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;   // 2 x 2 waves, 64 x 64 each
-
-  // per-lane global sources for this wave's 2 A fragments and 2 B fragments
-  const int8_t* asrc[2];
-  const int8_t* bsrc[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int msub = wave * 2 + j;                       // 0..7
-    int r = bm * BM + msub * 16 + (lane & 15);
-    r = r < M ? r : M - 1;
-    asrc[j] = A + (size_t)r * K + 16 * (lane >> 4);
-    int ntile = bn * (BN / 16) + wave * 2 + j;            // 0..NTt-1
-    ntile = ntile < NTt ? ntile : NTt - 1;
-    bsrc[j] = Wp + ((size_t)ntile * KT) * 1024 + lane * 16;
-  }
-
-  auto stage = [&](int buf, int kt) {
-    int8_t* base = smem + buf * 16384;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      glds16(asrc[j] + (size_t)kt * 64, base + (wave * 2 + j) * 1024);
-      glds16(bsrc[j] + (size_t)kt * 1024, base + 8192 + (wave * 2 + j) * 1024);
-    }
-  };
-
-  v4i acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < KT; ++kt) {
-    if (kt + 1 < KT) stage(cur ^ 1, kt + 1);
-    const int8_t* base = smem + cur * 16384;
-    v4i a[4], b[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v4i*>(base + (wm * 4 + i) * 1024 + lane * 16);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const v4i*>(base + 8192 + (wn * 4 + j) * 1024 + lane * 16);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_i8(a[i], b[j], acc[i][j]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    cur ^= 1;
-  }
-
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = bn * BN + (wn * 4 + j) * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm * BM + (wm * 4 + i) * 16 + 4 * (lane >> 4) + r;
-        store_out(out, M, N, row, col, acc[i][j][r], sa, sw, bias);
-      }
-    }
-}
-
-// LDS byte address of a __shared__ pointer, and a ds_read_b128 the compiler does not track (callers
-// order it with explicit lgkmcnt waits; see the ring kernel below)
-__device__ __forceinline__ uint32_t lds_off(const void* p) {
-  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
-}
-__device__ __forceinline__ v4i lds_read16(uint32_t addr) {
-  v4i r;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
-__device__ __forceinline__ int lds_read4(uint32_t addr) {
-  int r;
-  asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
-
-// n ds_read_b128 at addr + 1024 i (immediate offsets: no address VALU, no extra VGPRs)
-template <int I, int N>
-__device__ __forceinline__ void lds_read_row_(uint32_t addr, v4i (&f)[N]) {
-  if constexpr (I < N) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[I]) : "v"(addr), "n"(I * 1024));
-    lds_read_row_<I + 1, N>(addr, f);
-  }
-}
-template <int N>
-__device__ __forceinline__ void lds_read_row(uint32_t addr, v4i (&f)[N]) { lds_read_row_<0, N>(addr, f); }
-
-// ------------------------------------------------------------------------------------ big
-// Prefill GEMM (M > 128, K % 64 == 0, N % 8 == 0): BM x 256 block tile (BM = 256, or 128 when
-// 256-row tiles would leave CUs idle), 8 waves as 2 (M) x 4 (N), BK = 64, one block per CU.
-//  * Both operands go global -> LDS by global_load_lds into a ring of R = 4 stages (BM/16 + 16 KiB
-//    each; 128 KiB at BM = 256): 3 stages of DMA stay in flight across every barrier (counted
-//    vmcnt, bare s_barrier, LDS reads by inline asm so the compiler never drains the ring with a
-//    vmcnt(0) — the structure of the 128-row decode ring kernel below).
-//  * Fragments are double-buffered in registers: iteration s reads stage s + 1's fragments while
-//    the MFMAs consume stage s's, so LDS latency hides under 32 MFMAs per wave.
-//  * Operands are swapped in the MFMA (W tile as the A operand, activations as B), so the
-//    accumulator of a lane holds 4 consecutive output COLUMNS of one row: the epilogue scales,
-//    packs 4 bf16 into 8 bytes, and restages the wave's tile through LDS (XOR-swizzled 16-B
-//    chunks) to write full 128-B row segments with 16-B stores.
-//  * blockIdx -> tile: bijective XCD remap (each XCD gets a contiguous range), then groups of 4
-//    row tiles walked column-major, so an XCD's ~32 resident blocks share 4 A panels and 8 W panels
-//    in its L2.
-//  * APK: A arrives fragment-packed (pack_a_kernel: 1 KiB = 16 rows x 64 k per (row block, k-tile),
-//    the layout of the packed weights), so an A piece is 1 KiB of contiguous bytes instead of 16
-//    rows x 64 B — the pattern tools/ingest_bw.hip measured at ~18 B/clk/CU L2 -> LDS against
-//    ~60 for contiguous pieces.  The LDS image is identical, only the DMA source offsets change.
-// PRIO: s_setprio(1) around each k-tile's MFMA cluster (cdna guide T5: keeps hipcc from moving the
-// MFMAs across the barriers into the fragment reads / DMA issue; A/B knob prefill_prio)
-template <int BMV, int ISS, bool APK = false, bool PRIO = false>
-__global__ void __launch_bounds__(512, 1) w8a8_gemm_big_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
-                                                              const int8_t* __restrict__ Wp, const float* __restrict__ sw,
-                                                              const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                              int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
-  constexpr int R = 4, BNV = 256, NWV = 8;
-  constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
-  constexpr int MI = BMV / 32, NJ = 4;                        // row blocks / column tiles per wave
-  static_assert(PIECES % NWV == 0, "pieces per wave");
-  static_assert(R * STAGE <= 160 * 1024 && NWV * (BMV / 4) * 256 <= R * STAGE, "LDS budget");
-  __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
-
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  constexpr int GM = 4;
-  const int per_group = GM * grid_n;
-  const int grp = wgid / per_group, gm0 = grp * GM, gsz = min(GM, grid_m - gm0);
-  const int inr = wgid - grp * per_group;
-  const int bm = gm0 + inr % gsz, bn = inr / gsz;
-
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-
-  // this wave's DMA pieces p = wave + 8 i: A row block p (p < AP) or W tile p - AP.  Per-lane
-  // 32-bit offsets from the (wave-uniform) operand base: one VGPR per piece, SGPR base + VGPR
-  // offset addressing (M * K and the packed W stay below 4 GiB)
-  uint32_t off[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int p = wave + NWV * i;
-    if (p < AP && APK) {
-      const int rb = min(bm * (BMV / 16) + p, (M + 15) / 16 - 1);
-      off[i] = (uint32_t)rb * (uint32_t)KT * 1024u + lane * 16;
-    } else if (p < AP) {
-      const int row = min(bm * BMV + p * 16 + (lane & 15), M - 1);
-      off[i] = (uint32_t)row * (uint32_t)K + 16 * (lane >> 4);
-    } else {
-      const int t = min(bn * BP + (p - AP), NTt - 1);
-      off[i] = (uint32_t)t * (uint32_t)KT * 1024u + lane * 16;
-    }
-  }
-  // DMA of stage st into slot st % R.  Stages past the last k-tile re-load the last k-tile into
-  // their slot (never read again: every stage still to be read sits in another slot), so every
-  // stage is PPW pieces per wave, the loop is branch-free and the vmcnt counts are constants.
-  auto issue_piece = [&](int st, int i) {
-    const int kt = min(st, KT - 1);
-    const bool isa = wave + NWV * i < AP;
-    glds16((isa ? A + (size_t)kt * (APK ? 1024 : 64) : Wp + (size_t)kt * 1024) + off[i],
-           ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
-  };
-  auto issue = [&](int st) {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) issue_piece(st, i);
-  };
-  // fragment reads: one VGPR base per operand and slot, immediate offsets
-  const uint32_t ring0 = lds_off(ring) + lane * 16;
-  const uint32_t wbase = ring0 + (AP + wn * NJ) * 1024, abase = ring0 + wm * MI * 1024;
-  auto read_frags = [&](int st, v4i (&fw)[NJ], v4i (&fa)[MI]) {
-    const uint32_t so = (st % R) * STAGE;
-    const uint32_t wb = wbase + so, ab = abase + so;
-    lds_read_row<NJ>(wb, fw);
-    lds_read_row<MI>(ab, fa);
-  };
-  auto pin = [&](v4i (&fw)[NJ], v4i (&fa)[MI]) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(fw[j]));
-#pragma unroll
-    for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(fa[i]));
-  };
-
-  v4i acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
-  // fragments pinned after the reads that precede this call, accumulators pinned after the
-  // MFMAs: the MFMAs sit between the fragment reads and the next lgkmcnt wait (left alone,
-  // hipcc hoists the wait above them and the LDS latency is exposed every k-tile)
-  auto mma = [&](v4i (&fw)[NJ], v4i (&fa)[MI]) {
-    pin(fw, fa);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_i8(fw[j], fa[i], acc[i][j]);
-  };
-  auto pin_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(acc[i][j]));
-  };
-
-  // prologue: R stages in flight, stage 0's fragments in registers
-#pragma unroll
-  for (int st = 0; st < R; ++st) issue(st);
-  v4i w0[NJ], a0[MI], w1[NJ], a1[MI];
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 1) * PPW) : "memory");
-  __builtin_amdgcn_s_barrier();
-  read_frags(0, w0, a0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-  // k-tile s < KT - 1: stage s + 1's fragments -> (wx, ax) while the MFMAs consume (wc, ac):
-  // reads -> MFMAs -> lgkmcnt(0), the wave's own MFMAs cover the LDS latency (measured 3-8 %
-  // faster than reads -> lgkmcnt(0) -> MFMAs, where only the SIMD's other wave covers it)
-  auto full = [&](int s, v4i (&wc)[NJ], v4i (&ac)[MI], v4i (&wx)[NJ], v4i (&ax)[MI]) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 2) * PPW) : "memory");   // own DMA of s + 1
-    __builtin_amdgcn_s_barrier();                     // stage s + 1 landed everywhere; slot of s free
-    if constexpr (ISS == 0) issue(s + R);
-    read_frags(s + 1, wx, ax);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    if constexpr (ISS == 2) {
-      // DMA pieces interleaved into the MFMA stream: piece g after MFMA group g (a glds that
-      // stalls on a full memory queue then holds back only the MFMAs behind it)
-      pin(wc, ac);
-      constexpr int TOT = MI * NJ, GRP = TOT / (PPW + 1);
-#pragma unroll
-      for (int f = 0; f < TOT; ++f) {
-        const int i = f / NJ, j = f % NJ;
-        acc[i][j] = mfma_i8(wc[j], ac[i], acc[i][j]);
-        if ((f + 1) % GRP == 0 && (f + 1) / GRP <= PPW) {
-          asm volatile("" : "+v"(acc[i][j])::"memory");   // this MFMA issued before the piece
-          issue_piece(s + R, (f + 1) / GRP - 1);
-        }
-      }
-    } else {
-      mma(wc, ac);
-    }
-    pin_acc();
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    if constexpr (ISS == 1) {
-      asm volatile("" ::: "memory");                  // the pieces after every MFMA of the k-tile
-      issue(s + R);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  int s = 0;
-  for (; s + 2 < KT; s += 2) {
-    full(s, w0, a0, w1, a1);
-    full(s + 1, w1, a1, w0, a0);
-  }
-  if (s + 1 < KT) {
-    full(s, w0, a0, w1, a1);
-    mma(w1, a1);
-  } else {
-    mma(w0, a0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-load stages past the end
-
-  // epilogue: lane holds int32 out[row = rb*16 + (lane & 15)][col = tile*16 + 4 (lane >> 4) + r].
-  // The raw accumulators go to LDS first (one 16-B write per tile, freeing their registers), in
-  // halves of MI/2 row blocks per wave ([MI*8 rows][64 cols] int32, 256-B rows, 16-B chunk c of
-  // row m at c ^ (m & 15): conflict-free); each lane then owns 8 consecutive columns (its scales
-  // and bias loaded once), scales, packs bf16 and writes 16 B.
-  const int r16 = lane & 15, g4 = lane >> 4, c8 = lane & 7;
-  const int col0 = bn * BNV + wn * 64 + c8 * 8;
-  const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
-  float swv[8], bv[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int col = min(col0 + e, N - 1);
-    swv[e] = sw[col];
-    bv[e] = bf2f(bp[bias != nullptr ? col : 0]);        // absent bias: a zero word, no branch
-  }
-  __syncthreads();                                    // every wave is done with the ring
-  int8_t* wt = ring + wave * (MI * 8 * 256);
-  constexpr int HALF = MI / 2;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int i = 0; i < HALF; ++i) {
-      const int m = i * 16 + r16;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        *reinterpret_cast<v4i*>(wt + m * 256 + (((4 * j + g4) ^ (m & 15)) << 4)) = acc[h * HALF + i][j];
-    }
-    // (a wave's LDS operations complete in issue order: no wait between its writes and reads)
-#pragma unroll
-    for (int it = 0; it < HALF * 2; ++it) {
-      const int m = it * 8 + (lane >> 3);
-      const int row = bm * BMV + wm * MI * 16 + h * HALF * 16 + m;
-      const float sr = sa[min(row, M - 1)];
-      const v4i lo = *reinterpret_cast<const v4i*>(wt + m * 256 + (((2 * c8) ^ (m & 15)) << 4));
-      const v4i hi = *reinterpret_cast<const v4i*>(wt + m * 256 + (((2 * c8 + 1) ^ (m & 15)) << 4));
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = (float)lo[e] * sr * swv[e] + bv[e];
-        v[e + 4] = (float)hi[e] * sr * swv[e + 4] + bv[e + 4];
-      }
-      if (row < M && col0 < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col0) = pack8(v);   // N % 8 == 0
-    }
-  }
-}
-
-// Fragment-pack A [M, K] int8 for the APK prefill GEMM: piece (rb, kt) = 1 KiB at
-// (rb * KT + kt) * 1024, lane l's 16 B = A[16 rb + (l & 15)][64 kt + 16 (l >> 4) ..] (rows past M
-// repeat row M - 1; the GEMM never stores them).  One thread per 16 B; writes are contiguous.
-__global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ A, int8_t* __restrict__ Ap, int M, int K,
-                                                     int KT, int64_t total) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= total) return;
-  const int64_t piece = t >> 6;
-  const int lane = (int)(t & 63);
-  const int rb = (int)(piece / KT), kt = (int)(piece - (int64_t)rb * KT);
-  const int row = min(rb * 16 + (lane & 15), M - 1);
-  *reinterpret_cast<uint4*>(Ap + t * 16) =
-      *reinterpret_cast<const uint4*>(A + (size_t)row * K + (size_t)kt * 64 + 16 * (lane >> 4));
-}
-
-// ------------------------------------------------------------------------------------ x32
-// Prefill GEMM on v_mfma_i32_32x32x32_i8 with 256 x 256 block tiles (M >= 256, K % 64 == 0,
-// N % 8 == 0).  The LDS image is the big kernel's (1 KiB pieces of 16 rows x 64 k, activations
-// row-major or fragment-packed, weights packed), 4 stages of 32 KiB; what changes is the MFMA:
-//  * 8 waves as 2 (tokens) x 4 (columns), each 128 tokens x 64 columns = 4 x 2 blocks of 32 x 32.
-//    Per 32-k step a wave reads 6 fragments (4 activation + 2 weight blocks) for 8 MFMAs, so the
-//    LDS reads per MFMA-cycle are those of a 128 x 64 wave tile: the big kernel's 16x16x64 form
-//    holds its 64 x 64 tile's k-tile fragments (32 VGPRs) x 2 buffers + 64 accumulators, and at
-//    128 x 64 it spilled; a 32-k step's fragments are 24 VGPRs, so 128 accumulators + two steps of
-//    fragments fit, and a k-tile costs 1024 MFMA cycles per CU against 32 KiB of DMA (31 B/clk)
-//    and ~125 B/clk of LDS traffic.
-//  * A 32 x 32 x 32 operand of 32 rows = two stacked 16-row pieces: lane l reads piece 2 b +
-//    ((l >> 4) & 1), 16 B of lane slot (l & 15) + 16 (2 s + (l >> 5)) — row l & 31, k 32 s + 16 (l >> 5)
-//    of the 64-k tile (conflict-free: each 16-lane group covers the 64 banks once).
-//  * Operands swapped as in the big kernel (weights = A operand): a lane's accumulator holds one
-//    token (l & 31) and 4 runs of 4 consecutive columns 8 q + 4 (l >> 5).  The epilogue restages
-//    32 tokens x 64 columns per wave at a time (int32, XOR-swizzled 16-B chunks) and writes 16-B
-//    bf16 row chunks.
-//  * The two waves of each SIMD are de-phased: waves 0-3 issue a stage's LDS-DMA pieces right after
-//    the barrier, waves 4-7 after their second MFMA step, so after every barrier one wave per SIMD
-//    runs MFMAs while the other issues DMA (+4-10 % over issuing together).
-//  * Measured against the 128 x 256 16x16x64 kernel (tools/bench_ops.py --only x32, Llama-2-7B shapes):
-//    2.17-2.30 vs 2.10-2.15 POPS at M = 16384, behind it at <= 384 tiles (qkv at M = 2048: 1.77 vs
-//    2.05), so the launcher takes it from 512 tiles (two full rounds of the 256 CUs).  The same
-//    kernel on bf16 operands (v_mfma_f32_32x32x16_bf16) ran 1.19-1.24 PF against hipBLASLt's
-//    1.46-1.61 PF and was dropped.
-template <bool APK>
-__global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
-                                                              const int8_t* __restrict__ Wp, const float* __restrict__ sw,
-                                                              const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
-                                                              int M, int N, int K, int KT, int NTt, int grid_m, int grid_n) {
-  constexpr int R = 4, BMV = 256, BNV = 256, NWV = 8;
-  constexpr int AP = BMV / 16, BP = BNV / 16, PIECES = AP + BP, PPW = PIECES / NWV, STAGE = PIECES * 1024;
-  static_assert(R * STAGE <= 160 * 1024 && NWV * 32 * 256 <= R * STAGE, "LDS budget");
-  __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
-
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  constexpr int GM = 4;
-  const int per_group = GM * grid_n;
-  const int grp = wgid / per_group, gm0 = grp * GM, gsz = min(GM, grid_m - gm0);
-  const int inr = wgid - grp * per_group;
-  const int bm = gm0 + inr % gsz, bn = inr / gsz;
-
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const bool late = wave >= 4;                        // DMA after the second MFMA step (see above)
-  uint32_t off[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int p = wave + NWV * i;
-    if (p < AP && APK) {
-      const int rb = min(bm * (BMV / 16) + p, (M + 15) / 16 - 1);
-      off[i] = (uint32_t)rb * (uint32_t)KT * 1024u + lane * 16;
-    } else if (p < AP) {
-      const int row = min(bm * BMV + p * 16 + (lane & 15), M - 1);
-      off[i] = (uint32_t)row * (uint32_t)K + 16 * (lane >> 4);
-    } else {
-      const int t = min(bn * BP + (p - AP), NTt - 1);
-      off[i] = (uint32_t)t * (uint32_t)KT * 1024u + lane * 16;
-    }
-  }
-  auto issue = [&](int st) {
-    const int kt = min(st, KT - 1);
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const bool isa = wave + NWV * i < AP;
-      glds16((isa ? A + (size_t)kt * (APK ? 1024 : 64) : Wp + (size_t)kt * 1024) + off[i],
-             ring + (st % R) * STAGE + (wave + NWV * i) * 1024);
-    }
-  };
-  // lane's byte in a 32-row operand block: piece offset ((l >> 4) & 1) KiB, lane slot
-  // (l & 15) + 16 (l >> 5) = row l & 15 of the piece, 16-B k chunk l >> 5 (k-step 0; k-step 1 is
-  // chunks 2, 3: 32 slots = 512 B further)
-  const uint32_t lo = (((lane >> 4) & 1) << 10) + (((lane & 15) + 16 * (lane >> 5)) << 4);
-  const uint32_t ring0 = lds_off(ring) + lo;
-  const uint32_t abase = ring0 + (wm * 8) * 1024, wbase = ring0 + (AP + wn * 4) * 1024;
-  // fragments of stage st, k-step ks: fa[c] = activation block c (tokens 32 c..), fw[b] = weight block b
-  auto read_frags = [&](int st, int ks, v4i (&fa)[4], v4i (&fw)[2]) {
-    const uint32_t so = (st % R) * STAGE + ks * 512;
-    const uint32_t ab = abase + so, wb = wbase + so;
-    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fa[0]) : "v"(ab));
-    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fa[1]) : "v"(ab));
-    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(fa[2]) : "v"(ab));
-    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(fa[3]) : "v"(ab));
-    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fw[0]) : "v"(wb));
-    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(fw[1]) : "v"(wb));
-  };
-  v16i acc[4][2];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[c][b][r] = 0;
-  auto mma = [&](v4i (&fa)[4], v4i (&fw)[2]) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(fa[c]));
-#pragma unroll
-    for (int b = 0; b < 2; ++b) asm volatile("" : "+v"(fw[b]));
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        acc[c][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[b], fa[c], acc[c][b], 0, 0, 0);
-      }
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) asm volatile("" : "+v"(acc[c][b]));
-  };
-
-#pragma unroll
-  for (int st = 0; st < R; ++st) issue(st);
-  v4i xa[4], xw[2], ya[4], yw[2];
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 1) * PPW) : "memory");
-  __builtin_amdgcn_s_barrier();
-  read_frags(0, 0, xa, xw);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  for (int kt = 0; kt < KT; ++kt) {                   // x: (kt, step 0) in registers
-    read_frags(kt, 1, ya, yw);
-    mma(xa, xw);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (kt + 1 < KT) {                                // wave-uniform
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 2) * PPW) : "memory");   // own DMA of kt + 1
-      __builtin_amdgcn_s_barrier();                   // kt + 1 landed everywhere; slot of kt free
-      if (!late) issue(kt + R);
-      read_frags(kt + 1, 0, xa, xw);
-    }
-    mma(ya, yw);
-    if (late && kt + 1 < KT) issue(kt + R);           // waves 4-7: behind this k-tile's second MFMA step
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-load stages past the end
-
-  // epilogue: acc[c][b] register r -> token wm*128 + 32 c + (l & 31), column
-  // wn*64 + 32 b + 8 (r >> 2) + 4 (l >> 5) + (r & 3).  Per c: the wave's 32 tokens x 64 columns of
-  // int32 go to its LDS block (256-B rows, 16-B chunk k of token t at k ^ (t & 15)), then each lane
-  // takes 8 consecutive columns (chunk pair lane & 7) of tokens it * 8 + (lane >> 3).
-  const int c8 = lane & 7, tl = lane & 31, hi = lane >> 5;
-  const int col0 = bn * BNV + wn * 64 + c8 * 8;
-  const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
-  float swv[8], bv[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int col = min(col0 + e, N - 1);
-    swv[e] = sw[col];
-    bv[e] = bf2f(bp[bias != nullptr ? col : 0]);
-  }
-  __syncthreads();                                    // every wave is done with the ring
-  int8_t* wt = ring + wave * (32 * 256);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int k16 = 8 * b + 2 * q + hi;           // 16-B chunk (4 int32 columns) of the 64
-        const v4i v4 = v4i{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]};
-        *reinterpret_cast<v4i*>(wt + tl * 256 + ((k16 ^ (tl & 15)) << 4)) = v4;
-      }
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int t = it * 8 + (lane >> 3);
-      const int row = bm * BMV + wm * 128 + c * 32 + t;
-      const float sr = sa[min(row, M - 1)];
-      const v4i lo4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8) ^ (t & 15)) << 4));
-      const v4i hi4 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((2 * c8 + 1) ^ (t & 15)) << 4));
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = (float)lo4[e] * sr * swv[e] + bv[e];
-        v[e + 4] = (float)hi4[e] * sr * swv[e + 4] + bv[e + 4];
-      }
-      if (row < M && col0 < N) *reinterpret_cast<uint4*>(out + (size_t)row * N + col0) = pack8(v);   // N % 8 == 0
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------- ring
-// 65-128 decode rows (two micro-batches or one 128-row micro-batch) on an LDS-DMA ring.
-// The ldsa kernel above stages activations through VGPRs (global load -> ds_write -> barrier) with
-// two steps in flight, ~96 KiB per CU: at 128 rows every CU also re-reads the whole 512 KiB
-// activation matrix from L2, and with ~2-3 us of loaded memory latency that in-flight budget caps
-// a CU at ~30 GB/s (qkv 25.8 us for 50 MB).  Here BOTH operands go global -> LDS by
-// global_load_lds (no VGPR round trip, no ds_write) into a ring of R stages of C k-tiles, R - 1
-// stages (~110 KiB) in flight per CU, one barrier per stage:
-//   wait own DMA of stage s (counted vmcnt) -> barrier (stage s landed everywhere, slot of s - 1
-//   free) -> DMA stage s + R - 1 into that slot -> MFMA over stage s.
-// A stage holds the 8 row blocks x C activation fragments, the NTW x C weight tiles and (SCALED)
-// the C k-tiles' per-(token, 64) scales.  4 waves; wave w owns row blocks {2w, 2w + 1} for all NTW
-// tiles (2 NTW accumulators), reading 2 activation + NTW weight fragments per k-tile from LDS —
-// no k-split inside the workgroup, so no LDS reduction; everything the epilogue needs from
-// global memory is loaded at kernel start.  EPI_PART: blockIdx = group * S + slice (fp32 partial
-// slices for the next RMSNorm); EPI_GLUQ: NTW = 8 (64 features), the row maxima are wave-local.
-// LDS reads of DMA-filled ring slots go through inline asm: the compiler cannot tell ring slots
-// apart, and for a plain LDS load (or a fenced __syncthreads) it would wait for EVERY outstanding
-// LDS-DMA (vmcnt(0)), draining the ring each stage.  Ordering is explicit instead: counted vmcnt
-// for this wave's own DMA, a bare s_barrier for the other waves', lgkmcnt(0) before the MFMAs.
-
-// (Activation pieces here are 16 rows x 64 B fragments; tools/ingest_bw.hip measured that pattern
-// at ~18 B/clk/CU L2 -> LDS against ~60 for whole 128-B lines, which is why the ring2 kernel below
-// DMAs whole-line pieces.)  This kernel remains the 65-128-row form for per-token-scaled split-K.
-template <int NTW, int C, int R, bool SCALED, int EPI>
-__global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
-    const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
-    const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
-    int M, int N, int K, int NTt, int Mpad, int S, int KTC) {
-  constexpr int MB = 8, NWV = 4;
-  constexpr int APC = MB * C, WPC = NTW * C, SPC = SCALED ? (C + 1) / 2 : 0;
-  constexpr int PIECES = APC + WPC + SPC, STAGE = PIECES * 1024;
-  constexpr int PPW = PIECES / NWV, PEXTRA = PIECES % NWV;   // waves < PEXTRA issue PPW + 1 pieces
-  static_assert(R * STAGE <= 150 * 1024, "LDS ring budget");
-  static_assert(EPI != EPI_GLUQ || NTW == 8, "GLUQ: 8 tiles = 64 features per workgroup");
-  __shared__ __attribute__((aligned(1024))) int8_t ring[R * STAGE];
-  const int grp = EPI == EPI_PART ? (int)blockIdx.x / S : (int)blockIdx.x;
-  const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
-  const int kbeg = ks * KTC, KT = K / 64;
-  const int nt0 = grp * NTW;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int STEPS = (KTC + C - 1) / C;
-
-  // per-lane DMA sources of this wave's pieces (p = wave + i * NWV), advanced by k-tile
-  constexpr int PMAX = PPW + (PEXTRA ? 1 : 0);
-  const int8_t* src[PMAX];
-  int stride[PMAX], klocal[PMAX];
-#pragma unroll
-  for (int i = 0; i < PMAX; ++i) {
-    const int p = min(wave + i * NWV, PIECES - 1);
-    if (p < APC) {                            // activation fragment: row block p % MB
-      const int row = min((p % MB) * 16 + (lane & 15), M - 1);
-      src[i] = A + (size_t)row * K + (size_t)kbeg * 64 + 16 * (lane >> 4);
-      stride[i] = 64;
-      klocal[i] = p / MB;
-    } else if (p < APC + WPC) {                      // weight tile nt0 + q % NTW
-      const int q = p - APC;
-      src[i] = Wp + ((size_t)min(nt0 + q % NTW, NTt - 1) * KT + kbeg) * 1024 + lane * 16;
-      stride[i] = 1024;
-      klocal[i] = q / NTW;
-    } else {                                         // scales of k-tiles 2q, 2q + 1 (rows 4 x lane)
-      const int q = p - APC - WPC;
-      src[i] = reinterpret_cast<const int8_t*>(sa + (size_t)kbeg * Mpad + min(4 * (lane & 31), Mpad - 4));
-      stride[i] = Mpad * 4;
-      klocal[i] = 2 * q + (lane >> 5);
-    }
-  }
-  auto issue = [&](int st) {
-#pragma unroll
-    for (int i = 0; i < PMAX; ++i) {
-      if (i < PPW || wave < PEXTRA) {
-        const int p = wave + i * NWV;
-        const int kt = min(st * C + klocal[i], KTC - 1);   // past the slice: a valid, unused tile
-        glds16(src[i] + (size_t)kt * stride[i], ring + (st % R) * STAGE + p * 1024);
-      }
-    }
-  };
-  auto wait_ahead = [&](bool steady) {               // own DMA of the oldest stage landed
-    constexpr int NA = (R - 2) * (PPW + 1), NB = (R - 2) * PPW;
-    static_assert(NA < 64, "vmcnt range");
-    if (steady) {
-      if (wave < PEXTRA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  };
-
-  // epilogue operands, loaded now (the tail of the kernel never waits on memory)
-  float sw_t[NTW], b_t[NTW], sa_r[2][4];
-#pragma unroll
-  for (int t = 0; t < NTW; ++t) {
-    const int col = min((nt0 + t) * 16 + (lane & 15), N - 1);
-    sw_t[t] = sw[col];
-    b_t[t] = bias != nullptr ? bf2f(bias[col]) : 0.f;
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) sa_r[j][q] = SCALED ? 1.f : sa[min((2 * wave + j) * 16 + 4 * (lane >> 4) + q, M - 1)];
-
-  v4i acc[2][NTW];
-  v4f accf[2][NTW];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) { acc[j][t] = v4i{0, 0, 0, 0}; accf[j][t] = v4f{0.f, 0.f, 0.f, 0.f}; }
-
-#pragma unroll
-  for (int st = 0; st < R - 1; ++st)
-    if (st < STEPS) issue(st);
-  const uint32_t ring0 = lds_off(ring);
-  for (int s = 0; s < STEPS; ++s) {
-    wait_ahead(s + R - 2 < STEPS);
-    __builtin_amdgcn_s_barrier();
-    if (s + R - 1 < STEPS) issue(s + R - 1);
-    const uint32_t base = ring0 + (s % R) * STAGE;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (s * C + c < KTC) {                          // wave-uniform
-        v4i a[2], b[NTW];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) a[j] = lds_read16(base + (c * MB + 2 * wave + j) * 1024 + lane * 16);
-#pragma unroll
-        for (int t = 0; t < NTW; ++t) b[t] = lds_read16(base + (APC + c * NTW + t) * 1024 + lane * 16);
-        v4f sgv[2];
-        if constexpr (SCALED) {
-          const uint32_t scl = base + (APC + WPC + c / 2) * 1024 + (c & 1) * 512;
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            sgv[j] = __builtin_bit_cast(v4f, lds_read16(scl + ((2 * wave + j) * 16 + 4 * (lane >> 4)) * 4));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // the fragments' values are defined only after the wait: pin them behind it
-#pragma unroll
-        for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(a[j]));
-#pragma unroll
-        for (int t = 0; t < NTW; ++t) asm volatile("" : "+v"(b[t]));
-        if constexpr (SCALED) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(sgv[j]));
-        }
-        if constexpr (SCALED) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const v4f sg = sgv[j];
-#pragma unroll
-            for (int t = 0; t < NTW; ++t) fold(accf[j][t], mfma_i8(a[j], b[t], v4i{0, 0, 0, 0}), sg);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int t = 0; t < NTW; ++t) acc[j][t] = mfma_i8(a[j], b[t], acc[j][t]);
-        }
-      }
-    }
-  }
-
-  // epilogue: lane holds col (lane & 15) of each tile, rows 4 (lane >> 4) + q of its 2 row blocks
-  auto value = [&](int j, int t, int q) -> float {
-    return SCALED ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j][q];
-  };
-  if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      const int col = (nt0 + t) * 16 + (lane & 15);
-      if (nt0 + t >= NTt || col >= N) continue;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
-          if (row >= M) continue;
-          if constexpr (EPI == EPI_PART) {
-            reinterpret_cast<float*>(outv)[((size_t)ks * M + row) * N + col] =
-                value(j, t, q) * sw_t[t] + (ks == 0 ? b_t[t] : 0.f);
-          } else {
-            reinterpret_cast<bf16_t*>(outv)[(size_t)row * N + col] = f2bf(value(j, t, q) * sw_t[t] + b_t[t]);
-          }
-        }
-    }
-  } else {                                            // EPI_GLUQ: tiles (2p, 2p + 1) = (gate, up) of 16 features
-    const int Fo = N / 2, grp64 = nt0 / 8;
-    int8_t* hq = reinterpret_cast<int8_t*>(outv);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = (2 * wave + j) * 16 + 4 * (lane >> 4) + q;
-        float h[4], amax = 0.f;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          float g = bf2f(f2bf(value(j, 2 * p, q) * sw_t[2 * p] + b_t[2 * p]));     // the unfused GEMM output is bf16
-          float u = bf2f(f2bf(value(j, 2 * p + 1, q) * sw_t[2 * p + 1] + b_t[2 * p + 1]));
-          h[p] = g / (1.f + __expf(-g)) * u;
-          amax = fmaxf(amax, fabsf(h[p]));
-        }
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) amax = fmaxf(amax, __shfl_xor(amax, d, 64));
-        amax = fmaxf(amax, 1e-8f);
-        const bool live = nt0 + 7 < NTt;
-        if (live && row < M) {
-#pragma unroll
-          for (int p = 0; p < 4; ++p) hq[(size_t)row * Fo + (nt0 / 2 + p) * 16 + (lane & 15)] = quant_i8(h[p], 127.f / amax);
-        }
-        if (live && (lane & 15) == 0 && row < Mpad) os[(size_t)grp64 * Mpad + row] = row < M ? amax / 127.f : 0.f;
-      }
-  }
-}
-
 // ------------------------------------------------------------------------------------ ring2
 // 65-128 decode rows with DECOUPLED prefetch depths for the two operands.  Streaming weights from
 // HBM at full rate needs ~2.5-4 us of loaded latency covered, while the activation re-reads are
@@ -1533,8 +614,9 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // waves also DMA each stage's scales (one 1 KiB piece: 2 k-tiles x Mpad rows, lanes split over the
 // loader waves) into a third ring, and every k-tile's int32 MFMA result is folded in fp32.
 // EPI_PART: blockIdx = group * S + slice; slice ks reduces stages [NS ks / S, NS (ks + 1) / S).
-// WNT: weight DMA with the nontemporal cache policy (default); false = normal allocation, so the
-// other lane's read of the same layer can hit the memory-side cache (no default uses it)
+// Weights stream with the nontemporal cache policy (each byte is read once per step).
+// ROT: the k order is rotated per workgroup (65-128-row split-K, where the ~256 workgroups would
+// otherwise request the same activation lines at the same moment).
 // MS == 2 (129-256 rows, one 256-row decode micro-batch): the rows are cut into two halves of at
 // most 128 and each logical workgroup runs once per half.  The two halves of one weight panel are
 // blocks b and b + 8: under the observed round-robin dispatch they share an XCD, and the second
@@ -1552,17 +634,12 @@ __global__ void __launch_bounds__(256, 1) w8a8_gemv_ring_kernel(
 // (A restaged 16-B store epilogue — qkv's 12 x 8-B stores per lane as 6 x 16-B, gate_up's 8 x 4-B as
 // 2 x 16-B — measured neutral at 256 rows, 22.74 vs 22.77 us / 34.65 vs 34.69: the tail is not
 // store-issue bound here, so the direct per-fragment stores stay.)
-template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = true, bool SC = false, bool WNT = true, int MS = 1,
-          int NAL = 0, int NCW = 4, int DT = 0>
+template <int NTW, int NWL, int RW, int RA, int EPI, bool ROT = false, bool SC = false, int MS = 1, int NAL = 0,
+          int NCW = 4, int DT = 0>
 __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_kernel(
     const int8_t* __restrict__ A, const float* __restrict__ sa, const int8_t* __restrict__ Wp,
     const float* __restrict__ sw, const bf16_t* __restrict__ bias, void* __restrict__ outv, float* __restrict__ os,
-    int M, int N, int K, int NTt, int Mpad, int S = 1, int G = 0, int diag = 0) {
-  // diag (speed diagnostics only, results are garbage): 1 no activation DMA, 2 no weight DMA,
-  // 4 no MFMAs, 8 no LDS fragment reads and no MFMAs, 16 no epilogue, 32 exit at once, 64 the weight
-  // loaders re-read two k-tiles (weights L2-resident), 128 epilogue without its global stores.
-  // Scheduling A/B bits (results exact): 256 compute waves at s_setprio 1 for the whole loop, 512
-  // loader waves at s_setprio 1, 1024 s_setprio 1 around each k-tile's MFMA cluster
+    int M, int N, int K, int NTt, int Mpad, int S = 1, int G = 0) {
   constexpr int MB = 8, WST = 2 * NTW, WPW = WST / NWL, DW = RW - 1, DA = RA - 1, APW = 16 / NCW;
   constexpr int NTH = NCW == 8 ? NTW / 2 : NTW;       // tiles per compute wave
   // GLUQ: a compute wave's tiles must be whole 64-feature quant groups (4 gate/up pairs): NTH == 8
@@ -1602,7 +679,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     if ((j >> 1) >= gx || lbid >= G) return;          // whole workgroup: no barrier is left waiting
   }
   const int Ml = min(128, M - row0);                  // rows of this half (>= 1: MS == 2 only for M > 128)
-  if (diag & 32) return;                              // (diagnostic: launch + dispatch only)
   const int KT = K / 64, NSA = KT / 2;
   const int grp = EPI == EPI_PART ? lbid / S : lbid;
   const int ks = EPI == EPI_PART ? lbid % S : 0;
@@ -1640,9 +716,8 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
         const int8_t* ab = Ah + (size_t)phys(st) * 128;
 #pragma unroll
         for (int i = 0; i < APL; ++i)
-          if (!(diag & 1)) glds16(ab + aoff[i], aring + ((st % RA) * 16 + al * APL + i) * 1024);
+          glds16(ab + aoff[i], aring + ((st % RA) * 16 + al * APL + i) * 1024);
       };
-      if (diag & 512) __builtin_amdgcn_s_setprio(1);
       for (int st = 0; st < DA; ++st) issue(st);
       for (int s = 0; s < NS; ++s) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DA - 1) * APL) : "memory");   // own pieces of stage s
@@ -1665,19 +740,14 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     const uint32_t soff = (uint32_t)((lane >> 5) * Mpad + row0 + min(4 * (lane & 31), Mpad - row0 - 4));
     const bool smine = (lane % NWL) == lw;
     auto issue = [&](int st) {
-      const int p = (diag & 64) ? (phys(st) & 1) : phys(st);   // (diagnostic 64: L2-resident weights)
+      const int p = phys(st);
       const int8_t* wb = Wp + (size_t)p * 2048;
 #pragma unroll
-      for (int i = 0; i < WPW; ++i) {
-        if (diag & 2) continue;
-        if constexpr (WNT) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
-        else glds16(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
-      }
+      for (int i = 0; i < WPW; ++i) glds16_nt(wb + woff[i], wring + ((st % RW) * WST + lw * WPW + i) * 1024);
       if constexpr (SC) {
         if (smine) glds16(sa + (size_t)(2 * p) * Mpad + soff, sring + (st % RW) * 1024);
       }
     };
-    if (diag & 512) __builtin_amdgcn_s_setprio(1);
     for (int st = 0; st < DW; ++st) issue(st);
     for (int s = 0; s < NS; ++s) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DW - 1) * LPW) : "memory");   // own pieces of stage s
@@ -1698,7 +768,7 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       const int8_t* ab = Ah + (size_t)phys(st) * 128;
 #pragma unroll
       for (int i = 0; i < APW; ++i)
-        if (!(diag & 1)) glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
+        glds16(ab + aoff[i], aring + ((st % RA) * 16 + APW * wave + i) * 1024);
     }
   };
   // The MFMA operands are swapped (weight tile = A operand, activations = B): a lane's accumulator
@@ -1748,8 +818,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
       for (int j = 0; j < 2; ++j) f[2 + NTH + j][0] = lds_read4(s0 + (st % RW) * 1024 + c * 512 + j * 64);
     }
   };
-  const bool pflip = (diag & 1024) != 0;
-  if (diag & 256) __builtin_amdgcn_s_setprio(1);
   // DT == 2, the one-VALU fold: each k-tile's MFMA starts from the bit pattern of 1.5 * 2^23
   // (0x4B400000) instead of 0, so the int32 sum (|sum| <= 64 * 127^2 < 2^22) lands in the low
   // mantissa bits and the result, read as a float, is exactly 12582912 + sum: one v_fmac per
@@ -1779,7 +847,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   auto mma = [&](v4i (&f)[NF]) {
 #pragma unroll
     for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(f[i]));
-    if (pflip) __builtin_amdgcn_s_setprio(1);
     if constexpr (SC && DT == 2) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -1830,10 +897,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
 #pragma unroll
         for (int t = 0; t < NTH; ++t) asm volatile("" : "+v"(acc[j][t]));
     }
-    if (pflip) {
-      if (diag & 256) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
   };
   // barrier k certifies stage k (both operands) and frees the slots of stage k - 1
   auto sync_stage = [&](int st) {
@@ -1842,19 +905,18 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
     issue(st + DA);
   };
   v4i x[NF], y[NF];
-  const bool rd = !(diag & 8), mm = !(diag & 12);
   sync_stage(0);
-  if (rd) read_kt(0, 0, x);
+  read_kt(0, 0, x);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   for (int s = 0; s < NS; ++s) {                     // x holds k-tile (s, 0)
-    if (rd) read_kt(s, 1, y);
-    if (mm) mma(x);
+    read_kt(s, 1, y);
+    mma(x);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (s + 1 < NS) {                                 // wave-uniform
       sync_stage(s + 1);
-      if (rd) read_kt(s + 1, 0, x);
+      read_kt(s + 1, 0, x);
     }
-    if (mm) mma(y);
+    mma(y);
     if constexpr (DT == 2) {
       if ((s & 3) == 3 || s + 1 == NS) unbias();     // wave-uniform; the last stage always
     }
@@ -1862,7 +924,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if (diag & 16) return;                            // (diagnostic: no epilogue)
   // epilogue: lane holds row (2 wave + j) * 16 + (lane & 15), columns 4 (lane >> 4) .. + 3 of tile t
   const int g4 = 4 * (lane >> 4);
   if constexpr (EPI == EPI_OUT || EPI == EPI_PART) {
@@ -1881,7 +942,6 @@ __global__ void __launch_bounds__((NCW + NWL + NAL) * 64, 1) w8a8_gemv_ring2_ker
           const float a = SC || DT ? accf[j][t][q] : (float)acc[j][t][q] * sa_r[j];
           v[q] = a * epi_sw[cl + q] + ((EPI == EPI_OUT || ks == 0) ? epi_b[cl + q] : 0.f);
         }
-        if (diag & 128) { asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])); continue; }
         if constexpr (EPI == EPI_PART) {
           float* o = reinterpret_cast<float*>(outv) + ((size_t)ks * M + row) * N + col;
           if (col + 3 < N && (N & 3) == 0) *reinterpret_cast<v4f*>(o) = v4f{v[0], v[1], v[2], v[3]};
@@ -2247,20 +1307,8 @@ int launch_r256x(const void* Ap, const float* sa, const void* Wp, const float* s
 }  // namespace
 
 static int g_gemv_kw = 0, g_gemv_unroll = 0, g_gemv_ntw = 0, g_gemv_ring = 2;
-// prefill GEMM: 0 automatic, 1 the 128 x 128 two-buffer kernel, 2 / 3 the ring kernel (BM = 128)
-static int g_prefill_gemm = 0, g_prefill_iss = 2, g_prefill_apack = 1, g_prefill_prio = 0, g_prefill_x32 = 1;
-// the 256 x 256 x32 kernel: g_prefill_x32 0 never, 1 from 512 tiles (default), 2 from 192 tiles (tests)
-static bool x32_takes(int M, int grid_n) {
-  const int64_t tiles = (int64_t)((M + 255) / 256) * grid_n;
-  return g_prefill_x32 && M >= 256 && tiles >= (g_prefill_x32 == 2 ? 192 : 512);
-}
-// prefill_x32: 0 off, 1 the 256 x 256 32x32x32 kernel when the grid fills >= 1 round of CUs (M >= 256)
-extern "C" void edge_w8a8_prefill_x32(int v) { g_prefill_x32 = v; }
-extern "C" void edge_w8a8_prefill_prio(int v) { g_prefill_prio = v; }
-extern "C" void edge_w8a8_prefill_apack(int v) { g_prefill_apack = v; }
-// b: where the ring kernel issues a k-tile's DMA pieces (0 before its fragment reads, 1 after its
-// MFMAs, 2 interleaved into them: the default, 1-3 % ahead of 0 on the Llama-2-7B shapes)
-extern "C" void edge_w8a8_prefill_gemm(int v, int b) { g_prefill_gemm = v; g_prefill_iss = b; }
+extern "C" int edge_w8a8_prefill(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
+                                 void* out, int M, int N, int K, int KT, hipStream_t st);
 // tuning hooks (microbenchmarks): 0 = automatic choice
 extern "C" void edge_w8a8_gemv_config(int kw, int unroll) { g_gemv_kw = kw; g_gemv_unroll = unroll; }
 extern "C" void edge_w8a8_gemv_ntw(int ntw) { g_gemv_ntw = ntw; }
@@ -2287,76 +1335,41 @@ int launch_norm(const NormIn& na, const void* Wp, const float* sw, const void* b
   return (int)hipGetLastError();
 }
 
-template <int MB, int NTW, int TPW, int KH, int KPW, int D, int KTC, bool SC, int EP>
-int launch_ldsa(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
-                float* os, int M, int N, int K, int Mpad, hipStream_t st, int S = 1) {
-  const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_ldsa_kernel<MB, NTW, TPW, KH, KPW, D, KTC, SC, EP>),
-                     dim3((NTt + NTW - 1) / NTW * S), dim3(NTW / TPW * KH * 64), 0, st, (const int8_t*)A, sa,
-                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);
-  return (int)hipGetLastError();
-}
-
-template <int NTW, int C, int R, bool SC, int EP>
-int launch_ring(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
-                float* os, int M, int N, int K, int Mpad, hipStream_t st, int S, int KTC) {
-  const int NTt = (N + 15) / 16;
-  hipLaunchKernelGGL((w8a8_gemv_ring_kernel<NTW, C, R, SC, EP>), dim3((NTt + NTW - 1) / NTW * S), dim3(256), 0, st,
-                     (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S,
-                     KTC);
-  return (int)hipGetLastError();
-}
-
-// Ring kernels for 65-128 rows (geometries measured with tools/bench_ops.py --only ring):
-//  * grouped-scale split-K (o / down): ring2 with 8 compute waves (two per SIMD: the per-k-tile
-//    fold issues beside the partner's MFMAs), 2 weight + 2 activation loader waves, >= 4 stages
-//    per slice (down, K = 11008: 22.4 -> 20.1 us against the one-ring kernel);
-//  * qkv-like EPI_OUT (3 tiles) and the quantising GLU (8 tiles = one 64-feature group): ring2
-//    with dedicated weight loaders (the 2-lane bench 32.0k against 28.3k tok/s in round 2);
-//  * per-token-scaled split-K and the remaining shapes: the one-ring kernel (NTW for ~256 WGs).
-// -1: no ring kernel for this call.
+// 65-128 decode rows (two 64-row micro-batches, or one 128-row one) on the ring2 kernel (geometries
+// measured with tools/bench_ops.py --only ring):
+//  * split-K (o / down): 8 compute waves (two per SIMD: the grouped-scale per-k-tile fold issues
+//    beside the partner's MFMAs), 2 weight + 2 activation loader waves, >= 4 stages per slice
+//    (down, K = 11008: 22.4 -> 20.1 us against the earlier one-ring kernel);
+//  * qkv-like EPI_OUT (3 tiles) and the quantising GLU (8 tiles = one 64-feature group) with
+//    dedicated weight loaders (the 2-lane bench 32.0k against 28.3k tok/s in round 2).
+// K % 128 == 0 (split-K: >= 4 stages per slice; rows128_ok).  The quantising GLU takes it from 33
+// rows (gate_up at 64 rows: 26.6 us here against 33.9 for the weight-stationary GEMV; the ring's
+// surplus rows are clamped reads, never stored).  -1: no kernel for this call.
 template <int EP>
 int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                         float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
-  if (!g_gemv_ring || M <= 64 || M > 128 || K % 64 != 0 || (K / 64) % S != 0 || (EP == EPI_PART) != (S > 1)) return -1;
+  if (!g_gemv_ring || M <= (EP == EPI_GLUQ ? 32 : 64) || M > 128 || K % 128 != 0 || (EP == EPI_PART) != (S > 1))
+    return -1;
+  if (scaled && (Mpad < 16 || Mpad % 16 != 0)) return -1;
   const int NTt = (N + 15) / 16;
+#define RING2(NTWV, NWLV, RWV, RAV, EPV, SCV, NALV, NCWV, NW)                                                      \
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, EPV == EPI_PART, SCV, 1, NALV, NCWV>),  \
+                     dim3((NTt + NTWV - 1) / NTWV * S), dim3((NW) * 64), 0, st, (const int8_t*)A, sa,             \
+                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);               \
+  return (int)hipGetLastError()
   if constexpr (EP == EPI_PART) {
-    if (scaled && K % 128 == 0 && K / 128 >= 4 * S && Mpad >= 4 && Mpad % 4 == 0) {
-      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<4, 2, 8, 4, EPI_PART, true, true, true, 1, 2, 8>),
-                         dim3((NTt + 3) / 4 * S), dim3(12 * 64), 0, st, (const int8_t*)A, sa, (const int8_t*)Wp, sw,
-                         (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S);
-      return (int)hipGetLastError();
-    }
+    if (K / 128 < 4 * S) return -1;
+    if (scaled) { RING2(4, 2, 8, 4, EPI_PART, true, 2, 8, 12); }
+    RING2(4, 2, 8, 4, EPI_PART, false, 2, 8, 12);
+  } else if constexpr (EP == EPI_GLUQ) {
+    if (scaled || N % 128 != 0) return -1;
+    RING2(8, 4, 5, 4, EPI_GLUQ, false, 0, 4, 8);
+  } else if constexpr (EP == EPI_OUT) {
+    if (scaled) { RING2(3, 3, 12, 4, EPI_OUT, true, 0, 4, 7); }   // (the scale ring: 2 weight stages fewer)
+    RING2(3, 3, 14, 4, EPI_OUT, false, 0, 4, 7);
   }
-  if (!scaled && S == 1 && K % 128 == 0) {
-    if constexpr (EP == EPI_GLUQ) {
-      if (N % 128 == 0) {
-        hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<8, 4, 5, 4, EPI_GLUQ, false>), dim3((NTt + 7) / 8), dim3(8 * 64), 0,
-                           st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt,
-                           Mpad, 1);
-        return (int)hipGetLastError();
-      }
-    } else if constexpr (EP == EPI_OUT) {
-      hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<3, 3, 14, 4, EPI_OUT, false>), dim3((NTt + 2) / 3), dim3(7 * 64), 0,
-                         st, (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt,
-                         Mpad, 1);
-      return (int)hipGetLastError();
-    }
-  }
-  // per-(token, 64) scales with a short K: the per-k-tile fold serialises the MFMAs and the ring
-  // form measured slower than the LDS-staged kernel (o + down 24.8 us avg vs 12.1 / 22.3): off
-  if (scaled) return -1;
-  const int KTC = K / 64 / S;
-  if constexpr (EP == EPI_GLUQ) {
-    if (N % 128 != 0) return -1;
-    return launch_ring<8, 1, 8, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-  } else {
-    const int ntw = g_gemv_ntw > 0 ? g_gemv_ntw : max(1, min(4, (NTt * S + 128) / 256));
-    if (ntw == 1) return launch_ring<1, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-    if (ntw == 2) return launch_ring<2, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-    if (ntw == 3) return launch_ring<3, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-    return launch_ring<4, 2, 6, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S, KTC);
-  }
+#undef RING2
+  return -1;
 }
 
 // 129-256 rows (one 256-row decode micro-batch): ring2 with the rows cut in two halves that stream
@@ -2372,22 +1385,13 @@ int launch_ring_rows128(const void* A, const float* sa, const void* Wp, const fl
 //  * quantising gate_up: one round of 16-tile workgroups, 8 compute waves each owning one
 //    64-feature group (43.7 -> 34.7 us against two rounds of 8-tile ones);
 //  * qkv-like EPI_OUT: 3 tiles for N <= 8192, 6 for qkv-sized N, 8 beyond.
-static int g_r256_diag = 0, g_r256_rot = 0;
 template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int EPV, bool SCV, int NCWV = 4, int DTV = 0>
 int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out, float* os,
                 int M, int N, int K, int Mpad, hipStream_t st, int S) {
   const int NTt = (N + 15) / 16, G = (NTt + NTWV - 1) / NTWV * S;
-  // A/B: k order rotated per workgroup (the 32 CUs of an XCD then do not request the same
-  // activation lines at the same moment)
-  if (g_r256_rot) {
-    hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, true, SCV, true, 2, NALV, NCWV, DTV>),
-                       dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
-                       (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, true, 2, NALV, NCWV, DTV>),
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, SCV, 2, NALV, NCWV, DTV>),
                      dim3((G + 7) / 8 * 16), dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, sa,
-                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G, g_r256_diag);
+                     (const int8_t*)Wp, sw, (const bf16_t*)bias, out, os, M, N, K, NTt, Mpad, S, G);
   return (int)hipGetLastError();
 }
 
@@ -2417,9 +1421,6 @@ int launch_rows256(const void* A, const float* sa, const void* Wp, const float* 
   return -1;
 }
 
-// 65-128 rows (two decode micro-batches in one): LDS-staged activations, one tile per wave, 8 row
-// blocks of accumulators.  Instantiated for the k-tile counts of the 4096-hidden models (K = 4096
-// whole, and K = 4096 / 11008 / 14336 in 4 split-K slices); -1 = no kernel for this shape.
 }  // namespace
 
 // 129-256 decode rows on FRAGMENT-PACKED activations (w8a8_r256_kernel; the producers write the
@@ -2446,8 +1447,6 @@ extern "C" int edge_w8a8_r256(const void* Ap, const float* sa, const void* Wp, c
 #undef R256
 }
 
-extern "C" void edge_w8a8_rows256_diag(int v) { g_r256_diag = v; }
-extern "C" void edge_w8a8_rows256_rot(int v) { g_r256_rot = v; }
 // split-K slices the 129-256-row kernels use for a K (0: none): 2 for o-like K, 4 for down-like K
 // (fewer slices also cut the fp32 partial bytes the next RMSNorm reads;
 // profiles/bench_r3_down_splits_ab.jsonl, bench_r3_i8_o_splits_ab.jsonl)
@@ -2455,36 +1454,13 @@ extern "C" int edge_w8a8_rows256_splits(int K) { return K % 128 != 0 ? 0 : (K / 
 // whether the 129-256-row decode kernels take this K (whole K; split-K at rows256_splits(K))
 extern "C" int edge_w8a8_rows256_ok(int K) { return K % 128 == 0 && K / 128 >= 8; }
 
-// k-tile counts launch_rows128 has kernels for: the whole K (S = 1) or each of S split-K slices
+// whether the 65-128-row decode kernels (launch_ring_rows128) take this K: the whole K (S = 1) or S
+// split-K slices of >= 4 stages of 128 k
 extern "C" int edge_w8a8_rows128_ok(int K, int S) {
-  if (K <= 0 || S < 1 || K % 64 != 0 || (K / 64) % S != 0) return 0;
-  const int ktc = K / 64 / S;
-  return S > 1 ? (ktc == 16 || ktc == 43 || ktc == 56) : ktc == 64;
+  return K > 0 && S >= 1 && K % 128 == 0 && (S == 1 || K / 128 >= 4 * S);
 }
 
 namespace {
-template <int EP>
-int launch_rows128(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
-                   float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
-  {
-    const int r = launch_ring_rows128<EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, scaled, st, S);
-    if (r != -1) return r;
-  }
-  if (!edge_w8a8_rows128_ok(K, S) || (EP == EPI_PART) != (S > 1)) return -1;
-  const int ktc = K / 64 / S;
-#define R128(KTC)                                                                                                   \
-  if (ktc == KTC)                                                                                                   \
-    return scaled ? launch_ldsa<8, 4, 1, 4, 1, 2, KTC, true, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S) \
-                  : launch_ldsa<8, 4, 1, 4, 1, 2, KTC, false, EP>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st, S);
-  if constexpr (EP == EPI_PART) {
-    R128(16) R128(43) R128(56)
-  } else {
-    R128(64)
-  }
-#undef R128
-  return -1;
-}
-
 // EPI_OUT: 16 waves; KW = 16 while the LDS reduction fits (KW x NTW x MB KiB <= 128 KiB), else 8
 template <int MB, int AM>
 int launch_out(int ntw, int un, int kw, const void* A, const float* sa, const void* Wp, const float* sw,
@@ -2529,7 +1505,7 @@ extern "C" int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void*
     return r == -1 ? -2 : r;
   }
   if (M > 64) {
-    const int r = launch_rows128<EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, S);
+    const int r = launch_ring_rows128<EPI_PART>(A, sa, Wp, sw, bias, part, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, S);
     return r == -1 ? -2 : r;
   }
   // 2 tiles per workgroup for one row block, 4 for more (the binding sizes S for ~256 workgroups;
@@ -2597,7 +1573,7 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
   const int mblocks = (M + 15) / 16;
   if (a_mode == A_GROUP && Mpad < mblocks * 16) return -2;
   if (M > 64 && M <= 128 && epi == EPI_OUT && g_gemv_unroll != 1) {
-    const int r = launch_rows128<EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, 1);
+    const int r = launch_ring_rows128<EPI_OUT>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, Mpad, a_mode == A_GROUP, st, 1);
     if (r != -1) return r;
   }
   if (M > 128 && M <= 256 && (epi == EPI_OUT || epi == EPI_GLUQ) && a_mode == A_TOKEN && g_gemv_ring) {
@@ -2622,8 +1598,7 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
 #undef GQ
   }
   if (epi == EPI_GLU || epi == EPI_GLUQ) {
-    const bool ldsa = KT == 64 && K == 4096 && N % 128 == 0 && g_gemv_unroll != 1;
-    if (a_mode != A_TOKEN || M > (epi == EPI_GLUQ && ldsa ? 128 : 64) || N % (epi == EPI_GLUQ ? 128 : 32) != 0)
+    if (a_mode != A_TOKEN || M > (epi == EPI_GLUQ ? 128 : 64) || N % (epi == EPI_GLUQ ? 128 : 32) != 0)
       return -2;
     if (epi == EPI_GLUQ) {
       if (os == nullptr || Mpad < mblocks * 16) return -2;
@@ -2637,16 +1612,10 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
         return launch_one<1, 8, 2, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
       }
       if (mblocks <= 2) return launch_one<2, 8, 1, 8, 2, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
-      if (mblocks > 4) {
+      {
         const int r = launch_ring_rows128<EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, false, st, 1);
         if (r != -1) return r;
-      }
-      // K = 4096: activations staged in LDS (unroll knob 1 = the weight-stationary form)
-      if (ldsa) {
-        // 128 rows: 2 steps of prefetch (4 steps: 37.7 us, 4 k-tiles per wave-step: 40.9 us, against 35.8)
-        if (mblocks > 4) return launch_ldsa<8, 8, 1, 2, 2, 2, 64, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st);
-        if (g_gemv_kw == 2) return launch_ldsa<4, 8, 2, 4, 1, 4, 64, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st);
-        return launch_ldsa<4, 8, 1, 2, 4, 2, 64, false, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, st);
+        if (mblocks > 4) return -2;
       }
       // (4 waves with U = 2 / 4 and AGPR accumulators measured 45.6 / 41.4 us against 34.3 us here)
       return launch_one<4, 8, 1, 8, 1, A_TOKEN, EPI_GLUQ>(A, sa, Wp, sw, bias, out, os, M, N, K, KT, Mpad, st);
@@ -2655,39 +1624,8 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
     if (mblocks <= 2) return launch_one<2, 4, 2, 8, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
     return launch_one<4, 4, 2, 4, 2, A_TOKEN, EPI_GLU>(A, sa, Wp, sw, bias, out, nullptr, M, N, K, KT, Mpad, st);
   }
-  if (M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1) {   // (see edge_w8a8_gemm_apk)
-    // 128 x 256 tiles.  (The 256 x 256 form measured 2.21 vs 2.11 POPS on the K = 11008 down
-    // projection at M = 16384, but at 256 VGPRs it spilled ~290 B per lane, and spill traffic joins
-    // the ring's counted vmcnt — the same hazard that broke a decode kernel — so it is gone.)
-    const int grid_n = (NTt * 16 + 255) / 256;
-    const int grid_m = (M + 127) / 128;
-    if (x32_takes(M, grid_n)) {
-      const int gm2 = (M + 255) / 256;
-      hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A, sa,
-                         (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
-      return (int)hipGetLastError();
-    }
-#define BIGK(BMV, ISS)                                                                                           \
-  hipLaunchKernelGGL((w8a8_gemm_big_kernel<BMV, ISS>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)A, sa, \
-                     (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n)
-    const int iss = g_prefill_iss;
-    if (g_prefill_prio && iss == 2) {
-      hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, false, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
-                         (const int8_t*)A, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
-                         grid_m, grid_n);
-      return (int)hipGetLastError();
-    }
-    if (iss == 1) BIGK(128, 1); else if (iss == 2) BIGK(128, 2); else BIGK(128, 0);
-#undef BIGK
-    return (int)hipGetLastError();
-  }
-  if (M > 64 && K % 64 == 0 && K / 64 == KT) {
-    const int grid_n = (NTt * 16 + BN - 1) / BN;
-    const int grid_m = (M + BM - 1) / BM;
-    hipLaunchKernelGGL(w8a8_gemm_tiled_kernel, dim3(grid_n * grid_m), dim3(NT), 2 * 16384, st, (const int8_t*)A, sa,
-                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_n);
-    return (int)hipGetLastError();
-  }
+  if (M > 64 && K % 64 == 0 && K / 64 == KT && N % 8 == 0)       // prefill (gemm_i8_prefill.hip)
+    return edge_w8a8_prefill(A, sa, Wp, sw, bias, out, M, N, K, KT, st);
   if (M > 64) {
     // ragged-K prefill (tiny models): 64-row slabs through the GEMV
     for (int m0 = 0; m0 < M; m0 += 64) {
@@ -2714,45 +1652,6 @@ extern "C" int edge_w8a8_gemm(const void* A, const float* sa, const void* Wp, co
 #undef OUT
 }
 
-// Prefill GEMM with A fragment-packed first (APK form of w8a8_gemm_big_kernel).  Ap: scratch of
-// (M + 15) / 16 * 16 * K bytes from the caller's (stream-ordered) allocator.  Returns -2 when the
-// shape does not take the ring GEMM (the caller then runs edge_w8a8_gemm).
-// g_prefill_apack: 0 off, 1 automatic, 2 always.  Automatic = wide N at >= 2048 rows, where every A
-// panel is re-read by >= 32 column blocks (tools/bench_ops.py pgemm, Llama-2-7B shapes: gate_up
-// 1.91 -> 2.10 POPS and qkv 1.96 -> 2.04 at M = 16384; at N = 4096 or M = 512 the extra pass over
-// A costs more than the contiguous pieces save, o at M = 2048 1.85 -> 1.69)
-extern "C" int edge_w8a8_apack_ok(int M, int N, int K, int KT) {
-  const bool want = g_prefill_apack == 2 || (g_prefill_apack == 1 && N >= 8192 && M >= 2048);
-  return want && M > 128 && K % 64 == 0 && K / 64 == KT && N % 8 == 0 && g_prefill_gemm != 1 &&
-         (int64_t)((M + 15) / 16) * KT * 1024 < (int64_t)1 << 32;
-}
-
-extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw,
-                                  const void* bias, void* out, int M, int N, int K, int KT, hipStream_t st) {
-  if (!edge_w8a8_apack_ok(M, N, K, KT)) return -2;
-  const int64_t total = (int64_t)((M + 15) / 16) * KT * 64;
-  hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const int8_t*)A,
-                     (int8_t*)Ap, M, K, KT, total);
-  const int NTt = (N + 15) / 16;
-  const int grid_n = (NTt * 16 + 255) / 256;
-  const int grid_m = (M + 127) / 128;
-  if (x32_takes(M, grid_n)) {
-    const int gm2 = (M + 255) / 256;
-    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap, sa,
-                       (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
-    return (int)hipGetLastError();
-  }
-  if (g_prefill_prio)
-    hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
-                       (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
-                       grid_m, grid_n);
-  else
-    hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, 2, true>), dim3(grid_m * grid_n), dim3(512), 0, st,
-                       (const int8_t*)Ap, sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt,
-                       grid_m, grid_n);
-  return (int)hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------ bf16 ring2
 // bf16 decode projections at 17-256 rows on the ring2 kernel (DT = 1).  The bf16 fragment-packed
 // weight (ops.pack_bf16_weight: 1 KiB tiles of 16 rows x 32 k) and a row-major bf16 activation
@@ -2770,9 +1669,9 @@ template <int NTWV, int NWLV, int RWV, int RAV, int NALV, int NCWV, int EPV, int
 int launch_bfr(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int S, hipStream_t st) {
   const int NTt = N / 16, G = (NTt + NTWV - 1) / NTWV * S;
   const dim3 grid(MSV == 2 ? (G + 7) / 8 * 16 : G);
-  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, false, true, MSV, NALV, NCWV, 1>), grid,
+  hipLaunchKernelGGL((w8a8_gemv_ring2_kernel<NTWV, NWLV, RWV, RAV, EPV, false, false, MSV, NALV, NCWV, 1>), grid,
                      dim3((NCWV + NWLV + NALV) * 64), 0, st, (const int8_t*)A, nullptr, (const int8_t*)W, nullptr,
-                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G, 0);
+                     (const bf16_t*)bias, out, nullptr, M, N, 2 * K, NTt, 0, S, G);
   return (int)hipGetLastError();
 }
 

@@ -116,8 +116,8 @@ class W8A8Linear(nn.Module):
     def takes_packed(self, M: int) -> bool:
         """Whether this projection takes a fragment-packed activation at M rows (the 256-row decode
         GEMM on the GPU: ops.r256_ok; not split-K outputs, not the GLU projection)."""
-        return (self.w_packed.is_cuda and not self.split_k_out and not self.glu_blocked and
-                ops.r256_ok(M, self.out_features, self.in_features))
+        return (self.w_packed.is_cuda and ops.gpu_path(self.w_packed) and not self.split_k_out and
+                not self.glu_blocked and ops.r256_ok(M, self.out_features, self.in_features))
 
     def forward(self, x, add=None):
         """``add``: the other branch of a parallel-residual block, added to the output (in the

@@ -199,8 +199,8 @@ def test_w8a8_gemm(cuda, M, N, K):
     _close(out, ref, 1e-2, 1e-2)
 
 
-PREFILL_FORMS = {"auto": (0, 2), "tiled128": (1, 0), "ring256": (2, 0), "ring128": (3, 0), "ring256_late": (2, 1),
-                 "ring128_late": (3, 1), "ring256_ilv": (2, 2), "ring128_ilv": (3, 2)}
+# prefill_x32 knob: 1 = automatic (x32 from 512 tiles), 0 = the 128 x 256 ring kernel only, 2 = x32 from 192 tiles
+PREFILL_FORMS = {"auto": 1, "big": 0, "x32": 2}
 
 
 @pytest.mark.parametrize("apack", [0, 2])
@@ -218,11 +218,11 @@ def test_w8a8_prefill_layout_exact(cuda, apack, form, M, N, K):
     w = (torch.arange(N * K, device=cuda).view(N, K) % 113 - 56).to(torch.int8)
     wp = ops.pack_int8_weight(w)
     try:
-        C.tune("prefill_gemm", *PREFILL_FORMS[form])
+        C.tune("prefill_x32", PREFILL_FORMS[form], 0)
         C.tune("prefill_apack", apack, 0)
         out = C.w8a8_gemm(a, torch.ones(M, device=cuda), wp, torch.ones(N, device=cuda), None, N, K)
     finally:
-        C.tune("prefill_gemm", 0, 2)
+        C.tune("prefill_x32", 1, 0)
         C.tune("prefill_apack", 1, 0)
     assert torch.equal(out.float(), w[:, sel].t().float())
 
@@ -241,11 +241,11 @@ def test_w8a8_prefill_gemm(cuda, apack, form, M, N, K):
     bias = torch.randn(N, device=cuda, generator=g).bfloat16()
     wp = ops.pack_int8_weight(w)
     try:
-        C.tune("prefill_gemm", *PREFILL_FORMS[form])
+        C.tune("prefill_x32", PREFILL_FORMS[form], 0)
         C.tune("prefill_apack", apack, 0)
         out = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
     finally:
-        C.tune("prefill_gemm", 0, 2)
+        C.tune("prefill_x32", 1, 0)
         C.tune("prefill_apack", 1, 0)
     _close(out, _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32), 1e-2, 1e-2)
 

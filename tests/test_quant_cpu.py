@@ -95,26 +95,26 @@ def test_checkpoint_roundtrip(tmp_path, mode):
 
 
 def test_decode_rows_capability_table():
-    """The 65-128 row decode GEMVs exist for the k-tile counts of the 4096-hidden models only: the
-    Python gates (grouped attention output, split-K, fused GLU) must agree with the kernel table."""
+    """The 65-256 row decode kernels (ring2) take K % 128 == 0 (split-K: >= 4 stages of 128 k per
+    slice at 65-128 rows): the Python gates (grouped attention output, split-K, fused GLU) must
+    agree with the kernel table."""
     from edgellm import ops
     if not ops.available():
         pytest.skip("extension not built")
     assert all(ops.decode_rows_ok(M, K) for M in (1, 17, 64) for K in (64, 1000, 11008))
-    assert ops.decode_rows_ok(128, 4096) and ops.decode_rows_ok(65, 4096)
-    assert not ops.decode_rows_ok(100, 11008)
+    assert ops.decode_rows_ok(128, 4096) and ops.decode_rows_ok(65, 4096) and ops.decode_rows_ok(100, 11008)
+    assert not ops.decode_rows_ok(100, 1000) and not ops.decode_rows_ok(65, 4160)
     # 129-256 rows: the row-split ring2 kernels, any K % 128 == 0 with >= 8 stages
     assert ops.decode_rows_ok(129, 4096) and ops.decode_rows_ok(256, 11008, 4) and ops.decode_rows_ok(256, 1024)
     assert not ops.decode_rows_ok(257, 4096) and not ops.decode_rows_ok(200, 1000) and not ops.decode_rows_ok(200, 896)
-    for K in (4096, 11008, 14336):                      # o / down of Llama-2-7B, down of Llama-3-8B
+    for K in (2048, 4096, 11008, 14336):                # o / down of 2048-hidden models, Llama-2-7B, Llama-3-8B
         assert ops.decode_rows_ok(128, K, 4)
-    assert not ops.decode_rows_ok(128, 2048, 4)
+    assert not ops.decode_rows_ok(128, 1024, 4)         # 8 stages over 4 slices: < 4 per slice
     lin = W8A8Linear(11008, 4096, bias=False)
-    assert not lin.group_scales_ok(128)                 # whole-K 11008 at 128 rows: no kernel
-    lin.split_k_out = 4
     assert lin.group_scales_ok(128) and lin.group_scales_ok(64)
     up = W8A8Linear(4096, 22016, bias=False)
-    assert up.glu_rows_ok(128) and not W8A8Linear(2048, 11008, bias=False).glu_rows_ok(100)
+    assert up.glu_rows_ok(128) and W8A8Linear(2048, 11008, bias=False).glu_rows_ok(100)
+    assert not W8A8Linear(1000, 11008, bias=False).glu_rows_ok(100)
 
 
 @pytest.mark.parametrize("bounds", [[0, 3, 8], [0, 5, 11, 16]])

@@ -366,44 +366,6 @@ def rows256_rows(C, dev, M=256):
         del wps
     return out
 
-def rows256_diag(C, dev, M=256):
-    """Where a 256-row decode GEMM's time goes: the same launch with parts of the ring switched off
-    (tune ring2_256_diag: 1 no activation DMA, 2 no weight DMA, 4 no MFMAs, 8 no LDS reads or
-    MFMAs; results garbage, timing only), cache-cold weights."""
-    out = []
-    shapes = {"qkv": (12288, 4096, "out"), "o": (4096, 4096, "part"), "down": (4096, 11008, "part")}
-    for name, (N, K, kind) in shapes.items():
-        ncopy = max(2, (1 << 30) // (N * K) + 1)
-        w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
-        wps = [ops.pack_int8_weight(w) for _ in range(ncopy)]
-        sw = torch.rand(N, device=dev) * 0.01
-        qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-        sx = (torch.rand(K // 64, M, device=dev) if kind == "part" else torch.rand(M, device=dev)) * 0.01
-        ctr = [0]
-
-        def call():
-            ctr[0] = (ctr[0] + 1) % ncopy
-            if kind == "gluq":
-                return C.w8a8_gemm_gluq(qx, sx, wps[ctr[0]], sw, None, N, K)
-            if kind == "part":
-                return C.w8a8_gemm_splitk(qx, sx, wps[ctr[0]], sw, None, N, K, 0)
-            return C.w8a8_gemm(qx, sx, wps[ctr[0]], sw, None, N, K)
-
-        res = {}
-        for rnd in range(3):
-            for d in (0, 3, 11, 16, 27, 128, 128 + 11, 128 + 3):
-                C.tune("ring2_256_diag", d, 0)
-                res.setdefault(d, []).append(timeit(call, iters=10, per_graph=ncopy))
-        C.tune("ring2_256_diag", 0, 0)
-        row = dict(op="w8a8_rows256_diag", shape=name, M=M, N=N, K=K)
-        for d, ts in res.items():
-            row[f"diag{d}_us"] = round(min(ts), 2)
-        out.append(row)
-        print(row, flush=True)
-        del wps
-    return out
-
-
 def bf16_rows(C, dev, Ms=(8, 16, 32, 48, 64)):
     """bf16 decode projections at 1-64 rows (Llama-2-7B shapes), cache-cold: gemv_bf16.hip
     (1-4 row blocks of 16 per weight read) vs hipBLASLt through torch.nn.functional.linear."""
@@ -478,69 +440,6 @@ def bf16_ring_rows(C, dev, Ms=(32, 64, 128, 256)):
             out.append(row)
             print(row, flush=True)
         del ws, wps
-    return out
-
-
-def prio_rows(C, dev):
-    """Wave-priority A/B (cdna guide T5 / MI355X microarch item 4), interleaved in one process:
-    the 256-row decode GEMMs (ring2_256_diag scheduling bits: 256 compute waves prio 1, 512 loader
-    waves prio 1, 1024 prio 1 around each MFMA cluster; results exact) and the prefill GEMM
-    (prefill_prio: setprio around each k-tile's MFMA cluster)."""
-    out = []
-    shapes = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008)}
-    bits = (0, 256, 512, 1024, 256 | 1024)
-    for name, (N, K) in shapes.items():
-        ncopy = max(2, (1 << 30) // (N * K) + 1)
-        ws = [ops.pack_int8_weight(torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)) for _ in range(ncopy)]
-        s2 = torch.rand(N, device=dev) * 0.01
-        M = 256
-        a = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
-        s1 = torch.rand(M, device=dev) * 0.01
-        ctr = [0]
-        if name in ("o", "down"):
-            KT = K // 64
-            sg = torch.rand(KT, M, device=dev) * 0.01
-
-            def call():
-                ctr[0] = (ctr[0] + 1) % ncopy
-                return C.w8a8_gemm_splitk(a, sg, ws[ctr[0]], s2, None, N, K, 0)
-        elif name == "gate_up":
-            def call():
-                ctr[0] = (ctr[0] + 1) % ncopy
-                return C.w8a8_gemm_gluq(a, s1, ws[ctr[0]], s2, None, N, K)
-        else:
-            def call():
-                ctr[0] = (ctr[0] + 1) % ncopy
-                return C.w8a8_gemm(a, s1, ws[ctr[0]], s2, None, N, K)
-        res = {}
-        for _ in range(2):
-            for b in bits:
-                C.tune("ring2_256_diag", b, 0)
-                res.setdefault(b, []).append(timeit(call, iters=10, per_graph=ncopy))
-        C.tune("ring2_256_diag", 0, 0)
-        row = dict(op="rows256_prio", shape=name, M=M, N=N, K=K)
-        for b, ts in res.items():
-            row[f"bits{b}_us"] = round(min(ts), 2)
-        out.append(row)
-        print(row, flush=True)
-        del ws
-        for Mp in (2048, 16384):
-            w = ops.pack_int8_weight(torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev))
-            ap = torch.randint(-127, 128, (Mp, K), dtype=torch.int8, device=dev)
-            sp = torch.rand(Mp, device=dev) * 0.01
-            res = {}
-            per = max(2, min(20, int(4e11 // (Mp * N * K))))
-            for _ in range(2):
-                for pr in (0, 1):
-                    C.tune("prefill_prio", pr, 0)
-                    res.setdefault(pr, []).append(timeit(lambda: C.w8a8_gemm(ap, sp, w, s2, None, N, K), iters=5,
-                                                         per_graph=per))
-            C.tune("prefill_prio", 0, 0)
-            row = dict(op="prefill_prio", shape=name, M=Mp, N=N, K=K)
-            for pr, ts in res.items():
-                row[f"prio{pr}_TOPs"] = round(2 * Mp * N * K / min(ts) / 1e6, 1)
-            out.append(row)
-            print(row, flush=True)
     return out
 
 
@@ -647,16 +546,10 @@ def main():
         rows += batch1_rows(C, dev)
     if only is not None and "rows256" in only:
         rows += rows256_rows(C, dev)
-    if only is not None and "r256diag" in only:
-        rows += rows256_diag(C, dev)
     if only is not None and "bf16rows" in only:
         rows += bf16_rows(C, dev)
     if only is not None and "x32" in only:
         rows += x32_rows(C, dev)
-    if only is not None and "rot" in only:
-        rows += knob_ab_rows(C, dev, "ring2_256_rot", values=(0, 1))
-    if only is not None and "prio" in only:
-        rows += prio_rows(C, dev)
     if only is not None and "bf16ring" in only:
         rows += bf16_ring_rows(C, dev)
     if a.out:
