@@ -40,6 +40,9 @@ def add_runtime_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
                    help="torchrun pipelines: micro-batches each stage runs concurrently (YAML parallel.lanes)")
     g.add_argument("--pp_slack", type=int, default=None,
                    help="torchrun pipelines: extra ticks per hop, P2P overlapped with compute (YAML parallel.slack)")
+    g.add_argument("--pp_vocab_split", default=None, choices=["on", "off"],
+                   help="torchrun pipelines: split the LM head by vocabulary over the stages, rank 0 merging "
+                        "the sampler's candidates (default on; YAML parallel.vocab_split)")
     g.add_argument("--calib", default=None, choices=["stage", "full"],
                    help="torchrun + w8a8_smoothquant: calibrate each stage on the activations it receives "
                         "(stage, default) or the full model on every rank (full) (YAML parallel.calib)")
@@ -59,7 +62,8 @@ def pop_runtime(args: argparse.Namespace) -> dict:
     """Remove runtime-only keys so the remaining namespace is the reference's flag set."""
     keys = ["quant", "precision", "devices", "num_samples", "seed", "max_seq", "progress", "base_model_path",
             "no_legacy_decode", "no_reference_in_refiner", "merge", "serial", "headinfer_heads", "metrics_jsonl",
-            "prefill_chunk", "pp_size", "batch_size", "kv_dtype", "partition", "pp_lanes", "pp_slack", "calib"]
+            "prefill_chunk", "pp_size", "batch_size", "kv_dtype", "partition", "pp_lanes", "pp_slack", "calib",
+            "pp_vocab_split"]
     return {k: args.__dict__.pop(k) for k in keys if k in args.__dict__}
 
 
@@ -80,6 +84,8 @@ def resolve_runtime(cfg, rt: dict) -> dict:
     rt["pp_lanes"] = max(1, int(rt.get("pp_lanes") or getattr(par, "lanes", 1) or 1))
     rt["pp_slack"] = max(0, int(rt.get("pp_slack") if rt.get("pp_slack") is not None else getattr(par, "slack", 0) or 0))
     rt["calib"] = rt.get("calib") or getattr(par, "calib", "stage") or "stage"
+    vs = rt.get("pp_vocab_split")
+    rt["pp_vocab_split"] = (vs == "on") if vs is not None else bool(getattr(par, "vocab_split", True))
     rt.setdefault("kv_dtype", None)
     rt["kv_dtype"] = rt["kv_dtype"] or "bf16"
     return rt
@@ -157,19 +163,25 @@ def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch,
     group = agent_group(ranks, world)
     kvd = rt.get("kv_dtype") or "bf16"
     lanes, slack = int(rt.get("pp_lanes") or 1), int(rt.get("pp_slack") or 0)
+    vs = bool(rt.get("pp_vocab_split", False)) and len(ranks) > 1
     common = dict(max_batch=max_batch, max_seq=rt.get("max_seq", 2048), tag=tag, group=group, ranks=ranks,
-                  lanes=lanes, slack=slack)
+                  lanes=lanes, slack=slack, vocab_split=vs)
     if rank not in ranks:
         cfg, tok, source = _cfg_of(model_id, precision, torch.device("cpu"), rt.get("base_model_path"))
         eng = PipelineGenerator(None, -1, len(ranks), cfg=cfg, device=dev, **common)
         return eng, tok, source, None
     s_idx = ranks.index(rank)
-    M, b = PipelineGenerator.geometry(len(ranks), max_batch, lanes, slack)
+    M, b = PipelineGenerator.geometry(len(ranks), max_batch, lanes, slack, vocab_split=vs)
     stage, tok, source, bounds = load_stage(model_id, precision, quant, dev, rt.get("base_model_path"), s_idx,
                                             len(ranks), partition=rt.get("partition") or "balanced", group=group,
                                             ranks=ranks, calib=rt.get("calib") or "stage", rows=b,
                                             ctx=min(int(rt.get("max_seq", 2048)), 256))
     if kvd == "int8" and stage.cfg.head_dim not in (64, 128, 256):
         kvd = "bf16"
-    eng = PipelineGenerator(stage, s_idx, len(ranks), kv_dtype=kvd, **common)
+    shard = None
+    if vs:
+        # every member gets its rows of the head from the last stage (one P2P per rank, at load)
+        from ..parallel.vocab_head import shard_from_last_stage
+        shard = shard_from_last_stage(stage, stage.cfg, s_idx, len(ranks), group=group, ranks=ranks, device=dev)
+    eng = PipelineGenerator(stage, s_idx, len(ranks), kv_dtype=kvd, head_shard=shard, **common)
     return eng, tok, source, bounds

@@ -43,6 +43,8 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
                     help="torchrun pipeline: balanced | units (half-layer bounds) | uniform | '8,8,8,8'")
     ap.add_argument("--pp-lanes", type=int, default=1, help="torchrun pipeline: concurrent micro-batches per stage")
     ap.add_argument("--pp-slack", type=int, default=0, help="torchrun pipeline: extra ticks per stage hop")
+    ap.add_argument("--pp-vocab-split", default="on", choices=["on", "off"],
+                    help="torchrun pipeline (static batches): LM head split by vocabulary over the stages")
     ap.add_argument("--calib", default="stage", choices=["stage", "full"],
                     help="torchrun + w8a8_smoothquant: per-stage calibration over P2P (stage) or full model")
     ap.add_argument("--static-batches", action="store_true",
@@ -119,7 +121,8 @@ def build_pipeline_engine(args, launch):
     from .common import build_pp_engine
     rt = dict(max_seq=args.max_seq, kv_dtype=args.kv_dtype, base_model_path=args.base_model_path,
               partition=getattr(args, "partition", "balanced"), pp_lanes=getattr(args, "pp_lanes", 1),
-              pp_slack=getattr(args, "pp_slack", 0), calib=getattr(args, "calib", "stage"))
+              pp_slack=getattr(args, "pp_slack", 0), calib=getattr(args, "calib", "stage"),
+              pp_vocab_split=getattr(args, "pp_vocab_split", "on") == "on")
     eng, tok, src, bounds = build_pp_engine(args.model, args.precision, args.quant, rt, launch, tag=0,
                                             max_batch=args.max_batch)
     if launch[0] != 0:

@@ -54,6 +54,7 @@ class ParallelConfig:
     lanes: int = 1              # micro-batches each stage decodes concurrently on HIP streams
     slack: int = 0              # extra ticks per stage hop (1: every P2P hop overlapped with a tick)
     calib: str = "stage"        # SmoothQuant under torchrun: per-stage over P2P | full (every rank)
+    vocab_split: bool = True    # torchrun pipelines: LM head split by vocabulary over the stages
 
 
 @dataclass

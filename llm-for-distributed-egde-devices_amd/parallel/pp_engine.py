@@ -183,13 +183,16 @@ class PipelineGenerator:
     def __init__(self, stage_model: Optional[DecoderLM], rank: int, world: int, max_batch: int = 1,
                  max_seq: int = 2048, tag: int = 0, lanes: int = 1, n_micro: Optional[int] = None,
                  kv_dtype: str = "bf16", eos_every: int = 8, group=None, use_graphs: Optional[bool] = None,
-                 ranks: Optional[Sequence[int]] = None, cfg=None, device=None, slack: int = 0):
+                 ranks: Optional[Sequence[int]] = None, cfg=None, device=None, slack: int = 0,
+                 vocab_split: bool = False, head_shard=None):
         self.rank, self.world, self.tag, self.group = rank, world, tag, group
         self.ranks = list(ranks) if ranks is not None else list(range(world))
         assert len(self.ranks) == world
         self.grank = dist.get_rank() if dist.is_initialized() else 0
         self.member = stage_model is not None
-        M, b = self.geometry(world, max_batch, lanes, slack, n_micro)
+        # LM head split by vocabulary over the group (parallel/vocab_head.py): members pass their shard
+        self.vs_req = bool(vocab_split) and world > 1
+        M, b = self.geometry(world, max_batch, lanes, slack, n_micro, self.vs_req)
         self.M, self.b = M, b
         self.lanes, self.slack = lanes, slack
         self.cfg = stage_model.cfg if self.member else cfg
@@ -197,7 +200,8 @@ class PipelineGenerator:
         self.max_seq = min(max_seq, self.cfg.max_position_embeddings)   # as Generator
         if self.member:
             self.stage = PipelineStage(stage_model, rank, world, b, M, self.max_seq, group=group, lanes=lanes,
-                                       kv_dtype=kv_dtype, use_graphs=use_graphs, ranks=self.ranks, slack=slack)
+                                       kv_dtype=kv_dtype, use_graphs=use_graphs, ranks=self.ranks, slack=slack,
+                                       vocab_split=self.vs_req, head_shard=head_shard)
             self.device = stage_model.device
             self.nccl = self.stage.nccl
         else:
@@ -214,10 +218,15 @@ class PipelineGenerator:
         self._stopped = False
 
     @staticmethod
-    def geometry(world: int, max_batch: int, lanes: int = 1, slack: int = 0, n_micro: Optional[int] = None):
+    def geometry(world: int, max_batch: int, lanes: int = 1, slack: int = 0, n_micro: Optional[int] = None,
+                 vocab_split: bool = False):
         """(M micro-batches, b rows each) for ``max_batch`` sequences: M covers the micro-batch
-        groups a stage hop keeps in flight (P, or (1 + slack)(P - 1) + 2 with slack) times the lanes."""
-        groups = world if slack == 0 or world == 1 else (1 + slack) * (world - 1) + 2
+        groups a stage hop keeps in flight (P, or (1 + slack)(P - 1) + 2 with slack; (1 + slack)(P + 1)
+        with the vocab-split head) times the lanes."""
+        if vocab_split and world > 1:
+            groups = (1 + slack) * (world + 1)
+        else:
+            groups = world if slack == 0 or world == 1 else (1 + slack) * (world - 1) + 2
         M = max(n_micro or 0, groups * max(1, lanes))
         M = -(-M // max(1, lanes)) * max(1, lanes)
         return M, max(1, math.ceil(max_batch / M))
@@ -243,9 +252,18 @@ class PipelineGenerator:
             dist.broadcast(t, 0)
         return t
 
-    def _deliver(self, ts: Sequence[torch.Tensor]) -> None:
-        """The group's last stage -> global rank 0 (world P2P), in place on rank 0's buffers."""
-        src = self.ranks[-1]
+    def _result_stage(self, hdr, fl) -> int:
+        """Stage whose run holds a job's tokens: 0 under the vocab split (it merges the samples)
+        when the job's sampling shards, else the last; every rank derives it from the command."""
+        if self.vs_req and ops.shard_mode(float(fl[0]), int(hdr[7]), float(fl[1]), self.cfg.vocab_size,
+                                          bool(int(hdr[6]))) >= 0:
+            return 0
+        return self.world - 1
+
+    def _deliver(self, ts: Sequence[torch.Tensor], stage: Optional[int] = None) -> None:
+        """The group's result stage (default its last) -> global rank 0 (world P2P), in place on
+        rank 0's buffers."""
+        src = self.ranks[self.world - 1 if stage is None else stage]
         if src == 0:
             return
         for t in ts:
@@ -310,7 +328,7 @@ class PipelineGenerator:
         prompts = [ids_d[m * b:(m + 1) * b] for m in range(M)]
         res = st.run(prompts, T, sp, max_new - 1, seed=seed, prompt_lens=lens.view(M, b),
                      eos_token_id=None if eos < 0 else eos, eos_every=self.eos_every)
-        if st.is_last:
+        if res.tokens is not None:                   # the sampling stage (last, or 0 under the vocab split)
             out.copy_(torch.tensor(res.tokens, dtype=torch.long))
             timing[0] = res.elapsed_s
             timing[1] = res.stats.get("ttft_ms", 0.0) / 1e3
@@ -381,8 +399,8 @@ def generate_concurrent(jobs: Sequence[tuple], stop_at_eos: bool = True) -> List
 def _run_jobs(payload):
     """Every rank: compute its member jobs in order, then deliver each job's result to rank 0."""
     outs = [eng._run_local(hdr, fl, ids, lens) for eng, hdr, fl, ids, lens in payload]
-    for (eng, *_), o in zip(payload, outs):
-        eng._deliver(list(o))
+    for (eng, hdr, fl, *_), o in zip(payload, outs):
+        eng._deliver(list(o), eng._result_stage(hdr, fl))
     return outs
 
 

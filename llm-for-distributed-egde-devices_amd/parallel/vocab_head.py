@@ -88,3 +88,38 @@ def build_head_shard(cfg: ModelConfig, rank: int, world: int, model=None, seed: 
     w = full_weight[v0:v1].detach().to(dtype=dtype, device=device).contiguous()
     bias = full_bias[v0:v1].detach().to(dtype=dtype, device=device).contiguous() if full_bias is not None else None
     return HeadShard(w, bias, v0, cfg.vocab_size)
+
+
+@torch.no_grad()
+def shard_from_last_stage(model, cfg: ModelConfig, rank: int, world: int, group=None, ranks=None,
+                          device=None) -> HeadShard:
+    """Every pipeline rank's head shard from the stage that holds the head (the last): it sends
+    each other rank its rows once, over the group's P2P path, so the split works for any weight
+    source (random init, HF checkpoint, int8 checkpoint) without a rank re-reading the head.
+    Every member of the group must call this, in any order."""
+    import torch.distributed as dist
+    b = shard_bounds(cfg.vocab_size, world)
+    v0, v1 = b[rank], b[rank + 1]
+    granks = list(ranks) if ranks is not None else list(range(world))
+    nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+    dev = torch.device(device) if device is not None else model.device
+    cdev = dev if nccl else torch.device("cpu")
+    dtype = model.dtype
+    if rank == world - 1:
+        lm = model.lm_head
+        assert lm is None or not getattr(lm, "takes_quantized_input", False), "vocab split: 16-bit LM head only"
+        W = model.head_weight()
+        bias = lm.bias if lm is not None else None
+        for r in range(world - 1):
+            dist.send(W[b[r]:b[r + 1]].contiguous().to(cdev), granks[r], group=group)
+            if bias is not None:
+                dist.send(bias[b[r]:b[r + 1]].contiguous().to(cdev), granks[r], group=group)
+        return HeadShard(W[v0:v1].contiguous(), bias[v0:v1].contiguous() if bias is not None else None, v0,
+                         cfg.vocab_size)
+    w = torch.empty(v1 - v0, cfg.hidden_size, dtype=dtype, device=cdev)
+    dist.recv(w, granks[-1], group=group)
+    bias = None
+    if cfg.lm_head_bias:
+        bias = torch.empty(v1 - v0, dtype=dtype, device=cdev)
+        dist.recv(bias, granks[-1], group=group)
+    return HeadShard(w.to(dev), bias.to(dev) if bias is not None else None, v0, cfg.vocab_size)

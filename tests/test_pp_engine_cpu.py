@@ -33,7 +33,7 @@ def _cfg(arch):
     return tiny(arch, num_layers=6)
 
 
-def _worker(rank, world, port, arch, sp_kw, eos, q, prompts=PROMPTS):
+def _worker(rank, world, port, arch, sp_kw, eos, q, prompts=PROMPTS, vs=False):
     import edgellm  # noqa: F401
     from edgellm.parallel.partition import partition_model
     from edgellm.parallel.pp_engine import PipelineGenerator, serve_workers, stop_workers
@@ -43,7 +43,11 @@ def _worker(rank, world, port, arch, sp_kw, eos, q, prompts=PROMPTS):
     cfg = _cfg(arch)
     bounds = partition_model(cfg, world, "uniform")
     model = build_model(cfg, dtype=torch.float32, first=bounds[rank], last=bounds[rank + 1], seed=7)
-    eng = PipelineGenerator(model, rank, world, max_batch=6, max_seq=40, tag=3)
+    shard = None
+    if vs:                                       # LM head split by vocabulary over the ranks
+        from edgellm.parallel.vocab_head import shard_from_last_stage
+        shard = shard_from_last_stage(model, cfg, rank, world)
+    eng = PipelineGenerator(model, rank, world, max_batch=6, max_seq=40, tag=3, vocab_split=vs, head_shard=shard)
     if rank == 0:
         sp = SamplingParams(**sp_kw)
         res = eng.generate(prompts, sp, seed=11, eos_token_id=eos)
@@ -56,6 +60,7 @@ def _worker(rank, world, port, arch, sp_kw, eos, q, prompts=PROMPTS):
             pass
         again = eng.generate(prompts[:2], sp, seed=11, eos_token_id=eos)     # engine reuse, fewer rows
         stop_workers(eng)
+        assert eng.stage.vs == vs                # (the last run's sampling shards whenever vs)
         q.put((res.tokens, conf, again.tokens, eng.stage.M, eng.stage.b, ticks))
     else:
         n = serve_workers({3: eng})
@@ -64,11 +69,11 @@ def _worker(rank, world, port, arch, sp_kw, eos, q, prompts=PROMPTS):
     dist.destroy_process_group()
 
 
-def _run(world, arch, sp_kw, eos=None, prompts=PROMPTS):
+def _run(world, arch, sp_kw, eos=None, prompts=PROMPTS, vs=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, arch, sp_kw, eos, q, prompts)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, arch, sp_kw, eos, q, prompts, vs)) for r in range(world)]
     for p in ps:
         p.start()
     out = q.get(timeout=300)
@@ -82,10 +87,11 @@ GREEDY = dict(max_new_tokens=8, do_sample=False, repetition_penalty=1.1)
 SAMPLED = dict(max_new_tokens=8, do_sample=True, temperature=0.7, top_k=20, top_p=0.9, repetition_penalty=1.1)
 
 
+@pytest.mark.parametrize("vs", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("arch", ["llama", "gpt_neox"])
-def test_pp_engine_greedy_ragged_matches_unsplit(world, arch):
-    toks, conf, again, M, b, ticks = _run(world, arch, GREEDY)
+def test_pp_engine_greedy_ragged_matches_unsplit(world, arch, vs):
+    toks, conf, again, M, b, ticks = _run(world, arch, GREEDY, vs=vs)
     full = build_model(_cfg(arch), dtype=torch.float32, seed=7)
     sp = SamplingParams(**GREEDY)
     for p, t in zip(PROMPTS, toks):
@@ -94,9 +100,11 @@ def test_pp_engine_greedy_ragged_matches_unsplit(world, arch):
     assert abs(conf - confidence_score(full, [5, 9, 2, 7, 7, 1])) < 1e-5
 
 
-def test_pp_engine_sampling_matches_lanes():
-    """Seeded sampling: micro-batch m samples with seed + 7919 m, exactly as LaneGenerator's lane m."""
-    toks, _, _, M, b, _ = _run(2, "llama", SAMPLED)
+@pytest.mark.parametrize("vs", [False, True])
+def test_pp_engine_sampling_matches_lanes(vs):
+    """Seeded sampling: micro-batch m samples with seed + 7919 m, exactly as LaneGenerator's lane m
+    (also with the vocab-split head: one more micro-batch group, the same draws)."""
+    toks, _, _, M, b, _ = _run(2, "llama", SAMPLED, vs=vs)
     full = build_model(_cfg("llama"), dtype=torch.float32, seed=7)
     rows = PROMPTS + [PROMPTS[0]] * (M * b - len(PROMPTS))
     lg = LaneGenerator(full, lanes=M, max_batch=b, max_seq=40)
@@ -121,3 +129,5 @@ def test_pp_engine_eos_exit():
     assert ticks < full_ticks // 2, (ticks, full_ticks)
     want = Generator(full, max_batch=len(prompts), max_seq=40).generate(prompts, sp, eos_token_id=eos).tokens
     assert toks == want
+    toks, _, _, M, _, ticks = _run(2, "llama", dict(GREEDY, max_new_tokens=30), eos=eos, prompts=prompts, vs=True)
+    assert toks == want and ticks < (M + 29 * M + 4) // 2         # EOS agreement from rank 0
