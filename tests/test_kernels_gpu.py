@@ -135,11 +135,13 @@ def test_prefill_attention(cuda, Hq, Hkv, D, T, starts):
 @pytest.mark.parametrize("stag", [2, 1])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("Hq,Hkv,T,starts", [(8, 2, 600, (0, 300)), (4, 4, 1100, (0,)), (8, 8, 257, (0, 64)),
-                                            (4, 1, 40, (1000, 3))])
+                                            (4, 1, 40, (1000, 3)), (16, 4, 530, (0, 200))])
 def test_prefill_attention_fa128(cuda, stag, causal, Hq, Hkv, T, starts):
     """The D = 128 LDS-DMA ring kernel (fa_kernel) over many key tiles (ring wrap), partial query
     tiles, chunked prefill offsets, GQA, against the fp32 reference and the 16-row kernel; both the
-    staggered (waves 4-7 defer each tile's P.V one tile, 4-slot ring) and the lockstep form."""
+    staggered (waves 4-7 defer each tile's P.V one tile, 4-slot ring) and the lockstep form.  The
+    workgroup order (longest tiles first over all heads, KV groups on one XCD; or per head) only
+    moves work between CUs: the outputs are bit-identical."""
     C = ops.ext()
     D, B = 128, len(starts)
     S = max(starts) + T + 3
@@ -152,10 +154,15 @@ def test_prefill_attention_fa128(cuda, stag, causal, Hq, Hkv, T, starts):
     try:
         C.tune("prefill_fa", 2, stag)               # fa_kernel whatever the grid size
         out = C.prefill_attn(q, kc, vc, sp, scale, causal)
+        C.tune("prefill_fa_order", 0, 0)
+        per_head = C.prefill_attn(q, kc, vc, sp, scale, causal)
+        C.tune("prefill_fa_order", 1, 0)
         C.tune("prefill_fa", 0, 0)
         old = C.prefill_attn(q, kc, vc, sp, scale, causal)
     finally:
         C.tune("prefill_fa", 1, 0)
+        C.tune("prefill_fa_order", 1, 0)
+    assert torch.equal(out, per_head)
     _close(out, ref, 2e-2, 2e-2)
     _close(out, old, 2e-2, 2e-2)
 

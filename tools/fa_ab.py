@@ -1,11 +1,14 @@
 #!/usr/bin/env python
-"""Interleaved A/B of the flash-prefill wave schedules (tune ``prefill_fa`` second value as the binding
-reads it: 2 staggered (the default), 1 lockstep) at the TTFT-relevant causal shapes: several rounds in
-one process, variants rotated each round, median TF/s per variant.  Round 4
-(profiles/fa_schedule_ab_r4.json): staggered 3.5-5.5 % over lockstep at D = 128, lockstep +1 % at
-D = 64; a staggered form without the one-step V-fragment window was 1-3 % slower and was not kept.
+"""Interleaved A/B of flash-prefill launch variants at the TTFT-relevant causal shapes: several rounds
+in one process, variants rotated each round, median TF/s per variant.
 
-    python tools/fa_ab.py [--rounds 5] [--out file.json]
+  --knob stagger: wave schedules (tune ``prefill_fa`` second value as the binding reads it: 2 staggered,
+    the default, 1 lockstep).  Round 4 (profiles/fa_schedule_ab_r4.json): staggered 3.5-5.5 % over
+    lockstep at D = 128, lockstep +1 % at D = 64.
+  --knob order: workgroup order (tune ``prefill_fa_order``: 1 longest query tiles first over all heads,
+    the default, 0 longest first per head).  The shapes include the 4K chunks of a 32K prompt.
+
+    python tools/fa_ab.py [--knob order] [--rounds 5] [--out file.json]
 """
 import argparse
 import json
@@ -27,28 +30,41 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--knob", default="stagger", choices=["stagger", "order"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     C = ops.ext()
     rows = []
-    for T, Hq, Hkv, s0, D in ((32768, 32, 8, 0, 128), (4096, 32, 8, 28672, 128), (8192, 32, 8, 0, 128),
-                              (2048, 32, 32, 0, 128), (1024, 32, 8, 0, 64)):
+    shapes = [(32768, 32, 8, 0, 128), (4096, 32, 8, 28672, 128), (8192, 32, 8, 0, 128),
+              (2048, 32, 32, 0, 128), (1024, 32, 8, 0, 64)]
+    if a.knob == "order":
+        shapes = [(4096, 32, 8, 0, 128), (4096, 32, 8, 12288, 128)] + shapes
+    names = {2: "staggered", 1: "lockstep"} if a.knob == "stagger" else {1: "all_heads", 0: "per_head"}
+    order = list(names)
+
+    def setk(v):
+        if a.knob == "stagger":
+            C.tune("prefill_fa", 2, v)
+        else:
+            C.tune("prefill_fa", 2, 0)
+            C.tune("prefill_fa_order", v, 0)
+    for T, Hq, Hkv, s0, D in shapes:
         q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
         kc = torch.randn(1, Hkv, s0 + T, D, device=dev).bfloat16()
         vc = torch.randn_like(kc)
         sp = torch.full((1,), s0, dtype=torch.int32, device=dev)
         flops = 4 * T * (s0 + T / 2) * D * Hq
-        res = {2: [], 1: []}
-        order = [2, 1]
+        res = {k: [] for k in order}
         for r in range(a.rounds):
             for stg in order[r % 2:] + order[:r % 2]:
-                C.tune("prefill_fa", 2, stg)
+                setk(stg)
                 t = timeit(lambda: C.prefill_attn(q, kc, vc, sp, 1 / math.sqrt(D), True), iters=5,
                            per_graph=2 if T >= 16384 else 10)
                 res[stg].append(flops / t / 1e6)
         C.tune("prefill_fa", 1, 0)
-        row = dict(T=T, start=s0, Hq=Hq, Hkv=Hkv, D=D)
-        for stg, name in ((2, "staggered"), (1, "lockstep")):
+        C.tune("prefill_fa_order", 1, 0)
+        row = dict(T=T, start=s0, Hq=Hq, Hkv=Hkv, D=D, knob=a.knob)
+        for stg, name in names.items():
             v = sorted(res[stg])
             row[name + "_TFLOPs_median"] = round(v[len(v) // 2], 1)
             row[name + "_TFLOPs_all"] = [round(x, 1) for x in res[stg]]
