@@ -38,6 +38,19 @@ __device__ __forceinline__ void glds16_fa(const void* g, void* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
+// max / sum over lanes i and i ^ 32 by one v_permlane32_swap instead of a ds_bpermute round trip
+// (+0.5-1.4 % on the flash kernel, profiles/fa_v2_forms_ab_r5.json): the swap of x with itself
+// leaves the low half's values in r[0] and the high half's in r[1] on every lane.  Same operands,
+// same order as the shuffle form: bit-identical
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int D>
 struct Geo {
   static constexpr int DP = (D + 31) / 32 * 32;       // reduction-padded head dim
@@ -290,7 +303,7 @@ template <int D, bool CAUSAL, bool STG, bool HF>
 __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc, int64_t c_sb,
     int64_t c_sh, const int* __restrict__ start_pos, bf16_t* __restrict__ out, int T, int Hq, int Hkv,
-    float scale_log2, int order) {
+    float scale_log2, int order, int prio, float thr) {
   using G = FaGeo<D>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   // one-dimensional grid, longest (causal) query tile first over ALL heads and batch rows: the CUs
@@ -395,6 +408,10 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
   float alpha_p = 1.f;
   const char* vl_p = smem;
 
+  // static priority for the younger wave half (waves 4-7 lose VALU arbitration to their SIMD
+  // partners otherwise; the guard must be provably wave-uniform for s_setprio): A/B knob, 5 % slower
+  // with the staggered schedule (profiles/fa_softmax_knobs_ab_r5.json)
+  if (prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= FA_NT / 2) __builtin_amdgcn_s_setprio(1);
   if (ntiles > 0) issue(0);
   if (ntiles > 1) issue(1);
   for (int t = 0; t < ntiles; ++t) {
@@ -443,8 +460,12 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
         sacc[kb][r] = v;
         mx = fmaxf(mx, v);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m_i, mx * scale_log2);
+    mx = half_max(mx);
+    // the running max moves only when some query of the wave exceeds it by more than thr (log2
+    // units): below that the probabilities stay <= 2^thr against the old max and the O rescale is
+    // skipped.  thr = 0 (the default) is the exact online softmax: a rescale whenever a max moved
+    const float cand = mx * scale_log2;
+    const float mnew = __all(cand <= m_i + thr) ? m_i : fmaxf(m_i, cand);
     const float msafe = mnew == -INFINITY ? 0.f : mnew;
     // v_exp_f32 directly: exp2f adds a denormal-range fix-up (compare, select, add, multiply) to
     // every exponential; arguments here are <= 0 and a probability below 2^-126 may flush to 0
@@ -461,7 +482,7 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
           rs += pv;
           pb[kb][ks][j] = (short)f2e<HF>(pv);
         }
-    rs += __shfl_xor(rs, 32, 64);
+    rs = half_sum(rs);
     l_i = l_i * alpha + rs;
     m_i = mnew;
     if constexpr (STG) {
@@ -503,8 +524,11 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
 static int g_prefill_fa = 1;           // tune key "prefill_fa": 0 = the 16-row kernel only, 1 = auto, 2 = fa_kernel always
 static int g_prefill_fa_stag = 1;      // tune key "prefill_fa", second value: 1 = staggered wave halves, 0 = lockstep (A/B)
 static int g_prefill_fa_order = 1;     // tune key "prefill_fa_order": 1 = longest tiles first over all heads, 0 = per head (A/B)
+static int g_prefill_fa_prio = 0;      // tune key "prefill_fa_sm": a = static s_setprio 1 for waves 4-7 (A/B)
+static float g_prefill_fa_thr = 0.f;   // tune key "prefill_fa_sm": b = deferred-max threshold, log2 units (A/B)
 extern "C" void edge_prefill_fa(int v, int stag) { g_prefill_fa = v; g_prefill_fa_stag = stag; }
 extern "C" void edge_prefill_fa_order(int v) { g_prefill_fa_order = v; }
+extern "C" void edge_prefill_fa_sm(int prio, int thr) { g_prefill_fa_prio = prio; g_prefill_fa_thr = (float)thr; }
 
 namespace {
 template <bool HF>
@@ -535,12 +559,12 @@ int run_prefill(const void* q, const void* k_cache, const void* v_cache, int64_t
     }                                                                                                              \
     const dim3 g((T + FA_QT - 1) / FA_QT * Hq * B);                                                                   \
     if (g_prefill_fa_stag) {                                                                                       \
-      if (causal) hipLaunchKernelGGL((fa_kernel<DD, true, true, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, ARGS, g_prefill_fa_order); \
-      else hipLaunchKernelGGL((fa_kernel<DD, false, true, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, ARGS, g_prefill_fa_order);     \
+      if (causal) hipLaunchKernelGGL((fa_kernel<DD, true, true, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, ARGS, g_prefill_fa_order, g_prefill_fa_prio, g_prefill_fa_thr); \
+      else hipLaunchKernelGGL((fa_kernel<DD, false, true, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS_STG, st, ARGS, g_prefill_fa_order, g_prefill_fa_prio, g_prefill_fa_thr);     \
       break;                                                                                                       \
     }                                                                                                              \
-    if (causal) hipLaunchKernelGGL((fa_kernel<DD, true, false, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, ARGS, g_prefill_fa_order);    \
-    else hipLaunchKernelGGL((fa_kernel<DD, false, false, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, ARGS, g_prefill_fa_order);          \
+    if (causal) hipLaunchKernelGGL((fa_kernel<DD, true, false, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, ARGS, g_prefill_fa_order, g_prefill_fa_prio, g_prefill_fa_thr);    \
+    else hipLaunchKernelGGL((fa_kernel<DD, false, false, HF>), g, dim3(FA_NT), FaGeo<DD>::LDS, st, ARGS, g_prefill_fa_order, g_prefill_fa_prio, g_prefill_fa_thr);          \
   } while (0)
     if (D == 128) FA(128);
     else FA(64);

@@ -63,6 +63,7 @@ void edge_sample_rowwide_min(int v);
 void edge_sample_vec(int v);
 void edge_prefill_fa(int v, int stag);
 void edge_prefill_fa_order(int v);
+void edge_prefill_fa_sm(int prio, int thr);
 int edge_sample_timestamps(int enable, unsigned long long* host_out16);
 int edge_copy_head_block(void* dst, int64_t dst_sb, int64_t dst_sh, const void* src, int64_t src_sb, int64_t src_sh,
                          int B, int heads, int64_t row_bytes, int elem_bytes, hipStream_t st, int mode, int* used);
@@ -1125,6 +1126,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "sample_vec") edge_sample_vec((int)a);
     else if (what == "prefill_fa") edge_prefill_fa((int)a, b == 0 ? 1 : (int)b - 1);   // b: 0 default, 1 lockstep, 2 stagger
     else if (what == "prefill_fa_order") edge_prefill_fa_order((int)a);
+    else if (what == "prefill_fa_sm") edge_prefill_fa_sm((int)a, (int)b);
     else if (what == "gemv_norm") edge_w8a8_gemv_norm_cfg((int)a);
     else if (what == "r256_packed") edge_w8a8_r256_cfg((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);

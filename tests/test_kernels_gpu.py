@@ -167,6 +167,38 @@ def test_prefill_attention_fa128(cuda, stag, causal, Hq, Hkv, T, starts):
     _close(out, old, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("prio,thr", [(1, 0), (0, 8), (1, 8)])
+@pytest.mark.parametrize("growing", [False, True])
+def test_prefill_attention_fa_softmax_knobs(cuda, prio, thr, growing):
+    """fa_kernel's static priority (waves 4-7) leaves the output bit-identical; the deferred max
+    (rescale only when a score beats the running max by more than thr, log2 units) stays within the
+    fp32 reference's tolerance, also on keys whose scores keep growing along the sequence, which
+    forces rescales at tiles where only some queries' maxima moved."""
+    C = ops.ext()
+    B, T, Hq, Hkv, D = 2, 700, 8, 2, 128
+    S = T + 300
+    q = torch.randn(B, T, Hq, D, device=cuda).bfloat16()
+    kc = torch.randn(B, Hkv, S, D, device=cuda)
+    if growing:
+        kc = kc * torch.linspace(0.3, 4.0, S, device=cuda)[None, None, :, None]
+    kc = kc.bfloat16()
+    vc = torch.randn(B, Hkv, S, D, device=cuda).bfloat16()
+    sp = torch.tensor([0, 300], device=cuda, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = _ref.prefill_attention(q, kc, vc, sp, scale, True)
+    try:
+        C.tune("prefill_fa", 2, 0)
+        base = C.prefill_attn(q, kc, vc, sp, scale, True)
+        C.tune("prefill_fa_sm", prio, thr)
+        out = C.prefill_attn(q, kc, vc, sp, scale, True)
+    finally:
+        C.tune("prefill_fa_sm", 0, 0)
+        C.tune("prefill_fa", 1, 0)
+    if thr == 0:
+        assert torch.equal(out, base)
+    _close(out, ref, 2e-2, 2e-2)
+
+
 def test_prefill_attention_noncausal(cuda):
     C = ops.ext()
     q = torch.randn(2, 70, 4, 64, device=cuda).bfloat16()

@@ -5,6 +5,9 @@ in one process, variants rotated each round, median TF/s per variant.
   --knob stagger: wave schedules (tune ``prefill_fa`` second value as the binding reads it: 2 staggered,
     the default, 1 lockstep).  Round 4 (profiles/fa_schedule_ab_r4.json): staggered 3.5-5.5 % over
     lockstep at D = 128, lockstep +1 % at D = 64.
+  --knob sm: static s_setprio 1 for waves 4-7 and the deferred-max threshold (tune ``prefill_fa_sm``).
+  (Round 5 also measured hoisted loop-invariant DMA / LDS offsets, a buffer-resource DMA and the
+  permlane32 half reductions: profiles/fa_v2_forms_ab_r5.json; only the permlane form was kept.)
   --knob order: workgroup order (tune ``prefill_fa_order``: 1 longest query tiles first over all heads,
     the default, 0 longest first per head).  The shapes include the 4K chunks of a 32K prompt.
 
@@ -30,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--knob", default="stagger", choices=["stagger", "order"])
+    ap.add_argument("--knob", default="stagger", choices=["stagger", "order", "sm"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     C = ops.ext()
@@ -39,15 +42,19 @@ def main():
               (2048, 32, 32, 0, 128), (1024, 32, 8, 0, 64)]
     if a.knob == "order":
         shapes = [(4096, 32, 8, 0, 128), (4096, 32, 8, 12288, 128)] + shapes
-    names = {2: "staggered", 1: "lockstep"} if a.knob == "stagger" else {1: "all_heads", 0: "per_head"}
+    names = {"stagger": {2: "staggered", 1: "lockstep"}, "order": {1: "all_heads", 0: "per_head"},
+             "sm": {(0, 0): "exact", (1, 0): "prio", (0, 8): "thr8", (1, 8): "prio_thr8"}}[a.knob]
     order = list(names)
 
     def setk(v):
         if a.knob == "stagger":
             C.tune("prefill_fa", 2, v)
-        else:
+        elif a.knob == "order":
             C.tune("prefill_fa", 2, 0)
             C.tune("prefill_fa_order", v, 0)
+        else:
+            C.tune("prefill_fa", 2, 0)
+            C.tune("prefill_fa_sm", *v)
     for T, Hq, Hkv, s0, D in shapes:
         q = torch.randn(1, T, Hq, D, device=dev).bfloat16()
         kc = torch.randn(1, Hkv, s0 + T, D, device=dev).bfloat16()
@@ -56,13 +63,15 @@ def main():
         flops = 4 * T * (s0 + T / 2) * D * Hq
         res = {k: [] for k in order}
         for r in range(a.rounds):
-            for stg in order[r % 2:] + order[:r % 2]:
+            k = r % len(order)
+            for stg in order[k:] + order[:k]:
                 setk(stg)
                 t = timeit(lambda: C.prefill_attn(q, kc, vc, sp, 1 / math.sqrt(D), True), iters=5,
                            per_graph=2 if T >= 16384 else 10)
                 res[stg].append(flops / t / 1e6)
         C.tune("prefill_fa", 1, 0)
         C.tune("prefill_fa_order", 1, 0)
+        C.tune("prefill_fa_sm", 0, 0)
         row = dict(T=T, start=s0, Hq=Hq, Hkv=Hkv, D=D, knob=a.knob)
         for stg, name in names.items():
             v = sorted(res[stg])

@@ -1,0 +1,6 @@
+# flash prefill: hoisted loop-invariant offsets (numerics, interleaved A/B)
+set -o pipefail
+export PYTHONUNBUFFERED=1
+D=gpurun_out/r5t; mkdir -p $D
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_fp16_gpu.py -k "prefill" -x -q --timeout 120 --timeout-method thread > $D/tests.log 2>&1 || exit $?
+timeout -k 10 600 python3 tools/fa_ab.py --knob v2 --rounds 6 --out $D/fa_v2_ab.json > $D/fa_ab.log 2>&1 || exit $?
