@@ -11,7 +11,7 @@ def add_runtime_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     g = p.add_argument_group("edgellm runtime (not in the reference)")
     g.add_argument("--quant", default=None, choices=["none", "w8a8_smoothquant", "w8a8", "llm_int8", "cpu_dynamic"],
                    help="quantisation mode (default: none, or from YAML quant.mode)")
-    g.add_argument("--precision", default=None, help="fp16|bf16|fp32 (GPU runs bf16)")
+    g.add_argument("--precision", default=None, help="fp16|bf16|fp32 (GPU: fp16 and bf16 kernels; fp32 and INT8 models run bf16)")
     g.add_argument("--devices", default=None, help="comma list, e.g. cuda:0,cuda:1 (agents round-robin)")
     g.add_argument("--num_samples", type=int, default=None, help="evaluate only the first N samples")
     g.add_argument("--seed", type=int, default=0, help="sampling seed (the reference sets none)")

@@ -27,7 +27,7 @@ def parse(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--rest-port", type=int, default=8000)
     ap.add_argument("--no-rest", action="store_true")
     ap.add_argument("--model", default=None, help="attach a generation engine (preset, tiny:<arch> or HF dir)")
-    ap.add_argument("--precision", default="bf16", help="bf16 | fp16 | fp32 (GPU always computes in bf16)")
+    ap.add_argument("--precision", default="bf16", help="bf16 | fp16 | fp32 (GPU: fp16 and bf16 kernels; fp32 and INT8 models run bf16)")
     ap.add_argument("--quant", default="none")
     ap.add_argument("--device", default=None)
     ap.add_argument("--base_model_path", default=None)
