@@ -359,8 +359,14 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
       const int kr = pp * G::RPP + lane / G::CH;               // tile-relative key row
       const int key = min(t * FA_KT + kr, kend - 1);
       const int ch = (lane % G::CH) ^ G::swz(kr);              // source chunk for this LDS slot
-      const bf16_t* src = (isv ? vbase : kbase) + (size_t)key * D + ch * 8;
-      glds16_fa(src, slot + (isv ? G::TILE : 0) + pp * 1024);
+      // wave-uniform base (K or V rows: the piece index is the wave's) + a 32-bit lane offset: the
+      // SADDR form of the DMA, no 64-bit lane arithmetic per piece (23 vs 29 vector instructions
+      // per tile; +0.1-0.8 %, profiles/fa_saddr_ab_r5.json)
+      const uint64_t bp = reinterpret_cast<uint64_t>(isv ? vbase : kbase);
+      const char* base = reinterpret_cast<const char*>(
+          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bp >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bp));
+      glds16_fa(base + (uint32_t)(key * G::ROWB + ch * 16), slot + (isv ? G::TILE : 0) + pp * 1024);
     }
   };
 

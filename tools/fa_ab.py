@@ -8,6 +8,7 @@ in one process, variants rotated each round, median TF/s per variant.
   --knob sm: static s_setprio 1 for waves 4-7 and the deferred-max threshold (tune ``prefill_fa_sm``).
   (Round 5 also measured hoisted loop-invariant DMA / LDS offsets, a buffer-resource DMA and the
   permlane32 half reductions: profiles/fa_v2_forms_ab_r5.json; only the permlane form was kept.)
+  (The scalar-base DMA addressing was A/B'd the same way: profiles/fa_saddr_ab_r5.json.)
   --knob order: workgroup order (tune ``prefill_fa_order``: 1 longest query tiles first over all heads,
     the default, 0 longest first per head).  The shapes include the 4K chunks of a 32K prompt.
 
