@@ -18,6 +18,8 @@
 // split: issue early, ds_write after the barrier).
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 constexpr int NT = 256;
 constexpr int QT = 64;   // query rows per workgroup
@@ -49,6 +51,28 @@ __device__ __forceinline__ float half_max(float x) {
 __device__ __forceinline__ float half_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Transposed V reads in inline asm.  Through the builtin, the compiler's wait-count pass cannot tell
+// them from reads of the slot an LDS-DMA is still filling and puts an s_waitcnt vmcnt(0) before every
+// P.V: each tile then waits for the DMA of tile t + 2 it has just issued (the staggered half right
+// after issuing it).  The ring's own counted vmcnt + barrier already orders every V read after its
+// tile's DMA; here the reads are counted by lgkmcnt, and the wait names every destination ("+v")
+// so nothing reads them early (sched_barrier: no MFMA hoisted above the wait).
+template <int OFF>
+__device__ __forceinline__ v4s ds_tr16(uint32_t addr) {
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void wait_tr(v4s (&lo)[N], v4s (&hi)[N]) {
+  if constexpr (N == 4)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]),
+                 "+v"(hi[2]), "+v"(hi[3]));
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[0]), "+v"(lo[1]), "+v"(hi[0]), "+v"(hi[1]));
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int D>
@@ -388,25 +412,36 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
         for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
     }
     const int c16 = lane & 15, qq = c16 >> 2, pq = c16 & 3, g2 = (lane >> 4) & 1;
+    const uint32_t vb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)vl);
+    // the swizzle of key row 32 kb + 16 ks + r is r's (it repeats every 16 rows): per lane one
+    // address per (d-block, key quad), the step's rows as the instruction's immediate offset
+    uint32_t va[G::DB][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int db = 0; db < G::DB; ++db)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int kr1 = kb * 32 + ks * 16 + 4 * hf + qq, kr2 = kr1 + 8;
-#pragma unroll
-        for (int db = 0; db < G::DB; ++db) {
-          const int d0 = db * 32 + g2 * 16 + 4 * pq;
-          const char* a1 = vl + kr1 * G::ROWB + (((d0 >> 3) ^ G::swz(kr1)) << 4) + (d0 & 7) * 2;
-          const char* a2 = vl + kr2 * G::ROWB + (((d0 >> 3) ^ G::swz(kr2)) << 4) + (d0 & 7) * 2;
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
-          const v8s vf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[db] = mfma_32<HF>(vf, pb[kb][ks], o[db]);
-        }
-        // bound the V fragments the compiler keeps in flight to one 16-key step (register budget:
-        // 2 waves / SIMD = 256 VGPRs, and a spill would join this kernel's counted vmcnt)
-        asm volatile("" ::: "memory");
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int kr = 4 * hf + qq + 8 * h2, d0 = db * 32 + g2 * 16 + 4 * pq;
+        va[db][h2] = vb + kr * G::ROWB + (((d0 >> 3) ^ G::swz(kr)) << 4) + (d0 & 7) * 2;
       }
+    auto step = [&](auto kbc, auto ksc) {
+      constexpr int kb = decltype(kbc)::value, ks = decltype(ksc)::value, OFF = (kb * 32 + ks * 16) * G::ROWB;
+      v4s lo[G::DB], hi[G::DB];
+#pragma unroll
+      for (int db = 0; db < G::DB; ++db) {
+        lo[db] = ds_tr16<OFF>(va[db][0]);
+        hi[db] = ds_tr16<OFF>(va[db][1]);
+      }
+      wait_tr<G::DB>(lo, hi);
+#pragma unroll
+      for (int db = 0; db < G::DB; ++db) {
+        const v8s vf = v8s{lo[db][0], lo[db][1], lo[db][2], lo[db][3], hi[db][0], hi[db][1], hi[db][2], hi[db][3]};
+        o[db] = mfma_32<HF>(vf, pb[kb][ks], o[db]);
+      }
+    };
+    step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
   };
   const bool late = STG && wave >= FA_W / 2;                   // wave-uniform
   bool pend = false;
