@@ -55,10 +55,13 @@ __device__ __forceinline__ float half_sum(float x) {
 
 // Transposed V reads in inline asm.  Through the builtin, the compiler's wait-count pass cannot tell
 // them from reads of the slot an LDS-DMA is still filling and puts an s_waitcnt vmcnt(0) before every
-// P.V: each tile then waits for the DMA of tile t + 2 it has just issued (the staggered half right
-// after issuing it).  The ring's own counted vmcnt + barrier already orders every V read after its
-// tile's DMA; here the reads are counted by lgkmcnt, and the wait names every destination ("+v")
-// so nothing reads them early (sched_barrier: no MFMA hoisted above the wait).
+// P.V: each tile then waits for the DMA of tile t + 2 it has just issued.  The ring's own counted
+// vmcnt + barrier already orders every V read after its tile's DMA; here the reads are counted by
+// lgkmcnt, and the wait names every destination ("+v") so nothing reads them early (sched_barrier:
+// no MFMA hoisted above the wait).  The step's rows go in the immediate offset (P.V address work
+// 26 -> 11 vector instructions per tile).  Measured on one box against the builtin form: within 1 %
+// (profiles/fa_tr_asm_vs_builtin_ab_r5.json, prefill_ttft_32k_tr_ab_r5.jsonl) - the ~1-2 tiles
+// of look-ahead still covered the DMA's L2-hit latency.
 template <int OFF>
 __device__ __forceinline__ v4s ds_tr16(uint32_t addr) {
   v4s r;
