@@ -1,4 +1,5 @@
 # flash prefill: asm vs builtin transposed V reads on ONE box (interleaved kernel A/B, alternating 32K TTFT)
+# (ran on the A/B build with tune key prefill_fa_tr; the knob and the builtin form were removed after this measurement)
 set -o pipefail
 export PYTHONUNBUFFERED=1
 D=gpurun_out/r5za; mkdir -p $D
