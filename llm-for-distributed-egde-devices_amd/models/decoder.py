@@ -151,6 +151,10 @@ class Attention(nn.Module):
         return self.o(quant_if(attn, self.o))
 
 
+# prefill SwiGLU in the gate_up GEMM epilogue (EDGELLM_PREFILL_GLU=0: GEMM + blocked activation kernel)
+_PREFILL_GLU = os.environ.get("EDGELLM_PREFILL_GLU", "1") != "0"
+
+
 class MLP(nn.Module):
     def __init__(self, cfg: ModelConfig, dtype, device):
         super().__init__()
@@ -174,6 +178,13 @@ class MLP(nn.Module):
             if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and self.up.glu_rows_ok(x.q.shape[0]) \
                     and (x.q.shape[0] <= 64 or getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0])):
                 return self.down(self.up.glu(x), add=add)
+            if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and x.q.is_cuda and _PREFILL_GLU:
+                # prefill rows: silu(g) * u in the gate_up GEMM's epilogue (bf16 h, half the bytes
+                # of g / u), then the per-token quantisation for the down projection
+                h = ops.w8a8_prefill_glu(x.q, x.scale, self.up.w_packed, self.up.w_scale, self.up.bias,
+                                      self.up.out_features, self.up.in_features)
+                if h is not None:
+                    return self.down(QAct(*ops.quant_per_token(h)), add=add)
             return self.down(act_fn(self.up(x), "silu_glu_blocked", True), add=add)
         down_q = getattr(self.down, "takes_quantized_input", False)
         if self.act in ("gelu_tanh", "gelu") and down_q and isinstance(x, QAct) and x.q.dim() == 2 \

@@ -186,6 +186,14 @@ def layer_norm_quant(x, weight, bias, eps, residual=None):
     return _ref.layer_norm_quant(x, weight, bias, eps, residual)
 
 
+def w8a8_prefill_glu(qx, x_scale, w_packed, w_scale, bias, N: int, K: int):
+    """Prefill gate_up of a 16-blocked SwiGLU layer with silu(g) * u in the GEMM epilogue (GPU x32
+    kernel): bf16 h [M, N / 2], or None when the kernel does not take the shape."""
+    if not gpu_path(qx):
+        return None
+    return ext().w8a8_prefill_glu(qx, x_scale, w_packed, w_scale, bias, N, K)
+
+
 def quant_per_token(x):
     if _gpu(x):
         return ext().quant(x)

@@ -84,6 +84,8 @@ void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_gemv_ring(int on);
 void edge_w8a8_prefill_apack(int v);
 int edge_w8a8_apack_ok(int M, int N, int K, int KT);
+int edge_w8a8_prefill_glu(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
+                          void* out, int M, int N, int K, int KT, hipStream_t st);
 int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias,
                        void* out, int M, int N, int K, int KT, hipStream_t st);
 void edge_decode_attn_config(int target_wg);
@@ -563,6 +565,32 @@ void check_w8a8_operands(const at::Tensor& wp, const at::Tensor& sw, const std::
   TORCH_CHECK(sw.numel() == N);
   TORCH_CHECK(wp.numel() == (N + 15) / 16 * ((K + 63) / 64) * 1024, "packed weight has wrong size");
   if (bias) { need(*bias, at::kBFloat16, "bias"); TORCH_CHECK(bias->numel() == N); }
+}
+
+// Prefill gate_up of a 16-blocked SwiGLU layer with the SwiGLU in the GEMM epilogue: bf16 h [M, N / 2],
+// or None when the x32 kernel does not take the shape (the caller runs w8a8_gemm + act instead).
+std::optional<at::Tensor> w8a8_prefill_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp,
+                                           const at::Tensor& sw, const std::optional<at::Tensor>& bias, int64_t N,
+                                           int64_t K) {
+  DEVICE_GUARD(a);
+  need(a, at::kChar, "a");
+  TORCH_CHECK(a.size(-1) == K && a.is_contiguous(), "activation: contiguous [.., K]");
+  check_w8a8_operands(wp, sw, bias, N, K);
+  need(sa, at::kFloat, "a_scale");
+  const int64_t M = rows_of(a), KT = (K + 63) / 64;
+  TORCH_CHECK(sa.numel() == M, "per-token activation scales");
+  if (M <= 64 || N % 256 != 0 || K % 64 != 0) return std::nullopt;
+  auto os = a.sizes().vec();
+  os.back() = N / 2;
+  auto out = at::empty(os, a.options().dtype(at::kBFloat16));
+  const bool apk = edge_w8a8_apack_ok((int)M, (int)N, (int)K, (int)KT);
+  auto ap = apk ? at::empty({(M + 15) / 16 * 16 * K}, a.options()) : at::Tensor();
+  const int rc = edge_w8a8_prefill_glu(a.data_ptr(), apk ? ap.data_ptr() : nullptr, sa.data_ptr<float>(), wp.data_ptr(),
+                                       sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr, out.data_ptr(), (int)M,
+                                       (int)N, (int)K, (int)KT, stream());
+  if (rc == -2) return std::nullopt;
+  check(rc, "w8a8_prefill_glu");
+  return out;
 }
 
 // addend (optional, bf16 [.., N]): out = bf16(bf16(y) + addend) — the other branch of a parallel-
@@ -1098,6 +1126,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv_norm_on", []() { return edge_w8a8_gemv_norm_on() != 0; });
   m.def("w8a8_gemm_geluq", &w8a8_gemm_geluq, "W8A8 GEMV + GELU + per-(token, 64) int8 quantisation (M <= 64)");
   m.def("group_quant", &group_quant);
+  m.def("w8a8_prefill_glu", &w8a8_prefill_glu, "prefill gate_up (16-blocked SwiGLU) with silu(g) * u in the epilogue: bf16 h or None");
   m.def("sample", &sample);
   m.def("sample_shard", &sample_shard, "sampler phase 1 over a vocab shard (global ids)");
   m.def("sample_merge", &sample_merge, "sampler phase 2 over the shards' concatenated candidate lists");

@@ -250,7 +250,10 @@ __global__ void __launch_bounds__(256) pack_a_kernel(const int8_t* __restrict__ 
 //    2.05), so the launcher takes it from 512 tiles (two full rounds of the 256 CUs).  The same
 //    kernel on bf16 operands (v_mfma_f32_32x32x16_bf16) ran 1.19-1.24 PF against hipBLASLt's
 //    1.46-1.61 PF and was dropped.
-template <bool APK>
+// GLU: the gate_up projection of a 16-blocked SwiGLU layer (columns [gate(16) | up(16)] per 16
+// features, quant.linear.W8A8Linear.glu_blocked): the epilogue writes h = silu(g) * u in bf16 [M, N / 2]
+// instead of g / u [M, N], with g and u rounded to bf16 first, as the unfused path stores them.
+template <bool APK, bool GLU = false>
 __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                               const int8_t* __restrict__ Wp, const float* __restrict__ sw,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
@@ -360,6 +363,59 @@ __global__ void __launch_bounds__(512, 1) w8a8_gemm_x32_kernel(const int8_t* __r
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-load stages past the end
 
+  if constexpr (GLU) {
+    // the wave's 64 columns are two 32-column blocks [gate(16) | up(16)] = 32 features.  Lane:
+    // features (lane & 3) * 8 .. + 8 of the wave's 32 (block b = (lane & 3) >> 1; gate columns c0 ..
+    // c0 + 7, up 16 further), tokens it * 16 + (lane >> 2).  int32 restaged as below.
+    const int qg = lane & 3, bb = qg >> 1, c0 = bb * 32 + (qg & 1) * 8;
+    const int gcol = bn * BNV + wn * 64 + c0, F = N / 2;
+    const int f0 = (bn * BNV + wn * 64 + bb * 32) / 2 + (qg & 1) * 8;
+    const bf16_t* bp = bias != nullptr ? bias : g_zero_bf16;
+    float swg[8], swu[8], bgv[8], buv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int cg = min(gcol + e, N - 1), cu = min(gcol + 16 + e, N - 1);
+      swg[e] = sw[cg];
+      swu[e] = sw[cu];
+      bgv[e] = bf2f(bp[bias != nullptr ? cg : 0]);
+      buv[e] = bf2f(bp[bias != nullptr ? cu : 0]);
+    }
+    __syncthreads();                                  // every wave is done with the ring
+    int8_t* wt = ring + wave * (32 * 256);
+    const int tl = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k16 = 8 * b + 2 * q + hi;
+          const v4i v4 = v4i{acc[c][b][4 * q], acc[c][b][4 * q + 1], acc[c][b][4 * q + 2], acc[c][b][4 * q + 3]};
+          *reinterpret_cast<v4i*>(wt + tl * 256 + ((k16 ^ (tl & 15)) << 4)) = v4;
+        }
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int t = it * 16 + (lane >> 2);
+        const int row = bm * BMV + wm * 128 + c * 32 + t;
+        const float sr = sa[min(row, M - 1)];
+        const int kg = c0 >> 2, ku = (c0 + 16) >> 2;
+        const v4i g0 = *reinterpret_cast<const v4i*>(wt + t * 256 + ((kg ^ (t & 15)) << 4));
+        const v4i g1 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((kg + 1) ^ (t & 15)) << 4));
+        const v4i u0 = *reinterpret_cast<const v4i*>(wt + t * 256 + ((ku ^ (t & 15)) << 4));
+        const v4i u1 = *reinterpret_cast<const v4i*>(wt + t * 256 + (((ku + 1) ^ (t & 15)) << 4));
+        float h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int gi = e < 4 ? g0[e] : g1[e - 4], ui = e < 4 ? u0[e] : u1[e - 4];
+          const float g = bf2f(f2bf((float)gi * sr * swg[e] + bgv[e]));
+          const float u = bf2f(f2bf((float)ui * sr * swu[e] + buv[e]));
+          h[e] = g / (1.f + __expf(-g)) * u;
+        }
+        if (row < M && gcol < N) *reinterpret_cast<uint4*>(out + (size_t)row * F + f0) = pack8(h);
+      }
+    }
+    return;
+  }
   // epilogue: acc[c][b] register r -> token wm*128 + 32 c + (l & 31), column
   // wn*64 + 32 b + 8 (r >> 2) + 4 (l >> 5) + (r & 3).  Per c: the wave's 32 tokens x 64 columns of
   // int32 go to its LDS block (256-B rows, 16-B chunk k of token t at k ^ (t & 15)), then each lane
@@ -467,5 +523,28 @@ extern "C" int edge_w8a8_gemm_apk(const void* A, void* Ap, const float* sa, cons
   }
   hipLaunchKernelGGL((w8a8_gemm_big_kernel<128, true>), dim3(grid_m * grid_n), dim3(512), 0, st, (const int8_t*)Ap,
                      sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, grid_m, grid_n);
+  return (int)hipGetLastError();
+}
+
+// gate_up of a 16-blocked SwiGLU layer with the SwiGLU in the epilogue (x32 kernel, GLU): h = silu(g)
+// * u, bf16 [M, N / 2].  A row-major (per-token scales sa [M]); Ap: scratch of (M + 15) / 16 * 16 * K
+// bytes for the fragment-packed copy when edge_w8a8_apack_ok.  -2: the shape does not take the x32
+// kernel (the caller runs the GEMM and the blocked activation kernel instead).
+extern "C" int edge_w8a8_prefill_glu(const void* A, void* Ap, const float* sa, const void* Wp, const float* sw,
+                                     const void* bias, void* out, int M, int N, int K, int KT, hipStream_t st) {
+  if (M <= 64 || K % 64 != 0 || K / 64 != KT || N % 256 != 0) return -2;
+  const int NTt = N / 16, grid_n = N / 256;
+  if (!x32_takes(M, grid_n)) return -2;
+  const int gm2 = (M + 255) / 256;
+  if (Ap != nullptr && edge_w8a8_apack_ok(M, N, K, KT)) {
+    const int64_t total = (int64_t)((M + 15) / 16) * KT * 64;
+    hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const int8_t*)A,
+                       (int8_t*)Ap, M, K, KT, total);
+    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<true, true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)Ap,
+                       sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+  } else {
+    hipLaunchKernelGGL((w8a8_gemm_x32_kernel<false, true>), dim3(gm2 * grid_n), dim3(512), 0, st, (const int8_t*)A,
+                       sa, (const int8_t*)Wp, sw, (const bf16_t*)bias, (bf16_t*)out, M, N, K, KT, NTt, gm2, grid_n);
+  }
   return (int)hipGetLastError();
 }
