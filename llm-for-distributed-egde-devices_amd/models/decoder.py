@@ -178,7 +178,8 @@ class MLP(nn.Module):
             if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and self.up.glu_rows_ok(x.q.shape[0]) \
                     and (x.q.shape[0] <= 64 or getattr(self.down, "group_scales_ok", lambda m: False)(x.q.shape[0])):
                 return self.down(self.up.glu(x), add=add)
-            if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and x.q.is_cuda and _PREFILL_GLU:
+            if isinstance(x, QAct) and x.q.dim() == 2 and x.scale.dim() == 1 and x.q.is_cuda and x.q.is_contiguous() \
+                    and _PREFILL_GLU:
                 # prefill rows: silu(g) * u in the gate_up GEMM's epilogue (bf16 h, half the bytes
                 # of g / u), then the per-token quantisation for the down projection
                 h = ops.w8a8_prefill_glu(x.q, x.scale, self.up.w_packed, self.up.w_scale, self.up.bias,
