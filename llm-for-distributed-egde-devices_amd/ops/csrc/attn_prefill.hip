@@ -448,7 +448,10 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
   };
   const bool late = STG && wave >= FA_W / 2;                   // wave-uniform
   bool pend = false;
-  v8s pb_p[2][2];
+  // the staggered half's pending P lives in one of two named register sets that swap roles every
+  // tile (the loop body runs twice per iteration) instead of being copied each tile: ~30 fewer
+  // register moves per tile, +0.7-2 % (profiles/fa_pingpong_p_ab_r5.json)
+  v8s pbA[2][2], pbB[2][2];
   float alpha_p = 1.f;
   const char* vl_p = smem;
 
@@ -458,19 +461,21 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
   if (prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= FA_NT / 2) __builtin_amdgcn_s_setprio(1);
   if (ntiles > 0) issue(0);
   if (ntiles > 1) issue(1);
-  for (int t = 0; t < ntiles; ++t) {
+  // one key tile; pb receives this tile's P, pq holds the previous tile's (the staggered half's
+  // deferred P.V)
+  auto tile = [&](int t, v8s (&pb)[2][2], v8s (&pq)[2][2]) {
     if (t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                              // tile t landed; slot of t - 1 free
     if (t + 2 < ntiles) issue(t + 2);
     if constexpr (STG) {
       if (late && pend) {                                      // the previous tile's O^T += V^T P^T
-        pv(vl_p, pb_p, alpha_p);
+        pv(vl_p, pq, alpha_p);
         pend = false;
       }
     }
     const int k0 = t * FA_KT;
-    if (wq0 >= T || (CAUSAL && k0 > s0 + wq0 + 31)) continue;  // nothing visible for this wave
+    if (wq0 >= T || (CAUSAL && k0 > s0 + wq0 + 31)) return;    // nothing visible for this wave
     const char* kl = smem + (t % RING) * G::SLOT;
     const char* vl = kl + G::TILE;
 
@@ -515,7 +520,6 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     // every exponential; arguments here are <= 0 and a probability below 2^-126 may flush to 0
     const float alpha = __builtin_amdgcn_exp2f(m_i - msafe);
     float rs = 0.f;
-    v8s pb[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -531,20 +535,25 @@ __global__ void __launch_bounds__(FA_NT, 1) fa_kernel(
     m_i = mnew;
     if constexpr (STG) {
       if (late) {                                              // O^T update deferred one tile
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) pb_p[kb][ks] = pb[kb][ks];
         alpha_p = alpha;
         vl_p = vl;
         pend = true;
-        continue;
+        return;
       }
     }
     pv(vl, pb, alpha);
+  };
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    tile(t, pbA, pbB);
+    tile(t + 1, pbB, pbA);
   }
-  if constexpr (STG) {
-    if (late && pend) pv(vl_p, pb_p, alpha_p);                 // no DMA after the last tile: slot intact
+  if (t < ntiles) tile(t, pbA, pbB);
+  if constexpr (STG) {                                         // no DMA after the last tile: slot intact
+    if (late && pend) {                                        // the last tile's P: pbA if ntiles is odd
+      if (ntiles & 1) pv(vl_p, pbA, alpha_p);
+      else pv(vl_p, pbB, alpha_p);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // no DMA outlives the workgroup
 
