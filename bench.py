@@ -334,8 +334,104 @@ def _world1_env():
         os.environ.setdefault(k, v)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``python bench.py --gpus N`` without torchrun: start N fresh rank processes of this script
+    (one per GPU, torchrun's env contract: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT) and relay rank 0's stdout (the JSON line).  The parent never touches the GPU and
+    never execs; it only waits.  Watchdog: once any rank exits non-zero the others get
+    ``EDGELLM_LAUNCH_GRACE_S`` (default 30 s) to finish before they are terminated (a rank blocked
+    in a collective on a dead peer would otherwise hang), and ``EDGELLM_LAUNCH_TIMEOUT_S`` (default
+    0 = none) bounds the whole job.  Exit code: the worst child's (signals as 128 + signo).
+    The reference's multi-device mechanism this replaces: Llama_bf16_updated.py:31
+    (``device_map="auto"``)."""
+    import signal
+    import subprocess
+    import threading
+    port = _free_port()
+    grace = float(os.environ.get("EDGELLM_LAUNCH_GRACE_S", "30"))
+    limit = float(os.environ.get("EDGELLM_LAUNCH_TIMEOUT_S", "0"))
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", ROLE_RANK=str(r), ROLE_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TORCHELASTIC_RUN_ID="edgellm-bench")
+        env.setdefault("OMP_NUM_THREADS", "1")            # torchrun's default for multi-rank jobs
+        # rank 0's stdout is relayed line by line (the one JSON line); other ranks print to stderr
+        out = subprocess.PIPE if r == 0 else sys.stderr.fileno()
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                      stdout=out, text=True if r == 0 else None))
+
+    def relay(stream):
+        for line in stream:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
+
+    def kill_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(signo, _frame):
+        kill_all()
+        raise SystemExit(128 + signo)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    t0 = time.monotonic()
+    t_fail = None
+    try:
+        while any(p.poll() is None for p in procs):
+            now = time.monotonic()
+            if t_fail is None and any(p.returncode not in (None, 0) for p in procs):
+                t_fail = now
+                bad = [(i, p.returncode) for i, p in enumerate(procs) if p.returncode not in (None, 0)]
+                sys.stderr.write(f"[bench launcher] rank(s) {bad} failed; terminating the rest in {grace:.0f} s\n")
+            if (t_fail is not None and now - t_fail > grace) or (limit > 0 and now - t0 > limit):
+                sys.stderr.write("[bench launcher] terminating ranks still running\n")
+                kill_all()
+                deadline = time.monotonic() + 10
+                while any(p.poll() is None for p in procs) and time.monotonic() < deadline:
+                    time.sleep(0.1)
+                kill_all(signal.SIGKILL)
+                if t_fail is None:
+                    t_fail = now
+            time.sleep(0.1)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    th.join(timeout=5)
+    rcs = [p.wait() for p in procs]
+    worst = 0
+    for rc in rcs:
+        code = 128 - rc if rc < 0 else rc
+        worst = max(worst, code)
+    if limit > 0 and worst == 0 and t_fail is not None:
+        worst = 124
+    if worst:
+        sys.stderr.write(f"[bench launcher] job failed: rank exit codes {rcs}\n")
+    return worst
+
+
 def main(argv=None):
-    args = parse(argv)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = parse(raw)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us: start the N rank processes ourselves (the parent stays GPU-free)
+        raise SystemExit(launch_ranks(args.gpus, raw))
     if args.headinfer_heads is not None:
         args.lanes = 1          # the HeadInfer offload is host-orchestrated: one lane per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,7 +499,8 @@ def main(argv=None):
     if "per_rank" in res:
         out["bubble_frac_max"] = round(res["bubble_frac_max"], 4)
         out["per_rank"] = res["per_rank"]
-        for k in ("stage_cost_model_us", "stage_cost_spread", "slack", "host_issue_us_per_tick_max", "vocab_split"):
+        for k in ("stage_cost_model_us", "stage_cost_spread", "slack", "host_issue_us_per_tick_max", "vocab_split",
+                  "streams"):
             if k in res:
                 out[k] = res[k]
     print(json.dumps(out), flush=True)

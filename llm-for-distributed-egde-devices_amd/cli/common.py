@@ -95,6 +95,7 @@ def build_generator(model, rt: dict, max_batch: int = 1):
     """The decode engine for one agent / model as the runtime options ask: HeadInfer KV offload
     (``headinfer_heads``, chunked prefill), int8 KV cache, or the resident bf16 cache."""
     from ..engine import Generator
+    from ..engine.kv_cache import resolve_kv_dtype
     max_seq = rt.get("max_seq", 2048)
     h_on = rt.get("headinfer_heads")
     if h_on is not None and h_on < model.cfg.num_kv_heads:
@@ -103,9 +104,7 @@ def build_generator(model, rt: dict, max_batch: int = 1):
         chunk = min(int(rt.get("prefill_chunk") or 4096), max_seq)
         kv = HeadInferKV(model.cfg, max_batch, max_seq, int(h_on), model.device, chunk_size=chunk, dtype=model.dtype)
         return Generator(model, max_batch=max_batch, max_seq=max_seq, kv=kv)
-    kvd = rt.get("kv_dtype") or "bf16"
-    if kvd == "int8" and model.cfg.head_dim not in (64, 128, 256):
-        kvd = "bf16"
+    kvd = resolve_kv_dtype(rt.get("kv_dtype") or "bf16", model.cfg, model.dtype, model.device)
     return Generator(model, max_batch=max_batch, max_seq=max_seq, kv_dtype=kvd,
                      prefill_chunk=rt.get("prefill_chunk") if h_on is not None else None)
 
@@ -155,6 +154,7 @@ def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch,
     on the driver, rank 0).  ``gpus`` (YAML ``agents[].gpus``): the agent's rank group — one
     process per GPU, so GPU index = rank; default all ranks.  A rank outside the group holds a
     stub engine.  Returns (engine, tokenizer, source, bounds)."""
+    from ..engine.kv_cache import resolve_kv_dtype
     from ..parallel.pp_engine import PipelineGenerator, _cfg_of, load_stage
     rank, world, dev = launch
     ranks = sorted(int(g) for g in gpus) if gpus else list(range(world))
@@ -176,8 +176,7 @@ def build_pp_engine(model_id: str, precision: str, quant: str, rt: dict, launch,
                                             len(ranks), partition=rt.get("partition") or "balanced", group=group,
                                             ranks=ranks, calib=rt.get("calib") or "stage", rows=b,
                                             ctx=min(int(rt.get("max_seq", 2048)), 256))
-    if kvd == "int8" and stage.cfg.head_dim not in (64, 128, 256):
-        kvd = "bf16"
+    kvd = resolve_kv_dtype(kvd, stage.cfg, stage.dtype, dev)
     shard = None
     if vs:
         # every member gets its rows of the head from the last stage (one P2P per rank, at load)

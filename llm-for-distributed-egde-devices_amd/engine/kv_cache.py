@@ -22,11 +22,30 @@ import torch
 from ..models.configs import ModelConfig
 
 
+def resolve_kv_dtype(kv_dtype: str, cfg: ModelConfig, dtype=torch.bfloat16, device=None) -> str:
+    """The KV-cache dtype a model can run: int8 needs head_dim 64 / 128 / 256, and on the GPU a
+    bf16 model (the int8-KV kernels, attn_decode_i8.hip / kv_quant_append, take bf16 q / k / v);
+    otherwise the cache falls back to the model's 16-bit dtype, with a log line."""
+    if kv_dtype != "int8":
+        return kv_dtype
+    why = None
+    if cfg.head_dim not in (64, 128, 256):
+        why = f"head_dim {cfg.head_dim}"
+    elif dtype == torch.float16 and device is not None and torch.device(device).type == "cuda":
+        why = "an fp16 model"
+    if why is None:
+        return "int8"
+    from ..utils.log import get_logger
+    get_logger("kv_cache").info(f"int8 KV cache not available for {why}: using a 16-bit cache")
+    return "bf16"
+
+
 class KVCache:
     def __init__(self, cfg: ModelConfig, max_batch: int, max_seq: int, first_layer: int = 0,
                  last_layer: Optional[int] = None, dtype=torch.bfloat16, device=None,
                  num_kv_heads: Optional[int] = None, kv_dtype: str = "bf16"):
         assert kv_dtype in ("bf16", "int8"), kv_dtype
+        kv_dtype = resolve_kv_dtype(kv_dtype, cfg, dtype, device)
         self.cfg = cfg
         self.first = first_layer
         self.last = cfg.num_layers if last_layer is None else last_layer

@@ -77,14 +77,17 @@ def load_model(name_or_path: str, precision: str = "bf16", quant: str = "none", 
     """Returns (model, tokenizer, source) with source "checkpoint:<dir>", "int8-checkpoint:<dir>"
     (an edgellm quantised checkpoint: its stage is read directly, already quantised — ``quant``
     is then the checkpoint's own mode) or "random-init:<preset>".  ``units``: a half-layer stage."""
-    dtype = precision_dtype(precision, device, quant)
     qdir = quantized_checkpoint_dir(name_or_path, base_dir)
     if qdir is not None:
-        from ..quant.checkpoint import load_quantized
+        from ..quant.checkpoint import checkpoint_quant_mode, load_quantized
+        # the checkpoint's own INT8 mode sets the activation dtype (bf16 epilogues on the GPU),
+        # whatever --quant says (callers pass quant="none" for a checkpoint)
+        dtype = precision_dtype(precision, device, checkpoint_quant_mode(qdir))
         model = load_quantized(qdir, device=device, first=first, last=last, dtype=dtype, units=units)
         if quant not in (None, "none", model.quant_mode):
             log.warning(f"{qdir} holds {model.quant_mode} weights: --quant {quant} ignored")
         return model, load_tokenizer(qdir, model.cfg.vocab_size), f"int8-checkpoint:{qdir}"
+    dtype = precision_dtype(precision, device, quant)
     path = resolve_model_dir(name_or_path, base_dir)
     if path is not None:
         assert units is None, "half-layer stages of HF checkpoints: load the whole layers"

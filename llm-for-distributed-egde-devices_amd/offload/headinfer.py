@@ -41,7 +41,7 @@ from typing import List, Optional
 import torch
 
 from .. import ops
-from ..engine.kv_cache import KVCache
+from ..engine.kv_cache import KVCache, resolve_kv_dtype
 from ..models.configs import ModelConfig
 from ..models.layers import QAct
 
@@ -75,6 +75,7 @@ class HeadInferKV:
         and new-row buffers are sized by it instead of by the whole cache (``max_batch``).
         ``kv_dtype``: "bf16" or "int8" (int8 K/V + fp32 per-(token, head) scales on every tier)."""
         assert kv_dtype in ("bf16", "int8"), kv_dtype
+        kv_dtype = resolve_kv_dtype(kv_dtype, cfg, dtype, device)
         hk, D = cfg.num_kv_heads, cfg.head_dim
         assert 0 <= h_on <= hk, "h_on must be within [0, num_kv_heads]"
         self.cfg, self.first = cfg, first

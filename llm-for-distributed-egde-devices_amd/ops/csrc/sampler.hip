@@ -366,7 +366,8 @@ __global__ void __launch_bounds__(NT) argmax_chunk_kernel(const void* __restrict
 }
 
 // Per-chunk candidate superset -> pc[(row*C + c)*CCAP + s] as composite keys (unused slots 0),
-// pthr[row*C + c] = threshold key.  Thread t holds the chunk's elements [t * EPT, (t + 1) * EPT).
+// pthr[row*C + c] = threshold key.  Thread t holds EPT elements of the chunk in ``run_map``'s layout:
+// [t * EPT, (t + 1) * EPT) with `vec`, else t + j * NT (strided by the block size).
 // v0: global id of column 0 (vocab shard).
 template <bool BF16, int EPT>
 __global__ void __launch_bounds__(NT) topk_chunk_kernel(const void* __restrict__ logits,

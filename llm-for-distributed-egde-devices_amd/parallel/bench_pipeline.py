@@ -130,8 +130,16 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
                 stamps.append(time.perf_counter())
 
     sp = SamplingParams(max_new_tokens=S + 1, temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1)
+    fault = None
+    if os.environ.get("EDGELLM_FAULT_KILL_RANK", "") == str(rank):
+        # fault injection (tests): this rank dies hard at its first tick, as a crashed GPU process would
+        def fault(t):
+            sys.stderr.write(f"[edgellm fault] rank {rank} killed at tick {t}\n")
+            sys.stderr.flush()
+            os._exit(137)
     dist.barrier()
-    res_stage = stage.run(prompts, T, sp, S, seed=args.seed, hook=hook, watchdog=wd, stats_window=(t_a, t_b))
+    res_stage = stage.run(prompts, T, sp, S, seed=args.seed, hook=hook, watchdog=wd, stats_window=(t_a, t_b),
+                          fault=fault)
     wd.beat("report")
     fdt = torch.float64
     dt = torch.tensor([marks[t_b] - marks[t_a], marks[t_p] - marks[0]], device=cdev, dtype=fdt)
@@ -169,7 +177,11 @@ def run_pipeline_bench(args, build, model_config, kv_dtype=None):
                    bubble_frac_max=max(d.get("bubble_frac", 0.0) for d in per_rank),
                    host_issue_us_per_tick_max=max((d.get("host_issue_us_per_tick", 0.0) for d in per_rank),
                                                   default=0.0),
-                   ttft_ms=ttft[0] if ttft else None)
+                   ttft_ms=ttft[0] if ttft else None,
+                   # HIP streams per rank against the box's hardware queues (GPU_MAX_HW_QUEUES, 4 by
+                   # default): one compute stream per lane, one RCCL-internal stream per communicator
+                   streams=dict(compute=L, comm_groups=len({id(g) for g in stage.lane_groups}),
+                                hw_queues=int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))))
     dist.barrier()
     wd.stop()
     dist.destroy_process_group()

@@ -43,7 +43,7 @@ import torch.distributed as dist
 
 from .. import ops
 from ..engine.generate import GRAPH_BUCKET, SamplingParams, needs_host_sampler
-from ..engine.kv_cache import KVCache
+from ..engine.kv_cache import KVCache, resolve_kv_dtype
 from ..models.decoder import AttnCtx, DecoderLM
 from ..utils.tracing import debug_sync, trace_range
 
@@ -100,7 +100,7 @@ class PipelineStage:
         assert len(self.granks) == world, "one global rank per stage"
         self.h_on = headinfer_heads if offload else None
         self.prefill_chunk = max(1, prefill_chunk)
-        self.kv_dtype = kv_dtype
+        self.kv_dtype = kv_dtype = resolve_kv_dtype(kv_dtype, self.cfg, model.dtype, self.device)
         self.kv = None if offload else KVCache(self.cfg, micro_batch * n_micro, max_seq, self.first, self.last,
                                                model.dtype, self.device, kv_dtype=kv_dtype)
         self.attn_hook = None

@@ -151,6 +151,14 @@ def _cfg_of(model_id, precision, device, base_dir):
         from ..utils.tokenizer import load_tokenizer
         cfg = checkpoint_config(qdir)
         return cfg, load_tokenizer(qdir, cfg.vocab_size), f"int8-checkpoint:{qdir}"
+    from ..models.hf import resolve_model_dir
+    path = resolve_model_dir(model_id, base_dir)
+    if path is not None:
+        # an HF checkpoint: config.json + tokenizer only (no V x H embedding read on every rank)
+        from ..models.configs import from_hf_dir
+        from ..utils.tokenizer import load_tokenizer
+        cfg = from_hf_dir(path)
+        return cfg, load_tokenizer(path, cfg.vocab_size), f"checkpoint:{path}"
     m, tok, source = load_model(model_id, precision, "none", device, base_dir, first=0, last=0)
     return m.cfg, tok, source
 

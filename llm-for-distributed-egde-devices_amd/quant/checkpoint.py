@@ -43,6 +43,12 @@ def is_quantized_checkpoint(path: Optional[str]) -> bool:
         return json.load(fh).get("format") == FORMAT
 
 
+def checkpoint_quant_mode(path: str) -> str:
+    """The quantisation mode a checkpoint was written in (``quant_config.json`` "mode")."""
+    with open(os.path.join(path, "quant_config.json")) as f:
+        return json.load(f).get("mode", "none") or "none"
+
+
 def checkpoint_config(path: str) -> ModelConfig:
     with open(os.path.join(path, "quant_config.json")) as f:
         return ModelConfig(**json.load(f)["model_config"])

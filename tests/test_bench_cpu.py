@@ -81,6 +81,38 @@ def test_bench_pipeline_torchrun_cpu(n, lanes, vs):
     assert d["ttft_ms"] > 0 and d["host_issue_us_per_tick_max"] > 0
 
 
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_self_launch_cpu(n):
+    """``python bench.py --gpus N`` with no torchrun: the script starts its own N rank processes
+    and relays rank 0's single JSON line (the command form the driver uses for N = 1)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--gpus", str(n), "--device", "cpu", "--model", "tiny:llama", "--steps", "2",
+           "--warmup", "1", "--micro-batch", "2", "--prompt-len", "6", "--lanes", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert REQUIRED <= set(d) and d["n_gpus"] == n and d["world_size"] == n and len(d["per_rank"]) == n
+    assert d["config"]["parallelism"] == f"pp{n}" and d["value"] > 0
+
+
+def test_bench_self_launch_killed_rank_cpu(tmp_path):
+    """A rank that dies makes the launcher exit non-zero within its grace period instead of
+    hanging on the surviving ranks (they block in a collective on the dead peer)."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    # rank 1 kills itself when its pipeline stage starts (fault injection in the stage loop)
+    env.update(EDGELLM_FAULT_KILL_RANK="1", EDGELLM_LAUNCH_GRACE_S="5", EDGELLM_WATCHDOG_S="600")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--model", "tiny:llama", "--steps", "2",
+           "--warmup", "1", "--micro-batch", "2", "--prompt-len", "6", "--lanes", "1"]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert time.monotonic() - t0 < 240
+    assert "failed" in r.stderr and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 @pytest.mark.parametrize("n", [1, 2])
 def test_bench_headinfer_cpu(n):
     """BASELINE config 4 plumbing: --headinfer-heads offloads KV heads in the single-GPU engine and

@@ -258,3 +258,39 @@ def test_precision_dtype_honours_fp16(cuda):
     assert precision_dtype("fp16", cuda) == H16
     assert precision_dtype("bf16", cuda) == torch.bfloat16
     assert precision_dtype("fp16", cuda, "w8a8_smoothquant") == torch.bfloat16
+
+
+@pytest.mark.parametrize("mode", ["w8a8_smoothquant", "llm_int8"])
+def test_int8_checkpoint_with_fp16_precision(cuda, tmp_path, mode):
+    """An INT8 checkpoint loaded with the reference's fp16 precision runs bf16 activations (the
+    INT8 kernels' epilogues and the quantising norm take bf16) and decodes on the GPU."""
+    from edgellm.cli import quantize
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models.registry import load_model
+    out = quantize.main(["--model", "tiny:llama", "--quant", mode, "--out", str(tmp_path / "ck"),
+                         "--precision", "bf16", "--device", "cpu"])
+    m, _, source = load_model(out, "fp16", "none", cuda)
+    assert source.startswith("int8-checkpoint:") and m.dtype == torch.bfloat16
+    res = Generator(m, max_batch=1, max_seq=64).generate([[3, 1, 4, 1, 5, 9]], SamplingParams(max_new_tokens=6),
+                                                         seed=0)
+    assert len(res.tokens[0]) == 6
+
+
+@pytest.mark.parametrize("arch", ["llama", "gpt_neox"])
+def test_fp16_model_with_int8_kv_falls_back(cuda, arch):
+    """--precision fp16 --kv_dtype int8: the int8-KV kernels take bf16 q / k / v, so an fp16
+    model gets a 16-bit cache (logged) instead of failing at prefill; the tokens equal the
+    bf16-KV run's."""
+    from edgellm.cli.common import build_generator
+    from edgellm.engine import SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.offload import HeadInferKV
+    m = build_model(tiny(arch, num_layers=2), dtype=H16, device=cuda, seed=1)
+    g8 = build_generator(m, dict(max_seq=96, kv_dtype="int8"), max_batch=2)
+    assert not g8.kv.quantized and g8.kv.k.dtype == H16
+    sp = SamplingParams(max_new_tokens=8, do_sample=False)
+    prompts = [[5, 9, 2, 44, 17, 3], [8, 1, 77, 4, 12, 6]]
+    g16 = build_generator(m, dict(max_seq=96, kv_dtype="bf16"), max_batch=2)
+    assert g8.generate(prompts, sp, seed=0).tokens == g16.generate(prompts, sp, seed=0).tokens
+    hi = HeadInferKV(m.cfg, 1, 64, 0, cuda, dtype=H16, kv_dtype="int8")
+    assert not hi.q8
