@@ -7,33 +7,45 @@ on its own (Code/gRPC/server.py:14); here the pipeline's ``M x b`` KV rows becom
 ``engine.continuous.SlotDecoder`` does on one GPU:
 
 * ``PipelineSlotDecoder`` (driver, rank 0) has SlotDecoder's interface (``can_admit`` /
-  ``admit`` / ``step`` / ``poll`` / ``busy``), so ``serve.server.ServingEngine`` drives either.
-  Every call is one command broadcast to all ranks (``serve_workers`` runs it on theirs).
-* ``admit``: the prompt is prefilled into one free row on every stage (hidden states hop stage
-  to stage), the last stage samples the first token, and the row becomes ACTIVE.
+  ``admit`` / ``admit_batch`` / ``step`` / ``poll`` / ``busy``), so ``serve.server.ServingEngine``
+  drives either.  Every call is one command broadcast to all ranks (``serve_workers`` runs it on
+  theirs).
+* ``admit_batch``: every queued request that fits is admitted by ONE command: the prompts are
+  prefilled together in one ragged pass (right-padded, per-row last positions) into a scratch
+  cache on every stage (hidden states hop stage to stage once for the whole batch), their K/V rows
+  are copied into the free slot rows, and the last stage samples every first token in one launch.
 * ``step(n)``: n decode rounds of ALL rows through the usual micro-batched tick schedule (rank
   r computes item i = k M + m at tick i + r; hidden states go r -> r + 1, the tokens sampled on
-  the last stage come back to stage 0 one exchange later, M >= P keeps that ring full).  Free rows
-  ride along at position 0 with one key; ``pos`` / ``seq_lens`` advance by the active flags
-  (``ops.decode_advance``), so a free row never writes past its first cache slot.
+  the last stage come back to stage 0 one exchange later, M >= P keeps that ring full).  Each row
+  carries an on-device token budget: a row that reaches it stops advancing (its active flag drops
+  inside the decode body, on every stage alike), so ``n`` is not clipped to the shortest
+  remaining request — a nearly finished request no longer forces one command per token on all
+  the others.  Free rows ride along at position 0 with one key; ``pos`` / ``seq_lens`` advance by
+  the active flags (``ops.decode_advance``), so a finished or free row never writes past its slot.
+* on the GPU the decode body of each micro-batch (stage forward, and on the last stage the fused
+  sampler, the bookkeeping and the budget update) is a HIP graph per (micro-batch, KV-length
+  bucket), captured on its second use and replayed afterwards, as ``PipelineStage`` does; the P2P
+  exchanges stay outside the graphs.
 * a request that hits EOS or its token budget is released by ``poll`` at the next command
   boundary; its row is admitted to the next queued request at once, while the other rows keep
   decoding.
 
 One sampling configuration per session, as SlotDecoder (the fused sampler takes one per launch).
-Decode steps run eagerly (no graph capture: the active set changes between commands).  Greedy
-requests give exactly the tokens of a single-process ``Generator`` run.
+Greedy requests give exactly the tokens of a single-process ``Generator`` run.  The sampling rank
+of a slot session is the last stage (its full LM head): the vocabulary-split head of
+``PipelineStage`` runs in ``generate`` jobs, not in slot sessions.
 """
 from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from .. import ops
-from ..engine.generate import GenerationResult, SamplingParams
+from ..engine.generate import GRAPH_BUCKET, GenerationResult, SamplingParams, needs_host_sampler
+from ..engine.kv_cache import KVCache
 from ..models.decoder import AttnCtx
 
 CMD_SLOT_OPEN, CMD_SLOT_ADMIT, CMD_SLOT_STEP = 4, 5, 6
@@ -49,8 +61,11 @@ class _SlotSession:
         self.M, self.b = st.M, st.b
         self.width = width
         dev = st.device
+        # per row: active flag (pos / lens increments) and the decode rounds it may still take
         self.active = [torch.zeros(self.b, dtype=torch.int32, device=dev) for _ in range(self.M)]
+        self.budget = [torch.zeros(self.b, dtype=torch.int32, device=dev) for _ in range(self.M)]
         self.host_active = [0] * (self.M * self.b)
+        self.host_budget = [0] * (self.M * self.b)
         self.host_len = [1] * (self.M * self.b)        # keys each row attends over next (upper bound)
         self.col = 1                                   # out column the next decode round writes
         for m in range(self.M):
@@ -65,62 +80,95 @@ class _SlotSession:
             self.rng_adm = torch.tensor([(seed + 104729) & 0x7FFFFFFF, 0], dtype=torch.int32, device=dev)
             self.step_ = [torch.ones(1, dtype=torch.long, device=dev) for _ in range(self.M)]
             self.out = [torch.zeros(self.b, width, dtype=torch.long, device=dev) for _ in range(self.M)]
+        # decode graphs per (micro-batch, KV bucket): GPU, a sampler that stays on the device
+        self.use_graphs = bool(st.use_graphs and st.cuda and getattr(st.kv, "graph_safe", True)
+                               and not needs_host_sampler(sampling, st.cfg.vocab_size)
+                               and all(getattr(mm, "graph_safe", True) or getattr(mm, "graph_safe_rows", 0) >= self.b
+                                       for mm in st.model.modules()))
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._warm: Dict[int, bool] = {}
+        self._pool = None
 
     # ------------------------------------------------------------------ admission
     @torch.no_grad()
-    def admit(self, row: int, ids: torch.Tensor) -> torch.Tensor:
-        """Prefill ``ids`` [T] into ``row`` on this stage; the last stage samples the first token.
-        Returns a [1] token tensor (meaningful on the last stage)."""
+    def admit_batch(self, rows: Sequence[int], lens: Sequence[int], max_new: Sequence[int],
+                    ids_cat: torch.Tensor) -> torch.Tensor:
+        """Prefill k prompts (concatenated in ``ids_cat``, lengths ``lens``) into ``rows`` on this
+        stage in ONE ragged pass; the last stage samples every first token in one launch.  Returns
+        the k first tokens (meaningful on the last stage)."""
         st, eng = self.st, self.eng
-        m, i = divmod(row, self.b)
-        T = int(ids.numel())
+        k = len(rows)
         dev = st.device
         H = st.cfg.hidden_size
-        sp0 = torch.zeros(1, dtype=torch.int32, device=dev)
-        ctx = AttnCtx("prefill", 1, T, sp0, sp0 + T, T, st.kv.rows(row, row + 1), st.rope)
-        x_ids = ids.to(dev).view(1, T)
+        T = max(lens)
+        lens_t = torch.tensor(list(lens), dtype=torch.long)
+        # [k, T] right-padded; a pad repeats its row's first token (never a new penalty id)
+        ids = torch.empty(k, T, dtype=torch.long)
+        off = 0
+        flat = ids_cat.to("cpu", torch.long)
+        for i, n in enumerate(lens):
+            ids[i, :n] = flat[off:off + n]
+            ids[i, n:] = flat[off]
+            off += n
+        ids = ids.to(dev)
+        scratch = KVCache(st.cfg, k, T, st.kv.first, st.kv.last, st.model.dtype, dev, kv_dtype=st.kv_dtype)
+        sp0 = torch.zeros(k, dtype=torch.int32, device=dev)
+        last = (lens_t - 1).to(dev)
+        ctx = AttnCtx("prefill", k, T, sp0, sp0 + T, T, scratch.rows(0, k), st.rope, last_pos=last)
         hidden = None
         if not st.is_first:
-            hidden = torch.empty(T, H, dtype=st.model.dtype, device=dev)
+            hidden = torch.empty(k * T, H, dtype=st.model.dtype, device=dev)
             st._exchange([], [(hidden, st.prev)])
-        out = st.model(x_ids if st.is_first else None, ctx, hidden=hidden, logits="last")
-        tok = torch.zeros(1, dtype=torch.long, device=eng.cdev)
+        out = st.model(ids if st.is_first else None, ctx, hidden=hidden, logits="last")
         if not st.is_last:
             st._exchange([(out.contiguous(), st.next)], [])
-        else:
-            seen = self.seen[m][i:i + 1]
-            seen.zero_()
-            seen[0, x_ids[0]] = 1
+        # the prompt's K / V rows into the slot rows of the session's cache (one copy per tensor)
+        ridx = torch.tensor(list(rows), dtype=torch.long, device=dev)
+        for name in ("k", "v") + (("ks", "vs") if scratch.quantized else ()):
+            dst, src = getattr(st.kv, name), getattr(scratch, name)
+            dst[:, ridx, :, :T] = src
+        del scratch
+        toks = torch.zeros(k, dtype=torch.long, device=eng.cdev)
+        mb = [divmod(r, self.b) for r in rows]
+        if st.is_last:
+            seen = torch.zeros(k, st.cfg.vocab_size, dtype=torch.uint8, device=dev)
+            seen.scatter_(1, ids, 1)
             sp = self.sp
             nxt = ops.sample(out, seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, self.rng_adm,
                              sp.do_sample)
             self.rng_adm[1:].add_(1)
-            st.tok[m][i:i + 1].copy_(nxt)
-            self.out[m][i].zero_()
-            self.out[m][i, self.col - 1] = nxt[0]
-            tok.copy_(nxt.to(tok.device))
-        st.pos[m][i] = T
-        st.lens[m][i] = T + 1
-        self.active[m][i] = 1
-        self.host_active[row] = 1
-        self.host_len[row] = T + 1
-        return tok
+            for i, (m, j) in enumerate(mb):
+                self.seen[m][j].copy_(seen[i])
+                st.tok[m][j:j + 1].copy_(nxt[i:i + 1])
+                self.out[m][j].zero_()
+                self.out[m][j, self.col - 1:self.col].copy_(nxt[i:i + 1])
+            toks.copy_(nxt.to(toks.device))
+        for i, (m, j) in enumerate(mb):
+            n = int(lens[i])
+            b_left = max(0, int(max_new[i]) - 1)        # the first token came from the prefill
+            st.pos[m][j] = n
+            st.lens[m][j] = n + 1
+            self.active[m][j] = 1 if b_left > 0 else 0
+            self.budget[m][j] = b_left
+            r = rows[i]
+            self.host_active[r] = 1 if b_left > 0 else 0
+            self.host_budget[r] = b_left
+            self.host_len[r] = n + 1
+        return toks
 
     # ------------------------------------------------------------------ decode rounds
-    def _set_active(self, active: Sequence[int]):
-        """Rows released since the last command go back to position 0 with one key."""
+    def _release(self, released: Sequence[int]):
+        """Rows the driver released since the last command go back to position 0 with one key."""
         st = self.st
-        for r, a in enumerate(active):
-            a = int(a)
-            if a == self.host_active[r]:
-                continue
-            m, i = divmod(r, self.b)
-            self.active[m][i] = a
-            self.host_active[r] = a
-            if not a:
-                st.pos[m][i] = 0
-                st.lens[m][i] = 1
-                self.host_len[r] = 1
+        for r in released:
+            m, i = divmod(int(r), self.b)
+            self.active[m][i] = 0
+            self.budget[m][i] = 0
+            st.pos[m][i] = 0
+            st.lens[m][i] = 1
+            self.host_active[r] = 0
+            self.host_budget[r] = 0
+            self.host_len[r] = 1
 
     def _decode_body(self, m: int, max_len: int):
         st, b = self.st, self.b
@@ -132,17 +180,43 @@ class _SlotSession:
                              self.rng[m], sp.do_sample)
             ops.decode_advance(nxt, st.tok[m], self.out[m], self.step_[m], st.pos[m], st.lens[m], self.rng[m],
                                self.active[m])
-            return
-        st.hout[m].copy_(out)
-        st.pos[m].add_(self.active[m])
-        st.lens[m].add_(self.active[m])
+        else:
+            st.hout[m].copy_(out)
+            st.pos[m].add_(self.active[m])
+            st.lens[m].add_(self.active[m])
+        # every stage alike: a row that used its last round stops advancing
+        self.budget[m].sub_(self.active[m])
+        self.active[m].mul_(self.budget[m].gt(0).to(torch.int32))
+
+    def _bucket(self, n: int) -> int:
+        return min(self.st.max_seq, ((n + GRAPH_BUCKET - 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
+
+    def _decode(self, m: int, max_len: int):
+        if not self.use_graphs:
+            return self._decode_body(m, max_len)
+        bucket = self._bucket(max_len)
+        if not self._warm.get(m):
+            self._warm[m] = True
+            return self._decode_body(m, bucket)         # first decode of m: eager (warm-up)
+        g = self._graphs.get((m, bucket))
+        if g is None:
+            # every P2P of this tick has completed on the host's order (``_exchange``), and capture
+            # records without executing: the device is idle before the capture starts
+            torch.cuda.synchronize(self.st.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+                self._decode_body(m, bucket)
+            if self._pool is None:
+                self._pool = g.pool()
+            self._graphs[(m, bucket)] = g
+        g.replay()
 
     @torch.no_grad()
-    def step(self, n: int, active: Sequence[int]) -> torch.Tensor:
+    def step(self, n: int, released: Sequence[int]) -> torch.Tensor:
         """``n`` decode rounds of every row; returns the new tokens [M b, n] (last stage)."""
         st, eng = self.st, self.eng
         M, b, P = self.M, self.b, st.world
-        self._set_active(active)
+        self._release(released)
         # the tokens the last stage sampled since the previous round (admissions, the previous
         # command's final round) -> stage 0, which embeds them
         if P > 1 and (st.is_first or st.is_last):
@@ -173,10 +247,14 @@ class _SlotSession:
             st._exchange(sends, recvs)
             if 0 <= cur < n_items:
                 k, m = divmod(cur, M)
-                self._decode_body(m, min(st.max_seq, base[m] + k))
+                self._decode(m, min(st.max_seq, base[m] + k))
         for r in range(M * b):
             if self.host_active[r]:
-                self.host_len[r] += n
+                used = min(n, self.host_budget[r])
+                self.host_len[r] += used
+                self.host_budget[r] -= used
+                if self.host_budget[r] == 0:
+                    self.host_active[r] = 0
         c0 = self.col
         self.col += n
         if st.is_last:
@@ -192,14 +270,20 @@ def handle_slot_command(eng, hdr0: torch.Tensor) -> None:
         sp = _sampling_of(hdr0, fl)
         eng._slot_sess = _SlotSession(eng, sp, int(hdr0[2]), int(hdr0[3])) if eng.member else None
     elif cmd == CMD_SLOT_ADMIT:
-        ids = eng._bcast(torch.zeros(int(hdr0[3]), dtype=torch.long, device=eng.cdev))
-        tok = eng._slot_sess.admit(int(hdr0[2]), ids) if eng.member else torch.zeros(1, dtype=torch.long,
-                                                                                     device=eng.cdev)
-        eng._deliver([tok])
+        k, total = int(hdr0[2]), int(hdr0[3])
+        meta = eng._bcast(torch.zeros(k, 3, dtype=torch.long, device=eng.cdev))
+        ids = eng._bcast(torch.zeros(total, dtype=torch.long, device=eng.cdev))
+        if eng.member:
+            mt = meta.tolist()
+            toks = eng._slot_sess.admit_batch([x[0] for x in mt], [x[1] for x in mt], [x[2] for x in mt], ids)
+        else:
+            toks = torch.zeros(k, dtype=torch.long, device=eng.cdev)
+        eng._deliver([toks])
     elif cmd == CMD_SLOT_STEP:
-        act = eng._bcast(torch.zeros(eng.M * eng.b, dtype=torch.int32, device=eng.cdev))
+        nrel = int(hdr0[3])
+        rel = eng._bcast(torch.zeros(max(1, nrel), dtype=torch.int32, device=eng.cdev))
         n = int(hdr0[2])
-        toks = eng._slot_sess.step(n, act.tolist()) if eng.member else \
+        toks = eng._slot_sess.step(n, rel.tolist()[:nrel]) if eng.member else \
             torch.zeros(eng.M * eng.b, n, dtype=torch.long, device=eng.cdev)
         eng._deliver([toks])
     else:
@@ -237,6 +321,7 @@ class PipelineSlotDecoder:
         self.width = width
         self.gen = eng                               # (ServingEngine reads .gen.max_seq through us)
         self.slots: List[Optional[_Slot]] = [None] * self.B
+        self._released: List[int] = []               # rows freed by poll, reset on the next command
         self.steps = 0
         hdr = torch.zeros(_HDR, dtype=torch.long, device=eng.cdev)
         hdr[0], hdr[1], hdr[2], hdr[3] = CMD_SLOT_OPEN, eng.tag, int(seed), int(width)
@@ -266,43 +351,69 @@ class PipelineSlotDecoder:
 
     @torch.no_grad()
     def admit(self, ids: Sequence[int], max_new: int, eos: Optional[int] = None, tag=None) -> int:
-        assert self.can_admit(len(ids), max_new), "no slot / cache room for this request"
-        s = self.free_slots()[0]
+        return self.admit_batch([(ids, max_new, eos, tag)])[0]
+
+    @torch.no_grad()
+    def admit_batch(self, reqs: Sequence[tuple]) -> List[int]:
+        """Admit ``reqs`` = [(ids, max_new, eos, tag)] with ONE command (one ragged prefill on every
+        stage, one sampler launch); returns their slots."""
+        free = self.free_slots()
+        assert len(reqs) <= len(free), "more requests than free slots"
+        for ids, mx, _, _ in reqs:
+            assert self.can_admit(len(ids), mx), "no slot / cache room for this request"
         eng = self.eng
         t0 = time.perf_counter()
+        slots = free[:len(reqs)]
+        k = len(reqs)
+        meta = torch.tensor([[self.rows[s], len(r[0]), int(r[1])] for s, r in zip(slots, reqs)], dtype=torch.long,
+                            device=eng.cdev)
+        cat = [int(t) for r in reqs for t in r[0]]
         hdr = torch.zeros(_HDR, dtype=torch.long, device=eng.cdev)
-        hdr[0], hdr[1], hdr[2], hdr[3] = CMD_SLOT_ADMIT, eng.tag, self.rows[s], len(ids)
+        hdr[0], hdr[1], hdr[2], hdr[3] = CMD_SLOT_ADMIT, eng.tag, k, len(cat)
         eng._bcast(hdr)
-        x = eng._bcast(torch.tensor(list(ids), dtype=torch.long, device=eng.cdev))
-        tok = self.sess.admit(self.rows[s], x)
-        eng._deliver([tok])
-        self.slots[s] = _Slot(tag, len(ids), max_new, eos, t0, time.perf_counter(), [int(tok[0])])
-        return s
+        eng._bcast(meta)
+        x = eng._bcast(torch.tensor(cat, dtype=torch.long, device=eng.cdev))
+        self._flush_released()
+        toks = self.sess.admit_batch([self.rows[s] for s in slots], [len(r[0]) for r in reqs],
+                                     [int(r[1]) for r in reqs], x)
+        eng._deliver([toks])
+        first = toks.tolist()
+        t1 = time.perf_counter()
+        for s, r, tk in zip(slots, reqs, first):
+            ids, mx, eos, tag = r
+            self.slots[s] = _Slot(tag, len(ids), mx, eos, t0, t1, [int(tk)])
+        return slots
+
+    def _flush_released(self):
+        """Released rows are reset by the workers with the next STEP command; an admission reuses
+        a row directly (its prefill rewrites the row's whole state), so it is dropped from the list."""
+        taken = set(self.rows[s] for s, x in enumerate(self.slots) if x is not None)
+        self._released = [r for r in self._released if r not in taken]
 
     @torch.no_grad()
     def step(self, n: int = 1) -> int:
-        """Up to ``n`` decode rounds of every occupied slot, never past a slot's token budget."""
-        live = [x for x in self.slots if x is not None]
+        """``n`` decode rounds of every occupied slot (each row stops on the device at its token
+        budget, so the round count is not clipped to the shortest remaining request)."""
+        live = [x for x in self.slots if x is not None and len(x.tokens) < x.max_new]
         if not live:
             return 0
-        n = min(n, min(x.max_new - len(x.tokens) for x in live), self.width - self.sess.col)
+        n = min(n, max(x.max_new - len(x.tokens) for x in live), self.width - self.sess.col)
         if n <= 0:
             return 0
         eng = self.eng
-        act = [0] * (eng.M * eng.b)
-        for s, x in enumerate(self.slots):
-            if x is not None:
-                act[self.rows[s]] = 1
+        self._flush_released()
+        rel = list(self._released)
+        self._released = []
         hdr = torch.zeros(_HDR, dtype=torch.long, device=eng.cdev)
-        hdr[0], hdr[1], hdr[2] = CMD_SLOT_STEP, eng.tag, n
+        hdr[0], hdr[1], hdr[2], hdr[3] = CMD_SLOT_STEP, eng.tag, n, len(rel)
         eng._bcast(hdr)
-        a = eng._bcast(torch.tensor(act, dtype=torch.int32, device=eng.cdev))
-        toks = self.sess.step(n, a.tolist())
+        r = eng._bcast(torch.tensor(rel or [0], dtype=torch.int32, device=eng.cdev))
+        toks = self.sess.step(n, r.tolist()[:len(rel)])
         eng._deliver([toks])
         new = toks.tolist()
         for s, x in enumerate(self.slots):
             if x is not None:
-                x.tokens.extend(new[self.rows[s]])
+                x.tokens.extend(new[self.rows[s]][:max(0, x.max_new - len(x.tokens))])
         self.steps += n
         return n
 
@@ -321,4 +432,5 @@ class PipelineSlotDecoder:
                 done.append((x.tag, GenerationResult([toks], [x.prompt_len], now - x.t0, x.t_first - x.t0,
                                                      now - x.t_first, [])))
                 self.slots[s] = None
+                self._released.append(self.rows[s])
         return done

@@ -155,21 +155,28 @@ class ServingEngine:
                     continue
                 # admit every waiting request of this session's sampling configuration that fits;
                 # a request whose admission fails is failed alone and dropped
-                keep = []
+                keep, take = [], []
+                nfree = len(dec.free_slots())
                 for it in pending:
                     ids, sp, _, fut, t_sub = it
-                    if sp.key() == dec.sp.key() and dec.can_admit(len(ids), sp.max_new_tokens):
+                    if sp.key() == dec.sp.key() and len(take) < nfree and dec.can_admit(len(ids), sp.max_new_tokens):
+                        take.append(it)
+                    else:
+                        keep.append(it)
+                pending = keep
+                if take and hasattr(dec, "admit_batch"):
+                    # one command admits them all (pipeline: one ragged prefill per stage)
+                    dec.admit_batch([(it[0], it[1].max_new_tokens, eos, it) for it in take])
+                else:
+                    for it in take:
                         try:
-                            dec.admit(ids, sp.max_new_tokens, eos, tag=it)
+                            dec.admit(it[0], it[1].max_new_tokens, eos, tag=it)
                         except Exception as e:     # noqa: BLE001 - reported to that caller
                             if getattr(self.gen, "fatal_on_error", False):
                                 raise
                             self.stats["errors"] += 1
-                            if not fut.done():
-                                fut.set_exception(e)
-                    else:
-                        keep.append(it)
-                pending = keep
+                            if not it[3].done():
+                                it[3].set_exception(e)
                 if not dec.busy():
                     continue                       # nothing admitted: the head opens a new session
                 occ = sum(s is not None for s in dec.slots)
@@ -196,9 +203,13 @@ class ServingEngine:
         self.writer.write(event="request", mode="continuous", prompt_tokens=len(it[0]), generated_tokens=len(toks),
                           ttft_ms=res.prefill_s * 1e3, elapsed_s=res.elapsed_s, slots_busy=occ,
                           queue_ms=(time.perf_counter() - it[4]) * 1e3)
+        now = time.perf_counter()
         it[3].set_result({"tokens": toks, "text": self.tok.decode(toks, skip_special_tokens=True),
                           "tokens_per_s": len(toks) / res.elapsed_s if res.elapsed_s > 0 else 0.0,
-                          "queue_ms": (time.perf_counter() - it[4]) * 1e3, "batch_size": occ})
+                          "queue_ms": (now - it[4]) * 1e3, "batch_size": occ,
+                          # submission -> first token (queueing + admission prefill)
+                          "ttft_ms": ((now - it[4]) - (res.elapsed_s - res.prefill_s)) * 1e3,
+                          "latency_ms": (now - it[4]) * 1e3})
 
     # ------------------------------------------------------------------ static-batch worker
     def _loop(self):

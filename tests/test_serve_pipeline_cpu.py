@@ -105,3 +105,33 @@ def test_serve_cli_torchrun_shutdown_releases_every_rank(tmp_path):
         if p.poll() is None:
             p.kill()
     assert rc == 0, open(tmp_path / "serve.log").read()[-3000:]
+
+
+def test_continuous_batching_4_ranks_staggered(tmp_path):
+    """16 staggered greedy requests over a 4-rank pipeline (parallel.pp_slots): queued requests
+    are admitted together (one ragged prefill per command), every row stops on the device at its
+    own token budget, a short request submitted while long ones decode finishes before all of
+    them, and every answer equals the single-process Generator's."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models.registry import load_model
+    out = tmp_path / "load.json"
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.path.join(ROOT, "tests"), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "helpers", "pp_slots_load_worker.py"), str(out), "tiny:llama"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:]
+    got = json.loads(out.read_text())
+    order = got["order"]
+    assert sorted(order) == sorted(k for k, _, _ in got["requests"])
+    assert order.index("short") < min(order.index(k) for k, _, mx in got["requests"] if mx >= 20), order
+    model, _, _ = load_model("tiny:llama", "fp32", "none", "cpu")
+    gen = Generator(model, max_batch=1, max_seq=128)
+    for key, ids, mx in got["requests"]:
+        sp = SamplingParams(max_new_tokens=mx, do_sample=False, temperature=0.7, top_k=50, top_p=0.9,
+                            repetition_penalty=1.1)
+        assert got["tokens"][key] == gen.generate([ids], sp).tokens[0], key
+    m = got["metrics"]
+    assert m["requests"] == 16 and m["max_concurrent"] >= 8
