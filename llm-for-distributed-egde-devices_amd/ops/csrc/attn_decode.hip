@@ -24,7 +24,7 @@
 namespace {
 constexpr int NT = 256;
 constexpr int NW = NT / 64;
-constexpr int UNROLL = 4;
+constexpr int UNROLL_DEF = 4;   // key groups per wave per chunk (tune "decode_attn_unroll": 8 at MHA D = 128)
 
 struct Fuse {
   const int* pos;       // [B] cache position of the new token (seq_lens - 1)
@@ -68,7 +68,7 @@ template <int D> struct Lanes { static constexpr int v = (D / 8 <= 8) ? 8 : ((D 
 // (occupancy instead of a second register buffer), and FUSED keeps the new key in registers (no
 // append barrier); OCC = 0: two register buffers, no occupancy target.  NWV: waves per workgroup.
 // HF: q / K / V / out are IEEE fp16 instead of bf16 (the reference's fp16 agents); fp32 softmax.
-template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC, bool HF, int NWV = NW>
+template <int D, int G, bool DIRECT, bool FUSED, bool QOUT, int OCC, bool HF, int NWV = NW, int UNROLL = UNROLL_DEF>
 __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     int64_t c_sb, int64_t c_sh, const int* __restrict__ seq_lens, float scale_log2, int CH, int nsplit,
@@ -122,6 +122,11 @@ __global__ void __launch_bounds__(NWV * 64, OCC > 0 ? OCC : 1) decode_attn_kerne
     for (int u = 0; u < UNROLL; ++u) {
       const int k = base + kl + u * KPB;
       const size_t off = (size_t)(k < bound ? k : 0) * D + dc;
+      if (UNROLL > UNROLL_DEF && base + u * KPB >= bound) {   // wave-uniform: a whole group past the end
+        kr[u] = uint4{0, 0, 0, 0};                              // (masked in consume; zero, never NaN)
+        vr[u] = uint4{0, 0, 0, 0};
+        continue;
+      }
       if constexpr (OCC > 0) {                   // read once per step: nontemporal
         kr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(kb + off)));
         vr[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(vb + off)));
@@ -418,6 +423,9 @@ static int g_target_wg = 512;   // >= 2 workgroups per CU before splitting K
 static int g_attn_occ = 4;
 // query-head split for small grids (tune "decode_attn_gsplit"): 0 automatic, 1 off, 2 always (GQA)
 static int g_attn_gsplit = 0, g_attn_early = 1;
+// key groups per wave per chunk of the barrier-free MHA D = 128 form (4 / 8; tune "decode_attn_unroll")
+static int g_attn_unroll = 4;
+extern "C" void edge_decode_attn_unroll(int v) { g_attn_unroll = v == 8 ? 8 : 4; }
 // MHA grids below this many workgroups (batch 1: 32 on Llama-2-7B) take the double-buffered form:
 // each workgroup walks its keys in several chunks, and there the next chunk in flight beats the
 // single-buffered form's extra occupancy (tools/recipes/r4occ_b1.sh: 1 x 200 keys 8.71 -> 7.95 us,
@@ -442,6 +450,12 @@ void launch_attn(dim3 grid, size_t lds, hipStream_t st, const void* q, int64_t q
     constexpr int OCC4 = G <= 2 ? 4 : (G == 4 ? 2 : 1), OCC5 = G <= 2 ? 5 : OCC4;
     // (8- and 16-wave workgroups for batch-1 grids measured slower: Llama-3.2-1B decode step
     // 1.08 -> 1.19 ms with 8 waves)
+    if constexpr (D == 128 && G == 1) {
+      if (g_attn_occ == 4 && !small_grid && g_attn_unroll == 8) {
+        hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4, HF, NW, 8>), ATTN_ARGS);
+        return;
+      }
+    }
     if (g_attn_occ == 4 && !small_grid) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC4, HF>), ATTN_ARGS); return; }
     if (g_attn_occ == 5) { hipLaunchKernelGGL((decode_attn_kernel<D, G, DI, FU, QO, OCC5, HF>), ATTN_ARGS); return; }
   }

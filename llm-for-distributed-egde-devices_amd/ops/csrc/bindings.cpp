@@ -109,6 +109,8 @@ int edge_bf16_ring_min_rows();
 void edge_decode_attn_gsplit(int v);
 void edge_decode_attn_small(int v);
 void edge_decode_attn_early(int v);
+void edge_decode_attn_unroll(int v);
+void edge_w8a8_wreg_cfg(int v);
 int edge_w8a8_r256_ok(int M, int N, int K, int epi);
 int edge_w8a8_r256(const void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                    int M, int N, int K, int epi, hipStream_t st);
@@ -1150,6 +1152,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "decode_attn_small") edge_decode_attn_small((int)a);
     else if (what == "decode_attn_gsplit") edge_decode_attn_gsplit((int)a);
     else if (what == "decode_attn_early") edge_decode_attn_early((int)a);
+    else if (what == "decode_attn_unroll") edge_decode_attn_unroll((int)a);
     else if (what == "attn8_wave_max") edge_decode_attn_i8_wave_max((int)a);
     else if (what == "sample_rowwide") edge_sample_rowwide_min((int)a);
     else if (what == "sample_vec") edge_sample_vec((int)a);
@@ -1158,6 +1161,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (what == "prefill_fa_sm") edge_prefill_fa_sm((int)a, (int)b);
     else if (what == "gemv_norm") edge_w8a8_gemv_norm_cfg((int)a);
     else if (what == "r256_packed") edge_w8a8_r256_cfg((int)a);
+    else if (what == "r256_wreg") edge_w8a8_wreg_cfg((int)a);
     else TORCH_CHECK(false, "unknown tunable ", what);
   });
 }

@@ -1395,10 +1395,24 @@ int launch_r256(const void* A, const float* sa, const void* Wp, const float* sw,
   return (int)hipGetLastError();
 }
 
+}  // namespace
+// the weights-in-VGPR form (gemm_i8_wreg.hip); g_wreg: 0 off, 4 / 6 = stages in flight
+extern "C" int edge_w8a8_wreg(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
+                              void* out, float* os, int M, int N, int K, int Mpad, int epi, int da, hipStream_t st);
+static int g_wreg = 0;
+extern "C" void edge_w8a8_wreg_cfg(int v) { g_wreg = v; }
+namespace {
+
 template <int EP>
 int launch_rows256(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                    float* os, int M, int N, int K, int Mpad, bool scaled, hipStream_t st, int S) {
   if (M <= 128 || M > 256 || K % 128 != 0 || (EP == EPI_PART) != (S > 1) || (scaled && EP != EPI_PART)) return -1;
+  if constexpr (EP == EPI_GLUQ || EP == EPI_OUT) {
+    if (g_wreg && !scaled && S == 1) {
+      const int r = edge_w8a8_wreg(A, sa, Wp, sw, bias, out, os, M, N, K, Mpad, EP, g_wreg, st);
+      if (r != -2) return r;
+    }
+  }
   const int NTt = (N + 15) / 16;
   if constexpr (EP == EPI_PART) {
     if (K / 128 < 4 * S || (scaled && (Mpad < M || Mpad % 16 != 0))) return -1;

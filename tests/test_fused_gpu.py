@@ -43,6 +43,20 @@ def test_decode_attention_fused(cuda, Hq, Hkv, D, rot, lens, quant, occ):
         C.tune("decode_attn_occ", 4, 0)
 
 
+@pytest.mark.parametrize("lens", [(1, 17, 200), (150, 151, 152, 149), (4096, 1000, 3333), (513, 60), (127, 128, 129)])
+@pytest.mark.parametrize("quant", [False, True])
+@pytest.mark.parametrize("unroll", [4, 8])
+def test_decode_attention_fused_unroll(cuda, lens, quant, unroll):
+    """The barrier-free MHA D = 128 form (the bench's attention) with 4 or 8 key groups per wave
+    per chunk (tune decode_attn_unroll; 8 skips the loads of groups past the end)."""
+    C = ops.ext()
+    C.tune("decode_attn_unroll", unroll, 0)
+    try:
+        _check_decode_attention_fused(C, 32, 32, 128, 128, lens, quant)
+    finally:
+        C.tune("decode_attn_unroll", 4, 0)
+
+
 @pytest.mark.parametrize("Hq,Hkv,D,rot", [(32, 32, 128, 128), (32, 32, 80, 32), (8, 8, 256, 64), (12, 12, 64, 0),
                                           (32, 8, 64, 64), (32, 8, 128, 128)])
 @pytest.mark.parametrize("lens", [(1,), (200,), (255, 3), (300,), (700,)])

@@ -173,3 +173,62 @@ def test_r256_model_logits_unchanged(cuda):
             gen = Generator(model, max_batch=256, max_seq=32, use_graphs=False)
             outs.append(gen.generate(prompts, sp).tokens)
     assert outs[0] == outs[1]
+
+
+def _wreg(C, da):
+    class _Ctx:
+        def __enter__(self):
+            C.tune("r256_wreg", da, 0)
+
+        def __exit__(self, *a):
+            C.tune("r256_wreg", 0, 0)
+            return False
+    return _Ctx()
+
+
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("N", [12288, 4096, 22016, 2560])
+@pytest.mark.parametrize("da", [4, 6])
+def test_wreg_out_equals_ring2(cuda, M, N, da):
+    """The weights-in-VGPR 256-row kernel (gemm_i8_wreg.hip, EPI_OUT) gives ring2's bf16 outputs
+    bit for bit (the same exact int32 sums and fp32 epilogue) and matches the fp32 reference."""
+    C = ops.ext()
+    K = 4096
+    torch.manual_seed(M + N + da)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.01
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    bias = torch.randn(N, device=cuda).to(torch.bfloat16)
+    wp = ops.pack_int8_weight(w)
+    want = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+    with _wreg(C, da):
+        got = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+        again = C.w8a8_gemm(qx, sx, wp, sw, bias, N, K)
+    torch.cuda.synchronize()
+    assert torch.equal(got, again)
+    _close(got, _ref.w8a8_linear(qx, sx, w, sw, bias, torch.float32), 1e-2, 1e-2)
+    assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("F", [11008, 14336, 1024, 1152])
+def test_wreg_gluq_equals_ring2(cuda, M, F):
+    """The weights-in-VGPR quantising gate_up (SwiGLU + int8 per (token, 64 features), the amax
+    completed across 4 waves through LDS) gives ring2's int8 rows and scales exactly."""
+    C = ops.ext()
+    K = 4096
+    torch.manual_seed(M + F)
+    qx = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=cuda)
+    sx = torch.rand(M, device=cuda) * 0.004 + 1e-4
+    w = torch.randint(-127, 128, (2 * F, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(2 * F, device=cuda) * 0.004 + 1e-4
+    bias = torch.randn(2 * F, device=cuda).to(torch.bfloat16)
+    wb, swb, bb = _ref.block_glu_rows(w), _ref.block_glu_rows(sw), _ref.block_glu_rows(bias)
+    wp = ops.pack_int8_weight(wb)
+    q0, s0 = C.w8a8_gemm_gluq(qx, sx, wp, swb, bb, 2 * F, K)
+    with _wreg(C, 4):
+        q1, s1 = C.w8a8_gemm_gluq(qx, sx, wp, swb, bb, 2 * F, K)
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s0)
+    assert torch.equal(q1, q0)

@@ -47,7 +47,8 @@ def main():
     ap.add_argument("--copies", type=int, default=0, help="cache copies rotated (0: enough for > 512 MB)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="bf16,int8,int8wave",
-                    help="bf16 | int8 (workgroup-per-head split form) | int8wave (wave-per-head form)")
+                    help="bf16 | bf16u8 (8 key groups per wave per chunk) | int8 (workgroup-per-head split form) | "
+                         "int8wave (wave-per-head form); a kind may repeat (interleaved A/B)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv = (int(x) for x in a.heads.split("x"))
@@ -64,6 +65,8 @@ def main():
         rope = ops.rope_tables(D, S, 10000.0, device=dev)
         for kind in a.only.split(","):
             ops.ext().tune("attn8_wave_max", 1024 if kind == "int8wave" else 0, 0)
+            # bf16u8: the barrier-free MHA form with 8 key groups per wave per chunk (tune decode_attn_unroll)
+            ops.ext().tune("decode_attn_unroll", 8 if kind == "bf16u8" else 4, 0)
             caches = []
             for _ in range(n):
                 k = torch.randn(B, Hkv, S, D, device=dev).bfloat16()

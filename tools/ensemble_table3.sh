@@ -19,6 +19,7 @@ run() { name=$1; shift; timeout -k 10 ${T:-500} "$@" > gpurun_out/ens/$name.log 
 run combo_base_b1      $C --config configs/ensemble.yaml $D --num_samples 16
 run combo_base_b16     $C --config configs/ensemble.yaml $D --num_samples 64 --batch_size 16
 run combo_llmint8_b1   $C --config configs/ensemble_int8.yaml $D --num_samples 12
+run combo_w8a8_b1      $C --config configs/ensemble.yaml $D --num_samples 16 --quant w8a8_smoothquant
 run combo_w8a8_b16     $C --config configs/ensemble.yaml $D --num_samples 64 --batch_size 16 --quant w8a8_smoothquant
 run north_star_vote    $C --config configs/north_star.yaml $D --num_samples 32 --batch_size 16
 # agents sharing the GPU decode side by side on their own streams (orchestrator run_agents ->
