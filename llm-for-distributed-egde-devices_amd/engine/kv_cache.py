@@ -43,7 +43,8 @@ def resolve_kv_dtype(kv_dtype: str, cfg: ModelConfig, dtype=torch.bfloat16, devi
 class KVCache:
     def __init__(self, cfg: ModelConfig, max_batch: int, max_seq: int, first_layer: int = 0,
                  last_layer: Optional[int] = None, dtype=torch.bfloat16, device=None,
-                 num_kv_heads: Optional[int] = None, kv_dtype: str = "bf16"):
+                 num_kv_heads: Optional[int] = None, kv_dtype: str = "bf16", zero: bool = True):
+        """``zero=False``: uninitialised storage (a scratch cache whose rows a prefill writes in full)."""
         assert kv_dtype in ("bf16", "int8"), kv_dtype
         kv_dtype = resolve_kv_dtype(kv_dtype, cfg, dtype, device)
         self.cfg = cfg
@@ -54,15 +55,16 @@ class KVCache:
         shape = (self.last - self.first, max_batch, hk, max_seq, cfg.head_dim)
         self.quantized = kv_dtype == "int8"
         self.kv_dtype = kv_dtype
+        new = torch.zeros if zero else torch.empty
         if self.quantized:
             assert cfg.head_dim in (64, 128, 256), "int8 KV cache needs head_dim 64 / 128 / 256"
-            self.k = torch.zeros(shape, dtype=torch.int8, device=device)
-            self.v = torch.zeros(shape, dtype=torch.int8, device=device)
-            self.ks = torch.zeros(shape[:-1], dtype=torch.float32, device=device)
-            self.vs = torch.zeros(shape[:-1], dtype=torch.float32, device=device)
+            self.k = new(shape, dtype=torch.int8, device=device)
+            self.v = new(shape, dtype=torch.int8, device=device)
+            self.ks = new(shape[:-1], dtype=torch.float32, device=device)
+            self.vs = new(shape[:-1], dtype=torch.float32, device=device)
         else:
-            self.k = torch.zeros(shape, dtype=dtype, device=device)
-            self.v = torch.zeros(shape, dtype=dtype, device=device)
+            self.k = new(shape, dtype=dtype, device=device)
+            self.v = new(shape, dtype=dtype, device=device)
 
     @staticmethod
     def bytes_per_token(cfg: ModelConfig, dtype_bytes: int = 2) -> int:

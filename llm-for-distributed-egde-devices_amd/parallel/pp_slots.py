@@ -111,10 +111,18 @@ class _SlotSession:
             ids[i, n:] = flat[off]
             off += n
         ids = ids.to(dev)
-        scratch = KVCache(st.cfg, k, T, st.kv.first, st.kv.last, st.model.dtype, dev, kv_dtype=st.kv_dtype)
+        r0 = min(rows)
+        direct = sorted(rows) == list(range(r0, r0 + k))   # contiguous slot rows: prefill in place
+        scratch = None if direct else KVCache(st.cfg, k, T, st.kv.first, st.kv.last, st.model.dtype, dev,
+                                              kv_dtype=st.kv_dtype, zero=False)   # every row written [0, T)
+        order = sorted(range(k), key=lambda i: rows[i]) if direct else list(range(k))
+        if direct and order != list(range(k)):          # rows in cache order
+            rows, lens, max_new = [rows[i] for i in order], [lens[i] for i in order], [max_new[i] for i in order]
+            ids, lens_t = ids[order], lens_t[order]
         sp0 = torch.zeros(k, dtype=torch.int32, device=dev)
         last = (lens_t - 1).to(dev)
-        ctx = AttnCtx("prefill", k, T, sp0, sp0 + T, T, scratch.rows(0, k), st.rope, last_pos=last)
+        view = st.kv.rows(r0, r0 + k) if direct else scratch.rows(0, k)
+        ctx = AttnCtx("prefill", k, T, sp0, sp0 + T, T, view, st.rope, last_pos=last)
         hidden = None
         if not st.is_first:
             hidden = torch.empty(k * T, H, dtype=st.model.dtype, device=dev)
@@ -122,12 +130,13 @@ class _SlotSession:
         out = st.model(ids if st.is_first else None, ctx, hidden=hidden, logits="last")
         if not st.is_last:
             st._exchange([(out.contiguous(), st.next)], [])
-        # the prompt's K / V rows into the slot rows of the session's cache (one copy per tensor)
-        ridx = torch.tensor(list(rows), dtype=torch.long, device=dev)
-        for name in ("k", "v") + (("ks", "vs") if scratch.quantized else ()):
-            dst, src = getattr(st.kv, name), getattr(scratch, name)
-            dst[:, ridx, :, :T] = src
-        del scratch
+        if scratch is not None:
+            # the prompt's K / V rows into the slot rows of the session's cache (one copy per tensor)
+            ridx = torch.tensor(list(rows), dtype=torch.long, device=dev)
+            for name in ("k", "v") + (("ks", "vs") if scratch.quantized else ()):
+                dst, src = getattr(st.kv, name), getattr(scratch, name)
+                dst[:, ridx, :, :T] = src
+            del scratch
         toks = torch.zeros(k, dtype=torch.long, device=eng.cdev)
         mb = [divmod(r, self.b) for r in rows]
         if st.is_last:
@@ -142,7 +151,7 @@ class _SlotSession:
                 st.tok[m][j:j + 1].copy_(nxt[i:i + 1])
                 self.out[m][j].zero_()
                 self.out[m][j, self.col - 1:self.col].copy_(nxt[i:i + 1])
-            toks.copy_(nxt.to(toks.device))
+            toks[torch.tensor(order, device=toks.device)] = nxt.to(toks.device)   # the caller's order
         for i, (m, j) in enumerate(mb):
             n = int(lens[i])
             b_left = max(0, int(max_new[i]) - 1)        # the first token came from the prefill
