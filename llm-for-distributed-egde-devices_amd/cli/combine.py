@@ -72,7 +72,7 @@ def make_agent(name: str, model_id: str, precision: str, quant: str, device, sam
         model = split_model(model, devs)
         logger.info(f"{name}: {source} split over {[str(d) for d in devs]} at layers {model.bounds} ({quant})")
     else:
-        logger.info(f"{name}: {source} on {devs[0]} ({quant})")
+        logger.info(f"{name}: {source} on {devs[0]} ({quant}, {str(model.dtype).replace('torch.', '')})")
     gen = build_generator(model, rt, max_batch=int(rt.get("batch_size") or 1))
     return Agent(name, gen, tok, sampling, cpu_prompt)
 
@@ -135,6 +135,10 @@ def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_vari
     results = Results()
     eff = EfficiencyMeter([a.device for a in agents] + ([refiner.device] if refiner else []))
     bs = max(1, int(rt.get("batch_size") or 1))
+    # per-agent tokens/sec under both of the reference's definitions, per sample (a batch's rows share
+    # its generate wall): generated-only (the combiners, combine_model_fp_updated.py:106-108) and
+    # prompt + generated (the single-model scripts, Llama_bf16_updated.py:89-90)
+    agent_tps = {a.name: {"gen": [], "all": []} for a in agents}
     logger.info("Starting evaluation loop..." + (f" ({bs} questions per batch)" if bs > 1 else ""))
     todo = [i for i in range(len(rows)) if i not in done]
     for i in done:
@@ -174,6 +178,11 @@ def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_vari
                                         "final": res.final}) + "\n")
             if cpu_variant:
                 logger.info(f"[Q{i + 1}] Total time: {res.wall_s:.2f} sec\n")
+        for name, g in outs[0].results.items():
+            if name in agent_tps and g.elapsed_s > 0:
+                for toks, pl in zip(g.tokens, g.prompt_lens):
+                    agent_tps[name]["gen"].append(len(toks) / g.elapsed_s)
+                    agent_tps[name]["all"].append((len(toks) + pl) / g.elapsed_s)
         # QA agents' generated tokens of this batch (each result holds every row of the batch)
         eff.add(time.perf_counter() - t0, len(idx), sum(len(t) for g in outs[0].results.values() for t in g.tokens))
     means = results.means()
@@ -182,6 +191,11 @@ def _ensemble_loop(cfg, rt, agents, refiner, merge_kind, rows, devices, cpu_vari
     means.update(eff.summary())
     for line in format_efficiency_report(means):
         logger.info(line)
+    for name, d in agent_tps.items():
+        if d["gen"]:
+            g, a = sum(d["gen"]) / len(d["gen"]), sum(d["all"]) / len(d["all"])
+            means[f"tps_gen_{name}"], means[f"tps_all_{name}"] = g, a
+            logger.info(f"TPS {name:<14}→ {g:.2f} generated / {a:.2f} prompt+generated tok/s")
     return means
 
 

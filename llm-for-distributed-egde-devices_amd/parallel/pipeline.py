@@ -14,12 +14,16 @@ stage busy:
 Per tick each rank issues one grouped P2P exchange per lane through ``dist.batch_isend_irecv``
 (send the lane's previous outputs, receive its next inputs — grouped, so no send/recv ordering
 deadlock; on RCCL one ncclGroupStart/End), issued and completed on that lane's HIP stream, then
-runs its layers for the micro-batches of the tick.  Every lane has its OWN process group over the
-stage ranks (``lane_groups``; one RCCL communicator, hence one internal stream, per lane): a
-single communicator would queue lane l's hop behind lane l - 1's hop and compute.  A
-lane's hop therefore waits only for that lane's compute and runs beside the other lanes' compute,
-and no lane waits for the others at a tick boundary.  (Measured so far only under gloo — the
-2 / 4 / 8-rank rehearsals — and at RCCL world 1; the multi-GPU RCCL overlap is unmeasured.)  The same P2POp path runs under gloo on the CPU, which is how the
+runs its layers for the micro-batches of the tick.  By default all lanes share the stage group's
+communicator: each lane posts and completes its exchange on its own stream, and RCCL runs the
+lanes' hops one after another on its internal stream.  ``EDGELLM_LANE_GROUPS=1`` gives every lane
+its OWN process group (``lane_groups``; one RCCL communicator, hence one more internal stream, per
+lane), so a lane's hop waits only for that lane's compute.  It is opt-in: a process
+has GPU_MAX_HW_QUEUES = 4 hardware queues, and default + 2 lane streams + 3 communicator streams
+would share them, putting a spinning RCCL receive kernel in front of another stream's compute on
+one queue — a cross-rank dependency cycle; with one communicator the streams fit the queues.
+(Measured under gloo — the 2 / 4 / 8-rank rehearsals — and at RCCL world 1; the multi-GPU RCCL
+overlap is unmeasured.)  The same P2POp path runs under gloo on the CPU, which is how the
 multi-rank schedule is tested without GPUs.  The decode compute of each micro-batch is captured in
 a HIP graph per KV-length bucket (all buckets of a run are captured at the first capture, before
 any timed region); the P2P ops stay outside the graphs on RCCL's stream, ordered by stream waits,
@@ -128,12 +132,12 @@ class PipelineStage:
         self.p2p_bytes = 0
         self._copy_stream = None                      # host-staged sends (gloo with device tensors)
         self._plen, self._eos = None, None            # per-run: ragged prompt lengths, EOS id (last rank)
-        # one process group (communicator) per lane for the per-lane exchanges (lanes > 1 on GPU
-        # streams): only the stage ranks join its creation (use_local_synchronization)
+        # EDGELLM_LANE_GROUPS=1: one process group (communicator) per lane for the per-lane exchanges
+        # (lanes > 1 on GPU streams; only the stage ranks join its creation: use_local_synchronization)
         self.lane_groups = [group] * lanes
         import os
         if (self.streams is not None and dist.is_initialized() and world > 1
-                and os.environ.get("EDGELLM_LANE_GROUPS", "1") != "0"):
+                and os.environ.get("EDGELLM_LANE_GROUPS", "0") == "1"):
             self.lane_groups = [dist.new_group(self.granks, use_local_synchronization=True) for _ in range(lanes)]
         self.vs_req = bool(vocab_split) and world > 1
         self.shard = head_shard

@@ -72,14 +72,35 @@ class _SlotSession:
             st.pos[m].zero_()
             st.lens[m].fill_(1)
             st.tok[m].zero_()
-        if st.is_last:
-            V = st.cfg.vocab_size
-            self.seen = [torch.zeros(self.b, V, dtype=torch.uint8, device=dev) for _ in range(self.M)]
+        V = st.cfg.vocab_size
+        # vocabulary-split head (parallel/vocab_head.py) when the engine has one and the session's
+        # sampling shards: every rank runs its logits slice + sampler phase 1, rank 0 merges and owns
+        # the tokens; otherwise the last stage samples with the whole head
+        self.vs = vocab_split_session(eng, sampling)
+        self.samp = st.is_first if self.vs else st.is_last          # the rank that owns the tokens
+        if self.vs or st.is_last:
+            Vs = st.shard.Vs if self.vs else V
+            self.seen = [torch.zeros(self.b, Vs, dtype=torch.uint8, device=dev) for _ in range(self.M)]
             self.rng = [torch.tensor([(seed + 7919 * m) & 0x7FFFFFFF, 1], dtype=torch.int32, device=dev)
                         for m in range(self.M)]
+        if st.is_last:
             self.rng_adm = torch.tensor([(seed + 104729) & 0x7FFFFFFF, 0], dtype=torch.int32, device=dev)
+        if self.samp:
             self.step_ = [torch.ones(1, dtype=torch.long, device=dev) for _ in range(self.M)]
             self.out = [torch.zeros(self.b, width, dtype=torch.long, device=dev) for _ in range(self.M)]
+        if self.vs:
+            P = st.world
+            mode = ops.shard_mode(sampling.temperature, sampling.top_k, sampling.top_p, V, sampling.do_sample)
+            self.hfin = [torch.zeros(self.b, st.cfg.hidden_size, dtype=st.model.dtype, device=dev)
+                         for _ in range(self.M)]
+            self.cand: Dict[int, tuple] = {}
+            if st.is_first:
+                vb = st.vs_bounds
+                self.cand_in = [[tuple(torch.empty(shp, dtype=dt, device=dev) for shp, dt in
+                                       ops.shard_candidate_shapes(self.b, vb[r + 1] - vb[r], V, mode, dev))
+                                 for r in range(1, P)] for _ in range(self.M)]
+            else:
+                self.tokin = [torch.zeros(self.b, dtype=torch.long, device=dev) for _ in range(self.M)]
         # decode graphs per (micro-batch, KV bucket): GPU, a sampler that stays on the device
         self.use_graphs = bool(st.use_graphs and st.cuda and getattr(st.kv, "graph_safe", True)
                                and not needs_host_sampler(sampling, st.cfg.vocab_size)
@@ -139,15 +160,35 @@ class _SlotSession:
             del scratch
         toks = torch.zeros(k, dtype=torch.long, device=eng.cdev)
         mb = [divmod(r, self.b) for r in rows]
-        if st.is_last:
+        nxt = None
+        if st.is_last:                                 # the first tokens: the last stage's whole head
             seen = torch.zeros(k, st.cfg.vocab_size, dtype=torch.uint8, device=dev)
             seen.scatter_(1, ids, 1)
             sp = self.sp
             nxt = ops.sample(out, seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, self.rng_adm,
                              sp.do_sample)
             self.rng_adm[1:].add_(1)
+            if not self.vs:
+                for i, (m, j) in enumerate(mb):
+                    self.seen[m][j].copy_(seen[i])
+        if self.vs:
+            # the first tokens -> every rank: each marks the prompt and the token in its shard of the
+            # penalty flags, rank 0 (which merges from now on) keeps them as the rows' tokens
+            P = st.world
+            if st.is_last:
+                st._exchange([(nxt, r) for r in range(P - 1)], [])
+            else:
+                nxt = torch.empty(k, dtype=torch.long, device=dev)
+                st._exchange([], [(nxt, P - 1)])
             for i, (m, j) in enumerate(mb):
-                self.seen[m][j].copy_(seen[i])
+                row = torch.zeros(1, self.seen[m].shape[1], dtype=torch.uint8, device=dev)
+                for t in (ids[i], nxt[i:i + 1]):
+                    jj = t.view(-1) - st.shard.v0
+                    jj = jj[(jj >= 0) & (jj < row.shape[1])]
+                    row[0, jj] = 1
+                self.seen[m][j:j + 1].copy_(row)
+        if self.samp:
+            for i, (m, j) in enumerate(mb):
                 st.tok[m][j:j + 1].copy_(nxt[i:i + 1])
                 self.out[m][j].zero_()
                 self.out[m][j, self.col - 1:self.col].copy_(nxt[i:i + 1])
@@ -182,8 +223,13 @@ class _SlotSession:
     def _decode_body(self, m: int, max_len: int):
         st, b = self.st, self.b
         ctx = AttnCtx("decode", b, 1, st.pos[m], st.lens[m], max_len, st._rows(m), st.rope)
-        out = st.model(st.tok[m].view(b, 1) if st.is_first else None, ctx, hidden=None if st.is_first else st.hin[m])
-        if st.is_last:
+        out = st.model(st.tok[m].view(b, 1) if st.is_first else None, ctx, hidden=None if st.is_first else st.hin[m],
+                       logits="hidden" if self.vs else "last")
+        if st.is_last and self.vs:                    # the final-normed rows go to every rank's head shard
+            self.hfin[m].copy_(out)
+            st.pos[m].add_(self.active[m])
+            st.lens[m].add_(self.active[m])
+        elif st.is_last:
             sp = self.sp
             nxt = ops.sample(out, self.seen[m], sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty,
                              self.rng[m], sp.do_sample)
@@ -220,12 +266,98 @@ class _SlotSession:
             self._graphs[(m, bucket)] = g
         g.replay()
 
+    # ---------------------------------------------------------- vocabulary-split head (self.vs)
+    def _vs_shard(self, m: int):
+        """This rank's logits slice + sampler phase 1 for the rows of micro-batch m (in hfin[m])."""
+        st = self.st
+        self.cand[m] = st.shard.candidates(self.hfin[m], self.seen[m], self.sp, self.rng[m])
+        if not st.is_first:
+            self.rng[m][1:].add_(1)                   # rank 0 advances after its merge (same step)
+
+    def _vs_merge(self, m: int):
+        """Rank 0: phase 2 over every shard's candidates -> the token of each row of m, and the
+        decode bookkeeping of the sampling rank (out column, step, noise counter, penalty flags)."""
+        st, sp = self.st, self.sp
+        nxt = ops.sample_merge([self.cand[m]] + self.cand_in[m], st.cfg.vocab_size, sp.temperature, sp.top_k,
+                               sp.top_p, self.rng[m], sp.do_sample)
+        st.tok[m].copy_(nxt)
+        self.out[m].scatter_(1, self.step_[m].view(1, 1).expand(self.b, 1), nxt.view(self.b, 1))
+        self.rng[m][1:].add_(1)
+        self.step_[m].add_(1)
+        ops.seen_mark(self.seen[m], nxt, st.shard.v0)
+
+    @torch.no_grad()
+    def _step_vs(self, n: int) -> torch.Tensor:
+        """``n`` decode rounds with the vocabulary-split head.  Item i = k M + m runs on rank r at
+        tick i + r; its final-normed rows leave the last stage at tick i + P, every rank runs its
+        head shard then, rank 0 merges at i + P + 1 (the token item i + M embeds, M >= P + 1) and
+        sends it on at i + P + 2, when the other ranks mark it in their penalty shards.  The loop
+        drains every stage of the command's last round before it returns."""
+        st = self.st
+        M, b, P, R = self.M, self.b, st.world, st.rank
+        assert M >= P + 1, "the vocab-split head needs >= P + 1 micro-batches"
+        base = [max(self.host_len[m * b:(m + 1) * b]) for m in range(M)]
+        n_items = n * M
+        valid = lambda i: 0 <= i < n_items              # noqa: E731
+        for t in range(n_items + P + 2):
+            sends, recvs = [], []
+            prv, cur = t - 1 - R, t - R
+            if valid(prv) and not st.is_last:
+                sends.append((st.hout[prv % M], st.next))
+            if valid(cur) and not st.is_first:
+                recvs.append((st.hin[cur % M], st.prev))
+            # (after the hand-offs: P2P ops of a rank pair match in posting order)
+            hg, cg, mg = t - P, t - P - 1, t - P - 2
+            if valid(hg):
+                if st.is_last:
+                    sends.extend((self.hfin[hg % M], r) for r in range(P - 1))
+                else:
+                    recvs.append((self.hfin[hg % M], P - 1))
+            if valid(cg):
+                if st.is_first:
+                    recvs.extend((x, r + 1) for r, c in enumerate(self.cand_in[cg % M]) for x in c)
+                else:
+                    sends.extend((x, 0) for x in self.cand[cg % M])
+            if valid(mg):
+                if st.is_first:
+                    sends.extend((st.tok[mg % M], r) for r in range(1, P))
+                else:
+                    recvs.append((self.tokin[mg % M], 0))
+            st._exchange(sends, recvs)
+            if valid(mg) and not st.is_first:
+                ops.seen_mark(self.seen[mg % M], self.tokin[mg % M], st.shard.v0)
+            if valid(cg) and st.is_first:
+                self._vs_merge(cg % M)
+            if valid(hg):
+                self._vs_shard(hg % M)
+            if valid(cur):
+                k, m = divmod(cur, M)
+                self._decode(m, min(st.max_seq, base[m] + k))
+        self._advance_host(n)
+        c0 = self.col
+        self.col += n
+        if st.is_first:
+            return torch.cat([o[:, c0:c0 + n] for o in self.out]).to(self.eng.cdev)
+        return torch.zeros(M * b, n, dtype=torch.long, device=self.eng.cdev)
+
+    def _advance_host(self, n: int):
+        for r in range(self.M * self.b):
+            if self.host_active[r]:
+                used = min(n, self.host_budget[r])
+                self.host_len[r] += used
+                self.host_budget[r] -= used
+                if self.host_budget[r] == 0:
+                    self.host_active[r] = 0
+
     @torch.no_grad()
     def step(self, n: int, released: Sequence[int]) -> torch.Tensor:
-        """``n`` decode rounds of every row; returns the new tokens [M b, n] (last stage)."""
+        """``n`` decode rounds of every row; returns the new tokens [M b, n] (on the sampling rank:
+        the last stage, or rank 0 under the vocabulary-split head)."""
         st, eng = self.st, self.eng
         M, b, P = self.M, self.b, st.world
         self._release(released)
+        if self.vs:
+            return self._step_vs(n)
         # the tokens the last stage sampled since the previous round (admissions, the previous
         # command's final round) -> stage 0, which embeds them
         if P > 1 and (st.is_first or st.is_last):
@@ -257,18 +389,20 @@ class _SlotSession:
             if 0 <= cur < n_items:
                 k, m = divmod(cur, M)
                 self._decode(m, min(st.max_seq, base[m] + k))
-        for r in range(M * b):
-            if self.host_active[r]:
-                used = min(n, self.host_budget[r])
-                self.host_len[r] += used
-                self.host_budget[r] -= used
-                if self.host_budget[r] == 0:
-                    self.host_active[r] = 0
+        self._advance_host(n)
         c0 = self.col
         self.col += n
         if st.is_last:
             return torch.cat([o[:, c0:c0 + n] for o in self.out]).to(eng.cdev)
         return torch.zeros(M * b, n, dtype=torch.long, device=eng.cdev)
+
+
+def vocab_split_session(eng, sampling: SamplingParams) -> bool:
+    """Whether a slot session of ``eng`` samples with the vocabulary-split head (every rank derives
+    it alike from the engine and the session's sampling configuration)."""
+    return bool(getattr(eng, "vs_req", False) and eng.world > 1 and
+                ops.shard_mode(sampling.temperature, sampling.top_k, sampling.top_p, eng.cfg.vocab_size,
+                               sampling.do_sample) >= 0)
 
 
 def handle_slot_command(eng, hdr0: torch.Tensor) -> None:
@@ -278,6 +412,7 @@ def handle_slot_command(eng, hdr0: torch.Tensor) -> None:
         fl = eng._bcast(torch.zeros(4, dtype=torch.float64, device=eng.cdev))
         sp = _sampling_of(hdr0, fl)
         eng._slot_sess = _SlotSession(eng, sp, int(hdr0[2]), int(hdr0[3])) if eng.member else None
+        eng._slot_res = 0 if vocab_split_session(eng, sp) else eng.world - 1   # stage holding the tokens
     elif cmd == CMD_SLOT_ADMIT:
         k, total = int(hdr0[2]), int(hdr0[3])
         meta = eng._bcast(torch.zeros(k, 3, dtype=torch.long, device=eng.cdev))
@@ -287,14 +422,14 @@ def handle_slot_command(eng, hdr0: torch.Tensor) -> None:
             toks = eng._slot_sess.admit_batch([x[0] for x in mt], [x[1] for x in mt], [x[2] for x in mt], ids)
         else:
             toks = torch.zeros(k, dtype=torch.long, device=eng.cdev)
-        eng._deliver([toks])
+        eng._deliver([toks], eng._slot_res)
     elif cmd == CMD_SLOT_STEP:
         nrel = int(hdr0[3])
         rel = eng._bcast(torch.zeros(max(1, nrel), dtype=torch.int32, device=eng.cdev))
         n = int(hdr0[2])
         toks = eng._slot_sess.step(n, rel.tolist()[:nrel]) if eng.member else \
             torch.zeros(eng.M * eng.b, n, dtype=torch.long, device=eng.cdev)
-        eng._deliver([toks])
+        eng._deliver([toks], eng._slot_res)
     else:
         raise RuntimeError(f"unknown slot command {cmd}")
 
@@ -341,6 +476,7 @@ class PipelineSlotDecoder:
         eng._bcast(fl)
         self.sess = _SlotSession(eng, sampling, int(seed), int(width))
         eng._slot_sess = self.sess
+        eng._slot_res = 0 if self.sess.vs else eng.world - 1
 
     @property
     def col(self) -> int:
@@ -385,7 +521,7 @@ class PipelineSlotDecoder:
         self._flush_released()
         toks = self.sess.admit_batch([self.rows[s] for s in slots], [len(r[0]) for r in reqs],
                                      [int(r[1]) for r in reqs], x)
-        eng._deliver([toks])
+        eng._deliver([toks], eng._slot_res)
         first = toks.tolist()
         t1 = time.perf_counter()
         for s, r, tk in zip(slots, reqs, first):
@@ -418,7 +554,7 @@ class PipelineSlotDecoder:
         eng._bcast(hdr)
         r = eng._bcast(torch.tensor(rel or [0], dtype=torch.int32, device=eng.cdev))
         toks = self.sess.step(n, r.tolist()[:len(rel)])
-        eng._deliver([toks])
+        eng._deliver([toks], eng._slot_res)
         new = toks.tolist()
         for s, x in enumerate(self.slots):
             if x is not None:

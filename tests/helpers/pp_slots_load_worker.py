@@ -4,7 +4,7 @@ rank 0's ServingEngine serves 16 staggered greedy requests over a 4-stage gloo p
 short and submitted while long ones decode; writes every answer, the completion order and the
 engine metrics to argv[1].
 
-    pp_slots_load_worker.py OUT MODEL"""
+    pp_slots_load_worker.py OUT MODEL [VOCAB_SPLIT on|off]"""
 import argparse
 import json
 import sys
@@ -16,9 +16,10 @@ from edgellm.engine import SamplingParams
 
 def main():
     out_path, model = sys.argv[1], sys.argv[2]
+    vs = sys.argv[3] if len(sys.argv) > 3 else "off"
     args = argparse.Namespace(model=model, precision="fp32", quant="none", device="cpu", base_model_path=None,
                               max_batch=16, max_seq=128, kv_dtype="bf16", static_batches=False,
-                              pp_vocab_split="off", partition="units")   # tiny:llama: 2 layers = 4 half-layer units
+                              pp_vocab_split=vs, partition="units")   # tiny:llama: 2 layers = 4 half-layer units
     launch = _launch(args)
     engine = build_pipeline_engine(args, launch)          # ranks > 0 serve until the driver stops them
     greedy = dict(temperature=0.7, top_k=50, top_p=0.9, repetition_penalty=1.1, do_sample=False)
@@ -40,9 +41,10 @@ def main():
             time.sleep(0.01)                              # staggered arrivals
     res = {k: f.result(timeout=600)["tokens"] for k, f in futs.items()}
     metrics = engine.metrics()
+    vs_session = bool(getattr(engine.gen._slot_sess, "vs", False))
     engine.close()                                        # also releases ranks 1-3 (shutdown)
     json.dump({"requests": [[k, ids, mx] for k, ids, mx in reqs], "tokens": res, "order": order,
-               "metrics": metrics}, open(out_path, "w"))
+               "metrics": metrics, "vs_session": vs_session}, open(out_path, "w"))
 
 
 if __name__ == "__main__":

@@ -7,6 +7,7 @@ import os
 import subprocess
 import sys
 
+import pytest
 import torch
 
 from test_pp_cli_cpu import ROOT, _free_port
@@ -107,11 +108,13 @@ def test_serve_cli_torchrun_shutdown_releases_every_rank(tmp_path):
     assert rc == 0, open(tmp_path / "serve.log").read()[-3000:]
 
 
-def test_continuous_batching_4_ranks_staggered(tmp_path):
+@pytest.mark.parametrize("vs", ["off", "on"])
+def test_continuous_batching_4_ranks_staggered(tmp_path, vs):
     """16 staggered greedy requests over a 4-rank pipeline (parallel.pp_slots): queued requests
     are admitted together (one ragged prefill per command), every row stops on the device at its
     own token budget, a short request submitted while long ones decode finishes before all of
-    them, and every answer equals the single-process Generator's."""
+    them, and every answer equals the single-process Generator's.  ``vs`` on: the slots sample
+    with the vocabulary-split head (every rank's logits slice + phase 1, rank 0 merges)."""
     from edgellm.engine import Generator, SamplingParams
     from edgellm.models.registry import load_model
     out = tmp_path / "load.json"
@@ -119,7 +122,7 @@ def test_continuous_batching_4_ranks_staggered(tmp_path):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "helpers", "pp_slots_load_worker.py"), str(out), "tiny:llama"]
+           os.path.join(ROOT, "tests", "helpers", "pp_slots_load_worker.py"), str(out), "tiny:llama", vs]
     r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                        timeout=900)
     assert r.returncode == 0, r.stdout[-4000:]
@@ -135,3 +138,4 @@ def test_continuous_batching_4_ranks_staggered(tmp_path):
         assert got["tokens"][key] == gen.generate([ids], sp).tokens[0], key
     m = got["metrics"]
     assert m["requests"] == 16 and m["max_concurrent"] >= 8
+    assert got["vs_session"] == (vs == "on")

@@ -53,6 +53,12 @@ def main():
             d["lds_conflict"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
         if m.get("GRBM_GUI_ACTIVE"):
             d["gui_cycles_per_xcd"] = m["GRBM_GUI_ACTIVE"] / 8
+        if "TA_BUSY_avr" in m and m.get("GRBM_GUI_ACTIVE"):
+            # the average TA (one per CU) busy over the dispatch's GUI-active cycles
+            d["ta_busy_frac"] = m["TA_BUSY_avr"] / (m["GRBM_GUI_ACTIVE"] / 8)
+        if "FETCH_SIZE" in m:
+            # FETCH_SIZE (KB) counts half the bytes of wide streaming reads on gfx950: x2
+            d["fetch_MB_x2"] = 2 * m["FETCH_SIZE"] / 1024
         if d:
             print("\n" + ", ".join(f"{k} = {v:.3g}" for k, v in d.items()))
         print()
