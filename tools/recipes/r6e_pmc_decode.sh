@@ -14,3 +14,5 @@ for P in "$P1" "$P2"; do
   timeout -s KILL 400 rocprofv3 --pmc $P -d $D/p$i -o run --output-format csv -- python3 $B > $D/p$i.log 2>&1 || exit $?
 done
 python3 tools/pmc_summary.py "shipped decode kernels, bench.py 1 x 256 (r6)" --min-calls 100 $(find $D/p1 $D/p2 -name '*counter_collection.csv') > $D/pmc_summary.md
+# keep the summary, drop the raw per-dispatch CSVs (gpurun merges back at most 64 MiB)
+rm -rf $D/p1 $D/p2
