@@ -124,6 +124,11 @@ class Generator:
         self._pool = None
         self._warm = False                # a decode step of the current state ran eagerly
         self._state: Optional[_DecodeState] = None
+        # batch-1 decode through the persistent one-launch engine (engine/b1_engine.py): needs every CU
+        # of the GPU, so generators that decode concurrently on one device (co_generate, LaneGenerator)
+        # turn it off
+        from . import b1_engine
+        self.b1 = self.device.type == "cuda" and b1_engine.enabled()
 
     # ------------------------------------------------------------------ forward pieces
     @torch.no_grad()
@@ -153,7 +158,7 @@ class Generator:
 
     def _decode_step(self, st: _DecodeState, B: int, max_len: int, sp: SamplingParams):
         ctx = AttnCtx("decode", B, 1, st.pos, st.seq_lens, max_len, self.kv.rows(0, B), self.rope,
-                      attn_hook=self.attn_hook)
+                      attn_hook=self.attn_hook, b1=self.b1 and B == 1)
         logits = self.model(st.tok.view(B, 1), ctx)
         ops.sample_advance(logits, st.seen, sp.temperature, sp.top_k, sp.top_p, sp.repetition_penalty, st.rng,
                            st.tok, st.out, st.step, st.pos, st.seq_lens, st.ctr, sp.do_sample)
@@ -301,6 +306,8 @@ class Generator:
         if r["cuda"]:
             torch.cuda.synchronize()
         t_end = time.perf_counter()
+        for eng in getattr(self.model, "_b1_engines", {}).values():
+            eng.check()
         toks = []
         for row in st.out[:, :r["produced"]].tolist():
             if stop_at_eos and eos_token_id is not None and eos_token_id in row:
@@ -335,6 +342,8 @@ class LaneGenerator:
         assert lanes >= 1
         self.lanes = [Generator(model, max_batch=max_batch, max_seq=max_seq, use_graphs=use_graphs, **kw)
                       for _ in range(lanes)]
+        for g in self.lanes:
+            g.b1 = False                   # concurrent lanes: the one-launch engine needs every CU
         self.cuda = model.device.type == "cuda"
         self.streams = [torch.cuda.Stream(model.device) for _ in range(lanes)] if self.cuda else [None] * lanes
 
@@ -393,6 +402,9 @@ def co_generate(jobs: Sequence[tuple], eos_check_every: int = 8) -> List[Generat
     if not jobs:
         return []
     gens = [j[0] for j in jobs]
+    if len(gens) > 1:
+        for g in gens:
+            g.b1 = False                   # concurrent decode: the one-launch engine needs every CU
     cuda = gens[0].device.type == "cuda"
     streams = [torch.cuda.Stream(g.device) for g in gens] if cuda else [None] * len(gens)
     on = (lambda i: torch.cuda.stream(streams[i])) if cuda else (lambda i: _null_ctx())

@@ -61,6 +61,8 @@ class AttnCtx:
     # are right-padded to T, so a real token never attends to a pad (causal) and the pads' cache
     # entries lie past the row's length, where decode overwrites them before any read
     last_pos: Optional[torch.Tensor] = None
+    # batch-1 decode through the persistent one-launch engine (engine/b1_engine.py) when eligible
+    b1: bool = False
 
     def last_rows(self, device) -> torch.Tensor:
         """Flat row indices [B] of each sequence's last real token in a [B*T, H] activation."""
@@ -399,10 +401,30 @@ class DecoderLM(nn.Module):
             self._embed_wp_ver = ver
         return ops.linear_bf16(h, self.embed, None, packed=wp)
 
+    def _b1_engine(self, ctx: AttnCtx):
+        """The batch-1 persistent decode engine for this step, or None (not eligible / not batch 1)."""
+        if ctx.mode != "decode" or ctx.B != 1 or ctx.T != 1 or ctx.attn_hook is not None or not self.has_embed:
+            return None
+        kv = ctx.kv
+        if hasattr(kv, "cache"):                         # KVView: row 0 of a cache
+            if kv.r0 != 0:
+                return None
+            kv = kv.cache
+        if not hasattr(kv, "k") or not ops.gpu_path(self.embed):
+            return None
+        from ..engine import b1_engine
+        return b1_engine.engine_for(self, kv)
+
     def forward(self, ids: Optional[torch.Tensor], ctx: AttnCtx, hidden: Optional[torch.Tensor] = None,
                 logits: str = "last"):
         """First stage: ids [B, T]; later stages: hidden [B*T, H] from the previous stage.
         Returns logits on the last stage, otherwise the hidden handed to the next stage."""
+        if ctx.b1 and ids is not None:
+            eng = self._b1_engine(ctx)
+            if eng is not None:
+                # every layer in one launch (embedding -> engine -> final norm + LM head)
+                h = eng.run(ops.embedding(ids.reshape(-1), self.embed), ctx.start_pos)
+                return self.head(h, None, ctx, logits)
         x = self.embed_tokens(ids, ctx.start_pos, decode=ctx.mode == "decode") if self.has_embed else hidden
         x, residual = self.forward_layers(x, ctx, None)
         if self.has_head:

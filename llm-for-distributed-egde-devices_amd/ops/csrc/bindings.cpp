@@ -8,6 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <optional>
+#include <vector>
+
+#include "b1_engine.h"
 #include <tuple>
 
 extern "C" {
@@ -115,6 +118,8 @@ int edge_w8a8_r256_ok(int M, int N, int K, int epi);
 int edge_w8a8_r256(const void* Ap, const float* sa, const void* Wp, const float* sw, const void* bias, void* out,
                    int M, int N, int K, int epi, hipStream_t st);
 void edge_w8a8_r256_cfg(int on);
+int edge_b1_lds_bytes(int D, int xqb, int sxn, int scb);
+int edge_b1_decode(const B1Params* p, int G, int D, int HD, int lds, hipStream_t st);
 }
 
 namespace {
@@ -1088,11 +1093,55 @@ int64_t copy_head_block(at::Tensor& dst, const at::Tensor& src, int64_t mode) {
 
 // stream a device tensor's bytes through the cache hierarchy (MALL warm-up ahead of a reader)
 
+
+// Batch-1 persistent decode (b1_engine.hip; the layout and buffers come from engine/b1_engine.py).
+// t: ws, sw_q, sw_o, sw_gu, sw_d, gam1, gam2, rope, x0, xout, kc, vc, pos, gx, gq, ga, gr, gh, ctl [, stamps]
+// iv: fmax, kv_l, kv_h, L, H, Hq, Hkv, F, NQ, gpc_x, gpc_q, gpc_h, xqb, sxn, scb, G, D, HD, lds
+void b1_decode(const std::vector<torch::Tensor>& t, const std::vector<int64_t>& iv, double eps, double scale) {
+  TORCH_CHECK((t.size() == 19 || t.size() == 20) && iv.size() == 19, "b1_decode: argument count");
+  for (const auto& x : t) TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "b1_decode: contiguous GPU tensors");
+  const at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(t[0].device());
+  B1Params p{};
+  p.ws = (const int8_t*)t[0].data_ptr();
+  p.fmax = iv[0];
+  p.sw_q = t[1].data_ptr<float>();
+  p.sw_o = t[2].data_ptr<float>();
+  p.sw_gu = t[3].data_ptr<float>();
+  p.sw_d = t[4].data_ptr<float>();
+  p.gam1 = (const b1_bf16_t*)t[5].data_ptr();
+  p.gam2 = (const b1_bf16_t*)t[6].data_ptr();
+  p.rope = t[7].data_ptr<float>();
+  p.x0 = (const b1_bf16_t*)t[8].data_ptr();
+  p.xout = (b1_bf16_t*)t[9].data_ptr();
+  p.kc = (b1_bf16_t*)t[10].data_ptr();
+  p.vc = (b1_bf16_t*)t[11].data_ptr();
+  p.kv_l = iv[1];
+  p.kv_h = iv[2];
+  p.pos = t[12].data_ptr<int>();
+  p.gx = (uint64_t*)t[13].data_ptr();
+  p.gq = (uint64_t*)t[14].data_ptr();
+  p.ga = (uint64_t*)t[15].data_ptr();
+  p.gr = (uint64_t*)t[16].data_ptr();
+  p.gh = (uint64_t*)t[17].data_ptr();
+  p.ctl = t[18].data_ptr<int>();
+  p.stamps = t.size() == 20 ? (long long*)t[19].data_ptr() : nullptr;
+  p.L = (int)iv[3]; p.H = (int)iv[4]; p.Hq = (int)iv[5]; p.Hkv = (int)iv[6]; p.F = (int)iv[7]; p.NQ = (int)iv[8];
+  p.eps = (float)eps;
+  p.scale = (float)scale;
+  p.gpc_x = (int)iv[9]; p.gpc_q = (int)iv[10]; p.gpc_h = (int)iv[11];
+  p.xqb = (int)iv[12]; p.sxn = (int)iv[13]; p.scb = (int)iv[14];
+  check(edge_b1_decode(&p, (int)iv[15], (int)iv[16], (int)iv[17], (int)iv[18], stream()), "b1_decode");
+}
+
+int b1_lds_bytes(int D, int xqb, int sxn, int scb) { return edge_b1_lds_bytes(D, xqb, sxn, scb); }
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("copy_head_block", &copy_head_block, py::arg("dst"), py::arg("src"), py::arg("mode") = 0);
   m.doc() = "edgellm CDNA4 (gfx950) HIP kernels";
+  m.def("b1_decode", &b1_decode);
+  m.def("b1_lds_bytes", &b1_lds_bytes);
   m.def("norm", &norm);
   m.def("act", &act);
   m.def("quant", &quant);
