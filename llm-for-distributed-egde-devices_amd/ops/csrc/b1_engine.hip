@@ -44,7 +44,7 @@ constexpr int B1_NS = 256;                 // streaming threads (waves 0-3)
 constexpr int B1_NT = 512;                 // + the seam waves (4-7)
 constexpr int B1_MAXCU = 8;                // 16-column units per CU and projection
 constexpr int B1_MAXG = 512;               // CUs (workgroups) a launch may have
-constexpr int B1_GB = 16;                  // granules per seam-wave lane per sweep batch
+constexpr int B1_GB = 8;                   // granules per seam-wave thread per sweep batch
 constexpr unsigned B1_SPIN_LIMIT = 1u << 22;
 
 // B1Params: b1_engine.h (shared with the host bindings)
@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(B1_NT, 1) b1_decode_kernel(B1Params p) {
       // (4 dims each), KPW keys per wave, PB steps.  The cached rows do not depend on this step: the
       // streaming waves load their first batches while the seam wave gathers q / k / v.
       constexpr int DPL = HD / 16, SB = 8, KB = 16 * SB;
-      constexpr int LPK = HD / 4, KPW = 64 / LPK, PB = 16, VB = 4 * KPW * PB;
+      constexpr int LPK = HD / 4, KPW = 64 / LPK, PB = HD == 128 ? 8 : 16, VB = 4 * KPW * PB;
       using KT = typename std::conditional<DPL == 8, uint4, uint2>::type;
       const int lg = lane >> 4, li = lane & 15;
       const int kh = lane / LPK, dl = (lane % LPK) * 4;

@@ -13,7 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "llm-for-distributed-egde-devices_amd", "ops", "csrc")
-RING_FILES = ["gemm_i8.hip", "gemm_i8_prefill.hip", "attn_prefill.hip", "sampler.hip"]   # every file with an inline vmcnt
+RING_FILES = ["gemm_i8.hip", "gemm_i8_prefill.hip", "attn_prefill.hip", "sampler.hip", "b1_engine.hip"]   # every file with an inline vmcnt
 
 
 @pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="no hipcc")
