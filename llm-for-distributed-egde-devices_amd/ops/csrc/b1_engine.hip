@@ -173,9 +173,9 @@ __global__ void __launch_bounds__(B1_NT, 1) b1_decode_kernel(B1Params p) {
   const uint32_t sx_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) void*)sx);
   auto stream = [&](int nu, int kbw, bool grouped) {
     if (seamw) return;
-    // every older vector-memory op of this wave retires first: a store (a profiling stamp) may retire
-    // before an older DMA, so vmcnt(D - 1) below counts DMAs only from here on.  The seam before
-    // lasted longer than the prefetch's landing, so this costs nothing
+    // every older vector-memory op of this wave retires first, so vmcnt(D - 1) below counts this
+    // stream's DMAs only (a profiling stamp is a store).  The seam before lasted longer than the
+    // prefetch's landing, so this costs nothing
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int kw0 = w * kbw;
     for (int u = 0; u < nu; ++u) {
@@ -284,8 +284,9 @@ __global__ void __launch_bounds__(B1_NT, 1) b1_decode_kernel(B1Params p) {
   // 16 nuh(c') values of its units; layer 0: the dense embedding x0) and the norm weights in LDS.
   bf16_t* const xs = reinterpret_cast<bf16_t*>(scr);          // [H]
   float* const rsum = misc + 8;                                // [8] sums, [8] maxima
-  // the seam waves stage the next norm's weights during a seam (never while the streaming waves
-  // stream: LDS writes beside their in-flight LDS-DMA corrupted fragments in the measurements)
+  // the seam waves stage the next norm's weights during a seam, never while the streaming waves
+  // stream: staging beside the streams produced wrong fragments on random CUs in the measurements
+  // (cause not isolated; docs/BENCHMARKS.md, Round 6)
   auto stage_gamma = [&](const bf16_t* gam) {
     if (seamw)
       for (int v = sidx * 8; v < H; v += 8 * B1_NS) *reinterpret_cast<uint4*>(gs + v) = *reinterpret_cast<const uint4*>(gam + v);

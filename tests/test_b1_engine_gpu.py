@@ -204,3 +204,22 @@ def test_b1_engine_generator_graphs(cuda):
             assert len(gen._graphs) >= 1 and len(model._b1_engines) >= 1
     assert len(res[True]) == 24 and all(0 <= t < cfg.vocab_size for t in res[True])
     assert res[True][0] == res[False][0]
+
+
+@pytest.mark.parametrize("name", ["llama-2-7b", "llama-3.2-1b"])
+def test_b1_engine_deterministic_over_launches(cuda, name):
+    """The same step launched 40 times (same token, same position: the append rewrites the same row
+    with the same values) gives bit-identical outputs: no launch-to-launch race between the streams,
+    the seams and the granule tags (a fresh tag every launch)."""
+    from edgellm.engine import b1_engine
+    dev = torch.device("cuda", 0)
+    cfg, model, kv, g = _setup(name, 3, 150, dev)
+    eng = b1_engine.engine_for(model, kv)
+    x0 = model.embed[torch.tensor([7], device=dev)].contiguous()
+    sp = torch.full((1,), 150, dtype=torch.int32, device=dev)
+    ref = eng.run(x0, sp).clone()
+    outs = [eng.run(x0, sp).clone() for _ in range(40)]
+    torch.cuda.synchronize()
+    eng.check()
+    bad = [i for i, o in enumerate(outs) if not torch.equal(o, ref)]
+    assert not bad, bad
