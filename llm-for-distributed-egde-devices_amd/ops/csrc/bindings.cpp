@@ -83,6 +83,10 @@ int edge_llmint8_prep(const void* x, int M, int K, float thr, int cmax, void* q,
                       int* count, hipStream_t st);
 int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int* count, const void* wt,
                          const float* scb, int M, int N, int cmax, hipStream_t st);
+int edge_llmint8_prep_rows(const void* x, int M, int K, float thr, void* q, float* sa, int* cols, int* count,
+                           uint32_t* flags, uint32_t* take, hipStream_t st);
+int edge_llmint8_outlier_rows(void* out, const void* x, const int* cols, const int* count, const void* wt,
+                              const float* scb, int M, int N, int K, hipStream_t st);
 void edge_w8a8_gemv_ntw(int ntw);
 void edge_w8a8_gemv_ring(int on);
 void edge_w8a8_prefill_apack(int v);
@@ -794,6 +798,47 @@ void llmint8_outlier(at::Tensor& out, const at::Tensor& xo, const at::Tensor& co
         "llmint8_outlier");
 }
 
+// LLM.int8 preparation for any number of rows, uncapped (every outlier column to the 16-bit part):
+// (q int8 [M, K] with the outlier columns zeroed, per-token scales [M], outlier columns [K] (first
+// `count`), count [1]).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> llmint8_prep_rows(const at::Tensor& x, double thr) {
+  DEVICE_GUARD(x);
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [M, K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(K % 32 == 0 && M > 0, "llmint8_prep_rows: K % 32 == 0");
+  auto q = at::empty({M, K}, x.options().dtype(at::kChar));
+  auto sa = at::empty({M}, x.options().dtype(at::kFloat));
+  auto cols = at::empty({K}, x.options().dtype(at::kInt));
+  auto count = at::empty({1}, x.options().dtype(at::kInt));
+  auto bits = at::empty({2 * (K / 32)}, x.options().dtype(at::kInt));
+  uint32_t* flags = reinterpret_cast<uint32_t*>(bits.data_ptr<int>());
+  check(edge_llmint8_prep_rows(x.data_ptr(), (int)M, (int)K, (float)thr, q.data_ptr(), sa.data_ptr<float>(),
+                               cols.data_ptr<int>(), count.data_ptr<int>(), flags, flags + K / 32, stream()),
+        "llmint8_prep_rows");
+  return {q, sa, cols, count};
+}
+
+// out bf16 [M, N] += x[:, cols[:count]] . W^T[cols[:count]] * SCB / 127 (wt = int8 W^T [K, N]), in place.
+void llmint8_outlier_rows(at::Tensor& out, const at::Tensor& x, const at::Tensor& cols, const at::Tensor& count,
+                          const at::Tensor& wt, const at::Tensor& scb) {
+  DEVICE_GUARD(out);
+  need(out, at::kBFloat16, "out");
+  need(x, at::kBFloat16, "x");
+  need(cols, at::kInt, "cols");
+  need(count, at::kInt, "count");
+  need(wt, at::kChar, "weight_t");
+  need(scb, at::kFloat, "SCB");
+  const int64_t M = out.size(0), N = out.size(1), K = x.size(1);
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && x.dim() == 2 && x.is_contiguous() && x.size(0) == M &&
+                  wt.dim() == 2 && wt.is_contiguous() && wt.size(0) == K && wt.size(1) == N && cols.numel() == K &&
+                  scb.numel() == N,
+              "llmint8_outlier_rows: shapes");
+  check(edge_llmint8_outlier_rows(out.data_ptr(), x.data_ptr(), cols.data_ptr<int>(), count.data_ptr<int>(),
+                                  wt.data_ptr(), scb.data_ptr<float>(), (int)M, (int)N, (int)K, stream()),
+        "llmint8_outlier_rows");
+}
+
 // Per-(token, 64 columns) int8 quantisation: (q [M, K], scales [K/64, Mpad]).
 std::tuple<at::Tensor, at::Tensor> group_quant(const at::Tensor& x) {
   DEVICE_GUARD(x);
@@ -1156,6 +1201,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("addend") = py::none());
   m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
+  m.def("llmint8_prep_rows", &llmint8_prep_rows, "LLM.int8 preparation for any rows (uncapped, on the device)");
+  m.def("llmint8_outlier_rows", &llmint8_outlier_rows, "LLM.int8 outlier part for any rows, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");
   m.def("gemm_bf16_ring", &gemm_bf16_ring, "bf16 decode GEMM, 17-256 rows (ring2 kernel, bf16 MFMA)");
   m.def("bf16_ring_splits", [](int64_t N, int64_t K) { return (int64_t)edge_bf16_ring_splits((int)N, (int)K); });

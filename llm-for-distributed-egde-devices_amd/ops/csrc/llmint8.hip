@@ -14,6 +14,7 @@
 //            weight columns as rows of a transposed int8 copy (coalesced, N bytes per column).
 // Columns past CMAX (never seen with real activations; the list holds 256) stay in the int8
 // part, so nothing is dropped.  Every shape is static: the decode step is graph-capturable.
+// Inputs of more rows take the uncapped multi-workgroup form below ("any rows").
 #include "common.h"
 
 namespace {
@@ -154,6 +155,143 @@ __global__ void __launch_bounds__(256) llmint8_outlier_kernel(bf16_t* __restrict
     *o = f2bf(bf2f(*o) + acc[m] * s);
   }
 }
+
+// ---------------------------------------------------------------------------------- any rows
+// The same split for prefill-sized inputs (any M), still without a host round trip, and with no
+// cap: every column holding an |x| > threshold in any row goes to the 16-bit part, exactly the
+// bitsandbytes split.  Four launches, all of static shape:
+//   flags:   (K / 2048) x (M / 32) workgroups OR the column flags of their 32-row slab into a
+//            zeroed global bitmap (one atomic per 8 flagged columns, none for clean ones);
+//   compact: one wave turns the bitmap into the ordered column list + count (as in prep above);
+//   quant:   one workgroup per row: absmax over the kept columns, int8 with the outliers zeroed;
+//   outlier: 64 rows x 256 columns per workgroup: the rows' outlier values gathered from x into
+//            LDS 32 columns at a time, W^T rows read coalesced, fp32 sums, one rounding into out.
+constexpr int FR_ROWS = 32, OR_ROWS = 64, OR_COLS = 256, OR_J = 32;
+
+__global__ void __launch_bounds__(256) llmint8_flags_kernel(const bf16_t* __restrict__ x, int M, int K, float thr,
+                                                            uint32_t* __restrict__ flags) {
+  const int c8 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c8 >= K) return;
+  const int m0 = blockIdx.y * FR_ROWS, m1 = min(M, m0 + FR_ROWS);
+  uint32_t bits = 0;
+  for (int m = m0; m < m1; ++m) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + (size_t)m * K + c8), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bits |= (fabsf(v[j]) > thr ? 1u : 0u) << j;
+  }
+  if (bits) atomicOr(&flags[c8 / 32], bits << (c8 % 32));
+}
+
+// one wave: ordered compaction of the flag bitmap (words = K / 32) into cols [count]; take = the
+// bitmap of the accepted columns (all of them here: cmax = K)
+__global__ void __launch_bounds__(64) llmint8_compact_kernel(const uint32_t* __restrict__ flags, int words, int cmax,
+                                                             uint32_t* __restrict__ take, int* __restrict__ cols,
+                                                             int* __restrict__ count) {
+  const int lane = threadIdx.x;
+  int base = 0;
+  for (int w0 = 0; w0 < words; w0 += 64) {
+    const int w = w0 + lane;
+    const uint32_t f = w < words ? flags[w] : 0u;
+    int pc = __popc(f), incl = pc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int slot = base + incl - pc;
+    uint32_t acc = 0u, rest = f;
+    while (rest) {
+      const int b = __ffs(rest) - 1;
+      rest &= rest - 1;
+      if (slot < cmax) {
+        cols[slot] = w * 32 + b;
+        acc |= 1u << b;
+      }
+      ++slot;
+    }
+    if (w < words) take[w] = acc;
+    base += __shfl(incl, 63, 64);
+  }
+  if (lane == 0) *count = min(base, cmax);
+}
+
+// one workgroup per row: sa[m] = absmax over the kept columns / 127, q[m] int8 (outliers zeroed)
+__global__ void __launch_bounds__(256) llmint8_quant_rows_kernel(const bf16_t* __restrict__ x, int K,
+                                                                 const uint32_t* __restrict__ take,
+                                                                 int8_t* __restrict__ q, float* __restrict__ sa) {
+  __shared__ float wmax[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* xr = x + (size_t)m * K;
+  float am = 0.f;
+  for (int c8 = tid * 8; c8 < K; c8 += 256 * 8) {
+    const uint32_t tk = (take[c8 / 32] >> (c8 % 32)) & 0xffu;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c8), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!((tk >> j) & 1u)) am = fmaxf(am, fabsf(v[j]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+  if ((tid & 63) == 0) wmax[tid >> 6] = am;
+  __syncthreads();
+  const float rm = fmaxf(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])), 1e-8f);
+  if (tid == 0) sa[m] = rm / 127.f;
+  const float inv = 127.f / rm;
+  for (int c8 = tid * 8; c8 < K; c8 += 256 * 8) {
+    const uint32_t tk = (take[c8 / 32] >> (c8 % 32)) & 0xffu;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c8), v);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)((tk >> j) & 1u ? 0 : quant_i8(v[j], inv))) << (8 * j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      hi |= ((uint32_t)(uint8_t)((tk >> (4 + j)) & 1u ? 0 : quant_i8(v[4 + j], inv))) << (8 * j);
+    *reinterpret_cast<uint2*>(q + (size_t)m * K + c8) = make_uint2(lo, hi);
+  }
+}
+
+// out [M, N] bf16 += x[:, cols[:count]] . W^T[cols[:count]] * SCB / 127; grid (N / 256, M / 64)
+__global__ void __launch_bounds__(256) llmint8_outlier_rows_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ x,
+                                                                   const int* __restrict__ cols,
+                                                                   const int* __restrict__ count,
+                                                                   const int8_t* __restrict__ wt,
+                                                                   const float* __restrict__ scb, int M, int N, int K) {
+  __shared__ float xs[OR_J][OR_ROWS];         // [outlier column][row]: a thread's 64 rows are one LDS row
+  const int nt = *count;
+  if (nt == 0) return;                        // uniform: the common case costs one load
+  const int tid = threadIdx.x, n = blockIdx.x * OR_COLS + tid, m0 = blockIdx.y * OR_ROWS;
+  const int nc = min(n, N - 1);
+  float acc[OR_ROWS];
+#pragma unroll
+  for (int m = 0; m < OR_ROWS; ++m) acc[m] = 0.f;
+  for (int j0 = 0; j0 < nt; j0 += OR_J) {
+    __syncthreads();                          // previous chunk's readers are done
+    for (int i = tid; i < OR_J * OR_ROWS; i += 256) {
+      const int j = i / OR_ROWS, m = i - j * OR_ROWS;
+      xs[j][m] = (j0 + j < nt && m0 + m < M) ? bf2f(x[(size_t)(m0 + m) * K + cols[j0 + j]]) : 0.f;
+    }
+    __syncthreads();
+    const int jn = min(OR_J, nt - j0);
+    for (int j = 0; j < jn; ++j) {
+      const float w = (float)wt[(size_t)cols[j0 + j] * N + nc];
+#pragma unroll
+      for (int m = 0; m < OR_ROWS; ++m) acc[m] += xs[j][m] * w;
+    }
+  }
+  if (n >= N) return;
+  const float s = scb[n] / 127.f;
+  const int mr = min(OR_ROWS, M - m0);
+#pragma unroll
+  for (int m = 0; m < OR_ROWS; ++m) {
+    if (m < mr) {
+      bf16_t* o = out + (size_t)(m0 + m) * N + n;
+      *o = f2bf(bf2f(*o) + acc[m] * s);
+    }
+  }
+}
 }  // namespace
 
 // x bf16 [M, K] (M <= 16, K % 8 == 0, K <= 32768) -> q int8 [M, K], sa [M], cols [cmax], xo [M, cmax],
@@ -172,5 +310,31 @@ extern "C" int edge_llmint8_outlier(void* out, const float* xo, const int* cols,
   if (M <= 0 || M > 16) return -2;
   hipLaunchKernelGGL(llmint8_outlier_kernel, dim3((N + 255) / 256), dim3(256), 0, st, (bf16_t*)out, xo, cols, count,
                      (const int8_t*)wt, scb, M, N, cmax);
+  return (int)hipGetLastError();
+}
+
+// Any-rows preparation: x bf16 [M, K] (K % 32 == 0) -> q int8 [M, K] (outlier columns zeroed),
+// sa [M], cols [K] (first *count), count [1]; flags / take: scratch of K / 32 words each.
+extern "C" int edge_llmint8_prep_rows(const void* x, int M, int K, float thr, void* q, float* sa, int* cols, int* count,
+                                      uint32_t* flags, uint32_t* take, hipStream_t st) {
+  if (M <= 0 || K % 32 != 0 || K <= 0) return -2;
+  const int words = K / 32;
+  hipError_t e = hipMemsetAsync(flags, 0, (size_t)words * 4, st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(llmint8_flags_kernel, dim3((K + 2047) / 2048, (M + FR_ROWS - 1) / FR_ROWS), dim3(256), 0, st,
+                     (const bf16_t*)x, M, K, thr, flags);
+  hipLaunchKernelGGL(llmint8_compact_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)flags, words, K, take, cols,
+                     count);
+  hipLaunchKernelGGL(llmint8_quant_rows_kernel, dim3(M), dim3(256), 0, st, (const bf16_t*)x, K,
+                     (const uint32_t*)take, (int8_t*)q, sa);
+  return (int)hipGetLastError();
+}
+
+// out bf16 [M, N] += x[:, cols[:count]] . W^T[cols[:count]] * SCB / 127 (wt = int8 W^T [K, N]).
+extern "C" int edge_llmint8_outlier_rows(void* out, const void* x, const int* cols, const int* count, const void* wt,
+                                         const float* scb, int M, int N, int K, hipStream_t st) {
+  if (M <= 0 || N <= 0) return -2;
+  hipLaunchKernelGGL(llmint8_outlier_rows_kernel, dim3((N + OR_COLS - 1) / OR_COLS, (M + OR_ROWS - 1) / OR_ROWS),
+                     dim3(256), 0, st, (bf16_t*)out, (const bf16_t*)x, cols, count, (const int8_t*)wt, scb, M, N, K);
   return (int)hipGetLastError();
 }

@@ -211,14 +211,19 @@ class W8A8Linear(nn.Module):
 
 class LLMInt8Linear(nn.Module):
     takes_quantized_input = False
-    graph_safe = False   # outlier-column discovery is data dependent (host sync), like bnb ...
-    OUTLIER_CAP = 256    # ... except decode rows on GPU: ops/csrc/llmint8.hip finds them on the device
+    graph_safe = False   # outlier-column discovery is data dependent (host sync on CPU), like bnb ...
+    OUTLIER_CAP = 256    # ... on GPU ops/csrc/llmint8.hip finds the columns on the device: decode rows
+    #                      (<= 16, one fused kernel, at most 256 columns) and any rows (uncapped)
+    DECODE_ROWS = 16
+
+    def _device_ok(self) -> bool:
+        K = self.in_features
+        return ops.available() and self.w_packed.is_cuda and K % 32 == 0 and K <= 32768
 
     @property
     def graph_safe_rows(self) -> int:
-        """Batch sizes up to which forward() runs without a host sync (graph-capturable)."""
-        K = self.in_features
-        return 16 if (ops.available() and self.w_packed.is_cuda and K % 8 == 0 and K <= 32768) else 0
+        """Batch sizes up to which forward() runs without a host sync (graph-capturable): any on GPU."""
+        return 1 << 30 if self._device_ok() else 0
 
     def __init__(self, in_features: int, out_features: int, bias: bool, threshold: float = 6.0, device=None,
                  dtype=torch.bfloat16):
@@ -265,15 +270,21 @@ class LLMInt8Linear(nn.Module):
         K, N = self.in_features, self.out_features
         shp = x.shape[:-1]
         x2 = x.reshape(-1, K)
-        if x2.is_cuda and ops.gpu_path(x2) and x2.shape[0] <= self.graph_safe_rows and x2.dtype == torch.bfloat16:
-            # decode: outlier columns found on the device (llmint8.hip), no host sync
+        if x2.is_cuda and ops.gpu_path(x2) and x2.dtype == torch.bfloat16 and self._device_ok():
+            # outlier columns found on the device (llmint8.hip), no host sync at any row count
             C = ops.ext()
             if self._weight_t is None or self._weight_t.device != x2.device:
                 self._weight_t = self.weight_i8.t().contiguous()          # W^T: outlier columns as rows
                 self._w_deq = self.SCB / 127.0
-            q, sa, cols, xo, count = C.llmint8_prep(x2.contiguous(), self.threshold, self.OUTLIER_CAP)
-            out = ops.w8a8_linear(q, sa, self.w_packed, self._w_deq, self.bias, N, K)
-            C.llmint8_outlier(out, xo, cols, count, self._weight_t, self.SCB)
+            x2 = x2.contiguous()
+            if x2.shape[0] <= self.DECODE_ROWS:
+                q, sa, cols, xo, count = C.llmint8_prep(x2, self.threshold, self.OUTLIER_CAP)
+                out = ops.w8a8_linear(q, sa, self.w_packed, self._w_deq, self.bias, N, K)
+                C.llmint8_outlier(out, xo, cols, count, self._weight_t, self.SCB)
+            else:
+                q, sa, cols, count = C.llmint8_prep_rows(x2, self.threshold)
+                out = ops.w8a8_linear(q, sa, self.w_packed, self._w_deq, self.bias, N, K)
+                C.llmint8_outlier_rows(out, x2, cols, count, self._weight_t, self.SCB)
             return out.view(*shp, N)
         cols = (x2.abs() > self.threshold).any(0).nonzero().flatten()
         w_scale = self.SCB / 127.0

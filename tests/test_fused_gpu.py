@@ -451,9 +451,9 @@ def test_gemv_bf16_gelu(cuda, act, M, N, K):
 @pytest.mark.parametrize("K,N", [(2048, 3072), (2560, 10240), (8192, 2048)])
 @pytest.mark.parametrize("outliers", [0, 3, 300])
 def test_llmint8_device_outliers(cuda, M, K, N, outliers):
-    """LLM.int8 decode without a host sync (llmint8.hip) == the host-side outlier path: the same
-    columns go to the 16-bit part (300 > the 256-column cap: the overflow stays int8, so only the
-    first 256 columns may differ from bitsandbytes' split)."""
+    """LLM.int8 decode without a host sync (llmint8.hip, one fused prep kernel) == the uncapped
+    any-rows path: the same columns go to the 16-bit part (300 > the decode kernel's 256-column
+    cap: the overflow stays int8, so only the first 256 columns may differ from bitsandbytes' split)."""
     from edgellm.models.layers import Linear
     from edgellm.quant import LLMInt8Linear
     torch.manual_seed(M + K + outliers)
@@ -466,17 +466,92 @@ def test_llmint8_device_outliers(cuda, M, K, N, outliers):
         cols = torch.randperm(K, device=cuda)[:outliers]
         x[0, cols] = 8.0 + torch.rand(outliers, device=cuda) * 4
     x = x.bfloat16()
-    fast = m(x)                                         # device path (M <= 16)
+    fast = m(x)                                         # decode path (M <= 16, one fused prep kernel)
     m_slow = LLMInt8Linear.from_float(lin)
-    m_slow.OUTLIER_CAP = 10 ** 9
     x_slow = x.float()
-    # host path: the same math with data-dependent indexing (force it with a 17th row of zeros)
+    # the uncapped any-rows path (force it with a 17th row of zeros)
     slow = m_slow(torch.cat([x, torch.zeros(17 - M, K, device=cuda, dtype=x.dtype)]))[:M]
     if outliers <= LLMInt8Linear.OUTLIER_CAP:
         _close(fast, slow, 3e-2, 2e-2)
     ref = x_slow @ lin.weight.float().t() + lin.bias.float()
     rel = (fast.float() - ref).norm() / ref.norm()
     assert rel < 2e-2, rel
+
+
+def _llmint8_emulation(x, q_w, scb, bias, thr):
+    """fp32 emulation of the bitsandbytes split: columns with any |x| > thr in 16-bit against the
+    dequantised weight columns, the rest per-token int8 x per-row int8."""
+    xf = x.float()
+    cols = (xf.abs() > thr).any(0)
+    x_in = xf.masked_fill(cols[None, :], 0.0)
+    sa = x_in.abs().amax(1).clamp_min(1e-8) / 127.0
+    qx = torch.round(x_in / sa[:, None]).clamp(-127, 127)
+    w_deq = q_w.float() * (scb.float() / 127.0)[:, None]
+    out = (qx @ q_w.float().t()) * sa[:, None] * (scb.float() / 127.0)[None, :]
+    out = out + xf[:, cols] @ w_deq[:, cols].t()
+    return out + (bias.float() if bias is not None else 0.0), int(cols.sum())
+
+
+@pytest.mark.parametrize("M", [17, 200, 1000])
+@pytest.mark.parametrize("K,N", [(2048, 3072), (4096, 1000)])
+@pytest.mark.parametrize("outliers", [0, 5, 300, 1500])
+def test_llmint8_rows_device_outliers(cuda, M, K, N, outliers):
+    """LLM.int8 at prefill / large-batch rows on the device (llmint8.hip any-rows form, no host
+    sync, no column cap) == an fp32 emulation of the bitsandbytes split; every outlier column goes
+    to the 16-bit part (1500 columns here, past the decode kernel's 256)."""
+    from edgellm.models.layers import Linear
+    from edgellm.quant import LLMInt8Linear
+    torch.manual_seed(M + K + outliers)
+    lin = Linear(K, N, bias=True, device=cuda)
+    lin.weight.data.copy_(torch.randn(N, K, device=cuda) * 0.02)
+    lin.bias.data.copy_(torch.randn(N, device=cuda) * 0.1)
+    m = LLMInt8Linear.from_float(lin)
+    x = torch.randn(M, K, device=cuda)
+    if outliers:
+        cols = torch.randperm(K, device=cuda)[:outliers]
+        rows = torch.randint(0, M, (outliers,), device=cuda)      # one row per column: scattered
+        x[rows, cols] = (8.0 + torch.rand(outliers, device=cuda) * 4) * torch.sign(torch.randn(outliers, device=cuda))
+    x = x.bfloat16()
+    C = ops.ext()
+    q, sa, cl, count = C.llmint8_prep_rows(x, m.threshold)
+    want = torch.nonzero((x.float().abs() > m.threshold).any(0)).flatten()
+    assert int(count.item()) == want.numel()
+    assert torch.equal(cl[:want.numel()].long(), want)                 # ordered, complete
+    out = m(x)
+    ref, n_out = _llmint8_emulation(x, m.weight_i8, m.SCB, m.bias, m.threshold)
+    assert n_out == want.numel()
+    _close(out, ref, 3e-2, 2e-2)
+    rel = (out.float() - (x.float() @ lin.weight.float().t() + lin.bias.float())).norm() / ref.norm()
+    assert rel < 2e-2, rel
+
+
+def test_llmint8_rows_graph_capture(cuda):
+    """The any-rows LLM.int8 path has static shapes and no host sync: a captured replay equals
+    eager on new data with a different outlier set."""
+    from edgellm.models.layers import Linear
+    from edgellm.quant import LLMInt8Linear
+    torch.manual_seed(3)
+    K, N, M = 2048, 1024, 96
+    lin = Linear(K, N, bias=False, device=cuda)
+    lin.weight.data.copy_(torch.randn(N, K, device=cuda) * 0.02)
+    m = LLMInt8Linear.from_float(lin)
+    assert m.graph_safe_rows >= M
+    xin = torch.randn(M, K, device=cuda).bfloat16()
+    m(xin)                                              # W^T copy built outside the capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        m(xin)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        yout = m(xin)
+    x2 = torch.randn(M, K, device=cuda)
+    x2[7, torch.randperm(K, device=cuda)[:40]] = 10.0
+    xin.copy_(x2.bfloat16())
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(yout, m(xin))
 
 
 @pytest.mark.parametrize("M", [1, 16, 40, 64])
