@@ -294,8 +294,50 @@ struct NormIn {
 };
 constexpr int NRM_ROWS = 4;
 
+// The prologue's global loads (slices, residual, gamma) are issued by norm_load BEFORE the
+// weight stream and consumed by norm_prologue after it is issued: a wave's loads retire in issue
+// order, so prologue loads queued behind the weights would wait for the whole stream and leave
+// the norm, the MFMAs and the epilogue as a tail after the last weight byte.
 template <int NCH, int SMAX>
-__device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, int8_t* aq, float* nsa, float* nred) {
+struct NormRegs {
+  uint4 rv[NCH];
+  float4 pv[NCH][SMAX][2];                                // S <= SMAX slices (register budget)
+  uint4 gv[NCH];
+};
+
+template <int NCH, int SMAX>
+__device__ __forceinline__ void norm_load_now(const NormIn& na, int H, int M, NormRegs<NCH, SMAX>& r) {
+  const int t = threadIdx.x & 255, row = threadIdx.x >> 8;
+  if (row < M) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = min((c * 256 + t) * 8, H - 8);
+      r.rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e)
+                                  : uint4{0u, 0u, 0u, 0u};                 // no residual (a stage's first norm)
+#pragma unroll
+      for (int k = 0; k < SMAX; ++k)
+        if (k < na.S) {
+          const float4* p = reinterpret_cast<const float4*>(na.part + ((size_t)k * M + row) * H + e);
+          r.pv[c][k][0] = p[0];
+          r.pv[c][k][1] = p[1];
+        }
+      if constexpr (SMAX <= 2) r.gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
+    }
+  }
+}
+
+// hoisted for up to 2 slices; with 3-4 the held slices would spill, so those load in the prologue
+template <int NCH, int SMAX>
+__device__ __forceinline__ void norm_load(const NormIn& na, int H, int M, NormRegs<NCH, SMAX>& r) {
+  if constexpr (SMAX <= 2) {
+    norm_load_now(na, H, M, r);
+    asm volatile("" ::: "memory");                        // these loads issue before the weights
+  }
+}
+
+template <int NCH, int SMAX>
+__device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, int8_t* aq, float* nsa, float* nred,
+                                              const NormRegs<NCH, SMAX>& held) {
   const int t = threadIdx.x & 255, g = threadIdx.x >> 8, w = t >> 6;
   {                                                       // one pass: M <= NRM_ROWS = 4
     const int row = g;
@@ -303,21 +345,11 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
     float v[NCH][8];
     float ss = 0.f, amax = 0.f;
     if (act) {
-      uint4 rv[NCH];
-      float4 pv[NCH][SMAX][2];                            // S <= SMAX slices (register budget)
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int e = min((c * 256 + t) * 8, H - 8);
-        rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e)
-                                  : uint4{0u, 0u, 0u, 0u};                 // no residual (a stage's first norm)
-#pragma unroll
-        for (int k = 0; k < SMAX; ++k)
-          if (k < na.S) {
-            const float4* p = reinterpret_cast<const float4*>(na.part + ((size_t)k * M + row) * H + e);
-            pv[c][k][0] = p[0];
-            pv[c][k][1] = p[1];
-          }
-      }
+      NormRegs<NCH, SMAX> late;                           // 3-4 slices: loaded here, as late as possible
+      if constexpr (SMAX > 2) norm_load_now(na, H, M, late);
+      const NormRegs<NCH, SMAX>& regs = SMAX > 2 ? late : held;
+      const uint4* rv = regs.rv;
+      const auto& pv = regs.pv;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int e = (c * 256 + t) * 8;
@@ -366,7 +398,7 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
         const int e = (c * 256 + t) * 8;
         if (e < H) {
           float wf[8];
-          unpack8(*reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
+          unpack8(SMAX <= 2 ? held.gv[c] : *reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - 0.f) * rstd * wf[j];
         }
@@ -493,10 +525,12 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     issue_a(st, kbase);
   };
   // NRM: the first step's weight loads go out before the norm prologue; its activations after
+  NormRegs<(NRM > 0 ? NCH_N : 1), (NRM > 0 ? SMAX_N : 1)> nr;
   auto first = [&](Step& st, int kbase) {
     if constexpr (NRM > 0) {
+      norm_load(na, K, M, nr);
       issue_w(st, kbase);
-      norm_prologue<NCH_N, SMAX_N>(na, K, M, aq_l, nsa, nred);
+      norm_prologue(na, K, M, aq_l, nsa, nred, nr);
       issue_a(st, kbase);
     } else {
       issue(st, kbase);
@@ -526,9 +560,10 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4) {
       // batch-1 norm prologue: every step's weights (at most 2) in flight across it (K = 4096 with
       // 4 slices keeps one step: its prologue registers would spill)
+      norm_load(na, K, M, nr);
 #pragma unroll
       for (int i = 0; i < STEPS; ++i) issue_w(st[i], kbeg + kw + i * KW * U);
-      norm_prologue<NCH_N, SMAX_N>(na, K, M, aq_l, nsa, nred);
+      norm_prologue(na, K, M, aq_l, nsa, nred, nr);
 #pragma unroll
       for (int i = 0; i < STEPS; ++i) {
         issue_a(st[i], kbeg + kw + i * KW * U);
