@@ -599,6 +599,23 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
         st = nx;
       }
     }
+  } else if constexpr (MB == 1 && 2 * REG_EST <= (NW >= 16 ? 160 : 360)) {
+    // other k-range lengths (the down projection's 86 k-tiles per slice): one step of lookahead
+    // in two named register sets, the loop run twice per iteration (no copies of a set with
+    // loads outstanding).  Batch-1 down 11.6 us had three full memory round trips per wave here.
+    Step s0, s1;
+    int kt = kbeg + kw;
+    if (kt < kend) issue(s0, kt);
+    while (kt < kend) {
+      const int k1 = kt + KW * U;
+      if (k1 < kend) issue(s1, k1);
+      compute(s0, kt);
+      if (k1 >= kend) break;
+      const int k2 = k1 + KW * U;
+      if (k2 < kend) issue(s0, k2);
+      compute(s1, k1);
+      kt = k2;
+    }
   } else {
     for (int kt = kbeg + kw; kt < kend; kt += KW * U) {
       Step st;
