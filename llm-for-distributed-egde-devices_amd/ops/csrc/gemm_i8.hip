@@ -599,10 +599,13 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
         st = nx;
       }
     }
-  } else if constexpr (MB == 1 && 2 * REG_EST <= (NW >= 16 ? 160 : 360)) {
+  } else if constexpr (SCALED && MB <= 4 && 2 * REG_EST <= (NW >= 16 ? 160 : 360)) {
     // other k-range lengths (the down projection's 86 k-tiles per slice): one step of lookahead
     // in two named register sets, the loop run twice per iteration (no copies of a set with
     // loads outstanding).  Batch-1 down 11.6 us had three full memory round trips per wave here.
+    // Grouped-scale inputs only (the model's o / down): cache-cold down at 64 rows 39.4 -> 34.3 us,
+    // 1-32 rows unchanged; per-token inputs measured mixed (16 rows 14.5 -> 15.4 us), so they keep
+    // the plain loop (profiles/gemv_lookahead_rows_r6.jsonl).
     Step s0, s1;
     int kt = kbeg + kw;
     if (kt < kend) issue(s0, kt);
