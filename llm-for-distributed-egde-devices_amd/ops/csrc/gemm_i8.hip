@@ -321,15 +321,16 @@ __device__ __forceinline__ void norm_load_now(const NormIn& na, int H, int M, No
           r.pv[c][k][0] = p[0];
           r.pv[c][k][1] = p[1];
         }
-      if constexpr (SMAX <= 2) r.gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
+      if constexpr (NCH * SMAX <= 4) r.gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
     }
   }
 }
 
-// hoisted for up to 2 slices; with 3-4 the held slices would spill, so those load in the prologue
+// hoisted while NCH x SMAX <= 4 (K = 4096 with up to 2 slices, K = 2048 with up to 4); K = 4096
+// with 3-4 slices would spill, so those load in the prologue
 template <int NCH, int SMAX>
 __device__ __forceinline__ void norm_load(const NormIn& na, int H, int M, NormRegs<NCH, SMAX>& r) {
-  if constexpr (SMAX <= 2) {
+  if constexpr (NCH * SMAX <= 4) {
     norm_load_now(na, H, M, r);
     asm volatile("" ::: "memory");                        // these loads issue before the weights
   }
@@ -346,8 +347,8 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
     float ss = 0.f, amax = 0.f;
     if (act) {
       NormRegs<NCH, SMAX> late;                           // 3-4 slices: loaded here, as late as possible
-      if constexpr (SMAX > 2) norm_load_now(na, H, M, late);
-      const NormRegs<NCH, SMAX>& regs = SMAX > 2 ? late : held;
+      if constexpr (NCH * SMAX > 4) norm_load_now(na, H, M, late);
+      const NormRegs<NCH, SMAX>& regs = NCH * SMAX > 4 ? late : held;
       const uint4* rv = regs.rv;
       const auto& pv = regs.pv;
 #pragma unroll
@@ -398,7 +399,7 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
         const int e = (c * 256 + t) * 8;
         if (e < H) {
           float wf[8];
-          unpack8(SMAX <= 2 ? held.gv[c] : *reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
+          unpack8(NCH * SMAX <= 4 ? held.gv[c] : *reinterpret_cast<const uint4*>(na.gamma + min(e, H - 8)), wf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - 0.f) * rstd * wf[j];
         }
