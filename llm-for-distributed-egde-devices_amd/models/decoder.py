@@ -171,6 +171,8 @@ class MLP(nn.Module):
         if isinstance(x, PendingNorm):
             if getattr(self.up, "glu_blocked", False):     # batch 1: norm in the gate_up prologue
                 return self.down(self.up.glu(x), add=add)
+            if self.act == "silu_glu" and type(self.up) is Linear and not x.quant:
+                return self.down(self.up.forward_norm(x, glu=True), add=add)   # 16-bit gate_up
             x = x.materialize()
         if getattr(self.up, "glu_blocked", False):
             # W8A8 SwiGLU with 16-blocked gate_up rows: decode-sized batches take the fused
@@ -343,8 +345,7 @@ class DecoderLM(nn.Module):
         if first is None or not first.has_attn or first.norm1 is None or first.norm1.kind != "rms":
             return False
         qkv = first.attn.qkv
-        return bool(getattr(qkv, "takes_quantized_input", False) and
-                    getattr(qkv, "pending_norm_ok", lambda glu=False: False)())
+        return bool(getattr(qkv, "pending_norm_ok", lambda glu=False: False)())
 
     def embed_tokens(self, ids: torch.Tensor, start_pos: torch.Tensor, decode: bool = False):
         """ids [B, T] -> hidden [B*T, H] (``decode`` at batch 1 with a deferrable first norm: a

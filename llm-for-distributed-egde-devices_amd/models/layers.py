@@ -43,20 +43,22 @@ class PartialSum(NamedTuple):
 
 
 class PendingNorm(NamedTuple):
-    """RMSNorm + per-token int8 quant of a decode split-K PartialSum (+ residual, M <= 4 rows),
-    deferred into the prologue of the W8A8 GEMV that consumes it (ops.w8a8_gemv_norm): one launch
-    fewer per norm.  ``h`` is the residual-stream output [M, H], written by that GEMV.  ``materialize()``
-    runs the norm kernel instead (into ``h``) for a consumer that cannot take it."""
+    """RMSNorm (+ per-token int8 quant when ``quant``) of a decode split-K PartialSum (+ residual,
+    M <= 4 rows), deferred into the prologue of the GEMV that consumes it (W8A8: ops.w8a8_gemv_norm;
+    16-bit: ops.gemv_bf16_norm): one launch fewer per norm.  ``h`` is the residual-stream output
+    [M, H], written by that GEMV.  ``materialize()`` runs the norm kernel instead (into ``h``) for a
+    consumer that cannot take it."""
     parts: torch.Tensor
     residual: torch.Tensor
     weight: torch.Tensor
     eps: float
     h: torch.Tensor
+    quant: bool = True
 
-    def materialize(self) -> "QAct":
-        y, s, r = ops.rms_norm_parts(self.parts, self.residual, self.weight, self.eps, True)
+    def materialize(self):
+        y, s, r = ops.rms_norm_parts(self.parts, self.residual, self.weight, self.eps, self.quant)
         self.h.copy_(r.view_as(self.h))
-        return QAct(y, s)
+        return QAct(y, s) if self.quant else y
 
 
 class GroupQuantBF16(NamedTuple):
@@ -77,9 +79,41 @@ class Linear(nn.Module):
         self.bias = (nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device), requires_grad=False)
                      if bias else None)
 
+    def pending_norm_ok(self, glu: bool = False) -> bool:
+        """Whether this 16-bit projection takes a PendingNorm (its decode GEMV computes the RMSNorm
+        in its prologue, gemv_bf16.hip); glu: as the [gate | up] projection of a SwiGLU MLP."""
+        w = self.weight
+        return (w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and ops.available()
+                and self.in_features in (2048, 4096) and self.out_features % (32 if glu else 16) == 0
+                and not self.split_k_out and ops.gpu_path(w))
+
+    def packed_weight(self) -> torch.Tensor:
+        """The fragment-packed decode copy of the weight (``decode_weight`` without a sample input)."""
+        wp, ver = getattr(self, "_wp", None), self.weight._version
+        if wp is None or getattr(self, "_wp_ver", -1) != ver or wp.device != self.weight.device:
+            wp = self._wp = ops.pack_bf16_weight(self.weight.detach())
+            self._wp_ver = ver
+        return wp
+
+    def forward_norm(self, x: "PendingNorm", glu: bool = False):
+        """The decode GEMV over a PendingNorm (RMSNorm in the prologue); glu: silu(gate) * up."""
+        y = None
+        if self.pending_norm_ok(glu) and x.parts.dtype == torch.float32:
+            y = ops.gemv_bf16_norm(x.parts, x.residual, x.weight, x.eps, x.h, self.packed_weight(), self.bias,
+                                   self.out_features, glu=glu)
+        if y is not None:
+            return y
+        xm = x.materialize()
+        if glu:
+            return ops.linear_bf16(xm, self.weight, self.bias, glu=True, packed=self.decode_weight(xm, glu=True))
+        return self.forward(xm)
+
     def forward(self, x, add=None):
         """``add``: the other branch of a parallel-residual block, added to the output (in the
         decode GEMV's epilogue where that kernel runs)."""
+        if isinstance(x, PendingNorm):
+            assert add is None, "a PendingNorm consumer has no addend"
+            return self.forward_norm(x)
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(self.weight.dtype)
         wp = self.decode_weight(x)
@@ -137,10 +171,12 @@ class Norm(nn.Module):
                 else:
                     y, s, r = ops.rms_norm_quant(x, self.weight, self.eps, residual, packed=True)
                 return QAct(y, s, True), r
-        if defer and quant and isinstance(x, PartialSum) and self.kind == "rms" and ops.gemv_norm_ok(x.parts):
-            # residual None: a stage's first norm, over the embedding as one fp32 slice
+        if defer and isinstance(x, PartialSum) and self.kind == "rms" and ops.gemv_norm_ok(x.parts) \
+                and (quant or self.weight.dtype == x.dtype):
+            # residual None: a stage's first norm, over the embedding as one fp32 slice; a 16-bit
+            # consumer (not quant) takes the normalised rows in its own dtype
             h = torch.empty(x.parts.shape[1], x.parts.shape[2], dtype=self.weight.dtype, device=x.parts.device)
-            return PendingNorm(x.parts, residual, self.weight, self.eps, h), h
+            return PendingNorm(x.parts, residual, self.weight, self.eps, h, quant), h
         if isinstance(x, PartialSum):
             if self.kind == "rms" and x.parts.is_cuda and ops.gpu_path(x.parts):
                 y, s, r = ops.rms_norm_parts(x.parts, residual, self.weight, self.eps, quant)

@@ -114,6 +114,15 @@ def gemv_norm_ok(parts) -> bool:
         and parts.shape[2] in (2048, 4096) and available() and bool(ext().gemv_norm_on())
 
 
+def gemv_bf16_norm(parts, residual, gamma, eps: float, res_out, packed, bias, N: int, glu: bool = False):
+    """16-bit decode GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual (None: no residual)),
+    the norm in the GEMV's prologue (gemv_bf16.hip norm16_prologue, bit-identical to the norm
+    kernel); the new residual rows go to ``res_out``.  ``packed``: ``pack_bf16_weight(W)``;
+    ``glu``: W = [gate | up], returns silu(gate) * up [M, N / 2].  None when no kernel takes it."""
+    return ext().gemv_bf16_norm(parts, residual.contiguous() if residual is not None else None, gamma, eps, res_out,
+                                packed, bias, N, 1 if glu else 0)
+
+
 def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
                    glu_quant: bool = False):
     """Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual (None: no residual)), per-token int8, with

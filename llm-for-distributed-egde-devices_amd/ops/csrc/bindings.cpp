@@ -21,6 +21,9 @@ int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* g
                         const void* Wp, const float* sw, const void* bias, void* out, float* os, int M, int N, int K,
                         int epi, hipStream_t st);
 void edge_w8a8_gemv_norm_cfg(int on);
+int edge_gemv_bf16_norm(const float* part, int S, const void* res, const void* gamma, float eps, void* res_out,
+                        const void* W, const void* bias, void* out, int M, int N, int K, int epi, hipStream_t st,
+                        int h16);
 int edge_w8a8_gemv_norm_on();
 int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                           float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S, hipStream_t st);
@@ -897,6 +900,43 @@ std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_norm(
   return std::make_tuple(y, s);
 }
 
+// 16-bit decode GEMV (M <= 4) over RMSNorm(sum(parts) + residual) computed in its prologue
+// (gemv_bf16.hip norm16_prologue): epi 0 -> y [M, N], 1 -> SwiGLU of [gate | up], y [M, N / 2];
+// the new residual rows go to res_out.  None when no kernel takes the shape.
+std::optional<at::Tensor> gemv_bf16_norm(const at::Tensor& parts, const std::optional<at::Tensor>& residual,
+                                         const at::Tensor& gamma, double eps, const at::Tensor& res_out,
+                                         const at::Tensor& wp, const std::optional<at::Tensor>& bias, int64_t N,
+                                         int64_t epi) {
+  DEVICE_GUARD(parts);
+  need(parts, at::kFloat, "parts");
+  const bool h16 = gamma.scalar_type() == at::kHalf;
+  const auto dt = h16 ? at::kHalf : at::kBFloat16;
+  need(gamma, dt, "gamma");
+  need(res_out, dt, "res_out");
+  need(wp, dt, "weight");
+  TORCH_CHECK(parts.dim() == 3, "parts must be [S, M, K]");
+  const int64_t S = parts.size(0), M = parts.size(1), K = parts.size(2);
+  TORCH_CHECK(gamma.numel() == K && res_out.numel() == M * K, "gamma [K], res_out [M, K]");
+  TORCH_CHECK(wp.numel() == N * K, "packed weight [N, K]");
+  if (residual) {
+    need(*residual, dt, "residual");
+    TORCH_CHECK(residual->numel() == M * K && res_out.data_ptr() != residual->data_ptr(),
+                "residual [M, K], not aliasing res_out");
+  }
+  if (bias) { need(*bias, dt, "bias"); TORCH_CHECK(bias->numel() == N, "bias [N]"); }
+  TORCH_CHECK(epi == 0 || epi == 1, "epi 0 (out) or 1 (SwiGLU)");
+  if (M < 1 || M > 4 || S < 1 || S > 4 || (K != 2048 && K != 4096) || N % (epi == 1 ? 32 : 16) != 0)
+    return std::nullopt;
+  auto y = at::empty({M, epi == 1 ? N / 2 : N}, res_out.options());
+  const int r = edge_gemv_bf16_norm(parts.data_ptr<float>(), (int)S, residual ? residual->data_ptr() : nullptr,
+                                    gamma.data_ptr(), (float)eps, res_out.data_ptr(), wp.data_ptr(),
+                                    bias ? bias->data_ptr() : nullptr, y.data_ptr(), (int)M, (int)N, (int)K, (int)epi,
+                                    stream(), h16 ? 1 : 0);
+  if (r == -2) return std::nullopt;
+  check(r, "gemv_bf16_norm");
+  return y;
+}
+
 // gate_up projection (16-blocked rows) fused with silu(g) * u: returns bf16 h [M, N/2].
 at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                          const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
@@ -1201,6 +1241,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("addend") = py::none());
   m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
+  m.def("gemv_bf16_norm", &gemv_bf16_norm, "16-bit decode GEMV with the RMSNorm in its prologue (M <= 4)");
   m.def("llmint8_prep_rows", &llmint8_prep_rows, "LLM.int8 preparation for any rows (uncapped, on the device)");
   m.def("llmint8_outlier_rows", &llmint8_outlier_rows, "LLM.int8 outlier part for any rows, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");

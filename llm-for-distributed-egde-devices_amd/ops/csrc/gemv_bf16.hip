@@ -44,14 +44,133 @@ __device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
   return __builtin_bit_cast(v8s, __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p)));
 }
 
-template <int MB, int NTW, int U, int EPI, bool HF>
+// Decode RMSNorm prologue for the 16-bit GEMV (NRM > 0, M <= 4 rows, K 2048 / 4096): the activation
+// rows are RMSNorm(sum of S fp32 split-K slices + residual), computed in the consumer instead of a
+// norm launch of its own (rowwise.hip norm_kernel<NCH, RMS, HAS_RES, !QUANT, PART>: the same
+// element layout, reduction order and roundings, so the rows are bit-identical).  Four 256-thread
+// groups, one row each; the normalised 16-bit rows go to LDS, where the k-loop reads its A
+// fragments.  The slices, residual and gamma loads all issue before any use.  Workgroup 0 writes
+// the new residual rows.  NRM = 8 * NCH + SMAX (S <= SMAX slices).
+struct NormIn16 {
+  const float* part;      // [S][M][K] fp32 slices
+  const bf16_t* res;      // [M][K] residual in (null: none, a stage's first norm over the embedding)
+  const bf16_t* gamma;    // [K]
+  bf16_t* res_out;        // [M][K] residual out (must not alias res)
+  float eps;
+  int S;
+};
+constexpr int NRM16_ROWS = 4;
+
+template <int NCH, int SMAX>
+struct NormRegs16 {
+  uint4 rv[NCH], gv[NCH];
+  float4 pv[NCH][SMAX][2];
+};
+
+template <int NCH, int SMAX>
+__device__ __forceinline__ void norm16_load(const NormIn16& na, int H, int M, NormRegs16<NCH, SMAX>& nr) {
+  const int t = threadIdx.x & 255, row = threadIdx.x >> 8;
+  uint4 (&rv)[NCH] = nr.rv;
+  uint4 (&gv)[NCH] = nr.gv;
+  float4 (&pv)[NCH][SMAX][2] = nr.pv;
+  if (row < M) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = min((c * 256 + t) * 8, H - 8);
+      rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e) : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < SMAX; ++k)
+        if (k < na.S) {
+          const float4* p = reinterpret_cast<const float4*>(na.part + ((size_t)k * M + row) * H + e);
+          pv[c][k][0] = p[0];
+          pv[c][k][1] = p[1];
+        }
+      gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
+    }
+  }
+  asm volatile("" ::: "memory");                          // these loads issue before the weights
+}
+
+template <int NCH, int SMAX, bool HF>
+__device__ __forceinline__ void norm16_prologue(const NormIn16& na, int H, int M, bf16_t* xs, float* nred,
+                                                const NormRegs16<NCH, SMAX>& nr) {
+  const int t = threadIdx.x & 255, row = threadIdx.x >> 8, w = t >> 6;
+  const bool act = row < M;
+  const uint4* rv = nr.rv;
+  const uint4* gv = nr.gv;
+  const auto& pv = nr.pv;
+  float v[NCH][8];
+  float ss = 0.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < SMAX; ++k)
+        if (k < na.S) {
+          const float4 p0 = pv[c][k][0], p1 = pv[c][k][1];
+          v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
+          v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
+        }
+      if (e < H) {
+        unpack8e<HF>(pack8e<HF>(v[c]), v[c]);                 // the projection's 16-bit output
+        float r[8];
+        unpack8e<HF>(rv[c], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+        const uint4 u = pack8e<HF>(v[c]);                    // the residual stream in 16 bits
+        if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + (size_t)row * H + e) = u;
+        unpack8e<HF>(u, v[c]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (e < H) ? v[c][j] - 0.f : 0.f;
+        ss += d * d;
+      }
+    }
+    ss = wave_sum(ss);
+    if ((t & 63) == 0) nred[4 * row + w] = ss;
+  }
+  __syncthreads();
+  if (act) {
+    const float* gr = nred + 4 * row;
+    const float rstd = rsqrtf((((0.f + gr[0]) + gr[1]) + gr[2] + gr[3]) / (float)H + na.eps);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        float wf[8];
+        unpack8e<HF>(gv[c], wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - 0.f) * rstd * wf[j];
+        *reinterpret_cast<uint4*>(xs + (size_t)row * H + e) = pack8e<HF>(v[c]);
+      }
+    }
+  }
+  __syncthreads();                                        // the rows are complete in LDS
+}
+
+template <int MB, int NTW, int U, int EPI, bool HF, int NRM = 0>
 __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ out,
                                                             int M, int N, int K, int F, int S,
-                                                            const bf16_t* __restrict__ add) {
+                                                            const bf16_t* __restrict__ add, NormIn16 na) {
   static_assert(EPI != EPI_GLU || NTW % 2 == 0, "GLU: gate/up tile pairs");
   static_assert(MB * NTW <= 8 && MB * (EPI == EPI_GLU ? NTW / 2 : NTW) <= NW, "LDS reduction / output waves");
+  static_assert(NRM == 0 || (MB == 1 && NTW <= 4 && EPI != EPI_PART), "norm prologue: up to 4 rows, LDS budget");
   __shared__ v4f red[NW][MB * NTW][64];
+  constexpr int NCH_N = NRM / 8, SMAX_N = NRM % 8;
+  __shared__ __attribute__((aligned(16))) bf16_t xs[NRM > 0 ? NRM16_ROWS * NCH_N * 2048 : 8];
+  __shared__ float nred[16];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = 8 * (lane >> 4);
   // output column of tile j for this lane (EPI_GLU: gate tiles then the matching up tiles)
@@ -72,12 +191,27 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   for (int j = 0; j < NTW; ++j) wrow[j] = W + ((size_t)(min(col_of(j), N - 1) >> 4) * (2 * KP) * 64 + lane) * 8;
   const bf16_t* arow[MB];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) arow[mb] = A + (size_t)min(16 * mb + r, M - 1) * K + kq;
+  for (int mb = 0; mb < MB; ++mb) arow[mb] = (NRM > 0 ? xs : A) + (size_t)min(16 * mb + r, M - 1) * K + kq;
+  // NRM: the prologue's loads, then the first k-pair's weights, are in flight before the norm
+  // runs (a wave's loads retire in issue order: weights first would make the norm wait for them)
+  NormRegs16<(NRM > 0 ? NCH_N : 1), (NRM > 0 ? SMAX_N : 1)> nr;
+  v8s b0[NTW][2];
+  if constexpr (NRM > 0) {
+    norm16_load(na, K, M, nr);
+    const int k = min(kbeg + wave, kend - 1) * 64;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      b0[j][0] = ld_nt(wrow[j] + (size_t)k * 16);
+      b0[j][1] = ld_nt(wrow[j] + (size_t)k * 16 + 512);
+    }
+    norm16_prologue<NCH_N, SMAX_N, HF>(na, K, M, xs, nred, nr);
+  }
   v4f acc[MB][NTW];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[mb][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  bool first = NRM > 0;
   for (int kp = kbeg + wave; kp < kend; kp += NW * U) {
     v8s a[U][MB][2], b[U][NTW][2];
 #pragma unroll
@@ -85,8 +219,13 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
       const int k = min(kp + u * NW, kend - 1) * 64;        // clamped: loads never branch
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {                        // tiles 2 kp, 2 kp + 1: 2 KiB contiguous
-        b[u][j][0] = ld_nt(wrow[j] + (size_t)k * 16);
-        b[u][j][1] = ld_nt(wrow[j] + (size_t)k * 16 + 512);
+        if (NRM > 0 && u == 0 && first) {
+          b[u][j][0] = b0[j][0];
+          b[u][j][1] = b0[j][1];
+        } else {
+          b[u][j][0] = ld_nt(wrow[j] + (size_t)k * 16);
+          b[u][j][1] = ld_nt(wrow[j] + (size_t)k * 16 + 512);
+        }
       }
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
@@ -94,6 +233,7 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
         a[u][mb][1] = *reinterpret_cast<const v8s*>(arow[mb] + k + 32);
       }
     }
+    first = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (kp + u * NW < kend) {                             // wave-uniform (scalar) guard
@@ -165,12 +305,13 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   }
 }
 
-template <int MB, int NTW, int U, int EPI, bool HF>
+template <int MB, int NTW, int U, int EPI, bool HF, int NRM = 0>
 int launch_mb(const void* A, const void* W, const void* bias, void* out, int M, int N, int K, int F, int tiles,
-              hipStream_t st, int S, const void* add = nullptr) {
+              hipStream_t st, int S, const void* add = nullptr, const NormIn16& na = NormIn16{}) {
   const int groups = EPI == EPI_GLU ? tiles / (NTW / 2) : (tiles + NTW - 1) / NTW;
-  hipLaunchKernelGGL((gemv_bf16_kernel<MB, NTW, U, EPI, HF>), dim3(groups * S), dim3(NW * 64), 0, st, (const bf16_t*)A,
-                     (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S, (const bf16_t*)add);
+  hipLaunchKernelGGL((gemv_bf16_kernel<MB, NTW, U, EPI, HF, NRM>), dim3(groups * S), dim3(NW * 64), 0, st,
+                     (const bf16_t*)A, (const bf16_t*)W, (const bf16_t*)bias, (bf16_t*)out, M, N, K, F, S,
+                     (const bf16_t*)add, na);
   return (int)hipGetLastError();
 }
 
@@ -225,6 +366,46 @@ int gemv_run(const void* A, const void* W, const void* bias, void* out, int M, i
 #undef PICK
 }
 
+// The 16-bit GEMV over RMSNorm(sum(parts) + residual) (norm16_prologue): M <= 4, K 2048 / 4096,
+// S <= 4 slices; epi 0 (EPI_OUT) or 1 (EPI_GLU).  The geometry of gemv_run for one row block.
+template <bool HF, int NRM>
+int gemv_norm_geo(const NormIn16& na, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
+                  hipStream_t st) {
+  const int KP = K / 64, U = KP >= 64 ? 4 : 2;
+  if (epi == EPI_GLU) {
+    const int F = N / 2, ft = F / 16;
+    if (ft >= 512) {
+      if constexpr (NRM == 20) return -2;                // 4 tiles + 3-4 held slices of K = 4096: spills
+      else return launch_mb<1, 4, 2, EPI_GLU, HF, NRM>(nullptr, W, bias, out, M, N, K, F, ft, st, 1, nullptr, na);
+    }
+    return U == 4 ? launch_mb<1, 2, 4, EPI_GLU, HF, NRM>(nullptr, W, bias, out, M, N, K, F, ft, st, 1, nullptr, na)
+                  : launch_mb<1, 2, 2, EPI_GLU, HF, NRM>(nullptr, W, bias, out, M, N, K, F, ft, st, 1, nullptr, na);
+  }
+  const int nt = N / 16;
+  if (nt >= 1024) {
+    if constexpr (NRM == 20) return -2;
+    else return launch_mb<1, 4, 2, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
+  }
+  if (nt >= 512)
+    return U == 4 ? launch_mb<1, 2, 4, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na)
+                  : launch_mb<1, 2, 2, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
+  return U == 4 ? launch_mb<1, 1, 4, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na)
+                : launch_mb<1, 1, 2, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
+}
+
+template <bool HF>
+int gemv_norm_run(const NormIn16& na, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
+                  hipStream_t st) {
+  if (M < 1 || M > NRM16_ROWS || na.S < 1 || na.S > 4 || (K != 2048 && K != 4096) || N % 16 != 0 ||
+      (epi != EPI_OUT && epi != EPI_GLU) || (epi == EPI_GLU && N % 32 != 0) || na.res_out == nullptr ||
+      na.res == na.res_out)
+    return -2;
+  if (K == 4096) return na.S <= 2 ? gemv_norm_geo<HF, 18>(na, W, bias, out, M, N, K, epi, st)
+                                  : gemv_norm_geo<HF, 20>(na, W, bias, out, M, N, K, epi, st);
+  return na.S <= 2 ? gemv_norm_geo<HF, 10>(na, W, bias, out, M, N, K, epi, st)
+                   : gemv_norm_geo<HF, 12>(na, W, bias, out, M, N, K, epi, st);
+}
+
 // Split-K form: fp32 partial slices part [S, M, N] (bias in slice 0), one 16-column tile per group.
 template <bool HF>
 int gemv_splitk_run(const void* A, const void* W, const void* bias, float* part, int M, int N, int K, int S,
@@ -247,4 +428,15 @@ extern "C" int edge_gemv_bf16_splitk(const void* A, const void* W, const void* b
                                      int S, hipStream_t st, int h16) {
   return h16 ? gemv_splitk_run<true>(A, W, bias, part, M, N, K, S, st)
              : gemv_splitk_run<false>(A, W, bias, part, M, N, K, S, st);
+}
+
+// 16-bit decode GEMV (M <= 4) over RMSNorm(sum of S fp32 slices part [S, M, K] + res) in its
+// prologue; res may be null (a stage's first norm); res_out [M, K] gets the new residual rows
+// (workgroup 0).  epi 0: out [M, N]; 1: SwiGLU of W = [gate | up], out [M, N / 2].  -2: not taken.
+extern "C" int edge_gemv_bf16_norm(const float* part, int S, const void* res, const void* gamma, float eps,
+                                   void* res_out, const void* W, const void* bias, void* out, int M, int N, int K,
+                                   int epi, hipStream_t st, int h16) {
+  const NormIn16 na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};
+  return h16 ? gemv_norm_run<true>(na, W, bias, out, M, N, K, epi, st)
+             : gemv_norm_run<false>(na, W, bias, out, M, N, K, epi, st);
 }
