@@ -30,7 +30,7 @@ import torch.nn as nn
 from .. import ops
 from ..utils import tracing
 from .configs import ModelConfig
-from .layers import Linear, Norm, PartialSum, PendingNorm, QAct, act_fn, quant_if
+from .layers import Linear, Norm, PartialSum, PendingLN, PendingNorm, QAct, act_fn, quant_if
 
 # split-K slices of the bf16 o / down decode GEMVs (0 = off); N = 2048-4096 outputs have only
 # 128-256 tiles, so two slices put every CU to work
@@ -168,6 +168,10 @@ class MLP(nn.Module):
     def forward(self, x, add=None):
         """``add``: the attention branch of a parallel-residual block, added to the down
         projection's output (in its decode GEMV's epilogue)."""
+        if isinstance(x, PendingLN):
+            if self.act in ("gelu_tanh", "gelu") and type(self.up) is Linear:
+                return self.down(self.up.forward_ln(x, act=self.act), add=add)     # 16-bit up + GELU
+            x = x.materialize()
         if isinstance(x, PendingNorm):
             if getattr(self.up, "glu_blocked", False):     # batch 1: norm in the gate_up prologue
                 return self.down(self.up.glu(x), add=add)
@@ -238,6 +242,16 @@ class DecoderLayer(nn.Module):
             if has_mlp:
                 self.mlp.down.split_k_out = BF16_SPLIT_K
 
+    def _ln_deferred(self, x, qa: bool, qm: bool) -> bool:
+        """Parallel-residual 16-bit decode rows whose LayerNorm(s) the qkv / up GEMVs can compute."""
+        cfg = self.cfg
+        return (not qa and not qm and cfg.norm == "layer" and self.has_attn and self.has_mlp
+                and isinstance(x, torch.Tensor) and self.norm1 is not None
+                and (cfg.shared_input_norm or self.norm2 is not None)
+                and cfg.act in ("gelu_tanh", "gelu") and x.dim() == 2 and ops.gemv_ln_ok(x)
+                and _ln_consumer_ok(self.attn.qkv) and _ln_consumer_ok(self.mlp.up)
+                and x.dtype == self.norm1.weight.dtype)
+
     def forward(self, x, residual, ctx: AttnCtx):
         cfg = self.cfg
         if not cfg.parallel_residual:
@@ -258,6 +272,20 @@ class DecoderLayer(nn.Module):
             return self.mlp(n2), h2
         qa = self.attn.qkv.takes_quantized_input
         qm = self.mlp.up.takes_quantized_input
+        if self._ln_deferred(x, qa, qm):
+            # 16-bit decode at batch 1: each consumer computes the LayerNorm in its GEMV prologue
+            n1, h = self.norm1, torch.empty_like(x)
+            if cfg.shared_input_norm:
+                # phi: the qkv GEMV computes the norm and also writes it for the up projection
+                # (a second prologue would cost more than it saves: 1.726 -> 1.775 ms per step)
+                y = torch.empty_like(x)
+                pa = PendingLN(x, residual, n1.weight, n1.bias, n1.eps, h, y)
+                pm = y
+            else:                                              # gpt_neox: norm2 of h = x + residual
+                n2 = self.norm2
+                pa = PendingLN(x, residual, n1.weight, n1.bias, n1.eps, h)
+                pm = PendingLN(x, residual, n2.weight, n2.bias, n2.eps, h)
+            return self.mlp(pm, add=self.attn(pa, ctx)), h
         if cfg.shared_input_norm:                      # phi
             n, h = self.norm1(x, residual, quant=qa and qm)
             if qa != qm:                               # mixed modes: feed each consumer its form
@@ -270,6 +298,10 @@ class DecoderLayer(nn.Module):
         n1, h = self.norm1(x, residual, quant=qa)      # gpt_neox
         n2, _ = self.norm2(h, None, quant=qm)
         return self.mlp(n2, add=self.attn(n1, ctx)), h
+
+
+def _ln_consumer_ok(lin) -> bool:
+    return type(lin) is Linear and lin.pending_ln_ok()
 
 
 class DecoderLM(nn.Module):

@@ -61,6 +61,29 @@ class PendingNorm(NamedTuple):
         return QAct(y, s) if self.quant else y
 
 
+class PendingLN(NamedTuple):
+    """LayerNorm of 16-bit decode rows x (+ residual, M <= 4), deferred into the prologue of the
+    16-bit GEMV(s) that consume it (ops.gemv_bf16_ln; parallel-residual blocks, where the qkv and
+    the MLP up projection both read a norm of the same rows): no norm launch.  ``h`` = x + residual,
+    written by the consumer (every consumer writes the same bits); ``y`` (optional): the consumer
+    also writes the normalised rows there, for a second consumer that reads them as a plain input.
+    ``materialize()`` runs the norm kernel instead."""
+    x: torch.Tensor
+    residual: Optional[torch.Tensor]
+    weight: torch.Tensor
+    bias: Optional[torch.Tensor]
+    eps: float
+    h: torch.Tensor
+    y: Optional[torch.Tensor] = None
+
+    def materialize(self) -> torch.Tensor:
+        y, r = ops.layer_norm(self.x, self.weight, self.bias, self.eps, self.residual)
+        self.h.copy_(r.view_as(self.h))
+        if self.y is not None:
+            self.y.copy_(y.view_as(self.y))
+        return y
+
+
 class GroupQuantBF16(NamedTuple):
     """bf16 activation that a W8A8 consumer quantises per (token, 64 columns) on the fly."""
     x: torch.Tensor
@@ -108,9 +131,32 @@ class Linear(nn.Module):
             return ops.linear_bf16(xm, self.weight, self.bias, glu=True, packed=self.decode_weight(xm, glu=True))
         return self.forward(xm)
 
+    def pending_ln_ok(self) -> bool:
+        """Whether this 16-bit projection's decode GEMV can compute a LayerNorm in its prologue."""
+        w = self.weight
+        return (w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and ops.available()
+                and self.in_features <= 4096 and self.in_features % 64 == 0 and self.out_features % 16 == 0
+                and not self.split_k_out and ops.gpu_path(w))
+
+    def forward_ln(self, x: "PendingLN", act: Optional[str] = None):
+        """The decode GEMV over a PendingLN (LayerNorm in the prologue); act: its GELU epilogue."""
+        y = None
+        if self.pending_ln_ok() and x.x.dtype == self.weight.dtype:
+            y = ops.gemv_bf16_ln(x.x, x.residual, x.weight, x.bias, x.eps, x.h, self.packed_weight(), self.bias,
+                                 self.out_features, act, y_out=x.y)
+        if y is not None:
+            return y
+        xm = x.materialize()
+        if act is not None:
+            return ops.linear_bf16(xm, self.weight, self.bias, act=act, packed=self.decode_weight(xm))
+        return self.forward(xm)
+
     def forward(self, x, add=None):
         """``add``: the other branch of a parallel-residual block, added to the output (in the
         decode GEMV's epilogue where that kernel runs)."""
+        if isinstance(x, PendingLN):
+            assert add is None, "a PendingLN consumer has no addend"
+            return self.forward_ln(x)
         if isinstance(x, PendingNorm):
             assert add is None, "a PendingNorm consumer has no addend"
             return self.forward_norm(x)

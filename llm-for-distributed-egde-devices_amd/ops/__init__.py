@@ -123,6 +123,27 @@ def gemv_bf16_norm(parts, residual, gamma, eps: float, res_out, packed, bias, N:
                                 packed, bias, N, 1 if glu else 0)
 
 
+def gemv_ln_ok(x) -> bool:
+    """Whether a decode 16-bit GEMV can take the LayerNorm of these rows x [M, K] (+ residual) in
+    its prologue (gemv_bf16.hip ln16_prologue: M <= NORM_FUSE_MAX_ROWS, K <= 4096, K % 64 == 0)."""
+    return x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= min(4, NORM_FUSE_MAX_ROWS) and x.shape[1] <= 4096 \
+        and x.shape[1] % 64 == 0 and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous() \
+        and available() and bool(ext().gemv_norm_on())
+
+
+_LN_EPI = {None: 0, "gelu_tanh": 2, "gelu": 3}
+
+
+def gemv_bf16_ln(x, residual, gamma, beta, eps: float, res_out, packed, bias, N: int, act: Optional[str] = None,
+                 y_out=None):
+    """16-bit decode GEMV (M <= 4 rows) over LayerNorm(x + residual (None: none)) with the norm in
+    its prologue (bit-identical to the norm kernel); x + residual goes to ``res_out``, the
+    normalised rows to ``y_out`` when given (a second consumer's input); ``act``: None /
+    "gelu_tanh" / "gelu" epilogue.  None when no kernel takes the shape."""
+    return ext().gemv_bf16_ln(x, residual.contiguous() if residual is not None else None, gamma, beta, eps, res_out,
+                              packed, bias, N, _LN_EPI[act], y_out)
+
+
 def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
                    glu_quant: bool = False):
     """Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual (None: no residual)), per-token int8, with

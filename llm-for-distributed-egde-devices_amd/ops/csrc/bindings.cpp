@@ -24,6 +24,9 @@ void edge_w8a8_gemv_norm_cfg(int on);
 int edge_gemv_bf16_norm(const float* part, int S, const void* res, const void* gamma, float eps, void* res_out,
                         const void* W, const void* bias, void* out, int M, int N, int K, int epi, hipStream_t st,
                         int h16);
+int edge_gemv_bf16_ln(const void* x, const void* res, const void* gamma, const void* beta, float eps, void* res_out,
+                      const void* W, const void* bias, void* out, int M, int N, int K, int epi, hipStream_t st,
+                      int h16, void* y_out);
 int edge_w8a8_gemv_norm_on();
 int edge_w8a8_gemm_splitk(const void* A, const float* sa, const void* Wp, const float* sw, const void* bias,
                           float* part, int M, int N, int K, int KT, int a_mode, int Mpad, int S, hipStream_t st);
@@ -937,6 +940,47 @@ std::optional<at::Tensor> gemv_bf16_norm(const at::Tensor& parts, const std::opt
   return y;
 }
 
+// 16-bit decode GEMV (M <= 4) over LayerNorm(x + residual) computed in its prologue (the
+// parallel-residual decoders): epi 0 -> y [M, N], 2 / 3 -> gelu (tanh / erf); x + residual goes to
+// res_out.  None when no kernel takes the shape.
+std::optional<at::Tensor> gemv_bf16_ln(const at::Tensor& x, const std::optional<at::Tensor>& residual,
+                                       const at::Tensor& gamma, const std::optional<at::Tensor>& beta, double eps,
+                                       const at::Tensor& res_out, const at::Tensor& wp,
+                                       const std::optional<at::Tensor>& bias, int64_t N, int64_t epi,
+                                       const std::optional<at::Tensor>& y_out) {
+  DEVICE_GUARD(x);
+  const bool h16 = gamma.scalar_type() == at::kHalf;
+  const auto dt = h16 ? at::kHalf : at::kBFloat16;
+  need(x, dt, "x");
+  need(gamma, dt, "gamma");
+  need(res_out, dt, "res_out");
+  need(wp, dt, "weight");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [M, K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(gamma.numel() == K && res_out.numel() == M * K && wp.numel() == N * K, "gamma [K], res_out [M, K], W [N, K]");
+  if (beta) { need(*beta, dt, "beta"); TORCH_CHECK(beta->numel() == K, "beta [K]"); }
+  if (residual) {
+    need(*residual, dt, "residual");
+    TORCH_CHECK(residual->numel() == M * K && res_out.data_ptr() != residual->data_ptr(),
+                "residual [M, K], not aliasing res_out");
+  }
+  if (bias) { need(*bias, dt, "bias"); TORCH_CHECK(bias->numel() == N, "bias [N]"); }
+  if (y_out) {
+    need(*y_out, dt, "y_out");
+    TORCH_CHECK(y_out->numel() == M * K && y_out->data_ptr() != res_out.data_ptr(), "y_out [M, K]");
+  }
+  TORCH_CHECK(epi == 0 || epi == 2 || epi == 3, "epi 0 (out), 2 (gelu tanh), 3 (gelu erf)");
+  if (M < 1 || M > 4 || K > 4096 || K % 64 != 0 || N % 16 != 0) return std::nullopt;
+  auto y = at::empty({M, N}, res_out.options());
+  const int r = edge_gemv_bf16_ln(x.data_ptr(), residual ? residual->data_ptr() : nullptr, gamma.data_ptr(),
+                                  beta ? beta->data_ptr() : nullptr, (float)eps, res_out.data_ptr(), wp.data_ptr(),
+                                  bias ? bias->data_ptr() : nullptr, y.data_ptr(), (int)M, (int)N, (int)K, (int)epi,
+                                  stream(), h16 ? 1 : 0, y_out ? y_out->data_ptr() : nullptr);
+  if (r == -2) return std::nullopt;
+  check(r, "gemv_bf16_ln");
+  return y;
+}
+
 // gate_up projection (16-blocked rows) fused with silu(g) * u: returns bf16 h [M, N/2].
 at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                          const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
@@ -1242,6 +1286,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("llmint8_prep", &llmint8_prep, "LLM.int8 decode preparation (outlier columns on the device)");
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
   m.def("gemv_bf16_norm", &gemv_bf16_norm, "16-bit decode GEMV with the RMSNorm in its prologue (M <= 4)");
+  m.def("gemv_bf16_ln", &gemv_bf16_ln, "16-bit decode GEMV with the LayerNorm in its prologue (M <= 4)");
   m.def("llmint8_prep_rows", &llmint8_prep_rows, "LLM.int8 preparation for any rows (uncapped, on the device)");
   m.def("llmint8_outlier_rows", &llmint8_outlier_rows, "LLM.int8 outlier part for any rows, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");

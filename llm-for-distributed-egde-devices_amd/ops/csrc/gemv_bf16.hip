@@ -51,28 +51,48 @@ __device__ __forceinline__ v8s ld_nt(const bf16_t* p) {
 // groups, one row each; the normalised 16-bit rows go to LDS, where the k-loop reads its A
 // fragments.  The slices, residual and gamma loads all issue before any use.  Workgroup 0 writes
 // the new residual rows.  NRM = 8 * NCH + SMAX (S <= SMAX slices).
+// LN (NRM >= 64): LayerNorm of x + residual with 16-bit input rows x (the parallel-residual
+// decoders, Phi-2 / GPT-NeoX: norm_kernel<NCH, !RMS, HAS_RES, !QUANT, !PART>), K up to 4096.
 struct NormIn16 {
-  const float* part;      // [S][M][K] fp32 slices
+  const float* part;      // [S][M][K] fp32 slices (RMS)
   const bf16_t* res;      // [M][K] residual in (null: none, a stage's first norm over the embedding)
   const bf16_t* gamma;    // [K]
   bf16_t* res_out;        // [M][K] residual out (must not alias res)
   float eps;
   int S;
+  const bf16_t* x;        // [M][K] 16-bit input rows (LN)
+  const bf16_t* beta;     // [K] (LN; may be null)
+  bf16_t* y_out;          // [M][K] (LN; may be null): workgroup 0 also writes the normalised rows here
 };
 constexpr int NRM16_ROWS = 4;
 
-template <int NCH, int SMAX>
+template <int NCH, int SMAX, bool LN = false>
 struct NormRegs16 {
   uint4 rv[NCH], gv[NCH];
-  float4 pv[NCH][SMAX][2];
+  float4 pv[NCH][LN ? 1 : SMAX][2];
+  uint4 xv[NCH], bv[NCH];
 };
 
-template <int NCH, int SMAX>
-__device__ __forceinline__ void norm16_load(const NormIn16& na, int H, int M, NormRegs16<NCH, SMAX>& nr) {
+template <int NCH, int SMAX, bool LN>
+__device__ __forceinline__ void norm16_load(const NormIn16& na, int H, int M, NormRegs16<NCH, SMAX, LN>& nr) {
   const int t = threadIdx.x & 255, row = threadIdx.x >> 8;
   uint4 (&rv)[NCH] = nr.rv;
   uint4 (&gv)[NCH] = nr.gv;
-  float4 (&pv)[NCH][SMAX][2] = nr.pv;
+  auto& pv = nr.pv;
+  if constexpr (LN) {
+    if (row < M) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = min((c * 256 + t) * 8, H - 8);
+        nr.xv[c] = *reinterpret_cast<const uint4*>(na.x + (size_t)row * H + e);
+        rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e) : uint4{0u, 0u, 0u, 0u};
+        gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
+        nr.bv[c] = na.beta != nullptr ? *reinterpret_cast<const uint4*>(na.beta + e) : uint4{0u, 0u, 0u, 0u};
+      }
+    }
+    asm volatile("" ::: "memory");
+    return;
+  }
   if (row < M) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -89,6 +109,80 @@ __device__ __forceinline__ void norm16_load(const NormIn16& na, int H, int M, No
     }
   }
   asm volatile("" ::: "memory");                          // these loads issue before the weights
+}
+
+// LayerNorm form (norm_kernel's !RMS, HAS_RES, !PART path: x + residual rounded to 16 bits, the
+// mean, then the variance of the rounded row, gamma and beta)
+template <int NCH, bool HF>
+__device__ __forceinline__ void ln16_prologue(const NormIn16& na, int H, int M, bf16_t* xs, float* nred,
+                                              const NormRegs16<NCH, 1, true>& nr) {
+  const int t = threadIdx.x & 255, row = threadIdx.x >> 8, w = t >> 6;
+  const bool act = row < M;
+  float v[NCH][8];
+  float sm = 0.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        unpack8e<HF>(nr.xv[c], v[c]);
+        float r[8];
+        unpack8e<HF>(nr.rv[c], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+        const uint4 u = pack8e<HF>(v[c]);                    // the residual stream in 16 bits
+        if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + (size_t)row * H + e) = u;
+        unpack8e<HF>(u, v[c]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm += v[c][j];
+    sm = wave_sum(sm);
+    if ((t & 63) == 0) nred[4 * row + w] = sm;
+  }
+  __syncthreads();
+  float mean = 0.f, ss = 0.f;
+  if (act) {
+    const float* gr = nred + 4 * row;
+    mean = ((((0.f + gr[0]) + gr[1]) + gr[2]) + gr[3]) / (float)H;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (e < H) ? v[c][j] - mean : 0.f;
+        ss += d * d;
+      }
+    }
+    ss = wave_sum(ss);
+  }
+  __syncthreads();                                        // every group has read its sums
+  if (act && (t & 63) == 0) nred[4 * row + w] = ss;
+  __syncthreads();
+  if (act) {
+    const float* gr = nred + 4 * row;
+    const float rstd = rsqrtf(((((0.f + gr[0]) + gr[1]) + gr[2]) + gr[3]) / (float)H + na.eps);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        float wf[8], bf[8];
+        unpack8e<HF>(nr.gv[c], wf);
+        unpack8e<HF>(nr.bv[c], bf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - mean) * rstd * wf[j] + bf[j];
+        const uint4 u = pack8e<HF>(v[c]);
+        *reinterpret_cast<uint4*>(xs + (size_t)row * H + e) = u;
+        if (na.y_out != nullptr && blockIdx.x == 0) *reinterpret_cast<uint4*>(na.y_out + (size_t)row * H + e) = u;
+      }
+    }
+  }
+  __syncthreads();                                        // the rows are complete in LDS
 }
 
 template <int NCH, int SMAX, bool HF>
@@ -168,7 +262,9 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   static_assert(MB * NTW <= 8 && MB * (EPI == EPI_GLU ? NTW / 2 : NTW) <= NW, "LDS reduction / output waves");
   static_assert(NRM == 0 || (MB == 1 && NTW <= 4 && EPI != EPI_PART), "norm prologue: up to 4 rows, LDS budget");
   __shared__ v4f red[NW][MB * NTW][64];
-  constexpr int NCH_N = NRM / 8, SMAX_N = NRM % 8;
+  // NRM: 8 NCH + SMAX (RMSNorm over split-K slices), + 64 for the LayerNorm of 16-bit rows
+  constexpr bool LN_N = NRM >= 64;
+  constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N ? 1 : NRM % 8;
   __shared__ __attribute__((aligned(16))) bf16_t xs[NRM > 0 ? NRM16_ROWS * NCH_N * 2048 : 8];
   __shared__ float nred[16];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -194,7 +290,7 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
   for (int mb = 0; mb < MB; ++mb) arow[mb] = (NRM > 0 ? xs : A) + (size_t)min(16 * mb + r, M - 1) * K + kq;
   // NRM: the prologue's loads, then the first k-pair's weights, are in flight before the norm
   // runs (a wave's loads retire in issue order: weights first would make the norm wait for them)
-  NormRegs16<(NRM > 0 ? NCH_N : 1), (NRM > 0 ? SMAX_N : 1)> nr;
+  NormRegs16<(NRM > 0 ? NCH_N : 1), (NRM > 0 ? SMAX_N : 1), LN_N> nr;
   v8s b0[NTW][2];
   if constexpr (NRM > 0) {
     norm16_load(na, K, M, nr);
@@ -204,7 +300,8 @@ __global__ void __launch_bounds__(NW * 64) gemv_bf16_kernel(const bf16_t* __rest
       b0[j][0] = ld_nt(wrow[j] + (size_t)k * 16);
       b0[j][1] = ld_nt(wrow[j] + (size_t)k * 16 + 512);
     }
-    norm16_prologue<NCH_N, SMAX_N, HF>(na, K, M, xs, nred, nr);
+    if constexpr (LN_N) ln16_prologue<NCH_N, HF>(na, K, M, xs, nred, nr);
+    else norm16_prologue<NCH_N, SMAX_N, HF>(na, K, M, xs, nred, nr);
   }
   v4f acc[MB][NTW];
 #pragma unroll
@@ -382,15 +479,32 @@ int gemv_norm_geo(const NormIn16& na, const void* W, const void* bias, void* out
                   : launch_mb<1, 2, 2, EPI_GLU, HF, NRM>(nullptr, W, bias, out, M, N, K, F, ft, st, 1, nullptr, na);
   }
   const int nt = N / 16;
-  if (nt >= 1024) {
-    if constexpr (NRM == 20) return -2;
-    else return launch_mb<1, 4, 2, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
-  }
-  if (nt >= 512)
-    return U == 4 ? launch_mb<1, 2, 4, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na)
-                  : launch_mb<1, 2, 2, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
-  return U == 4 ? launch_mb<1, 1, 4, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na)
-                : launch_mb<1, 1, 2, EPI_OUT, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
+#define NPICK(EP)                                                                                              \
+  if (nt >= 1024) {                                                                                            \
+    if constexpr (NRM == 20) return -2;                                                                        \
+    else return launch_mb<1, 4, 2, EP, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);     \
+  }                                                                                                            \
+  if (nt >= 512)                                                                                               \
+    return U == 4 ? launch_mb<1, 2, 4, EP, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na)  \
+                  : launch_mb<1, 2, 2, EP, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na); \
+  return U == 4 ? launch_mb<1, 1, 4, EP, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na)    \
+                : launch_mb<1, 1, 2, EP, HF, NRM>(nullptr, W, bias, out, M, N, K, 0, nt, st, 1, nullptr, na);
+  if (epi == EPI_GELU_TANH) { NPICK(EPI_GELU_TANH) }
+  if (epi == EPI_GELU) { NPICK(EPI_GELU) }
+  NPICK(EPI_OUT)
+#undef NPICK
+}
+
+// LayerNorm prologue over 16-bit rows x (+ residual): K <= 4096 (K % 64 == 0), epi 0 / 2 / 3.
+template <bool HF>
+int gemv_ln_run(const NormIn16& na, const void* W, const void* bias, void* out, int M, int N, int K, int epi,
+                hipStream_t st) {
+  if (M < 1 || M > NRM16_ROWS || K > 4096 || K % 64 != 0 || N % 16 != 0 || na.x == nullptr ||
+      (epi != EPI_OUT && epi != EPI_GELU_TANH && epi != EPI_GELU) || na.res_out == nullptr || na.res == na.res_out ||
+      na.x == na.res_out || na.y_out == na.x || na.y_out == na.res_out)
+    return -2;
+  return K <= 2048 ? gemv_norm_geo<HF, 64 + 8>(na, W, bias, out, M, N, K, epi, st)
+                   : gemv_norm_geo<HF, 64 + 16>(na, W, bias, out, M, N, K, epi, st);
 }
 
 template <bool HF>
@@ -436,7 +550,20 @@ extern "C" int edge_gemv_bf16_splitk(const void* A, const void* W, const void* b
 extern "C" int edge_gemv_bf16_norm(const float* part, int S, const void* res, const void* gamma, float eps,
                                    void* res_out, const void* W, const void* bias, void* out, int M, int N, int K,
                                    int epi, hipStream_t st, int h16) {
-  const NormIn16 na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S};
+  const NormIn16 na{part, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, S, nullptr, nullptr,
+                    nullptr};
   return h16 ? gemv_norm_run<true>(na, W, bias, out, M, N, K, epi, st)
              : gemv_norm_run<false>(na, W, bias, out, M, N, K, epi, st);
+}
+
+// 16-bit decode GEMV (M <= 4) over LayerNorm(x + res) (res may be null) in its prologue; res_out
+// [M, K] gets x + res (workgroup 0), y_out (when not null) the normalised rows, for a second
+// consumer.  epi 0: out [M, N]; 2 / 3: gelu (tanh / erf).  -2: not taken.
+extern "C" int edge_gemv_bf16_ln(const void* x, const void* res, const void* gamma, const void* beta, float eps,
+                                 void* res_out, const void* W, const void* bias, void* out, int M, int N, int K,
+                                 int epi, hipStream_t st, int h16, void* y_out) {
+  const NormIn16 na{nullptr, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, 0, (const bf16_t*)x,
+                    (const bf16_t*)beta, (bf16_t*)y_out};
+  return h16 ? gemv_ln_run<true>(na, W, bias, out, M, N, K, epi, st)
+             : gemv_ln_run<false>(na, W, bias, out, M, N, K, epi, st);
 }

@@ -617,6 +617,56 @@ def test_gemv_bf16_norm_prologue_exact(cuda, M, K, N, S, res, glu, dt):
     assert torch.equal(y, ref), (y.float() - ref.float()).abs().max()
 
 
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("K,N", [(2048, 6144), (2560, 10240), (2560, 2560), (4096, 16384)])
+@pytest.mark.parametrize("act", [None, "gelu_tanh", "gelu"])
+@pytest.mark.parametrize("res", [True, False])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gemv_bf16_ln_prologue_exact(cuda, M, K, N, act, res, dt):
+    """16-bit decode GEMV with the LayerNorm of x (+ residual) in its prologue (gemv_bf16.hip
+    ln16_prologue) == the norm kernel followed by the plain / GELU GEMV, bit for bit, and the same
+    x + residual rows."""
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=cuda).to(dt)
+    resid = torch.randn(M, K, device=cuda).to(dt) if res else None
+    gamma = (torch.rand(K, device=cuda) + 0.5).to(dt)
+    beta = (torch.randn(K, device=cuda) * 0.1).to(dt)
+    w = (torch.randn(N, K, device=cuda) * 0.02).to(dt)
+    bias = (torch.randn(N, device=cuda) * 0.1).to(dt)
+    wp = ops.pack_bf16_weight(w)
+    h = torch.empty(M, K, device=cuda, dtype=dt)
+    yo = torch.empty(M, K, device=cuda, dtype=dt) if res else None     # the normalised rows too
+    y = ops.gemv_bf16_ln(x, resid, gamma, beta, 1e-5, h, wp, bias, N, act, y_out=yo)
+    assert y is not None
+    yr, hr = ops.layer_norm(x, gamma, beta, 1e-5, resid)
+    ref = ops.linear_bf16(yr, w, bias, act=act, packed=wp)
+    assert torch.equal(h, hr.view_as(h)), "residual rows differ"
+    assert yo is None or torch.equal(yo, yr.view_as(yo)), "normalised rows differ"
+    assert torch.equal(y, ref), (y.float() - ref.float()).abs().max()
+
+
+@pytest.mark.parametrize("arch", ["phi", "gpt_neox"])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_parallel_residual_decode_ln_fused_matches_unfused(cuda, arch, dt):
+    """Phi-2-like and GPT-NeoX-like 16-bit models generate the same greedy tokens at batch 1 with
+    their LayerNorms in the qkv / up GEMV prologues as with the norm kernels (gemv_norm 0)."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    cfg = tiny(arch, hidden_size=256, num_heads=4, num_kv_heads=4, head_dim=64, intermediate_size=1024,
+               rotary_dim=32, num_layers=3)
+    sp = SamplingParams(max_new_tokens=12, do_sample=False)
+    C = ops.ext()
+    outs = []
+    for on in (1, 0):
+        C.tune("gemv_norm", on, 0)
+        try:
+            m = build_model(cfg, dtype=dt, device=cuda, seed=11)
+            outs.append(Generator(m, max_batch=1, max_seq=64).generate([[1, 5, 9, 13, 2, 7]], sp, seed=0).tokens)
+        finally:
+            C.tune("gemv_norm", 1, 0)
+    assert outs[0] == outs[1]
+
+
 def test_bf16_llama_decode_norm_fused_matches_unfused(cuda):
     """A bf16 Llama (hidden 2048: the prologue's K) generates the same greedy tokens at batch 1
     with its RMSNorms in the qkv / gate_up GEMV prologues as with the norm kernels (gemv_norm 0),
