@@ -171,6 +171,8 @@ class MLP(nn.Module):
         if isinstance(x, PendingLN):
             if self.act in ("gelu_tanh", "gelu") and type(self.up) is Linear:
                 return self.down(self.up.forward_ln(x, act=self.act), add=add)     # 16-bit up + GELU
+            if x.quant and self.act in ("gelu_tanh", "gelu") and hasattr(self.up, "geluq"):
+                return self.down(self.up.geluq(x, self.act), add=add)              # W8A8 up + GELU + quant
             x = x.materialize()
         if isinstance(x, PendingNorm):
             if getattr(self.up, "glu_blocked", False):     # batch 1: norm in the gate_up prologue
@@ -252,6 +254,18 @@ class DecoderLayer(nn.Module):
                 and _ln_consumer_ok(self.attn.qkv) and _ln_consumer_ok(self.mlp.up)
                 and x.dtype == self.norm1.weight.dtype)
 
+    def _ln_deferred_w8a8(self, x, qa: bool, qm: bool) -> bool:
+        """GPT-NeoX W8A8 decode rows whose two LayerNorms the qkv / up GEMVs can compute (Phi shares
+        one norm between them, and only one prologue would take it: no gain, not taken)."""
+        cfg = self.cfg
+        return (qa and qm and cfg.norm == "layer" and not cfg.shared_input_norm and self.has_attn
+                and self.has_mlp and self.norm2 is not None and cfg.act in ("gelu_tanh", "gelu")
+                and isinstance(x, torch.Tensor) and x.dim() == 2 and x.dtype == torch.bfloat16
+                and ops.gemv_ln_ok(x) and self.norm1.weight.dtype == torch.bfloat16
+                and getattr(self.attn.qkv, "pending_ln_ok", lambda **k: False)()
+                and getattr(self.mlp.up, "pending_ln_ok", lambda **k: False)(geluq=True)
+                and getattr(self.mlp.down, "group_scales_ok", lambda m: False)(x.shape[0]))
+
     def forward(self, x, residual, ctx: AttnCtx):
         cfg = self.cfg
         if not cfg.parallel_residual:
@@ -272,6 +286,12 @@ class DecoderLayer(nn.Module):
             return self.mlp(n2), h2
         qa = self.attn.qkv.takes_quantized_input
         qm = self.mlp.up.takes_quantized_input
+        if self._ln_deferred_w8a8(x, qa, qm):
+            # W8A8 decode at batch 1 (GPT-NeoX): LayerNorm + int8 quant in the qkv / up GEMV prologues
+            n1, n2, h = self.norm1, self.norm2, torch.empty_like(x)
+            pa = PendingLN(x, residual, n1.weight, n1.bias, n1.eps, h, None, True)
+            pm = PendingLN(x, residual, n2.weight, n2.bias, n2.eps, h, None, True)
+            return self.mlp(pm, add=self.attn(pa, ctx)), h
         if self._ln_deferred(x, qa, qm):
             # 16-bit decode at batch 1: each consumer computes the LayerNorm in its GEMV prologue
             n1, h = self.norm1, torch.empty_like(x)

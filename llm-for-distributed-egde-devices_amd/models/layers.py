@@ -75,8 +75,13 @@ class PendingLN(NamedTuple):
     eps: float
     h: torch.Tensor
     y: Optional[torch.Tensor] = None
+    quant: bool = False              # the consumers are W8A8: int8 rows per token (QAct)
 
-    def materialize(self) -> torch.Tensor:
+    def materialize(self):
+        if self.quant:
+            q, s, r = ops.layer_norm_quant(self.x, self.weight, self.bias, self.eps, self.residual)
+            self.h.copy_(r.view_as(self.h))
+            return QAct(q, s)
         y, r = ops.layer_norm(self.x, self.weight, self.bias, self.eps, self.residual)
         self.h.copy_(r.view_as(self.h))
         if self.y is not None:

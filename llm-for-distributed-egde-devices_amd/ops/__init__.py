@@ -144,6 +144,20 @@ def gemv_bf16_ln(x, residual, gamma, beta, eps: float, res_out, packed, bias, N:
                               packed, bias, N, _LN_EPI[act], y_out)
 
 
+def w8a8_gemv_ln(x, residual, gamma, beta, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
+                 geluq: Optional[str] = None):
+    """W8A8 decode GEMV (M <= 4 rows) over LayerNorm(x + residual) of bf16 rows, int8 per token, the
+    norm in its prologue (bit-identical to layer_norm_quant); x + residual goes to ``res_out``.
+    Returns bf16 y [M, N], or with ``geluq`` ("gelu_tanh" / "gelu") the quantising GELU's
+    (q [M, N], scales [N/64, 16]).  None when no kernel takes the shape."""
+    epi = 0 if geluq is None else (4 if geluq == "gelu_tanh" else 5)
+    r = ext().w8a8_gemv_ln(x, residual.contiguous() if residual is not None else None, gamma, beta, eps, res_out,
+                           w_packed, w_scale, bias, N, K, epi)
+    if r is None:
+        return None
+    return r if geluq is not None else r[0]
+
+
 def w8a8_gemv_norm(parts, residual, gamma, eps: float, res_out, w_packed, w_scale, bias, N: int, K: int,
                    glu_quant: bool = False):
     """Decode W8A8 GEMV (M <= 4 rows) over RMSNorm(sum(parts) + residual (None: no residual)), per-token int8, with

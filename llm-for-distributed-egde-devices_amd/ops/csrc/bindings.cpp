@@ -21,6 +21,9 @@ int edge_w8a8_gemv_norm(const float* part, int S, const void* res, const void* g
                         const void* Wp, const float* sw, const void* bias, void* out, float* os, int M, int N, int K,
                         int epi, hipStream_t st);
 void edge_w8a8_gemv_norm_cfg(int on);
+int edge_w8a8_gemv_ln(const void* x, const void* res, const void* gamma, const void* beta, float eps, void* res_out,
+                      const void* Wp, const float* sw, const void* bias, void* out, float* os, int M, int N, int K,
+                      int epi, hipStream_t st);
 int edge_gemv_bf16_norm(const float* part, int S, const void* res, const void* gamma, float eps, void* res_out,
                         const void* W, const void* bias, void* out, int M, int N, int K, int epi, hipStream_t st,
                         int h16);
@@ -981,6 +984,47 @@ std::optional<at::Tensor> gemv_bf16_ln(const at::Tensor& x, const std::optional<
   return y;
 }
 
+// W8A8 decode GEMV (M <= 4) over LayerNorm(x + residual) of bf16 rows, int8 per token, computed
+// in its prologue: epi 0 -> (y bf16 [M, N], None); 4 / 5 -> gelu (tanh / erf) of the output, int8
+// per (token, 64 columns): (q [M, N], scales [N/64, 16]).  None when no kernel takes the shape.
+std::optional<std::tuple<at::Tensor, std::optional<at::Tensor>>> w8a8_gemv_ln(
+    const at::Tensor& x, const std::optional<at::Tensor>& residual, const at::Tensor& gamma,
+    const std::optional<at::Tensor>& beta, double eps, const at::Tensor& res_out, const at::Tensor& wp,
+    const at::Tensor& sw, const std::optional<at::Tensor>& bias, int64_t N, int64_t K, int64_t epi) {
+  DEVICE_GUARD(x);
+  need(x, at::kBFloat16, "x");
+  need(gamma, at::kBFloat16, "gamma");
+  need(res_out, at::kBFloat16, "res_out");
+  check_w8a8_operands(wp, sw, bias, N, K);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) == K, "x must be contiguous [M, K]");
+  const int64_t M = x.size(0);
+  TORCH_CHECK(gamma.numel() == K && res_out.numel() == M * K, "gamma [K], res_out [M, K]");
+  if (beta) { need(*beta, at::kBFloat16, "beta"); TORCH_CHECK(beta->numel() == K, "beta [K]"); }
+  if (residual) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == M * K && res_out.data_ptr() != residual->data_ptr(),
+                "residual [M, K], not aliasing res_out");
+  }
+  TORCH_CHECK(epi == 0 || epi == 4 || epi == 5, "epi 0 (out), 4 / 5 (gelu tanh / erf + grouped int8)");
+  if (!edge_w8a8_gemv_norm_on() || M < 1 || M > 4 || K > 4096 || K % 64 != 0 || N % (epi ? 64 : 16) != 0)
+    return std::nullopt;
+  at::Tensor y;
+  std::optional<at::Tensor> s;
+  if (epi == 0) {
+    y = at::empty({M, N}, res_out.options());
+  } else {
+    y = at::empty({M, N}, res_out.options().dtype(at::kChar));
+    s = at::zeros({N / 64, 16}, res_out.options().dtype(at::kFloat));
+  }
+  const int r = edge_w8a8_gemv_ln(x.data_ptr(), residual ? residual->data_ptr() : nullptr, gamma.data_ptr(),
+                                  beta ? beta->data_ptr() : nullptr, (float)eps, res_out.data_ptr(), wp.data_ptr(),
+                                  sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr, y.data_ptr(),
+                                  s ? s->data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, (int)epi, stream());
+  if (r == -2) return std::nullopt;
+  check(r, "w8a8_gemv_ln");
+  return std::make_tuple(y, s);
+}
+
 // gate_up projection (16-blocked rows) fused with silu(g) * u: returns bf16 h [M, N/2].
 at::Tensor w8a8_gemm_glu(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& wp, const at::Tensor& sw,
                          const std::optional<at::Tensor>& bias, int64_t N, int64_t K) {
@@ -1287,6 +1331,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("llmint8_outlier", &llmint8_outlier, "LLM.int8 decode outlier part, added in place");
   m.def("gemv_bf16_norm", &gemv_bf16_norm, "16-bit decode GEMV with the RMSNorm in its prologue (M <= 4)");
   m.def("gemv_bf16_ln", &gemv_bf16_ln, "16-bit decode GEMV with the LayerNorm in its prologue (M <= 4)");
+  m.def("w8a8_gemv_ln", &w8a8_gemv_ln, "W8A8 decode GEMV with the LayerNorm + int8 quant in its prologue (M <= 4)");
   m.def("llmint8_prep_rows", &llmint8_prep_rows, "LLM.int8 preparation for any rows (uncapped, on the device)");
   m.def("llmint8_outlier_rows", &llmint8_outlier_rows, "LLM.int8 outlier part for any rows, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");

@@ -291,6 +291,8 @@ struct NormIn {
   bf16_t* res_out;        // [M][K] residual out (must not alias res: other workgroups still read it)
   float eps;
   int S;
+  const bf16_t* x = nullptr;      // LN (NRM >= 64): [M][K] bf16 input rows, LayerNorm of x + res
+  const bf16_t* beta = nullptr;   // LN: [K] (may be null)
 };
 constexpr int NRM_ROWS = 4;
 
@@ -436,6 +438,128 @@ __device__ __forceinline__ void norm_prologue(const NormIn& na, int H, int M, in
   }
 }
 
+// LayerNorm prologue (NRM >= 64: the parallel-residual decoders, GPT-NeoX / Phi): the LayerNorm of
+// the bf16 rows x + residual, int8 per token, with norm_kernel<NCH, !RMS, HAS_RES, QUANT, !PART>'s
+// element layout, reduction order and roundings (bit-identical rows and scales).  Its loads issue
+// before the weight stream (ln_load), like the RMS form's.
+template <int NCH>
+struct LnRegs {
+  uint4 xv[NCH], rv[NCH], gv[NCH], bv[NCH];
+};
+
+template <int NCH>
+__device__ __forceinline__ void ln_load(const NormIn& na, int H, int M, LnRegs<NCH>& r) {
+  const int t = threadIdx.x & 255, row = threadIdx.x >> 8;
+  if (row < M) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = min((c * 256 + t) * 8, H - 8);
+      r.xv[c] = *reinterpret_cast<const uint4*>(na.x + (size_t)row * H + e);
+      r.rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + (size_t)row * H + e) : uint4{0u, 0u, 0u, 0u};
+      r.gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
+      r.bv[c] = na.beta != nullptr ? *reinterpret_cast<const uint4*>(na.beta + e) : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  asm volatile("" ::: "memory");                          // these loads issue before the weights
+}
+
+template <int NCH>
+__device__ __forceinline__ void ln_prologue(const NormIn& na, int H, int M, int8_t* aq, float* nsa, float* nred,
+                                            const LnRegs<NCH>& r) {
+  const int t = threadIdx.x & 255, row = threadIdx.x >> 8, w = t >> 6;
+  const bool act = row < M;
+  float v[NCH][8];
+  float sm = 0.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        unpack8(r.xv[c], v[c]);
+        float rr[8];
+        unpack8(r.rv[c], rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += rr[j];
+        const uint4 u = pack8(v[c]);                          // residual stream in bf16
+        if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + (size_t)row * H + e) = u;
+        unpack8(u, v[c]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm += v[c][j];
+    sm = wave_sum(sm);
+    if ((t & 63) == 0) nred[4 * row + w] = sm;
+  }
+  __syncthreads();
+  const float* gr = nred + 4 * (row < NRM_ROWS ? row : 0);
+  const float mean = ((((0.f + gr[0]) + gr[1]) + gr[2]) + gr[3]) / (float)H;
+  float ss = 0.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (e < H) ? v[c][j] - mean : 0.f;
+        ss += d * d;
+      }
+    }
+    ss = wave_sum(ss);
+  }
+  __syncthreads();
+  if (act && (t & 63) == 0) nred[4 * row + w] = ss;
+  __syncthreads();
+  const float rstd = rsqrtf(((((0.f + gr[0]) + gr[1]) + gr[2]) + gr[3]) / (float)H + na.eps);
+  __syncthreads();
+  float amax = 0.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        float wf[8], bf[8];
+        unpack8(r.gv[c], wf);
+        unpack8(r.bv[c], bf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (v[c][j] - mean) * rstd * wf[j] + bf[j];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[c][j]));
+    amax = wave_max(amax);
+    if ((t & 63) == 0) nred[4 * row + w] = amax;
+  }
+  __syncthreads();
+  float gm = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gm = fmaxf(gm, gr[i]);
+  gm = fmaxf(gm, 1e-8f);
+  const float inv = 127.f / gm;
+  if (act && t == 0) nsa[row] = gm / 127.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lo |= ((uint32_t)(uint8_t)quant_i8(v[c][j], inv)) << (8 * j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hi |= ((uint32_t)(uint8_t)quant_i8(v[c][4 + j], inv)) << (8 * j);
+        *reinterpret_cast<uint2*>(aq + (size_t)row * H + e) = make_uint2(lo, hi);
+      }
+    }
+  }
+  __syncthreads();                                        // aq complete
+}
+
 template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI, int NRM = 0>
 __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                  const int8_t* __restrict__ Wp, const float* __restrict__ sw,
@@ -447,7 +571,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   static_assert(NRM == 0 || (MB == 1 && AMODE == A_TOKEN && EPI != EPI_PART && NW == 16), "norm prologue: batch 1");
   // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
   // NRM = 8 * NCH + SMAX (norm_prologue<NCH, SMAX>)
-  constexpr int NCH_N = NRM / 8, SMAX_N = NRM % 8;
+  constexpr bool LN_N = NRM >= 64;                           // LayerNorm of bf16 rows (+ 64)
+  constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N ? 1 : NRM % 8;
   __shared__ int8_t aq_l[NRM > 0 ? NRM_ROWS * NCH_N * 2048 : 16];
   __shared__ float nsa[16], nred[16];
   constexpr bool GELUQ = EPI == EPI_GELUQT || EPI == EPI_GELUQE;
@@ -526,12 +651,21 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     issue_a(st, kbase);
   };
   // NRM: the first step's weight loads go out before the norm prologue; its activations after
-  NormRegs<(NRM > 0 ? NCH_N : 1), (NRM > 0 ? SMAX_N : 1)> nr;
+  NormRegs<(NRM > 0 && !LN_N ? NCH_N : 1), (NRM > 0 && !LN_N ? SMAX_N : 1)> nr;
+  LnRegs<(LN_N ? NCH_N : 1)> lr;
+  auto nload = [&]() {
+    if constexpr (LN_N) ln_load(na, K, M, lr);
+    else norm_load(na, K, M, nr);
+  };
+  auto nprologue = [&]() {
+    if constexpr (LN_N) ln_prologue(na, K, M, aq_l, nsa, nred, lr);
+    else norm_prologue(na, K, M, aq_l, nsa, nred, nr);
+  };
   auto first = [&](Step& st, int kbase) {
     if constexpr (NRM > 0) {
-      norm_load(na, K, M, nr);
+      nload();
       issue_w(st, kbase);
-      norm_prologue(na, K, M, aq_l, nsa, nred, nr);
+      nprologue();
       issue_a(st, kbase);
     } else {
       issue(st, kbase);
@@ -561,10 +695,10 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4) {
       // batch-1 norm prologue: every step's weights (at most 2) in flight across it (K = 4096 with
       // 4 slices keeps one step: its prologue registers would spill)
-      norm_load(na, K, M, nr);
+      nload();
 #pragma unroll
       for (int i = 0; i < STEPS; ++i) issue_w(st[i], kbeg + kw + i * KW * U);
-      norm_prologue(na, K, M, aq_l, nsa, nred, nr);
+      nprologue();
 #pragma unroll
       for (int i = 0; i < STEPS; ++i) {
         issue_a(st[i], kbeg + kw + i * KW * U);
@@ -1626,6 +1760,33 @@ extern "C" int edge_w8a8_gemv_norm(const float* part, int S, const void* res, co
     NRM_L(8, 2, 8, EPI_GLUQ, os);
   }
 #undef NRM_L
+  return -2;
+}
+
+// Decode GEMV (M <= 4 rows) whose activation rows are LayerNorm(x + res) of bf16 rows x, int8 per
+// token, computed in the kernel's prologue (ln_prologue; the parallel-residual decoders).  epi 0
+// (EPI_OUT: bf16 [M, N]) or EPI_GELUQT / EPI_GELUQE (gelu of the bf16 output, int8 per (token, 64
+// columns), `os` scales [N/64][16]).  K % 64 == 0, K <= 4096; res may be null; res_out written by
+// workgroup 0.  -2: not taken.
+extern "C" int edge_w8a8_gemv_ln(const void* x, const void* res, const void* gamma, const void* beta, float eps,
+                                 void* res_out, const void* Wp, const float* sw, const void* bias, void* out,
+                                 float* os, int M, int N, int K, int epi, hipStream_t st) {
+  if (!g_gemv_norm || M < 1 || M > NRM_ROWS || K % 64 != 0 || K > 4096 || N % 16 != 0 || res_out == nullptr ||
+      res == res_out || x == res_out || x == nullptr)
+    return -2;
+  NormIn na{nullptr, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, 0};
+  na.x = (const bf16_t*)x;
+  na.beta = (const bf16_t*)beta;
+#define LN_L(NTW, TG, KW, EP, OS)                                                                   \
+  return K <= 2048 ? launch_norm<NTW, TG, KW, EP, 64 + 8>(na, Wp, sw, bias, out, OS, M, N, K, st)  \
+                   : launch_norm<NTW, TG, KW, EP, 64 + 16>(na, Wp, sw, bias, out, OS, M, N, K, st)
+  if (epi == EPI_OUT) LN_L(3, 1, 16, EPI_OUT, nullptr);
+  if (epi == EPI_GELUQT || epi == EPI_GELUQE) {
+    if (N % 64 != 0 || os == nullptr) return -2;
+    if (epi == EPI_GELUQT) LN_L(4, 1, 16, EPI_GELUQT, os);
+    LN_L(4, 1, 16, EPI_GELUQE, os);
+  }
+#undef LN_L
   return -2;
 }
 

@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops import _ref
-from ..models.layers import GroupQuantBF16, Linear, PartialSum, PendingNorm, QAct
+from ..models.layers import GroupQuantBF16, Linear, PartialSum, PendingLN, PendingNorm, QAct
 
 # Decode MLP policy (A/B on MI355X, Llama-2-7B, profiles/bench_ops_r1_gemv16.json): the gate_up
 # GEMV quantises silu(g) * u in its own epilogue (8 tiles = 64 features per workgroup) for every
@@ -129,6 +129,14 @@ class W8A8Linear(nn.Module):
             if y is not None:
                 return y
             x = QAct(ops.unpack_a(x.q, M, K), x.scale)      # (a consumer that cannot take it)
+        if isinstance(x, PendingLN):                  # batch 1: the LayerNorm in this GEMV's prologue
+            y = None
+            if add is None and not self.split_k_out:
+                y = ops.w8a8_gemv_ln(x.x, x.residual, x.weight, x.bias, x.eps, x.h, self.w_packed, self.w_scale,
+                                     self.bias, self.out_features, self.in_features)
+            if y is not None:
+                return y
+            x = x.materialize()
         if isinstance(x, PendingNorm):                # batch 1: the norm runs in this GEMV's prologue
             y = None
             if add is None and not self.split_k_out:
@@ -198,9 +206,23 @@ class W8A8Linear(nn.Module):
         """Whether the fused up projection + GELU + grouped int8 quant takes M rows (GPU <= 64)."""
         return M <= 64 and self.out_features % 64 == 0 and not self.glu_blocked
 
+    def pending_ln_ok(self, geluq: bool = False) -> bool:
+        """Whether this projection's batch-1 GEMV can take a PendingLN (LayerNorm + int8 quant of bf16
+        rows in its prologue; geluq: as the quantising GELU up projection)."""
+        ok = self.w_packed.is_cuda and ops.gpu_path(self.w_packed) and not self.split_k_out \
+            and not self.glu_blocked and self.in_features <= 4096 and self.in_features % 64 == 0
+        return ok and self.out_features % (64 if geluq else 16) == 0
+
     def geluq(self, x: QAct, act: str) -> QAct:
-        """GELU MLP front half in one launch (ops.w8a8_geluq): int8 h per (token, 64 columns)."""
+        """GELU MLP front half in one launch (ops.w8a8_geluq): int8 h per (token, 64 columns).  A
+        PendingLN input (batch 1) is normalised and quantised in the same kernel's prologue."""
         K, N = self.in_features, self.out_features
+        if isinstance(x, PendingLN):
+            r = ops.w8a8_gemv_ln(x.x, x.residual, x.weight, x.bias, x.eps, x.h, self.w_packed, self.w_scale,
+                                 self.bias, N, K, geluq=act)
+            if r is not None:
+                return QAct(*r)
+            x = x.materialize()
         q, s = ops.w8a8_geluq(x.q.reshape(-1, K), x.scale.reshape(-1), self.w_packed, self.w_scale, self.bias, N, K,
                               act, w_ref=self._wref(x.q))
         return QAct(q, s)

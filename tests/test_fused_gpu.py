@@ -667,6 +667,57 @@ def test_parallel_residual_decode_ln_fused_matches_unfused(cuda, arch, dt):
     assert outs[0] == outs[1]
 
 
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("K,N", [(2048, 6144), (2048, 8192), (2560, 10240), (4096, 4096)])
+@pytest.mark.parametrize("geluq", [None, "gelu_tanh", "gelu"])
+@pytest.mark.parametrize("res", [True, False])
+def test_w8a8_gemv_ln_prologue_exact(cuda, M, K, N, geluq, res):
+    """W8A8 decode GEMV with LayerNorm + per-token int8 of bf16 rows in its prologue (gemm_i8.hip
+    ln_prologue) == layer_norm_quant followed by the plain / quantising-GELU GEMV, bit for bit."""
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    resid = torch.randn(M, K, device=cuda).bfloat16() if res else None
+    gamma = (torch.rand(K, device=cuda) + 0.5).bfloat16()
+    beta = (torch.randn(K, device=cuda) * 0.1).bfloat16()
+    w = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=cuda)
+    sw = torch.rand(N, device=cuda) * 0.01 + 1e-3
+    bias = (torch.randn(N, device=cuda) * 0.1).bfloat16()
+    wp = ops.pack_int8_weight(w)
+    h = torch.empty(M, K, device=cuda, dtype=torch.bfloat16)
+    r = ops.w8a8_gemv_ln(x, resid, gamma, beta, 1e-5, h, wp, sw, bias, N, K, geluq=geluq)
+    assert r is not None
+    q, s, hr = ops.layer_norm_quant(x, gamma, beta, 1e-5, resid)
+    assert torch.equal(h, hr.view_as(h)), "residual rows differ"
+    if geluq is None:
+        ref = ops.w8a8_linear(q, s, wp, sw, bias, N, K)
+        assert torch.equal(r, ref), (r.float() - ref.float()).abs().max()
+    else:
+        qr, sr = ops.w8a8_geluq(q, s, wp, sw, bias, N, K, geluq)
+        assert torch.equal(r[0], qr)
+        assert torch.equal(r[1][:, :M], sr[:, :M])
+
+
+def test_neox_w8a8_decode_ln_fused_matches_unfused(cuda):
+    """A GPT-NeoX-like W8A8 model generates the same greedy tokens at batch 1 with its two
+    LayerNorms (+ int8 quant) in the qkv / up GEMV prologues as with the norm kernels."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.quant import quantize_model
+    cfg = tiny("gpt_neox", hidden_size=256, num_heads=4, num_kv_heads=4, head_dim=64, intermediate_size=1024,
+               rotary_dim=32, num_layers=3)
+    sp = SamplingParams(max_new_tokens=12, do_sample=False)
+    C = ops.ext()
+    outs = []
+    for on in (1, 0):
+        C.tune("gemv_norm", on, 0)
+        try:
+            m = quantize_model(build_model(cfg, device=cuda, seed=11), "w8a8_smoothquant")
+            outs.append(Generator(m, max_batch=1, max_seq=64).generate([[1, 5, 9, 13, 2, 7]], sp, seed=0).tokens)
+        finally:
+            C.tune("gemv_norm", 1, 0)
+    assert outs[0] == outs[1]
+
+
 def test_bf16_llama_decode_norm_fused_matches_unfused(cuda):
     """A bf16 Llama (hidden 2048: the prologue's K) generates the same greedy tokens at batch 1
     with its RMSNorms in the qkv / gate_up GEMV prologues as with the norm kernels (gemv_norm 0),
