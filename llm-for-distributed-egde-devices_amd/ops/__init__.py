@@ -101,9 +101,11 @@ def unpack_a(q_packed, M: int, K: int):
     return t.permute(0, 3, 1, 2, 4).reshape(256, K)[:M].contiguous()
 
 
-# rows up to which decode norms move into the next GEMV's prologue (kernel: <= 4).  Measured on
-# Llama-2-7B W8A8: batch 1 p50 2.10 -> 1.96 ms; 4 rows 2.167 -> 2.179 ms (slower), so 1 by default
-NORM_FUSE_MAX_ROWS = int(os.environ.get("EDGELLM_NORM_FUSE_ROWS", "1"))
+# rows up to which decode norms move into the next GEMV's prologue (kernel: <= 4).  Round 4 (the
+# prologue's loads queued behind the weights): batch 1 2.10 -> 1.96 ms, 4 rows 2.167 -> 2.179 ms
+# (slower), so 1.  Round 6 (prologue loads first, profiles/norm_fuse_rows_ab_r6.jsonl): Llama-2-7B
+# W8A8 2 rows 2.108 -> 1.919 ms, 4 rows 2.155 -> 2.097; Llama-3.2-1B bf16 4 rows 0.811 -> 0.758: 4.
+NORM_FUSE_MAX_ROWS = int(os.environ.get("EDGELLM_NORM_FUSE_ROWS", "4"))
 
 
 def gemv_norm_ok(parts) -> bool:
