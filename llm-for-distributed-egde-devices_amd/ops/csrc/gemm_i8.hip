@@ -293,8 +293,12 @@ struct NormIn {
   int S;
   const bf16_t* x = nullptr;      // LN (NRM >= 64): [M][K] bf16 input rows, LayerNorm of x + res
   const bf16_t* beta = nullptr;   // LN: [K] (may be null)
+  float thr = 0.f;                // LLM.int8 (NRM >= 128): outlier threshold on |x|
+  const int8_t* wt = nullptr;     // LLM.int8: int8 W^T [K][N] (an outlier column is one row)
+  const float* scb = nullptr;     // LLM.int8: per-row weight absmax SCB [N]
 };
 constexpr int NRM_ROWS = 4;
+constexpr int L8_CMAX = 256;      // LLM.int8 outlier columns per row held in LDS (llmint8.hip's cap)
 
 // The prologue's global loads (slices, residual, gamma) are issued by norm_load BEFORE the
 // weight stream and consumed by norm_prologue after it is issued: a wave's loads retire in issue
@@ -560,6 +564,119 @@ __device__ __forceinline__ void ln_prologue(const NormIn& na, int H, int M, int8
   __syncthreads();                                        // aq complete
 }
 
+// LLM.int8 prologue (NRM >= 128, one row): llmint8.hip's decode preparation inside the GEMV, so a
+// batch-1 LLM.int8 projection is one launch instead of three (prep, GEMV, outlier add).  Threads
+// 0-255 hold the row in norm_prologue's layout (column (c 256 + t) 8 + j); columns with |x| > thr
+// are ranked in column order by a block prefix sum per chunk, the first L8_CMAX go to LDS (index,
+// value); the per-token absmax over the other columns, then int8 x with the taken columns zeroed.
+// The epilogue adds sum_j x[c_j] W^T[c_j][n] SCB[n] / 127 to the rounded output, in llmint8.hip's
+// order and roundings: the output bits equal prep + GEMV + outlier kernel.
+template <int NCH>
+struct L8Regs {
+  uint4 xv[NCH];
+};
+
+template <int NCH>
+__device__ __forceinline__ void l8_load(const NormIn& na, int H, L8Regs<NCH>& r) {
+  const int t = threadIdx.x;
+  if (t < 256) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) r.xv[c] = *reinterpret_cast<const uint4*>(na.x + min((c * 256 + t) * 8, H - 8));
+  }
+  asm volatile("" ::: "memory");                          // these loads issue before the weights
+}
+
+template <int NCH>
+__device__ __forceinline__ void l8_prologue(const NormIn& na, int H, int8_t* aq, float* nsa, float* nred, int* cols,
+                                            float* xo, int* scr, const L8Regs<NCH>& r) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const bool act = t < 256;
+  float v[NCH][8];
+  uint32_t take[NCH];
+  int base = 0;                                           // outliers in the chunks before c
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 256 + (act ? t : 0)) * 8;
+    uint32_t bits = 0;
+    if (act) {
+      unpack8(r.xv[c], v[c]);
+      if (e < H) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bits |= (fabsf(v[c][j]) > na.thr ? 1u : 0u) << j;
+      }
+    }
+    const int pc = __popc(bits);
+    int incl = pc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int tt = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += tt;
+    }
+    if (act && lane == 63) scr[w] = incl;                 // wave totals of this chunk
+    __syncthreads();
+    int wb = base;
+    if (act) {
+      for (int i = 0; i < w; ++i) wb += scr[i];
+    }
+    const int tot = scr[0] + scr[1] + scr[2] + scr[3];
+    __syncthreads();                                      // scr reused by the next chunk
+    uint32_t tk = 0;
+    if (act) {
+      int slot = wb + incl - pc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {                       // (static indices: v stays in registers)
+        if ((bits >> j) & 1u) {
+          if (slot < L8_CMAX) {
+            cols[slot] = e + j;
+            xo[slot] = v[c][j];
+            tk |= 1u << j;
+          }
+          ++slot;
+        }
+      }
+    }
+    take[c] = tk;
+    base += tot;
+  }
+  if (t == 0) scr[8] = min(base, L8_CMAX);
+  float am = 0.f;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!((take[c] >> j) & 1u)) am = fmaxf(am, fabsf(v[c][j]));
+      }
+    }
+    am = wave_max(am);
+    if (lane == 0) nred[w] = am;
+  }
+  __syncthreads();
+  const float rm = fmaxf(fmaxf(fmaxf(fmaxf(0.f, nred[0]), nred[1]), nred[2]), nred[3]);
+  const float gm = fmaxf(rm, 1e-8f);
+  if (t == 0) nsa[0] = gm / 127.f;
+  const float inv = 127.f / gm;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int e = (c * 256 + t) * 8;
+      if (e < H) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          lo |= ((uint32_t)(uint8_t)((take[c] >> j) & 1u ? 0 : quant_i8(v[c][j], inv))) << (8 * j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          hi |= ((uint32_t)(uint8_t)((take[c] >> (4 + j)) & 1u ? 0 : quant_i8(v[c][4 + j], inv))) << (8 * j);
+        *reinterpret_cast<uint2*>(aq + e) = make_uint2(lo, hi);
+      }
+    }
+  }
+  __syncthreads();                                        // aq, cols, xo, the count complete
+}
+
 template <int MB, int NTW, int TG, int KW, int U, int AMODE, int EPI, int NRM = 0>
 __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
                                                                  const int8_t* __restrict__ Wp, const float* __restrict__ sw,
@@ -571,8 +688,13 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   static_assert(NRM == 0 || (MB == 1 && AMODE == A_TOKEN && EPI != EPI_PART && NW == 16), "norm prologue: batch 1");
   // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
   // NRM = 8 * NCH + SMAX (norm_prologue<NCH, SMAX>)
-  constexpr bool LN_N = NRM >= 64;                           // LayerNorm of bf16 rows (+ 64)
-  constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N ? 1 : NRM % 8;
+  constexpr bool L8_N = NRM >= 128;                          // LLM.int8 preparation (+ 128)
+  constexpr bool LN_N = NRM >= 64 && !L8_N;                  // LayerNorm of bf16 rows (+ 64)
+  constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N || L8_N ? 1 : NRM % 8;
+  static_assert(!L8_N || (EPI == EPI_OUT && MB == 1), "LLM.int8 prologue: one row, plain output");
+  __shared__ int l8_cols[L8_N ? L8_CMAX : 1];
+  __shared__ float l8_xo[L8_N ? L8_CMAX : 1];
+  __shared__ int l8_scr[16];
   __shared__ int8_t aq_l[NRM > 0 ? NRM_ROWS * NCH_N * 2048 : 16];
   __shared__ float nsa[16], nred[16];
   constexpr bool GELUQ = EPI == EPI_GELUQT || EPI == EPI_GELUQE;
@@ -651,14 +773,17 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     issue_a(st, kbase);
   };
   // NRM: the first step's weight loads go out before the norm prologue; its activations after
-  NormRegs<(NRM > 0 && !LN_N ? NCH_N : 1), (NRM > 0 && !LN_N ? SMAX_N : 1)> nr;
+  NormRegs<(NRM > 0 && !LN_N && !L8_N ? NCH_N : 1), (NRM > 0 && !LN_N && !L8_N ? SMAX_N : 1)> nr;
   LnRegs<(LN_N ? NCH_N : 1)> lr;
+  L8Regs<(L8_N ? NCH_N : 1)> l8r;
   auto nload = [&]() {
-    if constexpr (LN_N) ln_load(na, K, M, lr);
+    if constexpr (L8_N) l8_load(na, K, l8r);
+    else if constexpr (LN_N) ln_load(na, K, M, lr);
     else norm_load(na, K, M, nr);
   };
   auto nprologue = [&]() {
-    if constexpr (LN_N) ln_prologue(na, K, M, aq_l, nsa, nred, lr);
+    if constexpr (L8_N) l8_prologue(na, K, aq_l, nsa, nred, l8_cols, l8_xo, l8_scr, l8r);
+    else if constexpr (LN_N) ln_prologue(na, K, M, aq_l, nsa, nred, lr);
     else norm_prologue(na, K, M, aq_l, nsa, nred, nr);
   };
   auto first = [&](Step& st, int kbase) {
@@ -782,8 +907,32 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     }
     __syncthreads();
   }
-  gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI>(&red[0][0][0], NRM > 0 ? nsa : sa, pre, outv, os, gmax, M, N, NTt, Mpad,
-                                              nt0, wave, lane, ks);
+  if constexpr (L8_N) {
+    // row 0 of each tile (lanes 0-15, q = 0): the int8 part as the EPI_OUT epilogue rounds it, then
+    // the outlier columns' 16-bit part (llmint8.hip llmint8_outlier_kernel's sum order and rounding)
+    if (wave < NTW && lane < 16 && nt0 + wave < NTt) {
+      const v4i* rb = &red[0][0][0];
+      int tot = rb[wave * 64 + lane][0];
+#pragma unroll
+      for (int w = 1; w < KR; ++w) tot += rb[(w * NTW + wave) * 64 + lane][0];
+      const int col = (nt0 + wave) * 16 + lane;
+      if (col < N) {
+        float y = (float)tot * nsa[0];
+        y = y * pre.s0[0] + pre.b0[0];
+        const int nt = l8_scr[8];
+        if (nt > 0) {
+          float a = 0.f;
+          for (int j = 0; j < nt; ++j) a += l8_xo[j] * (float)na.wt[(size_t)l8_cols[j] * N + col];
+          const float s = na.scb[col] / 127.f;
+          y = bf2f(f2bf(y)) + a * s;
+        }
+        reinterpret_cast<bf16_t*>(outv)[col] = f2bf(y);
+      }
+    }
+  } else {
+    gemv_epilogue<MB, NTW, NW, KR, SCALED, EPI>(&red[0][0][0], NRM > 0 ? nsa : sa, pre, outv, os, gmax, M, N, NTt,
+                                                Mpad, nt0, wave, lane, ks);
+  }
 }
 
 // ------------------------------------------------------------------------------------ ring2
@@ -1788,6 +1937,22 @@ extern "C" int edge_w8a8_gemv_ln(const void* x, const void* res, const void* gam
   }
 #undef LN_L
   return -2;
+}
+
+// LLM.int8 projection of one bf16 row in one launch (l8_prologue): out bf16 [1, N] = int8 GEMV of x
+// with its outlier columns (|x| > thr, the first 256 in column order) zeroed, per-token scale, sw =
+// SCB / 127 (+ bias), plus the outlier columns' part from wt = int8 W^T [K, N].  K % 64 == 0,
+// K <= 4096.  -2: not taken.
+extern "C" int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const float* sw, const void* bias,
+                                 const void* wt, const float* scb, void* out, int N, int K, hipStream_t st) {
+  if (K % 64 != 0 || K > 4096 || K < 64 || N % 16 != 0) return -2;
+  NormIn na{nullptr, nullptr, nullptr, nullptr, 0.f, 0};
+  na.x = (const bf16_t*)x;
+  na.thr = thr;
+  na.wt = (const int8_t*)wt;
+  na.scb = scb;
+  return K <= 2048 ? launch_norm<3, 1, 16, EPI_OUT, 128 + 8>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                   : launch_norm<3, 1, 16, EPI_OUT, 128 + 16>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
 }
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).

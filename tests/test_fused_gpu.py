@@ -478,6 +478,31 @@ def test_llmint8_device_outliers(cuda, M, K, N, outliers):
     assert rel < 2e-2, rel
 
 
+@pytest.mark.parametrize("K,N", [(2048, 3072), (2560, 10240), (4096, 4096), (2048, 16384)])
+@pytest.mark.parametrize("outliers", [0, 3, 40, 300])
+@pytest.mark.parametrize("bias", [True, False])
+def test_llmint8_one_launch_exact(cuda, K, N, outliers, bias):
+    """Batch-1 LLM.int8 in one launch (gemm_i8.hip l8_prologue: outlier columns, quantisation and the
+    outlier part inside the GEMV) == the three-launch decode path (llmint8_prep, the int8 GEMV,
+    llmint8_outlier), bit for bit, including past the 256-column cap."""
+    from edgellm.models.layers import Linear
+    from edgellm.quant import LLMInt8Linear
+    torch.manual_seed(K + N + outliers)
+    lin = Linear(K, N, bias=bias, device=cuda)
+    lin.weight.data.copy_(torch.randn(N, K, device=cuda) * 0.02)
+    if bias:
+        lin.bias.data.copy_(torch.randn(N, device=cuda) * 0.1)
+    m = LLMInt8Linear.from_float(lin)
+    x = torch.randn(1, K, device=cuda)
+    if outliers:
+        x[0, torch.randperm(K, device=cuda)[:outliers]] = 7.0 + torch.rand(outliers, device=cuda) * 4
+    x = x.bfloat16()
+    one = m(x)                                             # one launch (ONE_LAUNCH)
+    m.ONE_LAUNCH = False
+    three = m(x)                                           # prep + GEMV + outlier
+    assert torch.equal(one, three), (one.float() - three.float()).abs().max()
+
+
 def _llmint8_emulation(x, q_w, scb, bias, thr):
     """fp32 emulation of the bitsandbytes split: columns with any |x| > thr in 16-bit against the
     dequantised weight columns, the rest per-token int8 x per-row int8."""
