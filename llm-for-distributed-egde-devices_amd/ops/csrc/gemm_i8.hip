@@ -817,7 +817,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto fixed = [&](auto nk) {
     constexpr int NK = decltype(nk)::value, STEPS = (NK + KW * U - 1) / (KW * U);
     Step st[STEPS];
-    if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4) {
+    if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4 && (!L8_N || NCH_N <= 2)) {
       // batch-1 norm prologue: every step's weights (at most 2) in flight across it (K = 4096 with
       // 4 slices keeps one step: its prologue registers would spill)
       nload();
@@ -1942,17 +1942,23 @@ extern "C" int edge_w8a8_gemv_ln(const void* x, const void* res, const void* gam
 // LLM.int8 projection of one bf16 row in one launch (l8_prologue): out bf16 [1, N] = int8 GEMV of x
 // with its outlier columns (|x| > thr, the first 256 in column order) zeroed, per-token scale, sw =
 // SCB / 127 (+ bias), plus the outlier columns' part from wt = int8 W^T [K, N].  K % 64 == 0,
-// K <= 4096.  -2: not taken.
+// K <= 12288.  -2: not taken.
 extern "C" int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const float* sw, const void* bias,
                                  const void* wt, const float* scb, void* out, int N, int K, hipStream_t st) {
-  if (K % 64 != 0 || K > 4096 || K < 64 || N % 16 != 0) return -2;
+  if (K % 64 != 0 || K > 12288 || K < 64 || N % 16 != 0) return -2;
   NormIn na{nullptr, nullptr, nullptr, nullptr, 0.f, 0};
   na.x = (const bf16_t*)x;
   na.thr = thr;
   na.wt = (const int8_t*)wt;
   na.scb = scb;
-  return K <= 2048 ? launch_norm<3, 1, 16, EPI_OUT, 128 + 8>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
-                   : launch_norm<3, 1, 16, EPI_OUT, 128 + 16>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+  switch ((K + 2047) / 2048) {                            // row chunks of 2048 per 256 threads
+    case 1: return launch_norm<3, 1, 16, EPI_OUT, 128 + 8>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    case 2: return launch_norm<3, 1, 16, EPI_OUT, 128 + 16>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    case 3: return launch_norm<3, 1, 16, EPI_OUT, 128 + 24>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    case 4: return launch_norm<3, 1, 16, EPI_OUT, 128 + 32>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    case 5: return launch_norm<3, 1, 16, EPI_OUT, 128 + 40>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    default: return launch_norm<3, 1, 16, EPI_OUT, 128 + 48>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+  }
 }
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).

@@ -237,7 +237,7 @@ class LLMInt8Linear(nn.Module):
     OUTLIER_CAP = 256    # ... on GPU ops/csrc/llmint8.hip finds the columns on the device: decode rows
     #                      (<= 16, one fused kernel, at most 256 columns) and any rows (uncapped)
     DECODE_ROWS = 16
-    ONE_LAUNCH = True    # batch 1: ops/csrc/gemm_i8.hip l8_prologue (one launch per projection, K <= 4096)
+    ONE_LAUNCH = True    # batch 1: ops/csrc/gemm_i8.hip l8_prologue (one launch per projection, K <= 12288)
 
     def _device_ok(self) -> bool:
         K = self.in_features
@@ -300,7 +300,7 @@ class LLMInt8Linear(nn.Module):
                 self._weight_t = self.weight_i8.t().contiguous()          # W^T: outlier columns as rows
                 self._w_deq = self.SCB / 127.0
             x2 = x2.contiguous()
-            if x2.shape[0] == 1 and K <= 4096 and K % 64 == 0 and self.ONE_LAUNCH:
+            if x2.shape[0] == 1 and K <= 12288 and K % 64 == 0 and self.ONE_LAUNCH:
                 # batch 1: outlier discovery, quantisation and the outlier part inside the GEMV
                 out = C.llmint8_gemv(x2, self.threshold, self.w_packed, self._w_deq, self.bias, self._weight_t,
                                      self.SCB, N)

@@ -478,7 +478,8 @@ def test_llmint8_device_outliers(cuda, M, K, N, outliers):
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("K,N", [(2048, 3072), (2560, 10240), (4096, 4096), (2048, 16384)])
+@pytest.mark.parametrize("K,N", [(2048, 3072), (2560, 10240), (4096, 4096), (2048, 16384), (8192, 2048),
+                                 (10240, 2560), (11008, 4096)])
 @pytest.mark.parametrize("outliers", [0, 3, 40, 300])
 @pytest.mark.parametrize("bias", [True, False])
 def test_llmint8_one_launch_exact(cuda, K, N, outliers, bias):
