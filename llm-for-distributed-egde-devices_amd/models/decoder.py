@@ -173,7 +173,11 @@ class MLP(nn.Module):
                 return self.down(self.up.forward_ln(x, act=self.act), add=add)     # 16-bit up + GELU
             if x.quant and self.act in ("gelu_tanh", "gelu") and hasattr(self.up, "geluq"):
                 return self.down(self.up.geluq(x, self.act), add=add)              # W8A8 up + GELU + quant
-            x = x.materialize()
+            if not getattr(self.up, "takes_pending_x", False):
+                x = x.materialize()
+            else:                                      # LLM.int8: the norm in the up projection's prologue
+                return self.down(act_fn(self.up(x), self.act, getattr(self.down, "takes_quantized_input", False)),
+                                 add=add)
         if isinstance(x, PendingNorm):
             if getattr(self.up, "glu_blocked", False):     # batch 1: norm in the gate_up prologue
                 return self.down(self.up.glu(x), add=add)
@@ -254,6 +258,16 @@ class DecoderLayer(nn.Module):
                 and _ln_consumer_ok(self.attn.qkv) and _ln_consumer_ok(self.mlp.up)
                 and x.dtype == self.norm1.weight.dtype)
 
+    def _ln_deferred_l8(self, x, qa: bool, qm: bool) -> bool:
+        """Parallel-residual LLM.int8 rows at batch 1 whose LayerNorm(s) the one-launch qkv / up
+        projections can compute."""
+        cfg = self.cfg
+        ok = lambda m: getattr(m, "takes_pending_x", False) and m.pending_ln_ok()
+        return (not qa and not qm and cfg.norm == "layer" and self.has_attn and self.has_mlp
+                and isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.bfloat16
+                and (cfg.shared_input_norm or self.norm2 is not None) and ops.gemv_ln_ok(x)
+                and self.norm1.weight.dtype == torch.bfloat16 and ok(self.attn.qkv) and ok(self.mlp.up))
+
     def _ln_deferred_w8a8(self, x, qa: bool, qm: bool) -> bool:
         """GPT-NeoX W8A8 decode rows whose two LayerNorms the qkv / up GEMVs can compute (Phi shares
         one norm between them, and only one prologue would take it: no gain, not taken)."""
@@ -291,6 +305,18 @@ class DecoderLayer(nn.Module):
             n1, n2, h = self.norm1, self.norm2, torch.empty_like(x)
             pa = PendingLN(x, residual, n1.weight, n1.bias, n1.eps, h, None, True)
             pm = PendingLN(x, residual, n2.weight, n2.bias, n2.eps, h, None, True)
+            return self.mlp(pm, add=self.attn(pa, ctx)), h
+        if self._ln_deferred_l8(x, qa, qm):
+            # LLM.int8 at batch 1: the LayerNorm(s) inside the one-launch qkv / up projections
+            n1, h = self.norm1, torch.empty_like(x)
+            if cfg.shared_input_norm:                  # phi: qkv also writes the normalised row for up
+                y = torch.empty_like(x)
+                pa = PendingLN(x, residual, n1.weight, n1.bias, n1.eps, h, y)
+                pm = y
+            else:
+                n2 = self.norm2
+                pa = PendingLN(x, residual, n1.weight, n1.bias, n1.eps, h)
+                pm = PendingLN(x, residual, n2.weight, n2.bias, n2.eps, h)
             return self.mlp(pm, add=self.attn(pa, ctx)), h
         if self._ln_deferred(x, qa, qm):
             # 16-bit decode at batch 1: each consumer computes the LayerNorm in its GEMV prologue
@@ -397,7 +423,8 @@ class DecoderLM(nn.Module):
         if first is None or not first.has_attn or first.norm1 is None or first.norm1.kind != "rms":
             return False
         qkv = first.attn.qkv
-        return bool(getattr(qkv, "pending_norm_ok", lambda glu=False: False)())
+        ok = getattr(qkv, "pending_norm_ok", lambda glu=False: False)()
+        return ok is not False and ok != "x" and bool(ok)     # ("x": a consumer of the bf16 row itself)
 
     def embed_tokens(self, ids: torch.Tensor, start_pos: torch.Tensor, decode: bool = False):
         """ids [B, T] -> hidden [B*T, H] (``decode`` at batch 1 with a deferrable first norm: a

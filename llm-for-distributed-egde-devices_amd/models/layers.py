@@ -76,8 +76,15 @@ class PendingLN(NamedTuple):
     h: torch.Tensor
     y: Optional[torch.Tensor] = None
     quant: bool = False              # the consumers are W8A8: int8 rows per token (QAct)
+    rms: bool = False                # RMSNorm (no bias) instead of LayerNorm (LLM.int8 consumers only)
 
     def materialize(self):
+        if self.rms:
+            y, r = ops.rms_norm(self.x, self.weight, self.eps, self.residual)
+            self.h.copy_(r.view_as(self.h))
+            if self.y is not None:
+                self.y.copy_(y.view_as(self.y))
+            return y
         if self.quant:
             q, s, r = ops.layer_norm_quant(self.x, self.weight, self.bias, self.eps, self.residual)
             self.h.copy_(r.view_as(self.h))
@@ -146,7 +153,7 @@ class Linear(nn.Module):
     def forward_ln(self, x: "PendingLN", act: Optional[str] = None):
         """The decode GEMV over a PendingLN (LayerNorm in the prologue); act: its GELU epilogue."""
         y = None
-        if self.pending_ln_ok() and x.x.dtype == self.weight.dtype:
+        if self.pending_ln_ok() and x.x.dtype == self.weight.dtype and not x.rms:
             y = ops.gemv_bf16_ln(x.x, x.residual, x.weight, x.bias, x.eps, x.h, self.packed_weight(), self.bias,
                                  self.out_features, act, y_out=x.y)
         if y is not None:
@@ -222,7 +229,12 @@ class Norm(nn.Module):
                 else:
                     y, s, r = ops.rms_norm_quant(x, self.weight, self.eps, residual, packed=True)
                 return QAct(y, s, True), r
-        if defer and isinstance(x, PartialSum) and self.kind == "rms" and ops.gemv_norm_ok(x.parts) \
+        if defer == "x" and not quant and isinstance(x, torch.Tensor) and self.kind == "rms" and x.dim() == 2 \
+                and x.shape[0] == 1 and ops.gemv_ln_ok(x) and x.dtype == torch.bfloat16:
+            # an LLM.int8 consumer at batch 1: the norm of the bf16 row x (+ residual) in its prologue
+            h = torch.empty_like(x)
+            return PendingLN(x, residual, self.weight, None, self.eps, h, rms=True), h
+        if defer and defer != "x" and isinstance(x, PartialSum) and self.kind == "rms" and ops.gemv_norm_ok(x.parts) \
                 and (quant or self.weight.dtype == x.dtype):
             # residual None: a stage's first norm, over the embedding as one fp32 slice; a 16-bit
             # consumer (not quant) takes the normalised rows in its own dtype

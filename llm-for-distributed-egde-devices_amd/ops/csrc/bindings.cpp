@@ -94,6 +94,9 @@ int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int*
                          const float* scb, int M, int N, int cmax, hipStream_t st);
 int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const float* sw, const void* bias, const void* wt,
                       const float* scb, void* out, int N, int K, hipStream_t st);
+int edge_llmint8_gemv_norm(const void* x, const void* res, const void* gamma, const void* beta, float eps, int ln,
+                           void* res_out, void* y_out, float thr, const void* Wp, const float* sw, const void* bias,
+                           const void* wt, const float* scb, void* out, int N, int K, hipStream_t st);
 int edge_llmint8_prep_rows(const void* x, int M, int K, float thr, void* q, float* sa, int* cols, int* count,
                            uint32_t* flags, uint32_t* take, hipStream_t st);
 int edge_llmint8_outlier_rows(void* out, const void* x, const int* cols, const int* count, const void* wt,
@@ -832,6 +835,43 @@ std::optional<at::Tensor> llmint8_gemv(const at::Tensor& x, double thr, const at
   return out;
 }
 
+// The same over RMSNorm (ln false) / LayerNorm (ln true) of x + residual computed first; res_out gets
+// x + residual, y_out (optional) the normalised row.
+std::optional<at::Tensor> llmint8_gemv_norm(const at::Tensor& x, const std::optional<at::Tensor>& residual,
+                                            const at::Tensor& gamma, const std::optional<at::Tensor>& beta,
+                                            double eps, bool ln, const at::Tensor& res_out,
+                                            const std::optional<at::Tensor>& y_out, double thr, const at::Tensor& wp,
+                                            const at::Tensor& sw, const std::optional<at::Tensor>& bias,
+                                            const at::Tensor& wt, const at::Tensor& scb, int64_t N) {
+  DEVICE_GUARD(x);
+  need(x, at::kBFloat16, "x");
+  need(gamma, at::kBFloat16, "gamma");
+  need(res_out, at::kBFloat16, "res_out");
+  need(wt, at::kChar, "weight_t");
+  need(scb, at::kFloat, "SCB");
+  TORCH_CHECK(x.dim() == 2 && x.size(0) == 1 && x.is_contiguous(), "x must be contiguous [1, K]");
+  const int64_t K = x.size(1);
+  check_w8a8_operands(wp, sw, bias, N, K);
+  TORCH_CHECK(wt.dim() == 2 && wt.size(0) == K && wt.size(1) == N && wt.is_contiguous() && scb.numel() == N,
+              "weight_t [K, N], SCB [N]");
+  TORCH_CHECK(gamma.numel() == K && res_out.numel() == K, "gamma [K], res_out [1, K]");
+  if (beta) { need(*beta, at::kBFloat16, "beta"); TORCH_CHECK(beta->numel() == K, "beta [K]"); }
+  if (residual) {
+    need(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->numel() == K && residual->data_ptr() != res_out.data_ptr(), "residual [1, K]");
+  }
+  if (y_out) { need(*y_out, at::kBFloat16, "y_out"); TORCH_CHECK(y_out->numel() == K, "y_out [1, K]"); }
+  auto out = at::empty({1, N}, x.options());
+  const int r = edge_llmint8_gemv_norm(x.data_ptr(), residual ? residual->data_ptr() : nullptr, gamma.data_ptr(),
+                                       beta ? beta->data_ptr() : nullptr, (float)eps, ln ? 1 : 0, res_out.data_ptr(),
+                                       y_out ? y_out->data_ptr() : nullptr, (float)thr, wp.data_ptr(),
+                                       sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr, wt.data_ptr(),
+                                       scb.data_ptr<float>(), out.data_ptr(), (int)N, (int)K, stream());
+  if (r == -2) return std::nullopt;
+  check(r, "llmint8_gemv_norm");
+  return out;
+}
+
 // LLM.int8 preparation for any number of rows, uncapped (every outlier column to the 16-bit part):
 // (q int8 [M, K] with the outlier columns zeroed, per-token scales [M], outlier columns [K] (first
 // `count`), count [1]).
@@ -1358,6 +1398,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv_bf16_ln", &gemv_bf16_ln, "16-bit decode GEMV with the LayerNorm in its prologue (M <= 4)");
   m.def("w8a8_gemv_ln", &w8a8_gemv_ln, "W8A8 decode GEMV with the LayerNorm + int8 quant in its prologue (M <= 4)");
   m.def("llmint8_gemv", &llmint8_gemv, "LLM.int8 projection of one row in one launch (prep in the GEMV prologue)");
+  m.def("llmint8_gemv_norm", &llmint8_gemv_norm, "LLM.int8 projection of RMSNorm / LayerNorm(x + residual), one launch");
   m.def("llmint8_prep_rows", &llmint8_prep_rows, "LLM.int8 preparation for any rows (uncapped, on the device)");
   m.def("llmint8_outlier_rows", &llmint8_outlier_rows, "LLM.int8 outlier part for any rows, added in place");
   m.def("gemv_bf16_splitk", &gemv_bf16_splitk, "bf16 decode GEMV, split-K fp32 partial slices");

@@ -296,6 +296,7 @@ struct NormIn {
   float thr = 0.f;                // LLM.int8 (NRM >= 128): outlier threshold on |x|
   const int8_t* wt = nullptr;     // LLM.int8: int8 W^T [K][N] (an outlier column is one row)
   const float* scb = nullptr;     // LLM.int8: per-row weight absmax SCB [N]
+  bf16_t* y_out = nullptr;        // LLM.int8 of a normed row: the normalised row too (may be null)
 };
 constexpr int NRM_ROWS = 4;
 constexpr int L8_CMAX = 256;      // LLM.int8 outlier columns per row held in LDS (llmint8.hip's cap)
@@ -571,27 +572,117 @@ __device__ __forceinline__ void ln_prologue(const NormIn& na, int H, int M, int8
 // value); the per-token absmax over the other columns, then int8 x with the taken columns zeroed.
 // The epilogue adds sum_j x[c_j] W^T[c_j][n] SCB[n] / 127 to the rounded output, in llmint8.hip's
 // order and roundings: the output bits equal prep + GEMV + outlier kernel.
-template <int NCH>
+// SRC 1 / 2 (NRM = 192 + 8 NCH + SRC): the row is first the RMSNorm / LayerNorm of x + residual
+// (norm_kernel's HAS_RES path, rounded to bf16 as its output), so an LLM.int8 layer's norm is no
+// launch of its own either; workgroup 0 writes the new residual row and, when y_out is set, the
+// normalised row (for a second consumer).
+template <int NCH, int SRC>
 struct L8Regs {
   uint4 xv[NCH];
+  uint4 rv[SRC ? NCH : 1], gv[SRC ? NCH : 1], bv[SRC == 2 ? NCH : 1];
 };
 
-template <int NCH>
-__device__ __forceinline__ void l8_load(const NormIn& na, int H, L8Regs<NCH>& r) {
+template <int NCH, int SRC>
+__device__ __forceinline__ void l8_load(const NormIn& na, int H, L8Regs<NCH, SRC>& r) {
   const int t = threadIdx.x;
   if (t < 256) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) r.xv[c] = *reinterpret_cast<const uint4*>(na.x + min((c * 256 + t) * 8, H - 8));
+    for (int c = 0; c < NCH; ++c) {
+      const int e = min((c * 256 + t) * 8, H - 8);
+      r.xv[c] = *reinterpret_cast<const uint4*>(na.x + e);
+      if constexpr (SRC > 0) {
+        r.rv[c] = na.res != nullptr ? *reinterpret_cast<const uint4*>(na.res + e) : uint4{0u, 0u, 0u, 0u};
+        r.gv[c] = *reinterpret_cast<const uint4*>(na.gamma + e);
+      }
+      if constexpr (SRC == 2)
+        r.bv[c] = na.beta != nullptr ? *reinterpret_cast<const uint4*>(na.beta + e) : uint4{0u, 0u, 0u, 0u};
+    }
   }
   asm volatile("" ::: "memory");                          // these loads issue before the weights
 }
 
-template <int NCH>
+template <int NCH, int SRC>
 __device__ __forceinline__ void l8_prologue(const NormIn& na, int H, int8_t* aq, float* nsa, float* nred, int* cols,
-                                            float* xo, int* scr, const L8Regs<NCH>& r) {
+                                            float* xo, int* scr, const L8Regs<NCH, SRC>& r, bf16_t* y_out) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const bool act = t < 256;
   float v[NCH][8];
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) unpack8(r.xv[c], v[c]);
+  }
+  if constexpr (SRC > 0) {
+    float sm = 0.f;
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
+        if (e < H) {
+          float rr[8];
+          unpack8(r.rv[c], rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += rr[j];
+          const uint4 u = pack8(v[c]);                      // residual stream in bf16
+          if (blockIdx.x == 0) *reinterpret_cast<uint4*>(na.res_out + e) = u;
+          unpack8(u, v[c]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+        }
+      }
+      if constexpr (SRC == 2) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sm += v[c][j];
+        sm = wave_sum(sm);
+        if (lane == 0) nred[w] = sm;
+      }
+    }
+    float mean = 0.f;
+    if constexpr (SRC == 2) {
+      __syncthreads();
+      mean = ((((0.f + nred[0]) + nred[1]) + nred[2]) + nred[3]) / (float)H;
+      __syncthreads();
+    }
+    float ss = 0.f;
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (e < H) ? v[c][j] - mean : 0.f;
+          ss += d * d;
+        }
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) nred[w] = ss;
+    }
+    __syncthreads();
+    const float rstd = rsqrtf(((((0.f + nred[0]) + nred[1]) + nred[2]) + nred[3]) / (float)H + na.eps);
+    __syncthreads();                                      // nred is reused below
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int e = (c * 256 + t) * 8;
+        if (e < H) {
+          float wf[8], bf[8];
+          unpack8(r.gv[c], wf);
+          if constexpr (SRC == 2) unpack8(r.bv[c], bf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float tv = (v[c][j] - mean) * rstd * wf[j];
+            if constexpr (SRC == 2) tv += bf[j];
+            v[c][j] = tv;
+          }
+          const uint4 u = pack8(v[c]);                      // the norm's bf16 output row
+          if (y_out != nullptr && blockIdx.x == 0) *reinterpret_cast<uint4*>(y_out + e) = u;
+          unpack8(u, v[c]);
+        }
+      }
+    }
+  }
   uint32_t take[NCH];
   int base = 0;                                           // outliers in the chunks before c
 #pragma unroll
@@ -599,7 +690,6 @@ __device__ __forceinline__ void l8_prologue(const NormIn& na, int H, int8_t* aq,
     const int e = (c * 256 + (act ? t : 0)) * 8;
     uint32_t bits = 0;
     if (act) {
-      unpack8(r.xv[c], v[c]);
       if (e < H) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bits |= (fabsf(v[c][j]) > na.thr ? 1u : 0u) << j;
@@ -688,7 +778,8 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   static_assert(NRM == 0 || (MB == 1 && AMODE == A_TOKEN && EPI != EPI_PART && NW == 16), "norm prologue: batch 1");
   // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
   // NRM = 8 * NCH + SMAX (norm_prologue<NCH, SMAX>)
-  constexpr bool L8_N = NRM >= 128;                          // LLM.int8 preparation (+ 128)
+  constexpr bool L8_N = NRM >= 128;                          // LLM.int8 preparation (+ 128) ...
+  constexpr int L8SRC_N = NRM >= 192 ? NRM % 8 : 0;          // ... of a normed row (+ 192 + 1 RMS / 2 LN)
   constexpr bool LN_N = NRM >= 64 && !L8_N;                  // LayerNorm of bf16 rows (+ 64)
   constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N || L8_N ? 1 : NRM % 8;
   static_assert(!L8_N || (EPI == EPI_OUT && MB == 1), "LLM.int8 prologue: one row, plain output");
@@ -775,14 +866,14 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   // NRM: the first step's weight loads go out before the norm prologue; its activations after
   NormRegs<(NRM > 0 && !LN_N && !L8_N ? NCH_N : 1), (NRM > 0 && !LN_N && !L8_N ? SMAX_N : 1)> nr;
   LnRegs<(LN_N ? NCH_N : 1)> lr;
-  L8Regs<(L8_N ? NCH_N : 1)> l8r;
+  L8Regs<(L8_N ? NCH_N : 1), L8SRC_N> l8r;
   auto nload = [&]() {
     if constexpr (L8_N) l8_load(na, K, l8r);
     else if constexpr (LN_N) ln_load(na, K, M, lr);
     else norm_load(na, K, M, nr);
   };
   auto nprologue = [&]() {
-    if constexpr (L8_N) l8_prologue(na, K, aq_l, nsa, nred, l8_cols, l8_xo, l8_scr, l8r);
+    if constexpr (L8_N) l8_prologue(na, K, aq_l, nsa, nred, l8_cols, l8_xo, l8_scr, l8r, na.y_out);
     else if constexpr (LN_N) ln_prologue(na, K, M, aq_l, nsa, nred, lr);
     else norm_prologue(na, K, M, aq_l, nsa, nred, nr);
   };
@@ -817,7 +908,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   auto fixed = [&](auto nk) {
     constexpr int NK = decltype(nk)::value, STEPS = (NK + KW * U - 1) / (KW * U);
     Step st[STEPS];
-    if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4 && (!L8_N || NCH_N <= 2)) {
+    if constexpr (NRM > 0 && STEPS <= 2 && NCH_N * SMAX_N <= 4 && (!L8_N || NCH_N <= (L8SRC_N ? 1 : 2))) {
       // batch-1 norm prologue: every step's weights (at most 2) in flight across it (K = 4096 with
       // 4 slices keeps one step: its prologue registers would spill)
       nload();
@@ -1959,6 +2050,29 @@ extern "C" int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const
     case 5: return launch_norm<3, 1, 16, EPI_OUT, 128 + 40>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
     default: return launch_norm<3, 1, 16, EPI_OUT, 128 + 48>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
   }
+}
+
+// The same over the RMSNorm (ln 0) / LayerNorm (ln 1) of x + res (res may be null): res_out gets
+// x + res, y_out (may be null) the normalised row.  K <= 4096, K % 64 == 0.  -2: not taken.
+extern "C" int edge_llmint8_gemv_norm(const void* x, const void* res, const void* gamma, const void* beta, float eps,
+                                      int ln, void* res_out, void* y_out, float thr, const void* Wp, const float* sw,
+                                      const void* bias, const void* wt, const float* scb, void* out, int N, int K,
+                                      hipStream_t st) {
+  if (!g_gemv_norm || K % 64 != 0 || K > 4096 || N % 16 != 0 || res_out == nullptr || res == res_out ||
+      x == res_out || (y_out != nullptr && (y_out == x || y_out == res_out)))
+    return -2;
+  NormIn na{nullptr, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, 0};
+  na.x = (const bf16_t*)x;
+  na.beta = (const bf16_t*)beta;
+  na.thr = thr;
+  na.wt = (const int8_t*)wt;
+  na.scb = scb;
+  na.y_out = (bf16_t*)y_out;
+  if (K <= 2048)
+    return ln ? launch_norm<3, 1, 16, EPI_OUT, 192 + 8 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+              : launch_norm<3, 1, 16, EPI_OUT, 192 + 8 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+  return ln ? launch_norm<3, 1, 16, EPI_OUT, 192 + 16 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+            : launch_norm<3, 1, 16, EPI_OUT, 192 + 16 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
 }
 
 // sa: per-token [M] (a_mode 0) or per-group [KT][Mpad] (a_mode 1, M <= 64).

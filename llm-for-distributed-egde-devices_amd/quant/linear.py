@@ -239,6 +239,17 @@ class LLMInt8Linear(nn.Module):
     DECODE_ROWS = 16
     ONE_LAUNCH = True    # batch 1: ops/csrc/gemm_i8.hip l8_prologue (one launch per projection, K <= 12288)
 
+    def pending_norm_ok(self, glu: bool = False):
+        """Batch 1 on GPU: this projection takes the RMSNorm of a bf16 row x + residual in its one-launch
+        GEMV's prologue ("x": a PendingLN with rms=True; Norm(defer="x"))."""
+        return "x" if (self._device_ok() and self.ONE_LAUNCH and self.in_features <= 4096) else False
+
+    def pending_ln_ok(self) -> bool:
+        """Batch 1 on GPU: this projection takes the LayerNorm of x + residual in its prologue."""
+        return self._device_ok() and self.ONE_LAUNCH and self.in_features <= 4096
+
+    takes_pending_x = True           # MLP: hand a PendingLN to this projection instead of materialising
+
     def _device_ok(self) -> bool:
         K = self.in_features
         return ops.available() and self.w_packed.is_cuda and K % 32 == 0 and K <= 32768
@@ -288,6 +299,21 @@ class LLMInt8Linear(nn.Module):
         return out if add is None else out + add.view_as(out)
 
     def _forward(self, x):
+        if isinstance(x, PendingLN):
+            y = None
+            K, N = self.in_features, self.out_features
+            if (x.x.shape[0] == 1 and x.x.is_cuda and ops.gpu_path(x.x) and x.x.dtype == torch.bfloat16
+                    and self._device_ok() and self.ONE_LAUNCH and K <= 4096):
+                C = ops.ext()
+                if self._weight_t is None or self._weight_t.device != x.x.device:
+                    self._weight_t = self.weight_i8.t().contiguous()
+                    self._w_deq = self.SCB / 127.0
+                y = C.llmint8_gemv_norm(x.x.contiguous(), x.residual.contiguous() if x.residual is not None else None,
+                                        x.weight, x.bias, x.eps, not x.rms, x.h, x.y, self.threshold, self.w_packed,
+                                        self._w_deq, self.bias, self._weight_t, self.SCB, N)
+            if y is not None:
+                return y
+            x = x.materialize()
         if isinstance(x, QAct):
             x = (x.q.float() * x.scale[..., None]).to(torch.bfloat16)
         K, N = self.in_features, self.out_features

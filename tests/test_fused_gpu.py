@@ -504,6 +504,67 @@ def test_llmint8_one_launch_exact(cuda, K, N, outliers, bias):
     assert torch.equal(one, three), (one.float() - three.float()).abs().max()
 
 
+@pytest.mark.parametrize("K,N", [(2048, 3072), (2560, 10240), (4096, 4096)])
+@pytest.mark.parametrize("outliers", [0, 5, 300])
+@pytest.mark.parametrize("kind", ["rms", "ln"])
+@pytest.mark.parametrize("res", [True, False])
+def test_llmint8_norm_one_launch_exact(cuda, K, N, outliers, kind, res):
+    """Batch-1 LLM.int8 over RMSNorm / LayerNorm(x + residual) computed in the same launch ==
+    the norm kernel followed by the one-launch LLM.int8 projection, bit for bit (output, residual
+    row, and the normalised row written for a second consumer)."""
+    from edgellm.models.layers import Linear
+    from edgellm.quant import LLMInt8Linear
+    C = ops.ext()
+    torch.manual_seed(K + N + outliers)
+    lin = Linear(K, N, bias=True, device=cuda)
+    lin.weight.data.copy_(torch.randn(N, K, device=cuda) * 0.02)
+    lin.bias.data.copy_(torch.randn(N, device=cuda) * 0.1)
+    m = LLMInt8Linear.from_float(lin)
+    x = torch.randn(1, K, device=cuda)
+    if outliers:
+        x[0, torch.randperm(K, device=cuda)[:outliers]] = 30.0
+    x = x.bfloat16()
+    resid = torch.randn(1, K, device=cuda).bfloat16() if res else None
+    gamma = (torch.rand(K, device=cuda) * 2 + 0.5).bfloat16()
+    beta = (torch.randn(K, device=cuda) * 0.1).bfloat16() if kind == "ln" else None
+    if kind == "rms":
+        yr, hr = ops.rms_norm(x, gamma, 1e-5, resid)
+    else:
+        yr, hr = ops.layer_norm(x, gamma, beta, 1e-5, resid)
+    ref = m(yr.contiguous())                               # one launch, over the norm kernel's row
+    h, y = torch.empty_like(x), torch.empty_like(x)          # (the call above built m._weight_t)
+    out = C.llmint8_gemv_norm(x, resid, gamma, beta, 1e-5, kind == "ln", h, y, m.threshold, m.w_packed,
+                              m._w_deq, m.bias, m._weight_t, m.SCB, N)
+    assert out is not None
+    assert torch.equal(h, hr.view_as(h)) and torch.equal(y, yr.view_as(y))
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
+
+
+@pytest.mark.parametrize("arch", ["llama", "phi", "gpt_neox"])
+def test_llmint8_model_norm_fused_matches_unfused(cuda, arch):
+    """LLM.int8 Llama / Phi-like / NeoX-like models generate the same greedy tokens at batch 1 with
+    the norms inside the one-launch projections as with the norm kernels (gemv_norm 0)."""
+    from edgellm.engine import Generator, SamplingParams
+    from edgellm.models import build_model, tiny
+    from edgellm.quant import quantize_model
+    kw = dict(hidden_size=256, num_heads=4, num_kv_heads=4 if arch != "llama" else 2, intermediate_size=1024,
+              num_layers=3)
+    if arch != "llama":
+        kw.update(head_dim=64, rotary_dim=32)
+    cfg = tiny(arch, **kw)
+    sp = SamplingParams(max_new_tokens=12, do_sample=False)
+    C = ops.ext()
+    outs = []
+    for on in (1, 0):
+        C.tune("gemv_norm", on, 0)
+        try:
+            m = quantize_model(build_model(cfg, device=cuda, seed=13), "llm_int8")
+            outs.append(Generator(m, max_batch=1, max_seq=64).generate([[1, 5, 9, 13, 2, 7]], sp, seed=0).tokens)
+        finally:
+            C.tune("gemv_norm", 1, 0)
+    assert outs[0] == outs[1]
+
+
 def _llmint8_emulation(x, q_w, scb, bias, thr):
     """fp32 emulation of the bitsandbytes split: columns with any |x| > thr in 16-bit against the
     dequantised weight columns, the rest per-token int8 x per-row int8."""
