@@ -176,6 +176,10 @@ class MLP(nn.Module):
             if not getattr(self.up, "takes_pending_x", False):
                 x = x.materialize()
             else:                                      # LLM.int8: the norm in the up projection's prologue
+                if self.act == "silu_glu" and hasattr(self.up, "glu_norm"):
+                    h = self.up.glu_norm(x)            # + the SwiGLU in its epilogue
+                    if h is not None:
+                        return self.down(h, add=add)
                 return self.down(act_fn(self.up(x), self.act, getattr(self.down, "takes_quantized_input", False)),
                                  add=add)
         if isinstance(x, PendingNorm):

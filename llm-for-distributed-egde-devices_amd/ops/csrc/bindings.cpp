@@ -96,7 +96,7 @@ int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const float* sw,
                       const float* scb, void* out, int N, int K, hipStream_t st);
 int edge_llmint8_gemv_norm(const void* x, const void* res, const void* gamma, const void* beta, float eps, int ln,
                            void* res_out, void* y_out, float thr, const void* Wp, const float* sw, const void* bias,
-                           const void* wt, const float* scb, void* out, int N, int K, hipStream_t st);
+                           const void* wt, const float* scb, void* out, int N, int K, hipStream_t st, int glu);
 int edge_llmint8_prep_rows(const void* x, int M, int K, float thr, void* q, float* sa, int* cols, int* count,
                            uint32_t* flags, uint32_t* take, hipStream_t st);
 int edge_llmint8_outlier_rows(void* out, const void* x, const int* cols, const int* count, const void* wt,
@@ -842,7 +842,7 @@ std::optional<at::Tensor> llmint8_gemv_norm(const at::Tensor& x, const std::opti
                                             double eps, bool ln, const at::Tensor& res_out,
                                             const std::optional<at::Tensor>& y_out, double thr, const at::Tensor& wp,
                                             const at::Tensor& sw, const std::optional<at::Tensor>& bias,
-                                            const at::Tensor& wt, const at::Tensor& scb, int64_t N) {
+                                            const at::Tensor& wt, const at::Tensor& scb, int64_t N, bool glu) {
   DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(gamma, at::kBFloat16, "gamma");
@@ -861,12 +861,12 @@ std::optional<at::Tensor> llmint8_gemv_norm(const at::Tensor& x, const std::opti
     TORCH_CHECK(residual->numel() == K && residual->data_ptr() != res_out.data_ptr(), "residual [1, K]");
   }
   if (y_out) { need(*y_out, at::kBFloat16, "y_out"); TORCH_CHECK(y_out->numel() == K, "y_out [1, K]"); }
-  auto out = at::empty({1, N}, x.options());
+  auto out = at::empty({1, glu ? N / 2 : N}, x.options());
   const int r = edge_llmint8_gemv_norm(x.data_ptr(), residual ? residual->data_ptr() : nullptr, gamma.data_ptr(),
                                        beta ? beta->data_ptr() : nullptr, (float)eps, ln ? 1 : 0, res_out.data_ptr(),
                                        y_out ? y_out->data_ptr() : nullptr, (float)thr, wp.data_ptr(),
                                        sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr, wt.data_ptr(),
-                                       scb.data_ptr<float>(), out.data_ptr(), (int)N, (int)K, stream());
+                                       scb.data_ptr<float>(), out.data_ptr(), (int)N, (int)K, stream(), glu ? 1 : 0);
   if (r == -2) return std::nullopt;
   check(r, "llmint8_gemv_norm");
   return out;

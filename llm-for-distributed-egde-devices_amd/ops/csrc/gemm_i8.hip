@@ -779,7 +779,9 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   // NRM: the int8 activation row lives in LDS (norm_prologue), its per-token scale in nsa[0]
   // NRM = 8 * NCH + SMAX (norm_prologue<NCH, SMAX>)
   constexpr bool L8_N = NRM >= 128;                          // LLM.int8 preparation (+ 128) ...
-  constexpr int L8SRC_N = NRM >= 192 ? NRM % 8 : 0;          // ... of a normed row (+ 192 + 1 RMS / 2 LN)
+  constexpr int L8SRC_N = NRM >= 192 ? NRM % 8 : 0;          // ... of a normed row (+ 192 + 1 RMS / 2 LN
+  constexpr int L8S_N = L8SRC_N & 3;                         //     (+ 4: SwiGLU of [gate | up] tiles)
+  constexpr bool L8G_N = (L8SRC_N & 4) != 0;
   constexpr bool LN_N = NRM >= 64 && !L8_N;                  // LayerNorm of bf16 rows (+ 64)
   constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N || L8_N ? 1 : NRM % 8;
   static_assert(!L8_N || (EPI == EPI_OUT && MB == 1), "LLM.int8 prologue: one row, plain output");
@@ -806,7 +808,9 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   const int ks = EPI == EPI_PART ? (int)blockIdx.x % S : 0;
   const int kbeg = EPI == EPI_PART ? (int)((int64_t)KT * ks / S) : 0;
   const int kend = EPI == EPI_PART ? (int)((int64_t)KT * (ks + 1) / S) : KT;
-  const int nt0 = grp * NTW;
+  // L8G (SwiGLU, natural [gate | up] rows): the workgroup's 2 tiles are gate tile grp and up tile grp + NTt / 2
+  const int nt0 = L8G_N ? grp : grp * NTW;
+  static_assert(!L8G_N || (NTW == 2 && TG == 1), "LLM.int8 SwiGLU: one gate + one up tile per workgroup");
   // wave index in an SGPR: every k-loop guard below is then a scalar branch (an MFMA must never
   // sit under an EXEC-masked branch — it ignores EXEC and would add a clamped duplicate k-tile)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -816,7 +820,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   const v4i* wp[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
-    const int nt = min(nt0 + t0 + j, NTt - 1);
+    const int nt = L8G_N ? (j == 0 ? nt0 : nt0 + NTt / 2) : min(nt0 + t0 + j, NTt - 1);
     wp[j] = reinterpret_cast<const v4i*>(Wp + ((size_t)nt * KT) * 1024) + lane;
   }
   const int8_t* ap[MB];
@@ -866,7 +870,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   // NRM: the first step's weight loads go out before the norm prologue; its activations after
   NormRegs<(NRM > 0 && !LN_N && !L8_N ? NCH_N : 1), (NRM > 0 && !LN_N && !L8_N ? SMAX_N : 1)> nr;
   LnRegs<(LN_N ? NCH_N : 1)> lr;
-  L8Regs<(L8_N ? NCH_N : 1), L8SRC_N> l8r;
+  L8Regs<(L8_N ? NCH_N : 1), L8S_N> l8r;
   auto nload = [&]() {
     if constexpr (L8_N) l8_load(na, K, l8r);
     else if constexpr (LN_N) ln_load(na, K, M, lr);
@@ -998,7 +1002,33 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
     }
     __syncthreads();
   }
-  if constexpr (L8_N) {
+  if constexpr (L8G_N) {
+    // wave 0, lanes 0-15: gate and up columns of feature nt0 * 16 + lane, each as the plain L8
+    // epilogue below computes it (bf16), then silu(g) * u as rowwise.hip act_kernel MODE 0 does
+    if (wave == 0 && lane < 16) {
+      const v4i* rb = &red[0][0][0];
+      float gu[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        int tot = rb[jj * 64 + lane][0];
+#pragma unroll
+        for (int w = 1; w < KR; ++w) tot += rb[(w * NTW + jj) * 64 + lane][0];
+        const int col = (jj == 0 ? nt0 : nt0 + NTt / 2) * 16 + lane;
+        float y = (float)tot * nsa[0];
+        y = y * sw[col] + (bias != nullptr ? bf2f(bias[col]) : 0.f);
+        const int nt = l8_scr[8];
+        if (nt > 0) {
+          float a = 0.f;
+          for (int j = 0; j < nt; ++j) a += l8_xo[j] * (float)na.wt[(size_t)l8_cols[j] * N + col];
+          const float s = na.scb[col] / 127.f;
+          y = bf2f(f2bf(y)) + a * s;
+        }
+        gu[jj] = bf2f(f2bf(y));
+      }
+      const float g = gu[0], u = gu[1];
+      reinterpret_cast<bf16_t*>(outv)[nt0 * 16 + lane] = f2bf(g / (1.f + __expf(-g)) * u);
+    }
+  } else if constexpr (L8_N) {
     // row 0 of each tile (lanes 0-15, q = 0): the int8 part as the EPI_OUT epilogue rounds it, then
     // the outlier columns' 16-bit part (llmint8.hip llmint8_outlier_kernel's sum order and rounding)
     if (wave < NTW && lane < 16 && nt0 + wave < NTt) {
@@ -2057,9 +2087,9 @@ extern "C" int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const
 extern "C" int edge_llmint8_gemv_norm(const void* x, const void* res, const void* gamma, const void* beta, float eps,
                                       int ln, void* res_out, void* y_out, float thr, const void* Wp, const float* sw,
                                       const void* bias, const void* wt, const float* scb, void* out, int N, int K,
-                                      hipStream_t st) {
+                                      hipStream_t st, int glu) {
   if (!g_gemv_norm || K % 64 != 0 || K > 4096 || N % 16 != 0 || res_out == nullptr || res == res_out ||
-      x == res_out || (y_out != nullptr && (y_out == x || y_out == res_out)))
+      x == res_out || (y_out != nullptr && (y_out == x || y_out == res_out)) || (glu && (ln || N % 32 != 0)))
     return -2;
   NormIn na{nullptr, (const bf16_t*)res, (const bf16_t*)gamma, (bf16_t*)res_out, eps, 0};
   na.x = (const bf16_t*)x;
@@ -2068,6 +2098,9 @@ extern "C" int edge_llmint8_gemv_norm(const void* x, const void* res, const void
   na.wt = (const int8_t*)wt;
   na.scb = scb;
   na.y_out = (bf16_t*)y_out;
+  if (glu)                                  // SwiGLU of [gate | up] (N = 2F): out [1, N / 2]
+    return K <= 2048 ? launch_norm<2, 1, 16, EPI_OUT, 192 + 8 + 5>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                     : launch_norm<2, 1, 16, EPI_OUT, 192 + 16 + 5>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
   if (K <= 2048)
     return ln ? launch_norm<3, 1, 16, EPI_OUT, 192 + 8 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
               : launch_norm<3, 1, 16, EPI_OUT, 192 + 8 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);

@@ -298,7 +298,12 @@ class LLMInt8Linear(nn.Module):
         out = self._forward(x)
         return out if add is None else out + add.view_as(out)
 
-    def _forward(self, x):
+    def glu_norm(self, x: PendingLN):
+        """Batch 1, [gate | up] rows: silu(gate) * up of the projection of RMSNorm(x + residual), one
+        launch (bf16 [1, N / 2]); None when not taken (the caller materialises)."""
+        return self._forward(x, glu=True) if (x.rms and self.out_features % 32 == 0) else None
+
+    def _forward(self, x, glu: bool = False):
         if isinstance(x, PendingLN):
             y = None
             K, N = self.in_features, self.out_features
@@ -310,8 +315,8 @@ class LLMInt8Linear(nn.Module):
                     self._w_deq = self.SCB / 127.0
                 y = C.llmint8_gemv_norm(x.x.contiguous(), x.residual.contiguous() if x.residual is not None else None,
                                         x.weight, x.bias, x.eps, not x.rms, x.h, x.y, self.threshold, self.w_packed,
-                                        self._w_deq, self.bias, self._weight_t, self.SCB, N)
-            if y is not None:
+                                        self._w_deq, self.bias, self._weight_t, self.SCB, N, glu)
+            if y is not None or glu:
                 return y
             x = x.materialize()
         if isinstance(x, QAct):
