@@ -176,6 +176,10 @@ class MLP(nn.Module):
             if not getattr(self.up, "takes_pending_x", False):
                 x = x.materialize()
             else:                                      # LLM.int8: the norm in the up projection's prologue
+                if self.act in ("gelu_tanh", "gelu") and hasattr(self.up, "gelu_fused"):
+                    h = self.up.gelu_fused(x, self.act)        # + the GELU in its epilogue
+                    if h is not None:
+                        return self.down(h, add=add)
                 if self.act == "silu_glu" and hasattr(self.up, "glu_norm"):
                     h = self.up.glu_norm(x)            # + the SwiGLU in its epilogue
                     if h is not None:
@@ -222,6 +226,10 @@ class MLP(nn.Module):
             # bf16 decode (Phi-2, Pythia): up-projection GEMV with the GELU epilogue
             return self.down(ops.linear_bf16(x, self.up.weight, self.up.bias, act=self.act,
                                              packed=self.up.decode_weight(x)), add=add)
+        if self.act in ("gelu_tanh", "gelu") and hasattr(self.up, "gelu_fused"):
+            h = self.up.gelu_fused(x, self.act)               # LLM.int8 batch 1: GELU in the same launch
+            if h is not None:
+                return self.down(h, add=add)
         h = self.up(x)
         h = act_fn(h, self.act, down_q)
         return self.down(h, add=add)

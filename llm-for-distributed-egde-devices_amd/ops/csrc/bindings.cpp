@@ -93,10 +93,11 @@ int edge_llmint8_prep(const void* x, int M, int K, float thr, int cmax, void* q,
 int edge_llmint8_outlier(void* out, const float* xo, const int* cols, const int* count, const void* wt,
                          const float* scb, int M, int N, int cmax, hipStream_t st);
 int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const float* sw, const void* bias, const void* wt,
-                      const float* scb, void* out, int N, int K, hipStream_t st);
+                      const float* scb, void* out, int N, int K, hipStream_t st, int act);
 int edge_llmint8_gemv_norm(const void* x, const void* res, const void* gamma, const void* beta, float eps, int ln,
                            void* res_out, void* y_out, float thr, const void* Wp, const float* sw, const void* bias,
-                           const void* wt, const float* scb, void* out, int N, int K, hipStream_t st, int glu);
+                           const void* wt, const float* scb, void* out, int N, int K, hipStream_t st, int glu,
+                           int act);
 int edge_llmint8_prep_rows(const void* x, int M, int K, float thr, void* q, float* sa, int* cols, int* count,
                            uint32_t* flags, uint32_t* take, hipStream_t st);
 int edge_llmint8_outlier_rows(void* out, const void* x, const int* cols, const int* count, const void* wt,
@@ -816,7 +817,7 @@ void llmint8_outlier(at::Tensor& out, const at::Tensor& xo, const at::Tensor& co
 // columns, int8 quant, GEMV, outlier part): bf16 [1, N], or None when the shape is not taken.
 std::optional<at::Tensor> llmint8_gemv(const at::Tensor& x, double thr, const at::Tensor& wp, const at::Tensor& sw,
                                        const std::optional<at::Tensor>& bias, const at::Tensor& wt,
-                                       const at::Tensor& scb, int64_t N) {
+                                       const at::Tensor& scb, int64_t N, int64_t act) {
   DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(wt, at::kChar, "weight_t");
@@ -829,7 +830,7 @@ std::optional<at::Tensor> llmint8_gemv(const at::Tensor& x, double thr, const at
   auto out = at::empty({1, N}, x.options());
   const int r = edge_llmint8_gemv(x.data_ptr(), (float)thr, wp.data_ptr(), sw.data_ptr<float>(),
                                   bias ? bias->data_ptr() : nullptr, wt.data_ptr(), scb.data_ptr<float>(),
-                                  out.data_ptr(), (int)N, (int)K, stream());
+                                  out.data_ptr(), (int)N, (int)K, stream(), (int)act);
   if (r == -2) return std::nullopt;
   check(r, "llmint8_gemv");
   return out;
@@ -842,7 +843,8 @@ std::optional<at::Tensor> llmint8_gemv_norm(const at::Tensor& x, const std::opti
                                             double eps, bool ln, const at::Tensor& res_out,
                                             const std::optional<at::Tensor>& y_out, double thr, const at::Tensor& wp,
                                             const at::Tensor& sw, const std::optional<at::Tensor>& bias,
-                                            const at::Tensor& wt, const at::Tensor& scb, int64_t N, bool glu) {
+                                            const at::Tensor& wt, const at::Tensor& scb, int64_t N, bool glu,
+                                            int64_t act) {
   DEVICE_GUARD(x);
   need(x, at::kBFloat16, "x");
   need(gamma, at::kBFloat16, "gamma");
@@ -866,7 +868,8 @@ std::optional<at::Tensor> llmint8_gemv_norm(const at::Tensor& x, const std::opti
                                        beta ? beta->data_ptr() : nullptr, (float)eps, ln ? 1 : 0, res_out.data_ptr(),
                                        y_out ? y_out->data_ptr() : nullptr, (float)thr, wp.data_ptr(),
                                        sw.data_ptr<float>(), bias ? bias->data_ptr() : nullptr, wt.data_ptr(),
-                                       scb.data_ptr<float>(), out.data_ptr(), (int)N, (int)K, stream(), glu ? 1 : 0);
+                                       scb.data_ptr<float>(), out.data_ptr(), (int)N, (int)K, stream(), glu ? 1 : 0,
+                                       (int)act);
   if (r == -2) return std::nullopt;
   check(r, "llmint8_gemv_norm");
   return out;

@@ -782,6 +782,7 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
   constexpr int L8SRC_N = NRM >= 192 ? NRM % 8 : 0;          // ... of a normed row (+ 192 + 1 RMS / 2 LN
   constexpr int L8S_N = L8SRC_N & 3;                         //     (+ 4: SwiGLU of [gate | up] tiles)
   constexpr bool L8G_N = (L8SRC_N & 4) != 0;
+  constexpr int L8ACT_N = NRM >= 256 ? (NRM - 256) / 64 + 1 : 0;   // + 256 (+ 64): gelu tanh (erf) epilogue
   constexpr bool LN_N = NRM >= 64 && !L8_N;                  // LayerNorm of bf16 rows (+ 64)
   constexpr int NCH_N = (NRM % 64) / 8, SMAX_N = LN_N || L8_N ? 1 : NRM % 8;
   static_assert(!L8_N || (EPI == EPI_OUT && MB == 1), "LLM.int8 prologue: one row, plain output");
@@ -1046,6 +1047,11 @@ __global__ void __launch_bounds__(TG * KW * 64) w8a8_gemv_kernel(const int8_t* _
           for (int j = 0; j < nt; ++j) a += l8_xo[j] * (float)na.wt[(size_t)l8_cols[j] * N + col];
           const float s = na.scb[col] / 127.f;
           y = bf2f(f2bf(y)) + a * s;
+        }
+        if constexpr (L8ACT_N > 0) {                    // rowwise.hip act_kernel MODE 1 / 2 of the bf16 output
+          const float a = bf2f(f2bf(y));
+          if constexpr (L8ACT_N == 1) y = 0.5f * a * (1.f + tanhf(0.7978845608028654f * (a + 0.044715f * a * a * a)));
+          else y = 0.5f * a * (1.f + erff(a * 0.7071067811865476f));
         }
         reinterpret_cast<bf16_t*>(outv)[col] = f2bf(y);
       }
@@ -2065,13 +2071,20 @@ extern "C" int edge_w8a8_gemv_ln(const void* x, const void* res, const void* gam
 // SCB / 127 (+ bias), plus the outlier columns' part from wt = int8 W^T [K, N].  K % 64 == 0,
 // K <= 12288.  -2: not taken.
 extern "C" int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const float* sw, const void* bias,
-                                 const void* wt, const float* scb, void* out, int N, int K, hipStream_t st) {
+                                 const void* wt, const float* scb, void* out, int N, int K, hipStream_t st, int act) {
   if (K % 64 != 0 || K > 12288 || K < 64 || N % 16 != 0) return -2;
   NormIn na{nullptr, nullptr, nullptr, nullptr, 0.f, 0};
   na.x = (const bf16_t*)x;
   na.thr = thr;
   na.wt = (const int8_t*)wt;
   na.scb = scb;
+  if (act == 1 || act == 2) {                            // + gelu (tanh / erf) of the output, K <= 4096
+    if (K > 4096) return -2;
+    if (act == 1) return K <= 2048 ? launch_norm<3, 1, 16, EPI_OUT, 256 + 8>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                                   : launch_norm<3, 1, 16, EPI_OUT, 256 + 16>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    return K <= 2048 ? launch_norm<3, 1, 16, EPI_OUT, 320 + 8>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                     : launch_norm<3, 1, 16, EPI_OUT, 320 + 16>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+  }
   switch ((K + 2047) / 2048) {                            // row chunks of 2048 per 256 threads
     case 1: return launch_norm<3, 1, 16, EPI_OUT, 128 + 8>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
     case 2: return launch_norm<3, 1, 16, EPI_OUT, 128 + 16>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
@@ -2087,7 +2100,7 @@ extern "C" int edge_llmint8_gemv(const void* x, float thr, const void* Wp, const
 extern "C" int edge_llmint8_gemv_norm(const void* x, const void* res, const void* gamma, const void* beta, float eps,
                                       int ln, void* res_out, void* y_out, float thr, const void* Wp, const float* sw,
                                       const void* bias, const void* wt, const float* scb, void* out, int N, int K,
-                                      hipStream_t st, int glu) {
+                                      hipStream_t st, int glu, int act) {
   if (!g_gemv_norm || K % 64 != 0 || K > 4096 || N % 16 != 0 || res_out == nullptr || res == res_out ||
       x == res_out || (y_out != nullptr && (y_out == x || y_out == res_out)) || (glu && (ln || N % 32 != 0)))
     return -2;
@@ -2098,6 +2111,19 @@ extern "C" int edge_llmint8_gemv_norm(const void* x, const void* res, const void
   na.wt = (const int8_t*)wt;
   na.scb = scb;
   na.y_out = (bf16_t*)y_out;
+  if (act == 1 || act == 2) {              // + gelu (tanh / erf) of the output
+    if (glu) return -2;
+    if (act == 1) {
+      if (K <= 2048) return ln ? launch_norm<3, 1, 16, EPI_OUT, 256 + 8 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                               : launch_norm<3, 1, 16, EPI_OUT, 256 + 8 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+      return ln ? launch_norm<3, 1, 16, EPI_OUT, 256 + 16 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                : launch_norm<3, 1, 16, EPI_OUT, 256 + 16 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    }
+    if (K <= 2048) return ln ? launch_norm<3, 1, 16, EPI_OUT, 320 + 8 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+                             : launch_norm<3, 1, 16, EPI_OUT, 320 + 8 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+    return ln ? launch_norm<3, 1, 16, EPI_OUT, 320 + 16 + 2>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
+              : launch_norm<3, 1, 16, EPI_OUT, 320 + 16 + 1>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);
+  }
   if (glu)                                  // SwiGLU of [gate | up] (N = 2F): out [1, N / 2]
     return K <= 2048 ? launch_norm<2, 1, 16, EPI_OUT, 192 + 8 + 5>(na, Wp, sw, bias, out, nullptr, 1, N, K, st)
                      : launch_norm<2, 1, 16, EPI_OUT, 192 + 16 + 5>(na, Wp, sw, bias, out, nullptr, 1, N, K, st);

@@ -303,7 +303,22 @@ class LLMInt8Linear(nn.Module):
         launch (bf16 [1, N / 2]); None when not taken (the caller materialises)."""
         return self._forward(x, glu=True) if (x.rms and self.out_features % 32 == 0) else None
 
-    def _forward(self, x, glu: bool = False):
+    _ACT = {"gelu_tanh": 1, "gelu": 2}
+
+    def gelu_fused(self, x, act: str):
+        """Batch 1: gelu (tanh / erf) of this projection in the same launch (bf16 [1, N]), over a bf16
+        row or a PendingLN; None when not taken."""
+        if act not in self._ACT:
+            return None
+        if isinstance(x, PendingLN):
+            return self._forward(x, act=self._ACT[act])
+        if isinstance(x, torch.Tensor) and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.bfloat16 \
+                and x.is_cuda and ops.gpu_path(x) and self._device_ok() and self.ONE_LAUNCH \
+                and self.in_features <= 4096:
+            return self._forward(x, act=self._ACT[act])
+        return None
+
+    def _forward(self, x, glu: bool = False, act: int = 0):
         if isinstance(x, PendingLN):
             y = None
             K, N = self.in_features, self.out_features
@@ -315,8 +330,8 @@ class LLMInt8Linear(nn.Module):
                     self._w_deq = self.SCB / 127.0
                 y = C.llmint8_gemv_norm(x.x.contiguous(), x.residual.contiguous() if x.residual is not None else None,
                                         x.weight, x.bias, x.eps, not x.rms, x.h, x.y, self.threshold, self.w_packed,
-                                        self._w_deq, self.bias, self._weight_t, self.SCB, N, glu)
-            if y is not None or glu:
+                                        self._w_deq, self.bias, self._weight_t, self.SCB, N, glu, act)
+            if y is not None or glu or act:
                 return y
             x = x.materialize()
         if isinstance(x, QAct):
@@ -334,9 +349,11 @@ class LLMInt8Linear(nn.Module):
             if x2.shape[0] == 1 and K <= 12288 and K % 64 == 0 and self.ONE_LAUNCH:
                 # batch 1: outlier discovery, quantisation and the outlier part inside the GEMV
                 out = C.llmint8_gemv(x2, self.threshold, self.w_packed, self._w_deq, self.bias, self._weight_t,
-                                     self.SCB, N)
+                                     self.SCB, N, act)
                 if out is not None:
                     return out.view(*shp, N)
+                if act:
+                    return None
             if x2.shape[0] <= self.DECODE_ROWS:
                 q, sa, cols, xo, count = C.llmint8_prep(x2, self.threshold, self.OUTLIER_CAP)
                 out = ops.w8a8_linear(q, sa, self.w_packed, self._w_deq, self.bias, N, K)

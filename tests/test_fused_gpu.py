@@ -534,15 +534,22 @@ def test_llmint8_norm_one_launch_exact(cuda, K, N, outliers, kind, res):
     ref = m(yr.contiguous())                               # one launch, over the norm kernel's row
     h, y = torch.empty_like(x), torch.empty_like(x)          # (the call above built m._weight_t)
     out = C.llmint8_gemv_norm(x, resid, gamma, beta, 1e-5, kind == "ln", h, y, m.threshold, m.w_packed,
-                              m._w_deq, m.bias, m._weight_t, m.SCB, N, False)
+                              m._w_deq, m.bias, m._weight_t, m.SCB, N, False, 0)
     assert out is not None
     assert torch.equal(h, hr.view_as(h)) and torch.equal(y, yr.view_as(y))
     assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
     if kind == "rms" and N % 32 == 0:                      # + SwiGLU of [gate | up] in the epilogue
         g = C.llmint8_gemv_norm(x, resid, gamma, beta, 1e-5, False, h, None, m.threshold, m.w_packed,
-                                m._w_deq, m.bias, m._weight_t, m.SCB, N, True)
+                                m._w_deq, m.bias, m._weight_t, m.SCB, N, True, 0)
         assert g is not None and g.shape == (1, N // 2)
         assert torch.equal(g, ops.activation(ref, "silu_glu")), (g.float() - ops.activation(ref, "silu_glu").float()).abs().max()
+    for act, code in (("gelu_tanh", 1), ("gelu", 2)):                   # + GELU in the epilogue
+        g = C.llmint8_gemv_norm(x, resid, gamma, beta, 1e-5, kind == "ln", h, None, m.threshold, m.w_packed,
+                                m._w_deq, m.bias, m._weight_t, m.SCB, N, False, code)
+        assert g is not None and torch.equal(g, ops.activation(ref, act)), act
+        if kind == "rms":                                  # the raw-row form too
+            gr = m.gelu_fused(yr.contiguous(), act)
+            assert gr is not None and torch.equal(gr, ops.activation(ref, act)), act
 
 
 @pytest.mark.parametrize("arch", ["llama", "phi", "gpt_neox"])
